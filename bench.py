@@ -1,0 +1,217 @@
+"""Benchmark of the MCAQ spatial-adaptive-quantization hook path on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4] [--no-cpu]
+
+A step = the three backbone hooks (C3/C4/C5) of one batch: channel statistics,
+morphological complexity (phi1..5, MLP, bilateral), bit mapper, soft mask and
+the tile-wise 2..8-bit quant/dequant - every output the reference hook
+produces, computed by the HIP kernels on inputs already resident in HBM.  The
+YOLOv8 host network is not part of the step (not built yet: SURVEY 8f rank 1;
+ultralytics is unavailable) - `config.workload` says so.
+
+N > 1: one process per GPU (torch.distributed.run), each rank takes its own
+batch shard (weak scaling); the per-channel batch min/max is made global with
+one RCCL all-reduce per step, so every rank quantizes exactly like the
+reference run on the whole global batch.
+
+Prints ONE JSON line (rank 0).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.nn.functional as F
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from mcaq_yolo_amd import params  # noqa: E402
+from mcaq_yolo_amd.engine import HookPlan, ScaleGeom  # noqa: E402
+
+# BASELINE.json configs that fit this harness: name -> (per-GPU batch, channels, grid, mapper)
+CONFIGS = {
+    2: ("yolov8n", 32, (64, 128, 256), 8, "mlp"),
+    3: ("yolov8s", 64, (128, 256, 512), 16, "mlp"),
+    4: ("yolov8m", 32, (192, 384, 576), 8, "mlp"),   # bs256 = 32 per GPU x 8
+}
+SIZES = ((80, 80), (40, 40), (20, 20))  # C3/C4/C5 at 640x640 (strides 8/16/32)
+HBM_PEAK_GBS = 8000.0                   # MI355X_MICROARCH.md chip table (spec)
+
+
+def synth_features(B, C, H, W, seed, device):
+    """silu(1.5*randn + 2*bilinear_up(randn(B,C,H/8,W/8)))."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    lo = torch.randn(B, C, max(1, H // 8), max(1, W // 8), generator=g)
+    hi = torch.randn(B, C, H, W, generator=g)
+    up = F.interpolate(lo, size=(H, W), mode="bilinear", align_corners=False)
+    return F.silu(1.5 * hi + 2.0 * up).contiguous().to(device)
+
+
+def load_blobs(device):
+    import numpy as np
+    w = np.load(os.path.join(ROOT, "tests", "golden", "weights.npz"))
+    sd = {k: w[k] for k in w.files}
+    cm = torch.from_numpy(params.pack_complexity_mlp(params.sub(sd, "complexity_analyzer."))).to(device)
+    mm = torch.from_numpy(params.pack_mapper_mlp(params.sub(sd, "bit_mapper."))).to(device)
+    sm = torch.from_numpy(params.pack_soft_mask(params.sub(sd, "soft_mask."))).to(device)
+    return cm, mm, sm
+
+
+def cpu_baseline(cfg_id, budget_s=12.0):
+    """Oracle (numpy port of the reference path) on the host: one image per
+    hook scale per iteration, repeated for ~budget_s seconds -> images/s."""
+    import numpy as np
+    from oracle import mcaq_oracle as O
+    name, B, chans, grid, mapper = CONFIGS[cfg_id]
+    w = O.load_weights(os.path.join(ROOT, "tests", "golden", "weights.npz"))
+    xs = [synth_features(1, c, h, wd, 1000 * cfg_id + i, "cpu").numpy() for i, (c, (h, wd)) in
+          enumerate(zip(chans, SIZES))]
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        for x in xs:
+            O.hook_forward(x, w, grid, mapper=mapper)
+        n += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 4), "unit": "images/s", "cores": 1, "kind": "port",
+            "sample": "%d images x 3 hook scales (%s %s, batch 1) through oracle/mcaq_oracle.py, "
+                      "single-threaded numpy, %.1f s" % (n, name, "x".join(map(str, chans)), dt)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--eager", action="store_true", help="no HIP graph")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+        pg = dist.group.WORLD
+
+    name, B, chans, grid, mapper = CONFIGS[args.config]
+    feats = [synth_features(B, c, h, w, 1000 * args.config + i + 7919 * rank, dev)
+             for i, (c, (h, w)) in enumerate(zip(chans, SIZES))]
+    cm, mm, sm = load_blobs(dev)
+    plan = HookPlan([ScaleGeom(B, c, h, w, grid) for c, (h, w) in zip(chans, SIZES)], dev)
+    plan.prepare(feats, cm, mm, [sm, sm, sm], temperature=1.0, mapper_kind=mapper,
+                 batch_offset=rank * B, batch_total=world * B)
+    stream = torch.cuda.current_stream()
+
+    def step():
+        plan.launch(stream, pg)
+
+    use_graph = (world == 1) and not args.eager
+    graph = None
+    for _ in range(max(args.warmup, 1)):
+        step()
+    torch.cuda.synchronize()
+    if use_graph:
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step()
+        for _ in range(3):
+            graph.replay()
+        torch.cuda.synchronize()
+    run = graph.replay if graph is not None else step
+
+    # per-kernel device time (HIP events on the launch stream), untimed pass
+    L = plan.lib
+    from mcaq_yolo_amd import abi
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+    kt = {"stats": 0.0, "finalize": 0.0, "morph": 0.0, "quant": 0.0}
+    reps = 20
+    for _ in range(reps):
+        sh = abi.ctypes.c_void_p(stream.cuda_stream)
+        ev[0].record(stream)
+        L.mcaq_stats(plan._st, plan._n, sh)
+        ev[1].record(stream)
+        L.mcaq_finalize(plan._fz, plan._n, sh)
+        ev[2].record(stream)
+        L.mcaq_morph(plan._mo, plan._n, sh)
+        ev[3].record(stream)
+        L.mcaq_quant(plan._qs, plan._n, sh)
+        ev[4].record(stream)
+        torch.cuda.synchronize()
+        for i, k in enumerate(kt):
+            kt[k] += ev[i].elapsed_time(ev[i + 1]) * 1e3 / reps   # us
+
+    # ---- timed region
+    if pg is not None:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(args.steps):
+        run()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    dev_ms = e0.elapsed_time(e1)
+    step_s = max(wall, dev_ms / 1e3) / args.steps
+    if pg is not None:
+        import torch.distributed as dist
+        t = torch.tensor([step_s], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.barrier()
+        step_s = float(t.item())
+
+    elems = sum(B * c * h * w for c, (h, w) in zip(chans, SIZES))
+    alg_bytes = 12 * elems                       # 2 reads of x + 1 write of y, fp32
+    achieved = alg_bytes / step_s / 1e9
+    value = world * B / step_s
+    if rank == 0:
+        out = {
+            "metric": "images/sec @640x640 end-to-end MCAQ infer, 1/2/4/8 MI355X; % HBM roofline",
+            "value": round(value, 2),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(step_s * 1e3, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic silu(1.5*randn+2*up(randn)) C3/C4/C5 features, seeded weights",
+            "config": {"workload": "%s bs%d/GPU 640x640 MCAQ hook path C3/C4/C5 (grid %d, %s mapper); "
+                                   "YOLOv8 network excluded" % (name, B, grid, mapper),
+                       "global_batch": world * B, "grid_size": grid, "mapper": mapper,
+                       "parallelism": "dp%d" % world, "hip_graph": graph is not None},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "fused hook path (stats+finalize+morph+quant) per step",
+                         "alg_bytes_per_step": alg_bytes},
+            "kernels_us": {k: round(v, 2) for k, v in kt.items()},
+            "cpu_baseline": None,
+        }
+        if not args.no_cpu and world == 1:
+            out["cpu_baseline"] = cpu_baseline(args.config)
+        print(json.dumps(out), flush=True)
+    if pg is not None:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

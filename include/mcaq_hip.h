@@ -1,0 +1,135 @@
+/* mcaq_hip.h - C ABI of the MI355X (gfx950) MCAQ spatial-adaptive-quantization
+ * hook path.  Plain pointers (device memory) and sizes; every launcher is
+ * asynchronous on the given HIP stream and returns a hipError_t value.
+ *
+ * Reference interfaces replaced (yooooonjae/mcaq-yolo):
+ *   mcaq_launch_spatial_quantization  <- launch_spatial_quantization
+ *       (mcaq_yolo/ops/src/mcaq_kernel.cu:102-123, declared with C++ linkage
+ *        in mcaq_yolo/ops/src/mcaq_ops.cpp:7-16 and
+ *        mcaq_yolo/engine/MCAQPlugin.cpp:14-24; called by
+ *        MCAQPlugin::enqueue, MCAQPlugin.cpp:43-71)
+ *   mcaq_stats / mcaq_finalize / mcaq_morph / mcaq_quant
+ *       <- the per-scale hook body MCAQYOLO._make_mcaq_hook.hook
+ *          (mcaq_yolo/models/mcaq_yolo.py:409-455): analyzer
+ *          (core/morphology.py:939-973), bit mapper (core/bit_allocation.py:
+ *          42-80, 218-280), quantizer (core/quantization.py:604-746), split
+ *          into the three HBM passes of the fused design.
+ * Up to three hook scales (C3/C4/C5) are processed by one launch.
+ */
+#ifndef MCAQ_HIP_H_
+#define MCAQ_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef MCAQ_NO_HIP
+typedef void* hipStream_t;
+#else
+#include <hip/hip_runtime_api.h>
+#endif
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MCAQ_ABI_VERSION 1
+/* largest dynamic LDS request of the morph kernel (gfx950: 160 KiB per CU) */
+#define MCAQ_MORPH_LDS_LIMIT 163840
+
+/* ---- reference-compatible operator ----------------------------------------
+ * Same argument order as launch_spatial_quantization (mcaq_kernel.cu:102-111)
+ * with hipStream_t; output[n,c,h,w] = dequant(quant_b(input)) * mask[n,h,w]
+ * where b = clamp(rint(bit_map[n, min(h/tile_h, Ht-1), min(w/tile_w, Wt-1)]),
+ * 2, 8) and per-channel scale/zero-point come from min_vals/max_vals (C
+ * entries).  Rounding is half-to-even (torch.round), unlike the reference
+ * kernel's roundf; mask may be NULL.  Returns hipErrorInvalidValue on bad
+ * sizes.  No workspace. */
+int mcaq_launch_spatial_quantization(const float* input, const float* bit_map,
+                                     const float* min_vals, const float* max_vals,
+                                     const float* mask, float* output,
+                                     int N, int C, int H, int W, int tile_h, int tile_w,
+                                     int n_tiles_h, int n_tiles_w, hipStream_t stream);
+
+/* ---- pass 1: one streaming read of x ---------------------------------------
+ * gray[b,h,w]    = mean_c x[b,c,h,w] over the crop h<Hc, w<Wc, in CPU-ATen
+ *                  summation order (NULL to skip)
+ * absmean[b,h,w] = mean_c |x[b,c,h,w]| over the full map (NULL to skip)
+ * pmin/pmax      = per-(unit, channel) min/max partials, unit = 256 pixels of
+ *                  one image: mcaq_stats_units(B,H,W) x C floats each (NULL to
+ *                  skip). */
+typedef struct {
+  const float* x;  /* (B, C, H, W) fp32 contiguous */
+  float* gray;     /* (B, Hc, Wc) */
+  float* absmean;  /* (B, H, W) */
+  float* pmin;
+  float* pmax;
+  int B, C, H, W, Hc, Wc;
+  int unit_begin;  /* set by the launcher */
+} mcaq_stats_scale;
+int mcaq_stats(const mcaq_stats_scale* scales, int nscales, hipStream_t stream);
+int mcaq_stats_units(int B, int H, int W);
+
+/* ---- channel min/max over the batch (quantization.py:650-654) -------------- */
+typedef struct {
+  const float* pmin; /* partials from mcaq_stats (or NULL: copy min_in/max_in) */
+  const float* pmax;
+  const float* min_in;
+  const float* max_in;
+  float* min_out;    /* (C) */
+  float* max_out;    /* (C) */
+  int C, nunits, min_stride;
+  int block_begin;   /* set by the launcher */
+} mcaq_finalize_scale;
+int mcaq_finalize(const mcaq_finalize_scale* scales, int nscales, hipStream_t stream);
+
+/* ---- morph: one workgroup per image --------------------------------------
+ * flags: 1 phi, 2 complexity MLP + bilateral, 4 mapper, 8 soft mask,
+ * 16 continuous bits, 32 temperature given, 64 normalise C, 128 linear mapper,
+ * 256 Otsu binarize, 512 no Euler correction.  Parameter blobs are the packed
+ * reference state_dict tensors (mcaq_yolo_amd/params.py). */
+typedef struct {
+  const float* gray;
+  const float* absmean;
+  const float* cmlp;
+  const float* mapper;
+  const float* smask;
+  const float* c_in;
+  const float* bits_in;
+  float* phi_out;
+  float* cmlp_out;
+  float* c_out;
+  float* bits_out;
+  float* m_out;
+  uint8_t* edge_out;
+  uint8_t* bin_out;
+  float* gscratch;   /* mcaq_morph_scratch_bytes() bytes, or NULL when 0 */
+  int B, H, W, Hc, Wc, tile, ht, wt;
+  int batch_offset, batch_total;
+  int flags, hyst_iters;
+  float temperature, min_bits, max_bits;
+  int block_begin;   /* set by the launcher */
+} mcaq_morph_scale;
+int mcaq_morph(const mcaq_morph_scale* scales, int nscales, hipStream_t stream);
+size_t mcaq_morph_scratch_bytes(int B, int Hc, int Wc, int ht, int wt);
+
+/* ---- pass 2: y = dequant(quant_b(x)) * m ----------------------------------- */
+typedef struct {
+  const float* x;      /* (B, C, H, W) */
+  float* y;            /* (B, C, H, W) */
+  const float* bits;   /* (B, ht, wt) integer-valued */
+  const float* m;      /* (B, H, W) or NULL */
+  const float* xmin;   /* (C) */
+  const float* xmax;   /* (C) */
+  int B, C, H, W, ht, wt;
+  int bits_lo, nbits;  /* supported widths [bits_lo, bits_lo + nbits - 1] */
+  int compat_tile_h, compat_tile_w; /* >0: spatial_quantize tile indexing */
+  int unit_begin;      /* set by the launcher */
+} mcaq_quant_scale;
+int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream);
+
+int mcaq_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MCAQ_HIP_H_ */

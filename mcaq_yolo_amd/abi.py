@@ -1,0 +1,97 @@
+"""ctypes mirror of include/mcaq_hip.h and the loader of the native library.
+
+The product path runs ONLY through libmcaq_hip.so (built in-tree by
+__graft_entry__.build() / tools/build.py).  There is no CPU fallback: when the
+library is missing or no GPU is visible, `lib()` raises.
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libmcaq_hip.so")
+ABI_VERSION = 1
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+Fl = ctypes.c_float
+
+
+class StatsScale(ctypes.Structure):
+    _fields_ = [("x", P), ("gray", P), ("absmean", P), ("pmin", P), ("pmax", P),
+                ("B", I), ("C", I), ("H", I), ("W", I), ("Hc", I), ("Wc", I), ("unit_begin", I)]
+
+
+class FinalizeScale(ctypes.Structure):
+    _fields_ = [("pmin", P), ("pmax", P), ("min_in", P), ("max_in", P), ("min_out", P), ("max_out", P),
+                ("C", I), ("nunits", I), ("min_stride", I), ("block_begin", I)]
+
+
+class MorphScale(ctypes.Structure):
+    _fields_ = [("gray", P), ("absmean", P), ("cmlp", P), ("mapper", P), ("smask", P),
+                ("c_in", P), ("bits_in", P), ("phi_out", P), ("cmlp_out", P), ("c_out", P),
+                ("bits_out", P), ("m_out", P), ("edge_out", P), ("bin_out", P), ("gscratch", P),
+                ("B", I), ("H", I), ("W", I), ("Hc", I), ("Wc", I), ("tile", I), ("ht", I), ("wt", I),
+                ("batch_offset", I), ("batch_total", I), ("flags", I), ("hyst_iters", I),
+                ("temperature", Fl), ("min_bits", Fl), ("max_bits", Fl), ("block_begin", I)]
+
+
+class QuantScale(ctypes.Structure):
+    _fields_ = [("x", P), ("y", P), ("bits", P), ("m", P), ("xmin", P), ("xmax", P),
+                ("B", I), ("C", I), ("H", I), ("W", I), ("ht", I), ("wt", I),
+                ("bits_lo", I), ("nbits", I), ("compat_tile_h", I), ("compat_tile_w", I), ("unit_begin", I)]
+
+
+# morph stage flags (mcaq_morph.h)
+F_PHI, F_CMLP, F_MAPPER, F_SOFTMASK = 1, 2, 4, 8
+F_CONT, F_HAS_T, F_NORM_C, F_MAP_LINEAR = 16, 32, 64, 128
+F_BIN_OTSU, F_NO_EULER = 256, 512
+
+EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats", "mcaq_stats_units",
+           "mcaq_finalize", "mcaq_morph", "mcaq_morph_scratch_bytes", "mcaq_quant")
+
+_LIB = None
+
+
+class NativeLibraryMissing(RuntimeError):
+    pass
+
+
+def _declare(lib):
+    lib.mcaq_abi_version.restype = I
+    lib.mcaq_launch_spatial_quantization.restype = I
+    lib.mcaq_launch_spatial_quantization.argtypes = [P, P, P, P, P, P] + [I] * 8 + [P]
+    for n, st in (("mcaq_stats", StatsScale), ("mcaq_finalize", FinalizeScale),
+                  ("mcaq_morph", MorphScale), ("mcaq_quant", QuantScale)):
+        f = getattr(lib, n)
+        f.restype = I
+        f.argtypes = [ctypes.POINTER(st), I, P]
+    lib.mcaq_stats_units.restype = I
+    lib.mcaq_stats_units.argtypes = [I, I, I]
+    lib.mcaq_morph_scratch_bytes.restype = ctypes.c_size_t
+    lib.mcaq_morph_scratch_bytes.argtypes = [I, I, I, I, I]
+    return lib
+
+
+def load_library(path=LIB_PATH):
+    """dlopen the native library (no GPU needed: it only registers kernels)."""
+    if not os.path.exists(path):
+        raise NativeLibraryMissing(
+            "libmcaq_hip.so not built (%s); run `python -c 'import __graft_entry__ as g; g.build()'`" % path)
+    import torch  # noqa: F401  (loads torch's libamdhip64 first: one HIP runtime per process)
+    lib = _declare(ctypes.CDLL(path))
+    v = lib.mcaq_abi_version()
+    if v != ABI_VERSION:
+        raise NativeLibraryMissing("libmcaq_hip.so ABI %d != expected %d (rebuild)" % (v, ABI_VERSION))
+    return lib
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        _LIB = load_library()
+    return _LIB
+
+
+def check(err, what):
+    if err != 0:
+        raise RuntimeError("%s failed: hipError %d" % (what, err))

@@ -1,0 +1,144 @@
+// mcaq_math.h - exact fp32 arithmetic shared by the gfx950 kernels and the
+// host emulation build (tests/emu).  Every function here is a fixed sequence
+// of IEEE operations; the numpy oracle (oracle/mcaq_oracle.py) states the same
+// sequence, and tests compare the two bit for bit.
+//
+// Build rule: compile with -ffp-contract=off.  The reference (CPU ATen) never
+// fuses a multiply into an add except where it calls an FMA explicitly, so
+// every fused operation below is an explicit fmaf().
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__) || defined(__HIP_DEVICE_COMPILE__)
+#include <hip/hip_runtime.h>
+#define MCAQ_HD __host__ __device__ __forceinline__
+#else
+#include <cmath>
+#define MCAQ_HD inline
+#endif
+
+#include <math.h>
+
+namespace mcaq {
+
+// Correctly rounded fp32 transcendentals: evaluate in double, round once.
+// (ocml double and glibc double are both < 1 double-ulp, so the fp32 rounding
+// agrees except at points within ~1e-16 of an fp32 midpoint.)
+MCAQ_HD float cr_exp(float x) { return (float)exp((double)x); }
+MCAQ_HD float cr_log(float x) { return (float)log((double)x); }
+MCAQ_HD float cr_log2(float x) { return (float)log2((double)x); }
+MCAQ_HD float cr_log1p(float x) { return (float)log1p((double)x); }
+MCAQ_HD float cr_sqrt(float x) { return (float)sqrt((double)x); }
+MCAQ_HD float cr_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
+
+MCAQ_HD float bits_as_float(uint32_t u) {
+  union { uint32_t u; float f; } c; c.u = u; return c.f;
+}
+MCAQ_HD uint32_t float_as_bits(float f) {
+  union { uint32_t u; float f; } c; c.f = f; return c.u;
+}
+
+// CPU torch.log2 of the LBP arguments k/T^2 + 1e-10 is correctly rounded
+// except at these arguments (oracle LOG2_OVERRIDES, pinned by tests).
+MCAQ_HD float log2_ref(float a) {
+  const uint32_t b = float_as_bits(a);
+  switch (b) {
+    case 0x3F4ABC00u: return bits_as_float(0xBEAC50B0u);
+    case 0x3F553400u: return bits_as_float(0xBE871FE6u);
+    case 0x3F5F7400u: return bits_as_float(0xBE48E134u);
+    case 0x3F6C9400u: return bits_as_float(0xBDE91E32u);
+    case 0x3F78CC00u: return bits_as_float(0xBD28A796u);
+    case 0x3F7A7C00u: return bits_as_float(0xBD00B59Cu);
+    case 0x3F7B8000u: return bits_as_float(0xBCD1987Eu);
+    case 0x3F7BE800u: return bits_as_float(0xBCBE853Eu);
+    case 0x3F7CA400u: return bits_as_float(0xBC9C1DC6u);
+    case 0x3F7FFC00u: return bits_as_float(0xB8B8ABACu);
+    default: return cr_log2(a);
+  }
+}
+
+MCAQ_HD float fmax_(float a, float b) { return a > b ? a : b; }
+MCAQ_HD float fmin_(float a, float b) { return a < b ? a : b; }
+MCAQ_HD float clampf_(float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); }
+MCAQ_HD int imin_(int a, int b) { return a < b ? a : b; }
+MCAQ_HD int imax_(int a, int b) { return a > b ? a : b; }
+
+// ATen CPU multi_row_sum cascade (level_power 4, valid for n < 2^20):
+// rows are added into a0; after every full block of 16 the block folds into
+// a1, every 16 blocks a1 folds into a2, every 256 blocks a2 into a3.
+struct Cascade {
+  float a0, a1, a2, a3;
+  int i;
+  MCAQ_HD void init() { a0 = a1 = a2 = a3 = 0.0f; i = 0; }
+  MCAQ_HD void push(float v) {
+    a0 = a0 + v;
+    ++i;
+    if ((i & 15) == 0) {
+      a1 = a1 + a0; a0 = 0.0f;
+      if (i & 0xF0) return;
+      a2 = a2 + a1; a1 = 0.0f;
+      if (i & 0xF00) return;
+      a3 = a3 + a2; a2 = 0.0f;
+    }
+  }
+  MCAQ_HD float result() const { return ((a0 + a1) + a2) + a3; }
+};
+
+// Sum of n strided values in ATen's contiguous outer-reduction order.
+// tail == false: vectorized column (plain cascade); tail == true: row_sum
+// (4 interleaved cascades over rows k, k+4, ...; leftovers into partial 0).
+template <typename Load>
+MCAQ_HD float aten_sum(int n, bool tail, Load load) {
+  if (!tail) {
+    Cascade c; c.init();
+    for (int r = 0; r < n; ++r) c.push(load(r));
+    return c.result();
+  }
+  const int nilp = n / 4;
+  Cascade c0, c1, c2, c3;
+  c0.init(); c1.init(); c2.init(); c3.init();
+  for (int r = 0; r < nilp; ++r) {
+    c0.push(load(4 * r + 0));
+    c1.push(load(4 * r + 1));
+    c2.push(load(4 * r + 2));
+    c3.push(load(4 * r + 3));
+  }
+  float p0 = c0.result();
+  for (int r = 4 * nilp; r < n; ++r) p0 = p0 + load(r);
+  return ((p0 + c1.result()) + c2.result()) + c3.result();
+}
+
+// Column index where ATen's tail (row_sum) order starts for M columns.
+MCAQ_HD int aten_tail_start(int M) { return (M / 32) * 32; }
+
+// PyTorch upsample 'nearest' source index (UpSampleKernel nearest_idx).
+MCAQ_HD int nearest_src(int o, int in_size, int out_size) {
+  if (out_size == in_size) return o;
+  if (out_size == 2 * in_size) return o >> 1;
+  const float scale = (float)in_size / (float)out_size;
+  const int s = (int)floorf((float)o * scale);
+  return s < in_size - 1 ? s : in_size - 1;
+}
+
+// Quantization parameters (quantization.py:26-66) for integer bits b.
+struct QParam { float scale, zp, qmin, qmax; };
+MCAQ_HD QParam qparam(float xmin, float xmax, int b) {
+  QParam q;
+  const int qmin = -(1 << (b - 1)), qmax = (1 << (b - 1)) - 1;
+  float rng = xmax - xmin;
+  rng = rng < 1e-8f ? 1e-8f : rng;              // clamp(min=1e-8)
+  q.scale = rng / (float)(qmax - qmin);
+  float zp = (float)qmin - xmin / q.scale;
+  q.qmin = (float)qmin; q.qmax = (float)qmax;
+  q.zp = clampf_(zp, q.qmin, q.qmax);
+  return q;
+}
+// y = (clamp(rint(x/s + zp)) - zp) * s     (quantization.py:597-600)
+MCAQ_HD float quant_dequant(float x, const QParam& q) {
+  float t = x / q.scale + q.zp;
+  float r = clampf_(rintf(t), q.qmin, q.qmax);
+  return (r - q.zp) * q.scale;
+}
+
+}  // namespace mcaq

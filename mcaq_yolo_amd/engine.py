@@ -1,0 +1,238 @@
+"""Launch sequencing for the MCAQ hook path on MI355X.
+
+A step over up to three hook scales (C3/C4/C5) is four kernel launches on one
+HIP stream:
+
+    mcaq_stats     HBM pass 1: x -> gray, |x| channel means, min/max partials
+    mcaq_finalize  per-channel batch min/max      (+ optional RCCL all-reduce)
+    mcaq_morph     one workgroup per image: phi, complexity, bits, soft mask
+    mcaq_quant     HBM pass 2: y = dequant(quant_b(x)) * m
+
+All buffers of a `HookPlan` are allocated once, so `HookPlan.run` only
+enqueues launches and can be captured into a HIP graph (torch.cuda.CUDAGraph).
+There is no CPU path: non-CUDA tensors or a missing library raise.
+"""
+import ctypes
+
+import torch
+
+from . import abi
+
+
+def tile_size(H, grid_size):
+    """morphology.py:359-376: largest power of two <= max(4, H // grid)."""
+    raw = max(4, H // grid_size)
+    return 1 << (raw.bit_length() - 1)
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _require_cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("mcaq_yolo_amd runs on MI355X (HIP) only; got a %s tensor" % t.device)
+
+
+def _stream_handle(stream):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+class ScaleGeom:
+    """Shape bookkeeping for one hook scale."""
+
+    def __init__(self, B, C, H, W, grid_size):
+        self.B, self.C, self.H, self.W, self.grid = B, C, H, W, grid_size
+        self.tile = tile_size(H, grid_size)
+        self.ht, self.wt = H // self.tile, W // self.tile
+        self.Hc, self.Wc = self.ht * self.tile, self.wt * self.tile
+        if self.ht < 1 or self.wt < 1:
+            raise ValueError("feature map %dx%d smaller than one %d-pixel tile" % (H, W, self.tile))
+        if self.tile > 64:
+            raise ValueError("tile %d > 64 not supported (H=%d, grid=%d)" % (self.tile, H, grid_size))
+
+    @property
+    def key(self):
+        return (self.B, self.C, self.H, self.W, self.grid)
+
+
+class HookPlan:
+    """Buffers + launch descriptors for a fixed set of hook-scale shapes.
+
+    want: subset of {"phi", "cmlp", "debug"} extra outputs."""
+
+    def __init__(self, geoms, device, want=()):
+        if not 1 <= len(geoms) <= 3:
+            raise ValueError("1..3 scales per launch")
+        self.geoms = list(geoms)
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("HookPlan needs a CUDA (HIP) device")
+        self.lib = abi.lib()
+        d = self.device
+        self.bufs = []
+        for g in self.geoms:
+            units = self.lib.mcaq_stats_units(g.B, g.H, g.W)
+            nb = {}
+            nb["units"] = units
+            nb["gray"] = torch.empty(g.B, g.Hc, g.Wc, device=d)
+            nb["absmean"] = torch.empty(g.B, g.H, g.W, device=d)
+            nb["pmin"] = torch.empty(units, g.C, device=d)
+            nb["pmax"] = torch.empty(units, g.C, device=d)
+            nb["xmin"] = torch.empty(g.C, device=d)
+            nb["xmax"] = torch.empty(g.C, device=d)
+            nb["complexity"] = torch.empty(g.B, g.ht, g.wt, device=d)
+            nb["bits"] = torch.empty(g.B, g.ht, g.wt, device=d)
+            nb["m"] = torch.empty(g.B, 1, g.H, g.W, device=d)
+            nb["y"] = torch.empty(g.B, g.C, g.H, g.W, device=d)
+            nb["phi"] = torch.empty(g.B, g.ht, g.wt, 8, device=d) if "phi" in want else None
+            nb["cmlp"] = torch.empty(g.B, g.ht, g.wt, device=d) if "cmlp" in want else None
+            if "debug" in want:
+                nb["edge"] = torch.empty(g.B, g.Hc, g.Wc, device=d, dtype=torch.uint8)
+                nb["binmask"] = torch.empty(g.B, g.Hc, g.Wc, device=d, dtype=torch.uint8)
+            else:
+                nb["edge"] = nb["binmask"] = None
+            sb = self.lib.mcaq_morph_scratch_bytes(g.B, g.Hc, g.Wc, g.ht, g.wt)
+            nb["gscratch"] = torch.empty(max(sb, 16), device=d, dtype=torch.uint8) if sb else None
+            self.bufs.append(nb)
+
+    # ------------------------------------------------------------------
+    def run(self, feats, cmlp, mapper, smasks, stream=None, process_group=None, **kw):
+        """Enqueue one step (prepare + launch).  feats: list of (B,C,H,W) fp32
+        CUDA tensors matching the plan.  cmlp/mapper: packed blobs (CUDA fp32);
+        smasks: one packed soft-mask blob per scale or None
+        (smooth_transitions=False).  Keyword options: see prepare().  Returns
+        the buffer dicts (overwritten by the next run)."""
+        self.prepare(feats, cmlp, mapper, smasks, **kw)
+        self.launch(stream, process_group)
+        return self.bufs
+
+    def prepare(self, feats, cmlp, mapper, smasks, temperature=1.0, mapper_kind="mlp", continuous=False,
+                normalize=False, minmax=None, batch_offset=0, batch_total=None, binarize_otsu=False,
+                contour_components=True, min_bits=2.0, max_bits=8.0, quantize=True, hysteresis_iters=8):
+        """Validate inputs and build the launch descriptors (pointers are baked
+        in: the tensors must stay alive and in place until the last launch).
+        minmax: optional per-scale (xmin, xmax) frozen calibration stats."""
+        n = len(self.geoms)
+        L = self.lib
+        if len(feats) != n:
+            raise ValueError("expected %d feature maps" % n)
+        for f, g in zip(feats, self.geoms):
+            _require_cuda(f)
+            if f.dtype != torch.float32 or not f.is_contiguous() or tuple(f.shape) != (g.B, g.C, g.H, g.W):
+                raise ValueError("feature map must be contiguous fp32 %s, got %s %s"
+                                 % ((g.B, g.C, g.H, g.W), tuple(f.shape), f.dtype))
+        self._keep = (list(feats), cmlp, mapper, list(smasks), minmax)
+        with_mask = [sm is not None for sm in smasks]
+        # ---- pass 1
+        st = (abi.StatsScale * n)()
+        for i, (f, g, b) in enumerate(zip(feats, self.geoms, self.bufs)):
+            s = st[i]
+            s.x = _p(f)
+            s.gray = _p(b["gray"])
+            s.absmean = _p(b["absmean"]) if with_mask[i] else None
+            need_mm = quantize and (minmax is None or minmax[i] is None)
+            s.pmin = _p(b["pmin"]) if need_mm else None
+            s.pmax = _p(b["pmax"]) if need_mm else None
+            s.B, s.C, s.H, s.W, s.Hc, s.Wc = g.B, g.C, g.H, g.W, g.Hc, g.Wc
+        self._st = st
+        self._fz = self._qs = None
+        # ---- channel min/max
+        if quantize:
+            fz = (abi.FinalizeScale * n)()
+            for i, (g, b) in enumerate(zip(self.geoms, self.bufs)):
+                s = fz[i]
+                s.C, s.nunits, s.min_stride = g.C, b["units"], 1
+                s.min_out, s.max_out = _p(b["xmin"]), _p(b["xmax"])
+                if minmax is not None and minmax[i] is not None:
+                    lo, hi = minmax[i]
+                    _require_cuda(lo, hi)
+                    lo = lo.float().contiguous().reshape(-1)
+                    hi = hi.float().contiguous().reshape(-1)
+                    self._keep += (lo, hi)
+                    s.min_in, s.max_in = _p(lo), _p(hi)
+                    if lo.numel() == 1:
+                        s.min_stride = 0
+                else:
+                    s.pmin, s.pmax = _p(b["pmin"]), _p(b["pmax"])
+            self._fz = fz
+        # ---- morph
+        mo = (abi.MorphScale * n)()
+        flags = abi.F_PHI | abi.F_CMLP | abi.F_MAPPER | abi.F_HAS_T
+        if continuous:
+            flags |= abi.F_CONT
+        if normalize:
+            flags |= abi.F_NORM_C
+        if mapper_kind == "linear":
+            flags |= abi.F_MAP_LINEAR
+        if binarize_otsu:
+            flags |= abi.F_BIN_OTSU
+        if not contour_components:
+            flags |= abi.F_NO_EULER
+        T = max(float(temperature if temperature is not None else 1.0), 0.1)
+        for i, (g, b) in enumerate(zip(self.geoms, self.bufs)):
+            s = mo[i]
+            s.gray, s.absmean = _p(b["gray"]), _p(b["absmean"])
+            s.cmlp, s.mapper = _p(cmlp), _p(mapper) if mapper is not None else None
+            s.smask = _p(smasks[i]) if with_mask[i] else None
+            s.phi_out, s.cmlp_out = _p(b["phi"]), _p(b["cmlp"])
+            s.c_out, s.bits_out = _p(b["complexity"]), _p(b["bits"])
+            s.m_out = _p(b["m"]) if (with_mask[i] and quantize) else None
+            s.edge_out, s.bin_out = _p(b["edge"]), _p(b["binmask"])
+            s.gscratch = _p(b["gscratch"])
+            s.B, s.H, s.W, s.Hc, s.Wc = g.B, g.H, g.W, g.Hc, g.Wc
+            s.tile, s.ht, s.wt = g.tile, g.ht, g.wt
+            s.batch_offset = batch_offset
+            s.batch_total = batch_total if batch_total is not None else g.B
+            s.flags = flags | (abi.F_SOFTMASK if (with_mask[i] and quantize) else 0)
+            s.hyst_iters = hysteresis_iters
+            s.temperature, s.min_bits, s.max_bits = T, float(min_bits), float(max_bits)
+        self._mo = mo
+        # ---- pass 2
+        if quantize:
+            qs = (abi.QuantScale * n)()
+            lo_b = int(min_bits)
+            nb = int(max_bits) - lo_b + 1
+            for i, (f, g, b) in enumerate(zip(feats, self.geoms, self.bufs)):
+                s = qs[i]
+                s.x, s.y, s.bits = _p(f), _p(b["y"]), _p(b["bits"])
+                s.m = _p(b["m"]) if with_mask[i] else None
+                s.xmin, s.xmax = _p(b["xmin"]), _p(b["xmax"])
+                s.B, s.C, s.H, s.W, s.ht, s.wt = g.B, g.C, g.H, g.W, g.ht, g.wt
+                s.bits_lo, s.nbits = lo_b, nb
+            self._qs = qs
+        self._n = n
+
+    def launch(self, stream=None, process_group=None):
+        """Enqueue the prepared step on `stream` (default: current stream).
+        With a process group (batch sharded over ranks) the per-channel min/max
+        of every scale is combined by ONE all-reduce (max of [-min, max]) so
+        the quantizer sees the global-batch statistics of the reference."""
+        L = self.lib
+        n = self._n
+        sh = _stream_handle(stream)
+        abi.check(L.mcaq_stats(self._st, n, sh), "mcaq_stats")
+        if self._fz is not None:
+            abi.check(L.mcaq_finalize(self._fz, n, sh), "mcaq_finalize")
+            if process_group is not None:
+                sync_channel_minmax(self.bufs, process_group)
+        abi.check(L.mcaq_morph(self._mo, n, sh), "mcaq_morph")
+        if self._qs is not None:
+            abi.check(L.mcaq_quant(self._qs, n, sh), "mcaq_quant")
+        return self.bufs
+
+
+def sync_channel_minmax(bufs, process_group):
+    """Exact global-batch channel min/max across ranks with one all-reduce:
+    pack [-min_s, max_s] for every scale, reduce with MAX, unpack."""
+    import torch.distributed as dist
+    vec = torch.cat([t for b in bufs for t in (-b["xmin"], b["xmax"])])
+    dist.all_reduce(vec, op=dist.ReduceOp.MAX, group=process_group)
+    o = 0
+    for b in bufs:
+        C = b["xmin"].numel()
+        b["xmin"].copy_(-vec[o:o + C])
+        b["xmax"].copy_(vec[o + C:o + 2 * C])
+        o += 2 * C

@@ -1,0 +1,54 @@
+"""Pack reference-layout parameter tensors into the flat blobs the kernels read.
+
+The blob layouts are the CM_* / MM_* / SM_* offsets of
+mcaq_yolo_amd/csrc/mcaq_morph.h.  Input: mappings from the reference
+state_dict key suffixes (complexity_mlp.{0,1,3,4,6}.*, mapping_network.
+{0,1,3,4,6,7,9}.*, net.{0,2}.*) to tensors or arrays.
+"""
+import numpy as np
+
+CM_SIZE, MM_SIZE, SM_SIZE = 2881, 4865, 170
+
+
+def _f(a):
+    if hasattr(a, "detach"):
+        a = a.detach().cpu().numpy()
+    return np.asarray(a, np.float32).reshape(-1)
+
+
+def pack_complexity_mlp(sd, prefix="complexity_mlp."):
+    """morphology.py:81-90: Linear(8,64) LN(64) ReLU Linear(64,32) LN(32) ReLU Linear(32,1)."""
+    parts = [sd[prefix + "0.weight"], sd[prefix + "0.bias"], sd[prefix + "1.weight"], sd[prefix + "1.bias"],
+             sd[prefix + "3.weight"], sd[prefix + "3.bias"], sd[prefix + "4.weight"], sd[prefix + "4.bias"],
+             sd[prefix + "6.weight"], sd[prefix + "6.bias"]]
+    out = np.concatenate([_f(p) for p in parts])
+    if out.size != CM_SIZE:
+        raise ValueError("complexity MLP must be the reference 8-64-32-1 shape (got %d params)" % out.size)
+    return out
+
+
+def pack_mapper_mlp(sd, prefix="mapping_network."):
+    """bit_allocation.py:119-136 with hidden_dims [32, 64, 32]."""
+    parts = []
+    for lin, bn in ((0, 1), (3, 4), (6, 7)):
+        parts += [sd[prefix + "%d.weight" % lin], sd[prefix + "%d.bias" % lin]]
+        parts += [sd[prefix + "%d.%s" % (bn, k)] for k in ("weight", "bias", "running_mean", "running_var")]
+    parts += [sd[prefix + "9.weight"], sd[prefix + "9.bias"]]
+    out = np.concatenate([_f(p) for p in parts])
+    if out.size != MM_SIZE:
+        raise ValueError("bit mapper must use hidden_dims [32, 64, 32] (got %d params)" % out.size)
+    return out
+
+
+def pack_soft_mask(sd, prefix="net."):
+    """quantization.py:187-191: Conv2d(2,8,3) ReLU Conv2d(8,2,1)."""
+    parts = [sd[prefix + "0.weight"], sd[prefix + "0.bias"], sd[prefix + "2.weight"], sd[prefix + "2.bias"]]
+    out = np.concatenate([_f(p) for p in parts])
+    if out.size != SM_SIZE:
+        raise ValueError("soft mask must be the reference Conv2d(2,8,3)/Conv2d(8,2,1) net")
+    return out
+
+
+def sub(sd, prefix):
+    """Select keys under `prefix` and strip it."""
+    return {k[len(prefix):]: v for k, v in sd.items() if k.startswith(prefix)}

@@ -436,21 +436,26 @@ def linear(x, Wt, b):
     return (acc + b[None, :]).astype(f32)
 
 
+def tree_sum(x):
+    """Pairwise tree over the last axis (N a power of two): adjacent pairs are
+    added level by level.  This is the reduction order the HIP kernels use for
+    LayerNorm statistics (a 64-lane xor butterfly produces exactly this tree)."""
+    a = np.asarray(x, f32)
+    while a.shape[-1] > 1:
+        a = (a[..., 0::2] + a[..., 1::2]).astype(f32)
+    return a[..., 0]
+
+
 def layernorm(x, g, b, eps=1e-5):
-    """mean = seq_sum/N; var = seq_sum((x-mean)^2)/N; y = (x-mean)*rstd*g + b,
-    rstd = 1/sqrt(var+eps) (all fp32, no FMA)."""
+    """LayerNorm over the last axis with a fixed order (module docstring):
+    mean = tree_sum(x)/N; d = x - mean; var = tree_sum(d*d)/N;
+    rstd = 1/sqrt(var + eps); y = ((d * rstd) * g) + b   (fp32, no FMA)."""
     N = x.shape[-1]
-    s = np.zeros(x.shape[:-1], f32)
-    for k in range(N):
-        s = (s + x[..., k]).astype(f32)
-    mean = (s / f32(N)).astype(f32)
+    mean = (tree_sum(x) / f32(N)).astype(f32)
     d = (x - mean[..., None]).astype(f32)
-    v = np.zeros(x.shape[:-1], f32)
-    for k in range(N):
-        v = (v + (d[..., k] * d[..., k]).astype(f32)).astype(f32)
-    var = (v / f32(N)).astype(f32)
+    var = (tree_sum((d * d).astype(f32)) / f32(N)).astype(f32)
     rstd = (f32(1.0) / cr32(np.sqrt, (var + f32(eps)).astype(f32))).astype(f32)
-    return ((d * rstd[..., None]).astype(f32) * g[None, :] + b[None, :]).astype(f32)
+    return (((d * rstd[..., None]).astype(f32) * g[None, :]).astype(f32) + b[None, :]).astype(f32)
 
 
 def sigmoid(z):

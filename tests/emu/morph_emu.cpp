@@ -1,0 +1,23 @@
+// Host emulation of the gfx950 morph kernel (TEST TOOL, never shipped).
+// Compiles the very same mcaq_morph.h with g++ and runs morph_image() with a
+// single "thread", so tests can compare the kernel's arithmetic with the
+// numpy oracle on CPU.  Built by tests/emu/build_emu.py.
+#define MCAQ_NO_HIP 1
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+#include "../../mcaq_yolo_amd/csrc/mcaq_morph.h"
+
+extern "C" int emu_morph(const mcaq_morph_scale* s) {
+  using namespace mcaq;
+  const int P = s->Hc * s->Wc, NT = s->ht * s->wt;
+  std::vector<char> planes(plane_bytes(P) + 64), shm(fixed_bytes() + tile_bytes(NT) + 64);
+  for (int b = 0; b < s->B; ++b) {
+    Planes pl; Shared sh;
+    carve_planes(planes.data(), P, pl);
+    carve_shared(shm.data(), NT, sh);
+    Ctx ctx{0, 1};
+    morph_image(ctx, *s, b, pl, sh);
+  }
+  return 0;
+}

@@ -1,0 +1,118 @@
+"""Host emulation of the gfx950 morph kernel (same mcaq_morph.h source, one
+thread) against the oracle: every output bit-exact, on every golden case and
+both mappers, plus the option flags.  Catches arithmetic-order mistakes in the
+kernel source without a GPU."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, case_names, load_case, load_weights
+from oracle import mcaq_oracle as O
+
+sys.path.insert(0, os.path.join(ROOT, "tests", "emu"))
+import build_emu  # noqa: E402
+
+from mcaq_yolo_amd import abi, params  # noqa: E402
+
+f32 = np.float32
+
+
+@pytest.fixture(scope="module")
+def emu():
+    lib = ctypes.CDLL(build_emu.build())
+    lib.emu_morph.argtypes = [ctypes.POINTER(abi.MorphScale)]
+    W = load_weights()
+    blobs = (params.pack_complexity_mlp(params.sub(W, "complexity_analyzer.")),
+             params.pack_mapper_mlp(params.sub(W, "bit_mapper.")),
+             params.pack_soft_mask(params.sub(W, "soft_mask.")))
+    return lib, W, blobs
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def run_emu(emu, x, grid, flags, T=1.0, c_in=None, bits_in=None):
+    lib, W, (cm, mm, sm) = emu
+    B, C, H, Wd = x.shape
+    tile = O.tile_size(H, grid)
+    ht, wt = H // tile, Wd // tile
+    Hc, Wc = ht * tile, wt * tile
+    gray = O.channel_mean(x, Hc, Wc)
+    am = O.abs_channel_mean(x)
+    out = dict(phi=np.zeros((B, ht, wt, 8), f32), cmlp=np.zeros((B, ht, wt), f32),
+               c=np.zeros((B, ht, wt), f32), bits=np.zeros((B, ht, wt), f32),
+               m=np.zeros((B, H, Wd), f32), edge=np.zeros((B, Hc, Wc), np.uint8),
+               bin=np.zeros((B, Hc, Wc), np.uint8))
+    s = abi.MorphScale()
+    s.gray, s.absmean, s.cmlp, s.mapper, s.smask = _ptr(gray), _ptr(am), _ptr(cm), _ptr(mm), _ptr(sm)
+    s.c_in, s.bits_in = _ptr(c_in), _ptr(bits_in)
+    s.phi_out, s.cmlp_out, s.c_out = _ptr(out["phi"]), _ptr(out["cmlp"]), _ptr(out["c"])
+    s.bits_out, s.m_out, s.edge_out, s.bin_out = _ptr(out["bits"]), _ptr(out["m"]), _ptr(out["edge"]), _ptr(out["bin"])
+    s.B, s.H, s.W, s.Hc, s.Wc, s.tile, s.ht, s.wt = B, H, Wd, Hc, Wc, tile, ht, wt
+    s.batch_offset, s.batch_total = 0, B
+    s.flags = flags
+    s.hyst_iters = 8
+    s.temperature, s.min_bits, s.max_bits = max(T, 0.1), 2.0, 8.0
+    lib.emu_morph(ctypes.byref(s))
+    return out
+
+
+ALL = abi.F_PHI | abi.F_CMLP | abi.F_MAPPER | abi.F_SOFTMASK | abi.F_HAS_T
+CASES = [c for c in case_names() if c != "t64_c1"]
+
+
+@pytest.mark.parametrize("name", CASES)
+@pytest.mark.parametrize("mapper", ["mlp", "linear"])
+def test_emu_matches_oracle(emu, name, mapper):
+    d = load_case(name)
+    x = d["x"].astype(f32)
+    grid = int(d["grid"])
+    flags = ALL | (abi.F_MAP_LINEAR if mapper == "linear" else 0)
+    out = run_emu(emu, x, grid, flags)
+    ref = O.hook_forward(x, emu[1], grid, mapper=mapper)
+    _, I = O.phi_tiles(x, grid, internals=True)
+    assert np.array_equal(out["edge"], I["edge"])
+    assert np.array_equal(out["bin"], I["binmask"])
+    assert np.array_equal(out["phi"], ref["phi"])
+    assert np.array_equal(out["cmlp"], ref["c_mlp"])
+    assert np.array_equal(out["c"], ref["complexity"])
+    assert np.array_equal(out["bits"], ref["bits"])
+    assert np.array_equal(out["m"], ref["m"])
+    assert np.array_equal(out["bits"], d["bits_mlp" if mapper == "mlp" else "bits_lin"])
+
+
+def test_emu_options(emu):
+    """normalize_complexity, continuous bits, temperature, Otsu binarize,
+    no Euler correction, mapper-only and softmask-only stages."""
+    d = load_case("p4_c32")
+    x = d["x"].astype(f32)
+    W = emu[1]
+    # continuous + normalize + T=0.7
+    out = run_emu(emu, x, 8, ALL | abi.F_CONT | abi.F_NORM_C, T=0.7)
+    C, _, _ = O.analyzer_forward(x, W, 8)
+    want = O.mlp_mapper(O.normalize_complexity(C), W, 0.7, continuous=True)
+    assert np.array_equal(out["bits"], want)
+    # mapper-only from given complexity (linear, T=10 -> all 8)
+    c_in = d["complexity"].astype(f32).copy()
+    out = run_emu(emu, x, 8, abi.F_MAPPER | abi.F_MAP_LINEAR | abi.F_HAS_T, T=10.0, c_in=c_in)
+    assert np.all(out["bits"] == 8.0)
+    # softmask-only from given bits
+    bits_in = d["bits_lin"].astype(f32).copy()
+    out = run_emu(emu, x, 8, abi.F_SOFTMASK, bits_in=bits_in)
+    assert np.array_equal(out["m"], O.soft_mask(bits_in, x, W))
+
+
+def test_emu_otsu_binarize_and_no_euler(emu):
+    d = load_case("p3_c16")
+    x = d["x"].astype(f32)
+    out = run_emu(emu, x, 8, abi.F_PHI | abi.F_BIN_OTSU | abi.F_NO_EULER)
+    tile = 8
+    gray = O.normalize01(O.channel_mean(x, 80, 80))
+    thr = O.otsu_threshold(gray)
+    binm = (gray > thr[:, None, None]).astype(np.uint8)
+    assert np.array_equal(out["bin"], binm)
+    assert np.array_equal(out["phi"][..., 4], O.contour_tiles(binm, tile, contour_components=False))

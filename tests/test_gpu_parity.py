@@ -1,0 +1,211 @@
+"""GPU parity: the HIP path (through the C ABI) against the golden fixtures and
+the oracle.  Bit-exact everywhere the oracle is bit-exact:
+
+  gray, edge map, adaptive mask, phi, complexity, bits, m, channel min/max, y
+
+(the oracle reproduces the reference exactly on the decision path; against the
+fixtures themselves complexity is within 1e-6 relative and phi8 within 1 ulp,
+see test_oracle_cpu.py).  Tolerances are written where they apply.
+"""
+import numpy as np
+import pytest
+
+from conftest import case_names, load_case, load_weights
+from oracle import mcaq_oracle as O
+
+pytestmark = pytest.mark.gpu
+f32 = np.float32
+
+
+@pytest.fixture(scope="module")
+def dev():
+    import torch
+    from mcaq_yolo_amd import abi
+    abi.lib()   # fails loudly if the library is missing
+    return torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def blobs(dev):
+    import torch
+    from mcaq_yolo_amd import params
+    W = load_weights()
+    cm = torch.from_numpy(params.pack_complexity_mlp(params.sub(W, "complexity_analyzer."))).to(dev)
+    mm = torch.from_numpy(params.pack_mapper_mlp(params.sub(W, "bit_mapper."))).to(dev)
+    sm = torch.from_numpy(params.pack_soft_mask(params.sub(W, "soft_mask."))).to(dev)
+    return W, cm, mm, sm
+
+
+def run_plan(dev, blobs, xs, grid, mapper="mlp", T=1.0, **kw):
+    import torch
+    from mcaq_yolo_amd.engine import HookPlan, ScaleGeom
+    W, cm, mm, sm = blobs
+    feats = [torch.from_numpy(x).to(dev) for x in xs]
+    geoms = [ScaleGeom(*f.shape, grid) for f in feats]
+    plan = HookPlan(geoms, dev, want=("phi", "cmlp", "debug"))
+    bufs = plan.run(feats, cm, mm, [sm] * len(feats), temperature=T, mapper_kind=mapper, **kw)
+    torch.cuda.synchronize()
+    return [{k: (v.cpu().numpy() if hasattr(v, "cpu") else v) for k, v in b.items()} for b in bufs]
+
+
+def check_against_oracle(out, x, W, grid, mapper, T=1.0):
+    ref = O.hook_forward(x, W, grid, mapper=mapper, temperature=T)
+    B, C, H, Wd = x.shape
+    tile = O.tile_size(H, grid)
+    Hc, Wc = (H // tile) * tile, (Wd // tile) * tile
+    _, I = O.phi_tiles(x, grid, internals=True)
+    assert np.array_equal(out["gray"], I["gray_raw"]), "gray"
+    assert np.array_equal(out["absmean"], O.abs_channel_mean(x)), "absmean"
+    assert np.array_equal(out["edge"], I["edge"]), "edge"
+    assert np.array_equal(out["binmask"], I["binmask"]), "binmask"
+    assert np.array_equal(out["phi"], ref["phi"]), "phi"
+    assert np.array_equal(out["cmlp"], ref["c_mlp"]), "complexity MLP"
+    assert np.array_equal(out["complexity"], ref["complexity"]), "complexity"
+    assert np.array_equal(out["bits"], ref["bits"]), "bits"
+    assert np.array_equal(out["xmin"], ref["xmin"]) and np.array_equal(out["xmax"], ref["xmax"]), "minmax"
+    assert np.array_equal(out["m"][:, 0], ref["m"]), "soft mask"
+    assert np.array_equal(out["y"], ref["y"]), "y"
+    return ref
+
+
+@pytest.mark.parametrize("name", [c for c in case_names() if c not in ("t64_c1",)])
+@pytest.mark.parametrize("mapper", ["mlp", "linear"])
+def test_golden_case(dev, blobs, name, mapper):
+    d = load_case(name)
+    x = d["x"].astype(f32)
+    grid = int(d["grid"])
+    out = run_plan(dev, blobs, [x], grid, mapper)[0]
+    key = "mlp" if mapper == "mlp" else "lin"
+    # against the reference's own outputs
+    if "gray_raw" in d.files:
+        assert np.array_equal(out["gray"], d["gray_raw"])
+    assert np.array_equal(out["edge"], d["edge"])
+    assert np.array_equal(out["binmask"], d["binmask"])
+    assert np.array_equal(out["bits"], d["bits_" + key]), "tile bits must be bit-exact vs reference"
+    rel = np.abs(out["complexity"] - d["complexity"]) / np.abs(d["complexity"])
+    assert rel.max() < 1e-6
+    assert np.array_equal(out["xmin"], d["xmin"]) and np.array_equal(out["xmax"], d["xmax"])
+    tol_m = 0 if name != "b1_c16" else 1e-6
+    assert np.all(np.abs(out["m"][:, 0] - d["m_" + key]) <= tol_m * np.abs(d["m_" + key]))
+    if ("y_" + key) in d.files:
+        if name != "b1_c16":
+            assert np.array_equal(out["y"], d["y_" + key])
+        else:
+            assert np.allclose(out["y"], d["y_" + key], rtol=1e-4, atol=0)
+    # against the oracle: everything bit-exact
+    check_against_oracle(out, x, blobs[0], grid, mapper)
+
+
+def test_three_scales_one_launch(dev, blobs):
+    """C3/C4/C5 of one batch in a single set of launches == per-scale oracle."""
+    xs = [load_case(n)["x"].astype(f32) for n in ("full_p3", "full_p4", "full_p5")]
+    outs = run_plan(dev, blobs, xs, 8, "mlp")
+    for o, x in zip(outs, xs):
+        check_against_oracle(o, x, blobs[0], 8, "mlp")
+
+
+@pytest.mark.parametrize("shape,grid", [((3, 24, 48, 48), 8), ((2, 40, 36, 60), 8), ((4, 8, 80, 80), 16),
+                                        ((1, 12, 33, 41), 8)])
+def test_random_shapes_vs_oracle(dev, blobs, shape, grid):
+    rng = np.random.default_rng(sum(shape))
+    x = (rng.standard_normal(shape) * 1.5).astype(f32)
+    x = np.where(x > 0, x, x * f32(0.1)).astype(f32)
+    out = run_plan(dev, blobs, [x], grid, "linear")[0]
+    check_against_oracle(out, x, blobs[0], grid, "linear")
+
+
+def test_large_map_global_planes(dev, blobs):
+    """t64_c1 (640x640, tile 64): planes do not fit LDS -> global workspace path."""
+    d = load_case("t64_c1")
+    x = d["x"].astype(f32)
+    out = run_plan(dev, blobs, [x], 8, "linear")[0]
+    assert np.array_equal(out["edge"], d["edge"])
+    assert np.array_equal(out["binmask"], d["binmask"])
+    assert np.array_equal(out["bits"], d["bits_lin"])
+    assert np.array_equal(out["y"][:, :2], d["y_lin_head"])
+
+
+def test_constant_and_degenerate_inputs(dev, blobs):
+    """All-zero map (normalisation denominator 1e-8, flat Otsu), constant
+    channels (zero range -> scale clamp), all-positive channels (zp clamp)."""
+    x = np.zeros((2, 8, 40, 40), f32)
+    x[:, 3] = 1.5
+    x[:, 5] = np.linspace(0.1, 2.0, 1600, dtype=f32).reshape(40, 40)
+    out = run_plan(dev, blobs, [x], 8, "linear")[0]
+    check_against_oracle(out, x, blobs[0], 8, "linear")
+
+
+def test_options_vs_oracle(dev, blobs):
+    """continuous bits / normalize_complexity / temperature / frozen stats."""
+    import torch
+    d = load_case("p4_c32")
+    x = d["x"].astype(f32)
+    W = blobs[0]
+    out = run_plan(dev, blobs, [x], 8, "mlp", T=0.7, continuous=True, normalize=True)[0]
+    C, _, _ = O.analyzer_forward(x, W, 8)
+    assert np.array_equal(out["bits"], O.mlp_mapper(O.normalize_complexity(C), W, 0.7, continuous=True))
+    out = run_plan(dev, blobs, [x], 8, "mlp", T=10.0)[0]
+    assert np.all(out["bits"] == 8.0)
+    lo = torch.full((32,), -0.5, device=dev)
+    hi = torch.full((32,), 3.0, device=dev)
+    out = run_plan(dev, blobs, [x], 8, "linear", minmax=[(lo, hi)])[0]
+    ref = O.hook_forward(x, W, 8, mapper="linear", xmin=np.full(32, -0.5, f32), xmax=np.full(32, 3.0, f32))
+    assert np.array_equal(out["y"], ref["y"])
+
+
+def test_spatial_quantize_compat(dev):
+    """mcaq_launch_spatial_quantization (the reference kernel contract) vs the
+    oracle, divisible and remainder tiles, with and without mask; and the
+    reference's own parity test semantics (tests/test_smoke.py:226-246)."""
+    import ctypes
+    import torch
+    from mcaq_yolo_amd import abi
+    L = abi.lib()
+    rng = np.random.default_rng(7)
+    for (N, C, H, W_, Ht, Wt) in ((2, 8, 32, 32, 4, 4), (2, 5, 10, 13, 4, 3), (1, 3, 7, 9, 2, 2)):
+        x = rng.standard_normal((N, C, H, W_)).astype(f32)
+        bits = rng.integers(1, 10, (N, Ht, Wt)).astype(f32)
+        mask = rng.random((N, 1, H, W_)).astype(f32)
+        mn, mx = x.min(axis=(0, 2, 3)), x.max(axis=(0, 2, 3))
+        th, tw = H // Ht, W_ // Wt
+        for m in (None, mask):
+            tx, tb = torch.from_numpy(x).cuda(), torch.from_numpy(bits).cuda()
+            tmn, tmx = torch.from_numpy(mn).cuda(), torch.from_numpy(mx).cuda()
+            tm = torch.from_numpy(m).cuda() if m is not None else None
+            y = torch.empty_like(tx)
+            p = lambda t: None if t is None else ctypes.c_void_p(t.data_ptr())
+            err = L.mcaq_launch_spatial_quantization(p(tx), p(tb), p(tmn), p(tmx), p(tm), p(y), N, C, H, W_,
+                                                     th, tw, Ht, Wt,
+                                                     ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+            assert err == 0
+            torch.cuda.synchronize()
+            want = O.spatial_quantize_compat(x, bits, mn, mx, th, tw, m)
+            assert np.array_equal(y.cpu().numpy(), want)
+
+
+def test_bench_config_properties(dev, blobs):
+    """yolov8n bs32 640x640 (BASELINE config 2) at full size: determinism,
+    bits in [2, 8], per-channel min/max exact vs torch, and the first two
+    images bit-exact vs the oracle (batch min/max passed in)."""
+    import torch
+    from mcaq_yolo_amd.engine import HookPlan, ScaleGeom
+    W, cm, mm, sm = blobs
+    g = torch.Generator(device="cpu").manual_seed(2)
+    shapes = [(32, 64, 80, 80), (32, 128, 40, 40), (32, 256, 20, 20)]
+    feats = [torch.nn.functional.silu(1.5 * torch.randn(s, generator=g)).to(dev) for s in shapes]
+    plan = HookPlan([ScaleGeom(*s, 8) for s in shapes], dev)
+    bufs = plan.run(feats, cm, mm, [sm] * 3)
+    y1 = [b["y"].clone() for b in bufs]
+    bufs = plan.run(feats, cm, mm, [sm] * 3)
+    torch.cuda.synchronize()
+    for f, b, yy in zip(feats, bufs, y1):
+        assert torch.equal(b["y"], yy), "non-deterministic"
+        assert torch.equal(b["xmin"], f.amin(dim=(0, 2, 3))) and torch.equal(b["xmax"], f.amax(dim=(0, 2, 3)))
+        bits = b["bits"]
+        assert bool(((bits >= 2) & (bits <= 8) & (bits == bits.round())).all())
+        assert bool(torch.isfinite(b["y"]).all())
+    for f, b in zip(feats, bufs):
+        x2 = f[:2].cpu().numpy()
+        ref = O.hook_forward(x2, W, 8, xmin=b["xmin"].cpu().numpy(), xmax=b["xmax"].cpu().numpy())
+        assert np.array_equal(b["bits"][:2].cpu().numpy(), ref["bits"])
+        assert np.array_equal(b["y"][:2].cpu().numpy(), ref["y"])

@@ -1,0 +1,59 @@
+"""The C-ABI library: builds for gfx950, loads without a GPU, exports every
+symbol include/mcaq_hip.h declares, and its ctypes mirror matches the header."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+from mcaq_yolo_amd import abi
+
+HDR = os.path.join(ROOT, "include", "mcaq_hip.h")
+
+
+def declared_functions():
+    src = open(HDR).read()
+    return sorted(set(re.findall(r"^(?:int|size_t)\s+(mcaq_\w+)\s*\(", src, re.M)))
+
+
+def test_library_built_and_exports_header_symbols():
+    if not os.path.exists(abi.LIB_PATH):
+        pytest.skip("library not built (run __graft_entry__.build())")
+    lib = ctypes.CDLL(abi.LIB_PATH)
+    names = declared_functions()
+    assert set(names) == set(abi.EXPORTS)
+    for n in names:
+        assert hasattr(lib, n), n
+    assert lib.mcaq_abi_version() == abi.ABI_VERSION
+
+
+def test_struct_layouts_match_header():
+    """Field order / count of the ctypes mirrors equal the C structs."""
+    src = open(HDR).read()
+    for cname, py in (("mcaq_stats_scale", abi.StatsScale), ("mcaq_finalize_scale", abi.FinalizeScale),
+                      ("mcaq_morph_scale", abi.MorphScale), ("mcaq_quant_scale", abi.QuantScale)):
+        body = re.search(r"typedef struct \{([^{}]*)\} %s;" % cname, src).group(1)
+        body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+        fields = []
+        for decl in body.split(";"):
+            decl = decl.strip()
+            if not decl:
+                continue
+            names = decl.split(None, 1)[1] if not decl.startswith("const") else decl.split(None, 2)[2]
+            for n in names.split(","):
+                fields.append(n.strip().lstrip("*").strip())
+        assert fields == [f[0] for f in py._fields_], cname
+
+
+def test_invalid_args_rejected_without_gpu():
+    """Size validation happens before any launch (no GPU needed)."""
+    if not os.path.exists(abi.LIB_PATH):
+        pytest.skip("library not built")
+    lib = abi._declare(ctypes.CDLL(abi.LIB_PATH))
+    err = lib.mcaq_launch_spatial_quantization(None, None, None, None, None, None, 0, 1, 1, 1, 1, 1, 1, 1, None)
+    assert err != 0
+    s = abi.MorphScale()
+    s.tile = 3
+    assert lib.mcaq_morph(ctypes.byref(s), 1, None) != 0
+    assert lib.mcaq_stats(ctypes.byref(abi.StatsScale()), 0, None) != 0

@@ -1,0 +1,37 @@
+"""Build the in-tree native library mcaq_yolo_amd/lib/libmcaq_hip.so for gfx950.
+
+    python tools/build.py [--force]
+
+One hipcc invocation; the library links libamdhip64 by SONAME, so inside a
+Python process that imported torch first it binds to torch's HIP runtime (one
+runtime per process; checked by tests/test_lib_cpu.py on the GPU box)."""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(ROOT, "mcaq_yolo_amd", "csrc")
+OUT = os.path.join(ROOT, "mcaq_yolo_amd", "lib", "libmcaq_hip.so")
+SRCS = [os.path.join(CSRC, "mcaq_kernels.hip")]
+DEPS = SRCS + [os.path.join(CSRC, f) for f in ("mcaq_math.h", "mcaq_morph.h", "mcaq_tables.h")] + \
+    [os.path.join(ROOT, "include", "mcaq_hip.h")]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+         "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-result"]
+
+
+def build(force=False, verbose=True):
+    if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in DEPS):
+        return OUT
+    os.makedirs(os.path.dirname(OUT), exist_ok=True)
+    tmp = OUT + ".tmp"
+    cmd = [HIPCC] + FLAGS + ["-o", tmp] + SRCS
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv))
