@@ -113,10 +113,8 @@ def main():
     plan = HookPlan([ScaleGeom(B, c, h, w, grid) for c, (h, w) in zip(chans, SIZES)], dev)
     plan.prepare(feats, cm, mm, [sm, sm, sm], temperature=1.0, mapper_kind=mapper,
                  batch_offset=rank * B, batch_total=world * B)
-    stream = torch.cuda.current_stream()
-
     def step():
-        plan.launch(stream, pg)
+        plan.launch(torch.cuda.current_stream(), pg)   # the capture stream inside graph capture
 
     use_graph = (world == 1) and not args.eager
     graph = None
@@ -134,6 +132,7 @@ def main():
 
     # per-kernel device time (HIP events on the launch stream), untimed pass
     L = plan.lib
+    stream = torch.cuda.current_stream()
     from mcaq_yolo_amd import abi
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
     kt = {"stats": 0.0, "finalize": 0.0, "morph": 0.0, "quant": 0.0}

@@ -22,6 +22,13 @@
 
 using namespace mcaq;
 
+#if defined(MCAQ_STAMPS)
+namespace mcaq { __device__ unsigned long long g_mcaq_stamps[64]; }
+extern "C" int mcaq_read_stamps(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(mcaq::g_mcaq_stamps), sizeof(mcaq::g_mcaq_stamps));
+}
+#endif
+
 // ---------------------------------------------------------------------------
 // pass 1
 // ---------------------------------------------------------------------------
@@ -42,80 +49,95 @@ struct StatsArgs {
   int units_total;
 };
 
-// unit = one wave = 256 consecutive pixels (64 lanes x 4) of one image
+constexpr int ST_PIX = 256;   // pixels per workgroup (one per lane)
+constexpr int ST_CG = 16;     // channels per load group (= one ATen cascade block)
+
+// unit = one 256-thread workgroup = 256 consecutive pixels of one image.
+// Lane = pixel: the channel loop runs the ATen cascade in registers; each
+// 16-channel group is one cascade block (a0 summed from 0, then folded).
+// Channel min/max: the group's values go through an LDS transpose
+// [16 ch][256 px] and are reduced by 16 threads per channel.
 __global__ __launch_bounds__(256) void mcaq_stats_kernel(StatsArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int unit = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (unit >= a.units_total) return;
+  __shared__ float tmn[ST_CG][ST_PIX + 4];
+  __shared__ float tmx[ST_CG][ST_PIX + 4];
+  const int unit = blockIdx.x;
   int si = 0;
   while (si + 1 < a.nscales && unit >= a.s[si + 1].unit_begin) ++si;
   const mcaq_stats_scale& S = a.s[si];
+  const int tid = threadIdx.x;
   const int lu = unit - S.unit_begin;
   const int HW = S.H * S.W;
-  const int upi = (HW + 255) / 256;
+  const int upi = (HW + ST_PIX - 1) / ST_PIX;
   const int b = lu / upi, chunk = lu - b * upi;
   const int C = S.C;
   const float* xb = S.x + (size_t)b * C * HW;
   const bool cropped = (S.Hc != S.H) || (S.Wc != S.W);
-  const int cut = aten_tail_start(HW);
-  const int p0 = chunk * 256 + lane * 4;
-
-  Cascade cg[4], ca[4];
-  float sq[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) { cg[k].init(); ca[k].init(); sq[k] = 0.0f; }
-  bool valid[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) valid[k] = (p0 + k) < HW;
-  const bool vec4 = ((HW & 3) == 0) && valid[3];
+  const int p = chunk * ST_PIX + tid;
+  const bool valid = p < HW;
   const bool want_g = S.gray != nullptr, want_a = S.absmean != nullptr, want_m = S.pmin != nullptr;
+  const float* px = xb + (valid ? p : 0);
 
-  for (int c = 0; c < C; ++c) {
-    float v[4];
-    const float* row = xb + (size_t)c * HW;
-    if (vec4) {
-      const float4 q = *reinterpret_cast<const float4*>(row + p0);
-      v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
-    } else {
+  float g1 = 0.0f, g2 = 0.0f, g3 = 0.0f;   // cascade levels 1..3 (gray)
+  float a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;   // cascade levels 1..3 (|x|)
+  float ga0 = 0.0f, aa0 = 0.0f;            // open (partial) block
+  float sq = 0.0f;                          // sequential sum (cropped view)
+  int nblk = 0;
+  for (int c0 = 0; c0 < C; c0 += ST_CG) {
+    const int nc = C - c0 < ST_CG ? C - c0 : ST_CG;
+    float v[ST_CG];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = valid[k] ? row[p0 + k] : 0.0f;
+    for (int i = 0; i < ST_CG; ++i) v[i] = (valid && i < nc) ? px[(size_t)(c0 + i) * HW] : 0.0f;
+    float gb = 0.0f, ab = 0.0f;
+#pragma unroll
+    for (int i = 0; i < ST_CG; ++i) {
+      if (i < nc) { gb = gb + v[i]; ab = ab + fabsf(v[i]); sq = sq + v[i]; }
     }
-    float lmn = 3.402823466e38f, lmx = -3.402823466e38f;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (want_g) { cg[k].push(v[k]); sq[k] = sq[k] + v[k]; }
-      if (want_a) ca[k].push(fabsf(v[k]));
-      if (valid[k]) { lmn = fminf(lmn, v[k]); lmx = fmaxf(lmx, v[k]); }
+    if (nc == ST_CG) {       // a full cascade block: fold (Cascade::push at i % 16 == 0)
+      ++nblk;
+      g1 = g1 + gb; a1 = a1 + ab;
+      if ((nblk & 15) == 0) {
+        g2 = g2 + g1; g1 = 0.0f; a2 = a2 + a1; a1 = 0.0f;
+        if ((nblk & 255) == 0) { g3 = g3 + g2; g2 = 0.0f; a3 = a3 + a2; a2 = 0.0f; }
+      }
+    } else {
+      ga0 = gb; aa0 = ab;   // trailing partial block stays in a0
     }
     if (want_m) {
-      lmn = wave_min(lmn);
-      lmx = wave_max(lmx);
-      if (lane == 0) {
-        S.pmin[(size_t)lu * C + c] = lmn;
-        S.pmax[(size_t)lu * C + c] = lmx;
+#pragma unroll
+      for (int i = 0; i < ST_CG; ++i) {
+        tmn[i][tid] = valid ? v[i] : 3.402823466e38f;
+        tmx[i][tid] = valid ? v[i] : -3.402823466e38f;
       }
+      __syncthreads();
+      const int ci = tid >> 4, part = tid & 15;
+      float mn = tmn[ci][part * 16], mx = tmx[ci][part * 16];
+#pragma unroll
+      for (int k = 1; k < 16; ++k) { mn = fminf(mn, tmn[ci][part * 16 + k]); mx = fmaxf(mx, tmx[ci][part * 16 + k]); }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) { mn = fminf(mn, __shfl_xor(mn, o, 64)); mx = fmaxf(mx, __shfl_xor(mx, o, 64)); }
+      if (part == 0 && ci < nc) {
+        S.pmin[(size_t)lu * C + c0 + ci] = mn;
+        S.pmax[(size_t)lu * C + c0 + ci] = mx;
+      }
+      __syncthreads();
     }
   }
+  if (!valid) return;
   const float fC = (float)C;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int p = p0 + k;
-    if (!valid[k]) continue;
-    const bool tail = p >= cut;
-    if (want_a) {
-      float s = ca[k].result();
-      if (tail) s = aten_sum(C, true, [&](int r) { return fabsf(xb[(size_t)r * HW + p]); });
-      S.absmean[(size_t)b * HW + p] = s / fC;
-    }
-    if (want_g) {
-      const int h = p / S.W, w = p - (p / S.W) * S.W;
-      if (cropped) {
-        if (h < S.Hc && w < S.Wc) S.gray[((size_t)b * S.Hc + h) * S.Wc + w] = sq[k] / fC;
-      } else {
-        float s = cg[k].result();
-        if (tail) s = aten_sum(C, true, [&](int r) { return xb[(size_t)r * HW + p]; });
-        S.gray[(size_t)b * HW + p] = s / fC;
-      }
+  const bool tail = p >= aten_tail_start(HW);
+  if (want_a) {
+    float s = ((aa0 + a1) + a2) + a3;
+    if (tail) s = aten_sum(C, true, [&](int r) { return fabsf(xb[(size_t)r * HW + p]); });
+    S.absmean[(size_t)b * HW + p] = s / fC;
+  }
+  if (want_g) {
+    const int h = p / S.W, w = p - (p / S.W) * S.W;
+    if (cropped) {
+      if (h < S.Hc && w < S.Wc) S.gray[((size_t)b * S.Hc + h) * S.Wc + w] = sq / fC;
+    } else {
+      float s = ((ga0 + g1) + g2) + g3;
+      if (tail) s = aten_sum(C, true, [&](int r) { return xb[(size_t)r * HW + p]; });
+      S.gray[(size_t)b * HW + p] = s / fC;
     }
   }
 }
@@ -128,52 +150,85 @@ struct FinalizeArgs {
   int nscales;
 };
 
+// one workgroup = 64 channels x 4 unit-parts
 __global__ __launch_bounds__(256) void mcaq_finalize_kernel(FinalizeArgs a) {
+  __shared__ float rmn[4][64], rmx[4][64];
   int si = 0;
   while (si + 1 < a.nscales && (int)blockIdx.x >= a.s[si + 1].block_begin) ++si;
   const mcaq_finalize_scale& S = a.s[si];
-  const int c = ((int)blockIdx.x - S.block_begin) * 256 + threadIdx.x;
-  if (c >= S.C) return;
-  float mn, mx;
-  if (S.pmin) {
-    mn = 3.402823466e38f; mx = -3.402823466e38f;
-    for (int u = 0; u < S.nunits; ++u) {
-      mn = fminf(mn, S.pmin[(size_t)u * S.C + c]);
-      mx = fmaxf(mx, S.pmax[(size_t)u * S.C + c]);
+  const int cl = threadIdx.x & 63, part = threadIdx.x >> 6;
+  const int c = ((int)blockIdx.x - S.block_begin) * 64 + cl;
+  const bool cv = c < S.C;
+  float mn = 3.402823466e38f, mx = -3.402823466e38f;
+  if (cv) {
+    if (S.pmin) {
+      int u = part;
+      for (; u + 12 < S.nunits; u += 16) {
+        const float m0 = S.pmin[(size_t)u * S.C + c], m1 = S.pmin[(size_t)(u + 4) * S.C + c];
+        const float m2 = S.pmin[(size_t)(u + 8) * S.C + c], m3 = S.pmin[(size_t)(u + 12) * S.C + c];
+        const float x0 = S.pmax[(size_t)u * S.C + c], x1 = S.pmax[(size_t)(u + 4) * S.C + c];
+        const float x2 = S.pmax[(size_t)(u + 8) * S.C + c], x3 = S.pmax[(size_t)(u + 12) * S.C + c];
+        mn = fminf(mn, fminf(fminf(m0, m1), fminf(m2, m3)));
+        mx = fmaxf(mx, fmaxf(fmaxf(x0, x1), fmaxf(x2, x3)));
+      }
+      for (; u < S.nunits; u += 4) {
+        mn = fminf(mn, S.pmin[(size_t)u * S.C + c]);
+        mx = fmaxf(mx, S.pmax[(size_t)u * S.C + c]);
+      }
+    } else if (part == 0) {
+      mn = S.min_in[(size_t)S.min_stride * c];
+      mx = S.max_in[(size_t)S.min_stride * c];
     }
-  } else {
-    mn = S.min_in[(size_t)S.min_stride * c];
-    mx = S.max_in[(size_t)S.min_stride * c];
   }
-  S.min_out[c] = mn;
-  S.max_out[c] = mx;
+  rmn[part][cl] = mn; rmx[part][cl] = mx;
+  __syncthreads();
+  if (part == 0 && cv) {
+    S.min_out[c] = fminf(fminf(rmn[0][cl], rmn[1][cl]), fminf(rmn[2][cl], rmn[3][cl]));
+    S.max_out[c] = fmaxf(fmaxf(rmx[0][cl], rmx[1][cl]), fmaxf(rmx[2][cl], rmx[3][cl]));
+  }
 }
 
 // ---------------------------------------------------------------------------
-// morph: one workgroup per (scale, image)
+// morph pass A: one 1024-thread workgroup per (scale, image), planes in LDS
+// morph pass B: one 256-thread workgroup per (scale, image), tile grid in LDS
 // ---------------------------------------------------------------------------
-constexpr int MORPH_THREADS = 512;
+constexpr int MORPH_THREADS = 1024;
+constexpr int TILES_THREADS = 256;
+
+__device__ __forceinline__ int morph_scale_of(const MorphArgs& a) {
+  int si = 0;
+  while (si + 1 < a.nscales && (int)blockIdx.x >= a.s[si + 1].block_begin) ++si;
+  return si;
+}
 
 template <bool kLDS>
 __global__ __launch_bounds__(MORPH_THREADS) void mcaq_morph_kernel(MorphArgs a, int plane_stride) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  int si = 0;
-  while (si + 1 < a.nscales && (int)blockIdx.x >= a.s[si + 1].block_begin) ++si;
-  const MorphScale& S = a.s[si];
+  const MorphScale& S = a.s[morph_scale_of(a)];
   const int b = (int)blockIdx.x - S.block_begin;
-  if (b >= S.B) return;
-  const int P = S.Hc * S.Wc;
+  if (b >= S.B || !(S.flags & F_PHI)) return;
   Ctx ctx{(int)threadIdx.x, (int)blockDim.x};
   Shared sh;
   Planes pl;
   if (kLDS) {
-    carve_planes(smem, P, pl);
-    carve_shared(smem + plane_stride, S.ht * S.wt, sh);
+    carve_planes(smem, S.Hc, S.Wc, pl);
+    carve_shared(smem + plane_stride, sh);
   } else {
-    carve_planes((char*)S.gscratch + (size_t)b * plane_stride, P, pl);
-    carve_shared(smem, S.ht * S.wt, sh);
+    carve_planes((char*)S.gscratch + (size_t)b * plane_stride, S.Hc, S.Wc, pl);
+    carve_shared(smem, sh);
   }
-  morph_image(ctx, S, b, pl, sh);
+  morph_edges(ctx, S, b, pl, sh);
+}
+
+__global__ __launch_bounds__(TILES_THREADS) void mcaq_tiles_kernel(MorphArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const MorphScale& S = a.s[morph_scale_of(a)];
+  const int b = (int)blockIdx.x - S.block_begin;
+  if (b >= S.B) return;
+  Ctx ctx{(int)threadIdx.x, (int)blockDim.x};
+  Shared sh;
+  carve_shared(smem, sh);
+  morph_tiles(ctx, S, b, sh);
 }
 
 // ---------------------------------------------------------------------------
@@ -305,11 +360,11 @@ int mcaq_stats(const mcaq_stats_scale* scales, int nscales, hipStream_t stream) 
     a.s[i].unit_begin = units;
     const int HW = scales[i].H * scales[i].W;
     if (scales[i].B < 1 || scales[i].C < 1 || HW < 1) return (int)hipErrorInvalidValue;
-    units += scales[i].B * ((HW + 255) / 256);
+    units += scales[i].B * ((HW + ST_PIX - 1) / ST_PIX);
   }
   a.nscales = nscales;
   a.units_total = units;
-  hipLaunchKernelGGL(mcaq_stats_kernel, dim3((units + 3) / 4), dim3(256), 0, stream, a);
+  hipLaunchKernelGGL(mcaq_stats_kernel, dim3(units), dim3(256), 0, stream, a);
   return (int)hipGetLastError();
 }
 
@@ -323,24 +378,38 @@ int mcaq_finalize(const mcaq_finalize_scale* scales, int nscales, hipStream_t st
     a.s[i] = scales[i];
     a.s[i].block_begin = blocks;
     if (scales[i].C < 1 || !scales[i].min_out || !scales[i].max_out) return (int)hipErrorInvalidValue;
-    blocks += (scales[i].C + 255) / 256;
+    blocks += (scales[i].C + 63) / 64;
   }
   a.nscales = nscales;
   hipLaunchKernelGGL(mcaq_finalize_kernel, dim3(blocks), dim3(256), 0, stream, a);
   return (int)hipGetLastError();
 }
 
-static int morph_plan(const MorphScale* s, int n, int* lds_mode, int* plane_stride, size_t* dyn) {
-  int maxP = 0, maxNT = 0;
-  for (int i = 0; i < n; ++i) {
-    maxP = imax_(maxP, s[i].Hc * s[i].Wc);
-    maxNT = imax_(maxNT, s[i].ht * s[i].wt);
+// dynamic LDS available to the morph kernel: 160 KiB minus its static LDS
+// (the runtime rejects a launch whose static + dynamic LDS exceeds the CU's)
+static int morph_lds_budget() {
+  static int budget = -1;
+  if (budget < 0) {
+    hipFuncAttributes fa, fb;
+    if (hipFuncGetAttributes(&fa, (const void*)mcaq_morph_kernel<true>) != hipSuccess ||
+        hipFuncGetAttributes(&fb, (const void*)mcaq_morph_kernel<false>) != hipSuccess)
+      return MCAQ_MORPH_LDS_LIMIT - 4096;   // no device yet: conservative, not cached
+    const int st = imax_((int)fa.sharedSizeBytes, (int)fb.sharedSizeBytes);
+    budget = MCAQ_MORPH_LDS_LIMIT - ((st + 255) & ~255);
   }
-  const int pb = plane_bytes(maxP);
-  const int rest = fixed_bytes() + tile_bytes(maxNT);
-  if (pb + rest <= MCAQ_MORPH_LDS_LIMIT) {
+  return budget;
+}
+
+static int morph_plan(const MorphScale* s, int n, int* lds_mode, int* plane_stride, size_t* dyn) {
+  int pb = 0, rest = 0;
+  for (int i = 0; i < n; ++i) {
+    pb = imax_(pb, (plane_bytes(s[i].Hc, s[i].Wc) + 15) & ~15);
+    rest = imax_(rest, fixed_bytes() + tile_bytes(s[i].ht * s[i].wt));
+  }
+  const int limit = morph_lds_budget();
+  if (pb + rest <= limit) {
     *lds_mode = 1; *plane_stride = pb; *dyn = (size_t)(pb + rest);
-  } else if (rest <= MCAQ_MORPH_LDS_LIMIT) {
+  } else if (rest <= limit) {
     *lds_mode = 0; *plane_stride = pb; *dyn = (size_t)rest;
   } else {
     return (int)hipErrorInvalidValue;
@@ -350,7 +419,7 @@ static int morph_plan(const MorphScale* s, int n, int* lds_mode, int* plane_stri
 
 size_t mcaq_morph_scratch_bytes(int B, int Hc, int Wc, int ht, int wt) {
   MorphScale s{};
-  s.Hc = Hc; s.Wc = Wc; s.ht = ht; s.wt = wt;
+  s.Hc = Hc; s.Wc = Wc; s.ht = ht; s.wt = wt; s.H = 2 * Hc; s.W = 2 * Wc;  // conservative: H < Hc + tile
   int mode, stride; size_t dyn;
   if (morph_plan(&s, 1, &mode, &stride, &dyn)) return 0;
   return mode ? 0 : (size_t)B * stride;
@@ -359,40 +428,64 @@ size_t mcaq_morph_scratch_bytes(int B, int Hc, int Wc, int ht, int wt) {
 int mcaq_morph(const mcaq_morph_scale* scales, int nscales, hipStream_t stream) {
   if (nscales < 1 || nscales > 3) return (int)hipErrorInvalidValue;
   MorphArgs a;
-  int blocks = 0;
+  int blocks = 0, any_phi = 0, any_tiles = 0, tlds = 0;
   for (int i = 0; i < nscales; ++i) {
     memcpy(&a.s[i], &scales[i], sizeof(MorphScale));
     MorphScale& S = a.s[i];
+    if (S.B < 1 || S.ht < 1 || S.wt < 1) return (int)hipErrorInvalidValue;
     if (S.tile < 4 || (S.tile & (S.tile - 1)) || S.tile > 64) return (int)hipErrorInvalidValue;
     if (S.Hc != S.ht * S.tile || S.Wc != S.wt * S.tile || S.Hc > S.H || S.Wc > S.W) return (int)hipErrorInvalidValue;
+    // phi_out carries phi from pass A to pass B
+    if ((S.flags & F_PHI) && !S.phi_out) return (int)hipErrorInvalidValue;
+    if ((S.flags & F_CMLP) && (!S.phi_out || !S.cmlp)) return (int)hipErrorInvalidValue;
+    if ((S.flags & F_SOFTMASK) && (!S.smask || !S.absmean)) return (int)hipErrorInvalidValue;
     S.block_begin = blocks;
     blocks += S.B;
+    any_phi |= (S.flags & F_PHI) != 0;
+    const int tf = S.flags & (F_CMLP | F_MAPPER | F_SOFTMASK);
+    any_tiles |= tf != 0;
+    if (tf) tlds = imax_(tlds, tiles_lds_bytes(S.H, S.W, S.ht * S.wt));
   }
   a.nscales = nscales;
-  int mode, stride; size_t dyn;
-  int e = morph_plan(a.s, nscales, &mode, &stride, &dyn);
-  if (e) return e;
-  if (!mode)
-    for (int i = 0; i < nscales; ++i)
-      if (!a.s[i].gscratch && (a.s[i].flags & F_PHI)) return (int)hipErrorInvalidValue;
-  if (mode) {
-    static int set_true = 0;  // raise the dynamic LDS limit once (not during graph capture)
-    if ((int)dyn > set_true) {
-      hipError_t ae = hipFuncSetAttribute((const void*)mcaq_morph_kernel<true>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, MCAQ_MORPH_LDS_LIMIT);
-      if (ae != hipSuccess) return (int)ae;
-      set_true = MCAQ_MORPH_LDS_LIMIT;
+  if (any_phi) {
+    int mode, stride; size_t dyn;
+    int e = morph_plan(a.s, nscales, &mode, &stride, &dyn);
+    if (e) return e;
+    if (!mode)
+      for (int i = 0; i < nscales; ++i)
+        if (!a.s[i].gscratch && (a.s[i].flags & F_PHI)) return (int)hipErrorInvalidValue;
+    if (mode) {
+      static int set_true = 0;  // raise the dynamic LDS limit once (not during graph capture)
+      if ((int)dyn > set_true) {
+        hipError_t ae = hipFuncSetAttribute((const void*)mcaq_morph_kernel<true>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, morph_lds_budget());
+        if (ae != hipSuccess) return (int)ae;
+        set_true = morph_lds_budget();
+      }
+      hipLaunchKernelGGL(mcaq_morph_kernel<true>, dim3(blocks), dim3(MORPH_THREADS), dyn, stream, a, stride);
+    } else {
+      static int set_false = 0;
+      if ((int)dyn > set_false) {
+        hipError_t ae = hipFuncSetAttribute((const void*)mcaq_morph_kernel<false>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, morph_lds_budget());
+        if (ae != hipSuccess) return (int)ae;
+        set_false = morph_lds_budget();
+      }
+      hipLaunchKernelGGL(mcaq_morph_kernel<false>, dim3(blocks), dim3(MORPH_THREADS), dyn, stream, a, stride);
     }
-    hipLaunchKernelGGL(mcaq_morph_kernel<true>, dim3(blocks), dim3(MORPH_THREADS), dyn, stream, a, stride);
-  } else {
-    static int set_false = 0;
-    if ((int)dyn > set_false) {
-      hipError_t ae = hipFuncSetAttribute((const void*)mcaq_morph_kernel<false>,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, MCAQ_MORPH_LDS_LIMIT);
+    hipError_t le = hipGetLastError();
+    if (le != hipSuccess) return (int)le;
+  }
+  if (any_tiles) {
+    if (tlds > MCAQ_MORPH_LDS_LIMIT - 1024) return (int)hipErrorInvalidValue;
+    static int set_tiles = 0;
+    if (tlds > set_tiles) {
+      hipError_t ae = hipFuncSetAttribute((const void*)mcaq_tiles_kernel,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, MCAQ_MORPH_LDS_LIMIT - 1024);
       if (ae != hipSuccess) return (int)ae;
-      set_false = MCAQ_MORPH_LDS_LIMIT;
+      set_tiles = MCAQ_MORPH_LDS_LIMIT - 1024;
     }
-    hipLaunchKernelGGL(mcaq_morph_kernel<false>, dim3(blocks), dim3(MORPH_THREADS), dyn, stream, a, stride);
+    hipLaunchKernelGGL(mcaq_tiles_kernel, dim3(blocks), dim3(TILES_THREADS), (size_t)tlds, stream, a);
   }
   return (int)hipGetLastError();
 }

@@ -25,12 +25,19 @@ namespace mcaq {
 // Correctly rounded fp32 transcendentals: evaluate in double, round once.
 // (ocml double and glibc double are both < 1 double-ulp, so the fp32 rounding
 // agrees except at points within ~1e-16 of an fp32 midpoint.)
-MCAQ_HD float cr_exp(float x) { return (float)exp((double)x); }
-MCAQ_HD float cr_log(float x) { return (float)log((double)x); }
-MCAQ_HD float cr_log2(float x) { return (float)log2((double)x); }
-MCAQ_HD float cr_log1p(float x) { return (float)log1p((double)x); }
+// (out of line on the device: one copy of each ocml double routine keeps the
+// kernels' instruction footprint small)
+#if defined(__HIPCC__) || defined(__HIP_DEVICE_COMPILE__)
+#define MCAQ_CR __host__ __device__ __forceinline__
+#else
+#define MCAQ_CR inline
+#endif
+MCAQ_CR float cr_exp(float x) { return (float)exp((double)x); }
+MCAQ_CR float cr_log(float x) { return (float)log((double)x); }
+MCAQ_CR float cr_log2(float x) { return (float)log2((double)x); }
+MCAQ_CR float cr_log1p(float x) { return (float)log1p((double)x); }
 MCAQ_HD float cr_sqrt(float x) { return (float)sqrt((double)x); }
-MCAQ_HD float cr_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
+MCAQ_CR float cr_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
 
 MCAQ_HD float bits_as_float(uint32_t u) {
   union { uint32_t u; float f; } c; c.u = u; return c.f;

@@ -1,10 +1,18 @@
 // mcaq_morph.h - per-image morphology -> complexity -> bits -> soft mask.
 //
-// One workgroup owns one image of one hook scale (its planes live in LDS when
-// they fit, else in a global workspace).  The body is written as thread loops
-// (MFOR) separated by barriers (MSYNC) so that the identical source also runs
-// on the host with one thread (tests/emu), where it is checked against the
-// numpy oracle before it ever reaches the GPU.
+// One workgroup owns one image of one hook scale.  Its working set lives in
+// LDS when it fits (else in a global workspace): three fp32 planes (gray,
+// scratch, scratch), one byte plane (Canny direction) and 18 BIT planes
+// (32 pixels per word, built with wave ballots): edges (2, ping-pong), weak
+// edges, foreground mask, its boundary, the three Euler quad classes and the
+// ten uniform-LBP labels.  Hysteresis, erosion and every per-tile count are
+// word operations / popcounts on those bit planes.
+//
+// The body is written as thread loops (MFOR) separated by barriers (MSYNC) so
+// that the identical source also runs on the host with one thread
+// (tests/emu/), where it is checked bit-for-bit against the numpy oracle
+// before it reaches the GPU.  Device-only fast paths (wave shuffles, ballots,
+// fp32 MFMA) compute the same exact values as their host counterparts.
 //
 // Reference (yooooonjae/mcaq-yolo):
 //   morphology.py:826-873 (_phi_tiles_gpu) and helpers :379-739,
@@ -31,6 +39,9 @@ enum : int {
   MM_W1 = 0, MM_B1 = 96, MM_BN1 = 128, MM_W2 = 256, MM_B2 = 2304, MM_BN2 = 2368,
   MM_W3 = 2624, MM_B3 = 4672, MM_BN3 = 4704, MM_W4 = 4832, MM_B4 = 4864, MM_SIZE = 4865
 };
+// blob sizes including the MFMA A-operand copies appended by params.py
+// (mcaq_mlp_mfma.h: CMQ_* / MMQ_*)
+enum : int { CM_BLOB = 2881 + 512 + 2048, MM_BLOB = 4865 + 128 + 2048 + 2048 };
 // soft mask: Conv2d(2,8,3,pad 1) ReLU Conv2d(8,2,1)
 enum : int { SM_W1 = 0, SM_B1 = 144, SM_W2 = 152, SM_B2 = 168, SM_SIZE = 170 };
 
@@ -55,19 +66,30 @@ struct MorphArgs {
   int nscales;
 };
 
-// bytes of per-image plane storage: 3 fp32 planes + 4 byte planes
-MCAQ_HD int plane_bytes(int P) { return 16 * ((P + 3) & ~3); }
-// bytes of per-image tile storage (fp32 [NT][TILE_FLOATS])
-enum : int { TILE_FLOATS = 16 };
+// bit planes
+enum : int { BP_E0 = 0, BP_E1, BP_WK, BP_BIN, BP_BND, BP_Q1, BP_Q3, BP_QD, BP_L0, BP_COUNT = BP_L0 + 10 };
+
+MCAQ_HD int words_per_row(int Wc) { return (Wc + 31) >> 5; }
+// bytes of per-image plane storage
+MCAQ_HD int plane_bytes(int Hc, int Wc) {
+  const int P4 = (Hc * Wc + 3) & ~3;
+  return 13 * P4 + 4 * BP_COUNT * Hc * words_per_row(Wc);
+}
+// per-image tile storage: fp32 [NT][TILE_FLOATS]
+enum : int { TILE_FLOATS = 48 };
 MCAQ_HD int tile_bytes(int NT) { return 4 * TILE_FLOATS * NT; }
-// fixed shared scratch: 256 int hist + 2x256 double scan + reductions
-enum : int { RED_N = 1024 };
-MCAQ_HD int fixed_bytes() { return 256 * 4 + 2 * 256 * 8 * 2 + RED_N * 8 + 64; }
+// fixed shared scratch: 256-int histogram, 2 x 256 doubles, 2 x 64 reduction slots, flags
+MCAQ_HD int fixed_bytes() { return 1024 + 4096 + 512 + 64; }
+// after the tile array: folded mapper BatchNorms (256 floats), two compact
+// per-tile arrays (2 NT floats), or one + the nearest-upsample source tables
+// (NT floats + H + W ints)
+MCAQ_HD int extra_bytes(int H, int W, int NT) { return 4 * imax_(256, (imax_(2 * NT, NT + H + W) + 3) & ~3); }
 
 // tile array slots
 enum : int {
   T_PHI = 0,   // 8 floats
-  T_CMLP = 8, T_C = 9, T_CN = 10, T_BITS = 11, T_ACT = 12, T_MT = 13, T_SORT = 14, T_AUX = 15
+  T_CMLP = 8, T_C = 9, T_CN = 10, T_BITS = 11, T_ACT = 12, T_MT = 13, T_SORT = 14, T_AUX = 15,
+  T_TMP = 16   // up to 32 per-tile partials of the phi stage
 };
 
 // ---------------------------------------------------------------------------
@@ -78,84 +100,106 @@ struct Ctx { int tid, nthr; };
 #if defined(__HIP_DEVICE_COMPILE__)
 #define MSYNC() __syncthreads()
 #define MATOMIC_ADD(p, v) atomicAdd((p), (v))
-#define MATOMIC_OR(p, v) atomicOr((p), (v))
 #else
 #define MSYNC() do {} while (0)
 #define MATOMIC_ADD(p, v) (*(p) += (v))
-#define MATOMIC_OR(p, v) (*(p) |= (v))
 #endif
 #define MFOR(i, n) for (int i = ctx.tid; i < (n); i += ctx.nthr)
 
+// 2D thread loop over a rows x cols grid without per-element divisions
+#define MFOR2(r_, c_, rows, cols)                                                              \
+  for (int _i = ctx.tid, r_ = ctx.tid / (cols), c_ = ctx.tid - (ctx.tid / (cols)) * (cols),    \
+           _dr = ctx.nthr / (cols), _dc = ctx.nthr - (ctx.nthr / (cols)) * (cols);             \
+       _i < (rows) * (cols);                                                                   \
+       _i += ctx.nthr, r_ += _dr, c_ += _dc, r_ += (c_ >= (cols)), c_ -= (c_ >= (cols)) ? (cols) : 0)
+
+// diagnostic build only (-DMCAQ_STAMPS): per-stage cycle stamps of workgroup 0
+#if defined(MCAQ_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
+extern __device__ unsigned long long g_mcaq_stamps[64];
+#define MSTAMP(k)                                                                   \
+  do {                                                                              \
+    __syncthreads();                                                                \
+    if (ctx.tid == 0 && blockIdx.x == (unsigned)S.block_begin) g_mcaq_stamps[k] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define MSTAMP(k) do {} while (0)
+#endif
+
 struct Shared {
   int* hist;       // 256
-  double* scan0;   // 2 x 256 (ping-pong)
-  double* scan1;   // 2 x 256
-  float* redf;     // RED_N
-  int* redi;       // RED_N
-  int* flags;      // 16 ints
+  double* om;      // 256 (Otsu omega prefix)
+  double* mu;      // 256 (Otsu mu prefix)
+  float* redf;     // 64
+  int* redi;       // 64
+  int* flags;      // 16
   float* tiles;    // NT * TILE_FLOATS
 };
 
 struct Planes {
-  float *G, *A, *Bf;            // fp32 planes
-  uint8_t *E0, *E1, *Wk, *Bin;  // byte planes
+  float *G, *A, *Bf;   // fp32 planes (P4 each)
+  uint8_t* dir;        // byte plane
+  uint32_t* bp;        // BP_COUNT bit planes of Hc * WPR words
+  int WPR, plane_words;
+  MCAQ_HD uint32_t* bits(int k) const { return bp + k * plane_words; }
 };
 
-MCAQ_HD void carve_planes(char* base, int P, Planes& pl) {
-  const int P4 = (P + 3) & ~3;
+MCAQ_HD void carve_planes(char* base, int Hc, int Wc, Planes& pl) {
+  const int P4 = (Hc * Wc + 3) & ~3;
   pl.G = (float*)base;
   pl.A = pl.G + P4;
   pl.Bf = pl.A + P4;
-  uint8_t* u = (uint8_t*)(pl.Bf + P4);
-  pl.E0 = u; pl.E1 = u + P4; pl.Wk = u + 2 * P4; pl.Bin = u + 3 * P4;
+  pl.bp = (uint32_t*)(pl.Bf + P4);
+  pl.WPR = words_per_row(Wc);
+  pl.plane_words = Hc * pl.WPR;
+  pl.dir = (uint8_t*)(pl.bp + BP_COUNT * pl.plane_words);
 }
 
-MCAQ_HD void carve_shared(char* base, int NT, Shared& sh) {
+MCAQ_HD void carve_shared(char* base, Shared& sh) {
   sh.hist = (int*)base;
-  sh.scan0 = (double*)(base + 1024);
-  sh.scan1 = sh.scan0 + 512;
-  sh.redf = (float*)(sh.scan1 + 512);
-  sh.redi = (int*)(sh.redf + RED_N);
-  sh.flags = sh.redi + RED_N;
+  sh.om = (double*)(base + 1024);
+  sh.mu = sh.om + 256;
+  sh.redf = (float*)(sh.mu + 256);
+  sh.redi = (int*)(sh.redf + 64);
+  sh.flags = sh.redi + 64;
   sh.tiles = (float*)(sh.flags + 16);
-  (void)NT;
 }
 
-// ---- block reductions through shared memory (tree; exact ops only) --------
+// ---- reductions (exact operations only: min / max / integer / exact double) --
 MCAQ_HD void block_minmax(const Ctx& ctx, Shared& sh, float lmn, float lmx, float& mn, float& mx) {
-  float* rmn = sh.redf;
-  int* dummy = sh.redi; (void)dummy;
-  float* rmx = (float*)sh.redi;
-  rmn[ctx.tid] = lmn; rmx[ctx.tid] = lmx;
+#if defined(__HIP_DEVICE_COMPILE__)
+  for (int o = 32; o > 0; o >>= 1) { lmn = fminf(lmn, __shfl_xor(lmn, o, 64)); lmx = fmaxf(lmx, __shfl_xor(lmx, o, 64)); }
+  const int nw = ctx.nthr >> 6;
+  if ((ctx.tid & 63) == 0) { sh.redf[ctx.tid >> 6] = lmn; sh.redf[32 + (ctx.tid >> 6)] = lmx; }
   MSYNC();
-  for (int s = ctx.nthr / 2; s > 0; s >>= 1) {
-    if (ctx.tid < s) {
-      rmn[ctx.tid] = fmin_(rmn[ctx.tid], rmn[ctx.tid + s]);
-      rmx[ctx.tid] = fmax_(rmx[ctx.tid], rmx[ctx.tid + s]);
-    }
-    MSYNC();
-  }
-  mn = rmn[0]; mx = rmx[0];
+  mn = sh.redf[0]; mx = sh.redf[32];
+  for (int w = 1; w < nw; ++w) { mn = fminf(mn, sh.redf[w]); mx = fmaxf(mx, sh.redf[32 + w]); }
   MSYNC();
+#else
+  (void)ctx; (void)sh;
+  mn = lmn; mx = lmx;
+#endif
 }
 
 MCAQ_HD float block_max(const Ctx& ctx, Shared& sh, float v) {
-  float* r = sh.redf;
-  r[ctx.tid] = v;
-  MSYNC();
-  for (int s = ctx.nthr / 2; s > 0; s >>= 1) {
-    if (ctx.tid < s) r[ctx.tid] = fmax_(r[ctx.tid], r[ctx.tid + s]);
-    MSYNC();
-  }
-  float m = r[0];
-  MSYNC();
-  return m;
+  float mn = 0.0f, mx;
+  block_minmax(ctx, sh, 0.0f, v, mn, mx);
+  return mx;
+}
+
+MCAQ_HD int block_or(const Ctx& ctx, int v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  (void)ctx;
+  return __syncthreads_or(v);
+#else
+  (void)ctx;
+  return v;
+#endif
 }
 
 // ---- Otsu (morphology.py:398-418) on a [0,1] plane --------------------------
 // Histogram counts are integers (exact in any order); the double prefix sums
-// are exact because every partial sum fits in 53 bits, so a parallel scan
-// reproduces ATen's sequential double cumsum.
+// are exact because every partial sum fits in 53 bits, so one wave's parallel
+// scan reproduces ATen's sequential double cumsum.
 MCAQ_HD float otsu_threshold(const Ctx& ctx, Shared& sh, const float* v, int P) {
   MFOR(i, 256) sh.hist[i] = 0;
   MSYNC();
@@ -168,67 +212,108 @@ MCAQ_HD float otsu_threshold(const Ctx& ctx, Shared& sh, const float* v, int P) 
     }
   }
   MSYNC();
-  // total count (exact)
-  int* ri = sh.redi;
-  {
-    int loc = 0;
-    MFOR(i, 256) loc += sh.hist[i];
-    ri[ctx.tid] = loc;
-    MSYNC();
-    for (int s = ctx.nthr / 2; s > 0; s >>= 1) {
-      if (ctx.tid < s) ri[ctx.tid] += ri[ctx.tid + s];
-      MSYNC();
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (ctx.tid < 64) {
+    const int l = ctx.tid;
+    int hc[4], tot = 0;
+    for (int k = 0; k < 4; ++k) { hc[k] = sh.hist[4 * l + k]; tot += hc[k]; }
+    for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+    const float total = fmax_((float)tot, 1.0f);
+    float p[4];
+    double w[4], m[4];
+    for (int k = 0; k < 4; ++k) {
+      p[k] = (float)hc[k] / total;
+      const float c = ((float)(4 * l + k) + 0.5f) / 256.0f;
+      w[k] = (double)p[k];
+      m[k] = (double)(p[k] * c);
+      if (k) { w[k] = w[k] + w[k - 1]; m[k] = m[k] + m[k - 1]; }
     }
+    double sw = w[3], sm = m[3];     // inclusive scan of lane totals
+    for (int o = 1; o < 64; o <<= 1) {
+      const double uw = __shfl_up(sw, o, 64), um = __shfl_up(sm, o, 64);
+      if (l >= o) { sw = sw + uw; sm = sm + um; }
+    }
+    const double ew = sw - w[3], em = sm - m[3];   // exclusive offsets (exact)
+    const float mu_t = (float)__shfl(sm, 63, 64);
+    float best = -1.0f;
+    int bi = 0x7fffffff;
+    for (int k = 0; k < 4; ++k) {
+      const float om = (float)(ew + w[k]);
+      const float mu = (float)(em + m[k]);
+      float num = mu_t * om - mu;
+      num = num * num;
+      const float sb = num / (om * (1.0f - om) + 1e-12f);
+      if (sb > best) { best = sb; bi = 4 * l + k; }
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    }
+    if (l == 0) sh.flags[8] = bi;
   }
-  const float total = fmax_((float)ri[0], 1.0f);
   MSYNC();
-  double* w0 = sh.scan0;        // omega ping
-  double* w1 = sh.scan0 + 256;  // omega pong
-  double* m0 = sh.scan1;
-  double* m1 = sh.scan1 + 256;
-  MFOR(i, 256) {
+  const int idx = sh.flags[8];
+  MSYNC();
+#else
+  int tot = 0;
+  for (int i = 0; i < 256; ++i) tot += sh.hist[i];
+  const float total = fmax_((float)tot, 1.0f);
+  double cw = 0.0, cm = 0.0;
+  for (int i = 0; i < 256; ++i) {
     const float p = (float)sh.hist[i] / total;
-    const float c = ((float)i + 0.5f) / 256.0f;
-    w0[i] = (double)p;
-    m0[i] = (double)(p * c);
+    cw = cw + (double)p;
+    cm = cm + (double)(p * (((float)i + 0.5f) / 256.0f));
+    sh.om[i] = cw; sh.mu[i] = cm;
   }
-  MSYNC();
-  for (int off = 1; off < 256; off <<= 1) {
-    MFOR(i, 256) {
-      w1[i] = w0[i] + (i >= off ? w0[i - off] : 0.0);
-      m1[i] = m0[i] + (i >= off ? m0[i - off] : 0.0);
-    }
-    MSYNC();
-    double* t = w0; w0 = w1; w1 = t;
-    t = m0; m0 = m1; m1 = t;
-  }
-  const float mu_t = (float)m0[255];
-  // sigma_b and first argmax
-  float* rv = sh.redf;
-  int* rix = sh.redi;
-  float best = -1.0f; int bi = 0x7fffffff;
-  MFOR(i, 256) {
-    const float om = (float)w0[i];
-    const float mu = (float)m0[i];
+  const float mu_t = (float)sh.mu[255];
+  float best = -1.0f;
+  int idx = 0;
+  for (int i = 0; i < 256; ++i) {
+    const float om = (float)sh.om[i], mu = (float)sh.mu[i];
     float num = mu_t * om - mu;
     num = num * num;
-    const float den = om * (1.0f - om) + 1e-12f;
-    const float sb = num / den;
-    if (sb > best || (sb == best && i < bi)) { best = sb; bi = i; }
+    const float sb = num / (om * (1.0f - om) + 1e-12f);
+    if (sb > best) { best = sb; idx = i; }
   }
-  rv[ctx.tid] = best; rix[ctx.tid] = bi;
-  MSYNC();
-  for (int s = ctx.nthr / 2; s > 0; s >>= 1) {
-    if (ctx.tid < s) {
-      const float a = rv[ctx.tid], b = rv[ctx.tid + s];
-      const int ia = rix[ctx.tid], ib = rix[ctx.tid + s];
-      if (b > a || (b == a && ib < ia)) { rv[ctx.tid] = b; rix[ctx.tid] = ib; }
-    }
-    MSYNC();
-  }
-  const int idx = rix[0];
-  MSYNC();
+#endif
   return ((float)idx + 0.5f) / 256.0f;
+}
+
+// ---- bit planes --------------------------------------------------------------
+// Pack one predicate per (row h, word k, bit i) slot; every 32 consecutive
+// threads of a wave form one word (device: ballot).
+MCAQ_HD void put_bits(uint32_t* plane, int wi, int bit, bool pred) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const unsigned long long m = __ballot(pred);
+  if (bit == 0) plane[wi] = (uint32_t)(m >> (threadIdx.x & 32));
+#else
+  if (bit == 0) plane[wi] = 0u;
+  if (pred) plane[wi] |= 1u << bit;
+#endif
+}
+
+MCAQ_HD int popc(uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __popc(x);
+#else
+  return __builtin_popcount(x);
+#endif
+}
+
+// bits [x0, x0+n) of a row (n <= 32, may straddle a word boundary)
+MCAQ_HD uint32_t row_field(const uint32_t* row, int x0, int n, int WPR) {
+  const int k = x0 >> 5, s = x0 & 31;
+  uint64_t v = row[k];
+  if (s + n > 32 && k + 1 < WPR) v |= (uint64_t)row[k + 1] << 32;
+  v >>= s;
+  return (uint32_t)(n == 32 ? v : (v & ((1ull << n) - 1ull)));
+}
+// popcount of bits [x0, x0+n) of a row, any n
+MCAQ_HD int row_pop(const uint32_t* row, int x0, int n, int WPR) {
+  int c = 0;
+  for (int o = 0; o < n; o += 32) c += popc(row_field(row, x0 + o, n - o < 32 ? n - o : 32, WPR));
+  return c;
 }
 
 // ---- small fixed-size sums in ATen order ------------------------------------
@@ -408,16 +493,51 @@ MCAQ_HD void sort_tiles(const Ctx& ctx, float* tiles, int NT, int src) {
   MSYNC();
 }
 
-// ---- the per-image pipeline -------------------------------------------------
-MCAQ_HD void morph_image(const Ctx& ctx, const MorphScale& S, int b, Planes& pl, Shared& sh) {
-  const int Hc = S.Hc, Wc = S.Wc, P = Hc * Wc, T = S.tile, ht = S.ht, wt = S.wt, NT = ht * wt;
-  const int T2 = T * T;
-  float* tiles = sh.tiles;
-  const float K180 = (float)(180.0 / 3.14159265358979323846);
-  const float FOURPI = (float)(4.0 * 3.14159265358979323846);
-  const float LOG2_10 = (float)3.321928094887362;
+}  // namespace mcaq
+#if defined(__HIP_DEVICE_COMPILE__)
+#include "mcaq_mlp_mfma.h"   // fp32 MFMA versions of the tile MLPs (device only)
+#endif
+namespace mcaq {
 
-  if (S.flags & F_PHI) {
+// NMS direction bin (morphology.py:430-444).  The float angle is the correctly
+// rounded fp32 atan2 scaled by fp32(180/pi); a fast single-precision estimate
+// decides every pixel whose angle is > 1e-3 degrees from a bin edge, the exact
+// double-precision path the rest (same result as evaluating it everywhere).
+MCAQ_HD int nms_dir(float gx, float gy) {
+  const float K180 = (float)(180.0 / 3.14159265358979323846);
+  float a = atan2f(gy, gx) * K180;
+  if (a < 0.0f) a = a + 180.0f;
+  const float e0 = fabsf(a - 22.5f), e1 = fabsf(a - 67.5f), e2 = fabsf(a - 112.5f), e3 = fabsf(a - 157.5f);
+  if (fmin_(fmin_(e0, e1), fmin_(e2, e3)) < 1e-3f) {
+    a = cr_atan2(gy, gx) * K180;
+    if (a < 0.0f) a = a + 180.0f;
+  }
+  if (a >= 22.5f && a < 67.5f) return 1;
+  if (a >= 67.5f && a < 112.5f) return 2;
+  if (a >= 112.5f && a < 157.5f) return 3;
+  return 0;
+}
+
+// 16-byte store of 4 consecutive floats (p 16-byte aligned)
+MCAQ_HD void store4(float* p, const float (&v)[4]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+#else
+  p[0] = v[0]; p[1] = v[1]; p[2] = v[2]; p[3] = v[3];
+#endif
+}
+
+// ---- pass A: per-image pixel work -> phi (one 1024-thread workgroup per image)
+MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, Planes& pl, Shared& sh) {
+  const int Hc = S.Hc, Wc = S.Wc, P = Hc * Wc, T = S.tile, wt = S.wt, NT = S.ht * wt;
+  const int WPR = pl.WPR, RS = WPR * 32;   // words / bit slots per row
+  const float fT2 = (float)(T * T);
+  float* tiles = sh.tiles;
+  const int QPR = (Wc + 3) >> 2;           // 4-pixel quads per row
+  const int NQ = Hc * QPR;
+
+  MSTAMP(0);
+  {
     // -- gray (channel mean from the stats pass) + per-image normalise01
     const float* gin = S.gray + (size_t)b * P;
     float lmn = 3.402823466e38f, lmx = -3.402823466e38f;
@@ -426,356 +546,477 @@ MCAQ_HD void morph_image(const Ctx& ctx, const MorphScale& S, int b, Planes& pl,
     block_minmax(ctx, sh, lmn, lmx, mn, mx);
     const float den = (mx - mn) + 1e-8f;
     MFOR(p, P) pl.G[p] = (pl.G[p] - mn) / den;
-    MSYNC();
+    MSTAMP(1);
 
-    // -- Canny, cv2compat (morphology.py:458-509)
-    // 5x5 Gaussian blur, zero pad, oneDNN tap order
-    MFOR(p, P) {
-      const int h = p / Wc, w = p - (p / Wc) * Wc;
-      float acc = 0.0f;
+    // -- 5x5 Gaussian blur (zero pad; an out-of-image tap adds fma(w, 0, acc) == acc)
+    MFOR(q, NQ) {
+      const int h = q / QPR, w0 = (q - h * QPR) * 4;
+      float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
       for (int i = 0; i < 5; ++i) {
         const int hh = h + i - 2;
         if (hh < 0 || hh >= Hc) continue;
+        const float* row = pl.G + hh * Wc;
+        float seg[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) { const int ww = w0 - 2 + u; seg[u] = (ww >= 0 && ww < Wc) ? row[ww] : 0.0f; }
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
-          const int ww = w + j - 2;
-          if (ww < 0 || ww >= Wc) continue;
-          acc = fmaf(bits_as_float(k_gauss5_bits[i * 5 + j]), pl.G[hh * Wc + ww], acc);
+          const float k = bits_as_float(k_gauss5_bits[i * 5 + j]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[r] = fmaf(k, seg[r + j], acc[r]);
         }
       }
-      pl.A[p] = acc;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) if (w0 + r < Wc) pl.A[h * Wc + w0 + r] = acc[r];
     }
     MSYNC();
+    MSTAMP(2);
     const float thr = otsu_threshold(ctx, sh, pl.A, P);
     const float thr255 = thr * 255.0f;
     const float lo255 = 0.5f * thr255;
-    // Sobel of 255*blur, L1 magnitude and direction bin
-    uint8_t* dir = pl.E1;
-    MFOR(p, P) {
-      const int h = p / Wc, w = p - (p / Wc) * Wc;
-      float gx = 0.0f, gy = 0.0f;
+    MSTAMP(3);
+
+    // -- Sobel of 255*blur (zero pad), L1 magnitude -> Bf, direction -> dir
+    MFOR(q, NQ) {
+      const int h = q / QPR, w0 = (q - h * QPR) * 4;
+      float gx[4] = {0.0f, 0.0f, 0.0f, 0.0f}, gy[4] = {0.0f, 0.0f, 0.0f, 0.0f};
       for (int i = 0; i < 3; ++i) {
         const int hh = h + i - 1;
         if (hh < 0 || hh >= Hc) continue;
-        for (int j = 0; j < 3; ++j) {
-          const int ww = w + j - 1;
-          if (ww < 0 || ww >= Wc) continue;
-          const float v = pl.A[hh * Wc + ww] * 255.0f;
-          const float kx = (float)((j - 1) * (i == 1 ? 2 : 1));
-          const float ky = (float)((i - 1) * (j == 1 ? 2 : 1));
-          if (kx != 0.0f) gx = fmaf(kx, v, gx);
-          if (ky != 0.0f) gy = fmaf(ky, v, gy);
+        const float* row = pl.A + hh * Wc;
+        float v[6];
+#pragma unroll
+        for (int u = 0; u < 6; ++u) { const int ww = w0 - 1 + u; v[u] = (ww >= 0 && ww < Wc) ? row[ww] * 255.0f : 0.0f; }
+        const float kx = (i == 1) ? 2.0f : 1.0f;          // gx taps (i,0) = -kx, (i,2) = +kx
+        const float ky = (float)(i - 1);                    // gy taps (i,j) = ky * {1,2,1}
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          gx[r] = fmaf(-kx, v[r], gx[r]);
+          gx[r] = fmaf(kx, v[r + 2], gx[r]);
+          if (i != 1) {
+            gy[r] = fmaf(ky, v[r], gy[r]);
+            gy[r] = fmaf(2.0f * ky, v[r + 1], gy[r]);
+            gy[r] = fmaf(ky, v[r + 2], gy[r]);
+          }
         }
       }
-      pl.Bf[p] = fabsf(gx) + fabsf(gy);
-      float ang = cr_atan2(gy, gx) * K180;
-      if (ang < 0.0f) ang = ang + 180.0f;
-      uint8_t d = 0;
-      if (ang >= 22.5f && ang < 67.5f) d = 1;
-      else if (ang >= 67.5f && ang < 112.5f) d = 2;
-      else if (ang >= 112.5f && ang < 157.5f) d = 3;
-      dir[p] = d;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (w0 + r >= Wc) continue;
+        const int p = h * Wc + w0 + r;
+        pl.Bf[p] = fabsf(gx[r]) + fabsf(gy[r]);
+        pl.dir[p] = (uint8_t)nms_dir(gx[r], gy[r]);
+      }
     }
     MSYNC();
-    // NMS (replicate-shifted neighbours) + double threshold
-    MFOR(p, P) {
-      const int h = p / Wc, w = p - (p / Wc) * Wc;
-      const int d = dir[p];
-      int dy1, dx1;
-      if (d == 0) { dy1 = 0; dx1 = 1; }
-      else if (d == 1) { dy1 = -1; dx1 = 1; }
-      else if (d == 2) { dy1 = -1; dx1 = 0; }
-      else { dy1 = -1; dx1 = -1; }
-      const int h1 = imin_(imax_(h + dy1, 0), Hc - 1), w1 = imin_(imax_(w + dx1, 0), Wc - 1);
-      const int h2 = imin_(imax_(h - dy1, 0), Hc - 1), w2 = imin_(imax_(w - dx1, 0), Wc - 1);
-      const float m = pl.Bf[p];
-      const bool keep = (m >= pl.Bf[h1 * Wc + w1]) && (m >= pl.Bf[h2 * Wc + w2]);
-      const float nms = keep ? m : 0.0f;
-      pl.E0[p] = nms > thr255 ? 1 : 0;
-      pl.Wk[p] = nms > lo255 ? 1 : 0;
+    MSTAMP(4);
+    // -- NMS (replicate-shifted neighbours) + double threshold -> bit planes
+    uint32_t* E0 = pl.bits(BP_E0);
+    uint32_t* E1 = pl.bits(BP_E1);
+    uint32_t* WK = pl.bits(BP_WK);
+    MFOR2(h, sl, Hc, RS) {
+      const int k = sl >> 5, bit = sl & 31, w = sl;
+      bool strong = false, weak = false;
+      if (w < Wc) {
+        const int p = h * Wc + w;
+        const int d = pl.dir[p];
+        const int dy1 = (d == 0) ? 0 : -1;
+        const int dx1 = (d == 2) ? 0 : ((d == 3) ? -1 : 1);
+        const int h1 = imin_(imax_(h + dy1, 0), Hc - 1), w1 = imin_(imax_(w + dx1, 0), Wc - 1);
+        const int h2 = imin_(imax_(h - dy1, 0), Hc - 1), w2 = imin_(imax_(w - dx1, 0), Wc - 1);
+        const float m = pl.Bf[p];
+        const bool keep = (m >= pl.Bf[h1 * Wc + w1]) && (m >= pl.Bf[h2 * Wc + w2]);
+        const float nms = keep ? m : 0.0f;
+        strong = nms > thr255;
+        weak = nms > lo255;
+      }
+      put_bits(E0, h * WPR + k, bit, strong);
+      put_bits(WK, h * WPR + k, bit, weak);
     }
     MSYNC();
-    // hysteresis: Jacobi 3x3 dilation passes gated by weak, early exit when stable
-    uint8_t* src = pl.E0;
-    uint8_t* dst = pl.E1;
-    if (ctx.tid == 0) { sh.flags[0] = 0; sh.flags[1] = 0; sh.flags[2] = 0; }
-    MSYNC();
+    MSTAMP(5);
+    // -- hysteresis on words: e' = e | (weak & dilate3x3(e)), Jacobi, early exit
+    uint32_t* src = E0;
+    uint32_t* dst = E1;
     const int iters = S.hyst_iters < 1 ? 1 : S.hyst_iters;
     for (int it = 0; it < iters; ++it) {
       int changed = 0;
-      MFOR(p, P) {
-        uint8_t v = src[p];
-        if (!v && pl.Wk[p]) {
-          const int h = p / Wc, w = p - (p / Wc) * Wc;
-          for (int dy = -1; dy <= 1 && !v; ++dy) {
-            const int hh = h + dy;
-            if (hh < 0 || hh >= Hc) continue;
-            for (int dx = -1; dx <= 1; ++dx) {
-              const int ww = w + dx;
-              if (ww < 0 || ww >= Wc) continue;
-              if (src[hh * Wc + ww]) { v = 1; break; }
-            }
-          }
-          changed |= v;
+      MFOR2(h, k, Hc, WPR) {
+        const uint32_t cur = src[h * WPR + k];
+        uint32_t g = 0u;
+        for (int hh = imax_(h - 1, 0); hh <= imin_(h + 1, Hc - 1); ++hh) {
+          const uint32_t* row = src + hh * WPR;
+          const uint32_t c = row[k];
+          const uint32_t l = (c << 1) | (k > 0 ? row[k - 1] >> 31 : 0u);
+          const uint32_t r = (c >> 1) | (k + 1 < WPR ? row[k + 1] << 31 : 0u);
+          g |= c | l | r;
         }
-        dst[p] = v;
+        const uint32_t nv = cur | (WK[h * WPR + k] & g);
+        changed |= (nv != cur);
+        dst[h * WPR + k] = nv;
       }
-      if (ctx.tid == 0) sh.flags[(it + 1) % 3] = 0;
-      if (changed) MATOMIC_OR(&sh.flags[it % 3], 1);
-      MSYNC();
-      const int any = sh.flags[it % 3];
-      uint8_t* t = src; src = dst; dst = t;
+      const int any = block_or(ctx, changed);
+      uint32_t* t = src; src = dst; dst = t;
       if (!any) break;
     }
-    uint8_t* edge = src;     // final edge map
-    uint8_t* lbl = dst;      // free byte plane (LBP labels below)
-    MSYNC();
+    const uint32_t* edge = src;   // final edge bit plane
+    MSTAMP(6);
 
-    // -- foreground mask for phi5
+    // -- foreground mask for phi5 -> BIN bit plane
+    uint32_t* BIN = pl.bits(BP_BIN);
     if (S.flags & F_BIN_OTSU) {
       const float t2 = otsu_threshold(ctx, sh, pl.G, P);
-      MFOR(p, P) pl.Bin[p] = pl.G[p] > t2 ? 1 : 0;
-      MSYNC();
+      MFOR2(h, sl, Hc, RS) {
+        const int k = sl >> 5, bit = sl & 31;
+        put_bits(BIN, h * WPR + k, bit, sl < Wc && pl.G[h * Wc + sl] > t2);
+      }
     } else {
-      // adaptive threshold (morphology.py:551-573): g255 > G11(g255) - 2
+      // adaptive threshold (morphology.py:551-573): g255 > G11(g255, replicate) - 2.
+      // A separable fp32 estimate decides every pixel whose distance to the
+      // threshold exceeds the proven error bound k_g11_margin (tools/
+      // gen_tables.py); the others get the exact 121-tap sum in oneDNN order
+      // (taps kh-major / kw-minor, FMA from 0), i.e. the reference's value.
       MFOR(p, P) pl.A[p] = pl.G[p] * 255.0f;
       MSYNC();
-      MFOR(p, P) {
-        const int h = p / Wc, w = p - (p / Wc) * Wc;
-        float acc = 0.0f;
-        for (int i = 0; i < 11; ++i) {
-          const int hh = imin_(imax_(h + i - 5, 0), Hc - 1);
-          const float* row = pl.A + hh * Wc;
+      float* rowp = pl.Bf;    // horizontal 11-tap pass
+      MFOR(q, NQ) {
+        const int h = q / QPR, w0 = (q - h * QPR) * 4;
+        const float* row = pl.A + h * Wc;
+        float seg[14];
 #pragma unroll
-          for (int j = 0; j < 11; ++j) {
-            const int ww = imin_(imax_(w + j - 5, 0), Wc - 1);
-            acc = fmaf(bits_as_float(k_gauss11_bits[i * 11 + j]), row[ww], acc);
-          }
+        for (int u = 0; u < 14; ++u) seg[u] = row[imin_(imax_(w0 - 5 + u, 0), Wc - 1)];
+        float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int j = 0; j < 11; ++j) {
+          const float kk = bits_as_float(k_g11_sep_bits[j]);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[r] = fmaf(kk, seg[r + j], acc[r]);
         }
-        pl.Bin[p] = pl.A[p] > (acc - 2.0f) ? 1 : 0;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) if (w0 + r < Wc) rowp[h * Wc + w0 + r] = acc[r];
       }
       MSYNC();
-    }
-
-    // -- Sobel of the normalised gray (phi3) -> A = gx, Bf = gy; LBP labels
-    MFOR(p, P) {
-      const int h = p / Wc, w = p - (p / Wc) * Wc;
-      float gx = 0.0f, gy = 0.0f;
-      for (int i = 0; i < 3; ++i) {
-        const int hh = h + i - 1;
-        if (hh < 0 || hh >= Hc) continue;
-        for (int j = 0; j < 3; ++j) {
-          const int ww = w + j - 1;
-          if (ww < 0 || ww >= Wc) continue;
-          const float v = pl.G[hh * Wc + ww];
-          const float kx = (float)((j - 1) * (i == 1 ? 2 : 1));
-          const float ky = (float)((i - 1) * (j == 1 ? 2 : 1));
-          if (kx != 0.0f) gx = fmaf(kx, v, gx);
-          if (ky != 0.0f) gy = fmaf(ky, v, gy);
-        }
-      }
-      pl.A[p] = gx;
-      pl.Bf[p] = gy;
-      // uniform LBP label (morphology.py:630-646), replicate pad, nb >= center
-      const float c = pl.G[p];
-      const int hm = imax_(h - 1, 0), hp = imin_(h + 1, Hc - 1);
-      const int wm = imax_(w - 1, 0), wp = imin_(w + 1, Wc - 1);
-      int bit[8];
-      bit[0] = pl.G[hm * Wc + wm] >= c; bit[1] = pl.G[hm * Wc + w] >= c;
-      bit[2] = pl.G[hm * Wc + wp] >= c; bit[3] = pl.G[h * Wc + wp] >= c;
-      bit[4] = pl.G[hp * Wc + wp] >= c; bit[5] = pl.G[hp * Wc + w] >= c;
-      bit[6] = pl.G[hp * Wc + wm] >= c; bit[7] = pl.G[h * Wc + wm] >= c;
-      int n1 = 0, tr = 0;
+      const float marg = bits_as_float(k_g11_margin_bits[0]);
+      MFOR2(h, sl, Hc, RS) {
+        const int k = sl >> 5, bit = sl & 31, w = sl;
+        bool on = false;
+        if (w < Wc) {
+          float m = 0.0f;
 #pragma unroll
-      for (int k = 0; k < 8; ++k) { n1 += bit[k]; tr += bit[k] != bit[(k + 7) & 7]; }
-      lbl[p] = (uint8_t)(tr <= 2 ? n1 : 9);
+          for (int i = 0; i < 11; ++i)
+            m = fmaf(bits_as_float(k_g11_sep_bits[i]), rowp[imin_(imax_(h + i - 5, 0), Hc - 1) * Wc + w], m);
+          const float g = pl.A[h * Wc + w];
+          const float t = m - 2.0f;
+          if (fabsf(g - t) > marg) {
+            on = g > t;
+          } else {
+            float acc = 0.0f;
+            for (int i = 0; i < 11; ++i) {
+              const float* row = pl.A + imin_(imax_(h + i - 5, 0), Hc - 1) * Wc;
+              for (int j = 0; j < 11; ++j)
+                acc = fmaf(bits_as_float(k_gauss11_bits[i * 11 + j]), row[imin_(imax_(w + j - 5, 0), Wc - 1)], acc);
+            }
+            on = g > acc - 2.0f;
+          }
+        }
+        put_bits(BIN, h * WPR + k, bit, on);
+      }
     }
     MSYNC();
-    if (S.edge_out) MFOR(p, P) S.edge_out[(size_t)b * P + p] = edge[p];
-    if (S.bin_out) MFOR(p, P) S.bin_out[(size_t)b * P + p] = pl.Bin[p];
+    MSTAMP(7);
 
-    // -- per-tile descriptors phi1..phi5 + interactions
+    // -- Sobel of the normalised gray (phi3) -> A = gx, Bf = gy; uniform LBP label planes;
+    //    boundary and Euler quad-class planes of the mask
+    MFOR2(h, sl, Hc, RS) {
+      const int k = sl >> 5, bit = sl & 31, w = sl;
+      int lab = -1;
+      if (w < Wc) {
+        const int hm = imax_(h - 1, 0), hp = imin_(h + 1, Hc - 1);
+        const int wm = imax_(w - 1, 0), wp = imin_(w + 1, Wc - 1);
+        const float* r0 = pl.G + hm * Wc;
+        const float* r1 = pl.G + h * Wc;
+        const float* r2 = pl.G + hp * Wc;
+        const float c = r1[w];
+        // zero-padded Sobel taps, row-major
+        const float z00 = (h > 0 && w > 0) ? r0[wm] : 0.0f, z01 = h > 0 ? r0[w] : 0.0f;
+        const float z02 = (h > 0 && w + 1 < Wc) ? r0[wp] : 0.0f;
+        const float z10 = w > 0 ? r1[wm] : 0.0f, z12 = w + 1 < Wc ? r1[wp] : 0.0f;
+        const float z20 = (h + 1 < Hc && w > 0) ? r2[wm] : 0.0f, z21 = h + 1 < Hc ? r2[w] : 0.0f;
+        const float z22 = (h + 1 < Hc && w + 1 < Wc) ? r2[wp] : 0.0f;
+        float gx = 0.0f, gy = 0.0f;
+        gx = fmaf(-1.0f, z00, gx); gx = fmaf(1.0f, z02, gx);
+        gx = fmaf(-2.0f, z10, gx); gx = fmaf(2.0f, z12, gx);
+        gx = fmaf(-1.0f, z20, gx); gx = fmaf(1.0f, z22, gx);
+        gy = fmaf(-1.0f, z00, gy); gy = fmaf(-2.0f, z01, gy); gy = fmaf(-1.0f, z02, gy);
+        gy = fmaf(1.0f, z20, gy); gy = fmaf(2.0f, z21, gy); gy = fmaf(1.0f, z22, gy);
+        pl.A[h * Wc + w] = gx;
+        pl.Bf[h * Wc + w] = gy;
+        // LBP (morphology.py:630-646): replicate pad, nb >= center, circular order
+        int bt[8];
+        bt[0] = r0[wm] >= c; bt[1] = r0[w] >= c; bt[2] = r0[wp] >= c; bt[3] = r1[wp] >= c;
+        bt[4] = r2[wp] >= c; bt[5] = r2[w] >= c; bt[6] = r2[wm] >= c; bt[7] = r1[wm] >= c;
+        int n1 = 0, tr = 0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) { n1 += bt[q]; tr += bt[q] != bt[(q + 7) & 7]; }
+        lab = tr <= 2 ? n1 : 9;
+      }
+#pragma unroll
+      for (int q = 0; q < 10; ++q) put_bits(pl.bits(BP_L0 + q), h * WPR + k, bit, lab == q);
+    }
+    // boundary (m & ~erode3x3 with in-bounds neighbours) and Euler quad classes
+    // of the windows anchored at (h, w) over m[h-1..h][w-1..w] (zero padded)
+    uint32_t* BND = pl.bits(BP_BND);
+    uint32_t* Q1 = pl.bits(BP_Q1);
+    uint32_t* Q3 = pl.bits(BP_Q3);
+    uint32_t* QD = pl.bits(BP_QD);
+    MFOR2(h, k, Hc, WPR) {
+      const int nvalid = imin_(Wc - 32 * k, 32);
+      const uint32_t vmask = nvalid >= 32 ? 0xFFFFFFFFu : ((1u << nvalid) - 1u);
+      // pixel w+1 outside the image counts as 1 for the erosion (min over in-bounds)
+      const uint32_t rim = (k + 1 == WPR) ? (1u << (nvalid - 1)) : 0u;
+      uint32_t er = 0xFFFFFFFFu;
+      for (int hh = imax_(h - 1, 0); hh <= imin_(h + 1, Hc - 1); ++hh) {
+        const uint32_t* row = BIN + hh * WPR;
+        const uint32_t c = row[k];
+        const uint32_t l = (c << 1) | (k > 0 ? row[k - 1] >> 31 : 1u);
+        const uint32_t r = (c >> 1) | (k + 1 < WPR ? row[k + 1] << 31 : 0u) | rim;
+        er &= c & l & r;
+      }
+      const uint32_t m = BIN[h * WPR + k];
+      BND[h * WPR + k] = m & ~er;
+      const uint32_t D = m;
+      const uint32_t Cc = (m << 1) | (k > 0 ? BIN[h * WPR + k - 1] >> 31 : 0u);
+      const uint32_t Bq = h > 0 ? BIN[(h - 1) * WPR + k] : 0u;
+      const uint32_t Aq = h > 0 ? ((Bq << 1) | (k > 0 ? BIN[(h - 1) * WPR + k - 1] >> 31 : 0u)) : 0u;
+      const uint32_t odd = Aq ^ Bq ^ Cc ^ D;
+      const uint32_t pairs = (Aq & Bq) | (Aq & Cc) | (Aq & D) | (Bq & Cc) | (Bq & D) | (Cc & D);
+      Q1[h * WPR + k] = odd & ~pairs & vmask;
+      Q3[h * WPR + k] = odd & pairs & vmask;
+      QD[h * WPR + k] = (((Aq & D) & ~(Bq | Cc)) | ((Bq & Cc) & ~(Aq | D))) & vmask;
+    }
+    MSYNC();
+    if (S.edge_out) MFOR2(h, w, Hc, Wc) S.edge_out[(size_t)b * P + h * Wc + w] = (edge[h * WPR + (w >> 5)] >> (w & 31)) & 1u;
+    if (S.bin_out) MFOR2(h, w, Hc, Wc) S.bin_out[(size_t)b * P + h * Wc + w] = (BIN[h * WPR + (w >> 5)] >> (w & 31)) & 1u;
+    MSTAMP(8);
+
+    // -- per-tile partial quantities, one thread per (tile, item):
+    //    items [0,4)            gradient window sums gx, gx^2, gy, gy^2 (row-major order)
+    //    items [4,4+S)          log(n_s + 1), n_s = occupied s x s boxes of the edge map
+    //    items [4+S,14+S)       p_k * log2(p_k + 1e-10) of the uniform-LBP label k
+    //    items [14+S,20+S)      counts: edges, mask area, boundary, Euler quads q1, q3, qd
     int S_ = 0;
     for (int s = 2; s <= T; s *= 2) ++S_;
-    const int Mcols = S.batch_total * NT;
-    const int ycut = aten_tail_start(Mcols);
-    // constants of the weighted regression (morphology.py:604-619)
+    // item-major order (consecutive lanes = consecutive tiles of one item) with
+    // each item group padded to whole waves, so no wave mixes item kinds
+    const int NI = 20 + S_;
+    const int nG = (4 * NT + 63) & ~63, nB = (S_ * NT + 63) & ~63, nR = (16 * NT + 63) & ~63;
+    MFOR(u, nG + nB + nR) {
+      int v = u, it0 = 0, nit = 4;
+      if (v >= nG) {
+        v -= nG; it0 = 4; nit = S_;
+        if (v >= nB) { v -= nB; it0 = 4 + S_; nit = 16; }
+      }
+      if (v >= nit * NT) continue;
+      const int it = it0 + v / NT, t = v - (v / NT) * NT;
+      const int th = t / wt, tw = t - (t / wt) * wt;
+      const int h0 = th * T, w0 = tw * T;
+      float val;
+      if (it < 4) {
+        const float* plane = (it < 2) ? pl.A : pl.Bf;
+        float acc = 0.0f;
+        for (int yy = 0; yy < T; ++yy) {
+          const float* row = plane + (h0 + yy) * Wc + w0;
+          if (it & 1) { for (int xx = 0; xx < T; ++xx) acc = acc + row[xx] * row[xx]; }
+          else { for (int xx = 0; xx < T; ++xx) acc = acc + row[xx]; }
+        }
+        val = acc;
+      } else if (it < 4 + S_) {
+        // box counting (morphology.py:576-621): OR-fold s rows, then s columns
+        const int s = 2 << (it - 4);
+        int n = 0;
+        for (int by = 0; by < T; by += s) {
+          if (s <= 32) {
+            const int fw = T < 32 ? T : 32;
+            uint32_t starts = 0u;
+            for (int x = 0; x < fw; x += s) starts |= 1u << x;
+            for (int fx = 0; fx < T; fx += fw) {
+              uint32_t o = 0u;
+              for (int yy = 0; yy < s; ++yy) o |= row_field(edge + (h0 + by + yy) * WPR, w0 + fx, fw, WPR);
+              for (int sh2 = 1; sh2 < s; sh2 <<= 1) o |= o >> sh2;     // group OR onto its first bit
+              n += popc(o & starts);
+            }
+          } else {   // s >= 64: whole-word boxes
+            for (int bx = 0; bx < T; bx += s) {
+              int any = 0;
+              for (int yy = 0; yy < s && !any; ++yy) any = row_pop(edge + (h0 + by + yy) * WPR, w0 + bx, s, WPR) > 0;
+              n += any;
+            }
+          }
+        }
+        val = cr_log((float)n + 1.0f);
+      } else {
+        const int k = it - 4 - S_;
+        const uint32_t* plane = k < 10 ? pl.bits(BP_L0 + k)
+                              : (k == 10 ? edge : (k == 11 ? BIN : (k == 12 ? BND : (k == 13 ? Q1 : (k == 14 ? Q3 : QD)))));
+        int cnt = 0;
+        for (int yy = 0; yy < T; ++yy) cnt += row_pop(plane + (h0 + yy) * WPR, w0, T, WPR);
+        if (k < 10) {
+          const float pk = (float)cnt / fT2;
+          val = pk * log2_ref(pk + 1e-10f);
+        } else {
+          val = (float)cnt;
+        }
+      }
+      tiles[t * TILE_FLOATS + T_TMP + it] = val;
+    }
+    MSYNC();
+
+    // -- per-tile descriptors phi1..phi5 + interactions
+    const int ycut = aten_tail_start(S.batch_total * NT);
     float xs[8], ws[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      xs[i] = i < S_ ? cr_log((float)(2 << i)) : 0.0f;
-      ws[i] = i < S_ ? cr_exp(-0.1f * (float)i) : 0.0f;
+      xs[i] = i < S_ ? bits_as_float(k_frac_x_bits[i]) : 0.0f;
+      ws[i] = i < S_ ? bits_as_float(k_frac_w_bits[i]) : 0.0f;
     }
-    const float w_sum = small_sum(ws, S_, true);
-    float wx[8], wdx2[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) wx[i] = ws[i] * xs[i];
-    const float x_mean = small_sum(wx, S_, true) / w_sum;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) { const float dx = xs[i] - x_mean; wdx2[i] = ws[i] * (dx * dx); }
-    const float var = small_sum(wdx2, S_, true);
+    const float w_sum = bits_as_float(k_frac_st_bits[4 * S_ + 0]);
+    const float x_mean = bits_as_float(k_frac_st_bits[4 * S_ + 1]);
+    const float var = bits_as_float(k_frac_st_bits[4 * S_ + 2]);
 
     MFOR(t, NT) {
-      const int th = t / wt, tw = t - (t / wt) * wt;
-      const int h0 = th * T, w0 = tw * T;
-      // phi1: box counting (morphology.py:576-621)
-      float p1 = 1.0f;
+      const float* tv = tiles + t * TILE_FLOATS + T_TMP;
+      // phi1: weighted log-log regression slope (morphology.py:596-621)
+      float p1;
       if (S_ >= 2) {
-        float ys[8];
-        int si = 0;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) ys[i] = 0.0f;
-        for (int s = 2; s <= T; s *= 2, ++si) {
-          int n = 0;
-          for (int by = 0; by < T; by += s)
-            for (int bx = 0; bx < T; bx += s) {
-              int occ = 0;
-              for (int yy = 0; yy < s && !occ; ++yy)
-                for (int xx = 0; xx < s; ++xx)
-                  if (edge[(h0 + by + yy) * Wc + w0 + bx + xx]) { occ = 1; break; }
-              n += occ;
-            }
-          const float y = cr_log((float)n + 1.0f);
-#pragma unroll
-          for (int i = 0; i < 8; ++i) if (i == si) ys[i] = y;
-        }
         const bool tail = ((S.batch_offset + b) * NT + t) >= ycut;
-        float wy[8];
+        float ys[8], wy[8], cv[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) ys[i] = i < S_ ? tv[4 + i] : 0.0f;
 #pragma unroll
         for (int i = 0; i < 8; ++i) wy[i] = ws[i] * ys[i];
         const float y_mean = small_sum(wy, S_, tail) / w_sum;
-        float cv[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) cv[i] = (ws[i] * (xs[i] - x_mean)) * (ys[i] - y_mean);
         const float cov = small_sum(cv, S_, tail);
-        float df = -(cov / (var + 1e-12f));
-        df = clampf_(df, 1.0f, 2.0f);
-        p1 = df / 2.0f;
+        p1 = clampf_(-(cov / (var + 1e-12f)), 1.0f, 2.0f) / 2.0f;
       } else {
         p1 = 1.0f / 2.0f;
       }
-      // phi2: LBP histogram entropy; bins summed 8, 9, 0..7 (channels-last)
-      int cnt[10];
-#pragma unroll
-      for (int k = 0; k < 10; ++k) cnt[k] = 0;
-      // phi3 sums, phi4 count, phi5 area/perimeter/Euler
-      float sgx = 0.0f, sgx2 = 0.0f, sgy = 0.0f, sgy2 = 0.0f;
-      int ecount = 0, area = 0, perim = 0;
-      float esum = 0.0f;
-      for (int yy = 0; yy < T; ++yy) {
-        const int h = h0 + yy;
-        for (int xx = 0; xx < T; ++xx) {
-          const int w = w0 + xx;
-          const int q = h * Wc + w;
-          const int lb = lbl[q];
-#pragma unroll
-          for (int k = 0; k < 10; ++k) cnt[k] += (lb == k);
-          const float gx = pl.A[q], gy = pl.Bf[q];
-          sgx = sgx + gx; sgx2 = sgx2 + gx * gx;
-          sgy = sgy + gy; sgy2 = sgy2 + gy * gy;
-          ecount += edge[q];
-          const int m = pl.Bin[q];
-          area += m;
-          if (m) {
-            int mn3 = 1;
-            for (int dy = -1; dy <= 1; ++dy) {
-              const int hh = h + dy;
-              if (hh < 0 || hh >= Hc) continue;
-              for (int dx = -1; dx <= 1; ++dx) {
-                const int ww = w + dx;
-                if (ww < 0 || ww >= Wc) continue;
-                mn3 &= pl.Bin[hh * Wc + ww];
-              }
-            }
-            perim += 1 - mn3;
-          }
-          // Euler quad of window (h, w): m[h-1][w-1]*1 + m[h-1][w]*2 + m[h][w-1]*4 + m[h][w]*8
-          const int a = (h > 0 && w > 0) ? pl.Bin[q - Wc - 1] : 0;
-          const int bq = (h > 0) ? pl.Bin[q - Wc] : 0;
-          const int c = (w > 0) ? pl.Bin[q - 1] : 0;
-          const int idx = a + 2 * bq + 4 * c + 8 * m;
-          float e = 0.0f;
-          if (idx == 1 || idx == 2 || idx == 4 || idx == 8) e = 0.25f;
-          else if (idx == 7 || idx == 11 || idx == 13 || idx == 14) e = -0.25f;
-          else if (idx == 6 || idx == 9) e = -0.5f;
-          esum = esum + e;
-        }
-      }
-      float terms[10];
-      const float invT2 = (float)T2;
-#pragma unroll
-      for (int k = 0; k < 10; ++k) {
-        const float pk = (float)cnt[k] / invT2;
-        terms[k] = pk * log2_ref(pk + 1e-10f);
-      }
+      // phi2: LBP entropy, bins summed 8, 9, 0..7 (channels-last inner sum)
+      const float* terms = tv + 4 + S_;
       float ent = 0.0f;
-      ent = ent + terms[8]; ent = ent + terms[9];
+      ent = ent + terms[8];
+      ent = ent + terms[9];
 #pragma unroll
       for (int k = 0; k < 8; ++k) ent = ent + terms[k];
-      const float p2 = (-ent) / LOG2_10;
-      // phi3
-      const float mgx = sgx / invT2, mgx2 = sgx2 / invT2;
-      const float mgy = sgy / invT2, mgy2 = sgy2 / invT2;
-      const float vx = fmax_(mgx2 - mgx * mgx, 0.0f);
-      const float vy = fmax_(mgy2 - mgy * mgy, 0.0f);
-      const float v = vx + vy;
+      const float p2 = (-ent) / (float)3.321928094887362;
+      // phi3: gradient variance
+      const float mgx = tv[0] / fT2, mgx2 = tv[1] / fT2, mgy = tv[2] / fT2, mgy2 = tv[3] / fT2;
+      const float v = fmax_(mgx2 - mgx * mgx, 0.0f) + fmax_(mgy2 - mgy * mgy, 0.0f);
       const float p3 = v / (v + 1.0f);
-      // phi4
-      const float p4 = (float)ecount / invT2;
-      // phi5
-      const float fa = (float)area, fp = (float)perim;
-      float ic = (fp * fp) / (FOURPI * fa + 1e-6f);
+      // phi4 edge density, phi5 contour complexity
+      const float* cn = tv + 14 + S_;
+      const float p4 = cn[0] / fT2;
+      const float fa = cn[1], fp = cn[2];
+      float ic = (fp * fp) / ((float)(4.0 * 3.14159265358979323846) * fa + 1e-6f);
       if (!(S.flags & F_NO_EULER)) {
-        const float Kr = (esum / invT2) * invT2;
-        const float Kc = fmax_(rintf(Kr), 1.0f);
-        ic = ic / Kc;
+        // Euler sum = (q1 - q3 - 2 qd) / 4: a multiple of 0.25, exact in fp32
+        const float esum = (cn[3] - cn[4] - 2.0f * cn[5]) * 0.25f;
+        ic = ic / fmax_(rintf((esum / fT2) * fT2), 1.0f);
       }
-      float p5 = 1.0f - 1.0f / fmax_(ic, 1.0f);
-      if (!(area > 0)) p5 = 0.0f;
+      const float p5 = fa > 0.0f ? 1.0f - 1.0f / fmax_(ic, 1.0f) : 0.0f;
       const float p8 = cr_sqrt(p4 * p5 + 1e-12f);
       float* tp = tiles + t * TILE_FLOATS + T_PHI;
       tp[0] = p1; tp[1] = p2; tp[2] = p3; tp[3] = p4; tp[4] = p5;
       tp[5] = p1 * p2; tp[6] = p3 * p3; tp[7] = p8;
       if (S.phi_out) {
         float* o = S.phi_out + ((size_t)b * NT + t) * 8;
-#pragma unroll
         for (int k = 0; k < 8; ++k) o[k] = tp[k];
       }
     }
     MSYNC();
   }
+  MSTAMP(9);
+}
+
+// ---- pass B: per-image tile work (one 256-thread workgroup per image):
+// complexity MLP, bilateral, normalisation, bit mapper, soft mask, m plane.
+// LDS: Shared (fixed + tiles) | extra | bilateral weights (25 NT floats).
+MCAQ_HD int tiles_lds_bytes(int H, int W, int NT) {
+  return fixed_bytes() + tile_bytes(NT) + extra_bytes(H, W, NT) + 100 * NT;
+}
+
+MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh) {
+  const int ht = S.ht, wt = S.wt, NT = ht * wt;
+  float* tiles = sh.tiles;
+  float* extra = tiles + NT * TILE_FLOATS;            // compact per-tile arrays / tables
+  float* wbuf = (float*)((char*)extra + extra_bytes(S.H, S.W, NT));
+  const float* Pc = S.cmlp;
+  const float* Pmap = S.mapper;
+  MSTAMP(10);
+  if (S.flags & F_CMLP) {
+    MFOR(u, NT * 8) tiles[(u >> 3) * TILE_FLOATS + T_PHI + (u & 7)] = S.phi_out[(size_t)b * NT * 8 + u];
+    MSYNC();
+  }
 
   // -- complexity MLP + bilateral (morphology.py:959-968)
   if (S.flags & F_CMLP) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    for (int blk = ctx.tid >> 6; blk * 32 < NT; blk += ctx.nthr >> 6)
+      cmlp_block_mfma(Pc, tiles, NT, blk * 32, ctx.tid & 63);
+#else
     MFOR(t, NT) {
       float phi[8];
-#pragma unroll
       for (int k = 0; k < 8; ++k) phi[k] = tiles[t * TILE_FLOATS + T_PHI + k];
-      const float c = complexity_mlp_tile(S.cmlp, phi);
-      tiles[t * TILE_FLOATS + T_CMLP] = c;
-      if (S.cmlp_out) S.cmlp_out[(size_t)b * NT + t] = c;
+      tiles[t * TILE_FLOATS + T_CMLP] = complexity_mlp_tile(Pc, phi);
+    }
+#endif
+    MSYNC();
+    MFOR(t, NT) {
+      const float v = tiles[t * TILE_FLOATS + T_CMLP];
+      extra[t] = v;
+      if (S.cmlp_out) S.cmlp_out[(size_t)b * NT + t] = v;
     }
     MSYNC();
+    MSTAMP(11);
+    // range weights w = spatial * exp(-(d^2)/0.02), one thread per (tile, tap)
+    {
+      MFOR(u, NT * 25) {
+        const int t = u / 25, k = u - (u / 25) * 25;
+        const int th = t / wt, tw = t - (t / wt) * wt;
+        const int hh = imin_(imax_(th + k / 5 - 2, 0), ht - 1);
+        const int ww = imin_(imax_(tw + k % 5 - 2, 0), wt - 1);
+        const float d = extra[hh * wt + ww] - extra[t];
+        wbuf[u] = bits_as_float(k_bilat_sp_bits[k]) * cr_exp((-(d * d)) / 0.02f);
+      }
+      MSYNC();
+    }
     const int cut = aten_tail_start(NT);
     MFOR(t, NT) {
       const int th = t / wt, tw = t - (t / wt) * wt;
-      const float ctr = tiles[t * TILE_FLOATS + T_CMLP];
-      float wv[25], wp[25];
-#pragma unroll
-      for (int k = 0; k < 25; ++k) {
-        const int i = k / 5, j = k % 5;
-        const int hh = imin_(imax_(th + i - 2, 0), ht - 1);
-        const int ww = imin_(imax_(tw + j - 2, 0), wt - 1);
-        const float pv = tiles[(hh * wt + ww) * TILE_FLOATS + T_CMLP];
-        const float d = pv - ctr;
-        const float rw = cr_exp((-(d * d)) / 0.02f);
-        wv[k] = bits_as_float(k_bilat_sp_bits[k]) * rw;
-        wp[k] = wv[k] * pv;
-      }
+      const float ctr = extra[t];
+      // 25-row ATen outer sums of w*p and w: vector column = rows 0..15 folded,
+      // then 16..24 in a0; tail column = 4 interleaved partials (rows 4i+q),
+      // row 24 into partial 0.  Adding an exact +0 is an identity (sums never
+      // hold -0), so both orders are accumulated with selects in one loop.
       const bool tail = t >= cut;
-      const float num = aten_sum_n<25>(wp, tail);
-      const float den = aten_sum_n<25>(wv, tail);
-      const float c = clampf_(num / (den + 1e-8f), 0.0f, 1.0f);
+      float n0 = 0.0f, n1 = 0.0f, n2 = 0.0f, n3 = 0.0f, d0 = 0.0f, d1 = 0.0f, d2 = 0.0f, d3 = 0.0f;
+      for (int k = 0; k < 25; ++k) {
+        const int hh = imin_(imax_(th + k / 5 - 2, 0), ht - 1);
+        const int ww = imin_(imax_(tw + k % 5 - 2, 0), wt - 1);
+        const float pv = extra[hh * wt + ww];
+        const float wv = wbuf[t * 25 + k];
+        const float wp = wv * pv;
+        const int q = tail ? (k < 24 ? (k & 3) : 0) : (k < 16 ? 1 : 0);
+        n0 = n0 + (q == 0 ? wp : 0.0f); d0 = d0 + (q == 0 ? wv : 0.0f);
+        n1 = n1 + (q == 1 ? wp : 0.0f); d1 = d1 + (q == 1 ? wv : 0.0f);
+        n2 = n2 + (q == 2 ? wp : 0.0f); d2 = d2 + (q == 2 ? wv : 0.0f);
+        n3 = n3 + (q == 3 ? wp : 0.0f); d3 = d3 + (q == 3 ? wv : 0.0f);
+      }
+      float num, dsum;
+      if (tail) { num = ((n0 + n1) + n2) + n3; dsum = ((d0 + d1) + d2) + d3; }
+      else { num = n0 + n1; dsum = d0 + d1; }
+      const float c = clampf_(num / (dsum + 1e-8f), 0.0f, 1.0f);
       tiles[t * TILE_FLOATS + T_C] = c;
       if (S.c_out) S.c_out[(size_t)b * NT + t] = c;
     }
@@ -784,6 +1025,7 @@ MCAQ_HD void morph_image(const Ctx& ctx, const MorphScale& S, int b, Planes& pl,
     MFOR(t, NT) tiles[t * TILE_FLOATS + T_C] = S.c_in[(size_t)b * NT + t];
     MSYNC();
   }
+  MSTAMP(12);
 
   // -- optional percentile normalisation (models/mcaq_yolo.py:427-432) and mapper
   if (S.flags & F_MAPPER) {
@@ -812,24 +1054,42 @@ MCAQ_HD void morph_image(const Ctx& ctx, const MorphScale& S, int b, Planes& pl,
         const float c = tiles[t * TILE_FLOATS + csrc];
         const float rel = clampf_((c - lo) / (spread + 1e-8f), 0.0f, 1.0f);
         const float cn = spread > 1e-3f ? rel : clampf_(c, 0.0f, 1.0f);
-        const float bm = S.min_bits + (S.max_bits - S.min_bits) * cn;
-        const float bv = finish_bits(bm, S);
-        tiles[t * TILE_FLOATS + T_BITS] = bv;
-        if (S.bits_out) S.bits_out[(size_t)b * NT + t] = bv;
+        tiles[t * TILE_FLOATS + T_AUX] = S.min_bits + (S.max_bits - S.min_bits) * cn;
       }
     } else {
-      MFOR(t, NT) {
-        const float bm = mapper_mlp_tile(S.mapper, tiles[t * TILE_FLOATS + csrc], S.min_bits, S.max_bits);
-        const float bv = finish_bits(bm, S);
-        tiles[t * TILE_FLOATS + T_BITS] = bv;
-        if (S.bits_out) S.bits_out[(size_t)b * NT + t] = bv;
+#if defined(__HIP_DEVICE_COMPILE__)
+      // fold the three eval BatchNorms once per workgroup: alpha = inv*g,
+      // beta = b - (rm*inv)*g, inv = 1/sqrt(rv + eps)  (same values as bn_eval)
+      float* ab = extra;
+      MFOR(j, 128) {
+        const int L = j < 32 ? 0 : (j < 96 ? 1 : 2);
+        const int n = L == 1 ? 64 : 32;
+        const int jj = j - (L == 0 ? 0 : (L == 1 ? 32 : 96));
+        const float* bn = Pmap + (L == 0 ? MM_BN1 : (L == 1 ? MM_BN2 : MM_BN3));
+        const float inv = 1.0f / cr_sqrt(bn[3 * n + jj] + 1e-5f);
+        ab[j] = inv * bn[jj];
+        ab[128 + j] = bn[n + jj] - (bn[2 * n + jj] * inv) * bn[jj];
       }
+      MSYNC();
+      for (int blk = ctx.tid >> 6; blk * 32 < NT; blk += ctx.nthr >> 6)
+        mapper_block_mfma(Pmap, ab, tiles, NT, blk * 32, ctx.tid & 63, csrc, S.min_bits, S.max_bits);
+#else
+      MFOR(t, NT) tiles[t * TILE_FLOATS + T_AUX] =
+          mapper_mlp_tile(Pmap, tiles[t * TILE_FLOATS + csrc], S.min_bits, S.max_bits);
+#endif
+    }
+    MSYNC();
+    MFOR(t, NT) {
+      const float bv = finish_bits(tiles[t * TILE_FLOATS + T_AUX], S);
+      tiles[t * TILE_FLOATS + T_BITS] = bv;
+      if (S.bits_out) S.bits_out[(size_t)b * NT + t] = bv;
     }
     MSYNC();
   } else if ((S.flags & F_SOFTMASK) && S.bits_in) {
     MFOR(t, NT) tiles[t * TILE_FLOATS + T_BITS] = S.bits_in[(size_t)b * NT + t];
     MSYNC();
   }
+  MSTAMP(13);
 
   // -- learned soft mask m(p) (quantization.py:213-239)
   if (S.flags & F_SOFTMASK) {
@@ -848,64 +1108,88 @@ MCAQ_HD void morph_image(const Ctx& ctx, const MorphScale& S, int b, Planes& pl,
       lmx = fmax_(lmx, a);
     }
     const float amax = block_max(ctx, sh, lmx);
-    MFOR(t, NT) {
-      float* tp = tiles + t * TILE_FLOATS;
-      tp[T_AUX] = clampf_((tp[T_BITS] - 2.0f) / 6.0f, 0.0f, 1.0f);
-    }
-    MSYNC();
     const float* Pm = S.smask;
     const float den = amax + 1e-8f;
+    // the two conv input features, compact: f0 = bits feature, f1 = activation
+    float* f0a = extra;
+    float* f1a = extra + NT;
+    MFOR(t, NT) {
+      f0a[t] = clampf_((tiles[t * TILE_FLOATS + T_BITS] - 2.0f) / 6.0f, 0.0f, 1.0f);
+      f1a[t] = tiles[t * TILE_FLOATS + T_ACT] / den;
+    }
+    MSYNC();
     MFOR(t, NT) {
       const int i = t / wt, j = t - (t / wt) * wt;
       float hid[8];
 #pragma unroll
-      for (int oc = 0; oc < 8; ++oc) {
-        float acc = 0.0f;
-        for (int ki = 0; ki < 3; ++ki) {
-          const int ii = i + ki - 1;
-          if (ii < 0 || ii >= ht) continue;
-          for (int kj = 0; kj < 3; ++kj) {
-            const int jj = j + kj - 1;
-            if (jj < 0 || jj >= wt) continue;
-            const float* nb = tiles + (ii * wt + jj) * TILE_FLOATS;
-            acc = fmaf(Pm[SM_W1 + ((oc * 2 + 0) * 3 + ki) * 3 + kj], nb[T_AUX], acc);
-            acc = fmaf(Pm[SM_W1 + ((oc * 2 + 1) * 3 + ki) * 3 + kj], nb[T_ACT] / den, acc);
+      for (int oc = 0; oc < 8; ++oc) hid[oc] = 0.0f;
+      for (int ki = 0; ki < 3; ++ki) {
+        const int ii = i + ki - 1;
+        if (ii < 0 || ii >= ht) continue;
+        for (int kj = 0; kj < 3; ++kj) {
+          const int jj = j + kj - 1;
+          if (jj < 0 || jj >= wt) continue;
+          const float f0 = f0a[ii * wt + jj], f1 = f1a[ii * wt + jj];
+#pragma unroll
+          for (int oc = 0; oc < 8; ++oc) {
+            hid[oc] = fmaf(Pm[SM_W1 + ((oc * 2 + 0) * 3 + ki) * 3 + kj], f0, hid[oc]);
+            hid[oc] = fmaf(Pm[SM_W1 + ((oc * 2 + 1) * 3 + ki) * 3 + kj], f1, hid[oc]);
           }
         }
-        hid[oc] = fmax_(acc + Pm[SM_B1 + oc], 0.0f);
       }
       float l0 = Pm[SM_B2 + 0], l1 = Pm[SM_B2 + 1];
 #pragma unroll
       for (int ic = 0; ic < 8; ++ic) {
-        l0 = fmaf(Pm[SM_W2 + ic], hid[ic], l0);
-        l1 = fmaf(Pm[SM_W2 + 8 + ic], hid[ic], l1);
+        const float hv = fmax_(hid[ic] + Pm[SM_B1 + ic], 0.0f);
+        l0 = fmaf(Pm[SM_W2 + ic], hv, l0);
+        l1 = fmaf(Pm[SM_W2 + 8 + ic], hv, l1);
       }
       const float mxl = fmax_(l0, l1);
       const float e0 = cr_exp(l0 - mxl), e1 = cr_exp(l1 - mxl);
       tiles[t * TILE_FLOATS + T_MT] = e0 / (e0 + e1);
     }
     MSYNC();
+    MSTAMP(14);
     if (S.m_out) {
+      // compact m(tile) and the nearest-upsample source of every row / column
+      float* mt = extra;
+      int* rsrc = (int*)(extra + NT);
+      int* csrc = rsrc + H;
+      MFOR(t, NT) mt[t] = tiles[t * TILE_FLOATS + T_MT];
+      MFOR(h, H) rsrc[h] = nearest_src(h, ht, H) * wt;
+      MFOR(w, W) csrc[w] = nearest_src(w, wt, W);
+      MSYNC();
       float* mo = S.m_out + (size_t)b * H * W;
-      MFOR(p, H * W) {
-        const int h = p / W, w = p - (p / W) * W;
-        float acc = 0.0f;
+      const int qpr = (W + 3) >> 2;
+      MFOR(q, H * qpr) {
+        const int h = q / qpr, w0 = (q - h * qpr) * 4;
+        float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        int cs[8];
 #pragma unroll
+        for (int u = 0; u < 8; ++u) cs[u] = csrc[imin_(imax_(w0 - 2 + u, 0), W - 1)];
         for (int i = 0; i < 5; ++i) {
-          const int hh = imin_(imax_(h + i - 2, 0), H - 1);
-          const int si = nearest_src(hh, ht, H);
+          const int rb = rsrc[imin_(imax_(h + i - 2, 0), H - 1)];
+          float seg[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) seg[u] = mt[rb + cs[u]];
 #pragma unroll
           for (int j = 0; j < 5; ++j) {
-            const int ww = imin_(imax_(w + j - 2, 0), W - 1);
-            const int sj = nearest_src(ww, wt, W);
-            acc = fmaf(bits_as_float(k_smooth5_bits[i * 5 + j]), tiles[(si * wt + sj) * TILE_FLOATS + T_MT], acc);
+            const float k = bits_as_float(k_smooth5_bits[i * 5 + j]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[r] = fmaf(k, seg[r + j], acc[r]);
           }
         }
-        mo[p] = acc;
+        if (w0 + 3 < W && (W & 3) == 0) {
+          store4(mo + h * W + w0, acc);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) if (w0 + r < W) mo[h * W + w0 + r] = acc[r];
+        }
       }
     }
     MSYNC();
   }
+  MSTAMP(15);
 }
 
 }  // namespace mcaq

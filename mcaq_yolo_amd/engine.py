@@ -87,7 +87,7 @@ class HookPlan:
             nb["bits"] = torch.empty(g.B, g.ht, g.wt, device=d)
             nb["m"] = torch.empty(g.B, 1, g.H, g.W, device=d)
             nb["y"] = torch.empty(g.B, g.C, g.H, g.W, device=d)
-            nb["phi"] = torch.empty(g.B, g.ht, g.wt, 8, device=d) if "phi" in want else None
+            nb["phi"] = torch.empty(g.B, g.ht, g.wt, 8, device=d)   # pass A -> pass B of mcaq_morph
             nb["cmlp"] = torch.empty(g.B, g.ht, g.wt, device=d) if "cmlp" in want else None
             if "debug" in want:
                 nb["edge"] = torch.empty(g.B, g.Hc, g.Wc, device=d, dtype=torch.uint8)

@@ -1,19 +1,47 @@
 """Pack reference-layout parameter tensors into the flat blobs the kernels read.
 
 The blob layouts are the CM_* / MM_* / SM_* offsets of
-mcaq_yolo_amd/csrc/mcaq_morph.h.  Input: mappings from the reference
+mcaq_yolo_amd/csrc/mcaq_morph.h (reference parameter order), followed for the
+two MLPs by the weight matrices re-laid-out as fp32 MFMA A operands
+(CMQ_* / MMQ_* in mcaq_mlp_mfma.h).  Input: mappings from the reference
 state_dict key suffixes (complexity_mlp.{0,1,3,4,6}.*, mapping_network.
 {0,1,3,4,6,7,9}.*, net.{0,2}.*) to tensors or arrays.
 """
 import numpy as np
 
 CM_SIZE, MM_SIZE, SM_SIZE = 2881, 4865, 170
+CMQ_SIZE = CM_SIZE + 512 + 2048      # + MFMA A-operand copies (mcaq_mlp_mfma.h)
+MMQ_SIZE = MM_SIZE + 128 + 2048 + 2048
 
 
 def _f(a):
     if hasattr(a, "detach"):
         a = a.detach().cpu().numpy()
     return np.asarray(a, np.float32).reshape(-1)
+
+
+def mfma_a_operands(Wm):
+    """Weight matrix (N_out, K) -> A operands of v_mfma_f32_32x32x2_f32 for the
+    transposed product D[neuron][tile]: [block][step][lane] with lane l holding
+    W[32*block + (l & 31)][2*step + (l >> 5)] (K zero-padded to even)."""
+    Wm = np.asarray(Wm, np.float32)
+    n, k = Wm.shape
+    kp = k + (k & 1)
+    nb = (n + 31) // 32
+    Wp = np.zeros((nb * 32, kp), np.float32)
+    Wp[:n, :k] = Wm
+    lane = np.arange(64)
+    out = np.empty((nb, kp // 2, 64), np.float32)
+    for b in range(nb):
+        for s in range(kp // 2):
+            out[b, s] = Wp[32 * b + (lane & 31), 2 * s + (lane >> 5)]
+    return out.reshape(-1)
+
+
+def _np2(a):
+    if hasattr(a, "detach"):
+        a = a.detach().cpu().numpy()
+    return np.asarray(a, np.float32)
 
 
 def pack_complexity_mlp(sd, prefix="complexity_mlp."):
@@ -24,7 +52,8 @@ def pack_complexity_mlp(sd, prefix="complexity_mlp."):
     out = np.concatenate([_f(p) for p in parts])
     if out.size != CM_SIZE:
         raise ValueError("complexity MLP must be the reference 8-64-32-1 shape (got %d params)" % out.size)
-    return out
+    return np.concatenate([out, mfma_a_operands(_np2(sd[prefix + "0.weight"])),
+                           mfma_a_operands(_np2(sd[prefix + "3.weight"]))])
 
 
 def pack_mapper_mlp(sd, prefix="mapping_network."):
@@ -37,7 +66,7 @@ def pack_mapper_mlp(sd, prefix="mapping_network."):
     out = np.concatenate([_f(p) for p in parts])
     if out.size != MM_SIZE:
         raise ValueError("bit mapper must use hidden_dims [32, 64, 32] (got %d params)" % out.size)
-    return out
+    return np.concatenate([out] + [mfma_a_operands(_np2(sd[prefix + "%d.weight" % i])) for i in (0, 3, 6)])
 
 
 def pack_soft_mask(sd, prefix="net."):

@@ -10,14 +10,20 @@
 
 extern "C" int emu_morph(const mcaq_morph_scale* s) {
   using namespace mcaq;
-  const int P = s->Hc * s->Wc, NT = s->ht * s->wt;
-  std::vector<char> planes(plane_bytes(P) + 64), shm(fixed_bytes() + tile_bytes(NT) + 64);
+  const int NT = s->ht * s->wt;
+  std::vector<char> planes(plane_bytes(s->Hc, s->Wc) + 64), shm(fixed_bytes() + tile_bytes(NT) + 64);
+  std::vector<char> tshm(tiles_lds_bytes(s->H, s->W, NT) + 64);
   for (int b = 0; b < s->B; ++b) {
-    Planes pl; Shared sh;
-    carve_planes(planes.data(), P, pl);
-    carve_shared(shm.data(), NT, sh);
     Ctx ctx{0, 1};
-    morph_image(ctx, *s, b, pl, sh);
+    if (s->flags & F_PHI) {
+      Planes pl; Shared sh;
+      carve_planes(planes.data(), s->Hc, s->Wc, pl);
+      carve_shared(shm.data(), sh);
+      morph_edges(ctx, *s, b, pl, sh);
+    }
+    Shared sh2;
+    carve_shared(tshm.data(), sh2);
+    morph_tiles(ctx, *s, b, sh2);
   }
   return 0;
 }

@@ -116,3 +116,35 @@ def test_emu_otsu_binarize_and_no_euler(emu):
     binm = (gray > thr[:, None, None]).astype(np.uint8)
     assert np.array_equal(out["bin"], binm)
     assert np.array_equal(out["phi"][..., 4], O.contour_tiles(binm, tile, contour_components=False))
+
+
+def test_emu_adaptive_threshold_near_ties(emu):
+    """Pixels placed within the separable estimate's error margin of the
+    adaptive threshold (g255 ~ mean - 2) take the exact 121-tap path; the
+    mask must still equal the oracle's bit for bit."""
+    rng = np.random.default_rng(7)
+    H = Wd = 64
+    x = rng.uniform(0.2, 0.8, size=(1, 1, H, Wd)).astype(f32)
+    x[0, 0, 0, 0], x[0, 0, -1, -1] = 0.0, 1.0          # normalize01 is then the identity
+    k = O.K["gauss11_adaptive"].astype(np.float64)
+    kc = k[5, 5]
+    marg = float(np.frombuffer(np.uint32(0x3B926590).tobytes(), f32)[0])
+    targets = []
+    for i, h in enumerate(range(8, H - 8, 12)):
+        for j, w in enumerate(range(8, Wd - 8, 12)):
+            g = x[0, 0].astype(np.float64) * 255.0
+            win = g[h - 5:h + 6, w - 5:w + 6]
+            others = float((k * win).sum() - kc * g[h, w])
+            delta = (-1.5e-3, 0.0, 1.5e-3, 4e-4)[(i + j) % 4]
+            v = (others - 2.0 + delta) / (1.0 - kc)      # g255 = mean(g255) - 2 + delta
+            x[0, 0, h, w] = f32(v / 255.0)
+            targets.append((h, w))
+    gray = O.normalize01(O.channel_mean(x, H, Wd))
+    assert np.array_equal(gray, x[:, 0])
+    g255 = (gray * f32(255.0)).astype(f32)
+    mean = O.conv2d(g255, O.K["gauss11_adaptive"], pad="replicate")
+    gap = np.abs(g255 - (mean - f32(2.0)))
+    near = sum(gap[0, h, w] <= marg for h, w in targets)
+    assert near >= len(targets) // 2, "construction must land inside the margin"
+    out = run_emu(emu, x, 8, abi.F_PHI)
+    assert np.array_equal(out["bin"], O.adaptive_binarize(gray))

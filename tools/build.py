@@ -13,25 +13,26 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "mcaq_yolo_amd", "csrc")
 OUT = os.path.join(ROOT, "mcaq_yolo_amd", "lib", "libmcaq_hip.so")
 SRCS = [os.path.join(CSRC, "mcaq_kernels.hip")]
-DEPS = SRCS + [os.path.join(CSRC, f) for f in ("mcaq_math.h", "mcaq_morph.h", "mcaq_tables.h")] + \
+DEPS = SRCS + [os.path.join(CSRC, f) for f in ("mcaq_math.h", "mcaq_morph.h", "mcaq_tables.h", "mcaq_mlp_mfma.h")] + \
     [os.path.join(ROOT, "include", "mcaq_hip.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-result"]
 
 
-def build(force=False, verbose=True):
-    if not force and os.path.exists(OUT) and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in DEPS):
-        return OUT
-    os.makedirs(os.path.dirname(OUT), exist_ok=True)
-    tmp = OUT + ".tmp"
-    cmd = [HIPCC] + FLAGS + ["-o", tmp] + SRCS
+def build(force=False, verbose=True, stamps=False):
+    out = OUT.replace(".so", "_stamps.so") if stamps else OUT
+    if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in DEPS):
+        return out
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    tmp = out + ".tmp"
+    cmd = [HIPCC] + FLAGS + (["-DMCAQ_STAMPS"] if stamps else []) + ["-o", tmp] + SRCS
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, OUT)
-    return OUT
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv))
+    print(build(force="--force" in sys.argv, stamps="--stamps" in sys.argv))

@@ -10,6 +10,7 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+from oracle.ieee import aten_sum, cr32  # noqa: E402
 from oracle.mcaq_oracle import K  # noqa: E402
 
 HDR = os.path.join(ROOT, "mcaq_yolo_amd", "csrc", "mcaq_tables.h")
@@ -21,10 +22,52 @@ def table(name, arr):
     return "MCAQ_TABLE uint32_t %s_bits[%d] = {%s};\n" % (name, a.size, words)
 
 
+def fractal_constants():
+    """Box-counting regression terms that depend only on the number of scales
+    S = log2(tile) (morphology.py:596-617, oracle.fractal_tiles): x = log(s),
+    w = exp(-0.1 i), and per S the scalars w_sum, x_mean, var."""
+    f32 = np.float32
+    x = cr32(np.log, np.array([2.0 ** (i + 1) for i in range(6)], f32))
+    w = cr32(np.exp, (f32(-0.1) * np.arange(6, dtype=f32)).astype(f32))
+    st = np.zeros((7, 4), f32)
+    for S in range(2, 7):
+        ws, xs = w[:S], x[:S]
+        w_sum = aten_sum(ws[:, None])[0]
+        x_mean = (aten_sum((ws * xs).astype(f32)[:, None])[0] / w_sum).astype(f32)
+        dx = (xs - x_mean).astype(f32)
+        var = aten_sum((ws * (dx * dx).astype(f32)).astype(f32)[:, None])[0]
+        st[S, :3] = (w_sum, x_mean, var)
+    return x, w, st
+
+
+def separable_g11():
+    """1-D factor of the 11x11 adaptive-threshold kernel and a proven bound on
+    |separable fp32 estimate - exact oneDNN-order 121-tap fp32 sum| (+ the two
+    roundings of `mean - C` and of the comparison difference) for inputs in
+    [0, 255] (mcaq_morph.h, binarize)."""
+    f32 = np.float32
+    k2 = np.asarray(K["gauss11_adaptive"], f32).astype(np.float64)
+    k1 = np.sqrt(np.diag(k2)).astype(f32)
+    k1d = k1.astype(np.float64)
+    u = 2.0 ** -24
+    s1 = float(np.abs(k1d).sum())
+    s2 = float(np.abs(k2).sum())
+    e_exact = 121 * u * 255.0 * max(s2, 1.0)
+    e_sep = 22 * u * 255.0 * max(s1, 1.0) ** 2
+    e_kern = 255.0 * float(np.abs(np.outer(k1d, k1d) - k2).sum())
+    e_sub = 3 * u * 300.0
+    margin = 2.0 * (e_exact + e_sep + e_kern + e_sub)
+    return k1, np.array([margin], f32)
+
+
 def main():
+    fx, fw, fst = fractal_constants()
+    k1, marg = separable_g11()
     body = "".join(table(n, K[k]) for n, k in (
         ("k_gauss5", "gauss5_canny"), ("k_gauss11", "gauss11_adaptive"),
         ("k_smooth5", "smooth5_softmask"), ("k_bilat_sp", "bilateral_spatial")))
+    body += table("k_frac_x", fx) + table("k_frac_w", fw) + table("k_frac_st", fst)
+    body += table("k_g11_sep", k1) + table("k_g11_margin", marg)
     src = open(HDR).read()
     a = src.index("// @@TABLES@@")
     b = src.index("}  // namespace mcaq")
