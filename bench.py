@@ -134,20 +134,19 @@ def main():
     L = plan.lib
     stream = torch.cuda.current_stream()
     from mcaq_yolo_amd import abi
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
-    kt = {"stats": 0.0, "finalize": 0.0, "morph": 0.0, "quant": 0.0}
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    kt = {"stats": 0.0, "morph_finalize": 0.0, "quant": 0.0}
     reps = 20
+    nf = plan._n if plan._fz is not None else 0
     for _ in range(reps):
         sh = abi.ctypes.c_void_p(stream.cuda_stream)
         ev[0].record(stream)
         L.mcaq_stats(plan._st, plan._n, sh)
         ev[1].record(stream)
-        L.mcaq_finalize(plan._fz, plan._n, sh)
+        L.mcaq_morph_finalize(plan._mo, plan._n, plan._fz, nf, sh)
         ev[2].record(stream)
-        L.mcaq_morph(plan._mo, plan._n, sh)
-        ev[3].record(stream)
         L.mcaq_quant(plan._qs, plan._n, sh)
-        ev[4].record(stream)
+        ev[3].record(stream)
         torch.cuda.synchronize()
         for i, k in enumerate(kt):
             kt[k] += ev[i].elapsed_time(ev[i + 1]) * 1e3 / reps   # us

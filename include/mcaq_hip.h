@@ -32,7 +32,7 @@ typedef void* hipStream_t;
 extern "C" {
 #endif
 
-#define MCAQ_ABI_VERSION 1
+#define MCAQ_ABI_VERSION 2
 /* largest dynamic LDS request of the morph kernel (gfx950: 160 KiB per CU) */
 #define MCAQ_MORPH_LDS_LIMIT 163840
 
@@ -54,9 +54,9 @@ int mcaq_launch_spatial_quantization(const float* input, const float* bit_map,
  * gray[b,h,w]    = mean_c x[b,c,h,w] over the crop h<Hc, w<Wc, in CPU-ATen
  *                  summation order (NULL to skip)
  * absmean[b,h,w] = mean_c |x[b,c,h,w]| over the full map (NULL to skip)
- * pmin/pmax      = per-(unit, channel) min/max partials, unit = 256 pixels of
- *                  one image: mcaq_stats_units(B,H,W) x C floats each (NULL to
- *                  skip). */
+ * pmin/pmax      = per-(unit, channel) min/max partials, unit = 64, 128 or 256
+ *                  pixels of one image: mcaq_stats_units(B,C,H,W) x C floats
+ *                  each (NULL to skip). */
 typedef struct {
   const float* x;  /* (B, C, H, W) fp32 contiguous */
   float* gray;     /* (B, Hc, Wc) */
@@ -67,7 +67,7 @@ typedef struct {
   int unit_begin;  /* set by the launcher */
 } mcaq_stats_scale;
 int mcaq_stats(const mcaq_stats_scale* scales, int nscales, hipStream_t stream);
-int mcaq_stats_units(int B, int H, int W);
+int mcaq_stats_units(int B, int C, int H, int W);
 
 /* ---- channel min/max over the batch (quantization.py:650-654) -------------- */
 typedef struct {
@@ -110,6 +110,10 @@ typedef struct {
   int block_begin;   /* set by the launcher */
 } mcaq_morph_scale;
 int mcaq_morph(const mcaq_morph_scale* scales, int nscales, hipStream_t stream);
+/* mcaq_morph + mcaq_finalize in one launch: the channel min/max reduction
+ * runs as extra workgroups beside the per-image ones (fscales may be NULL). */
+int mcaq_morph_finalize(const mcaq_morph_scale* scales, int nscales,
+                        const mcaq_finalize_scale* fscales, int nfscales, hipStream_t stream);
 size_t mcaq_morph_scratch_bytes(int B, int Hc, int Wc, int ht, int wt);
 
 /* ---- pass 2: y = dequant(quant_b(x)) * m ----------------------------------- */

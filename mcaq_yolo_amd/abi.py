@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libmcaq_hip.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -47,7 +47,7 @@ F_CONT, F_HAS_T, F_NORM_C, F_MAP_LINEAR = 16, 32, 64, 128
 F_BIN_OTSU, F_NO_EULER = 256, 512
 
 EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats", "mcaq_stats_units",
-           "mcaq_finalize", "mcaq_morph", "mcaq_morph_scratch_bytes", "mcaq_quant")
+           "mcaq_finalize", "mcaq_morph", "mcaq_morph_finalize", "mcaq_morph_scratch_bytes", "mcaq_quant")
 
 _LIB = None
 
@@ -65,8 +65,10 @@ def _declare(lib):
         f = getattr(lib, n)
         f.restype = I
         f.argtypes = [ctypes.POINTER(st), I, P]
+    lib.mcaq_morph_finalize.restype = I
+    lib.mcaq_morph_finalize.argtypes = [ctypes.POINTER(MorphScale), I, ctypes.POINTER(FinalizeScale), I, P]
     lib.mcaq_stats_units.restype = I
-    lib.mcaq_stats_units.argtypes = [I, I, I]
+    lib.mcaq_stats_units.argtypes = [I, I, I, I]
     lib.mcaq_morph_scratch_bytes.restype = ctypes.c_size_t
     lib.mcaq_morph_scratch_bytes.argtypes = [I, I, I, I, I]
     return lib

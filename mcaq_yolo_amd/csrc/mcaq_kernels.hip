@@ -32,113 +32,304 @@ extern "C" int mcaq_read_stamps(unsigned long long* out) {
 // ---------------------------------------------------------------------------
 // pass 1
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ float wave_min(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
-  return v;
-}
-__device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
-}
-
 struct StatsArgs {
   mcaq_stats_scale s[3];
+  int ppl[3];          // pixels per lane of each scale (1, 2 or 4)
   int nscales;
   int units_total;
 };
 
-constexpr int ST_PIX = 256;   // pixels per workgroup (one per lane)
-constexpr int ST_CG = 16;     // channels per load group (= one ATen cascade block)
+constexpr int ST_CG = 16;     // channels per block (= one ATen cascade block)
+constexpr int ST_WAVES = 4;   // waves per workgroup; wave w owns blocks w, w+4, ...
+constexpr int ST_LDS = 4096;  // floats of LDS (block sums; tail block sums)
 
-// unit = one 256-thread workgroup = 256 consecutive pixels of one image.
-// Lane = pixel: the channel loop runs the ATen cascade in registers; each
-// 16-channel group is one cascade block (a0 summed from 0, then folded).
-// Channel min/max: the group's values go through an LDS transpose
-// [16 ch][256 px] and are reduced by 16 threads per channel.
-__global__ __launch_bounds__(256) void mcaq_stats_kernel(StatsArgs a) {
-  __shared__ float tmn[ST_CG][ST_PIX + 4];
-  __shared__ float tmx[ST_CG][ST_PIX + 4];
-  const int unit = blockIdx.x;
-  int si = 0;
-  while (si + 1 < a.nscales && unit >= a.s[si + 1].unit_begin) ++si;
-  const mcaq_stats_scale& S = a.s[si];
-  const int tid = threadIdx.x;
-  const int lu = unit - S.unit_begin;
+// Pixels per lane: enough pixels per unit for 16-byte rows when one round of
+// blocks covers the channels, fewer (more units in flight) when the channel
+// loop needs several rounds.  Requires H*W % ppl == 0.
+static inline int stats_ppl(int C, int HW) {
+  const int nblk = (C + ST_CG - 1) / ST_CG;
+  const int rounds = (nblk + ST_WAVES - 1) / ST_WAVES;
+  int ppl = rounds <= 1 ? 4 : (rounds == 2 ? 2 : 1);
+  while (ppl > 1 && HW % ppl) ppl >>= 1;
+  return ppl;
+}
+
+// Per-lane values of 16 channels -> per-channel reduction over the wave.
+// Reduce-scatter inside each 16-lane row with DPP lane swaps (partners l^8,
+// l^7, l^2, l^1: each flips the bit that picks the kept half and keeps the
+// bits picked before, so lane l ends with one channel reduced over all 16
+// lanes of its row), then two cross-row exchanges.  Min and max are exact in
+// any order.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int H, int CTRL>
+__device__ __forceinline__ void rs_step(float (&mn)[16], float (&mx)[16], bool up) {
+#pragma unroll
+  for (int i = 0; i < H; ++i) {
+    const float smn = up ? mn[i] : mn[i + H], kmn = up ? mn[i + H] : mn[i];
+    const float smx = up ? mx[i] : mx[i + H], kmx = up ? mx[i + H] : mx[i];
+    mn[i] = fminf(kmn, dpp_f<CTRL>(smn));
+    mx[i] = fmaxf(kmx, dpp_f<CTRL>(smx));
+  }
+}
+// returns channel c(l) = 8*b3 + 4*b2 + 2*b1 + b0 of lane l (b = bits of l & 15)
+__device__ __forceinline__ void wave_minmax16(float (&mn)[ST_CG], float (&mx)[ST_CG], int lane, float& omn, float& omx) {
+  rs_step<8, 0x128>(mn, mx, (lane & 8) != 0);   // row_ror:8      (l ^ 8)
+  rs_step<4, 0x141>(mn, mx, (lane & 4) != 0);   // row_half_mirror (l ^ 7)
+  rs_step<2, 0x4E>(mn, mx, (lane & 2) != 0);    // quad_perm 2301 (l ^ 2)
+  rs_step<1, 0xB1>(mn, mx, (lane & 1) != 0);    // quad_perm 1032 (l ^ 1)
+  float a = mn[0], b = mx[0];
+  a = fminf(a, __shfl_xor(a, 16, 64)); b = fmaxf(b, __shfl_xor(b, 16, 64));
+  a = fminf(a, __shfl_xor(a, 32, 64)); b = fmaxf(b, __shfl_xor(b, 32, 64));
+  omn = a; omx = b;
+}
+
+// Fold one 16-row block sum into cascade levels a1..a3 (Cascade::push at i % 16 == 0).
+struct Fold {
+  float a0, a1, a2, a3;
+  int n;
+  __device__ __forceinline__ void init() { a0 = a1 = a2 = a3 = 0.0f; n = 0; }
+  __device__ __forceinline__ void full(float s) {
+    ++n;
+    a1 = a1 + s;
+    if ((n & 15) == 0) {
+      a2 = a2 + a1; a1 = 0.0f;
+      if ((n & 255) == 0) { a3 = a3 + a2; a2 = 0.0f; }
+    }
+  }
+  __device__ __forceinline__ float result() const { return ((a0 + a1) + a2) + a3; }
+};
+
+// Tail-column order (ATen row_sum: 4 interleaved cascades over channels
+// c = 4r + k, leftovers into partial 0) of pixel p, for x and |x| at once;
+// the per-pixel slow path (C > 1024).
+__device__ __noinline__ void tail_sums(const float* xb, int HW, int p, int C, float& og, float& oa) {
+  Cascade cg[4], ca[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) { cg[k].init(); ca[k].init(); }
+  const int n4 = (C / 4) * 4;
+  for (int c0 = 0; c0 < n4; c0 += 16) {
+    const int n = imin_(16, n4 - c0);
+    float v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = xb[(size_t)(c0 + (i < n ? i : 0)) * HW + p];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      if (i < n) { cg[i & 3].push(v[i]); ca[i & 3].push(fabsf(v[i])); }
+    }
+  }
+  float g0 = cg[0].result(), a0 = ca[0].result();
+  for (int r = n4; r < C; ++r) {
+    const float v = xb[(size_t)r * HW + p];
+    g0 = g0 + v; a0 = a0 + fabsf(v);
+  }
+  og = ((g0 + cg[1].result()) + cg[2].result()) + cg[3].result();
+  oa = ((a0 + ca[1].result()) + ca[2].result()) + ca[3].result();
+}
+
+// sequential channel sum of pixel p (the order of a cropped view's mean)
+__device__ __noinline__ float seq_sum(const float* xb, int HW, int p, int C) {
+  float sq = 0.0f;
+  for (int c0 = 0; c0 < C; c0 += 16) {
+    const int n = imin_(16, C - c0);
+    float v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = xb[(size_t)(c0 + (i < n ? i : 0)) * HW + p];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) if (i < n) sq = sq + v[i];
+  }
+  return sq;
+}
+
+// unit = one 256-thread workgroup = 64*PPL consecutive pixels of one image,
+// all channels.  Lane l of every wave owns pixels PPL*l .. PPL*l+PPL-1 (one
+// 4*PPL-byte load per channel row); the channels are cut into 16-row ATen
+// cascade blocks, wave w takes blocks w, w+4, ... and produces each block's
+// per-pixel sums (rows added sequentially from 0, the cascade's a0).  Per
+// round the four waves' block sums meet in LDS and thread t folds them, in
+// block order, into pixel t's cascade levels a1..a3: the exact CPU-ATen order
+// of x.mean(dim=1).  Channel min/max partials of the unit go straight from
+// registers.  The last (< 32) pixels of an image reduce in ATen's row_sum
+// order instead: their 4 x ceil(C/64) independent 16-row block sums are spread
+// over the workgroup (one load round trip), then folded per pixel.
+template <int PPL, bool kVec>
+__device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, float* lds) {
+  float (*bsg)[256] = reinterpret_cast<float (*)[256]>(lds);
+  float (*bsa)[256] = reinterpret_cast<float (*)[256]>(lds + ST_WAVES * 256);
+  constexpr int UPIX = 64 * PPL;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int HW = S.H * S.W;
-  const int upi = (HW + ST_PIX - 1) / ST_PIX;
+  const int upi = (HW + UPIX - 1) / UPIX;
   const int b = lu / upi, chunk = lu - b * upi;
   const int C = S.C;
   const float* xb = S.x + (size_t)b * C * HW;
   const bool cropped = (S.Hc != S.H) || (S.Wc != S.W);
-  const int p = chunk * ST_PIX + tid;
-  const bool valid = p < HW;
   const bool want_g = S.gray != nullptr, want_a = S.absmean != nullptr, want_m = S.pmin != nullptr;
-  const float* px = xb + (valid ? p : 0);
+  const int base = chunk * UPIX;
+  const int q0 = base + lane * PPL;                    // first pixel of this lane
+  bool pv[PPL];
+#pragma unroll
+  for (int k = 0; k < PPL; ++k) pv[k] = q0 + k < HW;
+  const int nblk = (C + ST_CG - 1) / ST_CG;
+  const int rounds = (nblk + ST_WAVES - 1) / ST_WAVES;
 
-  float g1 = 0.0f, g2 = 0.0f, g3 = 0.0f;   // cascade levels 1..3 (gray)
-  float a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;   // cascade levels 1..3 (|x|)
-  float ga0 = 0.0f, aa0 = 0.0f;            // open (partial) block
-  float sq = 0.0f;                          // sequential sum (cropped view)
-  int nblk = 0;
-  for (int c0 = 0; c0 < C; c0 += ST_CG) {
-    const int nc = C - c0 < ST_CG ? C - c0 : ST_CG;
-    float v[ST_CG];
-#pragma unroll
-    for (int i = 0; i < ST_CG; ++i) v[i] = (valid && i < nc) ? px[(size_t)(c0 + i) * HW] : 0.0f;
-    float gb = 0.0f, ab = 0.0f;
-#pragma unroll
-    for (int i = 0; i < ST_CG; ++i) {
-      if (i < nc) { gb = gb + v[i]; ab = ab + fabsf(v[i]); sq = sq + v[i]; }
-    }
-    if (nc == ST_CG) {       // a full cascade block: fold (Cascade::push at i % 16 == 0)
-      ++nblk;
-      g1 = g1 + gb; a1 = a1 + ab;
-      if ((nblk & 15) == 0) {
-        g2 = g2 + g1; g1 = 0.0f; a2 = a2 + a1; a1 = 0.0f;
-        if ((nblk & 255) == 0) { g3 = g3 + g2; g2 = 0.0f; a3 = a3 + a2; a2 = 0.0f; }
-      }
-    } else {
-      ga0 = gb; aa0 = ab;   // trailing partial block stays in a0
-    }
-    if (want_m) {
+  Fold fg, fa;   // pixel `tid` (tid < UPIX)
+  fg.init(); fa.init();
+  for (int r = 0; r < rounds; ++r) {
+    const int blk = r * ST_WAVES + wv;
+    if (blk < nblk) {
+      const int c0 = blk * ST_CG;
+      const int nc = imin_(ST_CG, C - c0);
+      // branch-free loads (clamped addresses, invalid pixels masked later) so
+      // all 16 rows are in flight together
+      float v[ST_CG][PPL];
+      const int qa = pv[0] ? q0 : 0;
 #pragma unroll
       for (int i = 0; i < ST_CG; ++i) {
-        tmn[i][tid] = valid ? v[i] : 3.402823466e38f;
-        tmx[i][tid] = valid ? v[i] : -3.402823466e38f;
-      }
-      __syncthreads();
-      const int ci = tid >> 4, part = tid & 15;
-      float mn = tmn[ci][part * 16], mx = tmx[ci][part * 16];
+        const float* row = xb + (size_t)(c0 + (i < nc ? i : 0)) * HW;
+        if (kVec && PPL == 4) {
+          const float4 t = *reinterpret_cast<const float4*>(row + qa);
+          v[i][0] = t.x; v[i][1 % PPL] = t.y; v[i][2 % PPL] = t.z; v[i][3 % PPL] = t.w;
+        } else if (kVec && PPL == 2) {
+          const float2 t = *reinterpret_cast<const float2*>(row + qa);
+          v[i][0] = t.x; v[i][1 % PPL] = t.y;
+        } else {
 #pragma unroll
-      for (int k = 1; k < 16; ++k) { mn = fminf(mn, tmn[ci][part * 16 + k]); mx = fmaxf(mx, tmx[ci][part * 16 + k]); }
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) { mn = fminf(mn, __shfl_xor(mn, o, 64)); mx = fmaxf(mx, __shfl_xor(mx, o, 64)); }
-      if (part == 0 && ci < nc) {
-        S.pmin[(size_t)lu * C + c0 + ci] = mn;
-        S.pmax[(size_t)lu * C + c0 + ci] = mx;
+          for (int k = 0; k < PPL; ++k) v[i][k] = row[imin_(q0 + k, HW - 1)];
+        }
       }
-      __syncthreads();
+      float gb[PPL], ab[PPL];
+#pragma unroll
+      for (int k = 0; k < PPL; ++k) { gb[k] = 0.0f; ab[k] = 0.0f; }
+#pragma unroll
+      for (int i = 0; i < ST_CG; ++i) {
+        if (i < nc) {
+#pragma unroll
+          for (int k = 0; k < PPL; ++k) { gb[k] = gb[k] + v[i][k]; ab[k] = ab[k] + fabsf(v[i][k]); }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < PPL; ++k) { bsg[wv][lane * PPL + k] = gb[k]; bsa[wv][lane * PPL + k] = ab[k]; }
+      if (want_m) {
+        float mn[ST_CG], mx[ST_CG];
+#pragma unroll
+        for (int i = 0; i < ST_CG; ++i) {
+          float lo = 3.402823466e38f, hi = -3.402823466e38f;
+#pragma unroll
+          for (int k = 0; k < PPL; ++k) {
+            lo = fminf(lo, pv[k] ? v[i][k] : 3.402823466e38f);
+            hi = fmaxf(hi, pv[k] ? v[i][k] : -3.402823466e38f);
+          }
+          mn[i] = lo; mx[i] = hi;
+        }
+        float omn, omx;
+        wave_minmax16(mn, mx, lane, omn, omx);
+        if (lane < 16 && lane < nc) {
+          S.pmin[(size_t)lu * C + c0 + lane] = omn;
+          S.pmax[(size_t)lu * C + c0 + lane] = omx;
+        }
+      }
+    }
+    __syncthreads();
+    if (tid < UPIX) {
+      const int nslot = imin_(ST_WAVES, nblk - r * ST_WAVES);
+      for (int s = 0; s < nslot; ++s) {
+        const int blk2 = r * ST_WAVES + s;
+        if (C - blk2 * ST_CG >= ST_CG) { fg.full(bsg[s][tid]); fa.full(bsa[s][tid]); }
+        else { fg.a0 = bsg[s][tid]; fa.a0 = bsa[s][tid]; }   // trailing partial block stays in a0
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- tail columns (row_sum order), all in the image's last unit
+  const int tstart = imax_(aten_tail_start(HW), base);
+  const int tend = imin_(HW, base + UPIX);
+  const int ntail = tend - tstart;
+  const int nilp = C >> 2;                        // rows per interleaved cascade
+  const int nbt = (nilp + 15) >> 4;               // 16-row blocks per cascade
+  const bool need_tail = ntail > 0 && (want_a || (want_g && !cropped));
+  const bool coop = nbt <= 16;                    // 31 px x 4 x 16 x 2 floats fit the LDS
+  float tg = 0.0f, ta = 0.0f;
+  if (need_tail && coop) {
+    float* tsg = lds;                             // [px][k][j]
+    float* tsa = lds + ST_LDS / 2;
+    const int items = ntail * 4 * nbt;
+    for (int it = tid; it < items; it += 256) {
+      const int i = it / (4 * nbt), rem = it - i * (4 * nbt);
+      const int k = rem / nbt, j = rem - k * nbt;
+      const int p = tstart + i;
+      const int r0 = 16 * j, n = imin_(16, nilp - r0);
+      float v[16];
+#pragma unroll
+      for (int e = 0; e < 16; ++e) v[e] = xb[(size_t)(4 * (r0 + (e < n ? e : 0)) + k) * HW + p];
+      float sg = 0.0f, sa = 0.0f;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) if (e < n) { sg = sg + v[e]; sa = sa + fabsf(v[e]); }
+      tsg[it] = sg; tsa[it] = sa;
+    }
+    __syncthreads();
+    const int i = tid - (tstart - base);
+    if (i >= 0 && i < ntail) {
+      const int p = tstart + i;
+      float rg[4], ra[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        Fold cg, ca;
+        cg.init(); ca.init();
+        for (int j = 0; j < nbt; ++j) {
+          const float sg = tsg[(i * 4 + k) * nbt + j], sa = tsa[(i * 4 + k) * nbt + j];
+          if (nilp - 16 * j >= 16) { cg.full(sg); ca.full(sa); } else { cg.a0 = sg; ca.a0 = sa; }
+        }
+        rg[k] = cg.result(); ra[k] = ca.result();
+      }
+      for (int rr = 4 * nilp; rr < C; ++rr) {      // leftover rows into partial 0
+        const float v = xb[(size_t)rr * HW + p];
+        rg[0] = rg[0] + v; ra[0] = ra[0] + fabsf(v);
+      }
+      tg = ((rg[0] + rg[1]) + rg[2]) + rg[3];
+      ta = ((ra[0] + ra[1]) + ra[2]) + ra[3];
     }
   }
-  if (!valid) return;
+
+  if (tid >= UPIX) return;
+  const int p = base + tid;
+  if (p >= HW) return;
   const float fC = (float)C;
-  const bool tail = p >= aten_tail_start(HW);
-  if (want_a) {
-    float s = ((aa0 + a1) + a2) + a3;
-    if (tail) s = aten_sum(C, true, [&](int r) { return fabsf(xb[(size_t)r * HW + p]); });
-    S.absmean[(size_t)b * HW + p] = s / fC;
+  float sg = fg.result(), sa = fa.result();
+  if (need_tail && p >= tstart) {
+    if (coop) { sg = tg; sa = ta; }
+    else tail_sums(xb, HW, p, C, sg, sa);
   }
+  if (want_a) S.absmean[(size_t)b * HW + p] = sa / fC;
   if (want_g) {
-    const int h = p / S.W, w = p - (p / S.W) * S.W;
+    const int h = p / S.W, w = p - h * S.W;
     if (cropped) {
-      if (h < S.Hc && w < S.Wc) S.gray[((size_t)b * S.Hc + h) * S.Wc + w] = sq / fC;
+      // a cropped (non-contiguous) view reduces sequentially (L2-hot re-read)
+      if (h < S.Hc && w < S.Wc) {
+        const float sq = seq_sum(xb, HW, p, C);
+        S.gray[((size_t)b * S.Hc + h) * S.Wc + w] = sq / fC;
+      }
     } else {
-      float s = ((ga0 + g1) + g2) + g3;
-      if (tail) s = aten_sum(C, true, [&](int r) { return xb[(size_t)r * HW + p]; });
-      S.gray[(size_t)b * HW + p] = s / fC;
+      S.gray[(size_t)b * HW + p] = sg / fC;
     }
+  }
+}
+
+template <bool kVec>   // kVec: 8/16-byte row accesses for ppl 2/4 (host checks alignment)
+__global__ __launch_bounds__(256, 4) void mcaq_stats_kernel(StatsArgs a) {
+  __shared__ float lds[ST_LDS];
+  // heaviest (most channels per pixel) scales are the last ones: start them first
+  const int unit = a.units_total - 1 - (int)blockIdx.x;
+  int si = 0;
+  while (si + 1 < a.nscales && unit >= a.s[si + 1].unit_begin) ++si;
+  const int lu = unit - a.s[si].unit_begin;
+  switch (a.ppl[si]) {
+    case 4: stats_unit<4, kVec>(a.s[si], lu, lds); break;
+    case 2: stats_unit<2, kVec>(a.s[si], lu, lds); break;
+    default: stats_unit<1, kVec>(a.s[si], lu, lds); break;
   }
 }
 
@@ -148,44 +339,56 @@ __global__ __launch_bounds__(256) void mcaq_stats_kernel(StatsArgs a) {
 struct FinalizeArgs {
   mcaq_finalize_scale s[3];
   int nscales;
+  int nblocks;
 };
 
-// one workgroup = 64 channels x 4 unit-parts
-__global__ __launch_bounds__(256) void mcaq_finalize_kernel(FinalizeArgs a) {
-  __shared__ float rmn[4][64], rmx[4][64];
+// one workgroup = 64 channels x (blockDim / 64) unit-parts; `red` holds
+// 2 * blockDim floats of LDS.  Runs as its own kernel or as extra workgroups
+// of the morph launch (which leaves most CUs idle: the reduction is free there).
+__device__ __forceinline__ void finalize_body(const FinalizeArgs& a, int blk, float* red) {
   int si = 0;
-  while (si + 1 < a.nscales && (int)blockIdx.x >= a.s[si + 1].block_begin) ++si;
+  while (si + 1 < a.nscales && blk >= a.s[si + 1].block_begin) ++si;
   const mcaq_finalize_scale& S = a.s[si];
+  const int nthr = (int)blockDim.x, parts = nthr >> 6;
   const int cl = threadIdx.x & 63, part = threadIdx.x >> 6;
-  const int c = ((int)blockIdx.x - S.block_begin) * 64 + cl;
+  const int c = (blk - S.block_begin) * 64 + cl;
   const bool cv = c < S.C;
   float mn = 3.402823466e38f, mx = -3.402823466e38f;
   if (cv) {
     if (S.pmin) {
+      const float* pn = S.pmin + c;
+      const float* px = S.pmax + c;
+      const size_t st = (size_t)S.C * parts;
       int u = part;
-      for (; u + 12 < S.nunits; u += 16) {
-        const float m0 = S.pmin[(size_t)u * S.C + c], m1 = S.pmin[(size_t)(u + 4) * S.C + c];
-        const float m2 = S.pmin[(size_t)(u + 8) * S.C + c], m3 = S.pmin[(size_t)(u + 12) * S.C + c];
-        const float x0 = S.pmax[(size_t)u * S.C + c], x1 = S.pmax[(size_t)(u + 4) * S.C + c];
-        const float x2 = S.pmax[(size_t)(u + 8) * S.C + c], x3 = S.pmax[(size_t)(u + 12) * S.C + c];
+      for (; u + 3 * parts < S.nunits; u += 4 * parts) {
+        const size_t o = (size_t)u * S.C;
+        const float m0 = pn[o], m1 = pn[o + st], m2 = pn[o + 2 * st], m3 = pn[o + 3 * st];
+        const float x0 = px[o], x1 = px[o + st], x2 = px[o + 2 * st], x3 = px[o + 3 * st];
         mn = fminf(mn, fminf(fminf(m0, m1), fminf(m2, m3)));
         mx = fmaxf(mx, fmaxf(fmaxf(x0, x1), fmaxf(x2, x3)));
       }
-      for (; u < S.nunits; u += 4) {
-        mn = fminf(mn, S.pmin[(size_t)u * S.C + c]);
-        mx = fmaxf(mx, S.pmax[(size_t)u * S.C + c]);
+      for (; u < S.nunits; u += parts) {
+        mn = fminf(mn, pn[(size_t)u * S.C]);
+        mx = fmaxf(mx, px[(size_t)u * S.C]);
       }
     } else if (part == 0) {
       mn = S.min_in[(size_t)S.min_stride * c];
       mx = S.max_in[(size_t)S.min_stride * c];
     }
   }
-  rmn[part][cl] = mn; rmx[part][cl] = mx;
+  red[part * 64 + cl] = mn;
+  red[nthr + part * 64 + cl] = mx;
   __syncthreads();
   if (part == 0 && cv) {
-    S.min_out[c] = fminf(fminf(rmn[0][cl], rmn[1][cl]), fminf(rmn[2][cl], rmn[3][cl]));
-    S.max_out[c] = fmaxf(fmaxf(rmx[0][cl], rmx[1][cl]), fmaxf(rmx[2][cl], rmx[3][cl]));
+    for (int k = 1; k < parts; ++k) { mn = fminf(mn, red[k * 64 + cl]); mx = fmaxf(mx, red[nthr + k * 64 + cl]); }
+    S.min_out[c] = mn;
+    S.max_out[c] = mx;
   }
+}
+
+__global__ __launch_bounds__(256) void mcaq_finalize_kernel(FinalizeArgs a) {
+  __shared__ float red[2 * 256];
+  finalize_body(a, (int)blockIdx.x, red);
 }
 
 // ---------------------------------------------------------------------------
@@ -202,8 +405,13 @@ __device__ __forceinline__ int morph_scale_of(const MorphArgs& a) {
 }
 
 template <bool kLDS>
-__global__ __launch_bounds__(MORPH_THREADS) void mcaq_morph_kernel(MorphArgs a, int plane_stride) {
+__global__ __launch_bounds__(MORPH_THREADS) void mcaq_morph_kernel(MorphArgs a, int plane_stride, FinalizeArgs f) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nimg = a.s[a.nscales - 1].block_begin + a.s[a.nscales - 1].B;
+  if ((int)blockIdx.x >= nimg) {   // channel min/max workgroups ride along
+    finalize_body(f, (int)blockIdx.x - nimg, reinterpret_cast<float*>(smem));
+    return;
+  }
   const MorphScale& S = a.s[morph_scale_of(a)];
   const int b = (int)blockIdx.x - S.block_begin;
   if (b >= S.B || !(S.flags & F_PHI)) return;
@@ -232,7 +440,7 @@ __global__ __launch_bounds__(TILES_THREADS) void mcaq_tiles_kernel(MorphArgs a) 
 }
 
 // ---------------------------------------------------------------------------
-// pass 2: y = dequant(quant_b(x)) * m, one wave = 256 pixels x a channel slice
+// pass 2: y = dequant(quant_b(x)) * m
 // ---------------------------------------------------------------------------
 struct QuantArgs {
   mcaq_quant_scale s[3];
@@ -240,16 +448,24 @@ struct QuantArgs {
   int units_total;
 };
 
-constexpr int QSLICE = 16;     // channels per unit
+constexpr int QSLICE = 32;     // channels per unit (8 per wave)
+constexpr int QCW = 8;         // channels per wave
 constexpr int QMAXBITS = 15;   // max entries per channel in the LDS table
 
-__global__ __launch_bounds__(64) void mcaq_quant_kernel(QuantArgs a) {
-  __shared__ float qt[QSLICE * QMAXBITS * 2];
+// unit = 256 pixels x 32 channels of one image; lane l of every wave owns
+// pixels 4l..4l+3 (16-byte accesses), wave w channels 8w..8w+7 of the slice,
+// all eight rows loaded before any is computed.  Per-pixel tile bits and the
+// soft-mask value are fetched once; per-(channel, bits) scale / zero-point
+// come from an LDS table built by the workgroup (IEEE divisions, as
+// QuantizationParameters computes them).
+template <bool kVec>
+__global__ __launch_bounds__(256) void mcaq_quant_kernel(QuantArgs a) {
+  __shared__ float2 qt[QSLICE * QMAXBITS];
   const int unit = blockIdx.x;
   int si = 0;
   while (si + 1 < a.nscales && unit >= a.s[si + 1].unit_begin) ++si;
   const mcaq_quant_scale& S = a.s[si];
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int HW = S.H * S.W;
   const int upi = (HW + 255) / 256;
   const int nsl = (S.C + QSLICE - 1) / QSLICE;
@@ -260,24 +476,20 @@ __global__ __launch_bounds__(64) void mcaq_quant_kernel(QuantArgs a) {
   const int c0 = slice * QSLICE;
   const int nc = imin_(QSLICE, S.C - c0);
   const int NB = S.nbits;
-  for (int i = lane; i < nc * NB; i += 64) {
+  for (int i = tid; i < nc * NB; i += 256) {
     const int c = i / NB, k = i - (i / NB) * NB;
     const QParam q = qparam(S.xmin[c0 + c], S.xmax[c0 + c], S.bits_lo + k);
-    qt[2 * i + 0] = q.scale;
-    qt[2 * i + 1] = q.zp;
+    qt[i] = make_float2(q.scale, q.zp);
   }
-  __syncthreads();
 
-  const int p0 = chunk * 256 + lane * 4;
-  bool valid[4];
+  const int q0 = chunk * 256 + lane * 4;
+  bool pv[4];
   int kb[4];
   float mv[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const int p = p0 + k;
-    valid[k] = p < HW;
-    kb[k] = 0; mv[k] = 1.0f;
-    if (!valid[k]) continue;
+    const int p = imin_(q0 + k, HW - 1);
+    pv[k] = q0 + k < HW;
     const int h = p / S.W, w = p - (p / S.W) * S.W;
     int th, tw;
     if (S.compat_tile_h > 0) {   // spatial_quantize contract: h / tile_h, clamped
@@ -288,44 +500,58 @@ __global__ __launch_bounds__(64) void mcaq_quant_kernel(QuantArgs a) {
       tw = nearest_src(w, S.wt, S.W);
     }
     const float bv = S.bits[((size_t)b * S.ht + th) * S.wt + tw];
-    int bi = (int)rintf(bv);
-    bi = imin_(imax_(bi, S.bits_lo), S.bits_lo + NB - 1);
-    kb[k] = bi - S.bits_lo;
-    if (S.m) mv[k] = S.m[(size_t)b * HW + p];
+    kb[k] = imin_(imax_((int)rintf(bv), S.bits_lo), S.bits_lo + NB - 1) - S.bits_lo;
+    mv[k] = S.m ? S.m[(size_t)b * HW + p] : 1.0f;
   }
-  const bool vec4 = ((HW & 3) == 0) && valid[3];
-  const float* xb = S.x + ((size_t)b * S.C + c0) * HW;
-  float* yb = S.y + ((size_t)b * S.C + c0) * HW;
   const bool has_m = S.m != nullptr;
-  for (int c = 0; c < nc; ++c) {
-    const float* row = xb + (size_t)c * HW;
-    float* orow = yb + (size_t)c * HW;
-    float v[4];
-    if (vec4) {
-      const float4 q = *reinterpret_cast<const float4*>(row + p0);
-      v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
-    } else {
+  float qlo[4], qhi[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = valid[k] ? row[p0 + k] : 0.0f;
+  for (int k = 0; k < 4; ++k) {
+    const int bb = S.bits_lo + kb[k];
+    qlo[k] = (float)(-(1 << (bb - 1)));
+    qhi[k] = (float)((1 << (bb - 1)) - 1);
+  }
+  const int cw = wv * QCW;                 // first channel of this wave in the slice
+  const int ncw = imin_(QCW, nc - cw);     // may be <= 0 for a short last slice
+  const size_t rowbase = ((size_t)b * S.C + c0 + cw) * HW;
+  const float* xb = S.x + rowbase;
+  float* yb = S.y + rowbase;
+  float v[QCW][4];
+  const int qa = pv[0] ? q0 : 0;
+  if (ncw > 0) {
+#pragma unroll
+    for (int c = 0; c < QCW; ++c) {
+      const float* row = xb + (size_t)(c < ncw ? c : 0) * HW;
+      if (kVec) {
+        const float4 t = *reinterpret_cast<const float4*>(row + qa);
+        v[c][0] = t.x; v[c][1] = t.y; v[c][2] = t.z; v[c][3] = t.w;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[c][k] = row[imin_(q0 + k, HW - 1)];
+      }
     }
+  }
+  __syncthreads();   // qt ready
+  if (ncw <= 0) return;
+#pragma unroll
+  for (int c = 0; c < QCW; ++c) {
+    if (c >= ncw) break;
     float o[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
+      const float2 sz = qt[(cw + c) * NB + kb[k]];
       QParam q;
-      q.scale = qt[(c * NB + kb[k]) * 2 + 0];
-      q.zp = qt[(c * NB + kb[k]) * 2 + 1];
-      const int bb = S.bits_lo + kb[k];
-      q.qmin = (float)(-(1 << (bb - 1)));
-      q.qmax = (float)((1 << (bb - 1)) - 1);
-      float d = quant_dequant(v[k], q);
+      q.scale = sz.x; q.zp = sz.y; q.qmin = qlo[k]; q.qmax = qhi[k];
+      float d = quant_dequant(v[c][k], q);
       if (has_m) d = d * mv[k];
       o[k] = d;
     }
-    if (vec4) {
-      *reinterpret_cast<float4*>(orow + p0) = make_float4(o[0], o[1], o[2], o[3]);
+    float* orow = yb + (size_t)c * HW;
+    if (kVec) {
+      if (pv[0]) *reinterpret_cast<float4*>(orow + q0) = make_float4(o[0], o[1], o[2], o[3]);
     } else {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) if (valid[k]) orow[p0 + k] = o[k];
+      for (int k = 0; k < 4; ++k) if (pv[k]) orow[q0 + k] = o[k];
     }
   }
 }
@@ -359,29 +585,49 @@ int mcaq_stats(const mcaq_stats_scale* scales, int nscales, hipStream_t stream) 
     a.s[i] = scales[i];
     a.s[i].unit_begin = units;
     const int HW = scales[i].H * scales[i].W;
-    if (scales[i].B < 1 || scales[i].C < 1 || HW < 1) return (int)hipErrorInvalidValue;
-    units += scales[i].B * ((HW + ST_PIX - 1) / ST_PIX);
+    if (scales[i].B < 1 || scales[i].C < 1 || HW < 1 || !scales[i].x) return (int)hipErrorInvalidValue;
+    if ((scales[i].pmin == nullptr) != (scales[i].pmax == nullptr)) return (int)hipErrorInvalidValue;
+    a.ppl[i] = stats_ppl(scales[i].C, HW);
+    units += mcaq_stats_units(scales[i].B, scales[i].C, scales[i].H, scales[i].W);
   }
   a.nscales = nscales;
   a.units_total = units;
-  hipLaunchKernelGGL(mcaq_stats_kernel, dim3(units), dim3(256), 0, stream, a);
+  // 16-byte (ppl 4) / 8-byte (ppl 2) rows need 16/8-byte aligned bases
+  bool vec = true;
+  for (int i = 0; i < nscales; ++i) vec = vec && ((uintptr_t)scales[i].x & 15) == 0;
+  if (vec)
+    hipLaunchKernelGGL(mcaq_stats_kernel<true>, dim3(units), dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL(mcaq_stats_kernel<false>, dim3(units), dim3(256), 0, stream, a);
   return (int)hipGetLastError();
 }
 
-int mcaq_stats_units(int B, int H, int W) { return B * ((H * W + 255) / 256); }
+int mcaq_stats_units(int B, int C, int H, int W) {
+  const int HW = H * W;
+  return B * ((HW + 64 * stats_ppl(C, HW) - 1) / (64 * stats_ppl(C, HW)));
+}
 
-int mcaq_finalize(const mcaq_finalize_scale* scales, int nscales, hipStream_t stream) {
+static int finalize_args(const mcaq_finalize_scale* scales, int nscales, FinalizeArgs& a) {
   if (nscales < 1 || nscales > 3) return (int)hipErrorInvalidValue;
-  FinalizeArgs a;
   int blocks = 0;
   for (int i = 0; i < nscales; ++i) {
     a.s[i] = scales[i];
     a.s[i].block_begin = blocks;
     if (scales[i].C < 1 || !scales[i].min_out || !scales[i].max_out) return (int)hipErrorInvalidValue;
+    if (scales[i].pmin ? (!scales[i].pmax || scales[i].nunits < 1) : (!scales[i].min_in || !scales[i].max_in))
+      return (int)hipErrorInvalidValue;
     blocks += (scales[i].C + 63) / 64;
   }
   a.nscales = nscales;
-  hipLaunchKernelGGL(mcaq_finalize_kernel, dim3(blocks), dim3(256), 0, stream, a);
+  a.nblocks = blocks;
+  return 0;
+}
+
+int mcaq_finalize(const mcaq_finalize_scale* scales, int nscales, hipStream_t stream) {
+  FinalizeArgs a;
+  const int e = finalize_args(scales, nscales, a);
+  if (e) return e;
+  hipLaunchKernelGGL(mcaq_finalize_kernel, dim3(a.nblocks), dim3(256), 0, stream, a);
   return (int)hipGetLastError();
 }
 
@@ -426,7 +672,17 @@ size_t mcaq_morph_scratch_bytes(int B, int Hc, int Wc, int ht, int wt) {
 }
 
 int mcaq_morph(const mcaq_morph_scale* scales, int nscales, hipStream_t stream) {
+  return mcaq_morph_finalize(scales, nscales, nullptr, 0, stream);
+}
+
+int mcaq_morph_finalize(const mcaq_morph_scale* scales, int nscales, const mcaq_finalize_scale* fscales,
+                        int nfscales, hipStream_t stream) {
   if (nscales < 1 || nscales > 3) return (int)hipErrorInvalidValue;
+  FinalizeArgs fa{};
+  if (nfscales > 0) {
+    const int fe = finalize_args(fscales, nfscales, fa);
+    if (fe) return fe;
+  }
   MorphArgs a;
   int blocks = 0, any_phi = 0, any_tiles = 0, tlds = 0;
   for (int i = 0; i < nscales; ++i) {
@@ -447,10 +703,16 @@ int mcaq_morph(const mcaq_morph_scale* scales, int nscales, hipStream_t stream) 
     if (tf) tlds = imax_(tlds, tiles_lds_bytes(S.H, S.W, S.ht * S.wt));
   }
   a.nscales = nscales;
+  if (!any_phi && fa.nblocks > 0) {   // nothing to ride along with
+    hipLaunchKernelGGL(mcaq_finalize_kernel, dim3(fa.nblocks), dim3(256), 0, stream, fa);
+    const hipError_t fe = hipGetLastError();
+    if (fe != hipSuccess) return (int)fe;
+  }
   if (any_phi) {
     int mode, stride; size_t dyn;
     int e = morph_plan(a.s, nscales, &mode, &stride, &dyn);
     if (e) return e;
+    if (fa.nblocks > 0 && dyn < (size_t)(8 * MORPH_THREADS)) dyn = 8 * MORPH_THREADS;  // finalize_body's LDS
     if (!mode)
       for (int i = 0; i < nscales; ++i)
         if (!a.s[i].gscratch && (a.s[i].flags & F_PHI)) return (int)hipErrorInvalidValue;
@@ -462,7 +724,7 @@ int mcaq_morph(const mcaq_morph_scale* scales, int nscales, hipStream_t stream) 
         if (ae != hipSuccess) return (int)ae;
         set_true = morph_lds_budget();
       }
-      hipLaunchKernelGGL(mcaq_morph_kernel<true>, dim3(blocks), dim3(MORPH_THREADS), dyn, stream, a, stride);
+      hipLaunchKernelGGL(mcaq_morph_kernel<true>, dim3(blocks + fa.nblocks), dim3(MORPH_THREADS), dyn, stream, a, stride, fa);
     } else {
       static int set_false = 0;
       if ((int)dyn > set_false) {
@@ -471,7 +733,7 @@ int mcaq_morph(const mcaq_morph_scale* scales, int nscales, hipStream_t stream) 
         if (ae != hipSuccess) return (int)ae;
         set_false = morph_lds_budget();
       }
-      hipLaunchKernelGGL(mcaq_morph_kernel<false>, dim3(blocks), dim3(MORPH_THREADS), dyn, stream, a, stride);
+      hipLaunchKernelGGL(mcaq_morph_kernel<false>, dim3(blocks + fa.nblocks), dim3(MORPH_THREADS), dyn, stream, a, stride, fa);
     }
     hipError_t le = hipGetLastError();
     if (le != hipSuccess) return (int)le;
@@ -507,7 +769,12 @@ int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream) 
   }
   a.nscales = nscales;
   a.units_total = units;
-  hipLaunchKernelGGL(mcaq_quant_kernel, dim3(units), dim3(64), 0, stream, a);
+  bool vec = true;
+  for (int i = 0; i < nscales; ++i) vec = vec && ((scales[i].H * scales[i].W) & 3) == 0;
+  if (vec)
+    hipLaunchKernelGGL(mcaq_quant_kernel<true>, dim3(units), dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL(mcaq_quant_kernel<false>, dim3(units), dim3(256), 0, stream, a);
   return (int)hipGetLastError();
 }
 

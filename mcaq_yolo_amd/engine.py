@@ -3,10 +3,11 @@
 A step over up to three hook scales (C3/C4/C5) is four kernel launches on one
 HIP stream:
 
-    mcaq_stats     HBM pass 1: x -> gray, |x| channel means, min/max partials
-    mcaq_finalize  per-channel batch min/max      (+ optional RCCL all-reduce)
-    mcaq_morph     one workgroup per image: phi, complexity, bits, soft mask
-    mcaq_quant     HBM pass 2: y = dequant(quant_b(x)) * m
+    mcaq_stats            HBM pass 1: x -> gray, |x| channel means, min/max partials
+    mcaq_morph_finalize   one workgroup per image: phi, complexity, bits, soft
+                          mask; plus workgroups reducing the per-channel batch
+                          min/max                (+ optional RCCL all-reduce)
+    mcaq_quant            HBM pass 2: y = dequant(quant_b(x)) * m
 
 All buffers of a `HookPlan` are allocated once, so `HookPlan.run` only
 enqueues launches and can be captured into a HIP graph (torch.cuda.CUDAGraph).
@@ -74,7 +75,7 @@ class HookPlan:
         d = self.device
         self.bufs = []
         for g in self.geoms:
-            units = self.lib.mcaq_stats_units(g.B, g.H, g.W)
+            units = self.lib.mcaq_stats_units(g.B, g.C, g.H, g.W)
             nb = {}
             nb["units"] = units
             nb["gray"] = torch.empty(g.B, g.Hc, g.Wc, device=d)
@@ -214,11 +215,12 @@ class HookPlan:
         n = self._n
         sh = _stream_handle(stream)
         abi.check(L.mcaq_stats(self._st, n, sh), "mcaq_stats")
-        if self._fz is not None:
-            abi.check(L.mcaq_finalize(self._fz, n, sh), "mcaq_finalize")
-            if process_group is not None:
-                sync_channel_minmax(self.bufs, process_group)
-        abi.check(L.mcaq_morph(self._mo, n, sh), "mcaq_morph")
+        # the channel min/max reduction rides along as extra workgroups of the
+        # morph launch (the per-image workgroups leave most CUs idle)
+        nf = n if self._fz is not None else 0
+        abi.check(L.mcaq_morph_finalize(self._mo, n, self._fz, nf, sh), "mcaq_morph_finalize")
+        if self._fz is not None and process_group is not None:
+            sync_channel_minmax(self.bufs, process_group)
         if self._qs is not None:
             abi.check(L.mcaq_quant(self._qs, n, sh), "mcaq_quant")
         return self.bufs

@@ -209,3 +209,21 @@ def test_bench_config_properties(dev, blobs):
         ref = O.hook_forward(x2, W, 8, xmin=b["xmin"].cpu().numpy(), xmax=b["xmax"].cpu().numpy())
         assert np.array_equal(b["bits"][:2].cpu().numpy(), ref["bits"])
         assert np.array_equal(b["y"][:2].cpu().numpy(), ref["y"])
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 80, 80), (2, 128, 40, 40), (2, 256, 20, 20), (1, 200, 20, 20),
+                                   (1, 576, 20, 20), (1, 1100, 12, 12), (2, 130, 18, 22), (1, 67, 9, 13)])
+def test_stats_pass_orders(dev, blobs, shape):
+    """Pass 1 across its code paths: 4/2/1 pixels per lane, several channel
+    rounds, partial cascade blocks, leftover rows of the row_sum tail order,
+    the cooperative tail and the per-pixel tail (C > 1024): gray, |x| mean and
+    channel min/max bit-exact vs the oracle."""
+    rng = np.random.default_rng(shape[1] * 7 + shape[2])
+    x = (rng.standard_normal(shape) * 2.0).astype(f32)
+    grid = 8 if shape[2] >= 32 else 4
+    out = run_plan(dev, blobs, [x], grid, "linear")[0]
+    _, I = O.phi_tiles(x, grid, internals=True)
+    assert np.array_equal(out["gray"], I["gray_raw"]), "gray"
+    assert np.array_equal(out["absmean"], O.abs_channel_mean(x)), "absmean"
+    assert np.array_equal(out["xmin"], x.min(axis=(0, 2, 3))), "min"
+    assert np.array_equal(out["xmax"], x.max(axis=(0, 2, 3))), "max"

@@ -12,3 +12,4 @@ cat gpurun_out/bench.json
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 50 --warmup 5 --no-cpu > $GRAFT_REPO_ROOT/gpurun_out/prof.log 2>&1 || { tail -20 $GRAFT_REPO_ROOT/gpurun_out/prof.log; exit 1; }
 find $GRAFT_REPO_ROOT/gpurun_out/prof -name "*stats*" | head
 cd $GRAFT_REPO_ROOT && timeout -k 10 120 python tools/prof_stages.py 2 > gpurun_out/stages.log 2>&1; cat gpurun_out/stages.log
+cd $GRAFT_REPO_ROOT && timeout -k 10 120 python tools/prof_morph_stamps.py 2 > gpurun_out/stamps.log 2>&1; cat gpurun_out/stamps.log

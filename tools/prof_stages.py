@@ -55,6 +55,7 @@ def main():
         s.flags = f
     for i in range(n):   # per scale
         res["morph all scale%d" % i] = timeit(lambda: L.mcaq_morph(ctypes.byref(plan._mo[i]), 1, sh()))
+    res["morph_finalize all"] = timeit(lambda: L.mcaq_morph_finalize(plan._mo, n, plan._fz, n, sh()))
     res["quant"] = timeit(lambda: L.mcaq_quant(plan._qs, n, sh()))
     for k, v in res.items():
         print("%-24s %9.1f us" % (k, v))
