@@ -1,0 +1,538 @@
+"""Drop-in mirror of the reference's hot-path modules, running on the gfx950 kernels.
+
+Same class names, constructor arguments, forward signatures, parameter /
+buffer names (state_dict keys) and error behaviour as the reference:
+
+    MorphologicalComplexityAnalyzer   mcaq_yolo/core/morphology.py:17-973
+    ComplexityToBitMappingNetwork     mcaq_yolo/core/bit_allocation.py:83-303
+    LinearBitMapper                   mcaq_yolo/core/bit_allocation.py:12-80
+    LearnedSoftMask                   mcaq_yolo/core/quantization.py:168-239
+    SpatialAdaptiveQuantization       mcaq_yolo/core/quantization.py:242-754
+
+so a reference checkpoint loads unchanged (`load_state_dict`).  Every forward
+runs through libmcaq_hip.so (include/mcaq_hip.h); there is no CPU path - a
+non-CUDA tensor or a missing library raises.  The numeric contract is the
+reference's pure-PyTorch path (bit-exact decisions, tests/test_core_gpu.py).
+
+Scope: the inference path (eval mode).  The training-only branches - the
+fractional-bit STE quantizer, batch-statistics BatchNorm in the mapper,
+autograd through the complexity MLP - are the next row of SURVEY.md 8(f) and
+raise NotImplementedError here instead of silently computing something else.
+"""
+import ctypes
+from typing import Optional
+
+import torch
+import torch.nn as nn
+
+from . import abi
+from .engine import tile_size
+
+_CM_SIZE, _MM_SIZE, _SM_SIZE = 2881, 4865, 170
+
+
+# ---------------------------------------------------------------------------
+# helpers
+# ---------------------------------------------------------------------------
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _need_cuda(t, what):
+    if not torch.is_tensor(t):
+        raise TypeError("%s must be a torch.Tensor, got %s" % (what, type(t)))
+    if not t.is_cuda:
+        raise RuntimeError("mcaq_yolo_amd runs on MI355X (HIP) only: %s is on %s" % (what, t.device))
+
+
+def _f32c(t):
+    return t.detach().float().contiguous()
+
+
+_MFMA_IDX = {}
+
+
+def _mfma_a_operands(w):
+    """Device version of params.mfma_a_operands: (N_out, K) weight -> A operands
+    of v_mfma_f32_32x32x2_f32 ([block][step][lane], lane l holds
+    W[32*block + (l & 31)][2*step + (l >> 5)], K zero-padded to even)."""
+    n, k = w.shape
+    kp = k + (k & 1)
+    nb = (n + 31) // 32
+    key = (n, k, w.device)
+    idx = _MFMA_IDX.get(key)
+    if idx is None:
+        b = torch.arange(nb).view(nb, 1, 1)
+        s = torch.arange(kp // 2).view(1, kp // 2, 1)
+        lane = torch.arange(64).view(1, 1, 64)
+        idx = ((32 * b + (lane & 31)) * kp + 2 * s + (lane >> 5)).reshape(-1).to(w.device)
+        _MFMA_IDX[key] = idx
+    wp = torch.zeros(nb * 32, kp, device=w.device, dtype=torch.float32)
+    wp[:n, :k] = w
+    return wp.reshape(-1)[idx]
+
+
+class _BlobCache:
+    """Packs module parameters into the flat blob a kernel reads, on the device,
+    and re-packs only when a parameter changed (tensor version counters)."""
+
+    def __init__(self):
+        self.key = None
+        self.blob = None
+
+    def get(self, tensors, pack):
+        key = tuple((t.data_ptr(), t._version, t.device) for t in tensors)
+        if key != self.key:
+            with torch.no_grad():
+                self.blob = pack().contiguous()
+            self.key = key
+        return self.blob
+
+
+def _pack_cmlp(seq):
+    l0, ln1, l3, ln4, l6 = seq[0], seq[1], seq[3], seq[4], seq[6]
+    parts = [l0.weight, l0.bias, ln1.weight, ln1.bias, l3.weight, l3.bias, ln4.weight, ln4.bias,
+             l6.weight, l6.bias]
+    flat = torch.cat([p.detach().float().reshape(-1) for p in parts])
+    if flat.numel() != _CM_SIZE:
+        raise ValueError("complexity MLP must be the reference Linear(8,64)-LN-ReLU-Linear(64,32)-LN-ReLU-"
+                         "Linear(32,1) stack")
+    return torch.cat([flat, _mfma_a_operands(l0.weight.detach().float()),
+                      _mfma_a_operands(l3.weight.detach().float())])
+
+
+def _pack_mapper(seq):
+    parts = []
+    for li, bi in ((0, 1), (3, 4), (6, 7)):
+        lin, bn = seq[li], seq[bi]
+        parts += [lin.weight, lin.bias, bn.weight, bn.bias, bn.running_mean, bn.running_var]
+    parts += [seq[9].weight, seq[9].bias]
+    flat = torch.cat([p.detach().float().reshape(-1) for p in parts])
+    if flat.numel() != _MM_SIZE:
+        raise ValueError("bit mapper must use hidden_dims [32, 64, 32]")
+    return torch.cat([flat] + [_mfma_a_operands(seq[i].weight.detach().float()) for i in (0, 3, 6)])
+
+
+def _pack_softmask(seq):
+    parts = [seq[0].weight, seq[0].bias, seq[2].weight, seq[2].bias]
+    flat = torch.cat([p.detach().float().reshape(-1) for p in parts])
+    if flat.numel() != _SM_SIZE:
+        raise ValueError("soft mask must be the reference Conv2d(2,8,3)/Conv2d(8,2,1) net")
+    return flat
+
+
+def _morph_struct(B, H, W, tile, ht, wt, flags, **ptrs):
+    s = abi.MorphScale()
+    for k, v in ptrs.items():
+        setattr(s, k, _p(v))
+    s.B, s.H, s.W = B, H, W
+    s.Hc, s.Wc, s.tile, s.ht, s.wt = ht * tile, wt * tile, tile, ht, wt
+    s.batch_offset, s.batch_total = 0, B
+    s.flags = flags
+    s.hyst_iters = 8
+    s.temperature, s.min_bits, s.max_bits = 1.0, 2.0, 8.0
+    return s
+
+
+def _run_stats(x, gray=None, absmean=None, pmin=None, pmax=None, Hc=None, Wc=None):
+    B, C, H, W = x.shape
+    s = abi.StatsScale()
+    s.x, s.gray, s.absmean, s.pmin, s.pmax = _p(x), _p(gray), _p(absmean), _p(pmin), _p(pmax)
+    s.B, s.C, s.H, s.W = B, C, H, W
+    s.Hc, s.Wc = (H if Hc is None else Hc), (W if Wc is None else Wc)
+    abi.check(abi.lib().mcaq_stats(ctypes.byref(s), 1, _stream()), "mcaq_stats")
+
+
+def _channel_minmax(x, absmean=None):
+    """Per-channel min/max over (batch, H, W) (quantization.py:650-654) by pass 1
+    + the finalize reduction; optionally the |x| channel mean in the same read."""
+    B, C, H, W = x.shape
+    L = abi.lib()
+    units = L.mcaq_stats_units(B, C, H, W)
+    pmin = torch.empty(units, C, device=x.device)
+    pmax = torch.empty(units, C, device=x.device)
+    _run_stats(x, absmean=absmean, pmin=pmin, pmax=pmax)
+    xmin = torch.empty(C, device=x.device)
+    xmax = torch.empty(C, device=x.device)
+    f = abi.FinalizeScale()
+    f.pmin, f.pmax, f.min_out, f.max_out = _p(pmin), _p(pmax), _p(xmin), _p(xmax)
+    f.C, f.nunits, f.min_stride = C, units, 1
+    abi.check(L.mcaq_finalize(ctypes.byref(f), 1, _stream()), "mcaq_finalize")
+    return xmin, xmax
+
+
+# ---------------------------------------------------------------------------
+# morphology.py
+# ---------------------------------------------------------------------------
+class MorphologicalComplexityAnalyzer(nn.Module):
+    """morphology.py:17-973, tensor ("gpu") metric backend.
+
+    forward(features) -> complexity map (B, ht, wt) in [0, 1]:
+    channel mean -> phi1..phi5 per tile -> complexity MLP -> bilateral -> clamp
+    (morphology.py:939-973), computed by mcaq_stats + mcaq_morph."""
+
+    def __init__(self, grid_size: int = 8, device: str = "cuda", metric_backend: str = "gpu",
+                 canny_impl: str = "cv2compat", binarize_impl: str = "adaptive",
+                 contour_components: bool = True):
+        super().__init__()
+        if metric_backend != "gpu":
+            raise NotImplementedError("metric_backend=%r: only the tensor ('gpu') backend is on the MI355X path "
+                                      "(the cv2 backend is offline CPU scoring, out of scope)" % metric_backend)
+        if canny_impl != "cv2compat":
+            raise NotImplementedError("canny_impl=%r not implemented (SURVEY.md 8(f) rank 4)" % canny_impl)
+        if binarize_impl not in ("adaptive", "otsu"):
+            raise ValueError("binarize_impl must be 'adaptive' or 'otsu'")
+        self.grid_size = grid_size
+        self.device = device
+        self.metric_backend = metric_backend
+        self.canny_impl = canny_impl
+        self.binarize_impl = binarize_impl
+        self.contour_components = contour_components
+        self.complexity_mlp = nn.Sequential(
+            nn.Linear(8, 64), nn.LayerNorm(64), nn.ReLU(inplace=True),
+            nn.Linear(64, 32), nn.LayerNorm(32), nn.ReLU(inplace=True),
+            nn.Linear(32, 1), nn.Sigmoid(),
+        )
+        nn.init.xavier_uniform_(self.complexity_mlp[-2].weight, gain=3.0)
+        nn.init.zeros_(self.complexity_mlp[-2].bias)
+        self.register_buffer("feature_weights", torch.ones(5) / 5)
+        self._blob = _BlobCache()
+        if str(device).startswith("cuda") and torch.cuda.is_available():
+            self.to(device)
+
+    def _tile_size(self, H: int) -> int:
+        """morphology.py:359-376: largest power of two <= max(4, H // grid_size)."""
+        return tile_size(H, self.grid_size)
+
+    def _flags(self):
+        f = 0
+        if self.binarize_impl == "otsu":
+            f |= abi.F_BIN_OTSU
+        if not self.contour_components:
+            f |= abi.F_NO_EULER
+        return f
+
+    def cmlp_blob(self):
+        ps = [p for p in self.complexity_mlp.parameters()]
+        return self._blob.get(ps, lambda: _pack_cmlp(self.complexity_mlp))
+
+    def _run(self, features, want_c):
+        _need_cuda(features, "features")
+        if features.dim() != 4:
+            raise ValueError("features must be (B, C, H, W)")
+        x = features.float().contiguous()
+        B, C, H, W = x.shape
+        T = tile_size(H, self.grid_size)
+        ht, wt = H // T, W // T
+        if ht < 1 or wt < 1 or T > 64:
+            raise ValueError("feature map %dx%d: tile %d unsupported" % (H, W, T))
+        dev = x.device
+        gray = torch.empty(B, ht * T, wt * T, device=dev)
+        _run_stats(x, gray=gray, Hc=ht * T, Wc=wt * T)
+        phi = torch.empty(B, ht, wt, 8, device=dev)
+        flags = abi.F_PHI | self._flags()
+        ptrs = dict(gray=gray, phi_out=phi)
+        L = abi.lib()
+        if want_c:
+            flags |= abi.F_CMLP
+            ptrs["cmlp"] = self.cmlp_blob()
+            ptrs["c_out"] = torch.empty(B, ht, wt, device=dev)
+        scratch = L.mcaq_morph_scratch_bytes(B, ht * T, wt * T, ht, wt)
+        if scratch:
+            ptrs["gscratch"] = torch.empty(scratch, device=dev, dtype=torch.uint8)
+        s = _morph_struct(B, H, W, T, ht, wt, flags, **ptrs)
+        abi.check(L.mcaq_morph(ctypes.byref(s), 1, _stream()), "mcaq_morph")
+        return phi, ptrs.get("c_out")
+
+    @staticmethod
+    def _detailed(phi):
+        return {"fractal": phi[..., 0], "texture": phi[..., 1], "gradient": phi[..., 2],
+                "edge": phi[..., 3], "contour": phi[..., 4]}
+
+    def compute_phi_tiles(self, features: torch.Tensor):
+        """morphology.py:798-824: (phi (B,ht,wt,8), detailed dict of phi1..phi5)."""
+        phi, _ = self._run(features, want_c=False)
+        return phi, self._detailed(phi)
+
+    def forward(self, features: torch.Tensor, return_detailed: bool = False):
+        if self.training and torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            raise NotImplementedError("training-mode analyzer (autograd through the complexity MLP) is the QAT "
+                                      "path, SURVEY.md 8(f) rank 2; call .eval() or use torch.no_grad()")
+        phi, c = self._run(features, want_c=True)
+        if return_detailed:
+            return c, self._detailed(phi)
+        return c
+
+
+# ---------------------------------------------------------------------------
+# bit_allocation.py
+# ---------------------------------------------------------------------------
+def _normalize_complexity_shape(complexity):
+    """bit_allocation.py:145-172."""
+    if not isinstance(complexity, torch.Tensor):
+        raise TypeError(f"complexity must be torch.Tensor, got {type(complexity)}")
+    if complexity.dim() == 2:
+        complexity = complexity.unsqueeze(0)
+    elif complexity.dim() == 3:
+        pass
+    elif complexity.dim() == 4:
+        complexity = complexity.mean(dim=1)
+    else:
+        raise ValueError(f"Unsupported complexity dim={complexity.dim()}, expected 2, 3, or 4.")
+    return complexity
+
+
+def _run_mapper(c, flags, min_bits, max_bits, temperature, return_continuous, mapper_blob=None):
+    _need_cuda(c, "complexity")
+    c = _f32c(c)
+    B, ht, wt = c.shape
+    f = flags | abi.F_MAPPER
+    if temperature is not None:
+        f |= abi.F_HAS_T
+    if return_continuous:
+        f |= abi.F_CONT
+    bits = torch.empty(B, ht, wt, device=c.device)
+    s = _morph_struct(B, 4 * ht, 4 * wt, 4, ht, wt, f, c_in=c, bits_out=bits, mapper=mapper_blob)
+    s.temperature = max(float(temperature if temperature is not None else 1.0), 0.1)
+    s.min_bits, s.max_bits = float(min_bits), float(max_bits)
+    abi.check(abi.lib().mcaq_morph(ctypes.byref(s), 1, _stream()), "mcaq_morph(mapper)")
+    return bits
+
+
+class LinearBitMapper(nn.Module):
+    """bit_allocation.py:12-80: per-image 2-98 % percentile normalisation ->
+    b = b_min + (b_max - b_min) * C_n, x temperature, clamp, round."""
+
+    def __init__(self, min_bits: int = 2, max_bits: int = 8, eps_spread: float = 1e-3):
+        super().__init__()
+        self.min_bits = float(min_bits)
+        self.max_bits = float(max_bits)
+        if float(eps_spread) != 1e-3:
+            raise NotImplementedError("eps_spread other than the reference default 1e-3")
+        self.eps_spread = float(eps_spread)
+
+    def enforce_weight_constraints(self):
+        """No-op (parameter-free), as in the reference."""
+
+    def forward(self, complexity: torch.Tensor, temperature: Optional[float] = None,
+                return_continuous: bool = False) -> torch.Tensor:
+        c = _normalize_complexity_shape(complexity)
+        return _run_mapper(c, abi.F_MAP_LINEAR, self.min_bits, self.max_bits, temperature, return_continuous)
+
+
+class ComplexityToBitMappingNetwork(nn.Module):
+    """bit_allocation.py:83-303: z=[C, C^2, log1p C] -> 3 x (Linear, BN, ReLU)
+    -> Linear -> sigmoid -> [b_min, b_max] -> x temperature -> STE clamp / round.
+    Eval mode (BatchNorm running statistics)."""
+
+    def __init__(self, min_bits: int = 2, max_bits: int = 8, hidden_dims: list = [32, 64, 32],
+                 enforce_monotonicity: bool = True):
+        super().__init__()
+        if list(hidden_dims) != [32, 64, 32]:
+            raise NotImplementedError("hidden_dims other than the reference [32, 64, 32]")
+        self.min_bits = float(min_bits)
+        self.max_bits = float(max_bits)
+        self.enforce_monotonicity = enforce_monotonicity
+        layers = []
+        d = 3
+        for h in hidden_dims:
+            layers += [nn.Linear(d, h), nn.BatchNorm1d(h), nn.ReLU(inplace=True)]
+            d = h
+        layers += [nn.Linear(d, 1), nn.Sigmoid()]
+        self.mapping_network = nn.Sequential(*layers)
+        self.apply(self._init_weights)
+        self._blob = _BlobCache()
+
+    _normalize_complexity_shape = staticmethod(_normalize_complexity_shape)
+
+    def _init_weights(self, m):
+        if isinstance(m, nn.Linear):
+            nn.init.xavier_uniform_(m.weight, gain=0.5)
+            if self.enforce_monotonicity:
+                m.weight.data = torch.abs(m.weight.data)
+            if m.bias is not None:
+                nn.init.constant_(m.bias, 0.1)
+
+    def enforce_weight_constraints(self):
+        """Eq.18: |W| for Linear layers and BatchNorm gammas (bit_allocation.py:186-197)."""
+        if self.enforce_monotonicity:
+            for module in self.mapping_network.modules():
+                if isinstance(module, (nn.Linear, nn.BatchNorm1d)):
+                    module.weight.data = torch.abs(module.weight.data)
+
+    def mapper_blob(self):
+        net = self.mapping_network
+        ts = list(net.parameters()) + [net[i].running_mean for i in (1, 4, 7)] + \
+            [net[i].running_var for i in (1, 4, 7)]
+        return self._blob.get(ts, lambda: _pack_mapper(net))
+
+    def forward(self, complexity: torch.Tensor, temperature: Optional[float] = None,
+                return_continuous: bool = False) -> torch.Tensor:
+        if self.training:
+            raise NotImplementedError("training-mode mapper (batch-statistics BatchNorm, STE backward) is the QAT "
+                                      "path, SURVEY.md 8(f) rank 2; call .eval()")
+        c = _normalize_complexity_shape(complexity)
+        return _run_mapper(c, 0, self.min_bits, self.max_bits, temperature, return_continuous,
+                           mapper_blob=self.mapper_blob())
+
+
+# ---------------------------------------------------------------------------
+# quantization.py
+# ---------------------------------------------------------------------------
+class LearnedSoftMask(nn.Module):
+    """quantization.py:168-239: per-tile [bits_norm, |x| activation] -> conv3x3
+    -> ReLU -> conv1x1 -> softmax[0] -> nearest upsample -> 5x5 Gaussian
+    (replicate pad).  Returns m (B, 1, H, W)."""
+
+    def __init__(self, hidden: int = 8, kernel_size: int = 5):
+        super().__init__()
+        if hidden != 8 or kernel_size != 5:
+            raise NotImplementedError("soft mask hidden=8, kernel_size=5 only (reference defaults)")
+        self.net = nn.Sequential(nn.Conv2d(2, hidden, 3, padding=1), nn.ReLU(inplace=True),
+                                 nn.Conv2d(hidden, 2, 1))
+        nn.init.normal_(self.net[-1].weight, std=1e-3)
+        with torch.no_grad():
+            self.net[-1].bias.copy_(torch.tensor([4.0, 0.0]))
+        k = kernel_size
+        sigma = k / 3.0
+        xs = torch.arange(k, dtype=torch.float32) - k // 2
+        g1 = torch.exp(-xs ** 2 / (2 * sigma ** 2))
+        g1 = g1 / g1.sum()
+        self.register_buffer("smooth_kernel", (g1.unsqueeze(0) * g1.unsqueeze(1)).unsqueeze(0).unsqueeze(0))
+        self.kernel_size = k
+        self._blob = _BlobCache()
+
+    def blob(self):
+        return self._blob.get(list(self.net.parameters()), lambda: _pack_softmask(self.net))
+
+    def forward(self, bit_map: torch.Tensor, x: torch.Tensor, absmean: Optional[torch.Tensor] = None):
+        _need_cuda(bit_map, "bit_map")
+        _need_cuda(x, "x")
+        B, C, H, W = x.shape
+        bits = _f32c(bit_map)
+        _, ht, wt = bits.shape
+        if absmean is None:
+            absmean = torch.empty(B, H, W, device=x.device)
+            _run_stats(_f32c(x), absmean=absmean)
+        if 4 * ht > H or 4 * wt > W:
+            # the launcher's geometry check wants >= 4 pixels per tile (every
+            # hook tile grid has them: tile = pow2floor(max(4, H // grid)))
+            raise NotImplementedError("soft mask on a tile grid finer than 4 pixels per tile")
+        m = torch.empty(B, 1, H, W, device=x.device)
+        # tile / crop fields only satisfy the launcher: the soft-mask stage
+        # pools and upsamples over (H, W) like adaptive_avg_pool2d / nearest
+        s = _morph_struct(B, H, W, 4, ht, wt, abi.F_SOFTMASK, absmean=absmean, bits_in=bits,
+                          smask=self.blob(), m_out=m)
+        abi.check(abi.lib().mcaq_morph(ctypes.byref(s), 1, _stream()), "mcaq_morph(soft mask)")
+        return m
+
+
+class SpatialAdaptiveQuantization(nn.Module):
+    """quantization.py:242-754, inference: per-channel (batch, H, W) min/max (or
+    frozen calibration stats) -> per-tile 2..8-bit quant/dequant x m(p).
+    One read of x for min/max + |x| mean, one read + one write for y."""
+
+    def __init__(self, calibration_mode: str = "minmax", smooth_transitions: bool = True,
+                 per_channel: bool = True, learned_rounding: bool = False, momentum: float = 0.99):
+        super().__init__()
+        if calibration_mode != "minmax":
+            raise NotImplementedError("calibration_mode=%r: the hooks use 'minmax' "
+                                      "(models/mcaq_yolo.py:466-470)" % calibration_mode)
+        if learned_rounding:
+            raise NotImplementedError("learned_rounding is never enabled by the reference hooks")
+        self.calibration_mode = calibration_mode
+        self.smooth_transitions = smooth_transitions
+        self.per_channel = per_channel
+        self.momentum = momentum
+        self.register_buffer("running_min", None)
+        self.register_buffer("running_max", None)
+        self.register_buffer("num_batches_tracked", torch.tensor(0))
+        self.register_buffer("stats_frozen", torch.tensor(False))
+        self.learned_rounding = None
+        self.soft_mask = LearnedSoftMask() if smooth_transitions else None
+        self.register_buffer("calibration_histogram", None)
+        self.histogram_bins = 2048
+
+    def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys,
+                              unexpected_keys, error_msgs):
+        """quantization.py:297-312: materialise the lazy running_min/max buffers."""
+        for name in ("running_min", "running_max"):
+            key = prefix + name
+            if key in state_dict and getattr(self, name) is None:
+                setattr(self, name, torch.zeros_like(state_dict[key]))
+        super()._load_from_state_dict(state_dict, prefix, local_metadata, strict, missing_keys,
+                                      unexpected_keys, error_msgs)
+
+    def freeze_calibration(self):
+        self.stats_frozen = torch.tensor(True, device=self.stats_frozen.device)
+
+    def batch_minmax(self, x, absmean=None):
+        """Per-channel (or per-tensor) min/max of the batch, expanded to C entries."""
+        xmin, xmax = _channel_minmax(x, absmean)
+        if not self.per_channel:
+            xmin = xmin.amin().expand(x.shape[1]).contiguous()
+            xmax = xmax.amax().expand(x.shape[1]).contiguous()
+        return xmin, xmax
+
+    @torch.no_grad()
+    def update_running_stats(self, x: torch.Tensor):
+        """quantization.py:319-353: EMA(momentum) of the batch min/max."""
+        if bool(self.stats_frozen):
+            return
+        _need_cuda(x, "x")
+        xf = _f32c(x)
+        xmin, xmax = _channel_minmax(xf)
+        C = x.shape[1]
+        if self.per_channel:
+            shape = (1, C) + (1,) * (x.dim() - 2)
+            nmin, nmax = xmin.view(shape), xmax.view(shape)
+        else:
+            nmin, nmax = xmin.amin(), xmax.amax()
+        if self.running_min is None:
+            self.running_min, self.running_max = nmin.clone(), nmax.clone()
+        else:
+            self.running_min = self.momentum * self.running_min + (1 - self.momentum) * nmin
+            self.running_max = self.momentum * self.running_max + (1 - self.momentum) * nmax
+        self.num_batches_tracked += 1
+
+    def forward(self, x: torch.Tensor, bit_map: torch.Tensor, training: Optional[bool] = None) -> torch.Tensor:
+        if training is None:
+            training = self.training
+        if training:
+            raise NotImplementedError("training-mode quantizer (fractional bits + STE) is the QAT path, "
+                                      "SURVEY.md 8(f) rank 2; use update_running_stats() to calibrate")
+        _need_cuda(x, "x")
+        _need_cuda(bit_map, "bit_map")
+        xf = _f32c(x)
+        B, C, H, W = xf.shape
+        if bit_map.dim() != 3 or bit_map.shape[0] != B:
+            raise AssertionError(f"Batch size mismatch: {B} vs {bit_map.shape[0]}")
+        bits = _f32c(bit_map)
+        _, ht, wt = bits.shape
+        want_m = self.smooth_transitions and self.soft_mask is not None
+        absmean = torch.empty(B, H, W, device=xf.device) if want_m else None
+        if bool(self.stats_frozen) and self.running_min is not None:
+            xmin = self.running_min.reshape(-1).float().expand(C).contiguous() \
+                if self.running_min.numel() == 1 else self.running_min.reshape(-1).float().contiguous()
+            xmax = self.running_max.reshape(-1).float().expand(C).contiguous() \
+                if self.running_max.numel() == 1 else self.running_max.reshape(-1).float().contiguous()
+            if want_m:
+                _run_stats(xf, absmean=absmean)
+        else:
+            xmin, xmax = self.batch_minmax(xf, absmean)
+        m = self.soft_mask(bits, xf, absmean=absmean) if want_m else None
+        y = torch.empty_like(xf)
+        q = abi.QuantScale()
+        q.x, q.y, q.bits, q.m, q.xmin, q.xmax = _p(xf), _p(y), _p(bits), _p(m), _p(xmin), _p(xmax)
+        q.B, q.C, q.H, q.W, q.ht, q.wt = B, C, H, W, ht, wt
+        q.bits_lo, q.nbits = 2, 7
+        abi.check(abi.lib().mcaq_quant(ctypes.byref(q), 1, _stream()), "mcaq_quant")
+        return y
+
+    def extra_repr(self) -> str:
+        return (f"calibration_mode={self.calibration_mode}, smooth_transitions={self.smooth_transitions}, "
+                f"per_channel={self.per_channel}")

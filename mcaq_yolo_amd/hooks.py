@@ -1,0 +1,143 @@
+"""The MCAQ forward hook (models/mcaq_yolo.py:402-473) on the fused HIP path.
+
+`MCAQHooks` owns the hot-path modules under the reference's attribute names
+(`complexity_analyzer`, `bit_mapper`, `quantizers[str(idx)]`), so a reference
+MCAQYOLO state_dict restricted to those prefixes loads into it, and speaks
+the reference's hook protocol: the shared `_mcaq_state` dict with keys
+`active`, `temperature`, `quantize`, `calibrating`, `aux`; each hook appends
+`{layer, complexity, bit_map, features_q}` to `aux` and returns the quantized
+map (replacing the layer output) or None.
+
+Inference calls go through one `HookPlan` per feature shape: 3 launches
+(pass 1, morphology + channel min/max, pass 2) instead of the reference's
+analyzer -> mapper -> soft mask -> quantizer chain.  Calibration
+(`calibrating=True`) first folds the batch min/max into the quantizer's EMA
+statistics (quantization.py:319-353), then quantizes like inference.
+"""
+import torch
+import torch.nn as nn
+
+from .core import (ComplexityToBitMappingNetwork, LinearBitMapper, MorphologicalComplexityAnalyzer,
+                   SpatialAdaptiveQuantization)
+from .engine import HookPlan, ScaleGeom
+
+DEFAULT_INDICES = (4, 6, 9)   # models/mcaq_yolo.py:361 fallback (C3/C4/C5 of YOLOv8)
+
+
+class MCAQHooks(nn.Module):
+    def __init__(self, grid_size=8, min_bits=2, max_bits=8, bit_mapping="mlp", normalize_complexity=False,
+                 device="cuda", indices=DEFAULT_INDICES):
+        super().__init__()
+        self.complexity_analyzer = MorphologicalComplexityAnalyzer(grid_size=grid_size, device=device)
+        if bit_mapping == "mlp":
+            self.bit_mapper = ComplexityToBitMappingNetwork(min_bits=min_bits, max_bits=max_bits)
+        elif bit_mapping == "linear":
+            self.bit_mapper = LinearBitMapper(min_bits=min_bits, max_bits=max_bits)
+        else:
+            raise ValueError("bit_mapping must be 'mlp' or 'linear'")
+        self.bit_mapping = bit_mapping
+        self.normalize_complexity = normalize_complexity
+        self.quantizers = nn.ModuleDict()
+        self.backbone_out_indices = list(indices)
+        for idx in self.backbone_out_indices:
+            self.quantizers[str(idx)] = SpatialAdaptiveQuantization(calibration_mode="minmax",
+                                                                    smooth_transitions=True, per_channel=True)
+        self._mcaq_state = {"active": False}
+        self._handles = []
+        self._plans = {}
+        if str(device).startswith("cuda") and torch.cuda.is_available():
+            self.to(device)
+
+    # -- registration (models/mcaq_yolo.py:459-473)
+    def register(self, layers):
+        """Attach one forward hook per backbone index to `layers` (a list /
+        nn.Sequential of the detector's modules)."""
+        layers = list(layers)
+        for idx in self.backbone_out_indices:
+            if 0 <= idx < len(layers):
+                self._handles.append(layers[idx].register_forward_hook(self.make_hook(idx)))
+        return self
+
+    def remove(self):
+        for h in self._handles:
+            h.remove()
+        self._handles = []
+
+    def begin(self, temperature=1.0, quantize=True, calibrating=False):
+        """Open a forward (models/mcaq_yolo.py:556-561); returns the aux list."""
+        self._mcaq_state = {"active": True, "temperature": temperature, "quantize": quantize,
+                            "calibrating": calibrating, "aux": []}
+        return self._mcaq_state["aux"]
+
+    def end(self):
+        aux = self._mcaq_state.get("aux", [])
+        self._mcaq_state = {"active": False}
+        return aux
+
+    @staticmethod
+    def avg_bits(aux):
+        """models/mcaq_yolo.py:572-577: mean over scales of each bit map's mean."""
+        if not aux:
+            return None
+        return torch.stack([a["bit_map"].float().mean() for a in aux]).mean()
+
+    # -- the hook body (models/mcaq_yolo.py:409-455)
+    def make_hook(self, layer_idx):
+        def hook(module, inputs, output):
+            state = self._mcaq_state
+            if not state.get("active", False):
+                return None
+            if not torch.is_tensor(output) or output.dim() != 4:
+                return None
+            return self.run_scale(layer_idx, output, state)
+        return hook
+
+    def _plan(self, feat):
+        key = (tuple(feat.shape), feat.device, self.complexity_analyzer.grid_size)
+        plan = self._plans.get(key)
+        if plan is None:
+            plan = HookPlan([ScaleGeom(*feat.shape, self.complexity_analyzer.grid_size)], feat.device)
+            self._plans[key] = plan
+        return plan
+
+    def run_scale(self, layer_idx, feat, state):
+        if self.training:
+            raise NotImplementedError("training-mode hooks (continuous bits, STE quantizer) are the QAT path, "
+                                      "SURVEY.md 8(f) rank 2; call .eval()")
+        quantize = state.get("quantize", True)
+        quantizer = self.quantizers[str(layer_idx)]
+        x = feat.float().contiguous()
+        if state.get("calibrating", False) and quantize:
+            quantizer.update_running_stats(x)
+        plan = self._plan(x)
+        b = plan.bufs[0]
+        for k in ("y", "complexity", "bits"):      # fresh outputs: the caller keeps them
+            b[k] = torch.empty_like(b[k])
+        minmax = None
+        if bool(quantizer.stats_frozen) and quantizer.running_min is not None:
+            minmax = [(quantizer.running_min.reshape(-1), quantizer.running_max.reshape(-1))]
+        elif not quantizer.per_channel:
+            raise NotImplementedError("per-tensor statistics on the fused hook path")
+        an = self.complexity_analyzer
+        sm = quantizer.soft_mask.blob() if (quantizer.smooth_transitions and quantizer.soft_mask is not None) \
+            else None
+        mapper_blob = self.bit_mapper.mapper_blob() if self.bit_mapping == "mlp" else None
+        plan.run([x], an.cmlp_blob(), mapper_blob, [sm], temperature=state.get("temperature", 1.0),
+                 mapper_kind=self.bit_mapping, normalize=self.normalize_complexity, minmax=minmax,
+                 binarize_otsu=an.binarize_impl == "otsu", contour_components=an.contour_components,
+                 min_bits=self.bit_mapper.min_bits, max_bits=self.bit_mapper.max_bits, quantize=quantize)
+        feat_q = b["y"] if quantize else feat
+        state.setdefault("aux", []).append({"layer": layer_idx, "complexity": b["complexity"],
+                                            "bit_map": b["bits"], "features_q": feat_q})
+        return feat_q if quantize else None
+
+    def forward_features(self, feats, temperature=1.0, quantize=True):
+        """Run the hook body directly on a list of (C3, C4, C5) feature maps
+        (one per backbone index); returns (quantized maps, aux)."""
+        aux = self.begin(temperature=temperature, quantize=quantize)
+        outs = []
+        for idx, f in zip(self.backbone_out_indices, feats):
+            y = self.run_scale(idx, f, self._mcaq_state)
+            outs.append(f if y is None else y)
+        self.end()
+        return outs, aux

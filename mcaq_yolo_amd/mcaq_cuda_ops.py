@@ -1,0 +1,73 @@
+"""Drop-in for the reference's Torch extension `mcaq_cuda_ops`
+(mcaq_yolo/ops/src/mcaq_ops.cpp:22-77, kernel mcaq_kernel.cu:12-123).
+
+    spatial_quantize(input, bit_map, min_vals, max_vals, tile_h, tile_w, mask=None) -> Tensor
+
+Same signature, argument meaning, output ownership (a new tensor, inputs
+read-only) and errors (RuntimeError when min/max do not hold one entry per
+channel or the mask is not N*H*W); additionally the dtype / device /
+contiguity checks the reference lacks.  Runs
+mcaq_launch_spatial_quantization (include/mcaq_hip.h) on the current stream,
+asynchronously.  One deliberate difference: q is rounded half-to-even
+(torch.round, the reference's PyTorch path) instead of the CUDA kernel's
+roundf, so this op and SpatialAdaptiveQuantization._forward_pytorch agree
+bit-for-bit.
+
+To let the unmodified reference pick it up (`import mcaq_cuda_ops` at
+core/quantization.py:14-23) call `install()` before importing it.
+"""
+import ctypes
+import sys
+
+import torch
+
+from . import abi
+
+
+def _check(t, what):
+    if not torch.is_tensor(t):
+        raise TypeError("%s must be a Tensor" % what)
+    if not t.is_cuda:
+        raise RuntimeError("%s must be a CUDA (HIP) tensor, got %s" % (what, t.device))
+    if t.dtype != torch.float32:
+        raise RuntimeError("%s must be float32, got %s" % (what, t.dtype))
+    if not t.is_contiguous():
+        raise RuntimeError("%s must be contiguous" % what)
+
+
+def spatial_quantize(input, bit_map, min_vals, max_vals, tile_h, tile_w, mask=None):
+    for t, n in ((input, "input"), (bit_map, "bit_map"), (min_vals, "min_vals"), (max_vals, "max_vals")):
+        _check(t, n)
+    if input.dim() != 4:
+        raise RuntimeError("input must be (N, C, H, W)")
+    if bit_map.dim() != 3:
+        raise RuntimeError("bit_map must be (N, Ht, Wt)")
+    N, C, H, W = input.shape
+    if min_vals.numel() != C or max_vals.numel() != C:
+        raise RuntimeError("min_vals/max_vals must have one entry per channel (C=%d), got %d - expand "
+                           "per-tensor stats before calling (see SpatialAdaptiveQuantization._forward_cuda)"
+                           % (C, min_vals.numel()))
+    mptr = None
+    if mask is not None:
+        _check(mask, "mask")
+        if mask.numel() != N * H * W:
+            raise RuntimeError("mask must be (N, 1, H, W)")
+        mptr = ctypes.c_void_p(mask.data_ptr())
+    if bit_map.shape[0] != N:
+        raise RuntimeError("bit_map batch %d != input batch %d" % (bit_map.shape[0], N))
+    out = torch.empty_like(input)
+    if out.numel() == 0:
+        return out
+    n_th, n_tw = int(bit_map.shape[1]), int(bit_map.shape[2])
+    err = abi.lib().mcaq_launch_spatial_quantization(
+        ctypes.c_void_p(input.data_ptr()), ctypes.c_void_p(bit_map.data_ptr()),
+        ctypes.c_void_p(min_vals.data_ptr()), ctypes.c_void_p(max_vals.data_ptr()), mptr,
+        ctypes.c_void_p(out.data_ptr()), N, C, H, W, int(tile_h), int(tile_w), n_th, n_tw,
+        ctypes.c_void_p(torch.cuda.current_stream(input.device).cuda_stream))
+    abi.check(err, "mcaq_launch_spatial_quantization")
+    return out
+
+
+def install():
+    """Register this module as the top-level `mcaq_cuda_ops` extension."""
+    sys.modules["mcaq_cuda_ops"] = sys.modules[__name__]

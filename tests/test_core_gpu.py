@@ -1,0 +1,224 @@
+"""The drop-in module layer on the GPU: the reference's own smoke tests
+(mcaq_yolo/tests/test_smoke.py) restated against mcaq_yolo_amd.core, plus
+bit-exact parity of every module against the oracle / golden fixtures."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_case, load_weights
+from oracle import mcaq_oracle as O
+
+pytestmark = pytest.mark.gpu
+f32 = np.float32
+DEV = "cuda"
+
+
+def _sd(prefix):
+    W = load_weights()
+    return {k[len(prefix):]: torch.from_numpy(np.asarray(v)) for k, v in W.items() if k.startswith(prefix)}
+
+
+@pytest.fixture(scope="module")
+def mods():
+    from mcaq_yolo_amd import core
+    a = core.MorphologicalComplexityAnalyzer(device=DEV)
+    a.load_state_dict(_sd("complexity_analyzer."))
+    m = core.ComplexityToBitMappingNetwork().to(DEV)
+    m.load_state_dict(_sd("bit_mapper."))
+    q = core.SpatialAdaptiveQuantization().to(DEV)
+    q.soft_mask.load_state_dict(_sd("soft_mask."))
+    return a.eval(), m.eval(), q.eval()
+
+
+# ---- test_smoke.py restated -------------------------------------------------
+@pytest.mark.parametrize("H", [640, 80, 40, 20])
+def test_phi_tiles_shapes(H):
+    """test_smoke.py:33-47"""
+    from mcaq_yolo_amd.core import MorphologicalComplexityAnalyzer
+    a = MorphologicalComplexityAnalyzer(device=DEV)
+    x = torch.rand(2, 3, H, H, device=DEV)
+    phi, detailed = a.compute_phi_tiles(x)
+    tile = a._tile_size(H)
+    ht = H // tile
+    assert phi.shape == (2, ht, ht, 8), phi.shape
+    assert set(detailed) == {"fractal", "texture", "gradient", "edge", "contour"}
+    assert tile >= 4 and (tile & (tile - 1)) == 0
+    assert float(phi.min()) >= 0.0 and float(phi.max()) <= 1.0 + 1e-5
+
+
+def test_analyzer_forward_range():
+    """test_smoke.py:50-59 (inference half; the gradient half is the QAT path)"""
+    from mcaq_yolo_amd.core import MorphologicalComplexityAnalyzer
+    a = MorphologicalComplexityAnalyzer(device=DEV).eval()
+    c = a(torch.rand(2, 16, 80, 80, device=DEV))
+    assert c.dim() == 3 and 0.0 <= float(c.min()) and float(c.max()) <= 1.0
+
+
+def test_bit_mapper_range_and_temperature():
+    """test_smoke.py:74-84"""
+    from mcaq_yolo_amd.core import ComplexityToBitMappingNetwork
+    m = ComplexityToBitMappingNetwork(min_bits=2, max_bits=8).to(DEV).eval()
+    c = torch.rand(2, 8, 8, device=DEV)
+    b = m(c, temperature=1.0)
+    assert b.shape == (2, 8, 8)
+    assert float(b.min()) >= 2.0 and float(b.max()) <= 8.0
+    assert torch.allclose(b, torch.round(b))
+    b10 = m(c, temperature=10.0)
+    assert torch.allclose(b10, torch.full_like(b10, 8.0))
+
+
+def test_learned_soft_mask_near_identity_init():
+    """test_smoke.py:115-126 (forward half)"""
+    from mcaq_yolo_amd.core import LearnedSoftMask
+    mask = LearnedSoftMask().to(DEV)
+    x = torch.randn(2, 8, 32, 32, device=DEV)
+    m = mask(torch.full((2, 4, 4), 4.0, device=DEV), x)
+    assert m.shape == (2, 1, 32, 32)
+    assert float(m.min()) > 0.9, float(m.min())
+
+
+def test_calibration_freeze():
+    """test_smoke.py:129-139 via update_running_stats (the EMA of the
+    training-mode forward)."""
+    from mcaq_yolo_amd.core import SpatialAdaptiveQuantization
+    q = SpatialAdaptiveQuantization(smooth_transitions=False).to(DEV)
+    x = torch.randn(2, 4, 16, 16, device=DEV)
+    q.update_running_stats(x)
+    assert q.running_min is not None
+    assert torch.equal(q.running_min.reshape(-1), x.amin(dim=(0, 2, 3)))
+    x2 = torch.randn(2, 4, 16, 16, device=DEV)
+    q.update_running_stats(x2)
+    want = 0.99 * x.amin(dim=(0, 2, 3), keepdim=True) + (1 - 0.99) * x2.amin(dim=(0, 2, 3), keepdim=True)
+    assert torch.equal(q.running_min, want)
+    frozen = q.running_min.clone()
+    q.freeze_calibration()
+    q.update_running_stats(torch.randn(2, 4, 16, 16, device=DEV) * 100)
+    assert torch.allclose(q.running_min, frozen), "stats moved after freeze"
+
+
+def test_linear_bit_mapper_spatial_variance():
+    """test_smoke.py:188-196"""
+    from mcaq_yolo_amd.core import LinearBitMapper
+    m = LinearBitMapper(min_bits=2, max_bits=8)
+    c = (torch.linspace(0, 1, 16).reshape(1, 4, 4) * 0.05 + 0.4).to(DEV)
+    b = m(c, temperature=1.0)
+    assert float(b.min()) == 2.0 and float(b.max()) == 8.0
+    assert torch.unique(b).numel() >= 5
+
+
+def test_linear_bit_mapper_flat_map_absolute_fallback():
+    """test_smoke.py:199-211"""
+    from mcaq_yolo_amd.core import LinearBitMapper
+    m = LinearBitMapper(min_bits=2, max_bits=8)
+    bits = m(torch.full((1, 8, 8), 0.5, device=DEV))
+    assert int(bits.min()) == 5 and int(bits.max()) == 5
+    assert int(m(torch.full((1, 8, 8), 0.0, device=DEV)).max()) == 2
+    assert int(m(torch.full((1, 8, 8), 1.0, device=DEV)).min()) == 8
+
+
+def test_cuda_kernel_parity():
+    """test_smoke.py:226-246: the extension op vs the PyTorch-path semantics
+    (here bit-exact vs the oracle, not atol 1e-4), with and without m."""
+    from mcaq_yolo_amd import mcaq_cuda_ops
+    from mcaq_yolo_amd.core import SpatialAdaptiveQuantization
+    torch.manual_seed(0)
+    W = load_weights()
+    for smooth in (False, True):
+        q = SpatialAdaptiveQuantization(smooth_transitions=smooth).to(DEV).eval()
+        if smooth:
+            q.soft_mask.load_state_dict(_sd("soft_mask."))
+        x = torch.randn(2, 8, 32, 32, device=DEV)
+        bit_map = torch.randint(2, 9, (2, 4, 4), device=DEV).float()
+        y = q(x, bit_map)
+        xn, bn = x.cpu().numpy(), bit_map.cpu().numpy()
+        m = O.soft_mask(bn, xn, W) if smooth else None
+        ref = O.quantize(xn, bn, m)
+        assert np.array_equal(y.cpu().numpy(), ref)
+        # the reference extension contract: same numbers through spatial_quantize
+        mn = x.amin(dim=(0, 2, 3), keepdim=True)
+        mx = x.amax(dim=(0, 2, 3), keepdim=True)
+        mm = q.soft_mask(bit_map, x) if smooth else None
+        y2 = mcaq_cuda_ops.spatial_quantize(x.contiguous(), bit_map, mn, mx, 8, 8, mm)
+        assert torch.equal(y, y2)
+
+
+def test_spatial_quantize_errors():
+    """mcaq_ops.cpp:37-46 checks raise RuntimeError."""
+    from mcaq_yolo_amd import mcaq_cuda_ops
+    x = torch.randn(1, 4, 8, 8, device=DEV)
+    b = torch.full((1, 2, 2), 4.0, device=DEV)
+    with pytest.raises(RuntimeError, match="one entry per channel"):
+        mcaq_cuda_ops.spatial_quantize(x, b, torch.zeros(3, device=DEV), torch.ones(3, device=DEV), 4, 4)
+    with pytest.raises(RuntimeError, match="mask"):
+        mcaq_cuda_ops.spatial_quantize(x, b, torch.zeros(4, device=DEV), torch.ones(4, device=DEV), 4, 4,
+                                       torch.ones(1, 1, 4, 4, device=DEV))
+    with pytest.raises(RuntimeError, match="float32"):
+        mcaq_cuda_ops.spatial_quantize(x.half(), b, torch.zeros(4, device=DEV), torch.ones(4, device=DEV), 4, 4)
+
+
+# ---- module-level parity vs the oracle --------------------------------------
+@pytest.mark.parametrize("name", ["p3_c16", "p5_c32", "crop_c8", "rect_c8"])
+def test_modules_vs_oracle(mods, name):
+    a, m, q = mods
+    d = load_case(name)
+    x = d["x"].astype(f32)
+    W = load_weights()
+    grid = int(d["grid"]) if "grid" in d.files else 8
+    a.grid_size = grid
+    try:
+        xt = torch.from_numpy(x).to(DEV)
+        phi, _ = a.compute_phi_tiles(xt)
+        ref_phi = O.phi_tiles(x, grid)
+        assert np.array_equal(phi.cpu().numpy(), ref_phi)
+        C = a(xt)
+        refC, _, _ = O.analyzer_forward(x, W, grid)
+        assert np.array_equal(C.cpu().numpy(), refC)
+        bits = m(C, temperature=1.0)
+        assert np.array_equal(bits.cpu().numpy(), O.mlp_mapper(refC, W, 1.0))
+        y = q(xt, bits)
+        ref = O.hook_forward(x, W, grid)
+        assert np.array_equal(y.cpu().numpy(), ref["y"])
+    finally:
+        a.grid_size = 8
+
+
+def test_hooks_forward_features_vs_oracle():
+    """The hook protocol end to end (C3/C4/C5 of one batch) == oracle hook."""
+    from mcaq_yolo_amd.hooks import MCAQHooks
+    h = MCAQHooks(device=DEV).eval()
+    W = load_weights()
+    sd = {k: torch.from_numpy(np.asarray(v)) for k, v in W.items()
+          if k.startswith("complexity_analyzer.") or k.startswith("bit_mapper.")}
+    for idx in (4, 6, 9):
+        for k, v in W.items():
+            if k.startswith("soft_mask."):
+                sd["quantizers.%d.%s" % (idx, k)] = torch.from_numpy(np.asarray(v))
+    h.load_state_dict(sd, strict=False)
+    xs = [load_case(n)["x"].astype(f32) for n in ("full_p3", "full_p4", "full_p5")]
+    outs, aux = h.forward_features([torch.from_numpy(x).to(DEV) for x in xs], temperature=1.0)
+    assert [a_["layer"] for a_ in aux] == [4, 6, 9]
+    for x, y, a_ in zip(xs, outs, aux):
+        ref = O.hook_forward(x, W, 8)
+        assert np.array_equal(a_["bit_map"].cpu().numpy(), ref["bits"])
+        assert np.array_equal(y.cpu().numpy(), ref["y"])
+    avg = MCAQHooks.avg_bits(aux)
+    assert 2.0 <= float(avg) <= 8.0
+
+
+def test_hooks_on_a_module_chain():
+    """register_forward_hook wiring: the hooked layer's output is replaced by the
+    quantized map only while a forward is open (models/mcaq_yolo.py:409-455)."""
+    from mcaq_yolo_amd.hooks import MCAQHooks
+    torch.manual_seed(0)
+    layers = torch.nn.Sequential(*[torch.nn.Identity() for _ in range(10)]).to(DEV)
+    h = MCAQHooks(device=DEV, indices=(4,)).eval().register(layers)
+    x = torch.nn.functional.silu(torch.randn(2, 16, 40, 40, device=DEV))
+    assert torch.equal(layers(x), x)            # inactive: pass-through
+    aux = h.begin(temperature=1.0)
+    y = layers(x)
+    h.end()
+    assert len(aux) == 1 and torch.equal(y, aux[0]["features_q"]) and not torch.equal(y, x)
+    h.begin(quantize=False)
+    assert torch.equal(layers(x), x)            # quantize=False: aux only
+    h.end()
+    h.remove()
