@@ -200,18 +200,23 @@ MCAQ_HD int block_or(const Ctx& ctx, int v) {
 // Histogram counts are integers (exact in any order); the double prefix sums
 // are exact because every partial sum fits in 53 bits, so one wave's parallel
 // scan reproduces ATen's sequential double cumsum.
+MCAQ_HD void otsu_hist_add(Shared& sh, float x) {
+  if (x >= 0.0f && x <= 1.0f) {   // histc ignores out-of-range values
+    int k = (int)(x * 256.0f);
+    if (k > 255) k = 255;
+    MATOMIC_ADD(&sh.hist[k], 1);
+  }
+}
+MCAQ_HD float otsu_from_hist(const Ctx& ctx, Shared& sh);
 MCAQ_HD float otsu_threshold(const Ctx& ctx, Shared& sh, const float* v, int P) {
   MFOR(i, 256) sh.hist[i] = 0;
   MSYNC();
-  MFOR(p, P) {
-    const float x = v[p];
-    if (x >= 0.0f && x <= 1.0f) {
-      int k = (int)(x * 256.0f);
-      if (k > 255) k = 255;
-      MATOMIC_ADD(&sh.hist[k], 1);
-    }
-  }
+  MFOR(p, P) otsu_hist_add(sh, v[p]);
   MSYNC();
+  return otsu_from_hist(ctx, sh);
+}
+// threshold from a complete histogram in sh.hist (all threads; ends synced)
+MCAQ_HD float otsu_from_hist(const Ctx& ctx, Shared& sh) {
 #if defined(__HIP_DEVICE_COMPILE__)
   if (ctx.tid < 64) {
     const int l = ctx.tid;
@@ -527,6 +532,100 @@ MCAQ_HD void store4(float* p, const float (&v)[4]) {
 #endif
 }
 
+#if defined(__HIPCC__)
+// 3-wide horizontal dilation of word k of a 4-word register row
+__device__ __forceinline__ uint32_t dil3(const uint32_t (&rw)[4], int k) {
+  const uint32_t c = rw[k];
+  const uint32_t l = (c << 1) | (k > 0 ? rw[k > 0 ? k - 1 : 0] >> 31 : 0u);
+  const uint32_t r = (c >> 1) | (k < 3 ? rw[k < 3 ? k + 1 : 3] << 31 : 0u);
+  return c | l | r;
+}
+#endif
+
+// exact 121-tap adaptive mean of 255*G at (h, w), replicate pad, oneDNN
+// order (kh-major, kw-minor, FMA from 0); each row's 11 loads issue together
+MCAQ_HD float exact_g11(const float* G, int Hc, int Wc, int h, int w) {
+  float acc = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 11; ++i) {
+    const float* row = G + imin_(imax_(h + i - 5, 0), Hc - 1) * Wc;
+    float v[11];
+#pragma unroll
+    for (int j = 0; j < 11; ++j) v[j] = row[imin_(imax_(w + j - 5, 0), Wc - 1)] * 255.0f;
+#pragma unroll
+    for (int j = 0; j < 11; ++j) acc = fmaf(bits_as_float(k_gauss11_bits[i * 11 + j]), v[j], acc);
+  }
+  return acc;
+}
+
+// row_field without a branch around the second word (loads issue together)
+MCAQ_HD uint32_t row_field_bf(const uint32_t* row, int x0, int n, int WPR) {
+  const int k = x0 >> 5, sft = x0 & 31;
+  const uint64_t lo = row[k];
+  const uint64_t hi = row[imin_(k + 1, WPR - 1)];
+  uint64_t v = lo | ((sft + n > 32 && k + 1 < WPR) ? (hi << 32) : 0ull);
+  v >>= sft;
+  return n == 32 ? (uint32_t)v : (uint32_t)(v & ((1ull << n) - 1ull));
+}
+
+// popcount of a T x T window of a bit plane (T <= 32)
+template <int T>
+MCAQ_HD int tile_pop_t(const uint32_t* plane, int WPR, int h0, int w0) {
+  uint32_t f[T];
+#pragma unroll
+  for (int yy = 0; yy < T; ++yy) f[yy] = row_field_bf(plane + (h0 + yy) * WPR, w0, T, WPR);
+  int c = 0;
+#pragma unroll
+  for (int yy = 0; yy < T; ++yy) c += popc(f[yy]);
+  return c;
+}
+
+// occupied S x S boxes of a T x T window (T <= 16): OR-fold S rows, then S columns
+template <int T, int S>
+MCAQ_HD int box_count_s(const uint32_t (&f)[T]) {
+  uint32_t starts = 0u;
+#pragma unroll
+  for (int x = 0; x < T; x += S) starts |= 1u << x;
+  int n = 0;
+#pragma unroll
+  for (int by = 0; by < T; by += S) {
+    uint32_t o = 0u;
+#pragma unroll
+    for (int yy = 0; yy < S; ++yy) o |= f[by + yy];
+#pragma unroll
+    for (int sh2 = 1; sh2 < S; sh2 <<= 1) o |= o >> sh2;
+    n += popc(o & starts);
+  }
+  return n;
+}
+template <int T>
+MCAQ_HD int box_count_t(const uint32_t* plane, int WPR, int h0, int w0, int s) {
+  uint32_t f[T];
+#pragma unroll
+  for (int yy = 0; yy < T; ++yy) f[yy] = row_field_bf(plane + (h0 + yy) * WPR, w0, T, WPR);
+  if (s == 2) return box_count_s<T, 2>(f);
+  if (s == 4) return box_count_s<T, (T >= 4 ? 4 : 2)>(f);
+  if (s == 8) return box_count_s<T, (T >= 8 ? 8 : 2)>(f);
+  return box_count_s<T, (T >= 16 ? 16 : 2)>(f);
+}
+
+// rows per thread of the column-strip convolution stages
+constexpr int SR = 8;
+
+// sequential row-major sum of a T x T window (avg_pool2d order), unrolled so
+// all loads issue ahead of the dependent add chain
+template <int T, bool SQ>
+MCAQ_HD float tile_sum_t(const float* plane, int Wc, int h0, int w0) {
+  float acc = 0.0f;
+#pragma unroll
+  for (int yy = 0; yy < T; ++yy) {
+    const float* row = plane + (h0 + yy) * Wc + w0;
+#pragma unroll
+    for (int xx = 0; xx < T; ++xx) acc = SQ ? acc + row[xx] * row[xx] : acc + row[xx];
+  }
+  return acc;
+}
+
 // ---- pass A: per-image pixel work -> phi (one 1024-thread workgroup per image)
 MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, Planes& pl, Shared& sh) {
   const int Hc = S.Hc, Wc = S.Wc, P = Hc * Wc, T = S.tile, wt = S.wt, NT = S.ht * wt;
@@ -538,100 +637,167 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, Planes& pl,
 
   MSTAMP(0);
   {
-    // -- gray (channel mean from the stats pass) + per-image normalise01
+    // -- gray (channel mean from the stats pass) + per-image normalise01.
+    //    Up to GPT pixels per thread are loaded at once and kept in registers.
     const float* gin = S.gray + (size_t)b * P;
+    MFOR(i, 256) sh.hist[i] = 0;          // Otsu histogram, filled by the blur stage
     float lmn = 3.402823466e38f, lmx = -3.402823466e38f;
-    MFOR(p, P) { const float v = gin[p]; pl.G[p] = v; lmn = fmin_(lmn, v); lmx = fmax_(lmx, v); }
+    constexpr int GPT = 8;
+    const bool greg = P <= GPT * ctx.nthr;
+    float gv[GPT];
+    if (greg) {
+#pragma unroll
+      for (int i = 0; i < GPT; ++i) {
+        const int p = ctx.tid + i * ctx.nthr;
+        gv[i] = gin[p < P ? p : 0];
+        if (p < P) { lmn = fmin_(lmn, gv[i]); lmx = fmax_(lmx, gv[i]); }
+      }
+    } else {
+      MFOR(p, P) { const float v = gin[p]; pl.G[p] = v; lmn = fmin_(lmn, v); lmx = fmax_(lmx, v); }
+    }
     float mn, mx;
     block_minmax(ctx, sh, lmn, lmx, mn, mx);
     const float den = (mx - mn) + 1e-8f;
-    MFOR(p, P) pl.G[p] = (pl.G[p] - mn) / den;
+    if (greg) {
+#pragma unroll
+      for (int i = 0; i < GPT; ++i) {
+        const int p = ctx.tid + i * ctx.nthr;
+        if (p < P) pl.G[p] = (gv[i] - mn) / den;
+      }
+    } else {
+      MFOR(p, P) pl.G[p] = (pl.G[p] - mn) / den;
+    }
+    MSYNC();
     MSTAMP(1);
 
-    // -- 5x5 Gaussian blur (zero pad; an out-of-image tap adds fma(w, 0, acc) == acc)
-    MFOR(q, NQ) {
-      const int h = q / QPR, w0 = (q - h * QPR) * 4;
-      float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-      for (int i = 0; i < 5; ++i) {
-        const int hh = h + i - 2;
-        if (hh < 0 || hh >= Hc) continue;
-        const float* row = pl.G + hh * Wc;
-        float seg[8];
+    // -- 5x5 Gaussian blur (zero pad; an out-of-image tap adds fma(w, 0, acc) == acc
+    //    because acc >= +0), fused with the Otsu histogram of the result.
+    //    Column strips of SR rows per thread: consecutive threads own consecutive
+    //    columns (conflict-free LDS rows); all (SR+4) x 5 loads are branch-free
+    //    (clamped address, zero select) so they issue together; every output
+    //    still accumulates its 25 taps row-major from 0 (the oneDNN order).
+    {
+      const int nsr = (Hc + SR - 1) / SR;
+      MFOR2(st, w, nsr, Wc) {
+        const int r0 = st * SR;
+        float v[SR + 4][5];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) { const int ww = w0 - 2 + u; seg[u] = (ww >= 0 && ww < Wc) ? row[ww] : 0.0f; }
+        for (int t = 0; t < SR + 4; ++t) {
+          const int hh = r0 + t - 2;
+          const bool rv = hh >= 0 && hh < Hc;
+          const float* row = pl.G + imin_(imax_(hh, 0), Hc - 1) * Wc;
 #pragma unroll
-        for (int j = 0; j < 5; ++j) {
-          const float k = bits_as_float(k_gauss5_bits[i * 5 + j]);
+          for (int j = 0; j < 5; ++j) {
+            const int ww = w + j - 2;
+            const float x = row[imin_(imax_(ww, 0), Wc - 1)];
+            v[t][j] = (rv && ww >= 0 && ww < Wc) ? x : 0.0f;
+          }
+        }
 #pragma unroll
-          for (int r = 0; r < 4; ++r) acc[r] = fmaf(k, seg[r + j], acc[r]);
+        for (int r = 0; r < SR; ++r) {
+          float acc = 0.0f;
+#pragma unroll
+          for (int i = 0; i < 5; ++i)
+#pragma unroll
+            for (int j = 0; j < 5; ++j) acc = fmaf(bits_as_float(k_gauss5_bits[i * 5 + j]), v[r + i][j], acc);
+          if (r0 + r < Hc) {
+            pl.A[(r0 + r) * Wc + w] = acc;
+            otsu_hist_add(sh, acc);
+          }
         }
       }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) if (w0 + r < Wc) pl.A[h * Wc + w0 + r] = acc[r];
     }
     MSYNC();
     MSTAMP(2);
-    const float thr = otsu_threshold(ctx, sh, pl.A, P);
+    const float thr = otsu_from_hist(ctx, sh);
     const float thr255 = thr * 255.0f;
     const float lo255 = 0.5f * thr255;
     MSTAMP(3);
 
-    // -- Sobel of 255*blur (zero pad), L1 magnitude -> Bf, direction -> dir
-    MFOR(q, NQ) {
-      const int h = q / QPR, w0 = (q - h * QPR) * 4;
-      float gx[4] = {0.0f, 0.0f, 0.0f, 0.0f}, gy[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-      for (int i = 0; i < 3; ++i) {
-        const int hh = h + i - 1;
-        if (hh < 0 || hh >= Hc) continue;
-        const float* row = pl.A + hh * Wc;
-        float v[6];
+    // -- Sobel of 255*blur (zero pad), L1 magnitude -> Bf, direction -> dir.
+    //    Column strips as the blur.  Zero-weight taps are skipped and padded
+    //    taps add fma(k, 0, g) == g (g never holds -0: it starts at +0).
+    {
+      const int nsr = (Hc + SR - 1) / SR;
+      MFOR2(st, w, nsr, Wc) {
+        const int r0 = st * SR;
+        float v[SR + 2][3];
 #pragma unroll
-        for (int u = 0; u < 6; ++u) { const int ww = w0 - 1 + u; v[u] = (ww >= 0 && ww < Wc) ? row[ww] * 255.0f : 0.0f; }
-        const float kx = (i == 1) ? 2.0f : 1.0f;          // gx taps (i,0) = -kx, (i,2) = +kx
-        const float ky = (float)(i - 1);                    // gy taps (i,j) = ky * {1,2,1}
+        for (int t = 0; t < SR + 2; ++t) {
+          const int hh = r0 + t - 1;
+          const bool rv = hh >= 0 && hh < Hc;
+          const float* row = pl.A + imin_(imax_(hh, 0), Hc - 1) * Wc;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          gx[r] = fmaf(-kx, v[r], gx[r]);
-          gx[r] = fmaf(kx, v[r + 2], gx[r]);
-          if (i != 1) {
-            gy[r] = fmaf(ky, v[r], gy[r]);
-            gy[r] = fmaf(2.0f * ky, v[r + 1], gy[r]);
-            gy[r] = fmaf(ky, v[r + 2], gy[r]);
+          for (int j = 0; j < 3; ++j) {
+            const int ww = w + j - 1;
+            const float x = row[imin_(imax_(ww, 0), Wc - 1)] * 255.0f;
+            v[t][j] = (rv && ww >= 0 && ww < Wc) ? x : 0.0f;
           }
         }
-      }
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (w0 + r >= Wc) continue;
-        const int p = h * Wc + w0 + r;
-        pl.Bf[p] = fabsf(gx[r]) + fabsf(gy[r]);
-        pl.dir[p] = (uint8_t)nms_dir(gx[r], gy[r]);
+        for (int r = 0; r < SR; ++r) {
+          float gx = 0.0f, gy = 0.0f;
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            const float kx = (i == 1) ? 2.0f : 1.0f;    // gx taps (i,0) = -kx, (i,2) = +kx
+            const float ky = (float)(i - 1);             // gy taps (i,j) = ky * {1,2,1}
+            gx = fmaf(-kx, v[r + i][0], gx);
+            gx = fmaf(kx, v[r + i][2], gx);
+            if (i != 1) {
+              gy = fmaf(ky, v[r + i][0], gy);
+              gy = fmaf(2.0f * ky, v[r + i][1], gy);
+              gy = fmaf(ky, v[r + i][2], gy);
+            }
+          }
+          if (r0 + r < Hc) {
+            const int p = (r0 + r) * Wc + w;
+            pl.Bf[p] = fabsf(gx) + fabsf(gy);
+            pl.dir[p] = (uint8_t)nms_dir(gx, gy);
+          }
+        }
       }
     }
     MSYNC();
     MSTAMP(4);
-    // -- NMS (replicate-shifted neighbours) + double threshold -> bit planes
+    // -- NMS (replicate-shifted neighbours) + double threshold -> bit planes.
+    //    Column strips: directions + magnitudes of SR rows (one round trip),
+    //    then both neighbours of every row (one more), then the ballots.
     uint32_t* E0 = pl.bits(BP_E0);
     uint32_t* E1 = pl.bits(BP_E1);
     uint32_t* WK = pl.bits(BP_WK);
-    MFOR2(h, sl, Hc, RS) {
-      const int k = sl >> 5, bit = sl & 31, w = sl;
-      bool strong = false, weak = false;
-      if (w < Wc) {
-        const int p = h * Wc + w;
-        const int d = pl.dir[p];
-        const int dy1 = (d == 0) ? 0 : -1;
-        const int dx1 = (d == 2) ? 0 : ((d == 3) ? -1 : 1);
-        const int h1 = imin_(imax_(h + dy1, 0), Hc - 1), w1 = imin_(imax_(w + dx1, 0), Wc - 1);
-        const int h2 = imin_(imax_(h - dy1, 0), Hc - 1), w2 = imin_(imax_(w - dx1, 0), Wc - 1);
-        const float m = pl.Bf[p];
-        const bool keep = (m >= pl.Bf[h1 * Wc + w1]) && (m >= pl.Bf[h2 * Wc + w2]);
-        const float nms = keep ? m : 0.0f;
-        strong = nms > thr255;
-        weak = nms > lo255;
+    {
+      const int nsr = (Hc + SR - 1) / SR;
+      MFOR2(st, sl, nsr, RS) {
+        const int k = sl >> 5, bit = sl & 31, w = sl;
+        const int r0 = st * SR;
+        const int wc = imin_(w, Wc - 1);
+        int d[SR];
+        float m[SR], n1[SR], n2[SR];
+#pragma unroll
+        for (int r = 0; r < SR; ++r) {
+          const int p = imin_(r0 + r, Hc - 1) * Wc + wc;
+          d[r] = pl.dir[p];
+          m[r] = pl.Bf[p];
+        }
+#pragma unroll
+        for (int r = 0; r < SR; ++r) {
+          const int h = imin_(r0 + r, Hc - 1);
+          const int dy1 = (d[r] == 0) ? 0 : -1;
+          const int dx1 = (d[r] == 2) ? 0 : ((d[r] == 3) ? -1 : 1);
+          const int h1 = imin_(imax_(h + dy1, 0), Hc - 1), w1 = imin_(imax_(wc + dx1, 0), Wc - 1);
+          const int h2 = imin_(imax_(h - dy1, 0), Hc - 1), w2 = imin_(imax_(wc - dx1, 0), Wc - 1);
+          n1[r] = pl.Bf[h1 * Wc + w1];
+          n2[r] = pl.Bf[h2 * Wc + w2];
+        }
+#pragma unroll
+        for (int r = 0; r < SR; ++r) {
+          if (r0 + r >= Hc) continue;
+          const bool keep = (m[r] >= n1[r]) && (m[r] >= n2[r]);
+          const float nms = keep ? m[r] : 0.0f;
+          put_bits(E0, (r0 + r) * WPR + k, bit, w < Wc && nms > thr255);
+          put_bits(WK, (r0 + r) * WPR + k, bit, w < Wc && nms > lo255);
+        }
       }
-      put_bits(E0, h * WPR + k, bit, strong);
-      put_bits(WK, h * WPR + k, bit, weak);
     }
     MSYNC();
     MSTAMP(5);
@@ -639,25 +805,84 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, Planes& pl,
     uint32_t* src = E0;
     uint32_t* dst = E1;
     const int iters = S.hyst_iters < 1 ? 1 : S.hyst_iters;
-    for (int it = 0; it < iters; ++it) {
-      int changed = 0;
-      MFOR2(h, k, Hc, WPR) {
-        const uint32_t cur = src[h * WPR + k];
-        uint32_t g = 0u;
-        for (int hh = imax_(h - 1, 0); hh <= imin_(h + 1, Hc - 1); ++hh) {
-          const uint32_t* row = src + hh * WPR;
-          const uint32_t c = row[k];
-          const uint32_t l = (c << 1) | (k > 0 ? row[k - 1] >> 31 : 0u);
-          const uint32_t r = (c >> 1) | (k + 1 < WPR ? row[k + 1] << 31 : 0u);
-          g |= c | l | r;
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (Hc <= 128 && WPR <= 4) {
+      // one wave, planes in registers (lane l: rows 2l, 2l+1), neighbour rows by
+      // lane shuffles: no barrier per iteration.  Same Jacobi sweeps and the
+      // same stop rule as the workgroup loop below.
+      if (ctx.tid < 64) {
+        const int lane = ctx.tid;
+        uint32_t e[2][4], wk[2][4];
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int row = 2 * lane + rr;
+            const bool ok = row < Hc && k < WPR;
+            e[rr][k] = ok ? src[row * WPR + k] : 0u;
+            wk[rr][k] = ok ? WK[row * WPR + k] : 0u;
+          }
         }
-        const uint32_t nv = cur | (WK[h * WPR + k] & g);
-        changed |= (nv != cur);
-        dst[h * WPR + k] = nv;
+        for (int it = 0; it < iters; ++it) {
+          uint32_t up[4], dn[4], d[4][4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t u = (uint32_t)__shfl_up((int)e[1][k], 1, 64);
+            const uint32_t v = (uint32_t)__shfl_down((int)e[0][k], 1, 64);
+            up[k] = lane > 0 ? u : 0u;
+            dn[k] = lane < 63 ? v : 0u;
+          }
+          // horizontal 3-dilation of the 4 rows up, e0, e1, dn
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            d[0][k] = dil3(up, k);
+            d[1][k] = dil3(e[0], k);
+            d[2][k] = dil3(e[1], k);
+            d[3][k] = dil3(dn, k);
+          }
+          bool ch = false;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const uint32_t n0 = e[0][k] | (wk[0][k] & (d[0][k] | d[1][k] | d[2][k]));
+            const uint32_t n1 = e[1][k] | (wk[1][k] & (d[1][k] | d[2][k] | d[3][k]));
+            ch = ch || (n0 != e[0][k]) || (n1 != e[1][k]);
+            e[0][k] = n0; e[1][k] = n1;
+          }
+          if (!__any(ch)) break;
+        }
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int row = 2 * lane + rr;
+            if (row < Hc && k < WPR) src[row * WPR + k] = e[rr][k];
+          }
+        }
       }
-      const int any = block_or(ctx, changed);
-      uint32_t* t = src; src = dst; dst = t;
-      if (!any) break;
+      MSYNC();
+    } else
+#endif
+    {
+      for (int it = 0; it < iters; ++it) {
+        int changed = 0;
+        MFOR2(h, k, Hc, WPR) {
+          const uint32_t cur = src[h * WPR + k];
+          uint32_t g = 0u;
+          for (int hh = imax_(h - 1, 0); hh <= imin_(h + 1, Hc - 1); ++hh) {
+            const uint32_t* row = src + hh * WPR;
+            const uint32_t c = row[k];
+            const uint32_t l = (c << 1) | (k > 0 ? row[k - 1] >> 31 : 0u);
+            const uint32_t r = (c >> 1) | (k + 1 < WPR ? row[k + 1] << 31 : 0u);
+            g |= c | l | r;
+          }
+          const uint32_t nv = cur | (WK[h * WPR + k] & g);
+          changed |= (nv != cur);
+          dst[h * WPR + k] = nv;
+        }
+        const int any = block_or(ctx, changed);
+        uint32_t* t = src; src = dst; dst = t;
+        if (!any) break;
+      }
     }
     const uint32_t* edge = src;   // final edge bit plane
     MSTAMP(6);
@@ -676,92 +901,114 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, Planes& pl,
       // threshold exceeds the proven error bound k_g11_margin (tools/
       // gen_tables.py); the others get the exact 121-tap sum in oneDNN order
       // (taps kh-major / kw-minor, FMA from 0), i.e. the reference's value.
-      MFOR(p, P) pl.A[p] = pl.G[p] * 255.0f;
-      MSYNC();
-      float* rowp = pl.Bf;    // horizontal 11-tap pass
-      MFOR(q, NQ) {
-        const int h = q / QPR, w0 = (q - h * QPR) * 4;
-        const float* row = pl.A + h * Wc;
-        float seg[14];
+      // g255 = G * 255 is recomputed where read (same rounding as a stored plane).
+      float* rowp = pl.Bf;    // horizontal 11-tap pass, column strips, loads issued together
+      const int nsr = (Hc + SR - 1) / SR;
+      MFOR2(st, w, nsr, Wc) {
+        const int r0 = st * SR;
+        float v[SR][11];
 #pragma unroll
-        for (int u = 0; u < 14; ++u) seg[u] = row[imin_(imax_(w0 - 5 + u, 0), Wc - 1)];
-        float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        for (int r = 0; r < SR; ++r) {
+          const float* row = pl.G + imin_(r0 + r, Hc - 1) * Wc;
 #pragma unroll
-        for (int j = 0; j < 11; ++j) {
-          const float kk = bits_as_float(k_g11_sep_bits[j]);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[r] = fmaf(kk, seg[r + j], acc[r]);
+          for (int j = 0; j < 11; ++j) v[r][j] = row[imin_(imax_(w + j - 5, 0), Wc - 1)] * 255.0f;
         }
 #pragma unroll
-        for (int r = 0; r < 4; ++r) if (w0 + r < Wc) rowp[h * Wc + w0 + r] = acc[r];
+        for (int r = 0; r < SR; ++r) {
+          float acc = 0.0f;
+#pragma unroll
+          for (int j = 0; j < 11; ++j) acc = fmaf(bits_as_float(k_g11_sep_bits[j]), v[r][j], acc);
+          if (r0 + r < Hc) rowp[(r0 + r) * Wc + w] = acc;
+        }
       }
       MSYNC();
       const float marg = bits_as_float(k_g11_margin_bits[0]);
-      MFOR2(h, sl, Hc, RS) {
+      MFOR2(st, sl, nsr, RS) {   // vertical pass: column strips of SR rows, word-aligned lanes
         const int k = sl >> 5, bit = sl & 31, w = sl;
-        bool on = false;
-        if (w < Wc) {
-          float m = 0.0f;
+        const int r0 = st * SR;
+        bool on[SR];
 #pragma unroll
-          for (int i = 0; i < 11; ++i)
-            m = fmaf(bits_as_float(k_g11_sep_bits[i]), rowp[imin_(imax_(h + i - 5, 0), Hc - 1) * Wc + w], m);
-          const float g = pl.A[h * Wc + w];
-          const float t = m - 2.0f;
-          if (fabsf(g - t) > marg) {
-            on = g > t;
-          } else {
-            float acc = 0.0f;
-            for (int i = 0; i < 11; ++i) {
-              const float* row = pl.A + imin_(imax_(h + i - 5, 0), Hc - 1) * Wc;
-              for (int j = 0; j < 11; ++j)
-                acc = fmaf(bits_as_float(k_gauss11_bits[i * 11 + j]), row[imin_(imax_(w + j - 5, 0), Wc - 1)], acc);
+        for (int r = 0; r < SR; ++r) on[r] = false;
+        if (w < Wc) {
+          float v[SR + 10];
+#pragma unroll
+          for (int t = 0; t < SR + 10; ++t) v[t] = rowp[imin_(imax_(r0 + t - 5, 0), Hc - 1) * Wc + w];
+#pragma unroll
+          for (int r = 0; r < SR; ++r) {
+            if (r0 + r >= Hc) continue;
+            const int h = r0 + r;
+            float m = 0.0f;
+#pragma unroll
+            for (int i = 0; i < 11; ++i) m = fmaf(bits_as_float(k_g11_sep_bits[i]), v[r + i], m);
+            const float g = pl.G[h * Wc + w] * 255.0f;
+            const float t = m - 2.0f;
+            if (fabsf(g - t) > marg) {
+              on[r] = g > t;
+            } else {
+              on[r] = g > exact_g11(pl.G, Hc, Wc, h, w) - 2.0f;
             }
-            on = g > acc - 2.0f;
           }
         }
-        put_bits(BIN, h * WPR + k, bit, on);
+#pragma unroll
+        for (int r = 0; r < SR; ++r) if (r0 + r < Hc) put_bits(BIN, (r0 + r) * WPR + k, bit, on[r]);
       }
     }
     MSYNC();
     MSTAMP(7);
 
-    // -- Sobel of the normalised gray (phi3) -> A = gx, Bf = gy; uniform LBP label planes;
-    //    boundary and Euler quad-class planes of the mask
-    MFOR2(h, sl, Hc, RS) {
-      const int k = sl >> 5, bit = sl & 31, w = sl;
-      int lab = -1;
-      if (w < Wc) {
-        const int hm = imax_(h - 1, 0), hp = imin_(h + 1, Hc - 1);
-        const int wm = imax_(w - 1, 0), wp = imin_(w + 1, Wc - 1);
-        const float* r0 = pl.G + hm * Wc;
-        const float* r1 = pl.G + h * Wc;
-        const float* r2 = pl.G + hp * Wc;
-        const float c = r1[w];
-        // zero-padded Sobel taps, row-major
-        const float z00 = (h > 0 && w > 0) ? r0[wm] : 0.0f, z01 = h > 0 ? r0[w] : 0.0f;
-        const float z02 = (h > 0 && w + 1 < Wc) ? r0[wp] : 0.0f;
-        const float z10 = w > 0 ? r1[wm] : 0.0f, z12 = w + 1 < Wc ? r1[wp] : 0.0f;
-        const float z20 = (h + 1 < Hc && w > 0) ? r2[wm] : 0.0f, z21 = h + 1 < Hc ? r2[w] : 0.0f;
-        const float z22 = (h + 1 < Hc && w + 1 < Wc) ? r2[wp] : 0.0f;
-        float gx = 0.0f, gy = 0.0f;
-        gx = fmaf(-1.0f, z00, gx); gx = fmaf(1.0f, z02, gx);
-        gx = fmaf(-2.0f, z10, gx); gx = fmaf(2.0f, z12, gx);
-        gx = fmaf(-1.0f, z20, gx); gx = fmaf(1.0f, z22, gx);
-        gy = fmaf(-1.0f, z00, gy); gy = fmaf(-2.0f, z01, gy); gy = fmaf(-1.0f, z02, gy);
-        gy = fmaf(1.0f, z20, gy); gy = fmaf(2.0f, z21, gy); gy = fmaf(1.0f, z22, gy);
-        pl.A[h * Wc + w] = gx;
-        pl.Bf[h * Wc + w] = gy;
-        // LBP (morphology.py:630-646): replicate pad, nb >= center, circular order
-        int bt[8];
-        bt[0] = r0[wm] >= c; bt[1] = r0[w] >= c; bt[2] = r0[wp] >= c; bt[3] = r1[wp] >= c;
-        bt[4] = r2[wp] >= c; bt[5] = r2[w] >= c; bt[6] = r2[wm] >= c; bt[7] = r1[wm] >= c;
-        int n1 = 0, tr = 0;
+    // -- Sobel of the normalised gray (phi3) -> A = gx, Bf = gy; uniform LBP label planes.
+    //    Column strips: the (SR+2) x 3 replicate-clamped window values load
+    //    together; the zero-padded Sobel taps select 0 outside the image.
+    {
+      const int nsr = (Hc + SR - 1) / SR;
+      MFOR2(st, sl, nsr, RS) {
+        const int k = sl >> 5, bit = sl & 31, w = sl;
+        const int r0 = st * SR;
+        const int wc = imin_(w, Wc - 1);
+        const int wm = imax_(wc - 1, 0), wp = imin_(wc + 1, Wc - 1);
+        const bool cl = wc > 0, cr = wc + 1 < Wc;
+        float c[SR + 2][3];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) { n1 += bt[q]; tr += bt[q] != bt[(q + 7) & 7]; }
-        lab = tr <= 2 ? n1 : 9;
+        for (int t = 0; t < SR + 2; ++t) {
+          const float* row = pl.G + imin_(imax_(r0 + t - 1, 0), Hc - 1) * Wc;
+          c[t][0] = row[wm]; c[t][1] = row[wc]; c[t][2] = row[wp];
+        }
+#pragma unroll
+        for (int r = 0; r < SR; ++r) {
+          const int h = r0 + r;
+          int lab = -1;
+          if (w < Wc && h < Hc) {
+            const bool ru = h > 0, rd = h + 1 < Hc;
+            const float ctr = c[r + 1][1];
+            // zero-padded Sobel taps, row-major
+            const float z00 = (ru && cl) ? c[r][0] : 0.0f, z01 = ru ? c[r][1] : 0.0f;
+            const float z02 = (ru && cr) ? c[r][2] : 0.0f;
+            const float z10 = cl ? c[r + 1][0] : 0.0f, z12 = cr ? c[r + 1][2] : 0.0f;
+            const float z20 = (rd && cl) ? c[r + 2][0] : 0.0f, z21 = rd ? c[r + 2][1] : 0.0f;
+            const float z22 = (rd && cr) ? c[r + 2][2] : 0.0f;
+            float gx = 0.0f, gy = 0.0f;
+            gx = fmaf(-1.0f, z00, gx); gx = fmaf(1.0f, z02, gx);
+            gx = fmaf(-2.0f, z10, gx); gx = fmaf(2.0f, z12, gx);
+            gx = fmaf(-1.0f, z20, gx); gx = fmaf(1.0f, z22, gx);
+            gy = fmaf(-1.0f, z00, gy); gy = fmaf(-2.0f, z01, gy); gy = fmaf(-1.0f, z02, gy);
+            gy = fmaf(1.0f, z20, gy); gy = fmaf(2.0f, z21, gy); gy = fmaf(1.0f, z22, gy);
+            pl.A[h * Wc + w] = gx;
+            pl.Bf[h * Wc + w] = gy;
+            // LBP (morphology.py:630-646): replicate pad, nb >= center, circular order
+            int bt[8];
+            bt[0] = c[r][0] >= ctr; bt[1] = c[r][1] >= ctr; bt[2] = c[r][2] >= ctr; bt[3] = c[r + 1][2] >= ctr;
+            bt[4] = c[r + 2][2] >= ctr; bt[5] = c[r + 2][1] >= ctr; bt[6] = c[r + 2][0] >= ctr; bt[7] = c[r + 1][0] >= ctr;
+            int n1 = 0, tr = 0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) { n1 += bt[q]; tr += bt[q] != bt[(q + 7) & 7]; }
+            lab = tr <= 2 ? n1 : 9;
+          }
+          if (h < Hc) {
+#pragma unroll
+            for (int q = 0; q < 10; ++q) put_bits(pl.bits(BP_L0 + q), h * WPR + k, bit, lab == q);
+          }
+        }
       }
-#pragma unroll
-      for (int q = 0; q < 10; ++q) put_bits(pl.bits(BP_L0 + q), h * WPR + k, bit, lab == q);
     }
     // boundary (m & ~erode3x3 with in-bounds neighbours) and Euler quad classes
     // of the windows anchored at (h, w) over m[h-1..h][w-1..w] (zero padded)
@@ -823,18 +1070,27 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, Planes& pl,
       float val;
       if (it < 4) {
         const float* plane = (it < 2) ? pl.A : pl.Bf;
-        float acc = 0.0f;
-        for (int yy = 0; yy < T; ++yy) {
-          const float* row = plane + (h0 + yy) * Wc + w0;
-          if (it & 1) { for (int xx = 0; xx < T; ++xx) acc = acc + row[xx] * row[xx]; }
-          else { for (int xx = 0; xx < T; ++xx) acc = acc + row[xx]; }
+        const bool sq = (it & 1) != 0;
+        if (T == 4) val = sq ? tile_sum_t<4, true>(plane, Wc, h0, w0) : tile_sum_t<4, false>(plane, Wc, h0, w0);
+        else if (T == 8) val = sq ? tile_sum_t<8, true>(plane, Wc, h0, w0) : tile_sum_t<8, false>(plane, Wc, h0, w0);
+        else if (T == 16) val = sq ? tile_sum_t<16, true>(plane, Wc, h0, w0) : tile_sum_t<16, false>(plane, Wc, h0, w0);
+        else {
+          float acc = 0.0f;
+          for (int yy = 0; yy < T; ++yy) {
+            const float* row = plane + (h0 + yy) * Wc + w0;
+            if (sq) { for (int xx = 0; xx < T; ++xx) acc = acc + row[xx] * row[xx]; }
+            else { for (int xx = 0; xx < T; ++xx) acc = acc + row[xx]; }
+          }
+          val = acc;
         }
-        val = acc;
       } else if (it < 4 + S_) {
         // box counting (morphology.py:576-621): OR-fold s rows, then s columns
         const int s = 2 << (it - 4);
         int n = 0;
-        for (int by = 0; by < T; by += s) {
+        if (T == 4) n = box_count_t<4>(edge, WPR, h0, w0, s);
+        else if (T == 8) n = box_count_t<8>(edge, WPR, h0, w0, s);
+        else if (T == 16) n = box_count_t<16>(edge, WPR, h0, w0, s);
+        else for (int by = 0; by < T; by += s) {
           if (s <= 32) {
             const int fw = T < 32 ? T : 32;
             uint32_t starts = 0u;
@@ -859,7 +1115,10 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, Planes& pl,
         const uint32_t* plane = k < 10 ? pl.bits(BP_L0 + k)
                               : (k == 10 ? edge : (k == 11 ? BIN : (k == 12 ? BND : (k == 13 ? Q1 : (k == 14 ? Q3 : QD)))));
         int cnt = 0;
-        for (int yy = 0; yy < T; ++yy) cnt += row_pop(plane + (h0 + yy) * WPR, w0, T, WPR);
+        if (T == 4) cnt = tile_pop_t<4>(plane, WPR, h0, w0);
+        else if (T == 8) cnt = tile_pop_t<8>(plane, WPR, h0, w0);
+        else if (T == 16) cnt = tile_pop_t<16>(plane, WPR, h0, w0);
+        else for (int yy = 0; yy < T; ++yy) cnt += row_pop(plane + (h0 + yy) * WPR, w0, T, WPR);
         if (k < 10) {
           const float pk = (float)cnt / fT2;
           val = pk * log2_ref(pk + 1e-10f);
