@@ -32,7 +32,7 @@ typedef void* hipStream_t;
 extern "C" {
 #endif
 
-#define MCAQ_ABI_VERSION 2
+#define MCAQ_ABI_VERSION 3
 /* largest dynamic LDS request of the morph kernel (gfx950: 160 KiB per CU) */
 #define MCAQ_MORPH_LDS_LIMIT 163840
 
@@ -103,6 +103,9 @@ typedef struct {
   uint8_t* edge_out;
   uint8_t* bin_out;
   float* gscratch;   /* mcaq_morph_scratch_bytes() bytes, or NULL when 0 */
+  float* tile_tmp;   /* (B, ht*wt, 32) per-tile partial quantities, needed with
+                        flag 1: written by the edge / mask workgroups of the
+                        pixel pass, read by the tile pass */
   int B, H, W, Hc, Wc, tile, ht, wt;
   int batch_offset, batch_total;
   int flags, hyst_iters;

@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libmcaq_hip.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -29,7 +29,7 @@ class FinalizeScale(ctypes.Structure):
 class MorphScale(ctypes.Structure):
     _fields_ = [("gray", P), ("absmean", P), ("cmlp", P), ("mapper", P), ("smask", P),
                 ("c_in", P), ("bits_in", P), ("phi_out", P), ("cmlp_out", P), ("c_out", P),
-                ("bits_out", P), ("m_out", P), ("edge_out", P), ("bin_out", P), ("gscratch", P),
+                ("bits_out", P), ("m_out", P), ("edge_out", P), ("bin_out", P), ("gscratch", P), ("tile_tmp", P),
                 ("B", I), ("H", I), ("W", I), ("Hc", I), ("Wc", I), ("tile", I), ("ht", I), ("wt", I),
                 ("batch_offset", I), ("batch_total", I), ("flags", I), ("hyst_iters", I),
                 ("temperature", Fl), ("min_bits", Fl), ("max_bits", Fl), ("block_begin", I)]

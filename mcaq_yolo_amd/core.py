@@ -235,7 +235,7 @@ class MorphologicalComplexityAnalyzer(nn.Module):
         _run_stats(x, gray=gray, Hc=ht * T, Wc=wt * T)
         phi = torch.empty(B, ht, wt, 8, device=dev)
         flags = abi.F_PHI | self._flags()
-        ptrs = dict(gray=gray, phi_out=phi)
+        ptrs = dict(gray=gray, phi_out=phi, tile_tmp=torch.empty(B, ht * wt, 32, device=dev))
         L = abi.lib()
         if want_c:
             flags |= abi.F_CMLP

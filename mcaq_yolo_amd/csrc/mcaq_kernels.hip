@@ -398,9 +398,9 @@ __global__ __launch_bounds__(256) void mcaq_finalize_kernel(FinalizeArgs a) {
 constexpr int MORPH_THREADS = 1024;
 constexpr int TILES_THREADS = 256;
 
-__device__ __forceinline__ int morph_scale_of(const MorphArgs& a) {
+__device__ __forceinline__ int morph_scale_of(const MorphArgs& a, int img) {
   int si = 0;
-  while (si + 1 < a.nscales && (int)blockIdx.x >= a.s[si + 1].block_begin) ++si;
+  while (si + 1 < a.nscales && img >= a.s[si + 1].block_begin) ++si;
   return si;
 }
 
@@ -408,12 +408,14 @@ template <bool kLDS>
 __global__ __launch_bounds__(MORPH_THREADS) void mcaq_morph_kernel(MorphArgs a, int plane_stride, FinalizeArgs f) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nimg = a.s[a.nscales - 1].block_begin + a.s[a.nscales - 1].B;
-  if ((int)blockIdx.x >= nimg) {   // channel min/max workgroups ride along
-    finalize_body(f, (int)blockIdx.x - nimg, reinterpret_cast<float*>(smem));
+  if ((int)blockIdx.x >= 2 * nimg) {   // channel min/max workgroups ride along
+    finalize_body(f, (int)blockIdx.x - 2 * nimg, reinterpret_cast<float*>(smem));
     return;
   }
-  const MorphScale& S = a.s[morph_scale_of(a)];
-  const int b = (int)blockIdx.x - S.block_begin;
+  // two workgroups per image: role 0 = edge plane, role 1 = mask planes
+  const int img = (int)blockIdx.x >> 1, role = (int)blockIdx.x & 1;
+  const MorphScale& S = a.s[morph_scale_of(a, img)];
+  const int b = img - S.block_begin;
   if (b >= S.B || !(S.flags & F_PHI)) return;
   Ctx ctx{(int)threadIdx.x, (int)blockDim.x};
   Shared sh;
@@ -422,15 +424,15 @@ __global__ __launch_bounds__(MORPH_THREADS) void mcaq_morph_kernel(MorphArgs a, 
     carve_planes(smem, S.Hc, S.Wc, pl);
     carve_shared(smem + plane_stride, sh);
   } else {
-    carve_planes((char*)S.gscratch + (size_t)b * plane_stride, S.Hc, S.Wc, pl);
+    carve_planes((char*)S.gscratch + (size_t)(2 * b + role) * plane_stride, S.Hc, S.Wc, pl);
     carve_shared(smem, sh);
   }
-  morph_edges(ctx, S, b, pl, sh);
+  morph_edges(ctx, S, b, role, pl, sh);
 }
 
 __global__ __launch_bounds__(TILES_THREADS) void mcaq_tiles_kernel(MorphArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const MorphScale& S = a.s[morph_scale_of(a)];
+  const MorphScale& S = a.s[morph_scale_of(a, (int)blockIdx.x)];
   const int b = (int)blockIdx.x - S.block_begin;
   if (b >= S.B) return;
   Ctx ctx{(int)threadIdx.x, (int)blockDim.x};
@@ -668,7 +670,7 @@ size_t mcaq_morph_scratch_bytes(int B, int Hc, int Wc, int ht, int wt) {
   s.Hc = Hc; s.Wc = Wc; s.ht = ht; s.wt = wt; s.H = 2 * Hc; s.W = 2 * Wc;  // conservative: H < Hc + tile
   int mode, stride; size_t dyn;
   if (morph_plan(&s, 1, &mode, &stride, &dyn)) return 0;
-  return mode ? 0 : (size_t)B * stride;
+  return mode ? 0 : (size_t)2 * B * stride;   // edge + mask workgroup per image
 }
 
 int mcaq_morph(const mcaq_morph_scale* scales, int nscales, hipStream_t stream) {
@@ -691,14 +693,15 @@ int mcaq_morph_finalize(const mcaq_morph_scale* scales, int nscales, const mcaq_
     if (S.B < 1 || S.ht < 1 || S.wt < 1) return (int)hipErrorInvalidValue;
     if (S.tile < 4 || (S.tile & (S.tile - 1)) || S.tile > 64) return (int)hipErrorInvalidValue;
     if (S.Hc != S.ht * S.tile || S.Wc != S.wt * S.tile || S.Hc > S.H || S.Wc > S.W) return (int)hipErrorInvalidValue;
-    // phi_out carries phi from pass A to pass B
-    if ((S.flags & F_PHI) && !S.phi_out) return (int)hipErrorInvalidValue;
-    if ((S.flags & F_CMLP) && (!S.phi_out || !S.cmlp)) return (int)hipErrorInvalidValue;
+    // tile_tmp carries the per-tile partials from pass A to pass B; without
+    // F_PHI the complexity MLP reads phi from phi_out
+    if ((S.flags & F_PHI) && !S.tile_tmp) return (int)hipErrorInvalidValue;
+    if ((S.flags & F_CMLP) && (!S.cmlp || (!(S.flags & F_PHI) && !S.phi_out))) return (int)hipErrorInvalidValue;
     if ((S.flags & F_SOFTMASK) && (!S.smask || !S.absmean)) return (int)hipErrorInvalidValue;
     S.block_begin = blocks;
     blocks += S.B;
     any_phi |= (S.flags & F_PHI) != 0;
-    const int tf = S.flags & (F_CMLP | F_MAPPER | F_SOFTMASK);
+    const int tf = S.flags & (F_PHI | F_CMLP | F_MAPPER | F_SOFTMASK);
     any_tiles |= tf != 0;
     if (tf) tlds = imax_(tlds, tiles_lds_bytes(S.H, S.W, S.ht * S.wt));
   }
@@ -724,7 +727,7 @@ int mcaq_morph_finalize(const mcaq_morph_scale* scales, int nscales, const mcaq_
         if (ae != hipSuccess) return (int)ae;
         set_true = morph_lds_budget();
       }
-      hipLaunchKernelGGL(mcaq_morph_kernel<true>, dim3(blocks + fa.nblocks), dim3(MORPH_THREADS), dyn, stream, a, stride, fa);
+      hipLaunchKernelGGL(mcaq_morph_kernel<true>, dim3(2 * blocks + fa.nblocks), dim3(MORPH_THREADS), dyn, stream, a, stride, fa);
     } else {
       static int set_false = 0;
       if ((int)dyn > set_false) {
@@ -733,7 +736,7 @@ int mcaq_morph_finalize(const mcaq_morph_scale* scales, int nscales, const mcaq_
         if (ae != hipSuccess) return (int)ae;
         set_false = morph_lds_budget();
       }
-      hipLaunchKernelGGL(mcaq_morph_kernel<false>, dim3(blocks + fa.nblocks), dim3(MORPH_THREADS), dyn, stream, a, stride, fa);
+      hipLaunchKernelGGL(mcaq_morph_kernel<false>, dim3(2 * blocks + fa.nblocks), dim3(MORPH_THREADS), dyn, stream, a, stride, fa);
     }
     hipError_t le = hipGetLastError();
     if (le != hipSuccess) return (int)le;

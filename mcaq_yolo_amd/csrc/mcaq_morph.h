@@ -77,6 +77,8 @@ MCAQ_HD int plane_bytes(int Hc, int Wc) {
 }
 // per-image tile storage: fp32 [NT][TILE_FLOATS]
 enum : int { TILE_FLOATS = 48 };
+// per-tile partial quantities in the pass A -> pass B buffer (tile_tmp)
+enum : int { TT_STRIDE = 32 };
 MCAQ_HD int tile_bytes(int NT) { return 4 * TILE_FLOATS * NT; }
 // fixed shared scratch: 256-int histogram, 2 x 256 doubles, 2 x 64 reduction slots, flags
 MCAQ_HD int fixed_bytes() { return 1024 + 4096 + 512 + 64; }
@@ -116,12 +118,14 @@ struct Ctx { int tid, nthr; };
 // diagnostic build only (-DMCAQ_STAMPS): per-stage cycle stamps of workgroup 0
 #if defined(MCAQ_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
 extern __device__ unsigned long long g_mcaq_stamps[64];
+#define MSTAMP_INIT(base) const int mstamp_base = (base)
 #define MSTAMP(k)                                                                   \
   do {                                                                              \
     __syncthreads();                                                                \
-    if (ctx.tid == 0 && blockIdx.x == (unsigned)S.block_begin) g_mcaq_stamps[k] = __builtin_amdgcn_s_memtime(); \
+    if (ctx.tid == 0 && mstamp_base >= 0) g_mcaq_stamps[mstamp_base + (k)] = __builtin_amdgcn_s_memtime(); \
   } while (0)
 #else
+#define MSTAMP_INIT(base) do {} while (0)
 #define MSTAMP(k) do {} while (0)
 #endif
 
@@ -627,7 +631,7 @@ MCAQ_HD float tile_sum_t(const float* plane, int Wc, int h0, int w0) {
 }
 
 // ---- pass A: per-image pixel work -> phi (one 1024-thread workgroup per image)
-MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, Planes& pl, Shared& sh) {
+MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, Planes& pl, Shared& sh) {
   const int Hc = S.Hc, Wc = S.Wc, P = Hc * Wc, T = S.tile, wt = S.wt, NT = S.ht * wt;
   const int WPR = pl.WPR, RS = WPR * 32;   // words / bit slots per row
   const float fT2 = (float)(T * T);
@@ -635,6 +639,7 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, Planes& pl,
   const int QPR = (Wc + 3) >> 2;           // 4-pixel quads per row
   const int NQ = Hc * QPR;
 
+  MSTAMP_INIT(b == 0 ? 16 * role : -1);   // diagnostic build: image 0, slots 0-9 / 16-25
   MSTAMP(0);
   {
     // -- gray (channel mean from the stats pass) + per-image normalise01.
@@ -670,6 +675,18 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, Planes& pl,
     MSYNC();
     MSTAMP(1);
 
+    const uint32_t* edge = nullptr;      // final edge bit plane (edge workgroup)
+    uint32_t* BIN = pl.bits(BP_BIN);
+    uint32_t* BND = pl.bits(BP_BND);
+    uint32_t* Q1 = pl.bits(BP_Q1);
+    uint32_t* Q3 = pl.bits(BP_Q3);
+    uint32_t* QD = pl.bits(BP_QD);
+    // Two workgroups per image run the two independent halves of the
+    // descriptor pipeline side by side: role 0 = Canny edge plane (blur,
+    // Otsu, Sobel, NMS, hysteresis), role 1 = foreground mask / LBP /
+    // gradient planes.  Each reduces its planes to per-tile partial
+    // quantities (tile_tmp); pass B assembles phi from both.
+    if (role == 0) {
     // -- 5x5 Gaussian blur (zero pad; an out-of-image tap adds fma(w, 0, acc) == acc
     //    because acc >= +0), fused with the Otsu histogram of the result.
     //    Column strips of SR rows per thread: consecutive threads own consecutive
@@ -884,11 +901,11 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, Planes& pl,
         if (!any) break;
       }
     }
-    const uint32_t* edge = src;   // final edge bit plane
+    edge = src;
     MSTAMP(6);
 
+    } else {
     // -- foreground mask for phi5 -> BIN bit plane
-    uint32_t* BIN = pl.bits(BP_BIN);
     if (S.flags & F_BIN_OTSU) {
       const float t2 = otsu_threshold(ctx, sh, pl.G, P);
       MFOR2(h, sl, Hc, RS) {
@@ -1012,10 +1029,6 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, Planes& pl,
     }
     // boundary (m & ~erode3x3 with in-bounds neighbours) and Euler quad classes
     // of the windows anchored at (h, w) over m[h-1..h][w-1..w] (zero padded)
-    uint32_t* BND = pl.bits(BP_BND);
-    uint32_t* Q1 = pl.bits(BP_Q1);
-    uint32_t* Q3 = pl.bits(BP_Q3);
-    uint32_t* QD = pl.bits(BP_QD);
     MFOR2(h, k, Hc, WPR) {
       const int nvalid = imin_(Wc - 32 * k, 32);
       const uint32_t vmask = nvalid >= 32 ? 0xFFFFFFFFu : ((1u << nvalid) - 1u);
@@ -1042,8 +1055,9 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, Planes& pl,
       QD[h * WPR + k] = (((Aq & D) & ~(Bq | Cc)) | ((Bq & Cc) & ~(Aq | D))) & vmask;
     }
     MSYNC();
-    if (S.edge_out) MFOR2(h, w, Hc, Wc) S.edge_out[(size_t)b * P + h * Wc + w] = (edge[h * WPR + (w >> 5)] >> (w & 31)) & 1u;
-    if (S.bin_out) MFOR2(h, w, Hc, Wc) S.bin_out[(size_t)b * P + h * Wc + w] = (BIN[h * WPR + (w >> 5)] >> (w & 31)) & 1u;
+    }
+    if (role == 0 && S.edge_out) MFOR2(h, w, Hc, Wc) S.edge_out[(size_t)b * P + h * Wc + w] = (edge[h * WPR + (w >> 5)] >> (w & 31)) & 1u;
+    if (role == 1 && S.bin_out) MFOR2(h, w, Hc, Wc) S.bin_out[(size_t)b * P + h * Wc + w] = (BIN[h * WPR + (w >> 5)] >> (w & 31)) & 1u;
     MSTAMP(8);
 
     // -- per-tile partial quantities, one thread per (tile, item):
@@ -1053,18 +1067,24 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, Planes& pl,
     //    items [14+S,20+S)      counts: edges, mask area, boundary, Euler quads q1, q3, qd
     int S_ = 0;
     for (int s = 2; s <= T; s *= 2) ++S_;
-    // item-major order (consecutive lanes = consecutive tiles of one item) with
-    // each item group padded to whole waves, so no wave mixes item kinds
-    const int NI = 20 + S_;
-    const int nG = (4 * NT + 63) & ~63, nB = (S_ * NT + 63) & ~63, nR = (16 * NT + 63) & ~63;
-    MFOR(u, nG + nB + nR) {
-      int v = u, it0 = 0, nit = 4;
-      if (v >= nG) {
-        v -= nG; it0 = 4; nit = S_;
-        if (v >= nB) { v -= nB; it0 = 4 + S_; nit = 16; }
+    // items of this workgroup: edge role = box counts [4, 4+S) and the edge
+    // count 14+S; mask role = gradient sums [0,4), LBP terms [4+S, 14+S) and
+    // the mask counts [15+S, 20+S).  Item-major order (consecutive lanes =
+    // consecutive tiles of one item), each item group padded to whole waves.
+    float* ttmp = S.tile_tmp + (size_t)b * NT * TT_STRIDE;
+    const int nG = role ? (4 * NT + 63) & ~63 : (S_ * NT + 63) & ~63;
+    const int nR = role ? 15 * NT : NT;
+    MFOR(u, nG + nR) {
+      int it, t;
+      if (u < nG) {
+        const int nit = role ? 4 : S_;
+        if (u >= nit * NT) continue;
+        it = (role ? 0 : 4) + u / NT; t = u - (u / NT) * NT;
+      } else {
+        const int v = u - nG, kk = v / NT;
+        t = v - kk * NT;
+        it = role ? (kk < 10 ? 4 + S_ + kk : 15 + S_ + (kk - 10)) : 14 + S_;
       }
-      if (v >= nit * NT) continue;
-      const int it = it0 + v / NT, t = v - (v / NT) * NT;
       const int th = t / wt, tw = t - (t / wt) * wt;
       const int h0 = th * T, w0 = tw * T;
       float val;
@@ -1126,11 +1146,22 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, Planes& pl,
           val = (float)cnt;
         }
       }
-      tiles[t * TILE_FLOATS + T_TMP + it] = val;
+      ttmp[t * TT_STRIDE + it] = val;
     }
     MSYNC();
 
-    // -- per-tile descriptors phi1..phi5 + interactions
+  }
+  MSTAMP(9);
+}
+
+// phi1..phi5 + interactions from the per-tile partial quantities in
+// tiles[T_TMP..] (pass B; morphology.py:576-739, :860-864)
+MCAQ_HD void assemble_phi(const Ctx& ctx, const MorphScale& S, int b, float* tiles) {
+  const int T = S.tile, NT = S.ht * S.wt;
+  const float fT2 = (float)(T * T);
+  int S_ = 0;
+  for (int s = 2; s <= T; s *= 2) ++S_;
+  {
     const int ycut = aten_tail_start(S.batch_total * NT);
     float xs[8], ws[8];
 #pragma unroll
@@ -1195,7 +1226,6 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, Planes& pl,
     }
     MSYNC();
   }
-  MSTAMP(9);
 }
 
 // ---- pass B: per-image tile work (one 256-thread workgroup per image):
@@ -1212,8 +1242,21 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh)
   float* wbuf = (float*)((char*)extra + extra_bytes(S.H, S.W, NT));
   const float* Pc = S.cmlp;
   const float* Pmap = S.mapper;
+  MSTAMP_INIT(b == 0 ? 0 : -1);
   MSTAMP(10);
-  if (S.flags & F_CMLP) {
+  if (S.flags & F_PHI) {
+    // partial quantities of the edge and mask workgroups -> phi
+    int S_ = 0;
+    for (int s = 2; s <= S.tile; s *= 2) ++S_;
+    const int NI = 20 + S_;
+    const float* ttmp = S.tile_tmp + (size_t)b * NT * TT_STRIDE;
+    MFOR(u, NT * NI) {
+      const int t = u / NI, it = u - (u / NI) * NI;
+      tiles[t * TILE_FLOATS + T_TMP + it] = ttmp[t * TT_STRIDE + it];
+    }
+    MSYNC();
+    assemble_phi(ctx, S, b, tiles);
+  } else if (S.flags & F_CMLP) {
     MFOR(u, NT * 8) tiles[(u >> 3) * TILE_FLOATS + T_PHI + (u & 7)] = S.phi_out[(size_t)b * NT * 8 + u];
     MSYNC();
   }

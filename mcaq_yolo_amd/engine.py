@@ -88,7 +88,8 @@ class HookPlan:
             nb["bits"] = torch.empty(g.B, g.ht, g.wt, device=d)
             nb["m"] = torch.empty(g.B, 1, g.H, g.W, device=d)
             nb["y"] = torch.empty(g.B, g.C, g.H, g.W, device=d)
-            nb["phi"] = torch.empty(g.B, g.ht, g.wt, 8, device=d)   # pass A -> pass B of mcaq_morph
+            nb["phi"] = torch.empty(g.B, g.ht, g.wt, 8, device=d)
+            nb["tile_tmp"] = torch.empty(g.B, g.ht * g.wt, 32, device=d)   # pass A -> pass B of mcaq_morph
             nb["cmlp"] = torch.empty(g.B, g.ht, g.wt, device=d) if "cmlp" in want else None
             if "debug" in want:
                 nb["edge"] = torch.empty(g.B, g.Hc, g.Wc, device=d, dtype=torch.uint8)
@@ -183,6 +184,7 @@ class HookPlan:
             s.m_out = _p(b["m"]) if (with_mask[i] and quantize) else None
             s.edge_out, s.bin_out = _p(b["edge"]), _p(b["binmask"])
             s.gscratch = _p(b["gscratch"])
+            s.tile_tmp = _p(b["tile_tmp"])
             s.B, s.H, s.W, s.Hc, s.Wc = g.B, g.H, g.W, g.Hc, g.Wc
             s.tile, s.ht, s.wt = g.tile, g.ht, g.wt
             s.batch_offset = batch_offset

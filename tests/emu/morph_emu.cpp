@@ -16,10 +16,12 @@ extern "C" int emu_morph(const mcaq_morph_scale* s) {
   for (int b = 0; b < s->B; ++b) {
     Ctx ctx{0, 1};
     if (s->flags & F_PHI) {
-      Planes pl; Shared sh;
-      carve_planes(planes.data(), s->Hc, s->Wc, pl);
-      carve_shared(shm.data(), sh);
-      morph_edges(ctx, *s, b, pl, sh);
+      for (int role = 0; role < 2; ++role) {   // edge and mask workgroups
+        Planes pl; Shared sh;
+        carve_planes(planes.data(), s->Hc, s->Wc, pl);
+        carve_shared(shm.data(), sh);
+        morph_edges(ctx, *s, b, role, pl, sh);
+      }
     }
     Shared sh2;
     carve_shared(tshm.data(), sh2);

@@ -52,6 +52,8 @@ def run_emu(emu, x, grid, flags, T=1.0, c_in=None, bits_in=None):
     s.c_in, s.bits_in = _ptr(c_in), _ptr(bits_in)
     s.phi_out, s.cmlp_out, s.c_out = _ptr(out["phi"]), _ptr(out["cmlp"]), _ptr(out["c"])
     s.bits_out, s.m_out, s.edge_out, s.bin_out = _ptr(out["bits"]), _ptr(out["m"]), _ptr(out["edge"]), _ptr(out["bin"])
+    out["tile_tmp"] = np.zeros((B, ht * wt, 32), f32)
+    s.tile_tmp = _ptr(out["tile_tmp"])
     s.B, s.H, s.W, s.Hc, s.Wc, s.tile, s.ht, s.wt = B, H, Wd, Hc, Wc, tile, ht, wt
     s.batch_offset, s.batch_total = 0, B
     s.flags = flags

@@ -11,10 +11,13 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 from mcaq_yolo_amd import abi  # noqa: E402
 
-# (stamp interval, name): pass A (edges kernel) stamps 0..9, pass B (tiles kernel) 10..15
-STAGES = [(0, "gray+norm"), (1, "blur"), (2, "otsu"), (3, "sobel255+dir"), (4, "nms"), (5, "hysteresis"),
-          (6, "binarize"), (7, "sobel+lbp+planes"), (8, "phi tiles"),
-          (10, "phi load+cmlp"), (11, "bilateral"), (12, "mapper"), (13, "softmask tiles"), (14, "m plane")]
+# (stamp slot, next slot, name): pass A edge workgroup 0..9, mask workgroup 16..25,
+# pass B (tiles kernel) 10..15
+STAGES = [(0, 1, "E gray+norm"), (1, 2, "E blur+hist"), (2, 3, "E otsu"), (3, 4, "E sobel255+dir"),
+          (4, 5, "E nms"), (5, 6, "E hysteresis"), (8, 9, "E tile items"),
+          (16, 17, "M gray+norm"), (17, 23, "M binarize"), (23, 24, "M sobel+lbp+planes"), (24, 25, "M tile items"),
+          (10, 11, "B phi+cmlp"), (11, 12, "B bilateral"), (12, 13, "B mapper"), (13, 14, "B softmask tiles"),
+          (14, 15, "B m plane")]
 
 
 def main():
@@ -38,13 +41,13 @@ def main():
             L.mcaq_morph(ctypes.byref(plan._mo[i]), 1, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
         torch.cuda.synchronize()
         L.mcaq_read_stamps(ctypes.cast(buf, ctypes.c_void_p))
-        st = list(buf[:16])
-        ta, tb = st[9] - st[0], st[15] - st[10]
-        print("scale %d (%dx%d, C=%d): pass A %d ticks, pass B %d ticks"
-              % (i, bench.SIZES[i][0], bench.SIZES[i][1], chans[i], ta, tb))
-        for k, name in STAGES:
-            d = st[k + 1] - st[k]
-            print("   %-18s %8d  %5.1f%%" % (name, d, 100.0 * d / max(ta if k < 9 else tb, 1)))
+        st = list(buf[:32])
+        ta, tm, tb = st[9] - st[0], st[25] - st[16], st[15] - st[10]
+        print("scale %d (%dx%d, C=%d): pass A edge %d / mask %d ticks, pass B %d ticks"
+              % (i, bench.SIZES[i][0], bench.SIZES[i][1], chans[i], ta, tm, tb))
+        for k, k2, name in STAGES:
+            d = st[k2] - st[k]
+            print("   %-20s %8d" % (name, d))
 
 
 if __name__ == "__main__":
