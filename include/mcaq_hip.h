@@ -99,7 +99,8 @@ typedef struct {
   float* cmlp_out;
   float* c_out;
   float* bits_out;
-  float* m_out;
+  float* m_out;      /* (B, H, W) m plane, or NULL */
+  float* mt_out;     /* (B, ht, wt) soft-mask tile values m(tile), or NULL */
   uint8_t* edge_out;
   uint8_t* bin_out;
   float* gscratch;   /* mcaq_morph_scratch_bytes() bytes, or NULL when 0 */
@@ -125,6 +126,10 @@ typedef struct {
   float* y;            /* (B, C, H, W) */
   const float* bits;   /* (B, ht, wt) integer-valued */
   const float* m;      /* (B, H, W) or NULL */
+  const float* mt;     /* (B, ht, wt) soft-mask tile values: when set, m(p) is
+                          generated per pixel (nearest upsample + 5x5 Gaussian,
+                          replicate pad, quantization.py:235-238) and m is
+                          ignored */
   const float* xmin;   /* (C) */
   const float* xmax;   /* (C) */
   int B, C, H, W, ht, wt;

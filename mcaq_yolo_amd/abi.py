@@ -29,14 +29,14 @@ class FinalizeScale(ctypes.Structure):
 class MorphScale(ctypes.Structure):
     _fields_ = [("gray", P), ("absmean", P), ("cmlp", P), ("mapper", P), ("smask", P),
                 ("c_in", P), ("bits_in", P), ("phi_out", P), ("cmlp_out", P), ("c_out", P),
-                ("bits_out", P), ("m_out", P), ("edge_out", P), ("bin_out", P), ("gscratch", P), ("tile_tmp", P),
+                ("bits_out", P), ("m_out", P), ("mt_out", P), ("edge_out", P), ("bin_out", P), ("gscratch", P), ("tile_tmp", P),
                 ("B", I), ("H", I), ("W", I), ("Hc", I), ("Wc", I), ("tile", I), ("ht", I), ("wt", I),
                 ("batch_offset", I), ("batch_total", I), ("flags", I), ("hyst_iters", I),
                 ("temperature", Fl), ("min_bits", Fl), ("max_bits", Fl), ("block_begin", I)]
 
 
 class QuantScale(ctypes.Structure):
-    _fields_ = [("x", P), ("y", P), ("bits", P), ("m", P), ("xmin", P), ("xmax", P),
+    _fields_ = [("x", P), ("y", P), ("bits", P), ("m", P), ("mt", P), ("xmin", P), ("xmax", P),
                 ("B", I), ("C", I), ("H", I), ("W", I), ("ht", I), ("wt", I),
                 ("bits_lo", I), ("nbits", I), ("compat_tile_h", I), ("compat_tile_w", I), ("unit_begin", I)]
 

@@ -409,7 +409,7 @@ class LearnedSoftMask(nn.Module):
     def blob(self):
         return self._blob.get(list(self.net.parameters()), lambda: _pack_softmask(self.net))
 
-    def forward(self, bit_map: torch.Tensor, x: torch.Tensor, absmean: Optional[torch.Tensor] = None):
+    def _run(self, bit_map, x, absmean, plane):
         _need_cuda(bit_map, "bit_map")
         _need_cuda(x, "x")
         B, C, H, W = x.shape
@@ -422,13 +422,22 @@ class LearnedSoftMask(nn.Module):
             # the launcher's geometry check wants >= 4 pixels per tile (every
             # hook tile grid has them: tile = pow2floor(max(4, H // grid)))
             raise NotImplementedError("soft mask on a tile grid finer than 4 pixels per tile")
-        m = torch.empty(B, 1, H, W, device=x.device)
+        out = torch.empty(B, 1, H, W, device=x.device) if plane else torch.empty(B, ht, wt, device=x.device)
         # tile / crop fields only satisfy the launcher: the soft-mask stage
         # pools and upsamples over (H, W) like adaptive_avg_pool2d / nearest
-        s = _morph_struct(B, H, W, 4, ht, wt, abi.F_SOFTMASK, absmean=absmean, bits_in=bits,
-                          smask=self.blob(), m_out=m)
+        ptrs = dict(absmean=absmean, bits_in=bits, smask=self.blob())
+        ptrs["m_out" if plane else "mt_out"] = out
+        s = _morph_struct(B, H, W, 4, ht, wt, abi.F_SOFTMASK, **ptrs)
         abi.check(abi.lib().mcaq_morph(ctypes.byref(s), 1, _stream()), "mcaq_morph(soft mask)")
-        return m
+        return out
+
+    def forward(self, bit_map: torch.Tensor, x: torch.Tensor, absmean: Optional[torch.Tensor] = None):
+        return self._run(bit_map, x, absmean, plane=True)
+
+    def tile_values(self, bit_map, x, absmean=None):
+        """m per tile before upsampling/smoothing (B, Ht, Wt); the quant pass
+        turns it into m(p) on the fly."""
+        return self._run(bit_map, x, absmean, plane=False)
 
 
 class SpatialAdaptiveQuantization(nn.Module):
@@ -524,10 +533,10 @@ class SpatialAdaptiveQuantization(nn.Module):
                 _run_stats(xf, absmean=absmean)
         else:
             xmin, xmax = self.batch_minmax(xf, absmean)
-        m = self.soft_mask(bits, xf, absmean=absmean) if want_m else None
+        mt = self.soft_mask.tile_values(bits, xf, absmean=absmean) if want_m else None
         y = torch.empty_like(xf)
         q = abi.QuantScale()
-        q.x, q.y, q.bits, q.m, q.xmin, q.xmax = _p(xf), _p(y), _p(bits), _p(m), _p(xmin), _p(xmax)
+        q.x, q.y, q.bits, q.mt, q.xmin, q.xmax = _p(xf), _p(y), _p(bits), _p(mt), _p(xmin), _p(xmax)
         q.B, q.C, q.H, q.W, q.ht, q.wt = B, C, H, W, ht, wt
         q.bits_lo, q.nbits = 2, 7
         abi.check(abi.lib().mcaq_quant(ctypes.byref(q), 1, _stream()), "mcaq_quant")

@@ -430,7 +430,7 @@ __global__ __launch_bounds__(MORPH_THREADS) void mcaq_morph_kernel(MorphArgs a, 
   morph_edges(ctx, S, b, role, pl, sh);
 }
 
-__global__ __launch_bounds__(TILES_THREADS) void mcaq_tiles_kernel(MorphArgs a) {
+__global__ __launch_bounds__(TILES_THREADS) void mcaq_tiles_kernel(MorphArgs a, int wlds) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const MorphScale& S = a.s[morph_scale_of(a, (int)blockIdx.x)];
   const int b = (int)blockIdx.x - S.block_begin;
@@ -438,7 +438,7 @@ __global__ __launch_bounds__(TILES_THREADS) void mcaq_tiles_kernel(MorphArgs a) 
   Ctx ctx{(int)threadIdx.x, (int)blockDim.x};
   Shared sh;
   carve_shared(smem, sh);
-  morph_tiles(ctx, S, b, sh);
+  morph_tiles(ctx, S, b, sh, wlds);
 }
 
 // ---------------------------------------------------------------------------
@@ -453,6 +453,7 @@ struct QuantArgs {
 constexpr int QSLICE = 32;     // channels per unit (8 per wave)
 constexpr int QCW = 8;         // channels per wave
 constexpr int QMAXBITS = 15;   // max entries per channel in the LDS table
+constexpr int QMAXNT = 1024;   // max tiles per image for on-the-fly m(p)
 
 // unit = 256 pixels x 32 channels of one image; lane l of every wave owns
 // pixels 4l..4l+3 (16-byte accesses), wave w channels 8w..8w+7 of the slice,
@@ -463,6 +464,8 @@ constexpr int QMAXBITS = 15;   // max entries per channel in the LDS table
 template <bool kVec>
 __global__ __launch_bounds__(256) void mcaq_quant_kernel(QuantArgs a) {
   __shared__ float2 qt[QSLICE * QMAXBITS];
+  __shared__ float mts[QMAXNT];
+  __shared__ float mq[256];
   const int unit = blockIdx.x;
   int si = 0;
   while (si + 1 < a.nscales && unit >= a.s[si + 1].unit_begin) ++si;
@@ -483,6 +486,9 @@ __global__ __launch_bounds__(256) void mcaq_quant_kernel(QuantArgs a) {
     const QParam q = qparam(S.xmin[c0 + c], S.xmax[c0 + c], S.bits_lo + k);
     qt[i] = make_float2(q.scale, q.zp);
   }
+  const int NTq = S.ht * S.wt;
+  if (S.mt)
+    for (int i = tid; i < NTq; i += 256) mts[i] = S.mt[(size_t)b * NTq + i];
 
   const int q0 = chunk * 256 + lane * 4;
   bool pv[4];
@@ -503,9 +509,9 @@ __global__ __launch_bounds__(256) void mcaq_quant_kernel(QuantArgs a) {
     }
     const float bv = S.bits[((size_t)b * S.ht + th) * S.wt + tw];
     kb[k] = imin_(imax_((int)rintf(bv), S.bits_lo), S.bits_lo + NB - 1) - S.bits_lo;
-    mv[k] = S.m ? S.m[(size_t)b * HW + p] : 1.0f;
+    mv[k] = (S.m && !S.mt) ? S.m[(size_t)b * HW + p] : 1.0f;
   }
-  const bool has_m = S.m != nullptr;
+  const bool has_m = S.m != nullptr || S.mt != nullptr;
   float qlo[4], qhi[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
@@ -533,7 +539,31 @@ __global__ __launch_bounds__(256) void mcaq_quant_kernel(QuantArgs a) {
       }
     }
   }
-  __syncthreads();   // qt ready
+  __syncthreads();   // qt, mts ready
+  if (S.mt) {
+    // m(p) = 5x5 Gaussian (replicate pad) of the nearest-upsampled tile values,
+    // taps row-major from 0 - the m plane LearnedSoftMask produces
+    // (quantization.py:235-238), generated here instead of read from HBM.
+    // Wave w computes pixel w of every lane's quad; the quads meet in LDS.
+    {
+      const int p = imin_(q0 + wv, HW - 1);
+      const int h = p / S.W, w = p - (p / S.W) * S.W;
+      int cs[5];
+#pragma unroll
+      for (int j = 0; j < 5; ++j) cs[j] = nearest_src(imin_(imax_(w + j - 2, 0), S.W - 1), S.wt, S.W);
+      float acc = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        const int rb = nearest_src(imin_(imax_(h + i - 2, 0), S.H - 1), S.ht, S.H) * S.wt;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) acc = fmaf(bits_as_float(k_smooth5_bits[i * 5 + j]), mts[rb + cs[j]], acc);
+      }
+      mq[lane * 4 + wv] = acc;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) mv[k] = mq[lane * 4 + k];
+  }
   if (ncw <= 0) return;
 #pragma unroll
   for (int c = 0; c < QCW; ++c) {
@@ -743,6 +773,9 @@ int mcaq_morph_finalize(const mcaq_morph_scale* scales, int nscales, const mcaq_
   }
   if (any_tiles) {
     if (tlds > MCAQ_MORPH_LDS_LIMIT - 1024) return (int)hipErrorInvalidValue;
+    // stage the weight blobs in LDS when they fit beside the tile arrays
+    const int wlds = tlds + weights_lds_bytes() + 64 <= MCAQ_MORPH_LDS_LIMIT - 1024;
+    if (wlds) tlds += weights_lds_bytes() + 64;
     static int set_tiles = 0;
     if (tlds > set_tiles) {
       hipError_t ae = hipFuncSetAttribute((const void*)mcaq_tiles_kernel,
@@ -750,7 +783,7 @@ int mcaq_morph_finalize(const mcaq_morph_scale* scales, int nscales, const mcaq_
       if (ae != hipSuccess) return (int)ae;
       set_tiles = MCAQ_MORPH_LDS_LIMIT - 1024;
     }
-    hipLaunchKernelGGL(mcaq_tiles_kernel, dim3(blocks), dim3(TILES_THREADS), (size_t)tlds, stream, a);
+    hipLaunchKernelGGL(mcaq_tiles_kernel, dim3(blocks), dim3(TILES_THREADS), (size_t)tlds, stream, a, wlds);
   }
   return (int)hipGetLastError();
 }
@@ -766,7 +799,7 @@ int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream) 
     if (scales[i].nbits < 1 || scales[i].nbits > QMAXBITS || scales[i].bits_lo < 1 ||
         scales[i].bits_lo + scales[i].nbits - 1 > 16 || HW < 1 || scales[i].C < 1 ||
         scales[i].ht < 1 || scales[i].wt < 1 || !scales[i].x || !scales[i].y || !scales[i].bits ||
-        !scales[i].xmin || !scales[i].xmax)
+        !scales[i].xmin || !scales[i].xmax || (scales[i].mt && scales[i].ht * scales[i].wt > QMAXNT))
       return (int)hipErrorInvalidValue;
     units += scales[i].B * ((HW + 255) / 256) * ((scales[i].C + QSLICE - 1) / QSLICE);
   }

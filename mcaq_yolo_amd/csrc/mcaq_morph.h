@@ -1228,37 +1228,109 @@ MCAQ_HD void assemble_phi(const Ctx& ctx, const MorphScale& S, int b, float* til
   }
 }
 
+// batched copy of n values: every thread issues up to K loads before its
+// first store (a runtime-trip-count loop would pay one memory latency per
+// iteration); fs(u) loads item u, fd(u, v) stores it
+template <int K, class FS, class FD>
+MCAQ_HD void bcopy(const Ctx& ctx, int n, FS fs, FD fd) {
+  if (n <= K * ctx.nthr) {
+    float v[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) { const int u = ctx.tid + i * ctx.nthr; v[i] = u < n ? fs(u) : 0.0f; }
+#pragma unroll
+    for (int i = 0; i < K; ++i) { const int u = ctx.tid + i * ctx.nthr; if (u < n) fd(u, v[i]); }
+  } else {
+    MFOR(u, n) fd(u, fs(u));
+  }
+}
+
+// weight blobs staged in the tile kernel's LDS (float offsets, 16-B aligned)
+enum : int {
+  WL_CM = 0,
+  WL_MM = (CM_BLOB + 3) & ~3,
+  WL_SM = WL_MM + ((MM_BLOB + 3) & ~3),
+  WL_FLOATS = WL_SM + ((SM_SIZE + 3) & ~3),
+};
+MCAQ_HD int weights_lds_bytes() { return 4 * WL_FLOATS; }
+
+MCAQ_HD void stage_blob(const Ctx& ctx, float* dst, const float* src, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int n4 = n >> 2;
+  const float4* s4 = reinterpret_cast<const float4*>(src);
+  float4* d4 = reinterpret_cast<float4*>(dst);
+  constexpr int K = 12;
+  for (int base = 0; base < n4; base += K * ctx.nthr) {
+    float4 v[K];
+#pragma unroll
+    for (int i = 0; i < K; ++i) { const int u = base + ctx.tid + i * ctx.nthr; v[i] = s4[u < n4 ? u : 0]; }
+#pragma unroll
+    for (int i = 0; i < K; ++i) { const int u = base + ctx.tid + i * ctx.nthr; if (u < n4) d4[u] = v[i]; }
+  }
+  for (int u = 4 * n4 + ctx.tid; u < n; u += ctx.nthr) dst[u] = src[u];
+#else
+  MFOR(u, n) dst[u] = src[u];
+#endif
+}
+
+// sequential row-major sum of a K x K window of a global plane (adaptive_avg_pool
+// order), all loads issued together
+template <int K>
+MCAQ_HD float window_sum_t(const float* a, int W, int h0, int w0) {
+  float v[K * K];
+#pragma unroll
+  for (int y = 0; y < K; ++y)
+#pragma unroll
+    for (int x = 0; x < K; ++x) v[y * K + x] = a[(h0 + y) * W + w0 + x];
+  float s = 0.0f;
+#pragma unroll
+  for (int i = 0; i < K * K; ++i) s = s + v[i];
+  return s;
+}
+
 // ---- pass B: per-image tile work (one 256-thread workgroup per image):
-// complexity MLP, bilateral, normalisation, bit mapper, soft mask, m plane.
-// LDS: Shared (fixed + tiles) | extra | bilateral weights (25 NT floats).
+// phi assembly, complexity MLP, bilateral, normalisation, bit mapper, soft
+// mask (tile values; the m plane itself only on request).
+// LDS: Shared (fixed + tiles) | extra | bilateral weights (25 NT floats) |
+// staged weight blobs (when `wlds`).
 MCAQ_HD int tiles_lds_bytes(int H, int W, int NT) {
   return fixed_bytes() + tile_bytes(NT) + extra_bytes(H, W, NT) + 100 * NT;
 }
 
-MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh) {
+MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh, int wlds) {
   const int ht = S.ht, wt = S.wt, NT = ht * wt;
   float* tiles = sh.tiles;
   float* extra = tiles + NT * TILE_FLOATS;            // compact per-tile arrays / tables
   float* wbuf = (float*)((char*)extra + extra_bytes(S.H, S.W, NT));
+  float* wl = wbuf + ((25 * NT + 3) & ~3);            // staged weights (wlds)
   const float* Pc = S.cmlp;
   const float* Pmap = S.mapper;
+  const float* Pm = S.smask;
   MSTAMP_INIT(b == 0 ? 0 : -1);
   MSTAMP(10);
+  // stage the weight blobs this launch needs in LDS (one round trip; the MLP
+  // and conv loops then read LDS instead of L2)
+  if (wlds) {
+    if (S.flags & F_CMLP) { stage_blob(ctx, wl + WL_CM, S.cmlp, CM_BLOB); Pc = wl + WL_CM; }
+    if ((S.flags & F_MAPPER) && !(S.flags & F_MAP_LINEAR)) { stage_blob(ctx, wl + WL_MM, S.mapper, MM_BLOB); Pmap = wl + WL_MM; }
+    if (S.flags & F_SOFTMASK) { stage_blob(ctx, wl + WL_SM, S.smask, SM_SIZE); Pm = wl + WL_SM; }
+  }
   if (S.flags & F_PHI) {
     // partial quantities of the edge and mask workgroups -> phi
     int S_ = 0;
     for (int s = 2; s <= S.tile; s *= 2) ++S_;
     const int NI = 20 + S_;
     const float* ttmp = S.tile_tmp + (size_t)b * NT * TT_STRIDE;
-    MFOR(u, NT * NI) {
-      const int t = u / NI, it = u - (u / NI) * NI;
-      tiles[t * TILE_FLOATS + T_TMP + it] = ttmp[t * TT_STRIDE + it];
-    }
+    bcopy<16>(ctx, NT * NI,
+              [&](int u) { const int t = u / NI; return ttmp[t * TT_STRIDE + (u - t * NI)]; },
+              [&](int u, float v) { const int t = u / NI; tiles[t * TILE_FLOATS + T_TMP + (u - t * NI)] = v; });
     MSYNC();
     assemble_phi(ctx, S, b, tiles);
   } else if (S.flags & F_CMLP) {
-    MFOR(u, NT * 8) tiles[(u >> 3) * TILE_FLOATS + T_PHI + (u & 7)] = S.phi_out[(size_t)b * NT * 8 + u];
+    bcopy<16>(ctx, NT * 8, [&](int u) { return S.phi_out[(size_t)b * NT * 8 + u]; },
+              [&](int u, float v) { tiles[(u >> 3) * TILE_FLOATS + T_PHI + (u & 7)] = v; });
     MSYNC();
+  } else {
+    MSYNC();   // staged weights visible
   }
 
   // -- complexity MLP + bilateral (morphology.py:959-968)
@@ -1281,39 +1353,46 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh)
     }
     MSYNC();
     MSTAMP(11);
-    // range weights w = spatial * exp(-(d^2)/0.02), one thread per (tile, tap)
+    // range weights w = spatial * exp(-(d^2)/0.02), one thread per (tile, tap),
+    // up to BK items per thread with their exps in flight together
     {
-      MFOR(u, NT * 25) {
+      constexpr int BK = 12;
+      auto wgt = [&](int u) {
         const int t = u / 25, k = u - (u / 25) * 25;
         const int th = t / wt, tw = t - (t / wt) * wt;
         const int hh = imin_(imax_(th + k / 5 - 2, 0), ht - 1);
         const int ww = imin_(imax_(tw + k % 5 - 2, 0), wt - 1);
         const float d = extra[hh * wt + ww] - extra[t];
-        wbuf[u] = bits_as_float(k_bilat_sp_bits[k]) * cr_exp((-(d * d)) / 0.02f);
-      }
+        return bits_as_float(k_bilat_sp_bits[k]) * cr_exp((-(d * d)) / 0.02f);
+      };
+      bcopy<BK>(ctx, NT * 25, wgt, [&](int u, float v) { wbuf[u] = v; });
       MSYNC();
     }
     const int cut = aten_tail_start(NT);
     MFOR(t, NT) {
       const int th = t / wt, tw = t - (t / wt) * wt;
-      const float ctr = extra[t];
       // 25-row ATen outer sums of w*p and w: vector column = rows 0..15 folded,
       // then 16..24 in a0; tail column = 4 interleaved partials (rows 4i+q),
       // row 24 into partial 0.  Adding an exact +0 is an identity (sums never
       // hold -0), so both orders are accumulated with selects in one loop.
       const bool tail = t >= cut;
-      float n0 = 0.0f, n1 = 0.0f, n2 = 0.0f, n3 = 0.0f, d0 = 0.0f, d1 = 0.0f, d2 = 0.0f, d3 = 0.0f;
+      float pv[25], wv[25];
+#pragma unroll
       for (int k = 0; k < 25; ++k) {
         const int hh = imin_(imax_(th + k / 5 - 2, 0), ht - 1);
         const int ww = imin_(imax_(tw + k % 5 - 2, 0), wt - 1);
-        const float pv = extra[hh * wt + ww];
-        const float wv = wbuf[t * 25 + k];
-        const float wp = wv * pv;
+        pv[k] = extra[hh * wt + ww];
+        wv[k] = wbuf[t * 25 + k];
+      }
+      float n0 = 0.0f, n1 = 0.0f, n2 = 0.0f, n3 = 0.0f, d0 = 0.0f, d1 = 0.0f, d2 = 0.0f, d3 = 0.0f;
+#pragma unroll
+      for (int k = 0; k < 25; ++k) {
+        const float wp = wv[k] * pv[k];
         const int q = tail ? (k < 24 ? (k & 3) : 0) : (k < 16 ? 1 : 0);
-        n0 = n0 + (q == 0 ? wp : 0.0f); d0 = d0 + (q == 0 ? wv : 0.0f);
-        n1 = n1 + (q == 1 ? wp : 0.0f); d1 = d1 + (q == 1 ? wv : 0.0f);
-        n2 = n2 + (q == 2 ? wp : 0.0f); d2 = d2 + (q == 2 ? wv : 0.0f);
-        n3 = n3 + (q == 3 ? wp : 0.0f); d3 = d3 + (q == 3 ? wv : 0.0f);
+        n0 = n0 + (q == 0 ? wp : 0.0f); d0 = d0 + (q == 0 ? wv[k] : 0.0f);
+        n1 = n1 + (q == 1 ? wp : 0.0f); d1 = d1 + (q == 1 ? wv[k] : 0.0f);
+        n2 = n2 + (q == 2 ? wp : 0.0f); d2 = d2 + (q == 2 ? wv[k] : 0.0f);
+        n3 = n3 + (q == 3 ? wp : 0.0f); d3 = d3 + (q == 3 ? wv[k] : 0.0f);
       }
       float num, dsum;
       if (tail) { num = ((n0 + n1) + n2) + n3; dsum = ((d0 + d1) + d2) + d3; }
@@ -1324,7 +1403,8 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh)
     }
     MSYNC();
   } else if (S.c_in) {
-    MFOR(t, NT) tiles[t * TILE_FLOATS + T_C] = S.c_in[(size_t)b * NT + t];
+    bcopy<16>(ctx, NT, [&](int u) { return S.c_in[(size_t)b * NT + u]; },
+              [&](int u, float v) { tiles[u * TILE_FLOATS + T_C] = v; });
     MSYNC();
   }
   MSTAMP(12);
@@ -1388,7 +1468,8 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh)
     }
     MSYNC();
   } else if ((S.flags & F_SOFTMASK) && S.bits_in) {
-    MFOR(t, NT) tiles[t * TILE_FLOATS + T_BITS] = S.bits_in[(size_t)b * NT + t];
+    bcopy<16>(ctx, NT, [&](int u) { return S.bits_in[(size_t)b * NT + u]; },
+              [&](int u, float v) { tiles[u * TILE_FLOATS + T_BITS] = v; });
     MSYNC();
   }
   MSTAMP(13);
@@ -1398,19 +1479,26 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh)
     const int H = S.H, W = S.W;
     const float* am = S.absmean + (size_t)b * H * W;
     float lmx = -3.402823466e38f;
+    // per-tile mean |x| activation (adaptive_avg_pool2d windows)
+    const int KH = H / ht, KW = W / wt;
+    const bool even = KH * ht == H && KW * wt == W && KH == KW;
     MFOR(t, NT) {
       const int i = t / wt, j = t - (t / wt) * wt;
-      const int ha = (i * H) / ht, hb = ((i + 1) * H + ht - 1) / ht;
-      const int wa = (j * W) / wt, wb = ((j + 1) * W + wt - 1) / wt;
-      float s = 0.0f;
-      for (int h = ha; h < hb; ++h)
-        for (int w = wa; w < wb; ++w) s = s + am[h * W + w];
-      const float a = (s / (float)(hb - ha)) / (float)(wb - wa);
+      float a;
+      if (even && KH == 4) a = (window_sum_t<4>(am, W, i * 4, j * 4) / 4.0f) / 4.0f;
+      else if (even && KH == 8) a = (window_sum_t<8>(am, W, i * 8, j * 8) / 8.0f) / 8.0f;
+      else {
+        const int ha = (i * H) / ht, hb = ((i + 1) * H + ht - 1) / ht;
+        const int wa = (j * W) / wt, wb = ((j + 1) * W + wt - 1) / wt;
+        float s = 0.0f;
+        for (int h = ha; h < hb; ++h)
+          for (int w = wa; w < wb; ++w) s = s + am[h * W + w];
+        a = (s / (float)(hb - ha)) / (float)(wb - wa);
+      }
       tiles[t * TILE_FLOATS + T_ACT] = a;
       lmx = fmax_(lmx, a);
     }
     const float amax = block_max(ctx, sh, lmx);
-    const float* Pm = S.smask;
     const float den = amax + 1e-8f;
     // the two conv input features, compact: f0 = bits feature, f1 = activation
     float* f0a = extra;
@@ -1422,22 +1510,28 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh)
     MSYNC();
     MFOR(t, NT) {
       const int i = t / wt, j = t - (t / wt) * wt;
+      // 3x3 window (zero pad): (kh, kw) outer, ic inner, FMA from 0, + bias;
+      // out-of-grid taps are skipped exactly as the reference's zero taps
+      float f0[9], f1[9];
+      bool ok[9];
+#pragma unroll
+      for (int q = 0; q < 9; ++q) {
+        const int ii = i + q / 3 - 1, jj = j + q % 3 - 1;
+        ok[q] = ii >= 0 && ii < ht && jj >= 0 && jj < wt;
+        const int src = imin_(imax_(ii, 0), ht - 1) * wt + imin_(imax_(jj, 0), wt - 1);
+        f0[q] = f0a[src]; f1[q] = f1a[src];
+      }
       float hid[8];
 #pragma unroll
-      for (int oc = 0; oc < 8; ++oc) hid[oc] = 0.0f;
-      for (int ki = 0; ki < 3; ++ki) {
-        const int ii = i + ki - 1;
-        if (ii < 0 || ii >= ht) continue;
-        for (int kj = 0; kj < 3; ++kj) {
-          const int jj = j + kj - 1;
-          if (jj < 0 || jj >= wt) continue;
-          const float f0 = f0a[ii * wt + jj], f1 = f1a[ii * wt + jj];
+      for (int oc = 0; oc < 8; ++oc) {
+        float acc = 0.0f;
 #pragma unroll
-          for (int oc = 0; oc < 8; ++oc) {
-            hid[oc] = fmaf(Pm[SM_W1 + ((oc * 2 + 0) * 3 + ki) * 3 + kj], f0, hid[oc]);
-            hid[oc] = fmaf(Pm[SM_W1 + ((oc * 2 + 1) * 3 + ki) * 3 + kj], f1, hid[oc]);
-          }
+        for (int q = 0; q < 9; ++q) {
+          const float a0 = fmaf(Pm[SM_W1 + (oc * 2 + 0) * 9 + q], f0[q], acc);
+          const float a1 = fmaf(Pm[SM_W1 + (oc * 2 + 1) * 9 + q], f1[q], a0);
+          acc = ok[q] ? a1 : acc;
         }
+        hid[oc] = acc;
       }
       float l0 = Pm[SM_B2 + 0], l1 = Pm[SM_B2 + 1];
 #pragma unroll
@@ -1448,7 +1542,9 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh)
       }
       const float mxl = fmax_(l0, l1);
       const float e0 = cr_exp(l0 - mxl), e1 = cr_exp(l1 - mxl);
-      tiles[t * TILE_FLOATS + T_MT] = e0 / (e0 + e1);
+      const float mtv = e0 / (e0 + e1);
+      tiles[t * TILE_FLOATS + T_MT] = mtv;
+      if (S.mt_out) S.mt_out[(size_t)b * NT + t] = mtv;
     }
     MSYNC();
     MSTAMP(14);

@@ -86,7 +86,8 @@ class HookPlan:
             nb["xmax"] = torch.empty(g.C, device=d)
             nb["complexity"] = torch.empty(g.B, g.ht, g.wt, device=d)
             nb["bits"] = torch.empty(g.B, g.ht, g.wt, device=d)
-            nb["m"] = torch.empty(g.B, 1, g.H, g.W, device=d)
+            nb["mt"] = torch.empty(g.B, g.ht, g.wt, device=d)          # soft-mask tile values
+            nb["m"] = torch.empty(g.B, 1, g.H, g.W, device=d) if "debug" in want else None
             nb["y"] = torch.empty(g.B, g.C, g.H, g.W, device=d)
             nb["phi"] = torch.empty(g.B, g.ht, g.wt, 8, device=d)
             nb["tile_tmp"] = torch.empty(g.B, g.ht * g.wt, 32, device=d)   # pass A -> pass B of mcaq_morph
@@ -182,6 +183,7 @@ class HookPlan:
             s.phi_out, s.cmlp_out = _p(b["phi"]), _p(b["cmlp"])
             s.c_out, s.bits_out = _p(b["complexity"]), _p(b["bits"])
             s.m_out = _p(b["m"]) if (with_mask[i] and quantize) else None
+            s.mt_out = _p(b["mt"]) if (with_mask[i] and quantize) else None
             s.edge_out, s.bin_out = _p(b["edge"]), _p(b["binmask"])
             s.gscratch = _p(b["gscratch"])
             s.tile_tmp = _p(b["tile_tmp"])
@@ -201,7 +203,7 @@ class HookPlan:
             for i, (f, g, b) in enumerate(zip(feats, self.geoms, self.bufs)):
                 s = qs[i]
                 s.x, s.y, s.bits = _p(f), _p(b["y"]), _p(b["bits"])
-                s.m = _p(b["m"]) if with_mask[i] else None
+                s.mt = _p(b["mt"]) if with_mask[i] else None   # m(p) generated in the quant pass
                 s.xmin, s.xmax = _p(b["xmin"]), _p(b["xmax"])
                 s.B, s.C, s.H, s.W, s.ht, s.wt = g.B, g.C, g.H, g.W, g.ht, g.wt
                 s.bits_lo, s.nbits = lo_b, nb
