@@ -1,6 +1,6 @@
 """Benchmark of the MCAQ spatial-adaptive-quantization hook path on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4] [--no-cpu]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4] [--pipeline D] [--no-cpu]
 
 A step = the three backbone hooks (C3/C4/C5) of one batch: channel statistics,
 morphological complexity (phi1..5, MLP, bilateral), bit mapper, soft mask and
@@ -8,6 +8,11 @@ the tile-wise 2..8-bit quant/dequant - every output the reference hook
 produces, computed by the HIP kernels on inputs already resident in HBM.  The
 YOLOv8 host network is not part of the step (not built yet: SURVEY 8f rank 1;
 ultralytics is unavailable) - `config.workload` says so.
+
+Throughput: `--pipeline D` (default 2) independent batches are in flight on D
+HIP streams, so one batch's latency-bound per-image morphology overlaps the
+HBM passes of the next; `value` = images of all K timed steps / wall time.
+`config.latency_ms_single_batch` is one step with nothing beside it.
 
 N > 1: one process per GPU (torch.distributed.run), each rank takes its own
 batch shard (weak scaling); the per-channel batch min/max is made global with
@@ -29,7 +34,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from mcaq_yolo_amd import params  # noqa: E402
-from mcaq_yolo_amd.engine import HookPlan, ScaleGeom  # noqa: E402
+from mcaq_yolo_amd.engine import HookPlan, ScaleGeom, sync_channel_minmax  # noqa: E402
 
 # BASELINE.json configs that fit this harness: name -> (per-GPU batch, channels, grid, mapper)
 CONFIGS = {
@@ -83,12 +88,66 @@ def cpu_baseline(cfg_id, budget_s=12.0):
                       "single-threaded numpy, %.1f s" % (n, name, "x".join(map(str, chans)), dt)}
 
 
+class Runner:
+    """Issues hook-path steps.  `depth` independent HookPlans (own buffers) on
+    `depth` HIP streams: step i runs on plan/stream i % depth, so the per-image
+    morphology of one batch (latency-bound, ~1/3 of the CUs) overlaps the HBM
+    passes of the next.  Each step is one HIP-graph replay (N = 1) or two
+    graph replays around the RCCL min/max all-reduce (N > 1)."""
+
+    def __init__(self, plans, pg, use_graph):
+        self.plans, self.pg = plans, pg
+        self.streams = [torch.cuda.Stream() for _ in plans]
+        self.graphs = [None] * len(plans)
+        self.i = 0
+        if use_graph:
+            torch.cuda.synchronize()
+            for p, (plan, st) in enumerate(zip(plans, self.streams)):
+                with torch.cuda.stream(st):
+                    for _ in range(2):          # warm the launchers outside capture
+                        self._eager(plan, st)
+                st.synchronize()
+                gs = []
+                segs = [lambda pl=plan: pl.launch(torch.cuda.current_stream())] if pg is None else \
+                    [lambda pl=plan: pl.launch_pre(torch.cuda.current_stream()),
+                     lambda pl=plan: pl.launch_quant(torch.cuda.current_stream())]
+                for seg in segs:
+                    g = torch.cuda.CUDAGraph()
+                    with torch.cuda.graph(g, stream=st):
+                        seg()
+                    gs.append(g)
+                self.graphs[p] = gs
+            torch.cuda.synchronize()
+
+    def _eager(self, plan, st):
+        plan.launch(st, self.pg)
+
+    def step(self):
+        p = self.i % len(self.plans)
+        self.i += 1
+        plan, st, gs = self.plans[p], self.streams[p], self.graphs[p]
+        with torch.cuda.stream(st):
+            if gs is None:
+                plan.launch(st, self.pg)
+            elif self.pg is None:
+                gs[0].replay()
+            else:
+                gs[0].replay()
+                sync_channel_minmax(plan.bufs, self.pg)
+                gs[1].replay()
+
+    def sync(self):
+        for st in self.streams:
+            torch.cuda.current_stream().wait_stream(st)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--pipeline", type=int, default=2, help="batches in flight (independent plans/streams)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no HIP graph")
     args = ap.parse_args()
@@ -107,66 +166,77 @@ def main():
         pg = dist.group.WORLD
 
     name, B, chans, grid, mapper = CONFIGS[args.config]
-    feats = [synth_features(B, c, h, w, 1000 * args.config + i + 7919 * rank, dev)
-             for i, (c, (h, w)) in enumerate(zip(chans, SIZES))]
+    depth = max(1, args.pipeline)
     cm, mm, sm = load_blobs(dev)
-    plan = HookPlan([ScaleGeom(B, c, h, w, grid) for c, (h, w) in zip(chans, SIZES)], dev)
-    plan.prepare(feats, cm, mm, [sm, sm, sm], temperature=1.0, mapper_kind=mapper,
-                 batch_offset=rank * B, batch_total=world * B)
-    def step():
-        plan.launch(torch.cuda.current_stream(), pg)   # the capture stream inside graph capture
-
-    use_graph = (world == 1) and not args.eager
-    graph = None
-    for _ in range(max(args.warmup, 1)):
-        step()
+    geoms = [ScaleGeom(B, c, h, w, grid) for c, (h, w) in zip(chans, SIZES)]
+    plans, feats_all = [], []
+    for p in range(depth):
+        # each batch in flight has its own synthetic input (seeded per rank and slot)
+        feats = [synth_features(B, c, h, w, 1000 * args.config + i + 7919 * rank + 104729 * p, dev)
+                 for i, (c, (h, w)) in enumerate(zip(chans, SIZES))]
+        plan = HookPlan(geoms, dev)
+        plan.prepare(feats, cm, mm, [sm, sm, sm], temperature=1.0, mapper_kind=mapper,
+                     batch_offset=rank * B, batch_total=world * B)
+        plans.append(plan)
+        feats_all.append(feats)
     torch.cuda.synchronize()
-    if use_graph:
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            step()
-        for _ in range(3):
-            graph.replay()
-        torch.cuda.synchronize()
-    run = graph.replay if graph is not None else step
 
-    # per-kernel device time (HIP events on the launch stream), untimed pass
+    use_graph = not args.eager
+    runner = Runner(plans, pg, use_graph)
+    for _ in range(max(args.warmup, 1)):
+        runner.step()
+    runner.sync()
+    torch.cuda.synchronize()
+
+    # per-kernel device time: each kernel launched `reps` times back to back
+    # between two HIP events on the launch stream (one plan, no overlap)
+    plan = plans[0]
     L = plan.lib
     stream = torch.cuda.current_stream()
     from mcaq_yolo_amd import abi
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
-    kt = {"stats": 0.0, "morph_finalize": 0.0, "quant": 0.0}
-    reps = 20
+    sh = abi.ctypes.c_void_p(stream.cuda_stream)
     nf = plan._n if plan._fz is not None else 0
-    for _ in range(reps):
-        sh = abi.ctypes.c_void_p(stream.cuda_stream)
-        ev[0].record(stream)
-        L.mcaq_stats(plan._st, plan._n, sh)
-        ev[1].record(stream)
-        L.mcaq_morph_finalize(plan._mo, plan._n, plan._fz, nf, sh)
-        ev[2].record(stream)
-        L.mcaq_quant(plan._qs, plan._n, sh)
-        ev[3].record(stream)
+    launch = {"stats": lambda: L.mcaq_stats(plan._st, plan._n, sh),
+              "morph_finalize": lambda: L.mcaq_morph_finalize(plan._mo, plan._n, plan._fz, nf, sh),
+              "quant": lambda: L.mcaq_quant(plan._qs, plan._n, sh)}
+    kt = {}
+    reps = 20
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    for k, fn in launch.items():
+        fn()
         torch.cuda.synchronize()
-        for i, k in enumerate(kt):
-            kt[k] += ev[i].elapsed_time(ev[i + 1]) * 1e3 / reps   # us
+        e0.record(stream)
+        for _ in range(reps):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        kt[k] = e0.elapsed_time(e1) * 1e3 / reps   # us
+    # single-batch latency: one step at a time, nothing in flight beside it
+    lat = []
+    for _ in range(10):
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        runner.i = 0
+        runner.step()
+        runner.sync()
+        torch.cuda.synchronize()
+        lat.append(time.perf_counter() - t1)
+    latency_ms = sorted(lat)[len(lat) // 2] * 1e3
 
-    # ---- timed region
+    # ---- timed region: K steps, `depth` batches in flight
     if pg is not None:
         import torch.distributed as dist
         dist.barrier()
     torch.cuda.synchronize()
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
+    runner.i = 0
     t0 = time.perf_counter()
-    e0.record(stream)
     for _ in range(args.steps):
-        run()
-    e1.record(stream)
+        runner.step()
+    runner.sync()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    dev_ms = e0.elapsed_time(e1)
-    step_s = max(wall, dev_ms / 1e3) / args.steps
+    step_s = wall / args.steps
     if pg is not None:
         import torch.distributed as dist
         t = torch.tensor([step_s], device=dev, dtype=torch.float64)
@@ -179,6 +249,12 @@ def main():
     achieved = alg_bytes / step_s / 1e9
     value = world * B / step_s
     if rank == 0:
+        kern = {}
+        for k, nbytes in (("stats", 4 * elems), ("quant", 8 * elems)):
+            gbs = nbytes / (kt[k] * 1e-6) / 1e9
+            kern[k] = {"us": round(kt[k], 2), "alg_bytes": nbytes, "GB/s": round(gbs, 1),
+                       "frac": round(gbs / HBM_PEAK_GBS, 4)}
+        kern["morph_finalize"] = {"us": round(kt["morph_finalize"], 2), "bound": "latency (per-image chain)"}
         out = {
             "metric": "images/sec @640x640 end-to-end MCAQ infer, 1/2/4/8 MI355X; % HBM roofline",
             "value": round(value, 2),
@@ -195,12 +271,14 @@ def main():
             "config": {"workload": "%s bs%d/GPU 640x640 MCAQ hook path C3/C4/C5 (grid %d, %s mapper); "
                                    "YOLOv8 network excluded" % (name, B, grid, mapper),
                        "global_batch": world * B, "grid_size": grid, "mapper": mapper,
-                       "parallelism": "dp%d" % world, "hip_graph": graph is not None},
+                       "parallelism": "dp%d" % world, "hip_graph": use_graph,
+                       "batches_in_flight": depth, "latency_ms_single_batch": round(latency_ms, 4)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                         "kernel": "fused hook path (stats+finalize+morph+quant) per step",
+                         "kernel": "hook path step: mcaq_stats + mcaq_morph_kernel/mcaq_tiles_kernel + "
+                                   "mcaq_quant, 12 B per feature element per step",
                          "alg_bytes_per_step": alg_bytes},
-            "kernels_us": {k: round(v, 2) for k, v in kt.items()},
+            "kernels": kern,
             "cpu_baseline": None,
         }
         if not args.no_cpu and world == 1:

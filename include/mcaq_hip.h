@@ -86,7 +86,8 @@ int mcaq_finalize(const mcaq_finalize_scale* scales, int nscales, hipStream_t st
  * flags: 1 phi, 2 complexity MLP + bilateral, 4 mapper, 8 soft mask,
  * 16 continuous bits, 32 temperature given, 64 normalise C, 128 linear mapper,
  * 256 Otsu binarize, 512 no Euler correction.  Parameter blobs are the packed
- * reference state_dict tensors (mcaq_yolo_amd/params.py). */
+ * reference state_dict tensors (mcaq_yolo_amd/params.py), 16-byte aligned and
+ * zero-padded to a multiple of 4 floats (they are staged with 16-byte loads). */
 typedef struct {
   const float* gray;
   const float* absmean;

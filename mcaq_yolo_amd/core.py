@@ -93,6 +93,12 @@ class _BlobCache:
         return self.blob
 
 
+def _pad4(t):
+    """Blobs are read as 16-byte vectors: pad to a multiple of 4 floats."""
+    n = (-t.numel()) % 4
+    return torch.cat([t, t.new_zeros(n)]) if n else t
+
+
 def _pack_cmlp(seq):
     l0, ln1, l3, ln4, l6 = seq[0], seq[1], seq[3], seq[4], seq[6]
     parts = [l0.weight, l0.bias, ln1.weight, ln1.bias, l3.weight, l3.bias, ln4.weight, ln4.bias,
@@ -101,8 +107,8 @@ def _pack_cmlp(seq):
     if flat.numel() != _CM_SIZE:
         raise ValueError("complexity MLP must be the reference Linear(8,64)-LN-ReLU-Linear(64,32)-LN-ReLU-"
                          "Linear(32,1) stack")
-    return torch.cat([flat, _mfma_a_operands(l0.weight.detach().float()),
-                      _mfma_a_operands(l3.weight.detach().float())])
+    return _pad4(torch.cat([flat, _mfma_a_operands(l0.weight.detach().float()),
+                            _mfma_a_operands(l3.weight.detach().float())]))
 
 
 def _pack_mapper(seq):
@@ -114,7 +120,7 @@ def _pack_mapper(seq):
     flat = torch.cat([p.detach().float().reshape(-1) for p in parts])
     if flat.numel() != _MM_SIZE:
         raise ValueError("bit mapper must use hidden_dims [32, 64, 32]")
-    return torch.cat([flat] + [_mfma_a_operands(seq[i].weight.detach().float()) for i in (0, 3, 6)])
+    return _pad4(torch.cat([flat] + [_mfma_a_operands(seq[i].weight.detach().float()) for i in (0, 3, 6)]))
 
 
 def _pack_softmask(seq):
@@ -122,7 +128,7 @@ def _pack_softmask(seq):
     flat = torch.cat([p.detach().float().reshape(-1) for p in parts])
     if flat.numel() != _SM_SIZE:
         raise ValueError("soft mask must be the reference Conv2d(2,8,3)/Conv2d(8,2,1) net")
-    return flat
+    return _pad4(flat)
 
 
 def _morph_struct(B, H, W, tile, ht, wt, flags, **ptrs):

@@ -1253,25 +1253,6 @@ enum : int {
 };
 MCAQ_HD int weights_lds_bytes() { return 4 * WL_FLOATS; }
 
-MCAQ_HD void stage_blob(const Ctx& ctx, float* dst, const float* src, int n) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  const int n4 = n >> 2;
-  const float4* s4 = reinterpret_cast<const float4*>(src);
-  float4* d4 = reinterpret_cast<float4*>(dst);
-  constexpr int K = 12;
-  for (int base = 0; base < n4; base += K * ctx.nthr) {
-    float4 v[K];
-#pragma unroll
-    for (int i = 0; i < K; ++i) { const int u = base + ctx.tid + i * ctx.nthr; v[i] = s4[u < n4 ? u : 0]; }
-#pragma unroll
-    for (int i = 0; i < K; ++i) { const int u = base + ctx.tid + i * ctx.nthr; if (u < n4) d4[u] = v[i]; }
-  }
-  for (int u = 4 * n4 + ctx.tid; u < n; u += ctx.nthr) dst[u] = src[u];
-#else
-  MFOR(u, n) dst[u] = src[u];
-#endif
-}
-
 // sequential row-major sum of a K x K window of a global plane (adaptive_avg_pool
 // order), all loads issued together
 template <int K>
@@ -1307,24 +1288,64 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
   const float* Pm = S.smask;
   MSTAMP_INIT(b == 0 ? 0 : -1);
   MSTAMP(10);
-  // stage the weight blobs this launch needs in LDS (one round trip; the MLP
-  // and conv loops then read LDS instead of L2)
-  if (wlds) {
-    if (S.flags & F_CMLP) { stage_blob(ctx, wl + WL_CM, S.cmlp, CM_BLOB); Pc = wl + WL_CM; }
-    if ((S.flags & F_MAPPER) && !(S.flags & F_MAP_LINEAR)) { stage_blob(ctx, wl + WL_MM, S.mapper, MM_BLOB); Pmap = wl + WL_MM; }
-    if (S.flags & F_SOFTMASK) { stage_blob(ctx, wl + WL_SM, S.smask, SM_SIZE); Pm = wl + WL_SM; }
+  // One batched round trip: the per-tile partials of pass A and the weight
+  // blobs this launch needs go to LDS together (16-byte loads), so the phi
+  // assembly and the MLP / conv loops read LDS instead of L2.
+  int S_ = 0;
+  for (int s = 2; s <= S.tile; s *= 2) ++S_;
+  const int NI = 20 + S_;
+  const float* ttmp = S.tile_tmp + (size_t)b * NT * TT_STRIDE;
+#if defined(__HIP_DEVICE_COMPILE__)
+  {
+    // segments of float4s: [0] tile partials (row t: NI floats of 32 -> tiles[t][T_TMP..]),
+    // [1] complexity MLP, [2] mapper, [3] soft-mask net
+    const int q_t = (S.flags & F_PHI) ? NT * ((NI + 3) >> 2) : 0;
+    const int q_c = (wlds && (S.flags & F_CMLP)) ? (CM_BLOB + 3) >> 2 : 0;
+    const int q_m = (wlds && (S.flags & F_MAPPER) && !(S.flags & F_MAP_LINEAR)) ? (MM_BLOB + 3) >> 2 : 0;
+    const int q_s = (wlds && (S.flags & F_SOFTMASK)) ? (SM_SIZE + 3) >> 2 : 0;
+    const int qpt = (NI + 3) >> 2;
+    const int n = q_t + q_c + q_m + q_s;
+    auto src = [&](int u) -> const float4* {
+      if (u < q_t) { const int t = u / qpt; return reinterpret_cast<const float4*>(ttmp + t * TT_STRIDE) + (u - t * qpt); }
+      u -= q_t;
+      if (u < q_c) return reinterpret_cast<const float4*>(S.cmlp) + u;
+      u -= q_c;
+      if (u < q_m) return reinterpret_cast<const float4*>(S.mapper) + u;
+      return reinterpret_cast<const float4*>(S.smask) + (u - q_m);
+    };
+    auto dst = [&](int u) -> float4* {
+      if (u < q_t) { const int t = u / qpt; return reinterpret_cast<float4*>(tiles + t * TILE_FLOATS + T_TMP) + (u - t * qpt); }
+      u -= q_t;
+      if (u < q_c) return reinterpret_cast<float4*>(wl + WL_CM) + u;
+      u -= q_c;
+      if (u < q_m) return reinterpret_cast<float4*>(wl + WL_MM) + u;
+      return reinterpret_cast<float4*>(wl + WL_SM) + (u - q_m);
+    };
+    constexpr int K = 20;
+    for (int base = 0; base < n; base += K * ctx.nthr) {
+      float4 v[K];
+#pragma unroll
+      for (int i = 0; i < K; ++i) { const int u = base + ctx.tid + i * ctx.nthr; v[i] = *src(u < n ? u : 0); }
+#pragma unroll
+      for (int i = 0; i < K; ++i) { const int u = base + ctx.tid + i * ctx.nthr; if (u < n) *dst(u) = v[i]; }
+    }
+    if (q_c) Pc = wl + WL_CM;
+    if (q_m) Pmap = wl + WL_MM;
+    if (q_s) Pm = wl + WL_SM;
   }
+#else
+  if (S.flags & F_PHI)
+    MFOR(u, NT * NI) {
+      const int t = u / NI, it = u - (u / NI) * NI;
+      tiles[t * TILE_FLOATS + T_TMP + it] = ttmp[t * TT_STRIDE + it];
+    }
+#endif
   if (S.flags & F_PHI) {
     // partial quantities of the edge and mask workgroups -> phi
-    int S_ = 0;
-    for (int s = 2; s <= S.tile; s *= 2) ++S_;
-    const int NI = 20 + S_;
-    const float* ttmp = S.tile_tmp + (size_t)b * NT * TT_STRIDE;
-    bcopy<16>(ctx, NT * NI,
-              [&](int u) { const int t = u / NI; return ttmp[t * TT_STRIDE + (u - t * NI)]; },
-              [&](int u, float v) { const int t = u / NI; tiles[t * TILE_FLOATS + T_TMP + (u - t * NI)] = v; });
     MSYNC();
+    MSTAMP(26);
     assemble_phi(ctx, S, b, tiles);
+    MSTAMP(27);
   } else if (S.flags & F_CMLP) {
     bcopy<16>(ctx, NT * 8, [&](int u) { return S.phi_out[(size_t)b * NT * 8 + u]; },
               [&](int u, float v) { tiles[(u >> 3) * TILE_FLOATS + T_PHI + (u & 7)] = v; });
@@ -1338,6 +1359,7 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
 #if defined(__HIP_DEVICE_COMPILE__)
     for (int blk = ctx.tid >> 6; blk * 32 < NT; blk += ctx.nthr >> 6)
       cmlp_block_mfma(Pc, tiles, NT, blk * 32, ctx.tid & 63);
+    MSTAMP(28);
 #else
     MFOR(t, NT) {
       float phi[8];

@@ -210,6 +210,19 @@ class HookPlan:
             self._qs = qs
         self._n = n
 
+    def launch_pre(self, stream=None):
+        """Pass 1 + morphology (+ the channel min/max reduction)."""
+        L = self.lib
+        sh = _stream_handle(stream)
+        abi.check(L.mcaq_stats(self._st, self._n, sh), "mcaq_stats")
+        nf = self._n if self._fz is not None else 0
+        abi.check(L.mcaq_morph_finalize(self._mo, self._n, self._fz, nf, sh), "mcaq_morph_finalize")
+
+    def launch_quant(self, stream=None):
+        """Pass 2."""
+        if self._qs is not None:
+            abi.check(self.lib.mcaq_quant(self._qs, self._n, _stream_handle(stream)), "mcaq_quant")
+
     def launch(self, stream=None, process_group=None):
         """Enqueue the prepared step on `stream` (default: current stream).
         With a process group (batch sharded over ranks) the per-channel min/max

@@ -14,6 +14,12 @@ CMQ_SIZE = CM_SIZE + 512 + 2048      # + MFMA A-operand copies (mcaq_mlp_mfma.h)
 MMQ_SIZE = MM_SIZE + 128 + 2048 + 2048
 
 
+def _pad4(a):
+    """Blobs are read as 16-byte vectors: pad to a multiple of 4 floats."""
+    n = (-a.size) % 4
+    return np.concatenate([a, np.zeros(n, np.float32)]) if n else a
+
+
 def _f(a):
     if hasattr(a, "detach"):
         a = a.detach().cpu().numpy()
@@ -52,8 +58,8 @@ def pack_complexity_mlp(sd, prefix="complexity_mlp."):
     out = np.concatenate([_f(p) for p in parts])
     if out.size != CM_SIZE:
         raise ValueError("complexity MLP must be the reference 8-64-32-1 shape (got %d params)" % out.size)
-    return np.concatenate([out, mfma_a_operands(_np2(sd[prefix + "0.weight"])),
-                           mfma_a_operands(_np2(sd[prefix + "3.weight"]))])
+    return _pad4(np.concatenate([out, mfma_a_operands(_np2(sd[prefix + "0.weight"])),
+                                 mfma_a_operands(_np2(sd[prefix + "3.weight"]))]))
 
 
 def pack_mapper_mlp(sd, prefix="mapping_network."):
@@ -66,7 +72,7 @@ def pack_mapper_mlp(sd, prefix="mapping_network."):
     out = np.concatenate([_f(p) for p in parts])
     if out.size != MM_SIZE:
         raise ValueError("bit mapper must use hidden_dims [32, 64, 32] (got %d params)" % out.size)
-    return np.concatenate([out] + [mfma_a_operands(_np2(sd[prefix + "%d.weight" % i])) for i in (0, 3, 6)])
+    return _pad4(np.concatenate([out] + [mfma_a_operands(_np2(sd[prefix + "%d.weight" % i])) for i in (0, 3, 6)]))
 
 
 def pack_soft_mask(sd, prefix="net."):
@@ -75,7 +81,7 @@ def pack_soft_mask(sd, prefix="net."):
     out = np.concatenate([_f(p) for p in parts])
     if out.size != SM_SIZE:
         raise ValueError("soft mask must be the reference Conv2d(2,8,3)/Conv2d(8,2,1) net")
-    return out
+    return _pad4(out)
 
 
 def sub(sd, prefix):

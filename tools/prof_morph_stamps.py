@@ -16,7 +16,7 @@ from mcaq_yolo_amd import abi  # noqa: E402
 STAGES = [(0, 1, "E gray+norm"), (1, 2, "E blur+hist"), (2, 3, "E otsu"), (3, 4, "E sobel255+dir"),
           (4, 5, "E nms"), (5, 6, "E hysteresis"), (8, 9, "E tile items"),
           (16, 17, "M gray+norm"), (17, 23, "M binarize"), (23, 24, "M sobel+lbp+planes"), (24, 25, "M tile items"),
-          (10, 11, "B phi+cmlp"), (11, 12, "B bilateral"), (12, 13, "B mapper"), (13, 14, "B softmask tiles"),
+          (10, 26, "B stage loads"), (26, 27, "B assemble phi"), (27, 28, "B cmlp mfma"), (28, 11, "B cmlp out"), (11, 12, "B bilateral"), (12, 13, "B mapper"), (13, 14, "B softmask tiles"),
           (14, 15, "B m plane")]
 
 
