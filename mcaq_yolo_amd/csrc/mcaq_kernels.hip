@@ -177,71 +177,84 @@ __device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, fl
 
   Fold fg, fa;   // pixel `tid` (tid < UPIX)
   fg.init(); fa.init();
-  for (int r = 0; r < rounds; ++r) {
-    const int blk = r * ST_WAVES + wv;
-    if (blk < nblk) {
+  // MR rounds of 16-row blocks are loaded before the first is reduced (MR * 16
+  // * PPL = 64 floats per lane), so a unit with several channel rounds still
+  // pays about one memory latency per MR rounds
+  constexpr int MR = 4 / PPL;
+  for (int r0 = 0; r0 < rounds; r0 += MR) {
+    float v[MR][ST_CG][PPL];
+    const int qa = pv[0] ? q0 : 0;
+#pragma unroll
+    for (int rr = 0; rr < MR; ++rr) {
+      const int blk = imin_((r0 + rr) * ST_WAVES + wv, nblk - 1);   // clamped: branch-free loads
       const int c0 = blk * ST_CG;
       const int nc = imin_(ST_CG, C - c0);
-      // branch-free loads (clamped addresses, invalid pixels masked later) so
-      // all 16 rows are in flight together
-      float v[ST_CG][PPL];
-      const int qa = pv[0] ? q0 : 0;
 #pragma unroll
       for (int i = 0; i < ST_CG; ++i) {
         const float* row = xb + (size_t)(c0 + (i < nc ? i : 0)) * HW;
         if (kVec && PPL == 4) {
           const float4 t = *reinterpret_cast<const float4*>(row + qa);
-          v[i][0] = t.x; v[i][1 % PPL] = t.y; v[i][2 % PPL] = t.z; v[i][3 % PPL] = t.w;
+          v[rr][i][0] = t.x; v[rr][i][1 % PPL] = t.y; v[rr][i][2 % PPL] = t.z; v[rr][i][3 % PPL] = t.w;
         } else if (kVec && PPL == 2) {
           const float2 t = *reinterpret_cast<const float2*>(row + qa);
-          v[i][0] = t.x; v[i][1 % PPL] = t.y;
+          v[rr][i][0] = t.x; v[rr][i][1 % PPL] = t.y;
         } else {
 #pragma unroll
-          for (int k = 0; k < PPL; ++k) v[i][k] = row[imin_(q0 + k, HW - 1)];
+          for (int k = 0; k < PPL; ++k) v[rr][i][k] = row[imin_(q0 + k, HW - 1)];
         }
       }
-      float gb[PPL], ab[PPL];
+    }
 #pragma unroll
-      for (int k = 0; k < PPL; ++k) { gb[k] = 0.0f; ab[k] = 0.0f; }
+    for (int rr = 0; rr < MR; ++rr) {
+      const int r = r0 + rr;
+      if (r >= rounds) break;
+      const int blk = r * ST_WAVES + wv;
+      if (blk < nblk) {
+        const int c0 = blk * ST_CG;
+        const int nc = imin_(ST_CG, C - c0);
+        float gb[PPL], ab[PPL];
 #pragma unroll
-      for (int i = 0; i < ST_CG; ++i) {
-        if (i < nc) {
-#pragma unroll
-          for (int k = 0; k < PPL; ++k) { gb[k] = gb[k] + v[i][k]; ab[k] = ab[k] + fabsf(v[i][k]); }
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < PPL; ++k) { bsg[wv][lane * PPL + k] = gb[k]; bsa[wv][lane * PPL + k] = ab[k]; }
-      if (want_m) {
-        float mn[ST_CG], mx[ST_CG];
+        for (int k = 0; k < PPL; ++k) { gb[k] = 0.0f; ab[k] = 0.0f; }
 #pragma unroll
         for (int i = 0; i < ST_CG; ++i) {
-          float lo = 3.402823466e38f, hi = -3.402823466e38f;
+          if (i < nc) {
 #pragma unroll
-          for (int k = 0; k < PPL; ++k) {
-            lo = fminf(lo, pv[k] ? v[i][k] : 3.402823466e38f);
-            hi = fmaxf(hi, pv[k] ? v[i][k] : -3.402823466e38f);
+            for (int k = 0; k < PPL; ++k) { gb[k] = gb[k] + v[rr][i][k]; ab[k] = ab[k] + fabsf(v[rr][i][k]); }
           }
-          mn[i] = lo; mx[i] = hi;
         }
-        float omn, omx;
-        wave_minmax16(mn, mx, lane, omn, omx);
-        if (lane < 16 && lane < nc) {
-          S.pmin[(size_t)lu * C + c0 + lane] = omn;
-          S.pmax[(size_t)lu * C + c0 + lane] = omx;
+#pragma unroll
+        for (int k = 0; k < PPL; ++k) { bsg[wv][lane * PPL + k] = gb[k]; bsa[wv][lane * PPL + k] = ab[k]; }
+        if (want_m) {
+          float mn[ST_CG], mx[ST_CG];
+#pragma unroll
+          for (int i = 0; i < ST_CG; ++i) {
+            float lo = 3.402823466e38f, hi = -3.402823466e38f;
+#pragma unroll
+            for (int k = 0; k < PPL; ++k) {
+              lo = fminf(lo, pv[k] ? v[rr][i][k] : 3.402823466e38f);
+              hi = fmaxf(hi, pv[k] ? v[rr][i][k] : -3.402823466e38f);
+            }
+            mn[i] = lo; mx[i] = hi;
+          }
+          float omn, omx;
+          wave_minmax16(mn, mx, lane, omn, omx);
+          if (lane < 16 && lane < nc) {
+            S.pmin[(size_t)lu * C + c0 + lane] = omn;
+            S.pmax[(size_t)lu * C + c0 + lane] = omx;
+          }
         }
       }
-    }
-    __syncthreads();
-    if (tid < UPIX) {
-      const int nslot = imin_(ST_WAVES, nblk - r * ST_WAVES);
-      for (int s = 0; s < nslot; ++s) {
-        const int blk2 = r * ST_WAVES + s;
-        if (C - blk2 * ST_CG >= ST_CG) { fg.full(bsg[s][tid]); fa.full(bsa[s][tid]); }
-        else { fg.a0 = bsg[s][tid]; fa.a0 = bsa[s][tid]; }   // trailing partial block stays in a0
+      __syncthreads();
+      if (tid < UPIX) {
+        const int nslot = imin_(ST_WAVES, nblk - r * ST_WAVES);
+        for (int s = 0; s < nslot; ++s) {
+          const int blk2 = r * ST_WAVES + s;
+          if (C - blk2 * ST_CG >= ST_CG) { fg.full(bsg[s][tid]); fa.full(bsa[s][tid]); }
+          else { fg.a0 = bsg[s][tid]; fa.a0 = bsa[s][tid]; }   // trailing partial block stays in a0
+        }
       }
+      __syncthreads();
     }
-    __syncthreads();
   }
 
   // ---- tail columns (row_sum order), all in the image's last unit
@@ -412,6 +425,9 @@ __global__ __launch_bounds__(MORPH_THREADS) void mcaq_morph_kernel(MorphArgs a, 
     finalize_body(f, (int)blockIdx.x - 2 * nimg, reinterpret_cast<float*>(smem));
     return;
   }
+  // latency-bound per-image chain: win VALU / LDS issue arbitration against
+  // co-resident streaming waves of other batches in flight
+  __builtin_amdgcn_s_setprio(2);
   // two workgroups per image: role 0 = edge plane, role 1 = mask planes
   const int img = (int)blockIdx.x >> 1, role = (int)blockIdx.x & 1;
   const MorphScale& S = a.s[morph_scale_of(a, img)];
@@ -432,6 +448,7 @@ __global__ __launch_bounds__(MORPH_THREADS) void mcaq_morph_kernel(MorphArgs a, 
 
 __global__ __launch_bounds__(TILES_THREADS) void mcaq_tiles_kernel(MorphArgs a, int wlds) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  __builtin_amdgcn_s_setprio(2);
   const MorphScale& S = a.s[morph_scale_of(a, (int)blockIdx.x)];
   const int b = (int)blockIdx.x - S.block_begin;
   if (b >= S.B) return;

@@ -508,19 +508,26 @@ MCAQ_HD void sort_tiles(const Ctx& ctx, float* tiles, int NT, int src) {
 #endif
 namespace mcaq {
 
-// NMS direction bin (morphology.py:430-444).  The float angle is the correctly
-// rounded fp32 atan2 scaled by fp32(180/pi); a fast single-precision estimate
-// decides every pixel whose angle is > 1e-3 degrees from a bin edge, the exact
-// double-precision path the rest (same result as evaluating it everywhere).
+// NMS direction bin (morphology.py:430-444): the reference bins the fp32 angle
+// a = atan2(gy, gx) * fp32(180/pi) (+180 when negative) at 22.5 / 67.5 /
+// 112.5 / 157.5 degrees.  Fast path: the bin edges are the slopes tan(22.5)
+// and tan(67.5), so |gy| against t*|gx| (plus the sign of gx*gy between them)
+// decides every pixel whose slope is at least 3e-5*|gx| from an edge (>= 2.5e-4
+// degrees, ten times the fp32 angle's error); the others, and gx = gy = 0, take
+// the exact path: correctly rounded fp32 atan2 scaled by fp32(180/pi).
 MCAQ_HD int nms_dir(float gx, float gy) {
-  const float K180 = (float)(180.0 / 3.14159265358979323846);
-  float a = atan2f(gy, gx) * K180;
-  if (a < 0.0f) a = a + 180.0f;
-  const float e0 = fabsf(a - 22.5f), e1 = fabsf(a - 67.5f), e2 = fabsf(a - 112.5f), e3 = fabsf(a - 157.5f);
-  if (fmin_(fmin_(e0, e1), fmin_(e2, e3)) < 1e-3f) {
-    a = cr_atan2(gy, gx) * K180;
-    if (a < 0.0f) a = a + 180.0f;
+  const float ax = fabsf(gx), ay = fabsf(gy);
+  const float r1 = ay - 0.41421356237309503f * ax;
+  const float r2 = ay - 2.4142135623730949f * ax;
+  const float mg = 3e-5f * ax;
+  if (fabsf(r1) > mg && fabsf(r2) > mg) {
+    if (r1 < 0.0f) return 0;
+    if (r2 > 0.0f) return 2;
+    return ((gx > 0.0f) == (gy > 0.0f)) ? 1 : 3;
   }
+  const float K180 = (float)(180.0 / 3.14159265358979323846);
+  float a = cr_atan2(gy, gx) * K180;
+  if (a < 0.0f) a = a + 180.0f;
   if (a >= 22.5f && a < 67.5f) return 1;
   if (a >= 67.5f && a < 112.5f) return 2;
   if (a >= 112.5f && a < 157.5f) return 3;
@@ -844,10 +851,9 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, P
           uint32_t up[4], dn[4], d[4][4];
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
-            const uint32_t u = (uint32_t)__shfl_up((int)e[1][k], 1, 64);
-            const uint32_t v = (uint32_t)__shfl_down((int)e[0][k], 1, 64);
-            up[k] = lane > 0 ? u : 0u;
-            dn[k] = lane < 63 ? v : 0u;
+            // DPP wave_shr:1 / wave_shl:1 (lane l <- l-1 / l+1; 0 past the ends)
+            up[k] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)e[1][k], 0x138, 0xF, 0xF, false);
+            dn[k] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)e[0][k], 0x130, 0xF, 0xF, false);
           }
           // horizontal 3-dilation of the 4 rows up, e0, e1, dn
 #pragma unroll
