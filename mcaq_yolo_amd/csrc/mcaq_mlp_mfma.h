@@ -42,6 +42,12 @@ enum : int {
 
 __device__ __forceinline__ int d_neuron(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
 
+// value of x in lane l ^ 32 (v_permlane32_swap: a VALU lane swap, no LDS round trip)
+__device__ __forceinline__ float xhalf(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float((threadIdx.x & 32) ? r[0] : r[1]);
+}
+
 // B operand of k-step s built from a previous layer's D blocks
 template <int S>
 __device__ __forceinline__ float b_from_d(const f32x16* D, int half) {
@@ -52,10 +58,10 @@ __device__ __forceinline__ float b_from_d(const f32x16* D, int half) {
   const float x0 = D[blk][r0];
   const float x1 = D[blk][r0 + 1];
   if (H == 0) {
-    const float t = __shfl_xor(x1, 32, 64);
+    const float t = xhalf(x1);
     return half == 0 ? x0 : t;
   } else {
-    const float t = __shfl_xor(x0, 32, 64);
+    const float t = xhalf(x0);
     return half == 1 ? x1 : t;
   }
 }
@@ -67,7 +73,7 @@ __device__ __forceinline__ float tree32(const f32x16& d) {
   for (int g = 0; g < 4; ++g) q[g] = (d[4 * g] + d[4 * g + 1]) + (d[4 * g + 2] + d[4 * g + 3]);
   float u[4];
 #pragma unroll
-  for (int g = 0; g < 4; ++g) u[g] = q[g] + __shfl_xor(q[g], 32, 64);
+  for (int g = 0; g < 4; ++g) u[g] = q[g] + xhalf(q[g]);
   return (u[0] + u[1]) + (u[2] + u[3]);
 }
 
@@ -98,7 +104,7 @@ __device__ __forceinline__ void layernorm_d(f32x16* D, const float* g, const flo
 __device__ __forceinline__ float dot32_seq(const f32x16& d, const float* w, int half) {
   float other[16];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) other[r] = __shfl_xor(d[r], 32, 64);
+  for (int r = 0; r < 16; ++r) other[r] = xhalf(d[r]);
   float acc = 0.0f;
 #pragma unroll
   for (int n = 0; n < 32; ++n) {

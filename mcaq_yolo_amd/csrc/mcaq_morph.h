@@ -1135,7 +1135,7 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, P
             }
           }
         }
-        val = cr_log((float)n + 1.0f);
+        val = n <= 64 ? bits_as_float(k_lognp1_bits[n]) : cr_log((float)n + 1.0f);
       } else {
         const int k = it - 4 - S_;
         const uint32_t* plane = k < 10 ? pl.bits(BP_L0 + k)
@@ -1146,8 +1146,14 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, P
         else if (T == 16) cnt = tile_pop_t<16>(plane, WPR, h0, w0);
         else for (int yy = 0; yy < T; ++yy) cnt += row_pop(plane + (h0 + yy) * WPR, w0, T, WPR);
         if (k < 10) {
-          const float pk = (float)cnt / fT2;
-          val = pk * log2_ref(pk + 1e-10f);
+          // exact table of p * log2(p + 1e-10), p = cnt / T^2 (tools/gen_tables.py)
+          if (T == 4) val = bits_as_float(k_lbp_t4_bits[cnt]);
+          else if (T == 8) val = bits_as_float(k_lbp_t8_bits[cnt]);
+          else if (T == 16) val = bits_as_float(k_lbp_t16_bits[cnt]);
+          else {
+            const float pk = (float)cnt / fT2;
+            val = pk * log2_ref(pk + 1e-10f);
+          }
         } else {
           val = (float)cnt;
         }
@@ -1258,6 +1264,16 @@ enum : int {
   WL_FLOATS = WL_SM + ((SM_SIZE + 3) & ~3),
 };
 MCAQ_HD int weights_lds_bytes() { return 4 * WL_FLOATS; }
+// float4 index inside a blob of the u-th staged float4 (the ranges the device
+// path reads; all range bounds are multiples of 4 floats)
+MCAQ_HD int cm_q(int u) {
+  const int n1 = (CM_W2 - CM_B1) >> 2;
+  return u < n1 ? (CM_B1 >> 2) + u : (CM_B2 >> 2) + (u - n1);
+}
+MCAQ_HD int mm_q(int u) {
+  const int n1 = (MM_W2 - MM_B1) >> 2, n2 = (MM_W3 - MM_B2) >> 2;
+  return u < n1 ? (MM_B1 >> 2) + u : (u < n1 + n2 ? (MM_B2 >> 2) + (u - n1) : (MM_B3 >> 2) + (u - n1 - n2));
+}
 
 // sequential row-major sum of a K x K window of a global plane (adaptive_avg_pool
 // order), all loads issued together
@@ -1306,25 +1322,29 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
     // segments of float4s: [0] tile partials (row t: NI floats of 32 -> tiles[t][T_TMP..]),
     // [1] complexity MLP, [2] mapper, [3] soft-mask net
     const int q_t = (S.flags & F_PHI) ? NT * ((NI + 3) >> 2) : 0;
-    const int q_c = (wlds && (S.flags & F_CMLP)) ? (CM_BLOB + 3) >> 2 : 0;
-    const int q_m = (wlds && (S.flags & F_MAPPER) && !(S.flags & F_MAP_LINEAR)) ? (MM_BLOB + 3) >> 2 : 0;
+    // device-side MLPs read the MFMA operand copies, biases and norm terms, not
+    // the plain weight matrices: stage [CM_B1, CM_W2) and [CM_B2, end) of the
+    // complexity MLP, [MM_B1, MM_W2), [MM_B2, MM_W3), [MM_B3, end) of the mapper
+    const int q_c = (wlds && (S.flags & F_CMLP)) ? ((CM_BLOB + 3) >> 2) - (CM_B2 >> 2) + ((CM_W2 - CM_B1) >> 2) : 0;
+    const int q_m = (wlds && (S.flags & F_MAPPER) && !(S.flags & F_MAP_LINEAR))
+                        ? ((MM_BLOB + 3) >> 2) - (MM_B3 >> 2) + ((MM_W2 - MM_B1) >> 2) + ((MM_W3 - MM_B2) >> 2) : 0;
     const int q_s = (wlds && (S.flags & F_SOFTMASK)) ? (SM_SIZE + 3) >> 2 : 0;
     const int qpt = (NI + 3) >> 2;
     const int n = q_t + q_c + q_m + q_s;
     auto src = [&](int u) -> const float4* {
       if (u < q_t) { const int t = u / qpt; return reinterpret_cast<const float4*>(ttmp + t * TT_STRIDE) + (u - t * qpt); }
       u -= q_t;
-      if (u < q_c) return reinterpret_cast<const float4*>(S.cmlp) + u;
+      if (u < q_c) return reinterpret_cast<const float4*>(S.cmlp) + cm_q(u);
       u -= q_c;
-      if (u < q_m) return reinterpret_cast<const float4*>(S.mapper) + u;
+      if (u < q_m) return reinterpret_cast<const float4*>(S.mapper) + mm_q(u);
       return reinterpret_cast<const float4*>(S.smask) + (u - q_m);
     };
     auto dst = [&](int u) -> float4* {
       if (u < q_t) { const int t = u / qpt; return reinterpret_cast<float4*>(tiles + t * TILE_FLOATS + T_TMP) + (u - t * qpt); }
       u -= q_t;
-      if (u < q_c) return reinterpret_cast<float4*>(wl + WL_CM) + u;
+      if (u < q_c) return reinterpret_cast<float4*>(wl + WL_CM) + cm_q(u);
       u -= q_c;
-      if (u < q_m) return reinterpret_cast<float4*>(wl + WL_MM) + u;
+      if (u < q_m) return reinterpret_cast<float4*>(wl + WL_MM) + mm_q(u);
       return reinterpret_cast<float4*>(wl + WL_SM) + (u - q_m);
     };
     constexpr int K = 20;

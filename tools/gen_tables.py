@@ -11,7 +11,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from oracle.ieee import aten_sum, cr32  # noqa: E402
-from oracle.mcaq_oracle import K  # noqa: E402
+from oracle.mcaq_oracle import K, log2_torch  # noqa: E402
 
 HDR = os.path.join(ROOT, "mcaq_yolo_amd", "csrc", "mcaq_tables.h")
 
@@ -60,6 +60,20 @@ def separable_g11():
     return k1, np.array([margin], f32)
 
 
+def lbp_terms(T):
+    """p * log2(p + 1e-10) for p = k / T^2, k = 0..T^2 (the per-label entropy
+    term of morphology.py:640-650 as oracle.lbp_entropy_tiles computes it)."""
+    f32 = np.float32
+    p = (np.arange(T * T + 1, dtype=f32) / f32(T * T)).astype(f32)
+    return (p * log2_torch((p + f32(1e-10)).astype(f32))).astype(f32)
+
+
+def box_logs(n):
+    """fp32 log(k + 1), k = 0..n (box-count regression ordinates, oracle.fractal_tiles)."""
+    f32 = np.float32
+    return cr32(np.log, (np.arange(n + 1, dtype=f32) + f32(1.0)).astype(f32))
+
+
 def main():
     fx, fw, fst = fractal_constants()
     k1, marg = separable_g11()
@@ -68,6 +82,8 @@ def main():
         ("k_smooth5", "smooth5_softmask"), ("k_bilat_sp", "bilateral_spatial")))
     body += table("k_frac_x", fx) + table("k_frac_w", fw) + table("k_frac_st", fst)
     body += table("k_g11_sep", k1) + table("k_g11_margin", marg)
+    body += table("k_lbp_t4", lbp_terms(4)) + table("k_lbp_t8", lbp_terms(8)) + table("k_lbp_t16", lbp_terms(16))
+    body += table("k_lognp1", box_logs(64))
     src = open(HDR).read()
     a = src.index("// @@TABLES@@")
     b = src.index("}  // namespace mcaq")

@@ -3,7 +3,9 @@ set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 cd $GRAFT_REPO_ROOT
-timeout -k 10 120 python tools/prof_morph_stamps.py 2 > gpurun_out/stamps.log 2>&1; grep -v amdgpu gpurun_out/stamps.log | head -24
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; tail -3 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || { grep -E "FAIL|Error|assert" gpurun_out/pytest_gpu.log | head -30; exit $rc; }
+timeout -k 10 120 python tools/prof_morph_stamps.py 2 > gpurun_out/stamps.log 2>&1; grep -v amdgpu gpurun_out/stamps.log | head -21
 for d in 2 3; do
   timeout -k 10 300 python bench.py --steps 60 --warmup 10 --no-cpu --pipeline $d > gpurun_out/bench_p$d.json 2> gpurun_out/bench_p$d.err || { tail -20 gpurun_out/bench_p$d.err; exit 1; }
   python -c "import json;d=json.load(open('gpurun_out/bench_p$d.json'));k=d['kernels'];print('pipeline',$d,d['value'],d['ms_per_step'],d['roofline']['frac'],d['config']['latency_ms_single_batch'],k['stats']['us'],k['morph_finalize']['us'],k['quant']['us'])"
