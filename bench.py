@@ -246,6 +246,13 @@ def main():
 
     elems = sum(B * c * h * w for c, (h, w) in zip(chans, SIZES))
     alg_bytes = 12 * elems                       # 2 reads of x + 1 write of y, fp32
+    # HBM-side bytes per step from the rocprofv3 PMC passes of tools/pmc_traffic.sh
+    # (FETCH_SIZE and WRITE_SIZE in separate runs, FETCH doubled per the gfx950
+    # calibration), committed per config under profiles/
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "r01_pmc_traffic_config%d.json" % args.config)
+    if os.path.exists(tpath):
+        traffic = json.load(open(tpath)).get("step_total")
     achieved = alg_bytes / step_s / 1e9
     value = world * B / step_s
     if rank == 0:
@@ -274,7 +281,7 @@ def main():
                        "parallelism": "dp%d" % world, "hip_graph": use_graph,
                        "batches_in_flight": depth, "latency_ms_single_batch": round(latency_ms, 4)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": "hook path step: mcaq_stats + mcaq_morph_kernel/mcaq_tiles_kernel + "
                                    "mcaq_quant, 12 B per feature element per step",
                          "alg_bytes_per_step": alg_bytes},
