@@ -9,7 +9,7 @@ produces, computed by the HIP kernels on inputs already resident in HBM.  The
 YOLOv8 host network is not part of the step (not built yet: SURVEY 8f rank 1;
 ultralytics is unavailable) - `config.workload` says so.
 
-Throughput: `--pipeline D` (default 2) independent batches are in flight on D
+Throughput: `--pipeline D` (default 3) independent batches are in flight on D
 HIP streams, so one batch's latency-bound per-image morphology overlaps the
 HBM passes of the next; `value` = images of all K timed steps / wall time.
 `config.latency_ms_single_batch` is one step with nothing beside it.
@@ -147,7 +147,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
-    ap.add_argument("--pipeline", type=int, default=2, help="batches in flight (independent plans/streams)")
+    ap.add_argument("--pipeline", type=int, default=3, help="batches in flight (independent plans/streams)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no HIP graph")
     args = ap.parse_args()

@@ -1,15 +1,14 @@
 #!/bin/bash
-# One GPU session: parity tests, smoke, short bench, rocprof kernel stats.
+# One GPU session: parity tests, smoke, bench (default command), rocprof kernel stats.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; tail -5 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || exit $rc
+cd $GRAFT_REPO_ROOT
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; tail -3 gpurun_out/pytest_gpu.log; [ $rc -eq 0 ] || { grep -E "FAIL|Error|assert" gpurun_out/pytest_gpu.log | head -30; exit $rc; }
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { cat gpurun_out/smoke.log; exit 1; }
-cat gpurun_out/smoke.log
-timeout -k 10 300 python bench.py --steps 50 --warmup 10 > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail gpurun_out/bench.err; exit 1; }
+grep smoke gpurun_out/smoke.log
+timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { tail gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.json
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --steps 50 --warmup 5 --no-cpu > $GRAFT_REPO_ROOT/gpurun_out/prof.log 2>&1 || { tail -20 $GRAFT_REPO_ROOT/gpurun_out/prof.log; exit 1; }
-find $GRAFT_REPO_ROOT/gpurun_out/prof -name "*stats*" | head
-cd $GRAFT_REPO_ROOT && timeout -k 10 120 python tools/prof_stages.py 2 > gpurun_out/stages.log 2>&1; cat gpurun_out/stages.log
-cd $GRAFT_REPO_ROOT && timeout -k 10 120 python tools/prof_morph_stamps.py 2 > gpurun_out/stamps.log 2>&1; cat gpurun_out/stamps.log
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu > $GRAFT_REPO_ROOT/gpurun_out/prof.log 2>&1 || { tail -20 $GRAFT_REPO_ROOT/gpurun_out/prof.log; exit 1; }
+cat $GRAFT_REPO_ROOT/gpurun_out/prof/run_kernel_stats.csv
