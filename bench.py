@@ -157,12 +157,20 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    # MCAQ_BENCH_BACKEND=gloo + more ranks than GPUs: functional rehearsal of
+    # the N > 1 path on a one-GPU box (never a measurement)
+    backend = os.environ.get("MCAQ_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    local = local % max(ndev, 1) if backend != "nccl" else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     pg = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
         pg = dist.group.WORLD
 
     name, B, chans, grid, mapper = CONFIGS[args.config]
