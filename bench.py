@@ -141,6 +141,59 @@ class Runner:
             torch.cuda.current_stream().wait_stream(st)
 
 
+class SplitRunner:
+    """Software-pipelined schedule on three HIP streams: stream S runs the two
+    HBM passes back to back (pass 1 of batch i, then pass 2 of batch i - LAG);
+    streams M0 / M1 run the latency-bound morphology of alternate batches, each
+    starting when its batch's pass 1 has finished; pass 2 of a batch waits for
+    its morphology (event edges).  With LAG steps of HBM work in front of it,
+    a batch's morphology chain is hidden behind the other batches' streaming
+    passes.  Eager launches (each step is 4 kernels and 3 event edges)."""
+    LAG = 2
+
+    def __init__(self, plans, pg):
+        if len(plans) < self.LAG + 1:
+            raise ValueError("--schedule split needs --pipeline >= %d" % (self.LAG + 1))
+        self.plans, self.pg = plans, pg
+        self.S = torch.cuda.Stream()
+        self.M = [torch.cuda.Stream(), torch.cuda.Stream()]
+        self.ev_st = [torch.cuda.Event() for _ in plans]
+        self.ev_mo = [torch.cuda.Event() for _ in plans]
+        self.i = 0       # batches started
+        self.done = 0    # batches whose pass 2 is enqueued
+
+    def _quant(self, j):
+        p = j % len(self.plans)
+        plan = self.plans[p]
+        self.S.wait_event(self.ev_mo[p])
+        if self.pg is not None:
+            with torch.cuda.stream(self.S):
+                sync_channel_minmax(plan.bufs, self.pg)
+        plan.launch_quant(self.S)
+        self.done = j + 1
+
+    def step(self):
+        i = self.i
+        p = i % len(self.plans)
+        plan = self.plans[p]
+        plan.launch_stats(self.S)
+        self.ev_st[p].record(self.S)
+        m = self.M[i % 2]
+        m.wait_event(self.ev_st[p])
+        plan.launch_morph(m)
+        self.ev_mo[p].record(m)
+        self.i = i + 1
+        if i >= self.LAG:
+            self._quant(i - self.LAG)
+
+    def sync(self):
+        while self.done < self.i:
+            self._quant(self.done)
+        cur = torch.cuda.current_stream()
+        for st in [self.S] + self.M:
+            cur.wait_stream(st)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -149,7 +202,10 @@ def main():
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
     ap.add_argument("--pipeline", type=int, default=3, help="batches in flight (independent plans/streams)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--eager", action="store_true", help="no HIP graph")
+    ap.add_argument("--eager", action="store_true", help="no HIP graph (--schedule streams)")
+    ap.add_argument("--schedule", choices=("split", "streams"), default="streams",
+                    help="split: HBM passes on one stream, morphology on two (SplitRunner); "
+                         "streams: D independent per-batch streams, one HIP graph per step")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -189,8 +245,8 @@ def main():
         feats_all.append(feats)
     torch.cuda.synchronize()
 
-    use_graph = not args.eager
-    runner = Runner(plans, pg, use_graph)
+    use_graph = not args.eager and args.schedule == "streams"
+    runner = Runner(plans, pg, use_graph) if args.schedule == "streams" else SplitRunner(plans, pg)
     for _ in range(max(args.warmup, 1)):
         runner.step()
     runner.sync()
@@ -225,7 +281,6 @@ def main():
     for _ in range(10):
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        runner.i = 0
         runner.step()
         runner.sync()
         torch.cuda.synchronize()
@@ -237,10 +292,10 @@ def main():
         import torch.distributed as dist
         dist.barrier()
     torch.cuda.synchronize()
-    runner.i = 0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         runner.step()
+    t_enq = time.perf_counter() - t0
     runner.sync()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
@@ -287,7 +342,8 @@ def main():
                                    "YOLOv8 network excluded" % (name, B, grid, mapper),
                        "global_batch": world * B, "grid_size": grid, "mapper": mapper,
                        "parallelism": "dp%d" % world, "hip_graph": use_graph,
-                       "batches_in_flight": depth, "latency_ms_single_batch": round(latency_ms, 4)},
+                       "batches_in_flight": depth, "schedule": args.schedule, "latency_ms_single_batch": round(latency_ms, 4),
+                       "host_enqueue_us_per_step": round(t_enq / args.steps * 1e6, 1)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": "hook path step: mcaq_stats + mcaq_morph_kernel/mcaq_tiles_kernel + "

@@ -408,8 +408,9 @@ __global__ __launch_bounds__(256) void mcaq_finalize_kernel(FinalizeArgs a) {
 // morph pass A: one 1024-thread workgroup per (scale, image), planes in LDS
 // morph pass B: one 256-thread workgroup per (scale, image), tile grid in LDS
 // ---------------------------------------------------------------------------
-constexpr int MORPH_THREADS = 1024;
 constexpr int TILES_THREADS = 256;
+
+constexpr int MORPH_THREADS = 1024;
 
 __device__ __forceinline__ int morph_scale_of(const MorphArgs& a, int img) {
   int si = 0;
@@ -417,45 +418,65 @@ __device__ __forceinline__ int morph_scale_of(const MorphArgs& a, int img) {
   return si;
 }
 
+// Pass A packs several small images into one 1024-thread workgroup: image
+// group g owns threads [g*G, (g+1)*G), G = 1024 / ipw, and its own LDS planes.
+// The per-image chain is latency bound, so a 20x20 image needs no more than
+// 128 threads to finish as fast as alone -- packing 8 of them frees 7 CUs.
+// Every group runs the same barrier sequence (stage loops depend on the
+// scale's geometry only); a group past the batch end recomputes the last
+// image (identical values written twice) instead of idling at the barriers.
 template <bool kLDS>
-__global__ __launch_bounds__(MORPH_THREADS) void mcaq_morph_kernel(MorphArgs a, int plane_stride, FinalizeArgs f) {
+__global__ __launch_bounds__(MORPH_THREADS) void mcaq_morph_kernel(MorphArgs a, FinalizeArgs f) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int nimg = a.s[a.nscales - 1].block_begin + a.s[a.nscales - 1].B;
-  if ((int)blockIdx.x >= 2 * nimg) {   // channel min/max workgroups ride along
-    finalize_body(f, (int)blockIdx.x - 2 * nimg, reinterpret_cast<float*>(smem));
+  const int nwg = a.wg_begin[a.nscales];
+  if ((int)blockIdx.x >= nwg) {   // channel min/max workgroups ride along
+    finalize_body(f, (int)blockIdx.x - nwg, reinterpret_cast<float*>(smem));
     return;
   }
   // latency-bound per-image chain: win VALU / LDS issue arbitration against
   // co-resident streaming waves of other batches in flight
   __builtin_amdgcn_s_setprio(2);
-  // two workgroups per image: role 0 = edge plane, role 1 = mask planes
-  const int img = (int)blockIdx.x >> 1, role = (int)blockIdx.x & 1;
-  const MorphScale& S = a.s[morph_scale_of(a, img)];
-  const int b = img - S.block_begin;
-  if (b >= S.B || !(S.flags & F_PHI)) return;
-  Ctx ctx{(int)threadIdx.x, (int)blockDim.x};
+  int si = 0;
+  while (si + 1 < a.nscales && (int)blockIdx.x >= a.wg_begin[si + 1]) ++si;
+  const MorphScale& S = a.s[si];
+  // two workgroups per image group: role 0 = edge plane, role 1 = mask planes
+  const int wg = (int)blockIdx.x - a.wg_begin[si];
+  const int grp = wg >> 1, role = wg & 1;
+  const int ipw = a.ipw[si], G = MORPH_THREADS / ipw;
+  const int g = (int)threadIdx.x / G;
+  const int b = imin_(grp * ipw + g, S.B - 1);
+  Ctx ctx{(int)threadIdx.x - g * G, G};
   Shared sh;
   Planes pl;
+  char* base = smem + (size_t)g * a.gstride[si];
   if (kLDS) {
-    carve_planes(smem, S.Hc, S.Wc, pl);
-    carve_shared(smem + plane_stride, sh);
+    carve_planes(base, S.Hc, S.Wc, pl);
+    carve_shared(base + a.pstride[si], sh);
   } else {
-    carve_planes((char*)S.gscratch + (size_t)(2 * b + role) * plane_stride, S.Hc, S.Wc, pl);
-    carve_shared(smem, sh);
+    carve_planes((char*)S.gscratch + (size_t)(2 * b + role) * a.pstride[si], S.Hc, S.Wc, pl);
+    carve_shared(base, sh);
   }
   morph_edges(ctx, S, b, role, pl, sh);
 }
 
+// pass B: image group g of a workgroup owns threads [g*G, (g+1)*G) and its own
+// LDS tile arrays; the staged weights are shared by the workgroup.  A group
+// past the batch end recomputes the last image (identical values written twice).
 __global__ __launch_bounds__(TILES_THREADS) void mcaq_tiles_kernel(MorphArgs a, int wlds) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __builtin_amdgcn_s_setprio(2);
-  const MorphScale& S = a.s[morph_scale_of(a, (int)blockIdx.x)];
-  const int b = (int)blockIdx.x - S.block_begin;
-  if (b >= S.B) return;
-  Ctx ctx{(int)threadIdx.x, (int)blockDim.x};
+  int si = 0;
+  while (si + 1 < a.nscales && (int)blockIdx.x >= a.twg_begin[si + 1]) ++si;
+  const MorphScale& S = a.s[si];
+  const int ipw = a.tipw[si], G = TILES_THREADS / ipw;
+  const int g = (int)threadIdx.x / G;
+  const int b = imin_(((int)blockIdx.x - a.twg_begin[si]) * ipw + g, S.B - 1);
+  float* wl = wlds ? reinterpret_cast<float*>(smem) : nullptr;
+  char* base = smem + (wlds ? weights_lds_bytes() : 0) + (size_t)g * a.tgstride[si];
+  Ctx ctx{(int)threadIdx.x - g * G, G};
   Shared sh;
-  carve_shared(smem, sh);
-  morph_tiles(ctx, S, b, sh, wlds);
+  carve_shared(base, sh);
+  morph_tiles(ctx, S, b, sh, wl, (int)threadIdx.x, TILES_THREADS);
 }
 
 // ---------------------------------------------------------------------------
@@ -626,7 +647,14 @@ int mcaq_launch_spatial_quantization(const float* input, const float* bit_map, c
   return mcaq_quant(&q, 1, stream);
 }
 
+// EXPERIMENT knob: MCAQ_XSKIP bit 0 = skip morph/tiles, bit 1 = skip stats/quant
+static int xskip() {
+  static int v = -1;
+  if (v < 0) { const char* e = getenv("MCAQ_XSKIP"); v = e ? atoi(e) : 0; }
+  return v;
+}
 int mcaq_stats(const mcaq_stats_scale* scales, int nscales, hipStream_t stream) {
+  if (xskip() & 2) return 0;
   if (nscales < 1 || nscales > 3) return (int)hipErrorInvalidValue;
   StatsArgs a;
   int units = 0;
@@ -695,12 +723,11 @@ static int morph_lds_budget() {
   return budget;
 }
 
+// LDS mode for a set of scales: planes in LDS when every scale's image fits
 static int morph_plan(const MorphScale* s, int n, int* lds_mode, int* plane_stride, size_t* dyn) {
-  int pb = 0, rest = 0;
-  for (int i = 0; i < n; ++i) {
-    pb = imax_(pb, (plane_bytes(s[i].Hc, s[i].Wc) + 15) & ~15);
-    rest = imax_(rest, fixed_bytes() + tile_bytes(s[i].ht * s[i].wt));
-  }
+  int pb = 0;
+  for (int i = 0; i < n; ++i) pb = imax_(pb, (plane_bytes(s[i].Hc, s[i].Wc) + 15) & ~15);
+  const int rest = fixed_bytes();   // pass A keeps no tile array in LDS
   const int limit = morph_lds_budget();
   if (pb + rest <= limit) {
     *lds_mode = 1; *plane_stride = pb; *dyn = (size_t)(pb + rest);
@@ -710,6 +737,17 @@ static int morph_plan(const MorphScale* s, int n, int* lds_mode, int* plane_stri
     return (int)hipErrorInvalidValue;
   }
   return 0;
+}
+
+// images per pass A workgroup: the most (power of two, <= 16) whose planes fit
+// the LDS budget while each image keeps >= 64 threads and <= 8 pixels per thread
+static int morph_ipw(const MorphScale& S, int mode, int limit) {
+  if (!mode) return 1;   // planes in global scratch: one image per workgroup
+  const int per = ((plane_bytes(S.Hc, S.Wc) + 15) & ~15) + fixed_bytes();
+  const int P = S.Hc * S.Wc;
+  int ipw = 16;
+  while (ipw > 1 && (ipw * per > limit || MORPH_THREADS / ipw < 64 || P > 8 * (MORPH_THREADS / ipw))) ipw >>= 1;
+  return ipw;
 }
 
 size_t mcaq_morph_scratch_bytes(int B, int Hc, int Wc, int ht, int wt) {
@@ -733,7 +771,7 @@ int mcaq_morph_finalize(const mcaq_morph_scale* scales, int nscales, const mcaq_
     if (fe) return fe;
   }
   MorphArgs a;
-  int blocks = 0, any_phi = 0, any_tiles = 0, tlds = 0;
+  int blocks = 0, any_phi = 0, any_tiles = 0;
   for (int i = 0; i < nscales; ++i) {
     memcpy(&a.s[i], &scales[i], sizeof(MorphScale));
     MorphScale& S = a.s[i];
@@ -750,9 +788,9 @@ int mcaq_morph_finalize(const mcaq_morph_scale* scales, int nscales, const mcaq_
     any_phi |= (S.flags & F_PHI) != 0;
     const int tf = S.flags & (F_PHI | F_CMLP | F_MAPPER | F_SOFTMASK);
     any_tiles |= tf != 0;
-    if (tf) tlds = imax_(tlds, tiles_lds_bytes(S.H, S.W, S.ht * S.wt));
   }
   a.nscales = nscales;
+  if (xskip() & 1) { any_phi = 0; any_tiles = 0; }
   if (!any_phi && fa.nblocks > 0) {   // nothing to ride along with
     hipLaunchKernelGGL(mcaq_finalize_kernel, dim3(fa.nblocks), dim3(256), 0, stream, fa);
     const hipError_t fe = hipGetLastError();
@@ -762,50 +800,72 @@ int mcaq_morph_finalize(const mcaq_morph_scale* scales, int nscales, const mcaq_
     int mode, stride; size_t dyn;
     int e = morph_plan(a.s, nscales, &mode, &stride, &dyn);
     if (e) return e;
-    if (fa.nblocks > 0 && dyn < (size_t)(8 * MORPH_THREADS)) dyn = 8 * MORPH_THREADS;  // finalize_body's LDS
-    if (!mode)
-      for (int i = 0; i < nscales; ++i)
-        if (!a.s[i].gscratch && (a.s[i].flags & F_PHI)) return (int)hipErrorInvalidValue;
-    if (mode) {
-      static int set_true = 0;  // raise the dynamic LDS limit once (not during graph capture)
-      if ((int)dyn > set_true) {
-        hipError_t ae = hipFuncSetAttribute((const void*)mcaq_morph_kernel<true>,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, morph_lds_budget());
-        if (ae != hipSuccess) return (int)ae;
-        set_true = morph_lds_budget();
-      }
-      hipLaunchKernelGGL(mcaq_morph_kernel<true>, dim3(2 * blocks + fa.nblocks), dim3(MORPH_THREADS), dyn, stream, a, stride, fa);
-    } else {
-      static int set_false = 0;
-      if ((int)dyn > set_false) {
-        hipError_t ae = hipFuncSetAttribute((const void*)mcaq_morph_kernel<false>,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, morph_lds_budget());
-        if (ae != hipSuccess) return (int)ae;
-        set_false = morph_lds_budget();
-      }
-      hipLaunchKernelGGL(mcaq_morph_kernel<false>, dim3(2 * blocks + fa.nblocks), dim3(MORPH_THREADS), dyn, stream, a, stride, fa);
+    const int limit = morph_lds_budget();
+    int wg = 0;
+    dyn = 0;
+    for (int i = 0; i < nscales; ++i) {
+      const MorphScale& S = a.s[i];
+      a.wg_begin[i] = wg;
+      a.ipw[i] = 1; a.pstride[i] = 0; a.gstride[i] = 0;
+      if (!(S.flags & F_PHI)) continue;
+      if (!mode && !S.gscratch) return (int)hipErrorInvalidValue;
+      const int pb = (plane_bytes(S.Hc, S.Wc) + 15) & ~15;
+      a.ipw[i] = morph_ipw(S, mode, limit);
+      a.pstride[i] = mode ? pb : stride;
+      a.gstride[i] = (mode ? pb : 0) + fixed_bytes();
+      dyn = imax_((int)dyn, a.ipw[i] * a.gstride[i]);
+      wg += 2 * ((S.B + a.ipw[i] - 1) / a.ipw[i]);
     }
+    a.wg_begin[nscales] = wg;
+    if (fa.nblocks > 0 && dyn < (size_t)(8 * MORPH_THREADS)) dyn = 8 * MORPH_THREADS;  // finalize_body's LDS
+    const int grid = wg + fa.nblocks;
+    static int set[2] = {0, 0};  // raise the dynamic LDS limit once (not during graph capture)
+    const void* fn = mode ? (const void*)mcaq_morph_kernel<true> : (const void*)mcaq_morph_kernel<false>;
+    if ((int)dyn > set[mode]) {
+      hipError_t ae = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, limit);
+      if (ae != hipSuccess) return (int)ae;
+      set[mode] = limit;
+    }
+    if (mode) hipLaunchKernelGGL(mcaq_morph_kernel<true>, dim3(grid), dim3(MORPH_THREADS), dyn, stream, a, fa);
+    else hipLaunchKernelGGL(mcaq_morph_kernel<false>, dim3(grid), dim3(MORPH_THREADS), dyn, stream, a, fa);
     hipError_t le = hipGetLastError();
     if (le != hipSuccess) return (int)le;
   }
   if (any_tiles) {
-    if (tlds > MCAQ_MORPH_LDS_LIMIT - 1024) return (int)hipErrorInvalidValue;
-    // stage the weight blobs in LDS when they fit beside the tile arrays
-    const int wlds = tlds + weights_lds_bytes() + 64 <= MCAQ_MORPH_LDS_LIMIT - 1024;
-    if (wlds) tlds += weights_lds_bytes() + 64;
-    static int set_tiles = 0;
-    if (tlds > set_tiles) {
-      hipError_t ae = hipFuncSetAttribute((const void*)mcaq_tiles_kernel,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, MCAQ_MORPH_LDS_LIMIT - 1024);
-      if (ae != hipSuccess) return (int)ae;
-      set_tiles = MCAQ_MORPH_LDS_LIMIT - 1024;
+    // pass B packing: one image per workgroup when it has more than 32 tiles
+    // (one MLP block per wave), else 4 images of one wave each
+    int twg = 0, per = 0;
+    for (int i = 0; i < nscales; ++i) {
+      const MorphScale& S = a.s[i];
+      a.twg_begin[i] = twg;
+      a.tipw[i] = 1; a.tgstride[i] = 0;
+      if (!(S.flags & (F_PHI | F_CMLP | F_MAPPER | F_SOFTMASK))) continue;
+      const int NT = S.ht * S.wt;
+      const int G = imin_(TILES_THREADS, 64 * ((NT + 31) / 32));
+      a.tipw[i] = TILES_THREADS / G;
+      a.tgstride[i] = (tiles_lds_bytes(S.H, S.W, NT) + 15) & ~15;
+      per = imax_(per, a.tipw[i] * a.tgstride[i]);
+      twg += (S.B + a.tipw[i] - 1) / a.tipw[i];
     }
-    hipLaunchKernelGGL(mcaq_tiles_kernel, dim3(blocks), dim3(TILES_THREADS), (size_t)tlds, stream, a, wlds);
+    a.twg_begin[nscales] = twg;
+    const int lim = MCAQ_MORPH_LDS_LIMIT - 1024;
+    if (per > lim) return (int)hipErrorInvalidValue;
+    // stage the weight blobs in LDS when they fit beside the tile arrays
+    const int wlds = per + weights_lds_bytes() <= lim && !(xskip() & 4);
+    const size_t tdyn = (size_t)per + (wlds ? weights_lds_bytes() : 0);
+    static int set_tiles = 0;
+    if ((int)tdyn > set_tiles) {
+      hipError_t ae = hipFuncSetAttribute((const void*)mcaq_tiles_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+      if (ae != hipSuccess) return (int)ae;
+      set_tiles = lim;
+    }
+    hipLaunchKernelGGL(mcaq_tiles_kernel, dim3(twg), dim3(TILES_THREADS), tdyn, stream, a, wlds);
   }
   return (int)hipGetLastError();
 }
 
 int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream) {
+  if (xskip() & 2) return 0;
   if (nscales < 1 || nscales > 3) return (int)hipErrorInvalidValue;
   QuantArgs a;
   int units = 0;

@@ -64,6 +64,12 @@ using MorphScale = mcaq_morph_scale;  // include/mcaq_hip.h
 struct MorphArgs {
   MorphScale s[3];
   int nscales;
+  // pass A packing (set by the launcher): images per workgroup, LDS bytes per
+  // image group (planes + shared, or shared only), plane bytes per image, and
+  // the first workgroup of each scale (wg_begin[nscales] = pass A workgroups)
+  int ipw[3], gstride[3], pstride[3], wg_begin[4];
+  // pass B packing: images per workgroup, LDS bytes per image, first workgroup
+  int tipw[3], tgstride[3], twg_begin[4];
 };
 
 // bit planes
@@ -642,9 +648,6 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, P
   const int Hc = S.Hc, Wc = S.Wc, P = Hc * Wc, T = S.tile, wt = S.wt, NT = S.ht * wt;
   const int WPR = pl.WPR, RS = WPR * 32;   // words / bit slots per row
   const float fT2 = (float)(T * T);
-  float* tiles = sh.tiles;
-  const int QPR = (Wc + 3) >> 2;           // 4-pixel quads per row
-  const int NQ = Hc * QPR;
 
   MSTAMP_INIT(b == 0 ? 16 * role : -1);   // diagnostic build: image 0, slots 0-9 / 16-25
   MSTAMP(0);
@@ -1264,17 +1267,6 @@ enum : int {
   WL_FLOATS = WL_SM + ((SM_SIZE + 3) & ~3),
 };
 MCAQ_HD int weights_lds_bytes() { return 4 * WL_FLOATS; }
-// float4 index inside a blob of the u-th staged float4 (the ranges the device
-// path reads; all range bounds are multiples of 4 floats)
-MCAQ_HD int cm_q(int u) {
-  const int n1 = (CM_W2 - CM_B1) >> 2;
-  return u < n1 ? (CM_B1 >> 2) + u : (CM_B2 >> 2) + (u - n1);
-}
-MCAQ_HD int mm_q(int u) {
-  const int n1 = (MM_W2 - MM_B1) >> 2, n2 = (MM_W3 - MM_B2) >> 2;
-  return u < n1 ? (MM_B1 >> 2) + u : (u < n1 + n2 ? (MM_B2 >> 2) + (u - n1) : (MM_B3 >> 2) + (u - n1 - n2));
-}
-
 // sequential row-major sum of a K x K window of a global plane (adaptive_avg_pool
 // order), all loads issued together
 template <int K>
@@ -1290,76 +1282,101 @@ MCAQ_HD float window_sum_t(const float* a, int W, int h0, int w0) {
   return s;
 }
 
-// ---- pass B: per-image tile work (one 256-thread workgroup per image):
-// phi assembly, complexity MLP, bilateral, normalisation, bit mapper, soft
-// mask (tile values; the m plane itself only on request).
-// LDS: Shared (fixed + tiles) | extra | bilateral weights (25 NT floats) |
-// staged weight blobs (when `wlds`).
+// Copy of the weight ranges the device MLPs read into the staged blob `wl`
+// (every thread of the workgroup; wtid / wnthr: its index and count), and of
+// this image's tile partials into tiles[t][T_TMP..T_TMP+32), all loads issued
+// before the first store; addresses by selects only (no divergent branches
+// between the loads).
+#if defined(__HIP_DEVICE_COMPILE__)
+MCAQ_HD void stage_tiles(const Ctx& ctx, const MorphScale& S, int b, float* tiles, float* wl, int wtid, int wnthr) {
+  const int NT = S.ht * S.wt;
+  // tile partials: NT rows of 8 float4 (tile_tmp rows are contiguous)
+  const int q_t = (S.flags & F_PHI) ? NT * 8 : 0;
+  const float4* tsrc = reinterpret_cast<const float4*>(S.tile_tmp + (size_t)b * NT * TT_STRIDE);
+  // weights: [CM_B1, CM_W2) + [CM_B2, end) of the complexity MLP, [MM_B1, MM_W2) +
+  // [MM_B2, MM_W3) + [MM_B3, end) of the mapper, the whole soft-mask net
+  const int c1 = (CM_W2 - CM_B1) >> 2, c2 = ((CM_BLOB + 3) >> 2) - (CM_B2 >> 2);
+  const int m1 = (MM_W2 - MM_B1) >> 2, m2 = (MM_W3 - MM_B2) >> 2, m3 = ((MM_BLOB + 3) >> 2) - (MM_B3 >> 2);
+  const int q_c = (wl && (S.flags & F_CMLP)) ? c1 + c2 : 0;
+  const int q_m = (wl && (S.flags & F_MAPPER) && !(S.flags & F_MAP_LINEAR)) ? m1 + m2 + m3 : 0;
+  const int q_s = (wl && (S.flags & F_SOFTMASK)) ? (SM_SIZE + 3) >> 2 : 0;
+  const int nw = q_c + q_m + q_s;
+  const uintptr_t pc = (uintptr_t)S.cmlp, pm = (uintptr_t)S.mapper, ps = (uintptr_t)S.smask;
+  // float4 index u of the weight copy -> source address, float4 offset in wl
+  struct WSrc { const float4* p; int dq; };
+  auto wsrc = [&](int u) -> WSrc {
+    const int v = u - q_c, z = v - q_m;
+    const int qc = u < c1 ? (CM_B1 >> 2) + u : (CM_B2 >> 2) + (u - c1);
+    const int qm = v < m1 ? (MM_B1 >> 2) + v : (v < m1 + m2 ? (MM_B2 >> 2) + (v - m1) : (MM_B3 >> 2) + (v - m1 - m2));
+    const bool inc = u < q_c, inm = !inc && v < q_m;
+    const int q = inc ? qc : (inm ? qm : z);
+    // bit-mask select (a ternary chain becomes a private-memory lookup table)
+    const uintptr_t mc = (uintptr_t)0 - (uintptr_t)inc, mm = (uintptr_t)0 - (uintptr_t)inm;
+    const uintptr_t base = (pc & mc) | (pm & mm) | (ps & ~(mc | mm));
+    return WSrc{reinterpret_cast<const float4*>(base) + q, (inc ? (WL_CM >> 2) : (inm ? (WL_MM >> 2) : (WL_SM >> 2))) + q};
+  };
+  constexpr int KT = 4, KW = 8;
+  float4* wl4 = reinterpret_cast<float4*>(wl);
+  if (q_t <= KT * ctx.nthr && nw <= KW * wnthr) {
+    float4 vt[KT], vw[KW];
+    int dw[KW];
+#pragma unroll
+    for (int i = 0; i < KW; ++i) {
+      const int u = wtid + i * wnthr;
+      const WSrc ws = wsrc(u < nw ? u : 0);
+      dw[i] = ws.dq;
+      vw[i] = nw > 0 ? *ws.p : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < KT; ++i) {
+      const int u = ctx.tid + i * ctx.nthr;
+      vt[i] = q_t > 0 ? tsrc[u < q_t ? u : 0] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < KW; ++i) if (wtid + i * wnthr < nw) wl4[dw[i]] = vw[i];
+#pragma unroll
+    for (int i = 0; i < KT; ++i) {
+      const int u = ctx.tid + i * ctx.nthr;
+      if (u < q_t) reinterpret_cast<float4*>(tiles + (u >> 3) * TILE_FLOATS + T_TMP)[u & 7] = vt[i];
+    }
+  } else {
+    for (int u = wtid; u < nw; u += wnthr) { const WSrc ws = wsrc(u); wl4[ws.dq] = *ws.p; }
+    MFOR(u, q_t) reinterpret_cast<float4*>(tiles + (u >> 3) * TILE_FLOATS + T_TMP)[u & 7] = tsrc[u];
+  }
+}
+#endif
+
+// ---- pass B: per-image tile work, one group of threads per image (small
+// images share a workgroup): phi assembly, complexity MLP, bilateral,
+// normalisation, bit mapper, soft mask (tile values; the m plane itself only
+// on request).  LDS per image: Shared (fixed + tiles) | extra | bilateral
+// weights (25 NT floats); the staged weight blobs `wl` (or null) belong to the
+// workgroup.
 MCAQ_HD int tiles_lds_bytes(int H, int W, int NT) {
   return fixed_bytes() + tile_bytes(NT) + extra_bytes(H, W, NT) + 100 * NT;
 }
 
-MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh, int wlds) {
+MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh, float* wl, int wtid, int wnthr) {
   const int ht = S.ht, wt = S.wt, NT = ht * wt;
   float* tiles = sh.tiles;
   float* extra = tiles + NT * TILE_FLOATS;            // compact per-tile arrays / tables
   float* wbuf = (float*)((char*)extra + extra_bytes(S.H, S.W, NT));
-  float* wl = wbuf + ((25 * NT + 3) & ~3);            // staged weights (wlds)
   const float* Pc = S.cmlp;
   const float* Pmap = S.mapper;
   const float* Pm = S.smask;
   MSTAMP_INIT(b == 0 ? 0 : -1);
   MSTAMP(10);
-  // One batched round trip: the per-tile partials of pass A and the weight
-  // blobs this launch needs go to LDS together (16-byte loads), so the phi
-  // assembly and the MLP / conv loops read LDS instead of L2.
+#if defined(__HIP_DEVICE_COMPILE__)
+  stage_tiles(ctx, S, b, tiles, wl, wtid, wnthr);
+  if (wl && (S.flags & F_CMLP)) Pc = wl + WL_CM;
+  if (wl && (S.flags & F_MAPPER) && !(S.flags & F_MAP_LINEAR)) Pmap = wl + WL_MM;
+  if (wl && (S.flags & F_SOFTMASK)) Pm = wl + WL_SM;
+#else
+  (void)wl; (void)wtid; (void)wnthr;
   int S_ = 0;
   for (int s = 2; s <= S.tile; s *= 2) ++S_;
   const int NI = 20 + S_;
   const float* ttmp = S.tile_tmp + (size_t)b * NT * TT_STRIDE;
-#if defined(__HIP_DEVICE_COMPILE__)
-  {
-    // segments of float4s: [0] tile partials (row t: NI floats of 32 -> tiles[t][T_TMP..]),
-    // [1] complexity MLP, [2] mapper, [3] soft-mask net
-    const int q_t = (S.flags & F_PHI) ? NT * ((NI + 3) >> 2) : 0;
-    // device-side MLPs read the MFMA operand copies, biases and norm terms, not
-    // the plain weight matrices: stage [CM_B1, CM_W2) and [CM_B2, end) of the
-    // complexity MLP, [MM_B1, MM_W2), [MM_B2, MM_W3), [MM_B3, end) of the mapper
-    const int q_c = (wlds && (S.flags & F_CMLP)) ? ((CM_BLOB + 3) >> 2) - (CM_B2 >> 2) + ((CM_W2 - CM_B1) >> 2) : 0;
-    const int q_m = (wlds && (S.flags & F_MAPPER) && !(S.flags & F_MAP_LINEAR))
-                        ? ((MM_BLOB + 3) >> 2) - (MM_B3 >> 2) + ((MM_W2 - MM_B1) >> 2) + ((MM_W3 - MM_B2) >> 2) : 0;
-    const int q_s = (wlds && (S.flags & F_SOFTMASK)) ? (SM_SIZE + 3) >> 2 : 0;
-    const int qpt = (NI + 3) >> 2;
-    const int n = q_t + q_c + q_m + q_s;
-    auto src = [&](int u) -> const float4* {
-      if (u < q_t) { const int t = u / qpt; return reinterpret_cast<const float4*>(ttmp + t * TT_STRIDE) + (u - t * qpt); }
-      u -= q_t;
-      if (u < q_c) return reinterpret_cast<const float4*>(S.cmlp) + cm_q(u);
-      u -= q_c;
-      if (u < q_m) return reinterpret_cast<const float4*>(S.mapper) + mm_q(u);
-      return reinterpret_cast<const float4*>(S.smask) + (u - q_m);
-    };
-    auto dst = [&](int u) -> float4* {
-      if (u < q_t) { const int t = u / qpt; return reinterpret_cast<float4*>(tiles + t * TILE_FLOATS + T_TMP) + (u - t * qpt); }
-      u -= q_t;
-      if (u < q_c) return reinterpret_cast<float4*>(wl + WL_CM) + cm_q(u);
-      u -= q_c;
-      if (u < q_m) return reinterpret_cast<float4*>(wl + WL_MM) + mm_q(u);
-      return reinterpret_cast<float4*>(wl + WL_SM) + (u - q_m);
-    };
-    constexpr int K = 20;
-    for (int base = 0; base < n; base += K * ctx.nthr) {
-      float4 v[K];
-#pragma unroll
-      for (int i = 0; i < K; ++i) { const int u = base + ctx.tid + i * ctx.nthr; v[i] = *src(u < n ? u : 0); }
-#pragma unroll
-      for (int i = 0; i < K; ++i) { const int u = base + ctx.tid + i * ctx.nthr; if (u < n) *dst(u) = v[i]; }
-    }
-    if (q_c) Pc = wl + WL_CM;
-    if (q_m) Pmap = wl + WL_MM;
-    if (q_s) Pm = wl + WL_SM;
-  }
-#else
   if (S.flags & F_PHI)
     MFOR(u, NT * NI) {
       const int t = u / NI, it = u - (u / NI) * NI;

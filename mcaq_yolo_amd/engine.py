@@ -210,13 +210,20 @@ class HookPlan:
             self._qs = qs
         self._n = n
 
+    def launch_stats(self, stream=None):
+        """Pass 1 only."""
+        abi.check(self.lib.mcaq_stats(self._st, self._n, _stream_handle(stream)), "mcaq_stats")
+
+    def launch_morph(self, stream=None):
+        """Morphology passes A + B (+ the channel min/max reduction); needs pass 1."""
+        nf = self._n if self._fz is not None else 0
+        abi.check(self.lib.mcaq_morph_finalize(self._mo, self._n, self._fz, nf, _stream_handle(stream)),
+                  "mcaq_morph_finalize")
+
     def launch_pre(self, stream=None):
         """Pass 1 + morphology (+ the channel min/max reduction)."""
-        L = self.lib
-        sh = _stream_handle(stream)
-        abi.check(L.mcaq_stats(self._st, self._n, sh), "mcaq_stats")
-        nf = self._n if self._fz is not None else 0
-        abi.check(L.mcaq_morph_finalize(self._mo, self._n, self._fz, nf, sh), "mcaq_morph_finalize")
+        self.launch_stats(stream)
+        self.launch_morph(stream)
 
     def launch_quant(self, stream=None):
         """Pass 2."""

@@ -227,3 +227,15 @@ def test_stats_pass_orders(dev, blobs, shape):
     assert np.array_equal(out["absmean"], O.abs_channel_mean(x)), "absmean"
     assert np.array_equal(out["xmin"], x.min(axis=(0, 2, 3))), "min"
     assert np.array_equal(out["xmax"], x.max(axis=(0, 2, 3))), "max"
+
+
+@pytest.mark.parametrize("shape", [(5, 16, 20, 20), (6, 12, 40, 40), (3, 8, 24, 24)])
+def test_packed_workgroups_vs_oracle(dev, blobs, shape):
+    """Small images share a workgroup (pass A: up to 8 per 1024 threads, pass B:
+    4 per 256); batches that leave a workgroup partly filled (its spare groups
+    recompute the last image) stay bit-exact for every image."""
+    rng = np.random.default_rng(shape[0] * 31 + shape[2])
+    x = (rng.standard_normal(shape) * 1.5).astype(f32)
+    x = np.where(x > 0, x, x * f32(0.1)).astype(f32)
+    out = run_plan(dev, blobs, [x], 8, "mlp")[0]
+    check_against_oracle(out, x, blobs[0], 8, "mlp")
