@@ -155,8 +155,10 @@ class SplitRunner:
         if len(plans) < self.LAG + 1:
             raise ValueError("--schedule split needs --pipeline >= %d" % (self.LAG + 1))
         self.plans, self.pg = plans, pg
+        # the latency-bound morphology gets the high-priority queues
+        prio = int(os.environ.get("MCAQ_MORPH_PRIO", "-1"))
         self.S = torch.cuda.Stream()
-        self.M = [torch.cuda.Stream(), torch.cuda.Stream()]
+        self.M = [torch.cuda.Stream(priority=prio), torch.cuda.Stream(priority=prio)]
         self.ev_st = [torch.cuda.Event() for _ in plans]
         self.ev_mo = [torch.cuda.Event() for _ in plans]
         self.i = 0       # batches started

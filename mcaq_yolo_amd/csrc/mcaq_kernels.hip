@@ -740,13 +740,19 @@ static int morph_plan(const MorphScale* s, int n, int* lds_mode, int* plane_stri
 }
 
 // images per pass A workgroup: the most (power of two, <= 16) whose planes fit
-// the LDS budget while each image keeps >= 64 threads and <= 8 pixels per thread
+// the LDS budget while each image keeps >= 64 threads and <= 4 pixels per thread
+static int morph_ppt() {   // max pixels per thread of a packed image (experiment knob MCAQ_PPT)
+  static int v = -1;
+  if (v < 0) { const char* e = getenv("MCAQ_PPT"); v = e ? atoi(e) : 4; if (v < 1) v = 4; }
+  return v;
+}
+#define MCAQ_PPT morph_ppt()
 static int morph_ipw(const MorphScale& S, int mode, int limit) {
   if (!mode) return 1;   // planes in global scratch: one image per workgroup
   const int per = ((plane_bytes(S.Hc, S.Wc) + 15) & ~15) + fixed_bytes();
   const int P = S.Hc * S.Wc;
   int ipw = 16;
-  while (ipw > 1 && (ipw * per > limit || MORPH_THREADS / ipw < 64 || P > 8 * (MORPH_THREADS / ipw))) ipw >>= 1;
+  while (ipw > 1 && (ipw * per > limit || MORPH_THREADS / ipw < 64 || P > MCAQ_PPT * (MORPH_THREADS / ipw))) ipw >>= 1;
   return ipw;
 }
 
