@@ -734,3 +734,78 @@ def hook_forward(x, P, grid_size=8, mapper="mlp", temperature=1.0, smooth=True,
 def load_weights(path):
     d = np.load(path)
     return {k: d[k].astype(f32) if d[k].dtype.kind == "f" else d[k] for k in d.files}
+
+
+# ---------------------------------------------------------------------------
+# QAT quantizer: the training branch (BASELINE config 5)
+# ---------------------------------------------------------------------------
+def ema_running_stats(x, rmin=None, rmax=None, momentum=0.99):
+    """update_running_stats (quantization.py:319-353), per channel: the first
+    batch takes the batch min/max, later ones r <- momentum*r + (1-momentum)*new
+    (Python scalars rounded to fp32, then fp32 ops: SURVEY App. A.9)."""
+    xmin = x.min(axis=(0, 2, 3)).astype(f32)
+    xmax = x.max(axis=(0, 2, 3)).astype(f32)
+    if rmin is None:
+        return xmin, xmax
+    a, c = f32(momentum), f32(1.0 - momentum)
+    return (((a * rmin).astype(f32) + (c * xmin).astype(f32)).astype(f32),
+            ((a * rmax).astype(f32) + (c * xmax).astype(f32)).astype(f32))
+
+
+def _qdq(x, xmin, xmax, b):
+    """StraightThroughEstimator.forward (quantization.py:74-92) for integer bits b,
+    per-channel parameters: (clamp(rint(x/s + zp)) - zp) * s."""
+    s, zp, qmin, qmax = qparams(xmin, xmax, b)
+    s = s[None, :, None, None]
+    zp = zp[None, :, None, None]
+    t = ((x / s).astype(f32) + zp).astype(f32)
+    q = np.clip(rint32(t), qmin, qmax)
+    return ((q - zp).astype(f32) * s).astype(f32)
+
+
+def qat_forward(x, bits, xmin, xmax, m=None, max_bits=8):
+    """_forward_pytorch training branch (quantization.py:699-727, 733-737):
+    per pixel, with b the nearest-upsampled continuous tile bits,
+    xq = (1 - f) * Q_floor(b)(x) + f * Q_floor(b)+1(x), f = b - floor(b)
+    (Q_floor(b)+1 := Q_floor(b) past max_bits), y = xq * m.  Returns (y, parts)."""
+    B, C, H, W = x.shape
+    Ht, Wt = bits.shape[1:]
+    bits = bits.astype(f32)
+    bfl = np.floor(bits).astype(f32)
+    fr = (bits - bfl).astype(f32)
+    ri, ci = nearest_index(H, Ht), nearest_index(W, Wt)
+    bfu = bfl[:, ri][:, :, ci]
+    fu = fr[:, ri][:, :, ci][:, None]                       # (B, 1, H, W)
+    q_lo = np.zeros_like(x)
+    q_hi = np.zeros_like(x)
+    for bv in np.unique(bfu):
+        lo = int(bv)
+        ql = _qdq(x, xmin, xmax, lo)
+        qh = _qdq(x, xmin, xmax, lo + 1) if lo + 1 <= max_bits else ql
+        sel = (bfu == bv)[:, None]
+        q_lo = np.where(sel, ql, q_lo)
+        q_hi = np.where(sel, qh, q_hi)
+    one_m_f = (f32(1.0) - fu).astype(f32)
+    xq = ((one_m_f * q_lo).astype(f32) + (fu * q_hi).astype(f32)).astype(f32)
+    y = (xq * m[:, None]).astype(f32) if m is not None else xq
+    return y, {"xq": xq, "q_lo": q_lo, "q_hi": q_hi, "fu": fu, "one_m_f": one_m_f, "ri": ri, "ci": ci}
+
+
+def qat_backward(g, x, bits, xmin, xmax, m=None, max_bits=8):
+    """Gradients of qat_forward through the reference's autograd graph, with the
+    STE identity dQ/dx = 1 (quantization.py:94-118):
+      grad_x    = gm*(1-f) + gm*f,  gm = g*m               (elementwise, exact order)
+      grad_m    = sum_c g*xq                               (B, H, W)
+      grad_bits = sum over each tile's pixels of sum_c gm*(q_hi - q_lo)   (B, Ht, Wt)
+    The two sums are accumulated in float64 (ATen's reduction order is not
+    pinned; the kernels are compared within tolerance there)."""
+    B, C, H, W = x.shape
+    Ht, Wt = bits.shape[1:]
+    _, I = qat_forward(x, bits, xmin, xmax, m, max_bits)
+    gm = (g * m[:, None]).astype(f32) if m is not None else g.astype(f32)
+    gx = ((gm * I["one_m_f"]).astype(f32) + (gm * I["fu"]).astype(f32)).astype(f32)
+    gmask = (g.astype(f64) * I["xq"].astype(f64)).sum(axis=1) if m is not None else None
+    gfu = (gm.astype(f64) * (I["q_hi"].astype(f64) - I["q_lo"].astype(f64))).sum(axis=1)   # (B, H, W)
+    gb = np.zeros((B, Ht, Wt), f64)
+    np.add.at(gb, (np.arange(B)[:, None, None], I["ri"][None, :, None], I["ci"][None, None, :]), gfu)
+    return gx, gb, gmask
