@@ -14,6 +14,10 @@
  *          (core/morphology.py:939-973), bit mapper (core/bit_allocation.py:
  *          42-80, 218-280), quantizer (core/quantization.py:604-746), split
  *          into the three HBM passes of the fused design.
+ *   mcaq_qat_forward / mcaq_qat_backward / mcaq_ema_stats
+ *       <- SpatialAdaptiveQuantization training branch + StraightThroughEstimator
+ *          + update_running_stats (mcaq_yolo/core/quantization.py:699-727,
+ *          69-118, 319-353): the QAT quantizer of BASELINE config 5.
  * Up to three hook scales (C3/C4/C5) are processed by one launch.
  */
 #ifndef MCAQ_HIP_H_
@@ -32,7 +36,7 @@ typedef void* hipStream_t;
 extern "C" {
 #endif
 
-#define MCAQ_ABI_VERSION 3
+#define MCAQ_ABI_VERSION 4
 /* largest dynamic LDS request of the morph kernel (gfx950: 160 KiB per CU) */
 #define MCAQ_MORPH_LDS_LIMIT 163840
 
@@ -139,6 +143,39 @@ typedef struct {
   int unit_begin;      /* set by the launcher */
 } mcaq_quant_scale;
 int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream);
+
+/* ---- QAT quantizer (training branch) --------------------------------------
+ * forward:  y = ((1-f) Q_lo(x) + f Q_hi(x)) * m, lo = floor(b), f = b - lo,
+ *           Q_hi = Q_lo when lo = 8 (quantization.py:699-727, 733-737); b is
+ *           the nearest-upsampled CONTINUOUS tile bit map, Q_k the
+ *           per-channel k-bit quant/dequant with xmin/xmax (running stats).
+ * backward: gx = gm(1-f) + gm f with gm = g m (straight-through,
+ *           quantization.py:94-118); gm_out(p) = sum_c g xq (NULL: skip);
+ *           gb(t) = sum over tile t's pixels of sum_c (gm Q_hi - gm Q_lo)
+ *           (NULL: skip).  work: mcaq_qat_work_floats(B,C,H,W) floats of
+ *           device scratch (per-32-channel-slice partials of both sums). */
+typedef struct {
+  const float* x;      /* (B, C, H, W) */
+  const float* g;      /* (B, C, H, W) upstream gradient (backward) */
+  float* y;            /* (B, C, H, W) forward output */
+  float* gx;           /* (B, C, H, W) backward output */
+  float* gm;           /* (B, H, W) grad of m, or NULL */
+  float* gb;           /* (B, ht, wt) grad of the bit map, or NULL */
+  float* work;         /* backward scratch */
+  const float* bits;   /* (B, ht, wt) continuous bits */
+  const float* m;      /* (B, H, W) soft mask, or NULL */
+  const float* xmin;   /* (C) */
+  const float* xmax;   /* (C) */
+  int B, C, H, W, ht, wt;
+  int unit_begin, block_begin;  /* set by the launcher */
+} mcaq_qat_scale;
+int mcaq_qat_forward(const mcaq_qat_scale* scales, int nscales, hipStream_t stream);
+int mcaq_qat_backward(const mcaq_qat_scale* scales, int nscales, hipStream_t stream);
+size_t mcaq_qat_work_floats(int B, int C, int H, int W);
+/* running <- fp32(momentum) running + fp32(1 - momentum) batch, per channel
+ * (first != 0: running <- batch), in place. */
+int mcaq_ema_stats(const float* batch_min, const float* batch_max, float* running_min, float* running_max,
+                   int C, double momentum, int first, hipStream_t stream);
 
 int mcaq_abi_version(void);
 

@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libmcaq_hip.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -41,13 +41,21 @@ class QuantScale(ctypes.Structure):
                 ("bits_lo", I), ("nbits", I), ("compat_tile_h", I), ("compat_tile_w", I), ("unit_begin", I)]
 
 
+class QatScale(ctypes.Structure):
+    _fields_ = [("x", P), ("g", P), ("y", P), ("gx", P), ("gm", P), ("gb", P), ("work", P),
+                ("bits", P), ("m", P), ("xmin", P), ("xmax", P),
+                ("B", I), ("C", I), ("H", I), ("W", I), ("ht", I), ("wt", I),
+                ("unit_begin", I), ("block_begin", I)]
+
+
 # morph stage flags (mcaq_morph.h)
 F_PHI, F_CMLP, F_MAPPER, F_SOFTMASK = 1, 2, 4, 8
 F_CONT, F_HAS_T, F_NORM_C, F_MAP_LINEAR = 16, 32, 64, 128
 F_BIN_OTSU, F_NO_EULER = 256, 512
 
 EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats", "mcaq_stats_units",
-           "mcaq_finalize", "mcaq_morph", "mcaq_morph_finalize", "mcaq_morph_scratch_bytes", "mcaq_quant")
+           "mcaq_finalize", "mcaq_morph", "mcaq_morph_finalize", "mcaq_morph_scratch_bytes", "mcaq_quant",
+           "mcaq_qat_forward", "mcaq_qat_backward", "mcaq_qat_work_floats", "mcaq_ema_stats")
 
 _LIB = None
 
@@ -61,7 +69,8 @@ def _declare(lib):
     lib.mcaq_launch_spatial_quantization.restype = I
     lib.mcaq_launch_spatial_quantization.argtypes = [P, P, P, P, P, P] + [I] * 8 + [P]
     for n, st in (("mcaq_stats", StatsScale), ("mcaq_finalize", FinalizeScale),
-                  ("mcaq_morph", MorphScale), ("mcaq_quant", QuantScale)):
+                  ("mcaq_morph", MorphScale), ("mcaq_quant", QuantScale),
+                  ("mcaq_qat_forward", QatScale), ("mcaq_qat_backward", QatScale)):
         f = getattr(lib, n)
         f.restype = I
         f.argtypes = [ctypes.POINTER(st), I, P]
@@ -71,6 +80,10 @@ def _declare(lib):
     lib.mcaq_stats_units.argtypes = [I, I, I, I]
     lib.mcaq_morph_scratch_bytes.restype = ctypes.c_size_t
     lib.mcaq_morph_scratch_bytes.argtypes = [I, I, I, I, I]
+    lib.mcaq_qat_work_floats.restype = ctypes.c_size_t
+    lib.mcaq_qat_work_floats.argtypes = [I, I, I, I]
+    lib.mcaq_ema_stats.restype = I
+    lib.mcaq_ema_stats.argtypes = [P, P, P, P, I, ctypes.c_double, I, P]
     return lib
 
 

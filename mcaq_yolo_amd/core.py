@@ -14,16 +14,23 @@ runs through libmcaq_hip.so (include/mcaq_hip.h); there is no CPU path - a
 non-CUDA tensor or a missing library raises.  The numeric contract is the
 reference's pure-PyTorch path (bit-exact decisions, tests/test_core_gpu.py).
 
-Scope: the inference path (eval mode).  The training-only branches - the
-fractional-bit STE quantizer, batch-statistics BatchNorm in the mapper,
-autograd through the complexity MLP - are the next row of SURVEY.md 8(f) and
-raise NotImplementedError here instead of silently computing something else.
+Training (QAT, BASELINE config 5): the quantizer's per-element work - EMA
+running statistics, the fractional-bit forward and the straight-through
+backward - runs in the HIP kernels (mcaq_qat_forward / mcaq_qat_backward,
+mcaq_ema_stats) behind a torch.autograd.Function; the soft mask's forward is
+the HIP kernel and its (tile-sized) backward is recomputed with torch ops.
+The complexity MLP + bilateral and the bit mapper in train mode are tile-level
+(N_tiles x <=64) networks with batch-statistics BatchNorm: they run as torch
+autograd ops on the GPU, restating morphology.py:309-354, 939-973 and
+bit_allocation.py:199-280 (phi itself is no-grad side information computed by
+the morph kernel, as in the reference).
 """
 import ctypes
 from typing import Optional
 
 import torch
 import torch.nn as nn
+import torch.nn.functional as F
 
 from . import abi
 from .engine import tile_size
@@ -264,11 +271,35 @@ class MorphologicalComplexityAnalyzer(nn.Module):
         phi, _ = self._run(features, want_c=False)
         return phi, self._detailed(phi)
 
+    @staticmethod
+    def bilateral_filter(complexity_map, sigma_spatial: float = 2.0, sigma_range: float = 0.1,
+                         kernel_size: int = 5):
+        """morphology.py:309-354, differentiable torch restatement (training path;
+        inference runs it inside the morph kernel)."""
+        B, H, W = complexity_map.shape
+        pad = kernel_size // 2
+        patches = F.unfold(F.pad(complexity_map.unsqueeze(1), (pad, pad, pad, pad), mode="replicate"),
+                           kernel_size)
+        center = complexity_map.reshape(B, 1, H * W)
+        coords = torch.arange(kernel_size, dtype=torch.float32, device=complexity_map.device) - pad
+        yy, xx = torch.meshgrid(coords, coords, indexing="ij")
+        spatial_w = torch.exp(-(yy ** 2 + xx ** 2) / (2 * sigma_spatial ** 2)).reshape(1, -1, 1)
+        range_w = torch.exp(-((patches - center) ** 2) / (2 * sigma_range ** 2))
+        weights = spatial_w * range_w
+        filtered = (weights * patches).sum(dim=1) / (weights.sum(dim=1) + 1e-8)
+        return filtered.reshape(B, H, W)
+
     def forward(self, features: torch.Tensor, return_detailed: bool = False):
         if self.training and torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            raise NotImplementedError("training-mode analyzer (autograd through the complexity MLP) is the QAT "
-                                      "path, SURVEY.md 8(f) rank 2; call .eval() or use torch.no_grad()")
-        phi, c = self._run(features, want_c=True)
+            # morphology.py:939-973 with autograd into complexity_mlp: phi is
+            # no-grad side information (morph kernel), the MLP + bilateral run
+            # as torch ops on the (B*ht*wt, 8) tile features
+            phi, _ = self._run(features, want_c=False)
+            B, ht, wt, _ = phi.shape
+            c = self.complexity_mlp(phi.reshape(-1, 8)).reshape(B, ht, wt)
+            c = self.bilateral_filter(c).clamp(0.0, 1.0)
+        else:
+            phi, c = self._run(features, want_c=True)
         if return_detailed:
             return c, self._detailed(phi)
         return c
@@ -370,6 +401,25 @@ class ComplexityToBitMappingNetwork(nn.Module):
                 if isinstance(module, (nn.Linear, nn.BatchNorm1d)):
                     module.weight.data = torch.abs(module.weight.data)
 
+    def create_augmented_features(self, complexity: torch.Tensor) -> torch.Tensor:
+        """bit_allocation.py:199-216: z0 = [C, C^2, log1p C]."""
+        return torch.cat([complexity, complexity ** 2, torch.log1p(complexity)], dim=-1)
+
+    def _forward_train(self, complexity, temperature, return_continuous):
+        """bit_allocation.py:218-280 in train mode (BatchNorm over the batch's
+        tiles, straight-through clamp and round) as torch autograd ops."""
+        c = _normalize_complexity_shape(complexity).clamp(0.0, 1.0)
+        B, H, W = c.shape
+        h = self.mapping_network(self.create_augmented_features(c.reshape(-1, 1)))
+        bit_map = (self.min_bits + (self.max_bits - self.min_bits) * h).reshape(B, H, W)
+        if temperature is not None:
+            bit_map = bit_map * max(float(temperature), 0.1)
+        clamped = torch.clamp(bit_map, self.min_bits, self.max_bits)
+        bit_map = bit_map + (clamped - bit_map).detach()
+        if not return_continuous:
+            bit_map = bit_map + (torch.round(bit_map) - bit_map).detach()
+        return bit_map
+
     def mapper_blob(self):
         net = self.mapping_network
         ts = list(net.parameters()) + [net[i].running_mean for i in (1, 4, 7)] + \
@@ -379,8 +429,7 @@ class ComplexityToBitMappingNetwork(nn.Module):
     def forward(self, complexity: torch.Tensor, temperature: Optional[float] = None,
                 return_continuous: bool = False) -> torch.Tensor:
         if self.training:
-            raise NotImplementedError("training-mode mapper (batch-statistics BatchNorm, STE backward) is the QAT "
-                                      "path, SURVEY.md 8(f) rank 2; call .eval()")
+            return self._forward_train(complexity, temperature, return_continuous)
         c = _normalize_complexity_shape(complexity)
         return _run_mapper(c, 0, self.min_bits, self.max_bits, temperature, return_continuous,
                            mapper_blob=self.mapper_blob())
@@ -438,12 +487,114 @@ class LearnedSoftMask(nn.Module):
         return out
 
     def forward(self, bit_map: torch.Tensor, x: torch.Tensor, absmean: Optional[torch.Tensor] = None):
+        if torch.is_grad_enabled() and (bit_map.requires_grad or any(p.requires_grad for p in self.net.parameters())):
+            _need_cuda(x, "x")
+            if absmean is None:
+                B, C, H, W = x.shape
+                absmean = torch.empty(B, H, W, device=x.device)
+                _run_stats(_f32c(x), absmean=absmean)
+            return _SoftMaskFn.apply(bit_map, absmean, self, *self.net.parameters())
         return self._run(bit_map, x, absmean, plane=True)
+
+    def _torch_forward(self, bit_map, absmean):
+        """quantization.py:213-239 as torch ops (the backward recomputation);
+        absmean = x.abs().mean(1) from pass 1 (bit-identical to ATen's)."""
+        B, H, W = absmean.shape
+        Ht, Wt = bit_map.shape[-2:]
+        with torch.no_grad():
+            act = F.adaptive_avg_pool2d(absmean.unsqueeze(1), (Ht, Wt))
+            act = act / (act.amax(dim=(2, 3), keepdim=True) + 1e-8)
+        bits_norm = ((bit_map.unsqueeze(1).float() - 2.0) / 6.0).clamp(0.0, 1.0)
+        logits = self.net(torch.cat([bits_norm, act.float()], dim=1))
+        m = torch.softmax(logits, dim=1)[:, :1]
+        m = F.interpolate(m, size=(H, W), mode="nearest")
+        p = self.kernel_size // 2
+        return F.conv2d(F.pad(m, (p, p, p, p), mode="replicate"), self.smooth_kernel)
 
     def tile_values(self, bit_map, x, absmean=None):
         """m per tile before upsampling/smoothing (B, Ht, Wt); the quant pass
         turns it into m(p) on the fly."""
         return self._run(bit_map, x, absmean, plane=False)
+
+
+class _SoftMaskFn(torch.autograd.Function):
+    """m(p) forward by the morph kernel (bit-exact with the reference); backward
+    by recomputing the tile-sized soft-mask net with torch autograd."""
+
+    @staticmethod
+    def forward(ctx, bit_map, absmean, mod, *params):
+        ctx.mod = mod
+        ctx.save_for_backward(bit_map, absmean)
+        B, H, W = absmean.shape
+        m = mod._run(bit_map.detach(), torch.empty(B, 1, H, W, device=absmean.device), absmean, plane=True)
+        return m
+
+    @staticmethod
+    def backward(ctx, gm):
+        bit_map, absmean = ctx.saved_tensors
+        mod = ctx.mod
+        params = list(mod.net.parameters())
+        with torch.enable_grad():
+            b = bit_map.detach().requires_grad_(ctx.needs_input_grad[0])
+            m = mod._torch_forward(b, absmean)
+            ins = ([b] if ctx.needs_input_grad[0] else []) + [p for p in params if p.requires_grad]
+            grads = torch.autograd.grad(m, ins, gm, allow_unused=True) if ins else []
+        it = iter(grads)
+        gb = next(it) if ctx.needs_input_grad[0] else None
+        gp = [next(it) if p.requires_grad else None for p in params]
+        return (gb, None, None) + tuple(gp)
+
+
+def _qat_struct(x, bits, m, xmin, xmax):
+    B, C, H, W = x.shape
+    q = abi.QatScale()
+    q.x, q.bits, q.m, q.xmin, q.xmax = _p(x), _p(bits), _p(m), _p(xmin), _p(xmax)
+    q.B, q.C, q.H, q.W = B, C, H, W
+    q.ht, q.wt = bits.shape[-2], bits.shape[-1]
+    return q
+
+
+def qat_quantize(x, bits, m, xmin, xmax):
+    """Fractional-bit QAT forward (quantization.py:699-727, 733-737) on the HIP
+    kernel: y = ((1-f) Q_floor(b) + f Q_floor(b)+1)(x) * m.  No autograd."""
+    y = torch.empty_like(x)
+    q = _qat_struct(x, bits, m, xmin, xmax)
+    q.y = _p(y)
+    abi.check(abi.lib().mcaq_qat_forward(ctypes.byref(q), 1, _stream()), "mcaq_qat_forward")
+    return y
+
+
+def qat_quantize_backward(g, x, bits, m, xmin, xmax, want_gm=True, want_gb=True):
+    """Straight-through backward (quantization.py:94-118 + the autograd graph of
+    :699-737): (grad_x, grad_bits (B,ht,wt) or None, grad_m (B,H,W) or None)."""
+    B, C, H, W = x.shape
+    L = abi.lib()
+    gx = torch.empty_like(x)
+    gm = torch.empty(B, H, W, device=x.device) if (want_gm and m is not None) else None
+    gb = torch.empty(bits.shape, device=x.device) if want_gb else None
+    work = torch.empty(L.mcaq_qat_work_floats(B, C, H, W), device=x.device)
+    q = _qat_struct(x, bits, m, xmin, xmax)
+    q.g, q.gx, q.gm, q.gb, q.work = _p(g), _p(gx), _p(gm), _p(gb), _p(work)
+    abi.check(L.mcaq_qat_backward(ctypes.byref(q), 1, _stream()), "mcaq_qat_backward")
+    return gx, gb, gm
+
+
+class _QATQuantFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, bit_map, m, xmin, xmax):
+        xf, bits = _f32c(x), _f32c(bit_map)
+        mf = None if m is None else _f32c(m)
+        ctx.save_for_backward(xf, bits, mf, xmin, xmax)
+        return qat_quantize(xf, bits, mf, xmin, xmax)
+
+    @staticmethod
+    def backward(ctx, g):
+        xf, bits, mf, xmin, xmax = ctx.saved_tensors
+        gx, gb, gm = qat_quantize_backward(_f32c(g), xf, bits, mf, xmin, xmax,
+                                           want_gm=ctx.needs_input_grad[2], want_gb=ctx.needs_input_grad[1])
+        if gm is not None:
+            gm = gm.view(mf.shape)
+        return gx, gb, gm, None, None
 
 
 class SpatialAdaptiveQuantization(nn.Module):
@@ -494,32 +645,68 @@ class SpatialAdaptiveQuantization(nn.Module):
         return xmin, xmax
 
     @torch.no_grad()
-    def update_running_stats(self, x: torch.Tensor):
-        """quantization.py:319-353: EMA(momentum) of the batch min/max."""
+    def update_running_stats(self, x: torch.Tensor, absmean: Optional[torch.Tensor] = None):
+        """quantization.py:319-353: EMA(momentum) of the batch min/max (pass 1 +
+        finalize + mcaq_ema_stats; absmean, if given, is filled by the same read)."""
         if bool(self.stats_frozen):
             return
         _need_cuda(x, "x")
         xf = _f32c(x)
-        xmin, xmax = _channel_minmax(xf)
+        xmin, xmax = _channel_minmax(xf, absmean)
         C = x.shape[1]
         if self.per_channel:
             shape = (1, C) + (1,) * (x.dim() - 2)
             nmin, nmax = xmin.view(shape), xmax.view(shape)
         else:
             nmin, nmax = xmin.amin(), xmax.amax()
-        if self.running_min is None:
-            self.running_min, self.running_max = nmin.clone(), nmax.clone()
-        else:
-            self.running_min = self.momentum * self.running_min + (1 - self.momentum) * nmin
-            self.running_max = self.momentum * self.running_max + (1 - self.momentum) * nmax
+        first = self.running_min is None
+        # new tensors (not in place): an earlier forward may hold the old ones
+        rmin, rmax = torch.empty_like(nmin), torch.empty_like(nmax)
+        old_min = nmin if first else self.running_min.float().contiguous()
+        old_max = nmax if first else self.running_max.float().contiguous()
+        if not first and old_min.numel() != nmin.numel():
+            raise RuntimeError("running stats have %d entries, batch has %d" % (old_min.numel(), nmin.numel()))
+        rmin.copy_(old_min)
+        rmax.copy_(old_max)
+        abi.check(abi.lib().mcaq_ema_stats(_p(nmin), _p(nmax), _p(rmin), _p(rmax), nmin.numel(),
+                                           float(self.momentum), 1 if first else 0, _stream()), "mcaq_ema_stats")
+        self.running_min, self.running_max = rmin, rmax
         self.num_batches_tracked += 1
+
+    def _stats_c(self, t, C):
+        t = t.reshape(-1).float()
+        return (t.expand(C) if t.numel() == 1 else t).contiguous()
+
+    def _forward_train(self, x, bit_map):
+        """quantization.py:604-613 + 699-727, 733-737: EMA update, then the
+        fractional-bit straight-through quantizer x m(p)."""
+        _need_cuda(x, "x")
+        _need_cuda(bit_map, "bit_map")
+        B, C, H, W = x.shape
+        if bit_map.dim() != 3 or bit_map.shape[0] != B:
+            raise AssertionError(f"Batch size mismatch: {B} vs {bit_map.shape[0]}")
+        want_m = self.smooth_transitions and self.soft_mask is not None
+        absmean = torch.empty(B, H, W, device=x.device) if want_m else None
+        xf = _f32c(x)
+        if bool(self.stats_frozen):
+            if want_m:
+                _run_stats(xf, absmean=absmean)
+        else:
+            self.update_running_stats(xf, absmean)
+        # _calibrate_minmax (quantization.py:409-434): running stats in train
+        # mode or when frozen, else this batch's min/max
+        if self.running_min is not None and (self.training or bool(self.stats_frozen)):
+            xmin, xmax = self._stats_c(self.running_min, C), self._stats_c(self.running_max, C)
+        else:
+            xmin, xmax = self.batch_minmax(xf)
+        m = self.soft_mask(bit_map, x, absmean=absmean) if want_m else None
+        return _QATQuantFn.apply(x, bit_map, m, xmin, xmax)
 
     def forward(self, x: torch.Tensor, bit_map: torch.Tensor, training: Optional[bool] = None) -> torch.Tensor:
         if training is None:
             training = self.training
         if training:
-            raise NotImplementedError("training-mode quantizer (fractional bits + STE) is the QAT path, "
-                                      "SURVEY.md 8(f) rank 2; use update_running_stats() to calibrate")
+            return self._forward_train(x, bit_map)
         _need_cuda(x, "x")
         _need_cuda(bit_map, "bit_map")
         xf = _f32c(x)

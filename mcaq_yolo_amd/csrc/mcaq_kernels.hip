@@ -10,6 +10,8 @@
 //                                 mapper, soft mask (LDS resident planes)
 //   pass 2  mcaq_quant_kernel     one read of x + one write of y: tile-wise
 //                                 2..8-bit quant/dequant fused with m(p)
+//   QAT     mcaq_qat_kernel       fractional-bit forward / STE backward
+//                                 (mcaq_qat.h)
 //
 // Built with -ffp-contract=off (see mcaq_math.h).
 #include <hip/hip_runtime.h>
@@ -898,3 +900,5 @@ int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream) 
 }
 
 }  // extern "C"
+
+#include "mcaq_qat.h"

@@ -1,0 +1,279 @@
+// mcaq_qat.h - gfx950 kernels of the QAT (training) quantizer: the
+// fractional-bit forward and the straight-through backward of
+// SpatialAdaptiveQuantization._forward_pytorch, training branch
+// (mcaq_yolo/core/quantization.py:699-727, 733-737), the EMA running
+// statistics (update_running_stats, quantization.py:319-353), and their
+// extern "C" launchers (include/mcaq_hip.h).  Included by mcaq_kernels.hip.
+//
+// Per pixel p with tile bits b (nearest upsample of the continuous bit map),
+// lo = floor(b), f = b - lo, hi = lo + 1 (lo past 8):
+//   forward   xq = (1 - f) * Q_lo(x) + f * Q_hi(x),  y = xq * m
+//   backward  gm = g * m                      (g * 1 without a mask)
+//             grad_x    = gm * (1 - f) + gm * f          (STE, elementwise)
+//             grad_m(p) = sum_c g * xq                  (channel sum)
+//             grad_b(t) = sum_{p in t} sum_c (gm * Q_hi - gm * Q_lo)
+// Q_b is the inference quant/dequant with per-channel running min/max.
+// The HBM traffic: forward reads x (+ m plane) and writes y; backward reads
+// g and x (+ m) and writes grad_x, plus per-slice channel partials of the two
+// sums ((C/32) x 2 planes of B*H*W floats) that a small per-image kernel folds.
+#pragma once
+
+namespace mcaq {
+
+struct QatArgs {
+  mcaq_qat_scale s[3];
+  int nscales;
+  int units_total;
+};
+
+constexpr int QAT_LO = 1;   // table widths QAT_LO .. 8 (the reference's bc_int <= 8)
+constexpr int QAT_NB = 8;
+
+__device__ __forceinline__ size_t qat_slices(const mcaq_qat_scale& S) { return (size_t)((S.C + 31) / 32); }
+
+// unit = 256 pixels x 32 channels of one image (the pass-2 layout): lane l of
+// wave w owns pixels 4l..4l+3 and channels 8w..8w+7 of the slice.
+template <bool kBwd, bool kVec>
+__global__ __launch_bounds__(256) void mcaq_qat_kernel(QatArgs a) {
+  __shared__ float2 qt[32 * QAT_NB];
+  __shared__ float red[2][4][256];
+  const int unit = blockIdx.x;
+  int si = 0;
+  while (si + 1 < a.nscales && unit >= a.s[si + 1].unit_begin) ++si;
+  const mcaq_qat_scale& S = a.s[si];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int HW = S.H * S.W;
+  const int upi = (HW + 255) / 256;
+  const int nsl = (S.C + 31) / 32;
+  int lu = unit - S.unit_begin;
+  const int slice = lu % nsl; lu /= nsl;
+  const int chunk = lu % upi;
+  const int b = lu / upi;
+  const int c0 = slice * 32;
+  const int nc = imin_(32, S.C - c0);
+  for (int i = tid; i < nc * QAT_NB; i += 256) {
+    const int c = i / QAT_NB, k = i - c * QAT_NB;
+    const QParam q = qparam(S.xmin[c0 + c], S.xmax[c0 + c], QAT_LO + k);
+    qt[i] = make_float2(q.scale, q.zp);
+  }
+  const int q0 = chunk * 256 + lane * 4;
+  bool pv[4];
+  int kl[4], kh[4];
+  float fu[4], omf[4], mv[4], lmin[4], lmax[4], hmin[4], hmax[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int p = imin_(q0 + k, HW - 1);
+    pv[k] = q0 + k < HW;
+    const int h = p / S.W, w = p - (p / S.W) * S.W;
+    const float bv = S.bits[((size_t)b * S.ht + nearest_src(h, S.ht, S.H)) * S.wt + nearest_src(w, S.wt, S.W)];
+    const float fl = floorf(bv);
+    fu[k] = bv - fl;                 // exact (Sterbenz) for b >= 1
+    omf[k] = 1.0f - fu[k];
+    const int lo = imin_(imax_((int)fl, QAT_LO), QAT_LO + QAT_NB - 1);
+    const int hi = lo < 8 ? lo + 1 : lo;    // Q_hi := Q_lo past 8 bits (frac is 0 there)
+    kl[k] = lo - QAT_LO;
+    kh[k] = hi - QAT_LO;
+    lmin[k] = (float)(-(1 << (lo - 1))); lmax[k] = (float)((1 << (lo - 1)) - 1);
+    hmin[k] = (float)(-(1 << (hi - 1))); hmax[k] = (float)((1 << (hi - 1)) - 1);
+    mv[k] = S.m ? S.m[(size_t)b * HW + p] : 1.0f;
+  }
+  const bool has_m = S.m != nullptr;
+  const int cw = wv * 8;
+  const int ncw = imin_(8, nc - cw);
+  const size_t rowbase = ((size_t)b * S.C + c0 + imax_(0, imin_(cw, nc - 1))) * HW;
+  const float* xb = S.x + rowbase;
+  const int qa = pv[0] ? q0 : 0;
+  float v[8][4], gv[8][4];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const size_t ro = (size_t)(c < ncw ? c : 0) * HW;
+    if (kVec) {
+      const float4 t = *reinterpret_cast<const float4*>(xb + ro + qa);
+      v[c][0] = t.x; v[c][1] = t.y; v[c][2] = t.z; v[c][3] = t.w;
+      if (kBwd) {
+        const float4 u = *reinterpret_cast<const float4*>(S.g + rowbase + ro + qa);
+        gv[c][0] = u.x; gv[c][1] = u.y; gv[c][2] = u.z; gv[c][3] = u.w;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const size_t o = ro + imin_(q0 + k, HW - 1);
+        v[c][k] = xb[o];
+        if (kBwd) gv[c][k] = S.g[rowbase + o];
+      }
+    }
+  }
+  __syncthreads();   // qt ready
+  float sgm[4] = {0.f, 0.f, 0.f, 0.f}, sgf[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    if (c >= ncw) break;
+    float o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float2 zl = qt[(cw + c) * QAT_NB + kl[k]];
+      const float2 zh = qt[(cw + c) * QAT_NB + kh[k]];
+      QParam L, Hq;
+      L.scale = zl.x; L.zp = zl.y; L.qmin = lmin[k]; L.qmax = lmax[k];
+      Hq.scale = zh.x; Hq.zp = zh.y; Hq.qmin = hmin[k]; Hq.qmax = hmax[k];
+      const float ql = quant_dequant(v[c][k], L);
+      const float qh = quant_dequant(v[c][k], Hq);
+      const float xq = omf[k] * ql + fu[k] * qh;      // two rounded products, one rounded add
+      if (!kBwd) {
+        o[k] = has_m ? xq * mv[k] : xq;
+      } else {
+        const float g = gv[c][k];
+        const float gm = has_m ? g * mv[k] : g;
+        o[k] = gm * omf[k] + gm * fu[k];
+        sgm[k] += g * xq;
+        sgf[k] += gm * qh - gm * ql;
+      }
+    }
+    float* orow = (kBwd ? S.gx : S.y) + rowbase + (size_t)c * HW;
+    if (kVec) {
+      if (pv[0]) *reinterpret_cast<float4*>(orow + q0) = make_float4(o[0], o[1], o[2], o[3]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) if (pv[k]) orow[q0 + k] = o[k];
+    }
+  }
+  if (!kBwd) return;
+  // channel partials of this slice: waves in order, then one write per pixel
+#pragma unroll
+  for (int k = 0; k < 4; ++k) { red[0][wv][lane * 4 + k] = sgm[k]; red[1][wv][lane * 4 + k] = sgf[k]; }
+  __syncthreads();
+  const int p = chunk * 256 + tid;
+  if (p < HW) {
+    const float tm = ((red[0][0][tid] + red[0][1][tid]) + red[0][2][tid]) + red[0][3][tid];
+    const float tf = ((red[1][0][tid] + red[1][1][tid]) + red[1][2][tid]) + red[1][3][tid];
+    const size_t plane = (size_t)S.B * HW;
+    const size_t o = ((size_t)slice * S.B + b) * HW + p;
+    S.work[o] = tm;
+    S.work[(size_t)nsl * plane + o] = tf;
+  }
+}
+
+// one workgroup per (scale, image): grad_m(p) = sum over slices; grad_b(t) =
+// sum over the tile's pixels (row-major) of the slice sums.
+__global__ __launch_bounds__(256) void mcaq_qat_fold_kernel(QatArgs a) {
+  const int blk = blockIdx.x;
+  int si = 0;
+  while (si + 1 < a.nscales && blk >= a.s[si + 1].block_begin) ++si;
+  const mcaq_qat_scale& S = a.s[si];
+  const int b = blk - S.block_begin;
+  const int HW = S.H * S.W;
+  const int nsl = (S.C + 31) / 32;
+  const size_t plane = (size_t)S.B * HW;
+  const float* pm = S.work + (size_t)b * HW;
+  const float* pf = S.work + (size_t)nsl * plane + (size_t)b * HW;
+  if (S.gm)
+    for (int p = threadIdx.x; p < HW; p += 256) {
+      float t = pm[p];
+      for (int s = 1; s < nsl; ++s) t += pm[(size_t)s * plane + p];
+      S.gm[(size_t)b * HW + p] = t;
+    }
+  if (S.gb)
+    for (int t = threadIdx.x; t < S.ht * S.wt; t += 256) {
+      const int th = t / S.wt, tw = t - th * S.wt;
+      float acc = 0.0f;
+      for (int h = 0; h < S.H; ++h) {
+        if (nearest_src(h, S.ht, S.H) != th) continue;
+        for (int w = 0; w < S.W; ++w) {
+          if (nearest_src(w, S.wt, S.W) != tw) continue;
+          const int p = h * S.W + w;
+          float v = pf[p];
+          for (int s = 1; s < nsl; ++s) v += pf[(size_t)s * plane + p];
+          acc += v;
+        }
+      }
+      S.gb[(size_t)b * S.ht * S.wt + t] = acc;
+    }
+}
+
+// running <- a * running + c * batch (first batch: running <- batch),
+// a = fp32(momentum), c = fp32(1 - momentum) as Python evaluates them.
+__global__ __launch_bounds__(256) void mcaq_ema_kernel(const float* bmin, const float* bmax, float* rmin,
+                                                       float* rmax, int C, float am, float cm, int first) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  if (first) {
+    rmin[c] = bmin[c];
+    rmax[c] = bmax[c];
+  } else {
+    rmin[c] = am * rmin[c] + cm * bmin[c];
+    rmax[c] = am * rmax[c] + cm * bmax[c];
+  }
+}
+
+}  // namespace mcaq
+
+extern "C" {
+
+size_t mcaq_qat_work_floats(int B, int C, int H, int W) {
+  return 2 * (size_t)((C + 31) / 32) * (size_t)B * (size_t)H * (size_t)W;
+}
+
+static int qat_args(const mcaq_qat_scale* scales, int nscales, bool bwd, mcaq::QatArgs& a, int& blocks) {
+  if (nscales < 1 || nscales > 3 || !scales) return (int)hipErrorInvalidValue;
+  int units = 0;
+  blocks = 0;
+  for (int i = 0; i < nscales; ++i) {
+    const mcaq_qat_scale& s = scales[i];
+    if (s.B < 1 || s.C < 1 || s.H < 1 || s.W < 1 || s.ht < 1 || s.wt < 1 || s.ht > s.H || s.wt > s.W ||
+        !s.x || !s.bits || !s.xmin || !s.xmax)
+      return (int)hipErrorInvalidValue;
+    if (bwd ? (!s.g || !s.gx || !s.work) : !s.y) return (int)hipErrorInvalidValue;
+    a.s[i] = s;
+    a.s[i].unit_begin = units;
+    a.s[i].block_begin = blocks;
+    units += s.B * ((s.H * s.W + 255) / 256) * ((s.C + 31) / 32);
+    blocks += s.B;
+  }
+  a.nscales = nscales;
+  a.units_total = units;
+  return 0;
+}
+
+int mcaq_qat_forward(const mcaq_qat_scale* scales, int nscales, hipStream_t stream) {
+  mcaq::QatArgs a;
+  int blocks;
+  const int e = qat_args(scales, nscales, false, a, blocks);
+  if (e) return e;
+  bool vec = true;
+  for (int i = 0; i < nscales; ++i) vec = vec && ((scales[i].H * scales[i].W) & 3) == 0;
+  if (vec)
+    hipLaunchKernelGGL((mcaq::mcaq_qat_kernel<false, true>), dim3(a.units_total), dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL((mcaq::mcaq_qat_kernel<false, false>), dim3(a.units_total), dim3(256), 0, stream, a);
+  return (int)hipGetLastError();
+}
+
+int mcaq_qat_backward(const mcaq_qat_scale* scales, int nscales, hipStream_t stream) {
+  mcaq::QatArgs a;
+  int blocks;
+  const int e = qat_args(scales, nscales, true, a, blocks);
+  if (e) return e;
+  bool vec = true;
+  for (int i = 0; i < nscales; ++i) vec = vec && ((scales[i].H * scales[i].W) & 3) == 0;
+  if (vec)
+    hipLaunchKernelGGL((mcaq::mcaq_qat_kernel<true, true>), dim3(a.units_total), dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL((mcaq::mcaq_qat_kernel<true, false>), dim3(a.units_total), dim3(256), 0, stream, a);
+  hipError_t le = hipGetLastError();
+  if (le != hipSuccess) return (int)le;
+  bool fold = false;
+  for (int i = 0; i < nscales; ++i) fold = fold || scales[i].gm || scales[i].gb;
+  if (fold) hipLaunchKernelGGL(mcaq::mcaq_qat_fold_kernel, dim3(blocks), dim3(256), 0, stream, a);
+  return (int)hipGetLastError();
+}
+
+int mcaq_ema_stats(const float* batch_min, const float* batch_max, float* running_min, float* running_max,
+                   int C, double momentum, int first, hipStream_t stream) {
+  if (C < 1 || !batch_min || !batch_max || !running_min || !running_max) return (int)hipErrorInvalidValue;
+  const float am = (float)momentum, cm = (float)(1.0 - momentum);
+  hipLaunchKernelGGL(mcaq::mcaq_ema_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, batch_min, batch_max,
+                     running_min, running_max, C, am, cm, first ? 1 : 0);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -13,6 +13,7 @@ Inference calls go through one `HookPlan` per feature shape: 3 launches
 analyzer -> mapper -> soft mask -> quantizer chain.  Calibration
 (`calibrating=True`) first folds the batch min/max into the quantizer's EMA
 statistics (quantization.py:319-353), then quantizes like inference.
+Train mode (QAT) runs the modules one by one with autograd (`_run_scale_train`).
 """
 import torch
 import torch.nn as nn
@@ -100,10 +101,28 @@ class MCAQHooks(nn.Module):
             self._plans[key] = plan
         return plan
 
+    def _run_scale_train(self, layer_idx, feat, state):
+        """models/mcaq_yolo.py:409-455 in train mode (QAT, BASELINE config 5):
+        analyzer with autograd into complexity_mlp, continuous bits from the
+        train-mode mapper, fractional-bit STE quantizer (HIP forward/backward)."""
+        complexity = self.complexity_analyzer(feat)
+        if self.normalize_complexity:
+            B = complexity.shape[0]
+            flat = complexity.reshape(B, -1)
+            lo = torch.quantile(flat, 0.02, dim=1, keepdim=True).unsqueeze(-1)
+            hi = torch.quantile(flat, 0.98, dim=1, keepdim=True).unsqueeze(-1)
+            complexity = ((complexity - lo) / (hi - lo + 1e-8)).clamp(0.0, 1.0)
+        bit_map = self.bit_mapper(complexity, state.get("temperature", 1.0), return_continuous=True)
+        quantize = state.get("quantize", True)
+        quantizer = self.quantizers[str(layer_idx)]
+        feat_q = quantizer(feat, bit_map, training=True) if quantize else feat
+        state.setdefault("aux", []).append({"layer": layer_idx, "complexity": complexity,
+                                            "bit_map": bit_map, "features_q": feat_q})
+        return feat_q if quantize else None
+
     def run_scale(self, layer_idx, feat, state):
         if self.training:
-            raise NotImplementedError("training-mode hooks (continuous bits, STE quantizer) are the QAT path, "
-                                      "SURVEY.md 8(f) rank 2; call .eval()")
+            return self._run_scale_train(layer_idx, feat, state)
         quantize = state.get("quantize", True)
         quantizer = self.quantizers[str(layer_idx)]
         x = feat.float().contiguous()

@@ -32,7 +32,8 @@ def test_struct_layouts_match_header():
     """Field order / count of the ctypes mirrors equal the C structs."""
     src = open(HDR).read()
     for cname, py in (("mcaq_stats_scale", abi.StatsScale), ("mcaq_finalize_scale", abi.FinalizeScale),
-                      ("mcaq_morph_scale", abi.MorphScale), ("mcaq_quant_scale", abi.QuantScale)):
+                      ("mcaq_morph_scale", abi.MorphScale), ("mcaq_quant_scale", abi.QuantScale),
+                      ("mcaq_qat_scale", abi.QatScale)):
         body = re.search(r"typedef struct \{([^{}]*)\} %s;" % cname, src).group(1)
         body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
         fields = []

@@ -1,0 +1,172 @@
+"""QAT quantizer (training branch; BASELINE config 5) on the
+GPU through the C ABI: EMA running statistics, fractional-bit forward and
+straight-through backward against the reference's own train-mode fixtures
+(tests/golden/qat_*.npz) and the oracle (oracle/mcaq_oracle.py qat_*).
+
+Tolerances: y, grad_x and the running statistics are bit-exact; the two
+channel/tile sums (grad of m, grad of the bit map) are fp32 sums in a
+different order from ATen's, compared within 1e-4 of the largest magnitude."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, load_weights
+from oracle import mcaq_oracle as O
+
+pytestmark = pytest.mark.gpu
+f32 = np.float32
+DEV = "cuda"
+QAT_CASES = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.startswith("qat_") and f.endswith(".npz"))
+
+
+def T(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=f32)).to(DEV)
+
+
+def N(t):
+    return t.detach().cpu().numpy()
+
+
+def close_sum(got, ref, tol=1e-4):
+    ref = np.asarray(ref, np.float64)
+    scale = max(np.abs(ref).max(), 1e-30)
+    err = np.abs(np.asarray(got, np.float64) - ref).max()
+    assert err <= tol * scale, "max err %g vs scale %g" % (err, scale)
+
+
+def ema(x, r0min, r0max):
+    from mcaq_yolo_amd import abi, core
+    xmin, xmax = core._channel_minmax(T(x))
+    rmin, rmax = T(r0min).clone(), T(r0max).clone()
+    abi.check(abi.lib().mcaq_ema_stats(core._p(xmin), core._p(xmax), core._p(rmin), core._p(rmax), rmin.numel(),
+                                       0.99, 0, core._stream()), "ema")
+    return rmin, rmax
+
+
+@pytest.mark.parametrize("name", QAT_CASES)
+def test_qat_kernels_vs_reference_fixture(name):
+    from mcaq_yolo_amd import core
+    d = np.load(os.path.join(GOLDEN, name + ".npz"))
+    x, bits, g = d["x"], d["bits"], d["g"]
+    rmin, rmax = ema(x, d["r0min"], d["r0max"])
+    assert np.array_equal(N(rmin), d["rmin"]) and np.array_equal(N(rmax), d["rmax"]), "EMA"
+    smooth = bool(d["smooth"])
+    m = T(d["m"]) if smooth else None
+    y = core.qat_quantize(T(x), T(bits), m, rmin, rmax)
+    assert np.array_equal(N(y), d["y"]), "forward"
+    gx, gb, gm = core.qat_quantize_backward(T(g), T(x), T(bits), m, rmin, rmax)
+    assert np.array_equal(N(gx), d["gx"]), "grad x"
+    ogx, ogb, ogm = O.qat_backward(g, x, bits, d["rmin"], d["rmax"], d["m"] if smooth else None)
+    close_sum(N(gb), ogb)
+    if smooth:
+        close_sum(N(gm), ogm)
+    else:
+        assert gm is None
+        close_sum(N(gb), d["gbits"])
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 80, 80, 10, 10), (3, 40, 13, 17, 3, 4), (1, 33, 20, 20, 5, 5),
+                                   (2, 256, 20, 20, 5, 5)])
+def test_qat_kernels_vs_oracle(shape):
+    """Seeded random shapes incl. ragged H*W (not a multiple of 4), a partial
+    channel slice (C = 33, 40) and both ends of the bit range."""
+    from mcaq_yolo_amd import core
+    B, C, H, W, ht, wt = shape
+    rng = np.random.default_rng(sum(shape))
+    x = (rng.standard_normal((B, C, H, W)) * 1.5).astype(f32)
+    bits = rng.uniform(2.0, 8.0, (B, ht, wt)).astype(f32)
+    bits.reshape(-1)[:3] = [2.0, 8.0, 7.5]
+    m = rng.uniform(0.5, 1.0, (B, H, W)).astype(f32)
+    g = rng.standard_normal((B, C, H, W)).astype(f32)
+    mn, mx = x.min(axis=(0, 2, 3)), x.max(axis=(0, 2, 3))
+    for mm in (None, m):
+        y = core.qat_quantize(T(x), T(bits), None if mm is None else T(mm), T(mn), T(mx))
+        ref, _ = O.qat_forward(x, bits, mn, mx, mm)
+        assert np.array_equal(N(y), ref)
+        gx, gb, gm = core.qat_quantize_backward(T(g), T(x), T(bits), None if mm is None else T(mm), T(mn), T(mx))
+        ogx, ogb, ogm = O.qat_backward(g, x, bits, mn, mx, mm)
+        assert np.array_equal(N(gx), ogx)
+        close_sum(N(gb), ogb)
+        if mm is not None:
+            close_sum(N(gm), ogm)
+
+
+def test_qat_integer_bits_equal_inference_kernel():
+    """f = 0 everywhere: the QAT forward equals the pass-2 inference kernel,
+    at the full P3 shape of config 2 (yolov8n, bs 8 here)."""
+    from mcaq_yolo_amd import abi, core
+    B, C, H, W, ht, wt = 8, 64, 80, 80, 10, 10
+    gen = torch.Generator(device="cpu").manual_seed(11)
+    x = (torch.randn(B, C, H, W, generator=gen) * 2).to(DEV)
+    bits = torch.randint(2, 9, (B, ht, wt), generator=gen).float().to(DEV)
+    m = torch.rand(B, H, W, generator=gen).to(DEV)
+    xmin, xmax = core._channel_minmax(x)
+    y = core.qat_quantize(x, bits, m, xmin, xmax)
+    y2 = torch.empty_like(x)
+    q = abi.QuantScale()
+    q.x, q.y, q.bits, q.m, q.xmin, q.xmax = core._p(x), core._p(y2), core._p(bits), core._p(m), core._p(xmin), \
+        core._p(xmax)
+    q.B, q.C, q.H, q.W, q.ht, q.wt, q.bits_lo, q.nbits = B, C, H, W, ht, wt, 2, 7
+    abi.check(abi.lib().mcaq_quant(abi.ctypes.byref(q), 1, core._stream()), "mcaq_quant")
+    assert torch.equal(y, y2)
+
+
+@pytest.mark.parametrize("name", ["qat_p4_plain", "qat_p4_smooth", "qat_p5_smooth"])
+def test_quantizer_module_train_mode(name):
+    """SpatialAdaptiveQuantization in train mode (the reference module's
+    forward + autograd): running stats bit-exact, y and grads vs the
+    reference's own train-mode outputs."""
+    from mcaq_yolo_amd import core
+    d = np.load(os.path.join(GOLDEN, name + ".npz"))
+    smooth = bool(d["smooth"])
+    q = core.SpatialAdaptiveQuantization(smooth_transitions=smooth).to(DEV)
+    if smooth:
+        W = load_weights()
+        q.soft_mask.load_state_dict({k[len("soft_mask."):]: torch.from_numpy(np.asarray(v))
+                                     for k, v in W.items() if k.startswith("soft_mask.")})
+    q.running_min = T(d["r0min"]).view(1, -1, 1, 1)
+    q.running_max = T(d["r0max"]).view(1, -1, 1, 1)
+    q.train()
+    x = T(d["x"]).requires_grad_(True)
+    b = T(d["bits"]).requires_grad_(True)
+    y = q(x, b, training=True)
+    assert np.array_equal(N(q.running_min).reshape(-1), d["rmin"])
+    assert np.array_equal(N(q.running_max).reshape(-1), d["rmax"])
+    if smooth:   # m from the HIP soft mask (oracle-exact) vs the reference's CPU m: ulps apart
+        np.testing.assert_allclose(N(y), d["y"], rtol=1e-5, atol=1e-6)
+    else:
+        assert np.array_equal(N(y), d["y"])
+    y.backward(T(d["g"]))
+    if smooth:
+        np.testing.assert_allclose(N(x.grad), d["gx"], rtol=1e-5, atol=1e-6)
+    else:
+        assert np.array_equal(N(x.grad), d["gx"])
+    close_sum(N(b.grad), d["gbits"], tol=1e-3 if smooth else 1e-4)
+
+
+def test_hook_train_step_gradients():
+    """MCAQHooks in train mode: one QAT step over the three hook scales reaches
+    the complexity MLP, the bit mapper and the soft masks with finite grads."""
+    from mcaq_yolo_amd.hooks import MCAQHooks
+    torch.manual_seed(0)
+    h = MCAQHooks(device=DEV).train()
+    gen = torch.Generator(device="cpu").manual_seed(5)
+    feats = [torch.nn.functional.silu(1.5 * torch.randn(4, c, s, s, generator=gen)).to(DEV).requires_grad_(True)
+             for c, s in ((64, 80), (128, 40), (256, 20))]
+    outs, aux = h.forward_features(feats, temperature=1.0)
+    assert len(aux) == 3
+    for a in aux:
+        bm = a["bit_map"]
+        assert float(bm.min()) >= 2.0 and float(bm.max()) <= 8.0
+    loss = sum((o * o).mean() for o in outs) + 0.01 * torch.stack([a["bit_map"].mean() for a in aux]).mean()
+    loss.backward()
+    for f in feats:
+        assert f.grad is not None and torch.isfinite(f.grad).all()
+    named = dict(h.named_parameters())
+    for k in ("complexity_analyzer.complexity_mlp.0.weight", "bit_mapper.mapping_network.0.weight",
+              "quantizers.4.soft_mask.net.0.weight"):
+        gp = named[k].grad
+        assert gp is not None and torch.isfinite(gp).all() and float(gp.abs().sum()) > 0, k
+    assert all(q.running_min is not None for q in h.quantizers.values())
