@@ -1,6 +1,8 @@
 """Benchmark of the MCAQ spatial-adaptive-quantization hook path on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4] [--pipeline D] [--no-cpu]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5] [--pipeline D] [--no-cpu]
+
+(--config 5: the QAT training step of the hooks, `main_qat`.)
 
 A step = the three backbone hooks (C3/C4/C5) of one batch: channel statistics,
 morphological complexity (phi1..5, MLP, bilateral), bit mapper, soft mask and
@@ -63,6 +65,207 @@ def load_blobs(device):
     mm = torch.from_numpy(params.pack_mapper_mlp(params.sub(sd, "bit_mapper."))).to(device)
     sm = torch.from_numpy(params.pack_soft_mask(params.sub(sd, "soft_mask."))).to(device)
     return cm, mm, sm
+
+
+# BASELINE config 5: yolov8n QAT step, bs128 = 16 per GPU x 8 (weak scaling)
+QAT_CONFIG = ("yolov8n", 16, (64, 128, 256), 8, "mlp")
+
+
+def hook_state_dict(device):
+    """The seeded reference-layout weights (tests/golden/weights.npz) as an
+    MCAQHooks state_dict: one analyzer, one mapper, a soft mask per scale."""
+    import numpy as np
+    w = np.load(os.path.join(ROOT, "tests", "golden", "weights.npz"))
+    sd = {}
+    for k in w.files:
+        t = torch.from_numpy(np.array(w[k])).to(device)
+        if k.startswith("soft_mask."):
+            for idx in (4, 6, 9):
+                sd["quantizers.%d.%s" % (idx, k)] = t
+        else:
+            sd[k] = t
+    return sd
+
+
+def cpu_baseline_qat(budget_s=12.0):
+    """Oracle QAT quantizer (EMA + fractional-bit forward + STE backward, the
+    per-element part of the step) on one image per scale, ~budget_s seconds."""
+    import numpy as np
+    from oracle import mcaq_oracle as O
+    name, B, chans, grid, mapper = QAT_CONFIG
+    rng = np.random.default_rng(0)
+    xs = [synth_features(1, c, h, wd, 5000 + i, "cpu").numpy() for i, (c, (h, wd)) in enumerate(zip(chans, SIZES))]
+    gs = [rng.standard_normal(x.shape).astype(np.float32) for x in xs]
+    bs = [rng.uniform(2, 8, (1, h // 8, wd // 8)).astype(np.float32) for (h, wd) in SIZES]
+    ms = [rng.uniform(0.9, 1.0, (1, h, wd)).astype(np.float32) for (h, wd) in SIZES]
+    t0 = time.perf_counter()
+    n = 0
+    while True:
+        for x, g, b, m in zip(xs, gs, bs, ms):
+            rmin, rmax = O.ema_running_stats(x)
+            O.qat_forward(x, b, rmin, rmax, m)
+            O.qat_backward(g, x, b, rmin, rmax, m)
+        n += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt, 4), "unit": "images/s", "cores": 1, "kind": "port",
+            "sample": "%d images x 3 hook scales (%s, batch 1): EMA stats + QAT forward + STE backward through "
+                      "oracle/mcaq_oracle.py, single-threaded numpy, %.1f s (quantizer only)" % (n, name, dt)}
+
+
+def main_qat(args, world, rank, dev, pg):
+    """BASELINE config 5 at the hook level: one QAT training step of the three
+    MCAQ hooks (train mode) per batch - EMA statistics, analyzer (phi kernel +
+    complexity MLP with autograd), continuous bits (train-mode mapper), soft
+    mask, fractional-bit quantizer forward; backward from the upstream feature
+    gradients the YOLOv8 neck would return (synthetic, fixed), straight-through
+    into the backbone features and into the hook parameters; gradient
+    all-reduce (N > 1), clip 1.0, SGD step, |W| projection (train.py:615-641)."""
+    from mcaq_yolo_amd import abi, core
+    from mcaq_yolo_amd.hooks import MCAQHooks
+    name, B, chans, grid, mapper = QAT_CONFIG
+    torch.manual_seed(0)
+    h = MCAQHooks(grid_size=grid, bit_mapping=mapper, device=dev)
+    h.load_state_dict(hook_state_dict(dev), strict=False)
+    h.train()
+    if pg is not None:
+        for q in h.quantizers.values():
+            q.process_group = pg
+    feats = [synth_features(B, c, hh, ww, 5000 + i + 7919 * rank, dev).requires_grad_(True)
+             for i, (c, (hh, ww)) in enumerate(zip(chans, SIZES))]
+    gen = torch.Generator(device="cpu").manual_seed(77 + rank)
+    G = [(1e-3 * torch.randn(f.shape, generator=gen)).to(dev) for f in feats]
+    params_ = [p for p in h.parameters() if p.requires_grad]
+    opt = torch.optim.SGD(params_, lr=1e-3, momentum=0.9)
+    target_bits = 4.0
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        for f in feats:
+            f.grad = None
+        outs, aux = h.forward_features(feats, temperature=1.0)   # curriculum stage 3: temperature 1
+        lbit = (MCAQHooks.avg_bits(aux) - target_bits) ** 2
+        torch.autograd.backward(list(outs) + [0.1 * lbit], list(G) + [torch.ones((), device=dev)])
+        if pg is not None:
+            import torch.distributed as dist
+            flat = torch.cat([p.grad.reshape(-1) for p in params_])
+            dist.all_reduce(flat, group=pg)
+            flat /= world
+            o = 0
+            for p in params_:
+                n = p.numel()
+                p.grad.copy_(flat[o:o + n].view_as(p))
+                o += n
+        torch.nn.utils.clip_grad_norm_(params_, max_norm=1.0)
+        opt.step()
+        h.bit_mapper.enforce_weight_constraints()
+
+    # warm up on a side stream (lazy state: running stats, momentum buffers),
+    # then (N = 1) capture the whole step - forward, backward, clip, SGD,
+    # projection - as one HIP graph: ~300 small launches replayed at once
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(max(args.warmup, 3)):
+            step()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    use_graph = pg is None and not args.eager
+    run = step
+    if use_graph:
+        graph = torch.cuda.CUDAGraph()
+        opt.zero_grad(set_to_none=True)
+        with torch.cuda.graph(graph):
+            step()
+        run = graph.replay
+        for _ in range(2):
+            run()
+    torch.cuda.synchronize()
+
+    # per-kernel device time of the QAT quantizer over the three scales in one launch
+    L = abi.lib()
+    stream = torch.cuda.current_stream()
+    sh = abi.ctypes.c_void_p(stream.cuda_stream)
+    xs = [f.detach() for f in feats]
+    bits = [torch.rand(B, hh // grid, ww // grid, device=dev) * 6 + 2 for (hh, ww) in SIZES]
+    ms = [torch.rand(B, hh, ww, device=dev) * 0.1 + 0.9 for (hh, ww) in SIZES]
+    mm = [core._channel_minmax(x) for x in xs]
+    ys = [torch.empty_like(x) for x in xs]
+    gxs = [torch.empty_like(x) for x in xs]
+    gms = [torch.empty(B, hh, ww, device=dev) for (hh, ww) in SIZES]
+    gbs = [torch.empty_like(b) for b in bits]
+    works = [torch.empty(L.mcaq_qat_work_floats(*x.shape), device=dev) for x in xs]
+    arr = (abi.QatScale * 3)()
+    for i in range(3):
+        q = core._qat_struct(xs[i], bits[i], ms[i], mm[i][0], mm[i][1])
+        q.g, q.y, q.gx, q.gm, q.gb, q.work = core._p(G[i]), core._p(ys[i]), core._p(gxs[i]), core._p(gms[i]), \
+            core._p(gbs[i]), core._p(works[i])
+        arr[i] = q
+    kt = {}
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    for k, fn in (("qat_forward", lambda: L.mcaq_qat_forward(arr, 3, sh)),
+                  ("qat_backward", lambda: L.mcaq_qat_backward(arr, 3, sh))):
+        abi.check(fn(), k)
+        torch.cuda.synchronize()
+        e0.record(stream)
+        for _ in range(20):
+            fn()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        kt[k] = e0.elapsed_time(e1) * 1e3 / 20
+
+    if pg is not None:
+        import torch.distributed as dist
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    torch.cuda.synchronize()
+    step_s = (time.perf_counter() - t0) / args.steps
+    if pg is not None:
+        import torch.distributed as dist
+        t = torch.tensor([step_s], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.barrier()
+        step_s = float(t.item())
+    elems = sum(B * c * hh * ww for c, (hh, ww) in zip(chans, SIZES))
+    if rank == 0:
+        kern = {}
+        for k, nb in (("qat_forward", 8 * elems), ("qat_backward", 12 * elems)):
+            gbs_ = nb / (kt[k] * 1e-6) / 1e9
+            kern[k] = {"us": round(kt[k], 2), "alg_bytes": nb, "GB/s": round(gbs_, 1),
+                       "frac": round(gbs_ / HBM_PEAK_GBS, 4)}
+        achieved = 24 * elems / step_s / 1e9
+        out = {
+            "metric": "images/sec QAT hook step (BASELINE config 5), 1/2/4/8 MI355X; % HBM roofline",
+            "value": round(world * B / step_s, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 5), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic silu features + fixed synthetic upstream gradients, seeded weights",
+            "config": {"workload": "%s QAT bs%d/GPU 640x640 MCAQ hooks C3/C4/C5 train step (grid %d, %s mapper, "
+                                   "continuous bits, STE, stage-3 temperature 1); YOLOv8 network excluded"
+                                   % (name, B, grid, mapper),
+                       "global_batch": world * B, "parallelism": "dp%d" % world, "hip_graph": use_graph},
+            "roofline": {"bound": "hbm", "achieved": kern["qat_backward"]["GB/s"], "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": kern["qat_backward"]["frac"], "traffic": None,
+                         "kernel": "mcaq_qat_kernel<bwd> + fold (read g, x + write grad_x, 12 B per element)",
+                         "alg_bytes_per_launch": 12 * elems, "us_per_launch": kern["qat_backward"]["us"]},
+            "step_roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                              "kernel": "whole QAT step, 24 B per feature element (fwd 12 + bwd 12)",
+                              "alg_bytes_per_step": 24 * elems},
+            "kernels": kern,
+            "cpu_baseline": None,
+        }
+        if not args.no_cpu and world == 1:
+            out["cpu_baseline"] = cpu_baseline_qat()
+        print(json.dumps(out), flush=True)
+    if pg is not None:
+        import torch.distributed as dist
+        dist.destroy_process_group()
 
 
 def cpu_baseline(cfg_id, budget_s=12.0):
@@ -201,7 +404,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS))
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS) + [5],
+                    help="2/3/4: inference hook path; 5: QAT hook training step")
     ap.add_argument("--pipeline", type=int, default=3, help="batches in flight (independent plans/streams)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--eager", action="store_true", help="no HIP graph (--schedule streams)")
@@ -231,6 +435,8 @@ def main():
             dist.init_process_group(backend)
         pg = dist.group.WORLD
 
+    if args.config == 5:
+        return main_qat(args, world, rank, dev, pg)
     name, B, chans, grid, mapper = CONFIGS[args.config]
     depth = max(1, args.pipeline)
     cm, mm, sm = load_blobs(dev)

@@ -399,7 +399,7 @@ class ComplexityToBitMappingNetwork(nn.Module):
         if self.enforce_monotonicity:
             for module in self.mapping_network.modules():
                 if isinstance(module, (nn.Linear, nn.BatchNorm1d)):
-                    module.weight.data = torch.abs(module.weight.data)
+                    module.weight.data.abs_()   # in place: parameter storage stays put (graph capture)
 
     def create_augmented_features(self, complexity: torch.Tensor) -> torch.Tensor:
         """bit_allocation.py:199-216: z0 = [C, C^2, log1p C]."""
@@ -408,6 +408,7 @@ class ComplexityToBitMappingNetwork(nn.Module):
     def _forward_train(self, complexity, temperature, return_continuous):
         """bit_allocation.py:218-280 in train mode (BatchNorm over the batch's
         tiles, straight-through clamp and round) as torch autograd ops."""
+        _need_cuda(complexity, "complexity")
         c = _normalize_complexity_shape(complexity).clamp(0.0, 1.0)
         B, H, W = c.shape
         h = self.mapping_network(self.create_augmented_features(c.reshape(-1, 1)))
@@ -622,6 +623,10 @@ class SpatialAdaptiveQuantization(nn.Module):
         self.soft_mask = LearnedSoftMask() if smooth_transitions else None
         self.register_buffer("calibration_histogram", None)
         self.histogram_bins = 2048
+        self._frozen_cached = False
+        # data-parallel training: set to a torch.distributed group to make the
+        # EMA statistics global; None = this process's batch only
+        self.process_group = None
 
     def _load_from_state_dict(self, state_dict, prefix, local_metadata, strict, missing_keys,
                               unexpected_keys, error_msgs):
@@ -636,6 +641,14 @@ class SpatialAdaptiveQuantization(nn.Module):
     def freeze_calibration(self):
         self.stats_frozen = torch.tensor(True, device=self.stats_frozen.device)
 
+    def _frozen(self):
+        """bool(stats_frozen) without a device sync while a HIP graph is being
+        captured (the flag cannot change inside a captured step)."""
+        if self.stats_frozen.is_cuda and torch.cuda.is_current_stream_capturing():
+            return self._frozen_cached
+        self._frozen_cached = bool(self.stats_frozen)
+        return self._frozen_cached
+
     def batch_minmax(self, x, absmean=None):
         """Per-channel (or per-tensor) min/max of the batch, expanded to C entries."""
         xmin, xmax = _channel_minmax(x, absmean)
@@ -648,11 +661,20 @@ class SpatialAdaptiveQuantization(nn.Module):
     def update_running_stats(self, x: torch.Tensor, absmean: Optional[torch.Tensor] = None):
         """quantization.py:319-353: EMA(momentum) of the batch min/max (pass 1 +
         finalize + mcaq_ema_stats; absmean, if given, is filled by the same read)."""
-        if bool(self.stats_frozen):
+        if self._frozen():
             return
         _need_cuda(x, "x")
         xf = _f32c(x)
         xmin, xmax = _channel_minmax(xf, absmean)
+        if self.process_group is not None:
+            # data-parallel QAT: the EMA sees the global batch's min/max (one
+            # all-reduce, MAX over [-min, max]), as a single process would
+            import torch.distributed as dist
+            vec = torch.cat([-xmin, xmax])
+            dist.all_reduce(vec, op=dist.ReduceOp.MAX, group=self.process_group)
+            C0 = xmin.numel()
+            xmin, xmax = -vec[:C0], vec[C0:].contiguous()
+            xmin = xmin.contiguous()
         C = x.shape[1]
         if self.per_channel:
             shape = (1, C) + (1,) * (x.dim() - 2)
@@ -660,14 +682,20 @@ class SpatialAdaptiveQuantization(nn.Module):
         else:
             nmin, nmax = xmin.amin(), xmax.amax()
         first = self.running_min is None
-        # new tensors (not in place): an earlier forward may hold the old ones
-        rmin, rmax = torch.empty_like(nmin), torch.empty_like(nmax)
-        old_min = nmin if first else self.running_min.float().contiguous()
-        old_max = nmax if first else self.running_max.float().contiguous()
-        if not first and old_min.numel() != nmin.numel():
-            raise RuntimeError("running stats have %d entries, batch has %d" % (old_min.numel(), nmin.numel()))
-        rmin.copy_(old_min)
-        rmax.copy_(old_max)
+        if not first and self.running_min.numel() != nmin.numel():
+            raise RuntimeError("running stats have %d entries, batch has %d"
+                               % (self.running_min.numel(), nmin.numel()))
+        inplace = not first and all(t.dtype == torch.float32 and t.is_contiguous() and t.device == nmin.device
+                                    for t in (self.running_min, self.running_max))
+        if inplace:
+            # updated in place (persistent buffers: a captured HIP graph replays
+            # the EMA); consumers of the statistics take copies
+            rmin, rmax = self.running_min, self.running_max
+        else:
+            rmin, rmax = nmin.clone(), nmax.clone()
+            if not first:
+                rmin.copy_(self.running_min.reshape(nmin.shape))
+                rmax.copy_(self.running_max.reshape(nmax.shape))
         abi.check(abi.lib().mcaq_ema_stats(_p(nmin), _p(nmax), _p(rmin), _p(rmax), nmin.numel(),
                                            float(self.momentum), 1 if first else 0, _stream()), "mcaq_ema_stats")
         self.running_min, self.running_max = rmin, rmax
@@ -688,15 +716,18 @@ class SpatialAdaptiveQuantization(nn.Module):
         want_m = self.smooth_transitions and self.soft_mask is not None
         absmean = torch.empty(B, H, W, device=x.device) if want_m else None
         xf = _f32c(x)
-        if bool(self.stats_frozen):
+        frozen = self._frozen()
+        if frozen:
             if want_m:
                 _run_stats(xf, absmean=absmean)
         else:
             self.update_running_stats(xf, absmean)
         # _calibrate_minmax (quantization.py:409-434): running stats in train
-        # mode or when frozen, else this batch's min/max
-        if self.running_min is not None and (self.training or bool(self.stats_frozen)):
-            xmin, xmax = self._stats_c(self.running_min, C), self._stats_c(self.running_max, C)
+        # mode or when frozen, else this batch's min/max (copies: the running
+        # buffers are updated in place by later steps)
+        if self.running_min is not None and (self.training or frozen):
+            xmin = self._stats_c(self.running_min, C).clone()
+            xmax = self._stats_c(self.running_max, C).clone()
         else:
             xmin, xmax = self.batch_minmax(xf)
         m = self.soft_mask(bit_map, x, absmean=absmean) if want_m else None

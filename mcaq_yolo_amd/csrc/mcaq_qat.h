@@ -29,8 +29,6 @@ struct QatArgs {
 constexpr int QAT_LO = 1;   // table widths QAT_LO .. 8 (the reference's bc_int <= 8)
 constexpr int QAT_NB = 8;
 
-__device__ __forceinline__ size_t qat_slices(const mcaq_qat_scale& S) { return (size_t)((S.C + 31) / 32); }
-
 // unit = 256 pixels x 32 channels of one image (the pass-2 layout): lane l of
 // wave w owns pixels 4l..4l+3 and channels 8w..8w+7 of the slice.
 template <bool kBwd, bool kVec>
@@ -153,41 +151,64 @@ __global__ __launch_bounds__(256) void mcaq_qat_kernel(QatArgs a) {
   }
 }
 
-// one workgroup per (scale, image): grad_m(p) = sum over slices; grad_b(t) =
-// sum over the tile's pixels (row-major) of the slice sums.
+// one workgroup per (scale, image, tile row): the band of pixel rows whose
+// nearest tile row is th, in chunks of <= QAT_FOLD_LDS floats: per pixel the
+// slice partials are summed (slices in order) -> grad_m and an LDS row chunk;
+// thread tw < wt then adds its tile's pixels of the chunk row-major.
+constexpr int QAT_FOLD_LDS = 8192;
+
 __global__ __launch_bounds__(256) void mcaq_qat_fold_kernel(QatArgs a) {
+  __shared__ float pl[QAT_FOLD_LDS];
+  __shared__ int band[2];
   const int blk = blockIdx.x;
   int si = 0;
   while (si + 1 < a.nscales && blk >= a.s[si + 1].block_begin) ++si;
   const mcaq_qat_scale& S = a.s[si];
-  const int b = blk - S.block_begin;
+  const int lb = blk - S.block_begin;
+  const int b = lb / S.ht, th = lb - (lb / S.ht) * S.ht;
   const int HW = S.H * S.W;
   const int nsl = (S.C + 31) / 32;
   const size_t plane = (size_t)S.B * HW;
   const float* pm = S.work + (size_t)b * HW;
   const float* pf = S.work + (size_t)nsl * plane + (size_t)b * HW;
-  if (S.gm)
-    for (int p = threadIdx.x; p < HW; p += 256) {
-      float t = pm[p];
-      for (int s = 1; s < nsl; ++s) t += pm[(size_t)s * plane + p];
-      S.gm[(size_t)b * HW + p] = t;
-    }
-  if (S.gb)
-    for (int t = threadIdx.x; t < S.ht * S.wt; t += 256) {
-      const int th = t / S.wt, tw = t - th * S.wt;
-      float acc = 0.0f;
-      for (int h = 0; h < S.H; ++h) {
-        if (nearest_src(h, S.ht, S.H) != th) continue;
-        for (int w = 0; w < S.W; ++w) {
-          if (nearest_src(w, S.wt, S.W) != tw) continue;
-          const int p = h * S.W + w;
-          float v = pf[p];
-          for (int s = 1; s < nsl; ++s) v += pf[(size_t)s * plane + p];
-          acc += v;
-        }
+  if (threadIdx.x == 0) {
+    int rs = S.H, re = 0;
+    for (int h = 0; h < S.H; ++h)
+      if (nearest_src(h, S.ht, S.H) == th) { rs = imin_(rs, h); re = imax_(re, h + 1); }
+    band[0] = rs; band[1] = re;
+  }
+  __syncthreads();
+  const int rs = band[0], re = band[1];
+  int cs = 0, ce = 0;
+  const int tw = threadIdx.x;
+  if (tw < S.wt) {
+    cs = S.W;
+    for (int w = 0; w < S.W; ++w)
+      if (nearest_src(w, S.wt, S.W) == tw) { cs = imin_(cs, w); ce = imax_(ce, w + 1); }
+  }
+  const int rows_per_chunk = imax_(1, QAT_FOLD_LDS / S.W);
+  float acc = 0.0f;
+  for (int r0 = rs; r0 < re; r0 += rows_per_chunk) {
+    const int r1 = imin_(re, r0 + rows_per_chunk);
+    const int p0 = r0 * S.W, np = (r1 - r0) * S.W;
+    for (int i = threadIdx.x; i < np; i += 256) {
+      const int p = p0 + i;
+      if (S.gm) {
+        float t = pm[p];
+        for (int s = 1; s < nsl; ++s) t += pm[(size_t)s * plane + p];
+        S.gm[(size_t)b * HW + p] = t;
       }
-      S.gb[(size_t)b * S.ht * S.wt + t] = acc;
+      float v = pf[p];
+      for (int s = 1; s < nsl; ++s) v += pf[(size_t)s * plane + p];
+      pl[i] = v;
     }
+    __syncthreads();
+    if (tw < S.wt)
+      for (int r = 0; r < r1 - r0; ++r)
+        for (int w = cs; w < ce; ++w) acc += pl[r * S.W + w];
+    __syncthreads();
+  }
+  if (S.gb && tw < S.wt) S.gb[((size_t)b * S.ht + th) * S.wt + tw] = acc;
 }
 
 // running <- a * running + c * batch (first batch: running <- batch),
@@ -220,6 +241,7 @@ static int qat_args(const mcaq_qat_scale* scales, int nscales, bool bwd, mcaq::Q
   for (int i = 0; i < nscales; ++i) {
     const mcaq_qat_scale& s = scales[i];
     if (s.B < 1 || s.C < 1 || s.H < 1 || s.W < 1 || s.ht < 1 || s.wt < 1 || s.ht > s.H || s.wt > s.W ||
+        s.wt > 256 || s.W > QAT_FOLD_LDS ||
         !s.x || !s.bits || !s.xmin || !s.xmax)
       return (int)hipErrorInvalidValue;
     if (bwd ? (!s.g || !s.gx || !s.work) : !s.y) return (int)hipErrorInvalidValue;
@@ -227,7 +249,7 @@ static int qat_args(const mcaq_qat_scale* scales, int nscales, bool bwd, mcaq::Q
     a.s[i].unit_begin = units;
     a.s[i].block_begin = blocks;
     units += s.B * ((s.H * s.W + 255) / 256) * ((s.C + 31) / 32);
-    blocks += s.B;
+    blocks += s.B * s.ht;
   }
   a.nscales = nscales;
   a.units_total = units;

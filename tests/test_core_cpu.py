@@ -75,13 +75,14 @@ def test_cpu_tensors_raise_no_fallback():
                                        torch.zeros(4), torch.ones(4), 4, 4)
 
 
-def test_training_paths_not_silently_computed():
+def test_training_paths_have_no_cpu_fallback():
+    """The QAT (train-mode) paths run on the GPU only: CPU tensors raise."""
     m = core.ComplexityToBitMappingNetwork()
     m.train()
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(RuntimeError, match="HIP"):
         m(torch.rand(1, 4, 4))
     q = core.SpatialAdaptiveQuantization()
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(RuntimeError, match="HIP"):
         q(torch.rand(1, 4, 16, 16), torch.full((1, 4, 4), 4.0), training=True)
 
 
