@@ -170,3 +170,63 @@ def test_hook_train_step_gradients():
         gp = named[k].grad
         assert gp is not None and torch.isfinite(gp).all() and float(gp.abs().sum()) > 0, k
     assert all(q.running_min is not None for q in h.quantizers.values())
+
+
+def _allclose_rel(got, ref, rtol, floor=1e-30):
+    """max |got - ref| <= rtol * max(|ref|, floor).  `floor` covers gradients
+    that are zero in exact arithmetic (a Linear bias feeding a train-mode
+    BatchNorm), whose reference values are rounding noise."""
+    ref = np.asarray(ref, np.float64)
+    err = np.abs(np.asarray(got, np.float64) - ref).max()
+    scale = max(np.abs(ref).max(), floor)
+    assert err <= rtol * scale, "max err %g vs scale %g" % (err, scale)
+
+
+def test_analyzer_train_mode_vs_reference():
+    """Train-mode analyzer (phi on the morph kernel, complexity MLP + bilateral
+    with autograd) against the reference's own train-mode C and MLP grads
+    (tests/golden/train_analyzer.npz; GPU GEMM/LayerNorm ulps: 1e-5 / 1e-4)."""
+    from mcaq_yolo_amd import core
+    d = np.load(os.path.join(GOLDEN, "train_analyzer.npz"))
+    W = load_weights()
+    a = core.MorphologicalComplexityAnalyzer(device=DEV)
+    a.load_state_dict({k[len("complexity_analyzer."):]: torch.from_numpy(np.asarray(v))
+                       for k, v in W.items() if k.startswith("complexity_analyzer.")})
+    a.train()
+    c = a(T(d["x"]))
+    _allclose_rel(N(c), d["c"], 1e-5)
+    c.backward(T(d["gc"]))
+    gmax = max(np.abs(d[k]).max() for k in d.files if k.startswith("grad."))
+    for n, p in a.complexity_mlp.named_parameters():
+        _allclose_rel(N(p.grad), d["grad.complexity_mlp." + n], 1e-4, floor=1e-2 * gmax)
+
+
+@pytest.mark.parametrize("temp", [1, 3])
+def test_mapper_train_mode_vs_reference(temp):
+    """Train-mode bit mapper (batch-statistics BatchNorm, straight-through
+    clamp) against the reference: continuous bits, grads, BN running stats."""
+    from mcaq_yolo_amd import core
+    d = np.load(os.path.join(GOLDEN, "train_mapper.npz"))
+    W = load_weights()
+    t = "t%d" % temp
+    m = core.ComplexityToBitMappingNetwork().to(DEV)
+    m.load_state_dict({k[len("bit_mapper."):]: torch.from_numpy(np.asarray(v))
+                       for k, v in W.items() if k.startswith("bit_mapper.")})
+    m.train()
+    c = T(d[t + ".c"]).requires_grad_(True)
+    bits = m(c, float(temp), return_continuous=True)
+    _allclose_rel(N(bits), d[t + ".bits"], 1e-5)
+    bits.backward(T(d[t + ".gb"]))
+    _allclose_rel(N(c.grad), d[t + ".grad_c"], 1e-4)
+    gmax = max(np.abs(d[k]).max() for k in d.files if k.startswith(t + ".grad.mapping_network."))
+    for n, p in m.mapping_network.named_parameters():
+        ref = d[t + ".grad.mapping_network." + n]
+        if n in ("0.bias", "3.bias", "6.bias"):
+            # a Linear bias feeding a train-mode BatchNorm: zero in exact
+            # arithmetic, rounding noise in both implementations
+            assert np.abs(N(p.grad)).max() <= 1e-6 * np.abs(d[t + ".grad_c"]).max()
+            continue
+        _allclose_rel(N(p.grad), ref, 1e-4, floor=1e-2 * gmax)
+    for n, b in m.mapping_network.named_buffers():
+        if b.dtype.is_floating_point:
+            _allclose_rel(N(b), d[t + ".buf.mapping_network." + n], 1e-5)
