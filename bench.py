@@ -1,8 +1,10 @@
 """Benchmark of the MCAQ spatial-adaptive-quantization hook path on MI355X.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5] [--pipeline D] [--no-cpu]
+                    [--e2e [--amp]]
 
-(--config 5: the QAT training step of the hooks, `main_qat`.)
+(--config 5: the QAT training step of the hooks, `main_qat`; --e2e: the
+end-to-end image rate with the YOLOv8 network and NMS, `main_e2e`.)
 
 A step = the three backbone hooks (C3/C4/C5) of one batch: channel statistics,
 morphological complexity (phi1..5, MLP, bilateral), bit mapper, soft mask and
@@ -268,6 +270,107 @@ def main_qat(args, world, rank, dev, pg):
         dist.destroy_process_group()
 
 
+E2E_CONF, E2E_IOU, E2E_MAX_DET = 0.25, 0.45, 1000    # Predictor defaults (inference.py:45-48)
+
+
+def main_e2e(args, world, rank, dev, pg):
+    """End-to-end MCAQ inference (BASELINE metric): YOLOv8
+    (MIOpen convolutions, seeded weights) with the MCAQ hooks at C3/C4/C5 on
+    the HIP kernels, Detect decode, batched HIP NMS; N > 1: each rank its
+    batch shard, hook min/max all-reduced, detections all-gathered over RCCL.
+    N = 1: the whole step is one HIP graph."""
+    from mcaq_yolo_amd.postprocess import gather_detections, nms_padded
+    from mcaq_yolo_amd.yolo import MCAQYOLO
+    name, B, chans, grid, mapper = CONFIGS[args.config]
+    torch.manual_seed(0)
+    m = MCAQYOLO(name, grid_size=grid, bit_mapping=mapper, device=dev)
+    m.load_state_dict(hook_state_dict(dev), strict=False)
+    m.eval()
+    if pg is not None:
+        m.process_group, m.batch_offset, m.batch_total = pg, rank * B, world * B
+    g = torch.Generator(device="cpu").manual_seed(1000 * args.config + rank)
+    imgs = torch.rand(B, 3, 640, 640, generator=g).to(dev)
+    amp = args.amp
+
+    def step(hooks=True):
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            if hooks:
+                (y, _), aux = m(imgs, temperature=1.0, return_aux=True)
+            else:
+                y, _ = m.model(imgs)
+        out, cnt = nms_padded(y.float(), E2E_CONF, E2E_IOU, E2E_MAX_DET)
+        if pg is not None:
+            out, cnt = gather_detections(out, cnt, pg)
+        return out, cnt
+
+    def timed(fn, n):
+        if pg is not None:
+            import torch.distributed as dist
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            fn()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / n
+        if pg is not None:
+            import torch.distributed as dist
+            t = torch.tensor([dt], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt = float(t.item())
+        return dt
+
+    runs = {}
+    with torch.no_grad():
+        for hooks in (True, False):
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                for _ in range(max(args.warmup, 2)):
+                    step(hooks)
+            torch.cuda.current_stream().wait_stream(side)
+            torch.cuda.synchronize()
+            fn = lambda h=hooks: step(h)
+            if pg is None and not args.eager:
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):
+                    res = step(hooks)
+                fn = graph.replay
+                fn()
+            else:
+                res = step(hooks)
+            torch.cuda.synchronize()
+            runs[hooks] = (timed(fn, args.steps), res)
+    step_s, (out, cnt) = runs[True]
+    net_s = runs[False][0]
+    elems = sum(B * c * h * w for c, (h, w) in zip(chans, SIZES))
+    if rank == 0:
+        achieved = 12 * elems / step_s / 1e9
+        out_j = {
+            "metric": "images/sec @640x640 end-to-end MCAQ infer, 1/2/4/8 MI355X; % HBM roofline",
+            "value": round(world * B / step_s, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16-net/f32-hooks" if amp else "f32",
+            "data": "synthetic torch.rand images 640x640, seeded YOLOv8 + MCAQ weights",
+            "config": {"workload": "%s bs%d/GPU 640x640 end-to-end: YOLOv8 (MIOpen) + MCAQ hooks C3/C4/C5 (HIP) + "
+                                   "Detect decode + HIP NMS (conf %.2f, IoU %.2f, max_det %d)%s"
+                                   % (name, B, E2E_CONF, E2E_IOU, E2E_MAX_DET,
+                                      " + RCCL detection all-gather" if pg is not None else ""),
+                       "global_batch": world * B, "grid_size": grid, "mapper": mapper,
+                       "parallelism": "dp%d" % world, "hip_graph": pg is None and not args.eager,
+                       "network_only_ms_per_step": round(net_s * 1e3, 4),
+                       "mcaq_hooks_ms_per_step": round((step_s - net_s) * 1e3, 4),
+                       "detections_per_image": round(float(cnt.float().mean()), 2)},
+            "step_roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": round(achieved / HBM_PEAK_GBS, 4),
+                              "kernel": "MCAQ hook bytes (12 B per C3/C4/C5 element) over the whole e2e step"},
+        }
+        print(json.dumps(out_j), flush=True)
+    if pg is not None:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
 def cpu_baseline(cfg_id, budget_s=12.0):
     """Oracle (numpy port of the reference path) on the host: one image per
     hook scale per iteration, repeated for ~budget_s seconds -> images/s."""
@@ -408,6 +511,8 @@ def main():
                     help="2/3/4: inference hook path; 5: QAT hook training step")
     ap.add_argument("--pipeline", type=int, default=3, help="batches in flight (independent plans/streams)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--e2e", action="store_true", help="end-to-end: YOLOv8 network + hooks + NMS (main_e2e)")
+    ap.add_argument("--amp", action="store_true", help="--e2e: network under bf16 autocast (hooks stay fp32)")
     ap.add_argument("--eager", action="store_true", help="no HIP graph (--schedule streams)")
     ap.add_argument("--schedule", choices=("split", "streams"), default="streams",
                     help="split: HBM passes on one stream, morphology on two (SplitRunner); "
@@ -437,6 +542,8 @@ def main():
 
     if args.config == 5:
         return main_qat(args, world, rank, dev, pg)
+    if args.e2e:
+        return main_e2e(args, world, rank, dev, pg)
     name, B, chans, grid, mapper = CONFIGS[args.config]
     depth = max(1, args.pipeline)
     cm, mm, sm = load_blobs(dev)

@@ -18,6 +18,10 @@
  *       <- SpatialAdaptiveQuantization training branch + StraightThroughEstimator
  *          + update_running_stats (mcaq_yolo/core/quantization.py:699-727,
  *          69-118, 319-353): the QAT quantizer of BASELINE config 5.
+ *   mcaq_nms
+ *       <- ultralytics non_max_suppression + torchvision nms as called by
+ *          Predictor.postprocess / predict_batch (mcaq_yolo/inference.py:
+ *          213-219, 410-417): the detection postprocess of the e2e path.
  * Up to three hook scales (C3/C4/C5) are processed by one launch.
  */
 #ifndef MCAQ_HIP_H_
@@ -36,7 +40,7 @@ typedef void* hipStream_t;
 extern "C" {
 #endif
 
-#define MCAQ_ABI_VERSION 4
+#define MCAQ_ABI_VERSION 5
 /* largest dynamic LDS request of the morph kernel (gfx950: 160 KiB per CU) */
 #define MCAQ_MORPH_LDS_LIMIT 163840
 
@@ -176,6 +180,18 @@ size_t mcaq_qat_work_floats(int B, int C, int H, int W);
  * (first != 0: running <- batch), in place. */
 int mcaq_ema_stats(const float* batch_min, const float* batch_max, float* running_min, float* running_max,
                    int C, double momentum, int first, hipStream_t stream);
+
+/* ---- batched NMS of YOLOv8 Detect outputs ----------------------------------
+ * pred (B, no, N) fp32 with no = 4 + nc rows (cx, cy, w, h, class scores);
+ * per image: candidates with max class score > conf_thres, xyxy boxes,
+ * stable score-descending order, first max_nms, class offset cls*max_wh
+ * (agnostic: none), greedy IoU > iou_thres suppression (torchvision CPU
+ * arithmetic), first max_det kept.  out (B, max_det, 6) = x1 y1 x2 y2 conf
+ * cls (rows past counts[b] zeroed), counts (B) int32.  work:
+ * mcaq_nms_work_floats(B, max_det) floats.  N <= 16384 (8400 at 640x640). */
+int mcaq_nms(const float* pred, int B, int no, int N, int nc, float conf_thres, double iou_thres, int max_det,
+             int max_nms, float max_wh, int agnostic, float* out, int* counts, float* work, hipStream_t stream);
+size_t mcaq_nms_work_floats(int B, int max_det);
 
 int mcaq_abi_version(void);
 

@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libmcaq_hip.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -55,7 +55,8 @@ F_BIN_OTSU, F_NO_EULER = 256, 512
 
 EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats", "mcaq_stats_units",
            "mcaq_finalize", "mcaq_morph", "mcaq_morph_finalize", "mcaq_morph_scratch_bytes", "mcaq_quant",
-           "mcaq_qat_forward", "mcaq_qat_backward", "mcaq_qat_work_floats", "mcaq_ema_stats")
+           "mcaq_qat_forward", "mcaq_qat_backward", "mcaq_qat_work_floats", "mcaq_ema_stats",
+           "mcaq_nms", "mcaq_nms_work_floats")
 
 _LIB = None
 
@@ -84,6 +85,10 @@ def _declare(lib):
     lib.mcaq_qat_work_floats.argtypes = [I, I, I, I]
     lib.mcaq_ema_stats.restype = I
     lib.mcaq_ema_stats.argtypes = [P, P, P, P, I, ctypes.c_double, I, P]
+    lib.mcaq_nms.restype = I
+    lib.mcaq_nms.argtypes = [P, I, I, I, I, Fl, ctypes.c_double, I, I, Fl, I, P, P, P, P]
+    lib.mcaq_nms_work_floats.restype = ctypes.c_size_t
+    lib.mcaq_nms_work_floats.argtypes = [I, I]
     return lib
 
 

@@ -902,3 +902,4 @@ int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream) 
 }  // extern "C"
 
 #include "mcaq_qat.h"
+#include "mcaq_nms.h"

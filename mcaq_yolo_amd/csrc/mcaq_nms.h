@@ -1,0 +1,223 @@
+// mcaq_nms.h - gfx950 batched non-maximum suppression of YOLOv8 Detect
+// outputs: the postprocess of Predictor.predict / predict_batch
+// (mcaq_yolo/inference.py:213-219, 410-417), which calls ultralytics
+// `non_max_suppression(preds, conf_thres, iou_thres, max_det)` (ultralytics
+// 8.4.63, requirements-lock.txt:13; not vendored) whose suppression step is
+// torchvision's CPU `nms` kernel.  Restated from their published algorithm:
+//
+//   per image: candidates = anchors with max class score > conf_thres
+//              (score = max, cls = first argmax); box xywh -> xyxy
+//              (xy -/+ wh/2); order by score descending (stable: anchor
+//              index ascending on ties); keep the first max_nms;
+//              boxes offset by cls * max_wh (0 when agnostic);
+//              greedy: a candidate is kept unless IoU(kept, cand) > iou_thres
+//              for an earlier kept box, IoU = inter / (area_k + area_c - inter)
+//              in fp32, compared in double; the first max_det kept boxes.
+//
+// One 1024-thread workgroup per image.  Phase 1 streams the (4+nc, N) slab of
+// the image once (coalesced over anchors), compacting candidates into a
+// 64-bit key array in LDS (ordered-score << 32 | anchor << 18 | cls).  Phase 2
+// bitonic-sorts the keys in LDS.  Phase 3 walks the sorted list in chunks of
+// 256: every candidate is tested against the boxes kept so far (4 threads per
+// candidate), a 256 x 256 chunk-local suppression bit matrix is built (one
+// 64-bit word per thread), then one lane resolves the chunk sequentially
+// with bit operations - exactly the greedy order of the CPU kernel.
+#pragma once
+
+namespace mcaq {
+
+constexpr int NMS_THREADS = 1024;
+constexpr int NMS_MAX_ANCHORS = 16384;   // LDS key array (128 KiB)
+constexpr int NMS_CHUNK = 256;
+
+struct NmsArgs {
+  const float* pred;   // (B, no, N)
+  float* out;          // (B, max_det, 6)
+  int* counts;         // (B)
+  float* kept;         // (B, max_det, 8) workspace: offset box + area
+  int B, no, N, nc, max_det, max_nms, agnostic;
+  float conf, max_wh;
+  double iou;
+};
+
+// order-preserving map of a float to uint32, inverted: ascending key order =
+// descending score
+__device__ __forceinline__ unsigned int nms_score_key(float s) {
+  const unsigned int u = __float_as_uint(s);
+  const unsigned int o = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return ~o;
+}
+__device__ __forceinline__ float nms_key_score(unsigned int k) {
+  const unsigned int o = ~k;
+  const unsigned int u = (o & 0x80000000u) ? (o & 0x7fffffffu) : ~o;
+  return __uint_as_float(u);
+}
+
+// torchvision nms_kernel.cpp: i = the earlier (kept) box, j = the later one
+__device__ __forceinline__ bool nms_iou_gt(float4 bi, float ai, float4 bj, float aj, double thr) {
+  const float xx1 = fmaxf(bi.x, bj.x), yy1 = fmaxf(bi.y, bj.y);
+  const float xx2 = fminf(bi.z, bj.z), yy2 = fminf(bi.w, bj.w);
+  const float w = fmaxf(0.0f, __fsub_rn(xx2, xx1)), h = fmaxf(0.0f, __fsub_rn(yy2, yy1));
+  const float inter = __fmul_rn(w, h);
+  const float ovr = __fdiv_rn(inter, __fsub_rn(__fadd_rn(ai, aj), inter));
+  return (double)ovr > thr;
+}
+
+__global__ __launch_bounds__(NMS_THREADS) void mcaq_nms_kernel(NmsArgs a) {
+  __shared__ unsigned long long keys[NMS_MAX_ANCHORS];
+  __shared__ float4 cbox[NMS_CHUNK];        // offset boxes of the chunk
+  __shared__ float4 craw[NMS_CHUNK];        // xyxy boxes (output)
+  __shared__ float carea[NMS_CHUNK], cscore[NMS_CHUNK], ccls[NMS_CHUNK];
+  __shared__ int csup[NMS_CHUNK];
+  __shared__ unsigned long long cmask[NMS_CHUNK][4];
+  __shared__ int s_cnt, s_K;
+
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int N = a.N;
+  const float* P = a.pred + (size_t)b * a.no * N;
+  float* kept = a.kept + (size_t)b * a.max_det * 8;
+  float* out = a.out + (size_t)b * a.max_det * 6;
+  if (tid == 0) { s_cnt = 0; s_K = 0; }
+  __syncthreads();
+
+  // ---- phase 1: candidates (max class score > conf), compacted into LDS
+  for (int ai = tid; ai < N; ai += NMS_THREADS) {
+    float best = P[(size_t)4 * N + ai];
+    int bj = 0;
+    for (int c = 1; c < a.nc; ++c) {
+      const float v = P[(size_t)(4 + c) * N + ai];
+      if (v > best) { best = v; bj = c; }
+    }
+    if (best > a.conf) {
+      const int slot = atomicAdd(&s_cnt, 1);
+      keys[slot] = ((unsigned long long)nms_score_key(best) << 32) |
+                   ((unsigned long long)ai << 18) | (unsigned long long)bj;
+    }
+  }
+  __syncthreads();
+  const int n = s_cnt;
+  int np2 = 1;
+  while (np2 < n) np2 <<= 1;
+  for (int i = n + tid; i < np2; i += NMS_THREADS) keys[i] = ~0ull;
+  __syncthreads();
+
+  // ---- phase 2: bitonic sort (ascending key = score desc, anchor asc)
+  for (int k = 2; k <= np2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < np2; i += NMS_THREADS) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const unsigned long long x = keys[i], y = keys[ixj];
+          const bool up = (i & k) == 0;
+          if ((x > y) == up) { keys[i] = y; keys[ixj] = x; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+
+  // ---- phase 3: greedy suppression in chunks of 256 sorted candidates
+  const int nproc = n < a.max_nms ? n : a.max_nms;
+  for (int base = 0; base < nproc; base += NMS_CHUNK) {
+    const int cn = (nproc - base) < NMS_CHUNK ? (nproc - base) : NMS_CHUNK;
+    if (tid < cn) {
+      const unsigned long long key = keys[base + tid];
+      const int ai = (int)((key >> 18) & 0x3fffu);
+      const int cls = (int)(key & 0x3ffffu);
+      const float x = P[ai], y = P[(size_t)N + ai], w = P[(size_t)2 * N + ai], h = P[(size_t)3 * N + ai];
+      const float hw = __fdiv_rn(w, 2.0f), hh = __fdiv_rn(h, 2.0f);   // xywh2xyxy
+      const float4 r = make_float4(__fsub_rn(x, hw), __fsub_rn(y, hh), __fadd_rn(x, hw), __fadd_rn(y, hh));
+      const float fc = (float)cls;
+      const float off = a.agnostic ? 0.0f : __fmul_rn(fc, a.max_wh);
+      const float4 o = make_float4(__fadd_rn(r.x, off), __fadd_rn(r.y, off), __fadd_rn(r.z, off), __fadd_rn(r.w, off));
+      craw[tid] = r;
+      cbox[tid] = o;
+      carea[tid] = __fmul_rn(__fsub_rn(o.z, o.x), __fsub_rn(o.w, o.y));
+      cscore[tid] = nms_key_score((unsigned int)(key >> 32));
+      ccls[tid] = fc;
+      csup[tid] = 0;
+    }
+    __syncthreads();
+    const int K = s_K;
+    // candidates vs the boxes kept by earlier chunks: 4 threads per candidate
+    {
+      const int t = tid & (NMS_CHUNK - 1), g = tid >> 8;
+      if (t < cn && K > 0) {
+        const float4 bj = cbox[t];
+        const float aj = carea[t];
+        bool s = false;
+        for (int k = g; k < K && !s; k += 4) {
+          const float4 bk = *reinterpret_cast<const float4*>(kept + (size_t)k * 8);
+          const float ak = kept[(size_t)k * 8 + 4];
+          s = nms_iou_gt(bk, ak, bj, aj, a.iou);
+        }
+        if (s) csup[t] = 1;
+      }
+    }
+    // chunk-local matrix: row r, word w covers columns 64w..64w+63 (> r)
+    {
+      const int r = tid >> 2, w = tid & 3;
+      unsigned long long bits = 0;
+      if (r < cn) {
+        const float4 br = cbox[r];
+        const float ar = carea[r];
+        const int c0 = w * 64;
+        for (int q = 0; q < 64; ++q) {
+          const int c = c0 + q;
+          if (c > r && c < cn && nms_iou_gt(br, ar, cbox[c], carea[c], a.iou)) bits |= 1ull << q;
+        }
+      }
+      cmask[r][w] = bits;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      unsigned long long rm0 = 0, rm1 = 0, rm2 = 0, rm3 = 0;
+      int Kc = K;
+      for (int r = 0; r < cn && Kc < a.max_det; ++r) {
+        const unsigned long long wsel = (r < 64) ? rm0 : (r < 128) ? rm1 : (r < 192) ? rm2 : rm3;
+        if (csup[r] || ((wsel >> (r & 63)) & 1ull)) continue;
+        const float4 o = cbox[r];
+        float* kp = kept + (size_t)Kc * 8;
+        kp[0] = o.x; kp[1] = o.y; kp[2] = o.z; kp[3] = o.w; kp[4] = carea[r];
+        const float4 rr = craw[r];
+        float* op = out + (size_t)Kc * 6;
+        op[0] = rr.x; op[1] = rr.y; op[2] = rr.z; op[3] = rr.w; op[4] = cscore[r]; op[5] = ccls[r];
+        ++Kc;
+        rm0 |= cmask[r][0]; rm1 |= cmask[r][1]; rm2 |= cmask[r][2]; rm3 |= cmask[r][3];
+      }
+      s_K = Kc;
+    }
+    __syncthreads();
+    if (s_K >= a.max_det) break;
+  }
+  __syncthreads();
+  const int Kf = s_K;
+  for (int i = Kf * 6 + tid; i < a.max_det * 6; i += NMS_THREADS) out[i] = 0.0f;
+  if (tid == 0) a.counts[b] = Kf;
+}
+
+}  // namespace mcaq
+
+extern "C" {
+
+size_t mcaq_nms_work_floats(int B, int max_det) {
+  return (size_t)(B > 0 ? B : 0) * (size_t)(max_det > 0 ? max_det : 0) * 8;
+}
+
+int mcaq_nms(const float* pred, int B, int no, int N, int nc, float conf_thres, double iou_thres, int max_det,
+             int max_nms, float max_wh, int agnostic, float* out, int* counts, float* work, hipStream_t stream) {
+  if (B < 0 || nc < 1 || nc >= (1 << 18) || no != 4 + nc || N < 0 || N > mcaq::NMS_MAX_ANCHORS ||
+      max_det < 1 || max_nms < 1)
+    return (int)hipErrorInvalidValue;
+  if (B == 0) return 0;
+  if (!pred || !out || !counts || !work) return (int)hipErrorInvalidValue;
+  mcaq::NmsArgs a;
+  a.pred = pred; a.out = out; a.counts = counts; a.kept = work;
+  a.B = B; a.no = no; a.N = N; a.nc = nc; a.max_det = max_det; a.max_nms = max_nms;
+  a.agnostic = agnostic ? 1 : 0; a.conf = conf_thres; a.max_wh = max_wh; a.iou = iou_thres;
+  hipLaunchKernelGGL(mcaq::mcaq_nms_kernel, dim3(B), dim3(mcaq::NMS_THREADS), 0, stream, a);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

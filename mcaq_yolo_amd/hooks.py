@@ -44,6 +44,11 @@ class MCAQHooks(nn.Module):
             self.quantizers[str(idx)] = SpatialAdaptiveQuantization(calibration_mode="minmax",
                                                                     smooth_transitions=True, per_channel=True)
         self._mcaq_state = {"active": False}
+        # batch-sharded inference (one process per GPU): the per-channel batch
+        # min/max is made global by one all-reduce per hook, and the fractal
+        # regression's reduction order follows the image's global batch index
+        self.process_group = None
+        self.batch_offset, self.batch_total = 0, None
         self._handles = []
         self._plans = {}
         if str(device).startswith("cuda") and torch.cuda.is_available():
@@ -133,7 +138,7 @@ class MCAQHooks(nn.Module):
         for k in ("y", "complexity", "bits"):      # fresh outputs: the caller keeps them
             b[k] = torch.empty_like(b[k])
         minmax = None
-        if bool(quantizer.stats_frozen) and quantizer.running_min is not None:
+        if quantizer._frozen() and quantizer.running_min is not None:
             minmax = [(quantizer.running_min.reshape(-1), quantizer.running_max.reshape(-1))]
         elif not quantizer.per_channel:
             raise NotImplementedError("per-tensor statistics on the fused hook path")
@@ -144,7 +149,9 @@ class MCAQHooks(nn.Module):
         plan.run([x], an.cmlp_blob(), mapper_blob, [sm], temperature=state.get("temperature", 1.0),
                  mapper_kind=self.bit_mapping, normalize=self.normalize_complexity, minmax=minmax,
                  binarize_otsu=an.binarize_impl == "otsu", contour_components=an.contour_components,
-                 min_bits=self.bit_mapper.min_bits, max_bits=self.bit_mapper.max_bits, quantize=quantize)
+                 min_bits=self.bit_mapper.min_bits, max_bits=self.bit_mapper.max_bits, quantize=quantize,
+                 process_group=self.process_group if minmax is None else None,
+                 batch_offset=self.batch_offset, batch_total=self.batch_total)
         feat_q = b["y"] if quantize else feat
         state.setdefault("aux", []).append({"layer": layer_idx, "complexity": b["complexity"],
                                             "bit_map": b["bits"], "features_q": feat_q})

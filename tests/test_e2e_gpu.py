@@ -1,0 +1,155 @@
+"""End-to-end path on the GPU: the HIP batched NMS (mcaq_nms) bit-exact
+against the NMS restatement (oracle/nms_oracle.py), and MCAQYOLO (YOLOv8 +
+MCAQ hooks registered by backbone discovery) with every hook's bits and
+quantized features bit-exact against the hook oracle on the features that
+actually arrived at the hook."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_weights
+from oracle import mcaq_oracle as O
+from oracle import nms_oracle as NO
+
+pytestmark = pytest.mark.gpu
+f32 = np.float32
+DEV = "cuda"
+
+
+def _synthetic_preds(B, nc, N, seed, dense=0.3, ties=False, grid=False):
+    """Detect-like predictions: boxes clustered so that suppression matters,
+    a fraction `dense` of anchors above 0.25."""
+    rng = np.random.default_rng(seed)
+    p = np.zeros((B, 4 + nc, N), f32)
+    centres = rng.uniform(0, 640, (B, 12, 2)).astype(f32)
+    pick = rng.integers(0, 12, (B, N))
+    xy = centres[np.arange(B)[:, None], pick] + rng.normal(0, 12, (B, N, 2)).astype(f32)
+    if grid:      # quantised coordinates: exact IoU ties, identical boxes
+        xy = np.round(xy / 8) * 8
+    p[:, 0], p[:, 1] = xy[..., 0], xy[..., 1]
+    p[:, 2:4] = rng.uniform(8, 120, (B, 2, N)).astype(f32)
+    s = rng.uniform(0, 0.25 / max(dense, 1e-3), (B, nc, N)).astype(f32)
+    if ties:
+        s = np.round(s * 16) / 16
+    p[:, 4:] = s
+    return p
+
+
+def _check(p, conf=0.25, iou=0.45, max_det=300, agnostic=False, max_nms=30000):
+    from mcaq_yolo_amd.postprocess import nms_padded
+    out, cnt = nms_padded(torch.from_numpy(p).to(DEV), conf, iou, max_det, agnostic, max_nms)
+    out, cnt = out.cpu().numpy(), cnt.cpu().numpy()
+    ref = NO.non_max_suppression(p, conf, iou, max_det, agnostic, max_nms)
+    for b, r in enumerate(ref):
+        assert cnt[b] == r.shape[0], (b, cnt[b], r.shape)
+        assert np.array_equal(out[b, :cnt[b]], r), b
+        assert not out[b, cnt[b]:].any()
+    return cnt
+
+
+@pytest.mark.parametrize("B,nc,N,seed,kw", [
+    (4, 80, 8400, 0, {}),                                   # 640x640 head shape
+    (2, 80, 8400, 1, {"iou": 0.65, "max_det": 300}),         # eval NMS (utils/evaluation.py:197-203)
+    (3, 80, 8400, 2, {"max_det": 1000}),                     # Predictor default max_det
+    (2, 3, 5000, 3, {"agnostic": True}),
+    (2, 1, 3000, 4, {"max_det": 7}),                         # early stop at max_det
+    (2, 5, 2100, 5, {"max_nms": 500}),                       # max_nms truncation
+])
+def test_nms_matches_oracle(B, nc, N, seed, kw):
+    cnt = _check(_synthetic_preds(B, nc, N, seed), **kw)
+    assert cnt.min() > 0
+
+
+def test_nms_ties_and_duplicates():
+    _check(_synthetic_preds(3, 4, 4000, 7, ties=True, grid=True))
+    _check(_synthetic_preds(2, 4, 4000, 8, ties=True, grid=True), iou=0.0)
+
+
+def test_nms_empty_and_dense():
+    p = _synthetic_preds(2, 80, 8400, 9)
+    p[:, 4:] = 0.1
+    assert _check(p).sum() == 0                                    # no candidate
+    p = _synthetic_preds(1, 2, 16384, 10, dense=1.0)               # max anchors, every anchor a candidate
+    _check(p, conf=0.0, max_det=1000)
+
+
+def test_nms_list_api_and_errors():
+    from mcaq_yolo_amd.postprocess import non_max_suppression
+    p = _synthetic_preds(2, 80, 8400, 11)
+    dets = non_max_suppression(torch.from_numpy(p).to(DEV), 0.25, 0.45, max_det=300)
+    ref = NO.non_max_suppression(p, 0.25, 0.45, 300)
+    assert len(dets) == 2 and all(np.array_equal(d.cpu().numpy(), r) for d, r in zip(dets, ref))
+    with pytest.raises(NotImplementedError):
+        non_max_suppression(torch.from_numpy(p).to(DEV), classes=[0])
+    with pytest.raises(RuntimeError):
+        non_max_suppression(torch.from_numpy(p), 0.25)
+    with pytest.raises(RuntimeError):                          # N > 16384 anchors
+        non_max_suppression(torch.zeros(1, 84, 16385, device=DEV))
+
+
+def _mcaq_yolo(mapper="mlp"):
+    from mcaq_yolo_amd.yolo import MCAQYOLO
+    torch.manual_seed(0)
+    m = MCAQYOLO("yolov8n", grid_size=8, bit_mapping=mapper, device=DEV)
+    W = load_weights()
+    sd = {}
+    for k, v in W.items():
+        t = torch.from_numpy(np.asarray(v))
+        if k.startswith("soft_mask."):
+            for i in (4, 6, 9):
+                sd["quantizers.%d.%s" % (i, k)] = t
+        elif mapper == "mlp" or not k.startswith("bit_mapper."):
+            sd[k] = t
+    m.load_state_dict(sd, strict=False)
+    return m.eval()
+
+
+@pytest.mark.parametrize("mapper", ["mlp", "linear"])
+def test_mcaq_yolo_hooks_match_oracle(mapper):
+    m = _mcaq_yolo(mapper)
+    assert m.backbone_out_indices == [4, 6, 9]
+    raw = {}
+    hs = [m.model.model[i].register_forward_hook(lambda mod, a, o, k=i: raw.__setitem__(k, o.detach().clone()),
+                                                 prepend=True) for i in (4, 6, 9)]
+    g = torch.Generator().manual_seed(3)
+    x = torch.rand(2, 3, 320, 320, generator=g).to(DEV)
+    with torch.no_grad():
+        (y, _), aux = m(x, temperature=1.0, return_aux=True)
+    for h in hs:
+        h.remove()
+    assert aux["feature_layers"] == [4, 6, 9] and y.shape == (2, 84, 2100)
+    W = load_weights()
+    for layer, bits, fq in zip(aux["feature_layers"], aux["bit_map"], aux["quantized_features"]):
+        ref = O.hook_forward(raw[layer].cpu().numpy(), W, 8, mapper=mapper)
+        assert np.array_equal(bits.cpu().numpy(), ref["bits"]), layer
+        assert np.array_equal(fq.cpu().numpy(), ref["y"]), layer
+    bits_mean = np.mean([b.float().mean().item() for b in aux["bit_map"]])
+    assert abs(float(aux["avg_bits"]) - bits_mean) < 1e-6
+
+
+def test_mcaq_yolo_graph_capture_and_nms():
+    """The whole e2e inference step (network + 3 hooks + NMS) captured as one
+    HIP graph replays to the eager result."""
+    from mcaq_yolo_amd.postprocess import nms_padded
+    m = _mcaq_yolo("mlp")
+    x = torch.rand(2, 3, 256, 256, generator=torch.Generator().manual_seed(5)).to(DEV)
+
+    def step():
+        (y, _), aux = m(x)
+        out, cnt = nms_padded(y, 0.001, 0.45, 300)
+        return y, out, cnt, aux["bit_map"][0]
+
+    with torch.no_grad():
+        ref = [t.clone() for t in step()]
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            step()
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            outs = step()
+        graph.replay()
+        torch.cuda.synchronize()
+    for a, b in zip(ref, outs):
+        assert torch.equal(a, b)
