@@ -271,6 +271,52 @@ class MorphologicalComplexityAnalyzer(nn.Module):
         phi, _ = self._run(features, want_c=False)
         return phi, self._detailed(phi)
 
+    def score_image(self, features: torch.Tensor) -> torch.Tensor:
+        """morphology.py:923-937: per-image Eq.(8) score for curriculum sorting,
+        mean over tiles of sum_i alpha_i * phi_i (alpha = |feature_weights|
+        normalised to sum 1), clamped to [0, 1].  phi comes from the morph
+        kernel; the 5-term dot product is a (B, ht, wt) device reduction."""
+        phi, _ = self.compute_phi_tiles(features)
+        with torch.no_grad():
+            alpha = self.feature_weights.detach().abs().to(phi.device)
+            alpha = alpha / alpha.sum().clamp(min=1e-8)
+            c = (phi[..., :5] * alpha.view(1, 1, 1, 5)).sum(dim=-1)
+            return c.mean(dim=(1, 2)).clamp(0.0, 1.0)
+
+    def fit_feature_weights(self, batches, max_batches: int = 64):
+        """morphology.py:876-921: NNLS fit of alpha so Eq.(8) tracks the trained
+        complexity MLP (pre-bilateral), projected onto the simplex.  Offline
+        curriculum utility: phi and the MLP target are computed on the GPU, the
+        5-unknown NNLS solve runs on the host (scipy), as in the reference."""
+        import numpy as np
+        from scipy.optimize import nnls
+        Ps, Cs = [], []
+        dev = next(self.complexity_mlp.parameters()).device
+        for i, x in enumerate(batches):
+            if isinstance(x, dict):
+                x = x.get("img")
+            x = x.float()
+            if x.dim() == 3:
+                x = x.unsqueeze(0)
+            if x.max() > 1.5:
+                x = x / 255.0
+            x = x.to(dev)
+            phi, _ = self.compute_phi_tiles(x)
+            with torch.no_grad():
+                c = self.complexity_mlp(phi.reshape(-1, 8))
+            Ps.append(phi[..., :5].reshape(-1, 5).cpu())
+            Cs.append(c.reshape(-1, 1).cpu())
+            if i + 1 >= max_batches:
+                break
+        P = torch.cat(Ps).double().numpy()
+        C = torch.cat(Cs).double().numpy().ravel()
+        alpha, _ = nnls(P, C)
+        s = float(alpha.sum())
+        alpha = alpha / s if s > 1e-12 else np.ones(5) / 5.0
+        self.feature_weights.copy_(torch.as_tensor(alpha, dtype=self.feature_weights.dtype,
+                                                   device=self.feature_weights.device))
+        return alpha
+
     @staticmethod
     def bilateral_filter(complexity_map, sigma_spatial: float = 2.0, sigma_range: float = 0.1,
                          kernel_size: int = 5):

@@ -501,7 +501,7 @@ constexpr int QMAXNT = 1024;   // max tiles per image for on-the-fly m(p)
 // soft-mask value are fetched once; per-(channel, bits) scale / zero-point
 // come from an LDS table built by the workgroup (IEEE divisions, as
 // QuantizationParameters computes them).
-template <bool kVec>
+template <bool kVec, bool kNTL, bool kNTS>
 __global__ __launch_bounds__(256) void mcaq_quant_kernel(QuantArgs a) {
   __shared__ float2 qt[QSLICE * QMAXBITS];
   __shared__ float mts[QMAXNT];
@@ -571,7 +571,9 @@ __global__ __launch_bounds__(256) void mcaq_quant_kernel(QuantArgs a) {
     for (int c = 0; c < QCW; ++c) {
       const float* row = xb + (size_t)(c < ncw ? c : 0) * HW;
       if (kVec) {
-        const float4 t = *reinterpret_cast<const float4*>(row + qa);
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        const f4v t = kNTL ? __builtin_nontemporal_load(reinterpret_cast<const f4v*>(row + qa))
+                          : *reinterpret_cast<const f4v*>(row + qa);
         v[c][0] = t.x; v[c][1] = t.y; v[c][2] = t.z; v[c][3] = t.w;
       } else {
 #pragma unroll
@@ -620,7 +622,13 @@ __global__ __launch_bounds__(256) void mcaq_quant_kernel(QuantArgs a) {
     }
     float* orow = yb + (size_t)c * HW;
     if (kVec) {
-      if (pv[0]) *reinterpret_cast<float4*>(orow + q0) = make_float4(o[0], o[1], o[2], o[3]);
+      if (pv[0]) {
+        typedef float f4v __attribute__((ext_vector_type(4)));
+        const f4v ov = {o[0], o[1], o[2], o[3]};
+        // y is written once and not re-read by this step: streaming store
+        if (kNTS) __builtin_nontemporal_store(ov, reinterpret_cast<f4v*>(orow + q0));
+        else *reinterpret_cast<f4v*>(orow + q0) = ov;
+      }
     } else {
 #pragma unroll
       for (int k = 0; k < 4; ++k) if (pv[k]) orow[q0 + k] = o[k];
@@ -892,10 +900,26 @@ int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream) 
   a.units_total = units;
   bool vec = true;
   for (int i = 0; i < nscales; ++i) vec = vec && ((scales[i].H * scales[i].W) & 3) == 0;
-  if (vec)
-    hipLaunchKernelGGL(mcaq_quant_kernel<true>, dim3(units), dim3(256), 0, stream, a);
+  // MCAQ_QUANT_NT bit 0: streaming (nontemporal) stores of y, bit 1:
+  // nontemporal loads of x.  Default (measured): NT stores
+  // always; NT loads only when the launch reads > 256 MB of x (config 3),
+  // where nothing of x survives in L2/MALL anyway; at config 2 they cost 3 us.
+  static int nt_env = -2;
+  if (nt_env == -2) { const char* e = getenv("MCAQ_QUANT_NT"); nt_env = e ? atoi(e) : -1; }
+  size_t xbytes = 0;
+  for (int i = 0; i < nscales; ++i)
+    xbytes += (size_t)scales[i].B * scales[i].C * scales[i].H * scales[i].W * sizeof(float);
+  const int nt = nt_env >= 0 ? nt_env : (xbytes > ((size_t)256 << 20) ? 3 : 1);
+  if (!vec)
+    hipLaunchKernelGGL((mcaq_quant_kernel<false, false, false>), dim3(units), dim3(256), 0, stream, a);
+  else if (nt == 3)
+    hipLaunchKernelGGL((mcaq_quant_kernel<true, true, true>), dim3(units), dim3(256), 0, stream, a);
+  else if (nt == 2)
+    hipLaunchKernelGGL((mcaq_quant_kernel<true, true, false>), dim3(units), dim3(256), 0, stream, a);
+  else if (nt == 1)
+    hipLaunchKernelGGL((mcaq_quant_kernel<true, false, true>), dim3(units), dim3(256), 0, stream, a);
   else
-    hipLaunchKernelGGL(mcaq_quant_kernel<false>, dim3(units), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((mcaq_quant_kernel<true, false, false>), dim3(units), dim3(256), 0, stream, a);
   return (int)hipGetLastError();
 }
 

@@ -399,6 +399,17 @@ def contour_tiles(binmask, tile, contour_components=True):
     return np.where(area > 0, phi5, f32(0.0)).astype(f32)
 
 
+def score_image(x, grid_size=8, feature_weights=None):
+    """score_image (morphology.py:923-937): per-image mean over tiles of
+    sum(alpha * phi[..., :5]), alpha = |w| / max(sum|w|, 1e-8), clamp [0, 1]."""
+    phi = phi_tiles(x, grid_size)
+    w = np.full(5, 0.2, np.float32) if feature_weights is None else np.asarray(feature_weights, np.float32)
+    a = np.abs(w)
+    a = (a / max(np.float32(a.sum()), np.float32(1e-8))).astype(np.float32)
+    c = (phi[..., :5].astype(np.float64) * a.astype(np.float64)).sum(-1)
+    return np.clip(c.mean(axis=(1, 2)), 0.0, 1.0).astype(np.float32)
+
+
 def phi_tiles(x, grid_size=8, batch_offset=0, batch_total=None, internals=False):
     """_phi_tiles_gpu (morphology.py:826-873) -> phi (B, ht, wt, 8)."""
     B, C, H, W = x.shape

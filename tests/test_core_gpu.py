@@ -182,6 +182,24 @@ def test_modules_vs_oracle(mods, name):
         a.grid_size = 8
 
 
+@pytest.mark.parametrize("name", ["p3_c16", "p5_c32"])
+def test_score_image_vs_oracle(mods, name):
+    """Curriculum score (morphology.py:923-937) on the morph kernel's phi;
+    fp32 dot/mean reduction order differs from the float64 oracle: rtol 1e-5."""
+    a, _, _ = mods
+    x = load_case(name)["x"].astype(f32)
+    s = a.score_image(torch.from_numpy(x).to(DEV))
+    ref = O.score_image(x, 8, a.feature_weights.cpu().numpy())
+    assert s.shape == (x.shape[0],)
+    np.testing.assert_allclose(s.cpu().numpy(), ref, rtol=1e-5, atol=1e-6)
+    w0 = a.feature_weights.clone()
+    try:
+        alpha = a.fit_feature_weights([torch.from_numpy(x)], max_batches=1)
+        assert alpha.shape == (5,) and abs(alpha.sum() - 1.0) < 1e-6 and (alpha >= 0).all()
+    finally:
+        a.feature_weights.copy_(w0)
+
+
 def test_hooks_forward_features_vs_oracle():
     """The hook protocol end to end (C3/C4/C5 of one batch) == oracle hook."""
     from mcaq_yolo_amd.hooks import MCAQHooks
