@@ -140,12 +140,16 @@ def test_mcaq_yolo_graph_capture_and_nms():
         return y, out, cnt, aux["bit_map"][0]
 
     with torch.no_grad():
-        ref = [t.clone() for t in step()]
+        # warm up first: MIOpen settles its convolution solvers on the first
+        # calls of a shape, and the eager reference must use the same ones the
+        # captured graph will
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             step()
+            step()
         torch.cuda.current_stream().wait_stream(s)
+        ref = [t.clone() for t in step()]
         graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(graph):
             outs = step()
