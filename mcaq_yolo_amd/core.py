@@ -9,10 +9,17 @@ buffer names (state_dict keys) and error behaviour as the reference:
     LearnedSoftMask                   mcaq_yolo/core/quantization.py:168-239
     SpatialAdaptiveQuantization       mcaq_yolo/core/quantization.py:242-754
 
-so a reference checkpoint loads unchanged (`load_state_dict`).  Every forward
-runs through libmcaq_hip.so (include/mcaq_hip.h); there is no CPU path - a
-non-CUDA tensor or a missing library raises.  The numeric contract is the
-reference's pure-PyTorch path (bit-exact decisions, tests/test_core_gpu.py).
+so a reference checkpoint loads unchanged (`load_state_dict`).
+
+Dispatch (the reference's quantization.py:14-23, 631-634): CUDA (HIP) tensors
+run through libmcaq_hip.so (include/mcaq_hip.h) - a missing library raises,
+there is no silent torch fallback on the GPU; CPU tensors run this package's
+own pure-PyTorch path (`fallback.py`, BASELINE config 1).  The numeric
+contract is the reference's pure-PyTorch path (bit-exact decisions,
+tests/test_core_gpu.py, tests/test_fallback_cpu.py).  When autograd needs a
+gradient of a kernel-computed value (eval mode with grad enabled), the value
+comes from the kernel and the backward recomputes the tile-sized torch graph
+(`_kernel_value`), so gradients reach the reference's parameters.
 
 Training (QAT, BASELINE config 5): the quantizer's per-element work - EMA
 running statistics, the fractional-bit forward and the straight-through
@@ -32,7 +39,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from . import abi
+from . import abi, fallback
 from .engine import tile_size
 
 _CM_SIZE, _MM_SIZE, _SM_SIZE = 2881, 4865, 170
@@ -58,6 +65,41 @@ def _need_cuda(t, what):
 
 def _f32c(t):
     return t.detach().float().contiguous()
+
+
+def _wants_grad(inputs, params=()):
+    return torch.is_grad_enabled() and (any(t.requires_grad for t in inputs) or
+                                        any(p.requires_grad for p in params))
+
+
+class _KernelValue(torch.autograd.Function):
+    """Value from a HIP kernel, gradient from the torch restatement of the same
+    tile-sized function (recomputed in backward).  args = n_in inputs followed
+    by the module parameters torch_fn reads."""
+
+    @staticmethod
+    def forward(ctx, kernel_fn, torch_fn, n_in, *args):
+        ctx.torch_fn, ctx.n_in = torch_fn, n_in
+        ctx.save_for_backward(*args)
+        with torch.no_grad():
+            return kernel_fn(*[a.detach() for a in args[:n_in]])
+
+    @staticmethod
+    def backward(ctx, g):
+        args = ctx.saved_tensors
+        n_in = ctx.n_in
+        need = ctx.needs_input_grad[3:]
+        with torch.enable_grad():
+            ins = [a.detach().requires_grad_(bool(r)) for a, r in zip(args[:n_in], need[:n_in])]
+            out = ctx.torch_fn(*ins)
+            targets = [t for t, r in zip(ins, need[:n_in]) if r] + [p for p, r in zip(args[n_in:], need[n_in:]) if r]
+            grads = iter(torch.autograd.grad(out, targets, g, allow_unused=True) if targets else [])
+        return (None, None, None) + tuple(next(grads) if r else None for r in need)
+
+
+def _kernel_value(kernel_fn, torch_fn, inputs, params):
+    params = [p for p in params if p.requires_grad]
+    return _KernelValue.apply(kernel_fn, torch_fn, len(inputs), *inputs, *params)
 
 
 _MFMA_IDX = {}
@@ -195,10 +237,8 @@ class MorphologicalComplexityAnalyzer(nn.Module):
         if metric_backend != "gpu":
             raise NotImplementedError("metric_backend=%r: only the tensor ('gpu') backend is on the MI355X path "
                                       "(the cv2 backend is offline CPU scoring, out of scope)" % metric_backend)
-        if canny_impl != "cv2compat":
-            raise NotImplementedError("canny_impl=%r not implemented (SURVEY.md 8(f) rank 4)" % canny_impl)
-        if binarize_impl not in ("adaptive", "otsu"):
-            raise ValueError("binarize_impl must be 'adaptive' or 'otsu'")
+        # as the reference: 'legacy' / 'otsu' select the legacy variants, any
+        # other value the cv2-compatible defaults (morphology.py:451-455, 542-548)
         self.grid_size = grid_size
         self.device = device
         self.metric_backend = metric_backend
@@ -235,6 +275,8 @@ class MorphologicalComplexityAnalyzer(nn.Module):
 
     def _run(self, features, want_c):
         _need_cuda(features, "features")
+        if self.canny_impl == "legacy":
+            raise NotImplementedError("canny_impl='legacy' runs on the pure-PyTorch path (CPU tensors) only")
         if features.dim() != 4:
             raise ValueError("features must be (B, C, H, W)")
         x = features.float().contiguous()
@@ -268,7 +310,11 @@ class MorphologicalComplexityAnalyzer(nn.Module):
 
     def compute_phi_tiles(self, features: torch.Tensor):
         """morphology.py:798-824: (phi (B,ht,wt,8), detailed dict of phi1..phi5)."""
-        phi, _ = self._run(features, want_c=False)
+        if not features.is_cuda:
+            phi = fallback.phi_tiles(features, self.grid_size, self.canny_impl, self.binarize_impl,
+                                     self.contour_components)
+        else:
+            phi, _ = self._run(features, want_c=False)
         return phi, self._detailed(phi)
 
     def score_image(self, features: torch.Tensor) -> torch.Tensor:
@@ -335,15 +381,23 @@ class MorphologicalComplexityAnalyzer(nn.Module):
         filtered = (weights * patches).sum(dim=1) / (weights.sum(dim=1) + 1e-8)
         return filtered.reshape(B, H, W)
 
+    def _head(self, phi):
+        """complexity MLP -> bilateral -> clamp on the tile features (morphology.py:959-968)."""
+        B, ht, wt, _ = phi.shape
+        c = self.complexity_mlp(phi.reshape(-1, 8)).reshape(B, ht, wt)
+        return self.bilateral_filter(c).clamp(0.0, 1.0)
+
     def forward(self, features: torch.Tensor, return_detailed: bool = False):
-        if self.training and torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
-            # morphology.py:939-973 with autograd into complexity_mlp: phi is
-            # no-grad side information (morph kernel), the MLP + bilateral run
-            # as torch ops on the (B*ht*wt, 8) tile features
-            phi, _ = self._run(features, want_c=False)
-            B, ht, wt, _ = phi.shape
-            c = self.complexity_mlp(phi.reshape(-1, 8)).reshape(B, ht, wt)
-            c = self.bilateral_filter(c).clamp(0.0, 1.0)
+        if not features.is_cuda:
+            # pure-PyTorch path (morphology.py:939-973 on CPU tensors)
+            phi, _ = self.compute_phi_tiles(features)
+            c = self._head(phi)
+        elif _wants_grad((), self.complexity_mlp.parameters()):
+            # phi is no-grad side information (morph kernel); C is the kernel's
+            # value and its gradient reaches complexity_mlp through the torch
+            # restatement of the MLP + bilateral
+            phi, ck = self._run(features, want_c=True)
+            c = _kernel_value(lambda p: ck, self._head, [phi], list(self.complexity_mlp.parameters()))
         else:
             phi, c = self._run(features, want_c=True)
         if return_detailed:
@@ -386,6 +440,18 @@ def _run_mapper(c, flags, min_bits, max_bits, temperature, return_continuous, ma
     return bits
 
 
+def _finish_bits(bit_map, min_bits, max_bits, temperature, return_continuous):
+    """x max(T, 0.1), straight-through clamp to [min, max], straight-through
+    round-half-even (bit_allocation.py:72-79 / 264-278)."""
+    if temperature is not None:
+        bit_map = bit_map * max(float(temperature), 0.1)
+    clamped = torch.clamp(bit_map, min_bits, max_bits)
+    bit_map = bit_map + (clamped - bit_map).detach()
+    if not return_continuous:
+        bit_map = bit_map + (torch.round(bit_map) - bit_map).detach()
+    return bit_map
+
+
 class LinearBitMapper(nn.Module):
     """bit_allocation.py:12-80: per-image 2-98 % percentile normalisation ->
     b = b_min + (b_max - b_min) * C_n, x temperature, clamp, round."""
@@ -401,10 +467,33 @@ class LinearBitMapper(nn.Module):
     def enforce_weight_constraints(self):
         """No-op (parameter-free), as in the reference."""
 
+    def _forward_torch(self, c, temperature, return_continuous):
+        """bit_allocation.py:54-80 as torch ops (CPU path; the backward of the
+        GPU path): quantile lerp, spread gate, affine, temperature, straight-
+        through clamp and round."""
+        B = c.shape[0]
+        flat = c.reshape(B, -1).float()
+        lo = torch.quantile(flat, 0.02, dim=1, keepdim=True).unsqueeze(-1)
+        hi = torch.quantile(flat, 0.98, dim=1, keepdim=True).unsqueeze(-1)
+        spread = hi - lo
+        cn = torch.where(spread > self.eps_spread, ((c - lo) / (spread + 1e-8)).clamp(0.0, 1.0),
+                         c.clamp(0.0, 1.0))
+        return _finish_bits(self.min_bits + (self.max_bits - self.min_bits) * cn, self.min_bits,
+                            self.max_bits, temperature, return_continuous)
+
     def forward(self, complexity: torch.Tensor, temperature: Optional[float] = None,
                 return_continuous: bool = False) -> torch.Tensor:
         c = _normalize_complexity_shape(complexity)
-        return _run_mapper(c, abi.F_MAP_LINEAR, self.min_bits, self.max_bits, temperature, return_continuous)
+        if not c.is_cuda:
+            return self._forward_torch(c, temperature, return_continuous)
+
+        def kernel(cc):
+            return _run_mapper(cc, abi.F_MAP_LINEAR, self.min_bits, self.max_bits, temperature,
+                               return_continuous)
+        if _wants_grad((c,)):
+            return _kernel_value(kernel, lambda cc: self._forward_torch(cc, temperature, return_continuous),
+                                 [c], [])
+        return kernel(c)
 
 
 class ComplexityToBitMappingNetwork(nn.Module):
@@ -451,21 +540,15 @@ class ComplexityToBitMappingNetwork(nn.Module):
         """bit_allocation.py:199-216: z0 = [C, C^2, log1p C]."""
         return torch.cat([complexity, complexity ** 2, torch.log1p(complexity)], dim=-1)
 
-    def _forward_train(self, complexity, temperature, return_continuous):
-        """bit_allocation.py:218-280 in train mode (BatchNorm over the batch's
-        tiles, straight-through clamp and round) as torch autograd ops."""
-        _need_cuda(complexity, "complexity")
+    def _forward_torch(self, complexity, temperature, return_continuous):
+        """bit_allocation.py:247-280 as torch autograd ops: the CPU path, train
+        mode (BatchNorm over the batch's tiles) and the backward of the GPU
+        eval path."""
         c = _normalize_complexity_shape(complexity).clamp(0.0, 1.0)
         B, H, W = c.shape
         h = self.mapping_network(self.create_augmented_features(c.reshape(-1, 1)))
         bit_map = (self.min_bits + (self.max_bits - self.min_bits) * h).reshape(B, H, W)
-        if temperature is not None:
-            bit_map = bit_map * max(float(temperature), 0.1)
-        clamped = torch.clamp(bit_map, self.min_bits, self.max_bits)
-        bit_map = bit_map + (clamped - bit_map).detach()
-        if not return_continuous:
-            bit_map = bit_map + (torch.round(bit_map) - bit_map).detach()
-        return bit_map
+        return _finish_bits(bit_map, self.min_bits, self.max_bits, temperature, return_continuous)
 
     def mapper_blob(self):
         net = self.mapping_network
@@ -475,11 +558,17 @@ class ComplexityToBitMappingNetwork(nn.Module):
 
     def forward(self, complexity: torch.Tensor, temperature: Optional[float] = None,
                 return_continuous: bool = False) -> torch.Tensor:
-        if self.training:
-            return self._forward_train(complexity, temperature, return_continuous)
         c = _normalize_complexity_shape(complexity)
-        return _run_mapper(c, 0, self.min_bits, self.max_bits, temperature, return_continuous,
-                           mapper_blob=self.mapper_blob())
+        if self.training or not c.is_cuda:
+            return self._forward_torch(c, temperature, return_continuous)
+
+        def kernel(cc):
+            return _run_mapper(cc, 0, self.min_bits, self.max_bits, temperature, return_continuous,
+                               mapper_blob=self.mapper_blob())
+        if _wants_grad((c,), self.mapping_network.parameters()):
+            return _kernel_value(kernel, lambda cc: self._forward_torch(cc, temperature, return_continuous),
+                                 [c], list(self.mapping_network.parameters()))
+        return kernel(c)
 
 
 # ---------------------------------------------------------------------------
@@ -534,6 +623,11 @@ class LearnedSoftMask(nn.Module):
         return out
 
     def forward(self, bit_map: torch.Tensor, x: torch.Tensor, absmean: Optional[torch.Tensor] = None):
+        if not x.is_cuda:
+            # pure-PyTorch path: per-pixel channel mean of |x| (no grad to x)
+            if absmean is None:
+                absmean = x.detach().float().abs().mean(1)
+            return self._torch_forward(bit_map, absmean)
         if torch.is_grad_enabled() and (bit_map.requires_grad or any(p.requires_grad for p in self.net.parameters())):
             _need_cuda(x, "x")
             if absmean is None:
@@ -703,12 +797,41 @@ class SpatialAdaptiveQuantization(nn.Module):
             xmax = xmax.amax().expand(x.shape[1]).contiguous()
         return xmin, xmax
 
+    def _global_minmax(self, xmin, xmax):
+        """Batch-sharded data parallelism: min/max over the global batch with one
+        all-reduce (MAX over [-min, max]) when a process group is set."""
+        if self.process_group is None:
+            return xmin, xmax
+        import torch.distributed as dist
+        shape = xmin.shape
+        vec = torch.cat([-xmin.reshape(-1), xmax.reshape(-1)])
+        dist.all_reduce(vec, op=dist.ReduceOp.MAX, group=self.process_group)
+        n = xmin.numel()
+        return (-vec[:n]).reshape(shape).contiguous(), vec[n:].reshape(shape).contiguous()
+
+    def _batch_stats_torch(self, x):
+        """Per-channel (keepdim (1, C, 1, 1)) or per-tensor min/max of the batch
+        (quantization.py:330-338, 423-429)."""
+        if self.per_channel:
+            dims = [0] + list(range(2, x.dim()))
+            return x.amin(dim=dims, keepdim=True), x.amax(dim=dims, keepdim=True)
+        return x.min(), x.max()
+
+    @torch.no_grad()
+    def _update_running_stats_torch(self, x):
+        xmin, xmax = self._global_minmax(*self._batch_stats_torch(x.detach().float()))
+        self.running_min, self.running_max = fallback.ema_update(self.running_min, self.running_max, xmin,
+                                                                 xmax, self.momentum)
+        self.num_batches_tracked += 1
+
     @torch.no_grad()
     def update_running_stats(self, x: torch.Tensor, absmean: Optional[torch.Tensor] = None):
         """quantization.py:319-353: EMA(momentum) of the batch min/max (pass 1 +
         finalize + mcaq_ema_stats; absmean, if given, is filled by the same read)."""
         if self._frozen():
             return
+        if not x.is_cuda:
+            return self._update_running_stats_torch(x)
         _need_cuda(x, "x")
         xf = _f32c(x)
         xmin, xmax = _channel_minmax(xf, absmean)
@@ -779,9 +902,40 @@ class SpatialAdaptiveQuantization(nn.Module):
         m = self.soft_mask(bit_map, x, absmean=absmean) if want_m else None
         return _QATQuantFn.apply(x, bit_map, m, xmin, xmax)
 
+    def _minmax_for_quant(self, x):
+        """_calibrate_minmax (quantization.py:409-434): running statistics in
+        train mode or when frozen, else this batch's (all-reduced over the
+        process group, if any)."""
+        if self.running_min is not None and (self.training or self._frozen()):
+            return self.running_min.detach(), self.running_max.detach()
+        return self._global_minmax(*self._batch_stats_torch(x.detach().float()))
+
+    def _forward_torch(self, x, bit_map, training):
+        """The pure-PyTorch quantizer (quantization.py:604-634, 681-746) for CPU
+        tensors: one elementwise pass (fallback.quantize) at inference, the
+        fractional-bit straight-through quantizer in training."""
+        B, C, H, W = x.shape
+        if bit_map.dim() != 3 or bit_map.shape[0] != B:
+            raise AssertionError(f"Batch size mismatch: {B} vs {bit_map.shape[0]}")
+        if training:
+            self.update_running_stats(x)
+        xmin, xmax = self._minmax_for_quant(x)
+        xmin = xmin.reshape(-1).float().expand(C) if xmin.numel() == 1 else xmin.reshape(-1).float()
+        xmax = xmax.reshape(-1).float().expand(C) if xmax.numel() == 1 else xmax.reshape(-1).float()
+        if training:
+            xq = fallback.FractionalQuant.apply(x.float(), bit_map, xmin.contiguous(), xmax.contiguous())
+        else:
+            with torch.no_grad():
+                xq = fallback.quantize(x.detach().float(), bit_map.detach(), xmin, xmax).contiguous()
+        if self.smooth_transitions and self.soft_mask is not None:
+            xq = xq * self.soft_mask(bit_map, x)
+        return xq
+
     def forward(self, x: torch.Tensor, bit_map: torch.Tensor, training: Optional[bool] = None) -> torch.Tensor:
         if training is None:
             training = self.training
+        if not x.is_cuda:
+            return self._forward_torch(x, bit_map, training)
         if training:
             return self._forward_train(x, bit_map)
         _need_cuda(x, "x")

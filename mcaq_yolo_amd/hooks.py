@@ -13,7 +13,8 @@ Inference calls go through one `HookPlan` per feature shape: 3 launches
 analyzer -> mapper -> soft mask -> quantizer chain.  Calibration
 (`calibrating=True`) first folds the batch min/max into the quantizer's EMA
 statistics (quantization.py:319-353), then quantizes like inference.
-Train mode (QAT) runs the modules one by one with autograd (`_run_scale_train`).
+Train mode (QAT) and CPU tensors (the pure-PyTorch path) run the modules one
+by one with autograd (`_run_scale_modules`), exactly as the reference hook.
 """
 import torch
 import torch.nn as nn
@@ -106,10 +107,12 @@ class MCAQHooks(nn.Module):
             self._plans[key] = plan
         return plan
 
-    def _run_scale_train(self, layer_idx, feat, state):
-        """models/mcaq_yolo.py:409-455 in train mode (QAT, BASELINE config 5):
-        analyzer with autograd into complexity_mlp, continuous bits from the
-        train-mode mapper, fractional-bit STE quantizer (HIP forward/backward)."""
+    def _run_scale_modules(self, layer_idx, feat, state):
+        """models/mcaq_yolo.py:409-455 module by module: train mode (QAT,
+        BASELINE config 5: analyzer with autograd into complexity_mlp,
+        continuous bits from the train-mode mapper, fractional-bit STE
+        quantizer on the HIP kernels) and every CPU tensor (the pure-PyTorch
+        path, BASELINE config 1)."""
         complexity = self.complexity_analyzer(feat)
         if self.normalize_complexity:
             B = complexity.shape[0]
@@ -117,17 +120,18 @@ class MCAQHooks(nn.Module):
             lo = torch.quantile(flat, 0.02, dim=1, keepdim=True).unsqueeze(-1)
             hi = torch.quantile(flat, 0.98, dim=1, keepdim=True).unsqueeze(-1)
             complexity = ((complexity - lo) / (hi - lo + 1e-8)).clamp(0.0, 1.0)
-        bit_map = self.bit_mapper(complexity, state.get("temperature", 1.0), return_continuous=True)
+        bit_map = self.bit_mapper(complexity, state.get("temperature", 1.0), return_continuous=self.training)
         quantize = state.get("quantize", True)
         quantizer = self.quantizers[str(layer_idx)]
-        feat_q = quantizer(feat, bit_map, training=True) if quantize else feat
+        q_training = self.training or state.get("calibrating", False)
+        feat_q = quantizer(feat, bit_map, training=q_training) if quantize else feat
         state.setdefault("aux", []).append({"layer": layer_idx, "complexity": complexity,
                                             "bit_map": bit_map, "features_q": feat_q})
         return feat_q if quantize else None
 
     def run_scale(self, layer_idx, feat, state):
-        if self.training:
-            return self._run_scale_train(layer_idx, feat, state)
+        if self.training or not feat.is_cuda:
+            return self._run_scale_modules(layer_idx, feat, state)
         quantize = state.get("quantize", True)
         quantizer = self.quantizers[str(layer_idx)]
         x = feat.float().contiguous()
