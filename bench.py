@@ -1,32 +1,34 @@
 """Benchmark of the MCAQ spatial-adaptive-quantization hook path on MI355X.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5] [--pipeline D] [--no-cpu]
-                    [--e2e [--amp]]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2|3|4|5] [--pipeline D]
+                    [--no-cpu] [--no-e2e] [--e2e [--amp]] [--eager]
 
-(--config 5: the QAT training step of the hooks, `main_qat`; --e2e: the
-end-to-end image rate with the YOLOv8 network and NMS, `main_e2e`.)
-
-A step = the three backbone hooks (C3/C4/C5) of one batch: channel statistics,
-morphological complexity (phi1..5, MLP, bilateral), bit mapper, soft mask and
-the tile-wise 2..8-bit quant/dequant - every output the reference hook
-produces, computed by the HIP kernels on inputs already resident in HBM.  The
-YOLOv8 host network is not part of the step (not built yet: SURVEY 8f rank 1;
-ultralytics is unavailable) - `config.workload` says so.
+The headline (`metric`, `value`) is the HOOK PATH: a step = the three
+backbone hooks (C3/C4/C5) of one batch - channel statistics, morphological
+complexity (phi1..5, MLP, bilateral), bit mapper, soft mask and the tile-wise
+2..8-bit quant/dequant, every output the reference hook produces - computed
+by the HIP kernels on inputs already resident in HBM.  The end-to-end image
+rate (YOLOv8 network on MIOpen + hooks + HIP NMS, `run_e2e`) is measured in
+the same run and reported beside it under "e2e" (or alone with --e2e).
 
 Throughput: `--pipeline D` (default 3) independent batches are in flight on D
 HIP streams, so one batch's latency-bound per-image morphology overlaps the
-HBM passes of the next; `value` = images of all K timed steps / wall time.
-`config.latency_ms_single_batch` is one step with nothing beside it.
+HBM passes of the others; `value` = images of all K timed steps / wall time.
+`path_roofline` is the north-star figure (12 B per feature element over the
+step time); `roofline` is the dominant kernel, pass 2, timed with HIP events
+around each of its launches in the timed region.  `cpu_baseline` is this
+package's pure-PyTorch path (fallback.py) at the same config on the host.
 
 N > 1: one process per GPU (torch.distributed.run), each rank takes its own
 batch shard (weak scaling); the per-channel batch min/max is made global with
 one RCCL all-reduce per step, so every rank quantizes exactly like the
-reference run on the whole global batch.
+reference run on the whole global batch.  --config 5: the QAT training step.
 
 Prints ONE JSON line (rank 0).
 """
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -270,27 +272,49 @@ def main_qat(args, world, rank, dev, pg):
         dist.destroy_process_group()
 
 
+HOOK_METRIC = ("images/sec @640x640 MCAQ hook path (C3/C4/C5 complexity + bit mapper + 2-8 bit quant), "
+               "1/2/4/8 MI355X; % HBM roofline")
+E2E_METRIC = "images/sec @640x640 end-to-end MCAQ infer (YOLOv8 + hooks + NMS), 1/2/4/8 MI355X"
 E2E_CONF, E2E_IOU, E2E_MAX_DET = 0.25, 0.45, 1000    # Predictor defaults (inference.py:45-48)
+E2E_TARGET_CANDIDATES = 64       # anchors per image above conf after the class-bias shift (NMS does work)
 
 
-def main_e2e(args, world, rank, dev, pg):
-    """End-to-end MCAQ inference (BASELINE metric): YOLOv8
-    (MIOpen convolutions, seeded weights) with the MCAQ hooks at C3/C4/C5 on
-    the HIP kernels, Detect decode, batched HIP NMS; N > 1: each rank its
-    batch shard, hook min/max all-reduced, detections all-gathered over RCCL.
-    N = 1: the whole step is one HIP graph."""
+def _shift_class_bias(m, imgs, target=E2E_TARGET_CANDIDATES):
+    """Seeded random weights put every class score far below conf 0.25
+    (Detect.bias_init), so NMS would see no candidates.  Shift all class
+    biases by one constant so that about `target` anchors per image clear
+    the threshold: a detector-like workload, fixed by the seed."""
+    det = m.model.model[-1]
+    with torch.no_grad():
+        (y, _), _ = m(imgs, temperature=1.0, return_aux=True)
+        s = y[:, 4:].amax(dim=1).clamp(1e-7, 1 - 1e-7)             # (B, N) best class score
+        logit = torch.log(s) - torch.log1p(-s)
+        kth = logit.topk(min(target, logit.shape[1]), dim=1).values[:, -1]
+        thr = math.log(E2E_CONF / (1 - E2E_CONF))
+        delta = float(thr - kth.median()) + 1e-3
+        for seq in det.cv3:
+            seq[-1].bias.add_(delta)
+    return delta
+
+
+def run_e2e(cfg, steps, warmup, world, rank, dev, pg, amp=False, eager=False):
+    """End-to-end MCAQ inference: YOLOv8 (MIOpen
+    convolutions, seeded weights) with the MCAQ hooks at C3/C4/C5 on the HIP
+    kernels, Detect decode, batched HIP NMS; N > 1: each rank its batch shard,
+    hook min/max all-reduced, detections all-gathered over RCCL.  N = 1: the
+    whole step is one HIP graph.  Returns the measurement dict (rank 0)."""
     from mcaq_yolo_amd.postprocess import gather_detections, nms_padded
     from mcaq_yolo_amd.yolo import MCAQYOLO
-    name, B, chans, grid, mapper = CONFIGS[args.config]
+    name, B, chans, grid, mapper = CONFIGS[cfg]
     torch.manual_seed(0)
     m = MCAQYOLO(name, grid_size=grid, bit_mapping=mapper, device=dev)
     m.load_state_dict(hook_state_dict(dev), strict=False)
     m.eval()
     if pg is not None:
         m.process_group, m.batch_offset, m.batch_total = pg, rank * B, world * B
-    g = torch.Generator(device="cpu").manual_seed(1000 * args.config + rank)
+    g = torch.Generator(device="cpu").manual_seed(1000 * cfg + rank)
     imgs = torch.rand(B, 3, 640, 640, generator=g).to(dev)
-    amp = args.amp
+    delta = _shift_class_bias(m, imgs)
 
     def step(hooks=True):
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
@@ -326,12 +350,12 @@ def main_e2e(args, world, rank, dev, pg):
             side = torch.cuda.Stream()
             side.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(side):
-                for _ in range(max(args.warmup, 2)):
+                for _ in range(max(warmup, 2)):
                     step(hooks)
             torch.cuda.current_stream().wait_stream(side)
             torch.cuda.synchronize()
             fn = lambda h=hooks: step(h)
-            if pg is None and not args.eager:
+            if pg is None and not eager:
                 graph = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(graph):
                     res = step(hooks)
@@ -340,84 +364,91 @@ def main_e2e(args, world, rank, dev, pg):
             else:
                 res = step(hooks)
             torch.cuda.synchronize()
-            runs[hooks] = (timed(fn, args.steps), res)
+            runs[hooks] = (timed(fn, steps), res)
     step_s, (out, cnt) = runs[True]
     net_s = runs[False][0]
-    elems = sum(B * c * h * w for c, (h, w) in zip(chans, SIZES))
+    return {
+        "metric": E2E_METRIC, "value": round(world * B / step_s, 2), "unit": "images/s", "n_gpus": world,
+        "steps": steps, "warmup": warmup, "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16-net/f32-hooks" if amp else "f32",
+        "data": "synthetic torch.rand images 640x640, seeded YOLOv8 + MCAQ weights, class biases shifted "
+                "by %.3f so ~%d anchors/image clear conf %.2f" % (delta, E2E_TARGET_CANDIDATES, E2E_CONF),
+        "config": {"workload": "%s bs%d/GPU 640x640 end-to-end: YOLOv8 (MIOpen) + MCAQ hooks C3/C4/C5 (HIP) + "
+                               "Detect decode + HIP NMS (conf %.2f, IoU %.2f, max_det %d)%s"
+                               % (name, B, E2E_CONF, E2E_IOU, E2E_MAX_DET,
+                                  " + RCCL detection all-gather" if pg is not None else ""),
+                   "global_batch": world * B, "grid_size": grid, "mapper": mapper,
+                   "parallelism": "dp%d" % world, "hip_graph": pg is None and not eager,
+                   "network_only_ms_per_step": round(net_s * 1e3, 4),
+                   "mcaq_hooks_and_nms_ms_per_step": round((step_s - net_s) * 1e3, 4),
+                   "detections_per_image": round(float(cnt.float().mean()), 2)},
+    }
+
+
+def main_e2e(args, world, rank, dev, pg):
+    out = run_e2e(args.config, args.steps, args.warmup, world, rank, dev, pg, args.amp, args.eager)
     if rank == 0:
-        achieved = 12 * elems / step_s / 1e9
-        out_j = {
-            "metric": "images/sec @640x640 end-to-end MCAQ infer, 1/2/4/8 MI355X; % HBM roofline",
-            "value": round(world * B / step_s, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "bf16-net/f32-hooks" if amp else "f32",
-            "data": "synthetic torch.rand images 640x640, seeded YOLOv8 + MCAQ weights",
-            "config": {"workload": "%s bs%d/GPU 640x640 end-to-end: YOLOv8 (MIOpen) + MCAQ hooks C3/C4/C5 (HIP) + "
-                                   "Detect decode + HIP NMS (conf %.2f, IoU %.2f, max_det %d)%s"
-                                   % (name, B, E2E_CONF, E2E_IOU, E2E_MAX_DET,
-                                      " + RCCL detection all-gather" if pg is not None else ""),
-                       "global_batch": world * B, "grid_size": grid, "mapper": mapper,
-                       "parallelism": "dp%d" % world, "hip_graph": pg is None and not args.eager,
-                       "network_only_ms_per_step": round(net_s * 1e3, 4),
-                       "mcaq_hooks_ms_per_step": round((step_s - net_s) * 1e3, 4),
-                       "detections_per_image": round(float(cnt.float().mean()), 2)},
-            "step_roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                              "frac": round(achieved / HBM_PEAK_GBS, 4),
-                              "kernel": "MCAQ hook bytes (12 B per C3/C4/C5 element) over the whole e2e step"},
-        }
-        print(json.dumps(out_j), flush=True)
+        print(json.dumps(out), flush=True)
     if pg is not None:
         import torch.distributed as dist
         dist.destroy_process_group()
 
 
-def cpu_baseline(cfg_id, budget_s=12.0):
-    """Oracle (numpy port of the reference path) on the host: one image per
-    hook scale per iteration, repeated for ~budget_s seconds -> images/s."""
-    import numpy as np
-    from oracle import mcaq_oracle as O
+def cpu_baseline(cfg_id, budget_s=10.0):
+    """This package's pure-PyTorch path (fallback.py through MCAQHooks on CPU
+    tensors - the reference's own algorithm and op order, bit-exact against
+    its fixtures) at the config's full batch and shapes, on the host's
+    threads: whole batches of the three hooks until ~budget_s -> images/s."""
+    from mcaq_yolo_amd.hooks import MCAQHooks
     name, B, chans, grid, mapper = CONFIGS[cfg_id]
-    w = O.load_weights(os.path.join(ROOT, "tests", "golden", "weights.npz"))
-    xs = [synth_features(1, c, h, wd, 1000 * cfg_id + i, "cpu").numpy() for i, (c, (h, wd)) in
+    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    h = MCAQHooks(grid_size=grid, bit_mapping=mapper, device="cpu")
+    h.load_state_dict(hook_state_dict("cpu"), strict=False)
+    h.eval()
+    xs = [synth_features(B, c, hh, ww, 1000 * cfg_id + i, "cpu") for i, (c, (hh, ww)) in
           enumerate(zip(chans, SIZES))]
-    t0 = time.perf_counter()
-    n = 0
-    while True:
-        for x in xs:
-            O.hook_forward(x, w, grid, mapper=mapper)
-        n += 1
-        if time.perf_counter() - t0 > budget_s:
-            break
+    with torch.no_grad():
+        h.forward_features(xs)                # first-call allocations out of the timing
+        t0 = time.perf_counter()
+        n = 0
+        while True:
+            h.forward_features(xs)
+            n += 1
+            if time.perf_counter() - t0 > budget_s:
+                break
     dt = time.perf_counter() - t0
-    return {"value": round(n / dt, 4), "unit": "images/s", "cores": 1, "kind": "port",
-            "sample": "%d images x 3 hook scales (%s %s, batch 1) through oracle/mcaq_oracle.py, "
-                      "single-threaded numpy, %.1f s" % (n, name, "x".join(map(str, chans)), dt)}
+    return {"value": round(n * B / dt, 3), "unit": "images/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": "%d batches x %d images x 3 hook scales (%s %s, grid %d, %s mapper) through the package's "
+                      "pure-PyTorch path (mcaq_yolo_amd/fallback.py), fp32, %d threads, %.1f s"
+                      % (n, B, name, "x".join(map(str, chans)), grid, mapper, torch.get_num_threads(), dt)}
 
 
 class Runner:
     """Issues hook-path steps.  `depth` independent HookPlans (own buffers) on
     `depth` HIP streams: step i runs on plan/stream i % depth, so the per-image
-    morphology of one batch (latency-bound, ~1/3 of the CUs) overlaps the HBM
-    passes of the next.  Each step is one HIP-graph replay (N = 1) or two
-    graph replays around the RCCL min/max all-reduce (N > 1)."""
+    morphology of one batch (latency-bound) overlaps the HBM passes of the
+    others.  A step is two HIP-graph replays, [pass 1 + morphology] and
+    [pass 2] (with the RCCL min/max all-reduce between them when N > 1), with
+    timing events recorded on the step's stream before, between and after:
+    every pass-2 launch of the run is timed where it runs (`quant_us`)."""
 
     def __init__(self, plans, pg, use_graph):
         self.plans, self.pg = plans, pg
         self.streams = [torch.cuda.Stream() for _ in plans]
         self.graphs = [None] * len(plans)
         self.i = 0
+        self.marks = []          # (e_start, e_pre_done, e_quant_done) per step
         if use_graph:
             torch.cuda.synchronize()
             for p, (plan, st) in enumerate(zip(plans, self.streams)):
                 with torch.cuda.stream(st):
                     for _ in range(2):          # warm the launchers outside capture
-                        self._eager(plan, st)
+                        plan.launch(st, self.pg)
                 st.synchronize()
                 gs = []
-                segs = [lambda pl=plan: pl.launch(torch.cuda.current_stream())] if pg is None else \
-                    [lambda pl=plan: pl.launch_pre(torch.cuda.current_stream()),
-                     lambda pl=plan: pl.launch_quant(torch.cuda.current_stream())]
-                for seg in segs:
+                for seg in (lambda pl=plan: pl.launch_pre(torch.cuda.current_stream()),
+                            lambda pl=plan: pl.launch_quant(torch.cuda.current_stream())):
                     g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g, stream=st):
                         seg()
@@ -425,81 +456,34 @@ class Runner:
                 self.graphs[p] = gs
             torch.cuda.synchronize()
 
-    def _eager(self, plan, st):
-        plan.launch(st, self.pg)
-
     def step(self):
         p = self.i % len(self.plans)
         self.i += 1
         plan, st, gs = self.plans[p], self.streams[p], self.graphs[p]
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
         with torch.cuda.stream(st):
+            ev[0].record(st)
             if gs is None:
-                plan.launch(st, self.pg)
-            elif self.pg is None:
-                gs[0].replay()
+                plan.launch_pre(st)
             else:
                 gs[0].replay()
+            if self.pg is not None:
                 sync_channel_minmax(plan.bufs, self.pg)
+            ev[1].record(st)
+            if gs is None:
+                plan.launch_quant(st)
+            else:
                 gs[1].replay()
+            ev[2].record(st)
+        self.marks.append(ev)
 
     def sync(self):
         for st in self.streams:
             torch.cuda.current_stream().wait_stream(st)
 
-
-class SplitRunner:
-    """Software-pipelined schedule on three HIP streams: stream S runs the two
-    HBM passes back to back (pass 1 of batch i, then pass 2 of batch i - LAG);
-    streams M0 / M1 run the latency-bound morphology of alternate batches, each
-    starting when its batch's pass 1 has finished; pass 2 of a batch waits for
-    its morphology (event edges).  With LAG steps of HBM work in front of it,
-    a batch's morphology chain is hidden behind the other batches' streaming
-    passes.  Eager launches (each step is 4 kernels and 3 event edges)."""
-    LAG = 2
-
-    def __init__(self, plans, pg):
-        if len(plans) < self.LAG + 1:
-            raise ValueError("--schedule split needs --pipeline >= %d" % (self.LAG + 1))
-        self.plans, self.pg = plans, pg
-        # the latency-bound morphology gets the high-priority queues
-        prio = int(os.environ.get("MCAQ_MORPH_PRIO", "-1"))
-        self.S = torch.cuda.Stream()
-        self.M = [torch.cuda.Stream(priority=prio), torch.cuda.Stream(priority=prio)]
-        self.ev_st = [torch.cuda.Event() for _ in plans]
-        self.ev_mo = [torch.cuda.Event() for _ in plans]
-        self.i = 0       # batches started
-        self.done = 0    # batches whose pass 2 is enqueued
-
-    def _quant(self, j):
-        p = j % len(self.plans)
-        plan = self.plans[p]
-        self.S.wait_event(self.ev_mo[p])
-        if self.pg is not None:
-            with torch.cuda.stream(self.S):
-                sync_channel_minmax(plan.bufs, self.pg)
-        plan.launch_quant(self.S)
-        self.done = j + 1
-
-    def step(self):
-        i = self.i
-        p = i % len(self.plans)
-        plan = self.plans[p]
-        plan.launch_stats(self.S)
-        self.ev_st[p].record(self.S)
-        m = self.M[i % 2]
-        m.wait_event(self.ev_st[p])
-        plan.launch_morph(m)
-        self.ev_mo[p].record(m)
-        self.i = i + 1
-        if i >= self.LAG:
-            self._quant(i - self.LAG)
-
-    def sync(self):
-        while self.done < self.i:
-            self._quant(self.done)
-        cur = torch.cuda.current_stream()
-        for st in [self.S] + self.M:
-            cur.wait_stream(st)
+    def quant_us(self, first=0):
+        """Per-step pass-2 durations (us) of steps first.. (call after a sync)."""
+        return [e[1].elapsed_time(e[2]) * 1e3 for e in self.marks[first:]]
 
 
 def main():
@@ -510,13 +494,11 @@ def main():
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS) + [5],
                     help="2/3/4: inference hook path; 5: QAT hook training step")
     ap.add_argument("--pipeline", type=int, default=3, help="batches in flight (independent plans/streams)")
-    ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--e2e", action="store_true", help="end-to-end: YOLOv8 network + hooks + NMS (main_e2e)")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (YOLOv8 + hooks + NMS) leg")
+    ap.add_argument("--e2e", action="store_true", help="only the end-to-end line (run_e2e)")
     ap.add_argument("--amp", action="store_true", help="--e2e: network under bf16 autocast (hooks stay fp32)")
-    ap.add_argument("--eager", action="store_true", help="no HIP graph (--schedule streams)")
-    ap.add_argument("--schedule", choices=("split", "streams"), default="streams",
-                    help="split: HBM passes on one stream, morphology on two (SplitRunner); "
-                         "streams: D independent per-batch streams, one HIP graph per step")
+    ap.add_argument("--eager", action="store_true", help="no HIP graphs")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -548,7 +530,7 @@ def main():
     depth = max(1, args.pipeline)
     cm, mm, sm = load_blobs(dev)
     geoms = [ScaleGeom(B, c, h, w, grid) for c, (h, w) in zip(chans, SIZES)]
-    plans, feats_all = [], []
+    plans = []
     for p in range(depth):
         # each batch in flight has its own synthetic input (seeded per rank and slot)
         feats = [synth_features(B, c, h, w, 1000 * args.config + i + 7919 * rank + 104729 * p, dev)
@@ -556,19 +538,20 @@ def main():
         plan = HookPlan(geoms, dev)
         plan.prepare(feats, cm, mm, [sm, sm, sm], temperature=1.0, mapper_kind=mapper,
                      batch_offset=rank * B, batch_total=world * B)
+        plan.feats = feats
         plans.append(plan)
-        feats_all.append(feats)
     torch.cuda.synchronize()
 
-    use_graph = not args.eager and args.schedule == "streams"
-    runner = Runner(plans, pg, use_graph) if args.schedule == "streams" else SplitRunner(plans, pg)
+    use_graph = not args.eager
+    runner = Runner(plans, pg, use_graph)
     for _ in range(max(args.warmup, 1)):
         runner.step()
     runner.sync()
     torch.cuda.synchronize()
 
-    # per-kernel device time: each kernel launched `reps` times back to back
-    # between two HIP events on the launch stream (one plan, no overlap)
+    # pass 1 and the morphology launch alone (informational; pass 2 is timed
+    # inside the steps): each launched `reps` times back to back between two
+    # HIP events on the launch stream
     plan = plans[0]
     L = plan.lib
     stream = torch.cuda.current_stream()
@@ -576,8 +559,7 @@ def main():
     sh = abi.ctypes.c_void_p(stream.cuda_stream)
     nf = plan._n if plan._fz is not None else 0
     launch = {"stats": lambda: L.mcaq_stats(plan._st, plan._n, sh),
-              "morph_finalize": lambda: L.mcaq_morph_finalize(plan._mo, plan._n, plan._fz, nf, sh),
-              "quant": lambda: L.mcaq_quant(plan._qs, plan._n, sh)}
+              "morph_finalize": lambda: L.mcaq_morph_finalize(plan._mo, plan._n, plan._fz, nf, sh)}
     kt = {}
     reps = 20
     e0 = torch.cuda.Event(enable_timing=True)
@@ -603,6 +585,7 @@ def main():
     latency_ms = sorted(lat)[len(lat) // 2] * 1e3
 
     # ---- timed region: K steps, `depth` batches in flight
+    first_timed = len(runner.marks)
     if pg is not None:
         import torch.distributed as dist
         dist.barrier()
@@ -621,29 +604,37 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.barrier()
         step_s = float(t.item())
+    q_all = runner.quant_us()
+    q_timed = q_all[first_timed:]
+    quant_us = sum(q_timed) / len(q_timed)
 
     elems = sum(B * c * h * w for c, (h, w) in zip(chans, SIZES))
     alg_bytes = 12 * elems                       # 2 reads of x + 1 write of y, fp32
-    # HBM-side bytes per step from the rocprofv3 PMC passes of tools/pmc_traffic.sh
+    # HBM-side bytes per launch from the rocprofv3 PMC passes of tools/pmc_traffic.sh
     # (FETCH_SIZE and WRITE_SIZE in separate runs, FETCH doubled per the gfx950
     # calibration), committed per config under profiles/
     traffic, traffic_k = None, {}
-    tpath = os.path.join(ROOT, "profiles", "r01_pmc_traffic_config%d.json" % args.config)
+    tpath = os.path.join(ROOT, "profiles", "pmc_traffic_config%d.json" % args.config)
     if os.path.exists(tpath):
         tj = json.load(open(tpath))
         traffic = tj.get("step_total")
         traffic_k = {k: v["total"] for k, v in tj.get("kernels", {}).items()}
     achieved = alg_bytes / step_s / 1e9
     value = world * B / step_s
+    out = None
     if rank == 0:
-        kern = {}
-        for k, nbytes in (("stats", 4 * elems), ("quant", 8 * elems)):
-            gbs = nbytes / (kt[k] * 1e-6) / 1e9
-            kern[k] = {"us": round(kt[k], 2), "alg_bytes": nbytes, "GB/s": round(gbs, 1),
-                       "frac": round(gbs / HBM_PEAK_GBS, 4)}
-        kern["morph_finalize"] = {"us": round(kt["morph_finalize"], 2), "bound": "latency (per-image chain)"}
+        q_gbs = 8 * elems / (quant_us * 1e-6) / 1e9
+        kern = {"quant": {"us": round(quant_us, 2), "alg_bytes": 8 * elems, "GB/s": round(q_gbs, 1),
+                          "frac": round(q_gbs / HBM_PEAK_GBS, 4),
+                          "timing": "HIP events around every pass-2 launch of the timed region (%d launches, "
+                                    "%d batches in flight)" % (len(q_timed), depth)}}
+        gbs = 4 * elems / (kt["stats"] * 1e-6) / 1e9
+        kern["stats"] = {"us": round(kt["stats"], 2), "alg_bytes": 4 * elems, "GB/s": round(gbs, 1),
+                         "frac": round(gbs / HBM_PEAK_GBS, 4), "timing": "isolated, %d back-to-back launches" % reps}
+        kern["morph_finalize"] = {"us": round(kt["morph_finalize"], 2), "bound": "latency (per-image chain)",
+                                  "timing": "isolated, %d back-to-back launches" % reps}
         out = {
-            "metric": "images/sec @640x640 end-to-end MCAQ infer, 1/2/4/8 MI355X; % HBM roofline",
+            "metric": HOOK_METRIC,
             "value": round(value, 2),
             "unit": "images/s",
             "n_gpus": world,
@@ -655,26 +646,44 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic silu(1.5*randn+2*up(randn)) C3/C4/C5 features, seeded weights",
-            "config": {"workload": "%s bs%d/GPU 640x640 MCAQ hook path C3/C4/C5 (grid %d, %s mapper); "
-                                   "YOLOv8 network excluded" % (name, B, grid, mapper),
+            "config": {"workload": "%s bs%d/GPU 640x640 MCAQ hook path C3/C4/C5 (grid %d, %s mapper): channel "
+                                   "stats, phi1..5, complexity MLP, bilateral, bit mapper, soft mask, 2-8 bit "
+                                   "quant/dequant; YOLOv8 network excluded (see e2e)" % (name, B, grid, mapper),
                        "global_batch": world * B, "grid_size": grid, "mapper": mapper,
                        "parallelism": "dp%d" % world, "hip_graph": use_graph,
-                       "batches_in_flight": depth, "schedule": args.schedule, "latency_ms_single_batch": round(latency_ms, 4),
+                       "batches_in_flight": depth, "latency_ms_single_batch": round(latency_ms, 4),
                        "host_enqueue_us_per_step": round(t_enq / args.steps * 1e6, 1)},
-            # the dominant HBM kernel (pass 2): algorithmic bytes per launch over its
-            # HIP-event launch time; the whole step's figure is `step_roofline`
-            "roofline": {"bound": "hbm", "achieved": kern["quant"]["GB/s"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": kern["quant"]["frac"], "traffic": traffic_k.get("mcaq_quant_kernel"),
-                         "kernel": "mcaq_quant_kernel (pass 2: read x + write y, 8 B per feature element)",
-                         "alg_bytes_per_launch": 8 * elems, "us_per_launch": kern["quant"]["us"]},
-            "step_roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                              "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            # north star: the whole fused complexity + quant path,
+            # 12 B per feature element over the wall time of a step
+            "path_roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": round(achieved / HBM_PEAK_GBS, 4), "target_frac": 0.70, "traffic": traffic,
                               "kernel": "whole step: mcaq_stats + mcaq_morph_kernel + mcaq_tiles_kernel + "
                                         "mcaq_quant, 12 B per feature element per step",
                               "alg_bytes_per_step": alg_bytes},
+            # the dominant kernel (pass 2): algorithmic bytes per launch over its
+            # launch time, HIP events on its stream inside the timed region
+            "roofline": {"bound": "hbm", "achieved": kern["quant"]["GB/s"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": kern["quant"]["frac"], "traffic": traffic_k.get("mcaq_quant_kernel"),
+                         "kernel": "mcaq_quant_kernel (pass 2: read x + write y, 8 B per feature element)",
+                         "alg_bytes_per_launch": 8 * elems, "us_per_launch": kern["quant"]["us"],
+                         "us_per_launch_all_dispatches": round(sum(q_all) / len(q_all), 2),
+                         "dispatches": len(q_all)},
             "kernels": kern,
             "cpu_baseline": None,
         }
+    if not args.no_e2e and world == 1:
+        for p_ in plans:
+            p_.feats = None
+        del runner
+        try:
+            e2e = run_e2e(args.config, 20, 3, world, rank, dev, pg)
+            e2e.pop("metric", None)
+            if out is not None:
+                out["e2e"] = e2e
+        except Exception as exc:          # the hook-path line must still print
+            if out is not None:
+                out["e2e"] = {"error": repr(exc)[:300]}
+    if rank == 0:
         if not args.no_cpu and world == 1:
             out["cpu_baseline"] = cpu_baseline(args.config)
         print(json.dumps(out), flush=True)

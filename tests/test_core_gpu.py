@@ -51,6 +51,7 @@ def test_analyzer_forward_range():
     from mcaq_yolo_amd.core import MorphologicalComplexityAnalyzer
     a = MorphologicalComplexityAnalyzer(device=DEV).eval()
     c = a(torch.rand(2, 16, 80, 80, device=DEV))
+    c = c.detach()
     assert c.dim() == 3 and 0.0 <= float(c.min()) and float(c.max()) <= 1.0
 
 
@@ -172,12 +173,12 @@ def test_modules_vs_oracle(mods, name):
         assert np.array_equal(phi.cpu().numpy(), ref_phi)
         C = a(xt)
         refC, _, _ = O.analyzer_forward(x, W, grid)
-        assert np.array_equal(C.cpu().numpy(), refC)
+        assert np.array_equal(C.detach().cpu().numpy(), refC)
         bits = m(C, temperature=1.0)
-        assert np.array_equal(bits.cpu().numpy(), O.mlp_mapper(refC, W, 1.0))
+        assert np.array_equal(bits.detach().cpu().numpy(), O.mlp_mapper(refC, W, 1.0))
         y = q(xt, bits)
         ref = O.hook_forward(x, W, grid)
-        assert np.array_equal(y.cpu().numpy(), ref["y"])
+        assert np.array_equal(y.detach().cpu().numpy(), ref["y"])
     finally:
         a.grid_size = 8
 
@@ -240,3 +241,70 @@ def test_hooks_on_a_module_chain():
     assert torch.equal(layers(x), x)            # quantize=False: aux only
     h.end()
     h.remove()
+
+
+# ---- eval mode with autograd: kernel values, reference gradients ------------
+def test_eval_modules_keep_reference_gradients(mods):
+    """bit_allocation.py:42-80 / 218-280 and morphology.py:939-973 stay
+    differentiable in eval mode.  The GPU value is the kernel's (identical to
+    the no_grad call; the CPU pure-PyTorch path agrees within the MLP's
+    LayerNorm / GEMV ulps, 1e-6); the gradient equals the CPU path's gradient
+    (torch recomputation, GEMM ulps: rtol 1e-4)."""
+    from mcaq_yolo_amd import core
+    a, m, _ = mods
+    x = torch.from_numpy(load_case("p3_c16")["x"].astype(f32))
+    a_cpu = core.MorphologicalComplexityAnalyzer(device="cpu")
+    a_cpu.load_state_dict(_sd("complexity_analyzer."))
+    m_cpu = core.ComplexityToBitMappingNetwork()
+    m_cpu.load_state_dict(_sd("bit_mapper."))
+    lin = core.LinearBitMapper()
+    a_cpu.eval(), m_cpu.eval()
+    for mod in (a, m, a_cpu, m_cpu):
+        mod.zero_grad(set_to_none=True)
+    c_gpu = a(x.to(DEV))
+    c_cpu = a_cpu(x)
+    assert c_gpu.requires_grad
+    np.testing.assert_allclose(c_gpu.detach().cpu().numpy(), c_cpu.detach().numpy(), rtol=1e-6, atol=1e-7)
+    with torch.no_grad():
+        assert torch.equal(a(x.to(DEV)), c_gpu.detach())
+    cg = c_gpu.detach().clone().requires_grad_(True)
+    cc = c_gpu.detach().cpu().clone().requires_grad_(True)
+    for mg, mc in ((m, m_cpu), (lin, lin)):
+        bg = mg(cg, 1.0, return_continuous=True)
+        bc = mc(cc, 1.0, return_continuous=True)
+        np.testing.assert_allclose(bg.detach().cpu().numpy(), bc.detach().numpy(), rtol=1e-6, atol=1e-6)
+        w = torch.linspace(-1, 1, bg.numel()).view_as(bc)
+        (bg * w.to(DEV)).sum().backward()
+        (bc * w).sum().backward()
+        np.testing.assert_allclose(cg.grad.cpu().numpy(), cc.grad.numpy(), rtol=1e-4, atol=1e-6)
+        cg.grad = cc.grad = None
+    for (n, pg), (_, pc) in zip(m.mapping_network.named_parameters(), m_cpu.mapping_network.named_parameters()):
+        np.testing.assert_allclose(pg.grad.cpu().numpy(), pc.grad.numpy(), rtol=1e-4, atol=1e-6, err_msg=n)
+    (c_gpu * torch.linspace(0, 1, c_gpu.numel(), device=DEV).view_as(c_gpu)).sum().backward()
+    (c_cpu * torch.linspace(0, 1, c_cpu.numel()).view_as(c_cpu)).sum().backward()
+    for (n, pg), (_, pc) in zip(a.complexity_mlp.named_parameters(), a_cpu.complexity_mlp.named_parameters()):
+        np.testing.assert_allclose(pg.grad.cpu().numpy(), pc.grad.numpy(), rtol=1e-4, atol=1e-6, err_msg=n)
+    for mod in (a, m):
+        mod.zero_grad(set_to_none=True)
+
+
+@pytest.mark.parametrize("name", ["p3_c16", "odd_c20", "g16_c16"])
+def test_gpu_equals_cpu_torch_path(mods, name):
+    """The HIP path and the package's pure-PyTorch path give the same bits
+    and y on the same inputs (C within the MLP's LayerNorm / GEMV ulps)."""
+    from mcaq_yolo_amd.hooks import MCAQHooks
+    d = load_case(name)
+    grid = int(d["grid"])
+    x = torch.from_numpy(d["x"].astype(f32))
+    res = {}
+    for dev in ("cpu", DEV):
+        h = MCAQHooks(grid_size=grid, device=dev, indices=(4,))
+        sd = {k: v for k, v in _sd("").items() if k.startswith(("complexity_analyzer.", "bit_mapper."))}
+        sd.update({"quantizers.4." + k: v for k, v in _sd("").items() if k.startswith("soft_mask.")})
+        h.load_state_dict(sd, strict=False)
+        h.to(dev).eval()
+        with torch.no_grad():
+            outs, aux = h.forward_features([x.to(dev)])
+        res[dev] = (outs[0].cpu(), aux[0]["bit_map"].cpu(), aux[0]["complexity"].cpu())
+    assert torch.equal(res["cpu"][0], res[DEV][0]) and torch.equal(res["cpu"][1], res[DEV][1])
+    np.testing.assert_allclose(res["cpu"][2].numpy(), res[DEV][2].numpy(), rtol=1e-6, atol=1e-7)
