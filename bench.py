@@ -134,8 +134,9 @@ def main_qat(args, world, rank, dev, pg):
     h.load_state_dict(hook_state_dict(dev), strict=False)
     h.train()
     if pg is not None:
-        for q in h.quantizers.values():
-            q.process_group = pg
+        # global-batch EMA statistics and mapper BatchNorm
+        from mcaq_yolo_amd.dist import shard_hooks
+        shard_hooks(h, pg, rank, world, B)
     feats = [synth_features(B, c, hh, ww, 5000 + i + 7919 * rank, dev).requires_grad_(True)
              for i, (c, (hh, ww)) in enumerate(zip(chans, SIZES))]
     gen = torch.Generator(device="cpu").manual_seed(77 + rank)
@@ -152,15 +153,8 @@ def main_qat(args, world, rank, dev, pg):
         lbit = (MCAQHooks.avg_bits(aux) - target_bits) ** 2
         torch.autograd.backward(list(outs) + [0.1 * lbit], list(G) + [torch.ones((), device=dev)])
         if pg is not None:
-            import torch.distributed as dist
-            flat = torch.cat([p.grad.reshape(-1) for p in params_])
-            dist.all_reduce(flat, group=pg)
-            flat /= world
-            o = 0
-            for p in params_:
-                n = p.numel()
-                p.grad.copy_(flat[o:o + n].view_as(p))
-                o += n
+            from mcaq_yolo_amd.dist import allreduce_gradients
+            allreduce_gradients(params_, pg)           # one flat bucket over RCCL
         torch.nn.utils.clip_grad_norm_(params_, max_norm=1.0)
         opt.step()
         h.bit_mapper.enforce_weight_constraints()

@@ -135,10 +135,15 @@ class _BlobCache:
 
     def get(self, tensors, pack):
         key = tuple((t.data_ptr(), t._version, t.device) for t in tensors)
-        if key != self.key:
+        # under HIP-graph capture the pack is always recorded, so every replay
+        # rebuilds the blob from the live parameters (an optimizer step inside
+        # the captured step changes them in place); the captured blob holds
+        # data only after a replay, so the next eager call packs afresh
+        capturing = any(t.is_cuda for t in tensors) and torch.cuda.is_current_stream_capturing()
+        if capturing or key != self.key:
             with torch.no_grad():
                 self.blob = pack().contiguous()
-            self.key = key
+            self.key = None if capturing else key
         return self.blob
 
 

@@ -497,7 +497,7 @@ struct QuantArgs {
 constexpr int QSLICE = 32;     // channels per unit (8 per wave)
 constexpr int QCW = 8;         // channels per wave
 constexpr int QMAXBITS = 15;   // max entries per channel in the LDS table
-constexpr int QMAXNT = 1024;   // max tiles per image for on-the-fly m(p)
+constexpr int QMAXNT = 1024;   // max tiles per image whose m values are staged in LDS (more: read from L2)
 
 // unit = 256 pixels x 32 channels of one image; lane l of every wave owns
 // pixels 4l..4l+3 (16-byte accesses), wave w channels 8w..8w+7 of the slice,
@@ -505,7 +505,7 @@ constexpr int QMAXNT = 1024;   // max tiles per image for on-the-fly m(p)
 // soft-mask value are fetched once; per-(channel, bits) scale / zero-point
 // come from an LDS table built by the workgroup (IEEE divisions, as
 // QuantizationParameters computes them).
-template <bool kVec, bool kNTL, bool kNTS>
+template <bool kVec, bool kNTL, bool kNTS, bool kMtLds>
 __global__ __launch_bounds__(256) void mcaq_quant_kernel(QuantArgs a) {
   __shared__ float2 qt[QSLICE * QMAXBITS];
   __shared__ float mts[QMAXNT];
@@ -531,8 +531,10 @@ __global__ __launch_bounds__(256) void mcaq_quant_kernel(QuantArgs a) {
     qt[i] = make_float2(q.scale, q.zp);
   }
   const int NTq = S.ht * S.wt;
-  if (S.mt)
+  if (kMtLds && S.mt)
     for (int i = tid; i < NTq; i += 256) mts[i] = S.mt[(size_t)b * NTq + i];
+  // tile grids with more than QMAXNT tiles read their m values through L2
+  const float* mtab = kMtLds ? mts : (S.mt ? S.mt + (size_t)b * NTq : nullptr);
 
   const int q0 = chunk * 256 + lane * 4;
   bool pv[4];
@@ -602,7 +604,7 @@ __global__ __launch_bounds__(256) void mcaq_quant_kernel(QuantArgs a) {
       for (int i = 0; i < 5; ++i) {
         const int rb = nearest_src(imin_(imax_(h + i - 2, 0), S.H - 1), S.ht, S.H) * S.wt;
 #pragma unroll
-        for (int j = 0; j < 5; ++j) acc = fmaf(bits_as_float(k_smooth5_bits[i * 5 + j]), mts[rb + cs[j]], acc);
+        for (int j = 0; j < 5; ++j) acc = fmaf(bits_as_float(k_smooth5_bits[i * 5 + j]), mtab[rb + cs[j]], acc);
       }
       mq[lane * 4 + wv] = acc;
     }
@@ -661,14 +663,7 @@ int mcaq_launch_spatial_quantization(const float* input, const float* bit_map, c
   return mcaq_quant(&q, 1, stream);
 }
 
-// EXPERIMENT knob: MCAQ_XSKIP bit 0 = skip morph/tiles, bit 1 = skip stats/quant
-static int xskip() {
-  static int v = -1;
-  if (v < 0) { const char* e = getenv("MCAQ_XSKIP"); v = e ? atoi(e) : 0; }
-  return v;
-}
 int mcaq_stats(const mcaq_stats_scale* scales, int nscales, hipStream_t stream) {
-  if (xskip() & 2) return 0;
   if (nscales < 1 || nscales > 3) return (int)hipErrorInvalidValue;
   StatsArgs a;
   int units = 0;
@@ -755,12 +750,9 @@ static int morph_plan(const MorphScale* s, int n, int* lds_mode, int* plane_stri
 
 // images per pass A workgroup: the most (power of two, <= 16) whose planes fit
 // the LDS budget while each image keeps >= 64 threads and <= 4 pixels per thread
-static int morph_ppt() {   // max pixels per thread of a packed image (experiment knob MCAQ_PPT)
-  static int v = -1;
-  if (v < 0) { const char* e = getenv("MCAQ_PPT"); v = e ? atoi(e) : 4; if (v < 1) v = 4; }
-  return v;
-}
-#define MCAQ_PPT morph_ppt()
+#ifndef MCAQ_PPT
+#define MCAQ_PPT 4   // max pixels per thread of a packed image (build-time experiment define)
+#endif
 static int morph_ipw(const MorphScale& S, int mode, int limit) {
   if (!mode) return 1;   // planes in global scratch: one image per workgroup
   const int per = ((plane_bytes(S.Hc, S.Wc) + 15) & ~15) + fixed_bytes();
@@ -810,7 +802,6 @@ int mcaq_morph_finalize(const mcaq_morph_scale* scales, int nscales, const mcaq_
     any_tiles |= tf != 0;
   }
   a.nscales = nscales;
-  if (xskip() & 1) { any_phi = 0; any_tiles = 0; }
   if (!any_phi && fa.nblocks > 0) {   // nothing to ride along with
     hipLaunchKernelGGL(mcaq_finalize_kernel, dim3(fa.nblocks), dim3(256), 0, stream, fa);
     const hipError_t fe = hipGetLastError();
@@ -871,7 +862,7 @@ int mcaq_morph_finalize(const mcaq_morph_scale* scales, int nscales, const mcaq_
     const int lim = MCAQ_MORPH_LDS_LIMIT - 1024;
     if (per > lim) return (int)hipErrorInvalidValue;
     // stage the weight blobs in LDS when they fit beside the tile arrays
-    const int wlds = per + weights_lds_bytes() <= lim && !(xskip() & 4);
+    const int wlds = per + weights_lds_bytes() <= lim;
     const size_t tdyn = (size_t)per + (wlds ? weights_lds_bytes() : 0);
     static int set_tiles = 0;
     if ((int)tdyn > set_tiles) {
@@ -885,7 +876,6 @@ int mcaq_morph_finalize(const mcaq_morph_scale* scales, int nscales, const mcaq_
 }
 
 int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream) {
-  if (xskip() & 2) return 0;
   if (nscales < 1 || nscales > 3) return (int)hipErrorInvalidValue;
   QuantArgs a;
   int units = 0;
@@ -896,34 +886,45 @@ int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream) 
     if (scales[i].nbits < 1 || scales[i].nbits > QMAXBITS || scales[i].bits_lo < 1 ||
         scales[i].bits_lo + scales[i].nbits - 1 > 16 || HW < 1 || scales[i].C < 1 ||
         scales[i].ht < 1 || scales[i].wt < 1 || !scales[i].x || !scales[i].y || !scales[i].bits ||
-        !scales[i].xmin || !scales[i].xmax || (scales[i].mt && scales[i].ht * scales[i].wt > QMAXNT))
+        !scales[i].xmin || !scales[i].xmax)
       return (int)hipErrorInvalidValue;
     units += scales[i].B * ((HW + 255) / 256) * ((scales[i].C + QSLICE - 1) / QSLICE);
   }
   a.nscales = nscales;
   a.units_total = units;
+  // 16-byte rows: HW % 4 == 0 and 16-byte aligned x / y bases (a contiguous
+  // view may start at any float offset), else the scalar kernel
   bool vec = true;
-  for (int i = 0; i < nscales; ++i) vec = vec && ((scales[i].H * scales[i].W) & 3) == 0;
-  // MCAQ_QUANT_NT bit 0: streaming (nontemporal) stores of y, bit 1:
-  // nontemporal loads of x.  Default (measured): NT stores
-  // always; NT loads only when the launch reads > 256 MB of x (config 3),
-  // where nothing of x survives in L2/MALL anyway; at config 2 they cost 3 us.
-  static int nt_env = -2;
-  if (nt_env == -2) { const char* e = getenv("MCAQ_QUANT_NT"); nt_env = e ? atoi(e) : -1; }
+  for (int i = 0; i < nscales; ++i)
+    vec = vec && ((scales[i].H * scales[i].W) & 3) == 0 && (((uintptr_t)scales[i].x | (uintptr_t)scales[i].y) & 15) == 0;
+  // nontemporal policy (measured): bit 0 = streaming stores of
+  // y, bit 1 = nontemporal loads of x.  NT stores always; NT loads only when
+  // the launch reads > 256 MB of x (config 3), where nothing of x survives in
+  // L2/MALL anyway.  MCAQ_QUANT_NT (build-time define) pins it for A/B builds.
+#ifdef MCAQ_QUANT_NT
+  const int nt = MCAQ_QUANT_NT;
+#else
   size_t xbytes = 0;
   for (int i = 0; i < nscales; ++i)
     xbytes += (size_t)scales[i].B * scales[i].C * scales[i].H * scales[i].W * sizeof(float);
-  const int nt = nt_env >= 0 ? nt_env : (xbytes > ((size_t)256 << 20) ? 3 : 1);
-  if (!vec)
-    hipLaunchKernelGGL((mcaq_quant_kernel<false, false, false>), dim3(units), dim3(256), 0, stream, a);
+  const int nt = xbytes > ((size_t)256 << 20) ? 3 : 1;
+#endif
+  bool mt_lds = true;
+  for (int i = 0; i < nscales; ++i) mt_lds = mt_lds && (!scales[i].mt || scales[i].ht * scales[i].wt <= QMAXNT);
+  const dim3 g(units), t(256);
+  if (!mt_lds) {
+    if (vec) hipLaunchKernelGGL((mcaq_quant_kernel<true, false, true, false>), g, t, 0, stream, a);
+    else hipLaunchKernelGGL((mcaq_quant_kernel<false, false, false, false>), g, t, 0, stream, a);
+  } else if (!vec)
+    hipLaunchKernelGGL((mcaq_quant_kernel<false, false, false, true>), g, t, 0, stream, a);
   else if (nt == 3)
-    hipLaunchKernelGGL((mcaq_quant_kernel<true, true, true>), dim3(units), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((mcaq_quant_kernel<true, true, true, true>), g, t, 0, stream, a);
   else if (nt == 2)
-    hipLaunchKernelGGL((mcaq_quant_kernel<true, true, false>), dim3(units), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((mcaq_quant_kernel<true, true, false, true>), g, t, 0, stream, a);
   else if (nt == 1)
-    hipLaunchKernelGGL((mcaq_quant_kernel<true, false, true>), dim3(units), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((mcaq_quant_kernel<true, false, true, true>), g, t, 0, stream, a);
   else
-    hipLaunchKernelGGL((mcaq_quant_kernel<true, false, false>), dim3(units), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((mcaq_quant_kernel<true, false, false, true>), g, t, 0, stream, a);
   return (int)hipGetLastError();
 }
 

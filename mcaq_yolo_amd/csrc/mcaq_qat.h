@@ -228,6 +228,15 @@ __global__ __launch_bounds__(256) void mcaq_ema_kernel(const float* bmin, const 
 
 }  // namespace mcaq
 
+namespace mcaq {
+// 16-byte vector rows need 16-byte aligned bases of every per-element array
+static inline bool qat_aligned16(const mcaq_qat_scale& s, bool bwd) {
+  uintptr_t u = (uintptr_t)s.x;
+  u |= bwd ? ((uintptr_t)s.g | (uintptr_t)s.gx) : (uintptr_t)s.y;
+  return (u & 15) == 0;
+}
+}  // namespace mcaq
+
 extern "C" {
 
 size_t mcaq_qat_work_floats(int B, int C, int H, int W) {
@@ -262,7 +271,8 @@ int mcaq_qat_forward(const mcaq_qat_scale* scales, int nscales, hipStream_t stre
   const int e = qat_args(scales, nscales, false, a, blocks);
   if (e) return e;
   bool vec = true;
-  for (int i = 0; i < nscales; ++i) vec = vec && ((scales[i].H * scales[i].W) & 3) == 0;
+  for (int i = 0; i < nscales; ++i)
+    vec = vec && ((scales[i].H * scales[i].W) & 3) == 0 && mcaq::qat_aligned16(scales[i], false);
   if (vec)
     hipLaunchKernelGGL((mcaq::mcaq_qat_kernel<false, true>), dim3(a.units_total), dim3(256), 0, stream, a);
   else
@@ -276,7 +286,8 @@ int mcaq_qat_backward(const mcaq_qat_scale* scales, int nscales, hipStream_t str
   const int e = qat_args(scales, nscales, true, a, blocks);
   if (e) return e;
   bool vec = true;
-  for (int i = 0; i < nscales; ++i) vec = vec && ((scales[i].H * scales[i].W) & 3) == 0;
+  for (int i = 0; i < nscales; ++i)
+    vec = vec && ((scales[i].H * scales[i].W) & 3) == 0 && mcaq::qat_aligned16(scales[i], true);
   if (vec)
     hipLaunchKernelGGL((mcaq::mcaq_qat_kernel<true, true>), dim3(a.units_total), dim3(256), 0, stream, a);
   else

@@ -1,0 +1,104 @@
+"""Data parallelism for the hook path: one process per GPU, batch shards,
+RCCL over xGMI (torch.distributed backend "nccl"), gloo on CPU for tests.
+
+The reference is single-process (train.py:360, rank=-1); SURVEY 8(e) lists
+what sharding the batch needs for the results to equal the single-process
+run on the global batch:
+
+* inference: the per-channel batch min/max (quantization.py:650-654) -
+  `engine.sync_channel_minmax` / `SpatialAdaptiveQuantization.process_group`;
+  detections are all-gathered after NMS (`postprocess.gather_detections`);
+* QAT (BASELINE config 5): the quantizer's EMA min/max over the global batch
+  (same `process_group`), the bit mapper's train-mode BatchNorm1d statistics
+  over the global batch of tiles (bit_allocation.py:126) -
+  `sync_mapper_batchnorm`, and the gradient all-reduce - `allreduce_gradients`
+  (one flat bucket: the hook parameters are ~8 k floats, one latency-bound
+  collective instead of 30).
+"""
+import torch
+import torch.nn as nn
+
+
+class GroupBatchNorm1d(nn.BatchNorm1d):
+    """BatchNorm1d whose train-mode statistics span every rank of a process
+    group (sum, sum of squares and count all-reduced once per forward, with
+    autograd through the collective); eval mode and the state_dict are plain
+    BatchNorm1d's, so reference checkpoints load unchanged.  Works on CPU
+    (gloo) as well as on the GPU (RCCL), unlike torch.nn.SyncBatchNorm."""
+
+    def __init__(self, num_features, eps=1e-5, momentum=0.1, affine=True, track_running_stats=True,
+                 process_group=None):
+        super().__init__(num_features, eps, momentum, affine, track_running_stats)
+        self.process_group = process_group
+
+    @classmethod
+    def from_bn(cls, bn, process_group):
+        new = cls(bn.num_features, bn.eps, bn.momentum, bn.affine, bn.track_running_stats, process_group)
+        new.load_state_dict(bn.state_dict())
+        return new.to(bn.weight.device if bn.affine else bn.running_mean.device)
+
+    def forward(self, x):
+        if not self.training or self.process_group is None:
+            return super().forward(x)
+        from torch.distributed.nn.functional import all_reduce
+        n_local = torch.tensor([float(x.shape[0])], device=x.device, dtype=x.dtype)
+        stats = torch.cat([x.sum(dim=0), (x * x).sum(dim=0), n_local])
+        stats = all_reduce(stats, group=self.process_group)
+        C = x.shape[1]
+        n = stats[2 * C]
+        mean = stats[:C] / n
+        var = (stats[C:2 * C] / n - mean * mean).clamp(min=0.0)
+        if self.track_running_stats:
+            with torch.no_grad():
+                self.num_batches_tracked += 1
+                m = self.momentum if self.momentum is not None else 1.0 / float(self.num_batches_tracked)
+                unbiased = var.detach() * (n / (n - 1).clamp(min=1.0))
+                self.running_mean.mul_(1 - m).add_(m * mean.detach())
+                self.running_var.mul_(1 - m).add_(m * unbiased)
+        y = (x - mean) / torch.sqrt(var + self.eps)
+        return y * self.weight + self.bias if self.affine else y
+
+
+def sync_mapper_batchnorm(mapper, process_group):
+    """Swap the mapping network's BatchNorm1d layers (bit_allocation.py:126)
+    for GroupBatchNorm1d over `process_group`; returns the mapper."""
+    net = getattr(mapper, "mapping_network", None)
+    if net is None:
+        return mapper
+    for i, m in enumerate(net):
+        if isinstance(m, nn.BatchNorm1d) and not isinstance(m, GroupBatchNorm1d):
+            net[i] = GroupBatchNorm1d.from_bn(m, process_group)
+    if hasattr(mapper, "_blob"):
+        mapper._blob.key = None
+    return mapper
+
+
+def allreduce_gradients(params, process_group, average=True):
+    """Average the gradients of `params` over the group with ONE collective:
+    flatten into a single bucket, all_reduce, copy back (None grads count as
+    zeros and stay None)."""
+    import torch.distributed as dist
+    ps = [p for p in params if p.grad is not None]
+    if not ps:
+        return
+    flat = torch.cat([p.grad.reshape(-1) for p in ps])
+    dist.all_reduce(flat, group=process_group)
+    if average:
+        flat /= dist.get_world_size(process_group)
+    o = 0
+    for p in ps:
+        n = p.numel()
+        p.grad.copy_(flat[o:o + n].view_as(p.grad))
+        o += n
+
+
+def shard_hooks(hooks, process_group, rank, world, local_batch):
+    """Configure an MCAQHooks / MCAQYOLO for batch-sharded data parallelism:
+    min/max all-reduce in every quantizer, global-batch tile order for the
+    fractal regression, synced mapper BatchNorm for QAT."""
+    hooks.process_group = process_group
+    hooks.batch_offset, hooks.batch_total = rank * local_batch, world * local_batch
+    for q in hooks.quantizers.values():
+        q.process_group = process_group
+    sync_mapper_batchnorm(hooks.bit_mapper, process_group)
+    return hooks

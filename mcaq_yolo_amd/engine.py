@@ -244,7 +244,10 @@ class HookPlan:
         nf = n if self._fz is not None else 0
         abi.check(L.mcaq_morph_finalize(self._mo, n, self._fz, nf, sh), "mcaq_morph_finalize")
         if self._fz is not None and process_group is not None:
-            sync_channel_minmax(self.bufs, process_group)
+            # the collective runs on the launch stream: ordered after the
+            # finalize that writes xmin/xmax and before pass 2 that reads them
+            with torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream()):
+                sync_channel_minmax(self.bufs, process_group)
         if self._qs is not None:
             abi.check(L.mcaq_quant(self._qs, n, sh), "mcaq_quant")
         return self.bufs

@@ -87,6 +87,12 @@ def gather_detections(out, counts, group=None):
     (world * B_local, max_det, 6) + counts in rank order, one collective each."""
     import torch.distributed as dist
     world = dist.get_world_size(group)
+    if dist.get_backend(group) == "gloo":       # CPU rehearsal: gloo has no *_into_tensor gather
+        outs = [torch.empty_like(out) for _ in range(world)]
+        cnts = [torch.empty_like(counts) for _ in range(world)]
+        dist.all_gather(outs, out.contiguous(), group=group)
+        dist.all_gather(cnts, counts.contiguous(), group=group)
+        return torch.cat(outs), torch.cat(cnts)
     g_out = torch.empty((world * out.shape[0],) + tuple(out.shape[1:]), device=out.device, dtype=out.dtype)
     g_cnt = torch.empty(world * counts.shape[0], device=counts.device, dtype=counts.dtype)
     dist.all_gather_into_tensor(g_out, out.contiguous(), group=group)

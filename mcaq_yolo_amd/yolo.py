@@ -307,10 +307,27 @@ class MCAQYOLO(MCAQHooks):
         self.min_bits, self.max_bits = min_bits, max_bits
         self.device = device
         if weights is not None:
-            self.load_state_dict(_load_weights(weights), strict=False)
+            self.load_checkpoint(_load_weights(weights))
         if str(device).startswith("cuda") and torch.cuda.is_available():
             self.to(device)
         self.register(self.model.model)
+
+    def load_checkpoint(self, sd):
+        """Load a reference MCAQYOLO state_dict ('model.model.<i>...', hook
+        modules) or a bare ultralytics DetectionModel one ('model.<i>...',
+        remapped).  Non-strict like the reference's fallback (inference.py:
+        105-115), but a checkpoint that leaves detector weights unloaded
+        raises instead of silently running on random weights."""
+        if sd and not any(k.startswith("model.model.") for k in sd) and any(k.startswith("model.") for k in sd):
+            sd = {("model." + k if k.startswith("model.") else k): v for k, v in sd.items()}
+        res = self.load_state_dict(sd, strict=False)
+        missing = [k for k in res.missing_keys if k.startswith("model.") and not k.endswith("num_batches_tracked")]
+        if missing:
+            raise RuntimeError("checkpoint leaves %d detector tensors unloaded (first: %s)" % (len(missing), missing[0]))
+        if res.unexpected_keys:
+            warnings.warn("[MCAQ] %d unexpected checkpoint keys ignored (first: %s)"
+                          % (len(res.unexpected_keys), res.unexpected_keys[0]))
+        return res
 
     def forward(self, x, temperature=1.0, return_aux=True, targets=None, quantize=True):
         """models/mcaq_yolo.py:527-589."""

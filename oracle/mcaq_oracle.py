@@ -226,6 +226,41 @@ def canny_cv2compat(gray, hysteresis_iters=8, return_internals=False):
     return edge
 
 
+def _nms(mag, gx, gy):
+    d = nms_direction(gx, gy)
+    out = np.zeros_like(mag)
+    for k, ((dy1, dx1), (dy2, dx2)) in _NMS_NB.items():
+        keep = (mag >= _shift_rep(mag, dy1, dx1)) & (mag >= _shift_rep(mag, dy2, dx2))
+        out = np.where((d == k) & keep, mag, out)
+    return out
+
+
+def _hysteresis(strong, weak, iters):
+    edge = strong.astype(np.uint8)
+    for _ in range(max(1, iters)):
+        grown = _max3x3(edge, 0)
+        edge = np.where(weak & (grown > 0), np.uint8(1), edge).astype(np.uint8)
+    return edge
+
+
+def canny_legacy(gray):
+    """morphology.py:512-540 (canny_impl='legacy'): blur, Sobel of the blur,
+    L2 magnitude sqrt(gx^2 + gy^2 + 1e-12), NMS, per-image min-max
+    normalisation of the NMS map, Otsu of that map, 2 hysteresis rounds."""
+    blur = conv2d(gray, K["gauss5_canny"])
+    gx, gy = sobel(blur)
+    s = ((gx * gx).astype(f32) + (gy * gy).astype(f32)).astype(f32)
+    mag = cr32(np.sqrt, (s + f32(1e-12)).astype(f32))
+    n = normalize01(_nms(mag, gx, gy))
+    t = otsu_threshold(n)[:, None, None]
+    return _hysteresis(n > t, n > (f32(0.5) * t).astype(f32), 2)
+
+
+def otsu_binarize(gray):
+    """binarize_impl='otsu' (morphology.py:420-424, 546-547)."""
+    return (gray > otsu_threshold(gray)[:, None, None]).astype(np.uint8)
+
+
 def adaptive_binarize(gray, C=2.0):
     """morphology.py:551-573: g255 > G11(g255, replicate) - C."""
     g255 = (gray * f32(255.0)).astype(f32)
@@ -410,8 +445,10 @@ def score_image(x, grid_size=8, feature_weights=None):
     return np.clip(c.mean(axis=(1, 2)), 0.0, 1.0).astype(np.float32)
 
 
-def phi_tiles(x, grid_size=8, batch_offset=0, batch_total=None, internals=False):
-    """_phi_tiles_gpu (morphology.py:826-873) -> phi (B, ht, wt, 8)."""
+def phi_tiles(x, grid_size=8, batch_offset=0, batch_total=None, internals=False, canny_impl="cv2compat",
+              binarize_impl="adaptive", contour_components=True):
+    """_phi_tiles_gpu (morphology.py:826-873) -> phi (B, ht, wt, 8); the
+    analyzer switches of morphology.py:29-37 select the legacy variants."""
     B, C, H, W = x.shape
     tile = tile_size(H, grid_size)
     ht, wt = H // tile, W // tile
@@ -420,12 +457,14 @@ def phi_tiles(x, grid_size=8, batch_offset=0, batch_total=None, internals=False)
     gray = normalize01(graw)
     gx, gy = sobel(gray)
     edge, ci = canny_cv2compat(gray, return_internals=True)
-    binm = adaptive_binarize(gray)
+    if canny_impl == "legacy":
+        edge = canny_legacy(gray)
+    binm = otsu_binarize(gray) if binarize_impl == "otsu" else adaptive_binarize(gray)
     p1 = (fractal_tiles(edge, tile, batch_offset, batch_total) / f32(2.0)).astype(f32)
     p2 = lbp_entropy_tiles(gray, tile)
     p3 = gradvar_tiles(gx, gy, tile)
     p4 = tile_mean_seq(edge.astype(f32), tile)
-    p5 = contour_tiles(binm, tile)
+    p5 = contour_tiles(binm, tile, contour_components)
     p8 = cr32(np.sqrt, ((p4 * p5).astype(f32) + f32(1e-12)).astype(f32))
     phi = np.stack([p1, p2, p3, p4, p5, (p1 * p2).astype(f32), (p3 * p3).astype(f32), p8], axis=-1)
     if internals:
@@ -503,9 +542,9 @@ def bilateral(c, sigma_r=0.1):
     return out
 
 
-def analyzer_forward(x, P, grid_size=8, batch_offset=0, batch_total=None):
+def analyzer_forward(x, P, grid_size=8, batch_offset=0, batch_total=None, **opts):
     """MorphologicalComplexityAnalyzer.forward (morphology.py:939-973)."""
-    phi = phi_tiles(x, grid_size, batch_offset, batch_total)
+    phi = phi_tiles(x, grid_size, batch_offset, batch_total, **opts)
     B, ht, wt, _ = phi.shape
     c = complexity_mlp(phi.reshape(-1, 8), P).reshape(B, ht, wt)
     return np.clip(bilateral(c), f32(0.0), f32(1.0)).astype(f32), phi, c
@@ -726,9 +765,10 @@ def spatial_quantize_compat(x, bit_map, min_vals, max_vals, tile_h, tile_w, mask
 
 
 def hook_forward(x, P, grid_size=8, mapper="mlp", temperature=1.0, smooth=True,
-                 normalize=False, softmask_prefix="soft_mask.", xmin=None, xmax=None):
-    """analyzer -> (normalize) -> mapper -> quantizer.  Returns dict."""
-    C, phi, c_mlp = analyzer_forward(x, P, grid_size)
+                 normalize=False, softmask_prefix="soft_mask.", xmin=None, xmax=None, **opts):
+    """analyzer -> (normalize) -> mapper -> quantizer.  Returns dict.  opts:
+    the analyzer switches (canny_impl, binarize_impl, contour_components)."""
+    C, phi, c_mlp = analyzer_forward(x, P, grid_size, **opts)
     Cn = normalize_complexity(C) if normalize else C
     if mapper == "mlp":
         bits = mlp_mapper(Cn, P, temperature, continuous=False)

@@ -1,0 +1,174 @@
+"""Data-parallel pieces beyond the min/max all-reduce, on CPU with gloo
+(world_size 2; the GPU path runs the same code over RCCL):
+
+* postprocess.gather_detections - detections of every rank's shard, in rank
+  order (inference.py:213-219 / SURVEY 8(e));
+* the quantizer's EMA statistics over the global batch in QAT
+  (quantization.py:319-353 with `process_group`): every rank's running
+  min/max and its shard of y equal the single-process run on the full batch;
+* dist.sync_mapper_batchnorm + dist.allreduce_gradients: the train-mode bit
+  mapper (BatchNorm1d over the batch's tiles, bit_allocation.py:126) on two
+  shards gives the single-process bits, BN running statistics and parameter
+  gradients of the concatenated batch (summation order: rtol 1e-5 / 1e-4).
+Unmeasured on multi-GPU hardware here (one-GPU pool); correctness only."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import GOLDEN, load_weights
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(fn, world=2, *args):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_entry, args=(fn, r, world, port, q, args)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in range(world))
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def _entry(fn, rank, world, port, q, args):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "tests"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        q.put((rank, globals()[fn](rank, world, *args)))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def _sd(prefix):
+    W = load_weights()
+    return {k[len(prefix):]: torch.from_numpy(np.asarray(v)) for k, v in W.items() if k.startswith(prefix)}
+
+
+# ---------------------------------------------------------------------------
+def _gather_worker(rank, world):
+    from mcaq_yolo_amd.postprocess import gather_detections
+    g = torch.Generator().manual_seed(rank)
+    out = torch.rand(3, 10, 6, generator=g)
+    cnt = torch.tensor([rank, 2, 7], dtype=torch.int32)
+    go, gc = gather_detections(out, cnt, dist.group.WORLD)
+    return go.numpy(), gc.numpy()
+
+
+def test_gather_detections_two_ranks():
+    res = _run("_gather_worker")
+    want = np.concatenate([torch.rand(3, 10, 6, generator=torch.Generator().manual_seed(r)).numpy()
+                           for r in range(2)])
+    for r in range(2):
+        go, gc = res[r]
+        assert np.array_equal(go, want)
+        assert gc.tolist() == [0, 2, 7, 1, 2, 7]
+
+
+# ---------------------------------------------------------------------------
+def _qat_case():
+    d = np.load(os.path.join(GOLDEN, "qat_p4_smooth.npz"))
+    x = torch.from_numpy(d["x"])
+    x = torch.cat([x, torch.flip(x, dims=[0]) * 1.25])        # 4 images
+    bits = torch.from_numpy(d["bits"])
+    bits = torch.cat([bits, torch.flip(bits, dims=[0])])
+    return x, bits
+
+
+def _qat_ema_run(x, bits, group):
+    from mcaq_yolo_amd import core
+    q = core.SpatialAdaptiveQuantization()
+    q.soft_mask.load_state_dict(_sd("soft_mask."))
+    q.process_group = group
+    q.train()
+    ys = []
+    for step in range(3):
+        xx = x * (1.0 + 0.1 * step)
+        ys.append(q(xx, bits, training=True).detach())
+    return q.running_min.numpy(), q.running_max.numpy(), ys[-1].numpy()
+
+
+def _qat_ema_worker(rank, world):
+    x, bits = _qat_case()
+    n = x.shape[0] // world
+    return _qat_ema_run(x[rank * n:(rank + 1) * n], bits[rank * n:(rank + 1) * n], dist.group.WORLD)
+
+
+def test_qat_ema_statistics_two_ranks():
+    x, bits = _qat_case()
+    rmin, rmax, y = _qat_ema_run(x, bits, None)
+    res = _run("_qat_ema_worker")
+    n = x.shape[0] // 2
+    for r in range(2):
+        assert np.array_equal(res[r][0], rmin) and np.array_equal(res[r][1], rmax)
+        assert np.array_equal(res[r][2], y[r * n:(r + 1) * n])
+
+
+# ---------------------------------------------------------------------------
+def _mapper_run(c, g, group, world):
+    from mcaq_yolo_amd import core
+    from mcaq_yolo_amd import dist as mdist
+    m = core.ComplexityToBitMappingNetwork()
+    m.load_state_dict(_sd("bit_mapper."))
+    if group is not None:
+        mdist.sync_mapper_batchnorm(m, group)
+    m.train()
+    c = c.clone().requires_grad_(True)
+    bits = m(c, 1.0, return_continuous=True)
+    # the global loss is the sum of the ranks' losses; the collective's
+    # autograd carries every rank's share of the BatchNorm statistics, so the
+    # summed (not averaged) parameter gradients equal the single-process ones
+    (bits * g).sum().backward()
+    if group is not None:
+        mdist.allreduce_gradients(m.parameters(), group, average=False)
+    grads = {n: p.grad.numpy().copy() for n, p in m.mapping_network.named_parameters()}
+    bufs = {n: b.numpy().copy() for n, b in m.mapping_network.named_buffers() if b.dtype.is_floating_point}
+    return bits.detach().numpy(), grads, bufs, c.grad.numpy()
+
+
+def _mapper_case():
+    d = np.load(os.path.join(GOLDEN, "train_mapper.npz"))
+    return torch.from_numpy(d["t1.c"]), torch.from_numpy(d["t1.gb"])
+
+
+def _mapper_worker(rank, world):
+    c, g = _mapper_case()
+    n = c.shape[0] // world
+    return _mapper_run(c[rank * n:(rank + 1) * n], g[rank * n:(rank + 1) * n], dist.group.WORLD, world)
+
+
+def test_mapper_sync_batchnorm_and_grad_allreduce_two_ranks():
+    c, g = _mapper_case()
+    bits, grads, bufs, gc = _mapper_run(c, g, None, 1)
+    res = _run("_mapper_worker")
+    n = c.shape[0] // 2
+    gmax = max(np.abs(v).max() for v in grads.values())
+    for r in range(2):
+        rb, rg, rbuf, rgc = res[r]
+        np.testing.assert_allclose(rb, bits[r * n:(r + 1) * n], rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(rgc, gc[r * n:(r + 1) * n], rtol=1e-4, atol=1e-4 * np.abs(gc).max())
+        for k, v in grads.items():
+            np.testing.assert_allclose(rg[k], v, rtol=1e-4, atol=1e-4 * gmax, err_msg=k)
+        for k, v in bufs.items():
+            np.testing.assert_allclose(rbuf[k], v, rtol=1e-5, atol=1e-6, err_msg=k)

@@ -7,10 +7,12 @@ the oracle.  Bit-exact everywhere the oracle is bit-exact:
 fixtures themselves complexity is within 1e-6 relative and phi8 within 1 ulp,
 see test_oracle_cpu.py).  Tolerances are written where they apply.
 """
+import os
+
 import numpy as np
 import pytest
 
-from conftest import case_names, load_case, load_weights
+from conftest import GOLDEN, case_names, load_case, load_weights
 from oracle import mcaq_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -239,3 +241,81 @@ def test_packed_workgroups_vs_oracle(dev, blobs, shape):
     x = np.where(x > 0, x, x * f32(0.1)).astype(f32)
     out = run_plan(dev, blobs, [x], 8, "mlp")[0]
     check_against_oracle(out, x, blobs[0], 8, "mlp")
+
+
+OPT_GPU = sorted(f[:-4] for f in os.listdir(GOLDEN)
+                 if f.startswith("opt_") and f.endswith(".npz") and not f.startswith("opt_legacy"))
+
+
+@pytest.mark.parametrize("name", OPT_GPU)
+def test_analyzer_switches_vs_reference(dev, blobs, name):
+    """binarize_impl='otsu' and contour_components=False on the morph kernel
+    against the reference's own outputs (tests/golden/make_golden_r02.py) and
+    the oracle: edge, mask, phi1..7 and bits bit-exact, phi8 within 1 ulp of
+    the reference (bit-exact vs the oracle)."""
+    d = np.load(os.path.join(GOLDEN, name + ".npz"))
+    opts = {k[4:]: (str(d[k]) if d[k].dtype.kind == "U" else d[k].item()) for k in d.files if k.startswith("opt_")}
+    x = d["x"].astype(f32)
+    grid = int(d["grid"])
+    out = run_plan(dev, blobs, [x], grid, "mlp", binarize_otsu=opts.get("binarize_impl") == "otsu",
+                   contour_components=opts.get("contour_components", True))[0]
+    assert np.array_equal(out["edge"], d["edge"])
+    assert np.array_equal(out["binmask"], d["binmask"])
+    assert np.array_equal(out["phi"][..., :7], d["phi"][..., :7])
+    assert np.all(np.abs(out["phi"][..., 7] - d["phi"][..., 7]) <= np.spacing(np.abs(d["phi"][..., 7])))
+    assert np.array_equal(out["bits"], d["bits_mlp"])
+    ref = O.hook_forward(x, blobs[0], grid, **opts)
+    assert np.array_equal(out["phi"], ref["phi"])
+    assert np.array_equal(out["complexity"], ref["complexity"])
+    assert np.array_equal(out["y"], ref["y"])
+
+
+def _full_size_properties(dev, blobs, shapes, grid, seed):
+    """Determinism, bits in [2, 8] integers, exact channel min/max, finite y,
+    and the first two images of every scale bit-exact vs the oracle (with the
+    batch min/max the kernel computed) at a BASELINE config's full shapes."""
+    import torch
+    from mcaq_yolo_amd.engine import HookPlan, ScaleGeom
+    W, cm, mm, sm = blobs
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    feats = [torch.nn.functional.silu(1.5 * torch.randn(s, generator=g) +
+                                      torch.nn.functional.interpolate(torch.randn(s[0], s[1], s[2] // 8, s[3] // 8,
+                                                                                  generator=g), size=s[2:],
+                                                                      mode="bilinear")).to(dev) for s in shapes]
+    plan = HookPlan([ScaleGeom(*s, grid) for s in shapes], dev)
+    bufs = plan.run(feats, cm, mm, [sm] * len(shapes))
+    y1 = [b["y"].clone() for b in bufs]
+    bits1 = [b["bits"].clone() for b in bufs]
+    bufs = plan.run(feats, cm, mm, [sm] * len(shapes))
+    torch.cuda.synchronize()
+    seen = set()
+    for f, b, yy, bb in zip(feats, bufs, y1, bits1):
+        assert torch.equal(b["y"], yy) and torch.equal(b["bits"], bb), "non-deterministic"
+        assert torch.equal(b["xmin"], f.amin(dim=(0, 2, 3))) and torch.equal(b["xmax"], f.amax(dim=(0, 2, 3)))
+        bits = b["bits"]
+        assert bool(((bits >= 2) & (bits <= 8) & (bits == bits.round())).all())
+        seen |= set(bits.unique().tolist())
+        assert bool(torch.isfinite(b["y"]).all())
+    for f, b in zip(feats, bufs):
+        x2 = f[:2].cpu().numpy()
+        # batch_total: the fractal regression's ATen reduction order follows
+        # the tile's column in the whole batch (oracle fractal_tiles)
+        ref = O.hook_forward(x2, W, grid, xmin=b["xmin"].cpu().numpy(), xmax=b["xmax"].cpu().numpy(),
+                             batch_total=f.shape[0])
+        assert np.array_equal(b["bits"][:2].cpu().numpy(), ref["bits"])
+        assert np.array_equal(b["y"][:2].cpu().numpy(), ref["y"])
+    return seen
+
+
+def test_config3_yolov8s_bs64_grid16_properties(dev, blobs):
+    """BASELINE config 3 (yolov8s bs64, grid 16: P3 tile 4 / 20x20 tiles, the
+    LDS-tile stress case) at full size."""
+    seen = _full_size_properties(dev, blobs, [(64, 128, 80, 80), (64, 256, 40, 40), (64, 512, 20, 20)], 16, 3)
+    assert len(seen) >= 2
+
+
+def test_config4_yolov8m_slice_properties(dev, blobs):
+    """BASELINE config 4's per-GPU slice (yolov8m, 32 images: 192 x 80^2,
+    384 x 40^2, 576 x 20^2, grid 8) at full size."""
+    seen = _full_size_properties(dev, blobs, [(32, 192, 80, 80), (32, 384, 40, 40), (32, 576, 20, 20)], 8, 4)
+    assert len(seen) >= 2

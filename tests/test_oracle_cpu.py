@@ -7,15 +7,16 @@ exact; soft mask / y exact except the B=1 case (CPU conv takes an MKL path at
 batch 1), where they are within 1e-6 relative.
 """
 import math
+import os
 
 import numpy as np
 import pytest
 
-from conftest import case_names, load_case, load_weights
+from conftest import GOLDEN, case_names, load_case, load_weights
 from oracle import mcaq_oracle as O
 from oracle.ieee import aten_sum, fma32
 
-FAST = [c for c in case_names() if c not in ("t64_c1", "t32_c4")]
+FAST = [c for c in case_names() if c not in ("t64_c1", "t32_c4", "m_p3", "m_p4")]   # m_*: test_option_and_yolov8m_fixtures
 
 
 def rel(a, b):
@@ -163,3 +164,30 @@ def test_spatial_quantize_compat_vs_pytorch_semantics():
     y2 = O.quantize(x, bits, None, mn, mx)
     assert np.array_equal(y1, y2)
     assert math.isfinite(float(y1.sum()))
+
+
+OPT_CASES = sorted(f[4:-4] for f in os.listdir(GOLDEN) if f.startswith("opt_") and f.endswith(".npz"))
+
+
+def _opts(d):
+    return {k[4:]: (str(d[k]) if d[k].dtype.kind == "U" else d[k].item()) for k in d.files if k.startswith("opt_")}
+
+
+@pytest.mark.parametrize("name", ["opt_" + c for c in OPT_CASES] + ["case_m_p3", "case_m_p4"])
+def test_option_and_yolov8m_fixtures(name):
+    """The analyzer switches (binarize_impl='otsu', contour_components=False,
+    canny_impl='legacy') and the yolov8m C3/C4 shapes, against the reference's
+    own outputs (tests/golden/make_golden_r02.py)."""
+    d = np.load(os.path.join(GOLDEN, name + ".npz"))
+    W = load_weights()
+    x = d["x"].astype(np.float32)
+    opts = _opts(d)
+    phi, I = O.phi_tiles(x, int(d["grid"]), internals=True, **opts)
+    assert np.array_equal(I["edge"], d["edge"])
+    assert np.array_equal(I["binmask"], d["binmask"])
+    assert np.array_equal(phi[..., :7], d["phi"][..., :7])
+    assert np.all(np.abs(phi[..., 7] - d["phi"][..., 7]) <= np.spacing(np.abs(d["phi"][..., 7])))
+    C, _, _ = O.analyzer_forward(x, W, int(d["grid"]), **opts)
+    assert rel(C, d["complexity"]) < 1e-6
+    assert np.array_equal(O.mlp_mapper(C, W, 1.0), d["bits_mlp"])
+    assert np.array_equal(O.linear_mapper(C, 1.0), d["bits_lin"])

@@ -82,3 +82,19 @@ def test_nms_oracle_known_answers():
     q[0, 4, :] = [0.5, 0.5]
     assert NO.non_max_suppression(q, 0.1, 0.45)[0].shape == (1, 6)
     assert NO.non_max_suppression(q, 0.1, 1.0)[0].shape == (2, 6)
+
+
+def test_checkpoint_loading_checks_keys(tmp_path):
+    """a bare DetectionModel state_dict is remapped, a checkpoint
+    missing detector weights raises instead of running on random weights."""
+    from mcaq_yolo_amd.yolo import MCAQYOLO
+    torch.manual_seed(0)
+    src = MCAQYOLO("yolov8n", device="cpu")
+    bare = {k[len("model."):]: v for k, v in src.state_dict().items() if k.startswith("model.")}
+    dst = MCAQYOLO("yolov8n", device="cpu")
+    dst.load_checkpoint(bare)
+    k = "model.model.0.conv.weight"
+    assert torch.equal(dst.state_dict()[k], src.state_dict()[k])
+    partial = {kk: v for kk, v in src.state_dict().items() if not kk.startswith("model.model.22")}
+    with pytest.raises(RuntimeError, match="unloaded"):
+        dst.load_checkpoint(partial)
