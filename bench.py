@@ -16,7 +16,8 @@ HIP streams, so one batch's latency-bound per-image morphology overlaps the
 HBM passes of the others; `value` = images of all K timed steps / wall time.
 `path_roofline` is the north-star figure (12 B per feature element over the
 step time); `roofline` is the dominant kernel, pass 2, timed with HIP events
-around each of its launches in the timed region.  `cpu_baseline` is this
+around each of its launches in single-batch steps run in sequence (the
+context `rocprofv3 ... bench.py --pipeline 1` profiles).  `cpu_baseline` is this
 package's pure-PyTorch path (fallback.py) at the same config on the host.
 
 N > 1: one process per GPU (torch.distributed.run), each rank takes its own
@@ -27,6 +28,7 @@ reference run on the whole global batch.  --config 5: the QAT training step.
 Prints ONE JSON line (rank 0).
 """
 import argparse
+import ctypes
 import json
 import math
 import os
@@ -419,30 +421,31 @@ def cpu_baseline(cfg_id, budget_s=10.0):
 
 
 class Runner:
-    """Issues hook-path steps.  `depth` independent HookPlans (own buffers) on
-    `depth` HIP streams: step i runs on plan/stream i % depth, so the per-image
-    morphology of one batch (latency-bound) overlaps the HBM passes of the
-    others.  A step is two HIP-graph replays, [pass 1 + morphology] and
-    [pass 2] (with the RCCL min/max all-reduce between them when N > 1), with
-    timing events recorded on the step's stream before, between and after:
-    every pass-2 launch of the run is timed where it runs (`quant_us`)."""
+    """Issues hook-path steps.  Independent HookPlans (own inputs and
+    buffers) cycled over `depth` HIP streams: step i runs plan i % len(plans)
+    on stream i % depth, so the per-image morphology of one batch
+    (latency-bound) overlaps the HBM passes of the others.  A step is one
+    HIP-graph replay (N = 1), or two replays around the RCCL min/max
+    all-reduce (N > 1)."""
 
-    def __init__(self, plans, pg, use_graph):
+    def __init__(self, plans, pg, use_graph, depth):
         self.plans, self.pg = plans, pg
-        self.streams = [torch.cuda.Stream() for _ in plans]
+        self.streams = [torch.cuda.Stream() for _ in range(depth)]
         self.graphs = [None] * len(plans)
         self.i = 0
-        self.marks = []          # (e_start, e_pre_done, e_quant_done) per step
         if use_graph:
             torch.cuda.synchronize()
-            for p, (plan, st) in enumerate(zip(plans, self.streams)):
+            for p, plan in enumerate(plans):
+                st = self.streams[p % depth]
                 with torch.cuda.stream(st):
                     for _ in range(2):          # warm the launchers outside capture
                         plan.launch(st, self.pg)
                 st.synchronize()
+                segs = [lambda pl=plan: pl.launch(torch.cuda.current_stream())] if pg is None else \
+                    [lambda pl=plan: pl.launch_pre(torch.cuda.current_stream()),
+                     lambda pl=plan: pl.launch_quant(torch.cuda.current_stream())]
                 gs = []
-                for seg in (lambda pl=plan: pl.launch_pre(torch.cuda.current_stream()),
-                            lambda pl=plan: pl.launch_quant(torch.cuda.current_stream())):
+                for seg in segs:
                     g = torch.cuda.CUDAGraph()
                     with torch.cuda.graph(g, stream=st):
                         seg()
@@ -452,32 +455,48 @@ class Runner:
 
     def step(self):
         p = self.i % len(self.plans)
+        plan, st, gs = self.plans[p], self.streams[self.i % len(self.streams)], self.graphs[p]
         self.i += 1
-        plan, st, gs = self.plans[p], self.streams[p], self.graphs[p]
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
         with torch.cuda.stream(st):
-            ev[0].record(st)
             if gs is None:
-                plan.launch_pre(st)
+                plan.launch(st, self.pg)
+            elif self.pg is None:
+                gs[0].replay()
             else:
                 gs[0].replay()
-            if self.pg is not None:
                 sync_channel_minmax(plan.bufs, self.pg)
-            ev[1].record(st)
-            if gs is None:
-                plan.launch_quant(st)
-            else:
                 gs[1].replay()
-            ev[2].record(st)
-        self.marks.append(ev)
 
     def sync(self):
         for st in self.streams:
             torch.cuda.current_stream().wait_stream(st)
 
-    def quant_us(self, first=0):
-        """Per-step pass-2 durations (us) of steps first.. (call after a sync)."""
-        return [e[1].elapsed_time(e[2]) * 1e3 for e in self.marks[first:]]
+
+def kernel_timing(plan, reps=20):
+    """Per-launch device time of each kernel of a step, in sequence: `reps`
+    single-batch steps on one stream.  Pass 1 and pass 2 are launched through
+    hipExtLaunchKernel with start/stop events (mcaq_time_next_launch: the
+    dispatch's own start and end, as a kernel trace reports them); the
+    morphology launch (two kernels + finalize) by events around it."""
+    st = torch.cuda.current_stream()
+    L = plan.lib
+    names = ("stats", "morph_finalize", "quant")
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(reps)]
+    for e in ev:            # create the HIP events (lazily created on first record)
+        for x in e:
+            x.record(st)
+    torch.cuda.synchronize()
+    for e in ev:
+        L.mcaq_time_next_launch(ctypes.c_void_p(e[0].cuda_event), ctypes.c_void_p(e[1].cuda_event))
+        plan.launch_stats(st)
+        e[2].record(st)
+        plan.launch_morph(st)
+        e[3].record(st)
+        L.mcaq_time_next_launch(ctypes.c_void_p(e[4].cuda_event), ctypes.c_void_p(e[5].cuda_event))
+        plan.launch_quant(st)
+    torch.cuda.synchronize()
+    pairs = ((0, 1), (2, 3), (4, 5))
+    return {k: sum(e[a].elapsed_time(e[b]) for e in ev) * 1e3 / reps for k, (a, b) in zip(names, pairs)}
 
 
 def main():
@@ -487,7 +506,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS) + [5],
                     help="2/3/4: inference hook path; 5: QAT hook training step")
-    ap.add_argument("--pipeline", type=int, default=3, help="batches in flight (independent plans/streams)")
+    ap.add_argument("--pipeline", type=int, default=3, help="batches in flight (HIP streams)")
+    ap.add_argument("--inputs", type=int, default=0,
+                    help="distinct input batches cycled through (default max(3, pipeline): >= 276 MB of x at "
+                         "config 2, more than the 256 MiB Infinity Cache, so no step finds its input cached)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (YOLOv8 + hooks + NMS) leg")
     ap.add_argument("--e2e", action="store_true", help="only the end-to-end line (run_e2e)")
@@ -525,7 +547,7 @@ def main():
     cm, mm, sm = load_blobs(dev)
     geoms = [ScaleGeom(B, c, h, w, grid) for c, (h, w) in zip(chans, SIZES)]
     plans = []
-    for p in range(depth):
+    for p in range(max(args.inputs or max(3, depth), depth)):
         # each batch in flight has its own synthetic input (seeded per rank and slot)
         feats = [synth_features(B, c, h, w, 1000 * args.config + i + 7919 * rank + 104729 * p, dev)
                  for i, (c, (h, w)) in enumerate(zip(chans, SIZES))]
@@ -537,36 +559,13 @@ def main():
     torch.cuda.synchronize()
 
     use_graph = not args.eager
-    runner = Runner(plans, pg, use_graph)
+    runner = Runner(plans, pg, use_graph, depth)
     for _ in range(max(args.warmup, 1)):
         runner.step()
     runner.sync()
     torch.cuda.synchronize()
 
-    # pass 1 and the morphology launch alone (informational; pass 2 is timed
-    # inside the steps): each launched `reps` times back to back between two
-    # HIP events on the launch stream
-    plan = plans[0]
-    L = plan.lib
-    stream = torch.cuda.current_stream()
-    from mcaq_yolo_amd import abi
-    sh = abi.ctypes.c_void_p(stream.cuda_stream)
-    nf = plan._n if plan._fz is not None else 0
-    launch = {"stats": lambda: L.mcaq_stats(plan._st, plan._n, sh),
-              "morph_finalize": lambda: L.mcaq_morph_finalize(plan._mo, plan._n, plan._fz, nf, sh)}
-    kt = {}
-    reps = 20
-    e0 = torch.cuda.Event(enable_timing=True)
-    e1 = torch.cuda.Event(enable_timing=True)
-    for k, fn in launch.items():
-        fn()
-        torch.cuda.synchronize()
-        e0.record(stream)
-        for _ in range(reps):
-            fn()
-        e1.record(stream)
-        torch.cuda.synchronize()
-        kt[k] = e0.elapsed_time(e1) * 1e3 / reps   # us
+    kt = kernel_timing(plans[0])
     # single-batch latency: one step at a time, nothing in flight beside it
     lat = []
     for _ in range(10):
@@ -579,7 +578,6 @@ def main():
     latency_ms = sorted(lat)[len(lat) // 2] * 1e3
 
     # ---- timed region: K steps, `depth` batches in flight
-    first_timed = len(runner.marks)
     if pg is not None:
         import torch.distributed as dist
         dist.barrier()
@@ -598,9 +596,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.barrier()
         step_s = float(t.item())
-    q_all = runner.quant_us()
-    q_timed = q_all[first_timed:]
-    quant_us = sum(q_timed) / len(q_timed)
+    quant_us = kt["quant"]
 
     elems = sum(B * c * h * w for c, (h, w) in zip(chans, SIZES))
     alg_bytes = 12 * elems                       # 2 reads of x + 1 write of y, fp32
@@ -618,15 +614,15 @@ def main():
     out = None
     if rank == 0:
         q_gbs = 8 * elems / (quant_us * 1e-6) / 1e9
+        seq = "hipExtLaunchKernel start/stop events of each launch, 20 single-batch steps in sequence on one stream " \
+              "(the --pipeline 1 context of profiles/*_kernel_stats_pipeline1.csv)"
         kern = {"quant": {"us": round(quant_us, 2), "alg_bytes": 8 * elems, "GB/s": round(q_gbs, 1),
-                          "frac": round(q_gbs / HBM_PEAK_GBS, 4),
-                          "timing": "HIP events around every pass-2 launch of the timed region (%d launches, "
-                                    "%d batches in flight)" % (len(q_timed), depth)}}
+                          "frac": round(q_gbs / HBM_PEAK_GBS, 4), "timing": seq}}
         gbs = 4 * elems / (kt["stats"] * 1e-6) / 1e9
         kern["stats"] = {"us": round(kt["stats"], 2), "alg_bytes": 4 * elems, "GB/s": round(gbs, 1),
-                         "frac": round(gbs / HBM_PEAK_GBS, 4), "timing": "isolated, %d back-to-back launches" % reps}
+                         "frac": round(gbs / HBM_PEAK_GBS, 4), "timing": seq}
         kern["morph_finalize"] = {"us": round(kt["morph_finalize"], 2), "bound": "latency (per-image chain)",
-                                  "timing": "isolated, %d back-to-back launches" % reps}
+                                  "timing": seq}
         out = {
             "metric": HOOK_METRIC,
             "value": round(value, 2),
@@ -645,7 +641,8 @@ def main():
                                    "quant/dequant; YOLOv8 network excluded (see e2e)" % (name, B, grid, mapper),
                        "global_batch": world * B, "grid_size": grid, "mapper": mapper,
                        "parallelism": "dp%d" % world, "hip_graph": use_graph,
-                       "batches_in_flight": depth, "latency_ms_single_batch": round(latency_ms, 4),
+                       "batches_in_flight": depth, "input_batches": len(plans),
+                       "latency_ms_single_batch": round(latency_ms, 4),
                        "host_enqueue_us_per_step": round(t_enq / args.steps * 1e6, 1)},
             # north star: the whole fused complexity + quant path,
             # 12 B per feature element over the wall time of a step
@@ -655,13 +652,11 @@ def main():
                                         "mcaq_quant, 12 B per feature element per step",
                               "alg_bytes_per_step": alg_bytes},
             # the dominant kernel (pass 2): algorithmic bytes per launch over its
-            # launch time, HIP events on its stream inside the timed region
+            # launch time (HIP events on its stream, single-batch steps in sequence)
             "roofline": {"bound": "hbm", "achieved": kern["quant"]["GB/s"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": kern["quant"]["frac"], "traffic": traffic_k.get("mcaq_quant_kernel"),
                          "kernel": "mcaq_quant_kernel (pass 2: read x + write y, 8 B per feature element)",
-                         "alg_bytes_per_launch": 8 * elems, "us_per_launch": kern["quant"]["us"],
-                         "us_per_launch_all_dispatches": round(sum(q_all) / len(q_all), 2),
-                         "dispatches": len(q_all)},
+                         "alg_bytes_per_launch": 8 * elems, "us_per_launch": kern["quant"]["us"]},
             "kernels": kern,
             "cpu_baseline": None,
         }

@@ -148,6 +148,12 @@ typedef struct {
 } mcaq_quant_scale;
 int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream);
 
+/* Measurement: the calling thread's NEXT mcaq_stats / mcaq_quant launch is
+ * issued through hipExtLaunchKernel with these start/stop events (either may
+ * be NULL), which the runtime stamps at that dispatch's own start and end -
+ * the interval a rocprofv3 kernel trace reports.  Not for graph capture. */
+int mcaq_time_next_launch(hipEvent_t start, hipEvent_t stop);
+
 /* ---- QAT quantizer (training branch) --------------------------------------
  * forward:  y = ((1-f) Q_lo(x) + f Q_hi(x)) * m, lo = floor(b), f = b - lo,
  *           Q_hi = Q_lo when lo = 8 (quantization.py:699-727, 733-737); b is

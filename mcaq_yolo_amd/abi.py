@@ -56,7 +56,7 @@ F_BIN_OTSU, F_NO_EULER = 256, 512
 EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats", "mcaq_stats_units",
            "mcaq_finalize", "mcaq_morph", "mcaq_morph_finalize", "mcaq_morph_scratch_bytes", "mcaq_quant",
            "mcaq_qat_forward", "mcaq_qat_backward", "mcaq_qat_work_floats", "mcaq_ema_stats",
-           "mcaq_nms", "mcaq_nms_work_floats")
+           "mcaq_nms", "mcaq_nms_work_floats", "mcaq_time_next_launch")
 
 _LIB = None
 
@@ -89,6 +89,8 @@ def _declare(lib):
     lib.mcaq_nms.argtypes = [P, I, I, I, I, Fl, ctypes.c_double, I, I, Fl, I, P, P, P, P]
     lib.mcaq_nms_work_floats.restype = ctypes.c_size_t
     lib.mcaq_nms_work_floats.argtypes = [I, I]
+    lib.mcaq_time_next_launch.restype = I
+    lib.mcaq_time_next_launch.argtypes = [P, P]
     return lib
 
 

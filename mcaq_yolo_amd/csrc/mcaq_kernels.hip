@@ -14,6 +14,7 @@
 //                                 (mcaq_qat.h)
 //
 // Built with -ffp-contract=off (see mcaq_math.h).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -199,7 +200,11 @@ __device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, fl
           // morphology of the other in-flight batches gains ~3 % per step
           // (profiles/r01_stats_ntl_ab/)
           typedef float f4v __attribute__((ext_vector_type(4)));
+#if defined(MCAQ_STATS_PLAIN_LOADS)
+          const f4v t = *reinterpret_cast<const f4v*>(row + qa);
+#else
           const f4v t = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(row + qa));
+#endif
           v[rr][i][0] = t.x; v[rr][i][1 % PPL] = t.y; v[rr][i][2 % PPL] = t.z; v[rr][i][3 % PPL] = t.w;
         } else if (kVec && PPL == 2) {
           const float2 t = *reinterpret_cast<const float2*>(row + qa);
@@ -645,7 +650,28 @@ __global__ __launch_bounds__(256) void mcaq_quant_kernel(QuantArgs a) {
 // ---------------------------------------------------------------------------
 // extern "C" launchers
 // ---------------------------------------------------------------------------
+// Kernel timing (mcaq_time_next_launch): the next pass-1 / pass-2 launch of
+// the calling thread goes through hipExtLaunchKernel with start/stop events,
+// which the runtime stamps at the dispatch's own start and end (the interval
+// a kernel trace reports), instead of event packets around it on the stream.
+static thread_local hipEvent_t t_ev_start = nullptr, t_ev_stop = nullptr;
+template <typename F, typename... Args>
+static void launch_k(F kernel, dim3 grid, dim3 block, size_t shmem, hipStream_t stream, Args... args) {
+  if (t_ev_start || t_ev_stop) {
+    hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)shmem, stream, t_ev_start, t_ev_stop, 0u, args...);
+    t_ev_start = t_ev_stop = nullptr;
+  } else {
+    hipLaunchKernelGGL(kernel, grid, block, shmem, stream, args...);
+  }
+}
+
 extern "C" {
+
+int mcaq_time_next_launch(hipEvent_t start, hipEvent_t stop) {
+  t_ev_start = start;
+  t_ev_stop = stop;
+  return 0;
+}
 
 int mcaq_abi_version(void) { return MCAQ_ABI_VERSION; }
 
@@ -682,9 +708,9 @@ int mcaq_stats(const mcaq_stats_scale* scales, int nscales, hipStream_t stream) 
   bool vec = true;
   for (int i = 0; i < nscales; ++i) vec = vec && ((uintptr_t)scales[i].x & 15) == 0;
   if (vec)
-    hipLaunchKernelGGL(mcaq_stats_kernel<true>, dim3(units), dim3(256), 0, stream, a);
+    launch_k(mcaq_stats_kernel<true>, dim3(units), dim3(256), 0, stream, a);
   else
-    hipLaunchKernelGGL(mcaq_stats_kernel<false>, dim3(units), dim3(256), 0, stream, a);
+    launch_k(mcaq_stats_kernel<false>, dim3(units), dim3(256), 0, stream, a);
   return (int)hipGetLastError();
 }
 
@@ -913,18 +939,18 @@ int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream) 
   for (int i = 0; i < nscales; ++i) mt_lds = mt_lds && (!scales[i].mt || scales[i].ht * scales[i].wt <= QMAXNT);
   const dim3 g(units), t(256);
   if (!mt_lds) {
-    if (vec) hipLaunchKernelGGL((mcaq_quant_kernel<true, false, true, false>), g, t, 0, stream, a);
-    else hipLaunchKernelGGL((mcaq_quant_kernel<false, false, false, false>), g, t, 0, stream, a);
+    if (vec) launch_k((mcaq_quant_kernel<true, false, true, false>), g, t, 0, stream, a);
+    else launch_k((mcaq_quant_kernel<false, false, false, false>), g, t, 0, stream, a);
   } else if (!vec)
-    hipLaunchKernelGGL((mcaq_quant_kernel<false, false, false, true>), g, t, 0, stream, a);
+    launch_k((mcaq_quant_kernel<false, false, false, true>), g, t, 0, stream, a);
   else if (nt == 3)
-    hipLaunchKernelGGL((mcaq_quant_kernel<true, true, true, true>), g, t, 0, stream, a);
+    launch_k((mcaq_quant_kernel<true, true, true, true>), g, t, 0, stream, a);
   else if (nt == 2)
-    hipLaunchKernelGGL((mcaq_quant_kernel<true, true, false, true>), g, t, 0, stream, a);
+    launch_k((mcaq_quant_kernel<true, true, false, true>), g, t, 0, stream, a);
   else if (nt == 1)
-    hipLaunchKernelGGL((mcaq_quant_kernel<true, false, true, true>), g, t, 0, stream, a);
+    launch_k((mcaq_quant_kernel<true, false, true, true>), g, t, 0, stream, a);
   else
-    hipLaunchKernelGGL((mcaq_quant_kernel<true, false, false, true>), g, t, 0, stream, a);
+    launch_k((mcaq_quant_kernel<true, false, false, true>), g, t, 0, stream, a);
   return (int)hipGetLastError();
 }
 
