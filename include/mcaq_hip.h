@@ -32,6 +32,7 @@
 
 #ifdef MCAQ_NO_HIP
 typedef void* hipStream_t;
+typedef void* hipEvent_t;
 #else
 #include <hip/hip_runtime_api.h>
 #endif

@@ -420,8 +420,16 @@ __global__ __launch_bounds__(256) void mcaq_finalize_kernel(FinalizeArgs a) {
 // morph pass B: one 256-thread workgroup per (scale, image), tile grid in LDS
 // ---------------------------------------------------------------------------
 constexpr int TILES_THREADS = 256;
-
-constexpr int MORPH_THREADS = 1024;
+#ifndef MCAQ_MORPH_THREADS
+#define MCAQ_MORPH_THREADS 1024
+#endif
+#ifndef MCAQ_MORPH_MINW     // min waves per SIMD of pass A: 4 -> <= 128 VGPRs
+#define MCAQ_MORPH_MINW 4
+#endif
+#ifndef MCAQ_TILES_MINW     // min waves per SIMD of pass B (register budget 512 / MINW)
+#define MCAQ_TILES_MINW 1
+#endif
+constexpr int MORPH_THREADS = MCAQ_MORPH_THREADS;
 
 __device__ __forceinline__ int morph_scale_of(const MorphArgs& a, int img) {
   int si = 0;
@@ -437,7 +445,7 @@ __device__ __forceinline__ int morph_scale_of(const MorphArgs& a, int img) {
 // scale's geometry only); a group past the batch end recomputes the last
 // image (identical values written twice) instead of idling at the barriers.
 template <bool kLDS>
-__global__ __launch_bounds__(MORPH_THREADS) void mcaq_morph_kernel(MorphArgs a, FinalizeArgs f) {
+__global__ __launch_bounds__(MORPH_THREADS, MCAQ_MORPH_MINW) void mcaq_morph_kernel(MorphArgs a, FinalizeArgs f) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nwg = a.wg_begin[a.nscales];
   if ((int)blockIdx.x >= nwg) {   // channel min/max workgroups ride along
@@ -473,7 +481,7 @@ __global__ __launch_bounds__(MORPH_THREADS) void mcaq_morph_kernel(MorphArgs a, 
 // pass B: image group g of a workgroup owns threads [g*G, (g+1)*G) and its own
 // LDS tile arrays; the staged weights are shared by the workgroup.  A group
 // past the batch end recomputes the last image (identical values written twice).
-__global__ __launch_bounds__(TILES_THREADS) void mcaq_tiles_kernel(MorphArgs a, int wlds) {
+__global__ __launch_bounds__(TILES_THREADS, MCAQ_TILES_MINW) void mcaq_tiles_kernel(MorphArgs a, int wlds) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __builtin_amdgcn_s_setprio(2);
   int si = 0;
