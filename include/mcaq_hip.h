@@ -154,6 +154,9 @@ int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream);
  * be NULL), which the runtime stamps at that dispatch's own start and end -
  * the interval a rocprofv3 kernel trace reports.  Not for graph capture. */
 int mcaq_time_next_launch(hipEvent_t start, hipEvent_t stop);
+/* the same for the launch after `skip` others of this thread (pass 1, pass 2,
+ * the QAT kernels: e.g. skip = 1 times the fold launch of mcaq_qat_backward) */
+int mcaq_time_launch(int skip, hipEvent_t start, hipEvent_t stop);
 
 /* ---- QAT quantizer (training branch) --------------------------------------
  * forward:  y = ((1-f) Q_lo(x) + f Q_hi(x)) * m, lo = floor(b), f = b - lo,

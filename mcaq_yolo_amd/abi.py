@@ -51,12 +51,12 @@ class QatScale(ctypes.Structure):
 # morph stage flags (mcaq_morph.h)
 F_PHI, F_CMLP, F_MAPPER, F_SOFTMASK = 1, 2, 4, 8
 F_CONT, F_HAS_T, F_NORM_C, F_MAP_LINEAR = 16, 32, 64, 128
-F_BIN_OTSU, F_NO_EULER = 256, 512
+F_BIN_OTSU, F_NO_EULER, F_CANNY_LEGACY = 256, 512, 1024
 
 EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats", "mcaq_stats_units",
            "mcaq_finalize", "mcaq_morph", "mcaq_morph_finalize", "mcaq_morph_scratch_bytes", "mcaq_quant",
            "mcaq_qat_forward", "mcaq_qat_backward", "mcaq_qat_work_floats", "mcaq_ema_stats",
-           "mcaq_nms", "mcaq_nms_work_floats", "mcaq_time_next_launch")
+           "mcaq_nms", "mcaq_nms_work_floats", "mcaq_time_next_launch", "mcaq_time_launch")
 
 _LIB = None
 
@@ -91,6 +91,8 @@ def _declare(lib):
     lib.mcaq_nms_work_floats.argtypes = [I, I]
     lib.mcaq_time_next_launch.restype = I
     lib.mcaq_time_next_launch.argtypes = [P, P]
+    lib.mcaq_time_launch.restype = I
+    lib.mcaq_time_launch.argtypes = [I, P, P]
     return lib
 
 

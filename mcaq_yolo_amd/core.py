@@ -272,6 +272,8 @@ class MorphologicalComplexityAnalyzer(nn.Module):
             f |= abi.F_BIN_OTSU
         if not self.contour_components:
             f |= abi.F_NO_EULER
+        if self.canny_impl == "legacy":
+            f |= abi.F_CANNY_LEGACY
         return f
 
     def cmlp_blob(self):
@@ -280,8 +282,6 @@ class MorphologicalComplexityAnalyzer(nn.Module):
 
     def _run(self, features, want_c):
         _need_cuda(features, "features")
-        if self.canny_impl == "legacy":
-            raise NotImplementedError("canny_impl='legacy' runs on the pure-PyTorch path (CPU tensors) only")
         if features.dim() != 4:
             raise ValueError("features must be (B, C, H, W)")
         x = features.float().contiguous()

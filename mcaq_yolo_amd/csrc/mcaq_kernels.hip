@@ -663,9 +663,10 @@ __global__ __launch_bounds__(256) void mcaq_quant_kernel(QuantArgs a) {
 // which the runtime stamps at the dispatch's own start and end (the interval
 // a kernel trace reports), instead of event packets around it on the stream.
 static thread_local hipEvent_t t_ev_start = nullptr, t_ev_stop = nullptr;
+static thread_local int t_ev_skip = 0;
 template <typename F, typename... Args>
 static void launch_k(F kernel, dim3 grid, dim3 block, size_t shmem, hipStream_t stream, Args... args) {
-  if (t_ev_start || t_ev_stop) {
+  if ((t_ev_start || t_ev_stop) && t_ev_skip-- == 0) {
     hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)shmem, stream, t_ev_start, t_ev_stop, 0u, args...);
     t_ev_start = t_ev_stop = nullptr;
   } else {
@@ -676,8 +677,14 @@ static void launch_k(F kernel, dim3 grid, dim3 block, size_t shmem, hipStream_t 
 extern "C" {
 
 int mcaq_time_next_launch(hipEvent_t start, hipEvent_t stop) {
+  return mcaq_time_launch(0, start, stop);
+}
+
+int mcaq_time_launch(int skip, hipEvent_t start, hipEvent_t stop) {
+  if (skip < 0) return (int)hipErrorInvalidValue;
   t_ev_start = start;
   t_ev_stop = stop;
+  t_ev_skip = skip;
   return 0;
 }
 

@@ -57,6 +57,7 @@ enum : int {
   F_MAP_LINEAR = 128, // LinearBitMapper instead of the MLP
   F_BIN_OTSU = 256,   // binarize_impl='otsu'
   F_NO_EULER = 512,   // contour_components=False
+  F_CANNY_LEGACY = 1024,  // canny_impl='legacy'
 };
 
 using MorphScale = mcaq_morph_scale;  // include/mcaq_hip.h
@@ -697,6 +698,9 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, P
     // gradient planes.  Each reduces its planes to per-tile partial
     // quantities (tile_tmp); pass B assembles phi from both.
     if (role == 0) {
+    // canny_impl='legacy' (morphology.py:512-540): Sobel of the blur itself,
+    // L2 magnitude, Otsu of the min-max normalised NMS map, 2 hysteresis rounds
+    const bool legacy = (S.flags & F_CANNY_LEGACY) != 0;
     // -- 5x5 Gaussian blur (zero pad; an out-of-image tap adds fma(w, 0, acc) == acc
     //    because acc >= +0), fused with the Otsu histogram of the result.
     //    Column strips of SR rows per thread: consecutive threads own consecutive
@@ -729,16 +733,17 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, P
             for (int j = 0; j < 5; ++j) acc = fmaf(bits_as_float(k_gauss5_bits[i * 5 + j]), v[r + i][j], acc);
           if (r0 + r < Hc) {
             pl.A[(r0 + r) * Wc + w] = acc;
-            otsu_hist_add(sh, acc);
+            if (!legacy) otsu_hist_add(sh, acc);
           }
         }
       }
     }
     MSYNC();
     MSTAMP(2);
-    const float thr = otsu_from_hist(ctx, sh);
+    const float thr = legacy ? 0.0f : otsu_from_hist(ctx, sh);
     const float thr255 = thr * 255.0f;
     const float lo255 = 0.5f * thr255;
+    const float gsc = legacy ? 1.0f : 255.0f;    // x * 1.0f == x
     MSTAMP(3);
 
     // -- Sobel of 255*blur (zero pad), L1 magnitude -> Bf, direction -> dir.
@@ -757,7 +762,7 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, P
 #pragma unroll
           for (int j = 0; j < 3; ++j) {
             const int ww = w + j - 1;
-            const float x = row[imin_(imax_(ww, 0), Wc - 1)] * 255.0f;
+            const float x = row[imin_(imax_(ww, 0), Wc - 1)] * gsc;
             v[t][j] = (rv && ww >= 0 && ww < Wc) ? x : 0.0f;
           }
         }
@@ -778,7 +783,7 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, P
           }
           if (r0 + r < Hc) {
             const int p = (r0 + r) * Wc + w;
-            pl.Bf[p] = fabsf(gx) + fabsf(gy);
+            pl.Bf[p] = legacy ? sqrtf((gx * gx + gy * gy) + 1e-12f) : fabsf(gx) + fabsf(gy);
             pl.dir[p] = (uint8_t)nms_dir(gx, gy);
           }
         }
@@ -792,6 +797,7 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, P
     uint32_t* E0 = pl.bits(BP_E0);
     uint32_t* E1 = pl.bits(BP_E1);
     uint32_t* WK = pl.bits(BP_WK);
+    float lmn = 3.402823466e38f, lmx = -3.402823466e38f;   // legacy: NMS map range
     {
       const int nsr = (Hc + SR - 1) / SR;
       MFOR2(st, sl, nsr, RS) {
@@ -821,17 +827,45 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, P
           if (r0 + r >= Hc) continue;
           const bool keep = (m[r] >= n1[r]) && (m[r] >= n2[r]);
           const float nms = keep ? m[r] : 0.0f;
-          put_bits(E0, (r0 + r) * WPR + k, bit, w < Wc && nms > thr255);
-          put_bits(WK, (r0 + r) * WPR + k, bit, w < Wc && nms > lo255);
+          if (legacy) {
+            if (w < Wc) {
+              pl.A[(r0 + r) * Wc + w] = nms;     // the blur plane is free after Sobel
+              lmn = fmin_(lmn, nms); lmx = fmax_(lmx, nms);
+            }
+          } else {
+            put_bits(E0, (r0 + r) * WPR + k, bit, w < Wc && nms > thr255);
+            put_bits(WK, (r0 + r) * WPR + k, bit, w < Wc && nms > lo255);
+          }
         }
       }
     }
     MSYNC();
+    if (legacy) {
+      // normalise01 of the NMS map, its Otsu threshold t, strong > t, weak > t/2
+      float mn, mx;
+      block_minmax(ctx, sh, lmn, lmx, mn, mx);
+      const float den = (mx - mn) + 1e-8f;
+      MFOR(p, P) {
+        const float v = (pl.A[p] - mn) / den;
+        pl.A[p] = v;
+        otsu_hist_add(sh, v);
+      }
+      MSYNC();
+      const float t = otsu_from_hist(ctx, sh);
+      const float tl = 0.5f * t;
+      MFOR2(h, sl, Hc, RS) {
+        const int k = sl >> 5, bit = sl & 31;
+        const float v = pl.A[h * Wc + imin_(sl, Wc - 1)];
+        put_bits(E0, h * WPR + k, bit, sl < Wc && v > t);
+        put_bits(WK, h * WPR + k, bit, sl < Wc && v > tl);
+      }
+      MSYNC();
+    }
     MSTAMP(5);
     // -- hysteresis on words: e' = e | (weak & dilate3x3(e)), Jacobi, early exit
     uint32_t* src = E0;
     uint32_t* dst = E1;
-    const int iters = S.hyst_iters < 1 ? 1 : S.hyst_iters;
+    const int iters = legacy ? 2 : (S.hyst_iters < 1 ? 1 : S.hyst_iters);
 #if defined(__HIP_DEVICE_COMPILE__)
     if (Hc <= 128 && WPR <= 4) {
       // one wave, planes in registers (lane l: rows 2l, 2l+1), neighbour rows by

@@ -26,19 +26,25 @@ struct QatArgs {
   int units_total;
 };
 
+#ifndef MCAQ_QAT_MINW
+#define MCAQ_QAT_MINW 4
+#endif
 constexpr int QAT_LO = 1;   // table widths QAT_LO .. 8 (the reference's bc_int <= 8)
 constexpr int QAT_NB = 8;
 
 // unit = 256 pixels x 32 channels of one image (the pass-2 layout): lane l of
-// wave w owns pixels 4l..4l+3 and channels 8w..8w+7 of the slice.
+// wave w owns pixels 4l..4l+3 and channels 8w..8w+7 of the slice (channel
+// loop fully unrolled: the compiler schedules the loads; issuing all of them
+// ahead of the table/barrier, or streaming two channels at a time under an
+// 8-workgroup/CU register cap, measured slower at config 5).
 template <bool kBwd, bool kVec>
-__global__ __launch_bounds__(256) void mcaq_qat_kernel(QatArgs a) {
+__global__ __launch_bounds__(256, MCAQ_QAT_MINW) void mcaq_qat_kernel(QatArgs a) {
   __shared__ float2 qt[32 * QAT_NB];
   __shared__ float red[2][4][256];
   const int unit = blockIdx.x;
   int si = 0;
   while (si + 1 < a.nscales && unit >= a.s[si + 1].unit_begin) ++si;
-  const mcaq_qat_scale& S = a.s[si];
+  const mcaq_qat_scale S = si == 0 ? a.s[0] : si == 1 ? a.s[1] : a.s[2];   // by value: no indexed kernarg copy
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int HW = S.H * S.W;
   const int upi = (HW + 255) / 256;
@@ -57,7 +63,7 @@ __global__ __launch_bounds__(256) void mcaq_qat_kernel(QatArgs a) {
   const int q0 = chunk * 256 + lane * 4;
   bool pv[4];
   int kl[4], kh[4];
-  float fu[4], omf[4], mv[4], lmin[4], lmax[4], hmin[4], hmax[4];
+  float fu[4], omf[4], mv[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int p = imin_(q0 + k, HW - 1);
@@ -68,11 +74,8 @@ __global__ __launch_bounds__(256) void mcaq_qat_kernel(QatArgs a) {
     fu[k] = bv - fl;                 // exact (Sterbenz) for b >= 1
     omf[k] = 1.0f - fu[k];
     const int lo = imin_(imax_((int)fl, QAT_LO), QAT_LO + QAT_NB - 1);
-    const int hi = lo < 8 ? lo + 1 : lo;    // Q_hi := Q_lo past 8 bits (frac is 0 there)
     kl[k] = lo - QAT_LO;
-    kh[k] = hi - QAT_LO;
-    lmin[k] = (float)(-(1 << (lo - 1))); lmax[k] = (float)((1 << (lo - 1)) - 1);
-    hmin[k] = (float)(-(1 << (hi - 1))); hmax[k] = (float)((1 << (hi - 1)) - 1);
+    kh[k] = (lo < 8 ? lo + 1 : lo) - QAT_LO;    // Q_hi := Q_lo past 8 bits (frac is 0 there)
     mv[k] = S.m ? S.m[(size_t)b * HW + p] : 1.0f;
   }
   const bool has_m = S.m != nullptr;
@@ -81,46 +84,46 @@ __global__ __launch_bounds__(256) void mcaq_qat_kernel(QatArgs a) {
   const size_t rowbase = ((size_t)b * S.C + c0 + imax_(0, imin_(cw, nc - 1))) * HW;
   const float* xb = S.x + rowbase;
   const int qa = pv[0] ? q0 : 0;
-  float v[8][4], gv[8][4];
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const size_t ro = (size_t)(c < ncw ? c : 0) * HW;
-    if (kVec) {
-      const float4 t = *reinterpret_cast<const float4*>(xb + ro + qa);
-      v[c][0] = t.x; v[c][1] = t.y; v[c][2] = t.z; v[c][3] = t.w;
-      if (kBwd) {
-        const float4 u = *reinterpret_cast<const float4*>(S.g + rowbase + ro + qa);
-        gv[c][0] = u.x; gv[c][1] = u.y; gv[c][2] = u.z; gv[c][3] = u.w;
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const size_t o = ro + imin_(q0 + k, HW - 1);
-        v[c][k] = xb[o];
-        if (kBwd) gv[c][k] = S.g[rowbase + o];
-      }
-    }
-  }
   __syncthreads();   // qt ready
   float sgm[4] = {0.f, 0.f, 0.f, 0.f}, sgf[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
     if (c >= ncw) break;
+    const size_t ro = (size_t)c * HW;
+    float v[4], gv[4];
+    if (kVec) {
+      const float4 t = *reinterpret_cast<const float4*>(xb + ro + qa);
+      v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+      if (kBwd) {
+        const float4 u = *reinterpret_cast<const float4*>(S.g + rowbase + ro + qa);
+        gv[0] = u.x; gv[1] = u.y; gv[2] = u.z; gv[3] = u.w;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const size_t o = ro + imin_(q0 + k, HW - 1);
+        v[k] = xb[o];
+        if (kBwd) gv[k] = S.g[rowbase + o];
+      }
+    }
     float o[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const float2 zl = qt[(cw + c) * QAT_NB + kl[k]];
       const float2 zh = qt[(cw + c) * QAT_NB + kh[k]];
+      const int lo = kl[k] + QAT_LO, hi = kh[k] + QAT_LO;
       QParam L, Hq;
-      L.scale = zl.x; L.zp = zl.y; L.qmin = lmin[k]; L.qmax = lmax[k];
-      Hq.scale = zh.x; Hq.zp = zh.y; Hq.qmin = hmin[k]; Hq.qmax = hmax[k];
-      const float ql = quant_dequant(v[c][k], L);
-      const float qh = quant_dequant(v[c][k], Hq);
+      L.scale = zl.x; L.zp = zl.y;
+      L.qmin = (float)(-(1 << (lo - 1))); L.qmax = (float)((1 << (lo - 1)) - 1);
+      Hq.scale = zh.x; Hq.zp = zh.y;
+      Hq.qmin = (float)(-(1 << (hi - 1))); Hq.qmax = (float)((1 << (hi - 1)) - 1);
+      const float ql = quant_dequant(v[k], L);
+      const float qh = quant_dequant(v[k], Hq);
       const float xq = omf[k] * ql + fu[k] * qh;      // two rounded products, one rounded add
       if (!kBwd) {
         o[k] = has_m ? xq * mv[k] : xq;
       } else {
-        const float g = gv[c][k];
+        const float g = gv[k];
         const float gm = has_m ? g * mv[k] : g;
         o[k] = gm * omf[k] + gm * fu[k];
         sgm[k] += g * xq;
@@ -129,7 +132,13 @@ __global__ __launch_bounds__(256) void mcaq_qat_kernel(QatArgs a) {
     }
     float* orow = (kBwd ? S.gx : S.y) + rowbase + (size_t)c * HW;
     if (kVec) {
-      if (pv[0]) *reinterpret_cast<float4*>(orow + q0) = make_float4(o[0], o[1], o[2], o[3]);
+      typedef float f4v __attribute__((ext_vector_type(4)));
+      const f4v ov = {o[0], o[1], o[2], o[3]};
+#ifdef MCAQ_QAT_PLAIN_STORES
+      if (pv[0]) *reinterpret_cast<f4v*>(orow + q0) = ov;
+#else
+      if (pv[0]) __builtin_nontemporal_store(ov, reinterpret_cast<f4v*>(orow + q0));   // written once, streamed
+#endif
     } else {
 #pragma unroll
       for (int k = 0; k < 4; ++k) if (pv[k]) orow[q0 + k] = o[k];
@@ -152,63 +161,115 @@ __global__ __launch_bounds__(256) void mcaq_qat_kernel(QatArgs a) {
 }
 
 // one workgroup per (scale, image, tile row): the band of pixel rows whose
-// nearest tile row is th, in chunks of <= QAT_FOLD_LDS floats: per pixel the
-// slice partials are summed (slices in order) -> grad_m and an LDS row chunk;
-// thread tw < wt then adds its tile's pixels of the chunk row-major.
-constexpr int QAT_FOLD_LDS = 8192;
+// nearest tile row is th (binary search: nearest_src is monotone).  The
+// per-slice channel partials of the backward kernel are summed per pixel,
+// slices in order, the slice loads of a pixel issued together -> grad_m and
+// an LDS chunk of the band; each pixel column is summed over the band's rows,
+// then each tile over its columns (short dependent chains: rows + columns,
+// not rows x columns).  fp32 sums in a different order than the reference's
+// upsample backward: grad_bits is checked to a tolerance.
+#ifndef MCAQ_FOLD_LDS
+#define MCAQ_FOLD_LDS 8192
+#endif
+constexpr int QAT_FOLD_LDS = MCAQ_FOLD_LDS;    // floats of pixel chunk
+constexpr int QAT_FOLD_SL = 8;        // slices loaded together
+
+// first index i in [0, n) with nearest_src(i, in, n) >= v (n if none)
+__device__ __forceinline__ int band_start(int v, int in, int n) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (nearest_src(mid, in, n) >= v) hi = mid; else lo = mid + 1;
+  }
+  return lo;
+}
+
+constexpr int QAT_FOLD_PX = 4;        // pixels per thread per round
+
+// per thread: pixels i0 + 256 j (j < QAT_FOLD_PX, i < np) of the chunk at p0;
+// all slice loads of a round issued before the first add, slices summed in order
+__device__ __forceinline__ void slice_sums(const float* pm, const float* pf, size_t plane, int nsl, int p0,
+                                           int i0, int np, float (&am)[QAT_FOLD_PX], float (&af)[QAT_FOLD_PX]) {
+  for (int s0 = 0; s0 < nsl; s0 += QAT_FOLD_SL) {
+    float vm[QAT_FOLD_PX][QAT_FOLD_SL], vf[QAT_FOLD_PX][QAT_FOLD_SL];
+#pragma unroll
+    for (int j = 0; j < QAT_FOLD_PX; ++j) {
+      const int p = p0 + imin_(i0 + 256 * j, np - 1);
+#pragma unroll
+      for (int k = 0; k < QAT_FOLD_SL; ++k) {
+        const size_t o = (size_t)imin_(s0 + k, nsl - 1) * plane + p;
+        vm[j][k] = pm[o];
+        vf[j][k] = pf[o];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < QAT_FOLD_PX; ++j)
+#pragma unroll
+      for (int k = 0; k < QAT_FOLD_SL; ++k)
+        if (s0 + k < nsl) {
+          am[j] = (s0 + k == 0) ? vm[j][k] : am[j] + vm[j][k];
+          af[j] = (s0 + k == 0) ? vf[j][k] : af[j] + vf[j][k];
+        }
+  }
+}
 
 __global__ __launch_bounds__(256) void mcaq_qat_fold_kernel(QatArgs a) {
   __shared__ float pl[QAT_FOLD_LDS];
-  __shared__ int band[2];
+  __shared__ float col[QAT_FOLD_LDS];
   const int blk = blockIdx.x;
   int si = 0;
   while (si + 1 < a.nscales && blk >= a.s[si + 1].block_begin) ++si;
-  const mcaq_qat_scale& S = a.s[si];
+  const mcaq_qat_scale S = si == 0 ? a.s[0] : si == 1 ? a.s[1] : a.s[2];
   const int lb = blk - S.block_begin;
   const int b = lb / S.ht, th = lb - (lb / S.ht) * S.ht;
-  const int HW = S.H * S.W;
+  const int H = S.H, W = S.W, HW = H * W, wt = S.wt;
   const int nsl = (S.C + 31) / 32;
   const size_t plane = (size_t)S.B * HW;
   const float* pm = S.work + (size_t)b * HW;
   const float* pf = S.work + (size_t)nsl * plane + (size_t)b * HW;
-  if (threadIdx.x == 0) {
-    int rs = S.H, re = 0;
-    for (int h = 0; h < S.H; ++h)
-      if (nearest_src(h, S.ht, S.H) == th) { rs = imin_(rs, h); re = imax_(re, h + 1); }
-    band[0] = rs; band[1] = re;
-  }
-  __syncthreads();
-  const int rs = band[0], re = band[1];
-  int cs = 0, ce = 0;
-  const int tw = threadIdx.x;
-  if (tw < S.wt) {
-    cs = S.W;
-    for (int w = 0; w < S.W; ++w)
-      if (nearest_src(w, S.wt, S.W) == tw) { cs = imin_(cs, w); ce = imax_(ce, w + 1); }
-  }
-  const int rows_per_chunk = imax_(1, QAT_FOLD_LDS / S.W);
-  float acc = 0.0f;
+  const int rs = band_start(th, S.ht, H), re = band_start(th + 1, S.ht, H);
+  const int rows_per_chunk = imax_(1, QAT_FOLD_LDS / W);
+#if defined(MCAQ_FOLD_EXP) && MCAQ_FOLD_EXP == 1
+  if (threadIdx.x < 1) S.gb[((size_t)b * S.ht + th) * wt] = (float)(re - rs);
+  return;
+#endif
+  for (int w = threadIdx.x; w < W; w += 256) col[w] = 0.0f;
   for (int r0 = rs; r0 < re; r0 += rows_per_chunk) {
     const int r1 = imin_(re, r0 + rows_per_chunk);
-    const int p0 = r0 * S.W, np = (r1 - r0) * S.W;
-    for (int i = threadIdx.x; i < np; i += 256) {
-      const int p = p0 + i;
-      if (S.gm) {
-        float t = pm[p];
-        for (int s = 1; s < nsl; ++s) t += pm[(size_t)s * plane + p];
-        S.gm[(size_t)b * HW + p] = t;
+    const int p0 = r0 * W, np = (r1 - r0) * W;
+    for (int i0 = threadIdx.x; i0 < np; i0 += 256 * QAT_FOLD_PX) {
+      float am[QAT_FOLD_PX], af[QAT_FOLD_PX];
+      slice_sums(pm, pf, plane, nsl, p0, i0, np, am, af);
+#pragma unroll
+      for (int j = 0; j < QAT_FOLD_PX; ++j) {
+        const int i = i0 + 256 * j;
+        if (i < np) {
+          if (S.gm) S.gm[(size_t)b * HW + p0 + i] = am[j];
+          pl[i] = af[j];
+        }
       }
-      float v = pf[p];
-      for (int s = 1; s < nsl; ++s) v += pf[(size_t)s * plane + p];
-      pl[i] = v;
     }
     __syncthreads();
-    if (tw < S.wt)
-      for (int r = 0; r < r1 - r0; ++r)
-        for (int w = cs; w < ce; ++w) acc += pl[r * S.W + w];
+    // per pixel column: the band's rows of this chunk, in order
+    if (S.gb)
+      for (int w = threadIdx.x; w < W; w += 256) {
+        float t = col[w];
+        for (int r = 0; r < r1 - r0; ++r) t += pl[r * W + w];
+        col[w] = t;
+      }
     __syncthreads();
   }
-  if (S.gb && tw < S.wt) S.gb[((size_t)b * S.ht + th) * S.wt + tw] = acc;
+  if (!S.gb) return;
+#if defined(MCAQ_FOLD_EXP) && MCAQ_FOLD_EXP == 2
+  return;
+#endif
+  // tile tw: its columns, in order
+  for (int tw = threadIdx.x; tw < wt; tw += 256) {
+    const int cs = band_start(tw, wt, W), ce = band_start(tw + 1, wt, W);
+    float t = 0.0f;
+    for (int w = cs; w < ce; ++w) t += col[w];
+    S.gb[((size_t)b * S.ht + th) * wt + tw] = t;
+  }
 }
 
 // running <- a * running + c * batch (first batch: running <- batch),
@@ -250,7 +311,7 @@ static int qat_args(const mcaq_qat_scale* scales, int nscales, bool bwd, mcaq::Q
   for (int i = 0; i < nscales; ++i) {
     const mcaq_qat_scale& s = scales[i];
     if (s.B < 1 || s.C < 1 || s.H < 1 || s.W < 1 || s.ht < 1 || s.wt < 1 || s.ht > s.H || s.wt > s.W ||
-        s.wt > 256 || s.W > QAT_FOLD_LDS ||
+        s.W > QAT_FOLD_LDS ||
         !s.x || !s.bits || !s.xmin || !s.xmax)
       return (int)hipErrorInvalidValue;
     if (bwd ? (!s.g || !s.gx || !s.work) : !s.y) return (int)hipErrorInvalidValue;
@@ -258,7 +319,7 @@ static int qat_args(const mcaq_qat_scale* scales, int nscales, bool bwd, mcaq::Q
     a.s[i].unit_begin = units;
     a.s[i].block_begin = blocks;
     units += s.B * ((s.H * s.W + 255) / 256) * ((s.C + 31) / 32);
-    blocks += s.B * s.ht;
+    blocks += s.B * s.ht;          // fold: one workgroup per (image, tile row)
   }
   a.nscales = nscales;
   a.units_total = units;
@@ -274,9 +335,9 @@ int mcaq_qat_forward(const mcaq_qat_scale* scales, int nscales, hipStream_t stre
   for (int i = 0; i < nscales; ++i)
     vec = vec && ((scales[i].H * scales[i].W) & 3) == 0 && mcaq::qat_aligned16(scales[i], false);
   if (vec)
-    hipLaunchKernelGGL((mcaq::mcaq_qat_kernel<false, true>), dim3(a.units_total), dim3(256), 0, stream, a);
+    launch_k((mcaq::mcaq_qat_kernel<false, true>), dim3(a.units_total), dim3(256), 0, stream, a);
   else
-    hipLaunchKernelGGL((mcaq::mcaq_qat_kernel<false, false>), dim3(a.units_total), dim3(256), 0, stream, a);
+    launch_k((mcaq::mcaq_qat_kernel<false, false>), dim3(a.units_total), dim3(256), 0, stream, a);
   return (int)hipGetLastError();
 }
 
@@ -289,14 +350,17 @@ int mcaq_qat_backward(const mcaq_qat_scale* scales, int nscales, hipStream_t str
   for (int i = 0; i < nscales; ++i)
     vec = vec && ((scales[i].H * scales[i].W) & 3) == 0 && mcaq::qat_aligned16(scales[i], true);
   if (vec)
-    hipLaunchKernelGGL((mcaq::mcaq_qat_kernel<true, true>), dim3(a.units_total), dim3(256), 0, stream, a);
+    launch_k((mcaq::mcaq_qat_kernel<true, true>), dim3(a.units_total), dim3(256), 0, stream, a);
   else
-    hipLaunchKernelGGL((mcaq::mcaq_qat_kernel<true, false>), dim3(a.units_total), dim3(256), 0, stream, a);
+    launch_k((mcaq::mcaq_qat_kernel<true, false>), dim3(a.units_total), dim3(256), 0, stream, a);
   hipError_t le = hipGetLastError();
   if (le != hipSuccess) return (int)le;
   bool fold = false;
   for (int i = 0; i < nscales; ++i) fold = fold || scales[i].gm || scales[i].gb;
-  if (fold) hipLaunchKernelGGL(mcaq::mcaq_qat_fold_kernel, dim3(blocks), dim3(256), 0, stream, a);
+  if (fold) launch_k(mcaq::mcaq_qat_fold_kernel, dim3(blocks), dim3(256), 0, stream, a);
+#ifdef MCAQ_FOLD_TWICE
+  if (fold) launch_k(mcaq::mcaq_qat_fold_kernel, dim3(blocks), dim3(256), 0, stream, a);
+#endif
   return (int)hipGetLastError();
 }
 

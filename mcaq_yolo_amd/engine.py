@@ -114,7 +114,7 @@ class HookPlan:
 
     def prepare(self, feats, cmlp, mapper, smasks, temperature=1.0, mapper_kind="mlp", continuous=False,
                 normalize=False, minmax=None, batch_offset=0, batch_total=None, binarize_otsu=False,
-                contour_components=True, min_bits=2.0, max_bits=8.0, quantize=True, hysteresis_iters=8):
+                contour_components=True, canny_legacy=False, min_bits=2.0, max_bits=8.0, quantize=True, hysteresis_iters=8):
         """Validate inputs and build the launch descriptors (pointers are baked
         in: the tensors must stay alive and in place until the last launch).
         minmax: optional per-scale (xmin, xmax) frozen calibration stats."""
@@ -174,6 +174,8 @@ class HookPlan:
             flags |= abi.F_BIN_OTSU
         if not contour_components:
             flags |= abi.F_NO_EULER
+        if canny_legacy:
+            flags |= abi.F_CANNY_LEGACY
         T = max(float(temperature if temperature is not None else 1.0), 0.1)
         for i, (g, b) in enumerate(zip(self.geoms, self.bufs)):
             s = mo[i]

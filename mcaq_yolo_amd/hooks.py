@@ -153,7 +153,7 @@ class MCAQHooks(nn.Module):
         plan.run([x], an.cmlp_blob(), mapper_blob, [sm], temperature=state.get("temperature", 1.0),
                  mapper_kind=self.bit_mapping, normalize=self.normalize_complexity, minmax=minmax,
                  binarize_otsu=an.binarize_impl == "otsu", contour_components=an.contour_components,
-                 min_bits=self.bit_mapper.min_bits, max_bits=self.bit_mapper.max_bits, quantize=quantize,
+                 canny_legacy=an.canny_impl == "legacy", min_bits=self.bit_mapper.min_bits, max_bits=self.bit_mapper.max_bits, quantize=quantize,
                  process_group=self.process_group if minmax is None else None,
                  batch_offset=self.batch_offset, batch_total=self.batch_total)
         feat_q = b["y"] if quantize else feat

@@ -9,7 +9,7 @@ import sys
 import numpy as np
 import pytest
 
-from conftest import ROOT, case_names, load_case, load_weights
+from conftest import GOLDEN, ROOT, case_names, load_case, load_weights
 from oracle import mcaq_oracle as O
 
 sys.path.insert(0, os.path.join(ROOT, "tests", "emu"))
@@ -150,3 +150,29 @@ def test_emu_adaptive_threshold_near_ties(emu):
     assert near >= len(targets) // 2, "construction must land inside the margin"
     out = run_emu(emu, x, 8, abi.F_PHI)
     assert np.array_equal(out["bin"], O.adaptive_binarize(gray))
+
+
+OPT_CASES = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.startswith("opt_") and f.endswith(".npz"))
+
+
+@pytest.mark.parametrize("name", OPT_CASES)
+def test_emu_analyzer_switches_vs_reference(emu, name):
+    """canny_impl='legacy', binarize_impl='otsu', contour_components=False
+    through the kernel source against the reference's own outputs
+    (tests/golden/make_golden_r02.py) and the oracle."""
+    d = np.load(os.path.join(GOLDEN, name + ".npz"))
+    opts = {k[4:]: (str(d[k]) if d[k].dtype.kind == "U" else d[k].item()) for k in d.files if k.startswith("opt_")}
+    x = d["x"].astype(f32)
+    grid = int(d["grid"])
+    flags = ALL | (abi.F_BIN_OTSU if opts.get("binarize_impl") == "otsu" else 0) | \
+        (0 if opts.get("contour_components", True) else abi.F_NO_EULER) | \
+        (abi.F_CANNY_LEGACY if opts.get("canny_impl") == "legacy" else 0)
+    out = run_emu(emu, x, grid, flags)
+    assert np.array_equal(out["edge"], d["edge"])
+    assert np.array_equal(out["bin"], d["binmask"])
+    assert np.array_equal(out["phi"][..., :7], d["phi"][..., :7])
+    assert np.array_equal(out["bits"], d["bits_mlp"])
+    ref = O.hook_forward(x, emu[1], grid, **opts)
+    assert np.array_equal(out["phi"], ref["phi"])
+    assert np.array_equal(out["c"], ref["complexity"])
+    assert np.array_equal(out["m"], ref["m"])

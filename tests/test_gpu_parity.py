@@ -243,13 +243,12 @@ def test_packed_workgroups_vs_oracle(dev, blobs, shape):
     check_against_oracle(out, x, blobs[0], 8, "mlp")
 
 
-OPT_GPU = sorted(f[:-4] for f in os.listdir(GOLDEN)
-                 if f.startswith("opt_") and f.endswith(".npz") and not f.startswith("opt_legacy"))
+OPT_GPU = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.startswith("opt_") and f.endswith(".npz"))
 
 
 @pytest.mark.parametrize("name", OPT_GPU)
 def test_analyzer_switches_vs_reference(dev, blobs, name):
-    """binarize_impl='otsu' and contour_components=False on the morph kernel
+    """binarize_impl='otsu', contour_components=False and canny_impl='legacy' on the morph kernel
     against the reference's own outputs (tests/golden/make_golden_r02.py) and
     the oracle: edge, mask, phi1..7 and bits bit-exact, phi8 within 1 ulp of
     the reference (bit-exact vs the oracle)."""
@@ -258,7 +257,8 @@ def test_analyzer_switches_vs_reference(dev, blobs, name):
     x = d["x"].astype(f32)
     grid = int(d["grid"])
     out = run_plan(dev, blobs, [x], grid, "mlp", binarize_otsu=opts.get("binarize_impl") == "otsu",
-                   contour_components=opts.get("contour_components", True))[0]
+                   contour_components=opts.get("contour_components", True),
+                   canny_legacy=opts.get("canny_impl") == "legacy")[0]
     assert np.array_equal(out["edge"], d["edge"])
     assert np.array_equal(out["binmask"], d["binmask"])
     assert np.array_equal(out["phi"][..., :7], d["phi"][..., :7])
