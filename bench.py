@@ -209,8 +209,7 @@ def main_qat(args, world, rank, dev, pg):
     reps = 20
     for k, fn, skip in (("qat_forward", lambda: L.mcaq_qat_forward(arr, 3, sh), 0),
                         ("qat_backward_kernel", lambda: L.mcaq_qat_backward(arr, 3, sh), 0),
-                        ("qat_fold", lambda: L.mcaq_qat_backward(arr, 3, sh), 1),
-                        ("qat_fold2", lambda: L.mcaq_qat_backward(arr, 3, sh), int(os.environ.get("FOLD2", "1")))):
+                        ("qat_fold", lambda: L.mcaq_qat_backward(arr, 3, sh), 1)):
         abi.check(fn(), k)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
         for a_, b_ in ev:
@@ -246,7 +245,7 @@ def main_qat(args, world, rank, dev, pg):
         pix = sum(B * hh * ww for (hh, ww) in SIZES)
         fold_b = sum(4 * 2 * ((c + 31) // 32) * B * hh * ww for c, (hh, ww) in zip(chans, SIZES)) + 4 * pix
         for k, nb in (("qat_forward", 8 * elems + 4 * pix), ("qat_backward_kernel", 12 * elems + 4 * pix),
-                      ("qat_fold", fold_b), ("qat_fold2", fold_b), ("qat_backward", 12 * elems + 4 * pix)):
+                      ("qat_fold", fold_b), ("qat_backward", 12 * elems + 4 * pix)):
             gbs_ = nb / (kt[k] * 1e-6) / 1e9
             kern[k] = {"us": round(kt[k], 2), "alg_bytes": nb, "GB/s": round(gbs_, 1),
                        "frac": round(gbs_ / HBM_PEAK_GBS, 4)}

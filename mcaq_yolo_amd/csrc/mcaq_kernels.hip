@@ -49,10 +49,20 @@ constexpr int ST_LDS = 4096;  // floats of LDS (block sums; tail block sums)
 // Pixels per lane: enough pixels per unit for 16-byte rows when one round of
 // blocks covers the channels, fewer (more units in flight) when the channel
 // loop needs several rounds.  Requires H*W % ppl == 0.
+#ifndef MCAQ_STATS_MAXPPL
+#define MCAQ_STATS_MAXPPL 4
+#endif
+#ifndef MCAQ_STATS_MINW
+#define MCAQ_STATS_MINW 4
+#endif
+#ifndef MCAQ_STATS_LANE_FLOATS   // x values a lane loads before reducing
+#define MCAQ_STATS_LANE_FLOATS 64
+#endif
 static inline int stats_ppl(int C, int HW) {
   const int nblk = (C + ST_CG - 1) / ST_CG;
   const int rounds = (nblk + ST_WAVES - 1) / ST_WAVES;
   int ppl = rounds <= 1 ? 4 : (rounds == 2 ? 2 : 1);
+  if (ppl > MCAQ_STATS_MAXPPL) ppl = MCAQ_STATS_MAXPPL;
   while (ppl > 1 && HW % ppl) ppl >>= 1;
   return ppl;
 }
@@ -183,12 +193,13 @@ __device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, fl
   // MR rounds of 16-row blocks are loaded before the first is reduced (MR * 16
   // * PPL = 64 floats per lane), so a unit with several channel rounds still
   // pays about one memory latency per MR rounds
-  constexpr int MR = 4 / PPL;
+  constexpr int MR = MCAQ_STATS_LANE_FLOATS / (ST_CG * PPL) > 0 ? MCAQ_STATS_LANE_FLOATS / (ST_CG * PPL) : 1;
   for (int r0 = 0; r0 < rounds; r0 += MR) {
     float v[MR][ST_CG][PPL];
     const int qa = pv[0] ? q0 : 0;
 #pragma unroll
     for (int rr = 0; rr < MR; ++rr) {
+      if (r0 + rr >= rounds) break;                                 // uniform
       const int blk = imin_((r0 + rr) * ST_WAVES + wv, nblk - 1);   // clamped: branch-free loads
       const int c0 = blk * ST_CG;
       const int nc = imin_(ST_CG, C - c0);
@@ -343,18 +354,22 @@ __device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, fl
 }
 
 template <bool kVec>   // kVec: 8/16-byte row accesses for ppl 2/4 (host checks alignment)
-__global__ __launch_bounds__(256, 4) void mcaq_stats_kernel(StatsArgs a) {
+__global__ __launch_bounds__(256, MCAQ_STATS_MINW) void mcaq_stats_kernel(StatsArgs a) {
   __shared__ float lds[ST_LDS];
   // heaviest (most channels per pixel) scales are the last ones: start them first
   const int unit = a.units_total - 1 - (int)blockIdx.x;
   int si = 0;
   while (si + 1 < a.nscales && unit >= a.s[si + 1].unit_begin) ++si;
   const int lu = unit - a.s[si].unit_begin;
-  switch (a.ppl[si]) {
-    case 4: stats_unit<4, kVec>(a.s[si], lu, lds); break;
-    case 2: stats_unit<2, kVec>(a.s[si], lu, lds); break;
-    default: stats_unit<1, kVec>(a.s[si], lu, lds); break;
+  const mcaq_stats_scale S = si == 0 ? a.s[0] : si == 1 ? a.s[1] : a.s[2];   // by value: no indexed kernarg copy
+  const int ppl = si == 0 ? a.ppl[0] : si == 1 ? a.ppl[1] : a.ppl[2];
+  if constexpr (MCAQ_STATS_MAXPPL >= 4) {
+    if (ppl == 4) { stats_unit<4, kVec>(S, lu, lds); return; }
   }
+  if constexpr (MCAQ_STATS_MAXPPL >= 2) {
+    if (ppl == 2) { stats_unit<2, kVec>(S, lu, lds); return; }
+  }
+  stats_unit<1, kVec>(S, lu, lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -444,7 +459,7 @@ __device__ __forceinline__ int morph_scale_of(const MorphArgs& a, int img) {
 // Every group runs the same barrier sequence (stage loops depend on the
 // scale's geometry only); a group past the batch end recomputes the last
 // image (identical values written twice) instead of idling at the barriers.
-template <bool kLDS>
+template <bool kLDS, bool kLegacy = false>
 __global__ __launch_bounds__(MORPH_THREADS, MCAQ_MORPH_MINW) void mcaq_morph_kernel(MorphArgs a, FinalizeArgs f) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int nwg = a.wg_begin[a.nscales];
@@ -475,7 +490,7 @@ __global__ __launch_bounds__(MORPH_THREADS, MCAQ_MORPH_MINW) void mcaq_morph_ker
     carve_planes((char*)S.gscratch + (size_t)(2 * b + role) * a.pstride[si], S.Hc, S.Wc, pl);
     carve_shared(base, sh);
   }
-  morph_edges(ctx, S, b, role, pl, sh);
+  morph_edges<kLegacy>(ctx, S, b, role, pl, sh);
 }
 
 // pass B: image group g of a workgroup owns threads [g*G, (g+1)*G) and its own
@@ -871,15 +886,25 @@ int mcaq_morph_finalize(const mcaq_morph_scale* scales, int nscales, const mcaq_
     a.wg_begin[nscales] = wg;
     if (fa.nblocks > 0 && dyn < (size_t)(8 * MORPH_THREADS)) dyn = 8 * MORPH_THREADS;  // finalize_body's LDS
     const int grid = wg + fa.nblocks;
-    static int set[2] = {0, 0};  // raise the dynamic LDS limit once (not during graph capture)
-    const void* fn = mode ? (const void*)mcaq_morph_kernel<true> : (const void*)mcaq_morph_kernel<false>;
-    if ((int)dyn > set[mode]) {
-      hipError_t ae = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, limit);
+    // canny_impl='legacy' is an analyzer option: one value for every scale of a launch
+    const int leg = (a.s[0].flags & F_CANNY_LEGACY) ? 1 : 0;
+    for (int i = 1; i < nscales; ++i)
+      if (((a.s[i].flags & F_CANNY_LEGACY) ? 1 : 0) != leg) return (int)hipErrorInvalidValue;
+    static int set[4] = {0, 0, 0, 0};  // raise the dynamic LDS limit once (not during graph capture)
+    const int var = 2 * leg + mode;
+    const void* fns[4] = {(const void*)mcaq_morph_kernel<false>, (const void*)mcaq_morph_kernel<true>,
+                          (const void*)mcaq_morph_kernel<false, true>, (const void*)mcaq_morph_kernel<true, true>};
+    if ((int)dyn > set[var]) {
+      hipError_t ae = hipFuncSetAttribute(fns[var], hipFuncAttributeMaxDynamicSharedMemorySize, limit);
       if (ae != hipSuccess) return (int)ae;
-      set[mode] = limit;
+      set[var] = limit;
     }
-    if (mode) hipLaunchKernelGGL(mcaq_morph_kernel<true>, dim3(grid), dim3(MORPH_THREADS), dyn, stream, a, fa);
-    else hipLaunchKernelGGL(mcaq_morph_kernel<false>, dim3(grid), dim3(MORPH_THREADS), dyn, stream, a, fa);
+    switch (var) {
+      case 0: hipLaunchKernelGGL((mcaq_morph_kernel<false>), dim3(grid), dim3(MORPH_THREADS), dyn, stream, a, fa); break;
+      case 1: hipLaunchKernelGGL((mcaq_morph_kernel<true>), dim3(grid), dim3(MORPH_THREADS), dyn, stream, a, fa); break;
+      case 2: hipLaunchKernelGGL((mcaq_morph_kernel<false, true>), dim3(grid), dim3(MORPH_THREADS), dyn, stream, a, fa); break;
+      default: hipLaunchKernelGGL((mcaq_morph_kernel<true, true>), dim3(grid), dim3(MORPH_THREADS), dyn, stream, a, fa); break;
+    }
     hipError_t le = hipGetLastError();
     if (le != hipSuccess) return (int)le;
   }

@@ -644,7 +644,59 @@ MCAQ_HD float tile_sum_t(const float* plane, int Wc, int h0, int w0) {
   return acc;
 }
 
+// Sobel of gsc*blur (zero pad) -> magnitude Bf, NMS direction dir; column
+// strips as the blur.  Zero-weight taps are skipped and padded taps add
+// fma(k, 0, g) == g (g never holds -0: it starts at +0).  Default: gsc = 255,
+// L1 magnitude; canny_impl='legacy': gsc = 1, sqrt(gx^2 + gy^2 + 1e-12).
+// Separate instantiations keep the default path's registers unchanged.
+template <bool kLegacy>
+MCAQ_HD void sobel_stage(const Ctx& ctx, Planes& pl, int Hc, int Wc) {
+  {
+    const int nsr = (Hc + SR - 1) / SR;
+    MFOR2(st, w, nsr, Wc) {
+      const int r0 = st * SR;
+      float v[SR + 2][3];
+#pragma unroll
+      for (int t = 0; t < SR + 2; ++t) {
+        const int hh = r0 + t - 1;
+        const bool rv = hh >= 0 && hh < Hc;
+        const float* row = pl.A + imin_(imax_(hh, 0), Hc - 1) * Wc;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          const int ww = w + j - 1;
+          const float x = row[imin_(imax_(ww, 0), Wc - 1)] * (kLegacy ? 1.0f : 255.0f);
+          v[t][j] = (rv && ww >= 0 && ww < Wc) ? x : 0.0f;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < SR; ++r) {
+        float gx = 0.0f, gy = 0.0f;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const float kx = (i == 1) ? 2.0f : 1.0f;    // gx taps (i,0) = -kx, (i,2) = +kx
+          const float ky = (float)(i - 1);             // gy taps (i,j) = ky * {1,2,1}
+          gx = fmaf(-kx, v[r + i][0], gx);
+          gx = fmaf(kx, v[r + i][2], gx);
+          if (i != 1) {
+            gy = fmaf(ky, v[r + i][0], gy);
+            gy = fmaf(2.0f * ky, v[r + i][1], gy);
+            gy = fmaf(ky, v[r + i][2], gy);
+          }
+        }
+        if (r0 + r < Hc) {
+          const int p = (r0 + r) * Wc + w;
+          pl.Bf[p] = kLegacy ? sqrtf((gx * gx + gy * gy) + 1e-12f) : fabsf(gx) + fabsf(gy);
+          pl.dir[p] = (uint8_t)nms_dir(gx, gy);
+        }
+      }
+    }
+  }
+}
+
 // ---- pass A: per-image pixel work -> phi (one 1024-thread workgroup per image)
+// kLegacy: the canny_impl='legacy' instantiation (a separate kernel on the
+// device, so the default edge path keeps its register allocation)
+template <bool kLegacy>
 MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, Planes& pl, Shared& sh) {
   const int Hc = S.Hc, Wc = S.Wc, P = Hc * Wc, T = S.tile, wt = S.wt, NT = S.ht * wt;
   const int WPR = pl.WPR, RS = WPR * 32;   // words / bit slots per row
@@ -700,7 +752,7 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, P
     if (role == 0) {
     // canny_impl='legacy' (morphology.py:512-540): Sobel of the blur itself,
     // L2 magnitude, Otsu of the min-max normalised NMS map, 2 hysteresis rounds
-    const bool legacy = (S.flags & F_CANNY_LEGACY) != 0;
+    constexpr bool legacy = kLegacy;
     // -- 5x5 Gaussian blur (zero pad; an out-of-image tap adds fma(w, 0, acc) == acc
     //    because acc >= +0), fused with the Otsu histogram of the result.
     //    Column strips of SR rows per thread: consecutive threads own consecutive
@@ -743,52 +795,10 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, P
     const float thr = legacy ? 0.0f : otsu_from_hist(ctx, sh);
     const float thr255 = thr * 255.0f;
     const float lo255 = 0.5f * thr255;
-    const float gsc = legacy ? 1.0f : 255.0f;    // x * 1.0f == x
     MSTAMP(3);
 
-    // -- Sobel of 255*blur (zero pad), L1 magnitude -> Bf, direction -> dir.
-    //    Column strips as the blur.  Zero-weight taps are skipped and padded
-    //    taps add fma(k, 0, g) == g (g never holds -0: it starts at +0).
-    {
-      const int nsr = (Hc + SR - 1) / SR;
-      MFOR2(st, w, nsr, Wc) {
-        const int r0 = st * SR;
-        float v[SR + 2][3];
-#pragma unroll
-        for (int t = 0; t < SR + 2; ++t) {
-          const int hh = r0 + t - 1;
-          const bool rv = hh >= 0 && hh < Hc;
-          const float* row = pl.A + imin_(imax_(hh, 0), Hc - 1) * Wc;
-#pragma unroll
-          for (int j = 0; j < 3; ++j) {
-            const int ww = w + j - 1;
-            const float x = row[imin_(imax_(ww, 0), Wc - 1)] * gsc;
-            v[t][j] = (rv && ww >= 0 && ww < Wc) ? x : 0.0f;
-          }
-        }
-#pragma unroll
-        for (int r = 0; r < SR; ++r) {
-          float gx = 0.0f, gy = 0.0f;
-#pragma unroll
-          for (int i = 0; i < 3; ++i) {
-            const float kx = (i == 1) ? 2.0f : 1.0f;    // gx taps (i,0) = -kx, (i,2) = +kx
-            const float ky = (float)(i - 1);             // gy taps (i,j) = ky * {1,2,1}
-            gx = fmaf(-kx, v[r + i][0], gx);
-            gx = fmaf(kx, v[r + i][2], gx);
-            if (i != 1) {
-              gy = fmaf(ky, v[r + i][0], gy);
-              gy = fmaf(2.0f * ky, v[r + i][1], gy);
-              gy = fmaf(ky, v[r + i][2], gy);
-            }
-          }
-          if (r0 + r < Hc) {
-            const int p = (r0 + r) * Wc + w;
-            pl.Bf[p] = legacy ? sqrtf((gx * gx + gy * gy) + 1e-12f) : fabsf(gx) + fabsf(gy);
-            pl.dir[p] = (uint8_t)nms_dir(gx, gy);
-          }
-        }
-      }
-    }
+    // -- Sobel (-> Bf magnitude, dir direction), see sobel_stage
+    sobel_stage<kLegacy>(ctx, pl, Hc, Wc);
     MSYNC();
     MSTAMP(4);
     // -- NMS (replicate-shifted neighbours) + double threshold -> bit planes.
@@ -797,8 +807,7 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, P
     uint32_t* E0 = pl.bits(BP_E0);
     uint32_t* E1 = pl.bits(BP_E1);
     uint32_t* WK = pl.bits(BP_WK);
-    float lmn = 3.402823466e38f, lmx = -3.402823466e38f;   // legacy: NMS map range
-    {
+    if constexpr (!legacy) {
       const int nsr = (Hc + SR - 1) / SR;
       MFOR2(st, sl, nsr, RS) {
         const int k = sl >> 5, bit = sl & 31, w = sl;
@@ -827,21 +836,27 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, P
           if (r0 + r >= Hc) continue;
           const bool keep = (m[r] >= n1[r]) && (m[r] >= n2[r]);
           const float nms = keep ? m[r] : 0.0f;
-          if (legacy) {
-            if (w < Wc) {
-              pl.A[(r0 + r) * Wc + w] = nms;     // the blur plane is free after Sobel
-              lmn = fmin_(lmn, nms); lmx = fmax_(lmx, nms);
-            }
-          } else {
-            put_bits(E0, (r0 + r) * WPR + k, bit, w < Wc && nms > thr255);
-            put_bits(WK, (r0 + r) * WPR + k, bit, w < Wc && nms > lo255);
-          }
+          put_bits(E0, (r0 + r) * WPR + k, bit, w < Wc && nms > thr255);
+          put_bits(WK, (r0 + r) * WPR + k, bit, w < Wc && nms > lo255);
         }
       }
-    }
-    MSYNC();
-    if (legacy) {
-      // normalise01 of the NMS map, its Otsu threshold t, strong > t, weak > t/2
+      MSYNC();
+    } else {
+      // legacy: the NMS map itself (into the blur plane, free after Sobel),
+      // normalise01, its Otsu threshold t, strong > t, weak > t/2
+      float lmn = 3.402823466e38f, lmx = -3.402823466e38f;
+      MFOR(p, P) {
+        const int h = p / Wc, w = p - (p / Wc) * Wc;
+        const int d = pl.dir[p];
+        const float m = pl.Bf[p];
+        const int dy1 = (d == 0) ? 0 : -1;
+        const int dx1 = (d == 2) ? 0 : ((d == 3) ? -1 : 1);
+        const int h1 = imin_(imax_(h + dy1, 0), Hc - 1), w1 = imin_(imax_(w + dx1, 0), Wc - 1);
+        const int h2 = imin_(imax_(h - dy1, 0), Hc - 1), w2 = imin_(imax_(w - dx1, 0), Wc - 1);
+        const float nms = (m >= pl.Bf[h1 * Wc + w1] && m >= pl.Bf[h2 * Wc + w2]) ? m : 0.0f;
+        pl.A[p] = nms;
+        lmn = fmin_(lmn, nms); lmx = fmax_(lmx, nms);
+      }
       float mn, mx;
       block_minmax(ctx, sh, lmn, lmx, mn, mx);
       const float den = (mx - mn) + 1e-8f;

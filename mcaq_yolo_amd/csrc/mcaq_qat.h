@@ -34,9 +34,10 @@ constexpr int QAT_NB = 8;
 
 // unit = 256 pixels x 32 channels of one image (the pass-2 layout): lane l of
 // wave w owns pixels 4l..4l+3 and channels 8w..8w+7 of the slice (channel
-// loop fully unrolled: the compiler schedules the loads; issuing all of them
-// ahead of the table/barrier, or streaming two channels at a time under an
-// 8-workgroup/CU register cap, measured slower at config 5).
+// loop fully unrolled: the compiler schedules the loads).  Measured slower at
+// config 5: all loads issued ahead of the table and barrier;
+// two channels at a time under an 8-workgroup/CU register cap; one-wave
+// workgroups walking all 32 channels of a slice (every unit resident at once).
 template <bool kBwd, bool kVec>
 __global__ __launch_bounds__(256, MCAQ_QAT_MINW) void mcaq_qat_kernel(QatArgs a) {
   __shared__ float2 qt[32 * QAT_NB];
@@ -134,11 +135,7 @@ __global__ __launch_bounds__(256, MCAQ_QAT_MINW) void mcaq_qat_kernel(QatArgs a)
     if (kVec) {
       typedef float f4v __attribute__((ext_vector_type(4)));
       const f4v ov = {o[0], o[1], o[2], o[3]};
-#ifdef MCAQ_QAT_PLAIN_STORES
-      if (pv[0]) *reinterpret_cast<f4v*>(orow + q0) = ov;
-#else
       if (pv[0]) __builtin_nontemporal_store(ov, reinterpret_cast<f4v*>(orow + q0));   // written once, streamed
-#endif
     } else {
 #pragma unroll
       for (int k = 0; k < 4; ++k) if (pv[k]) orow[q0 + k] = o[k];
@@ -168,10 +165,7 @@ __global__ __launch_bounds__(256, MCAQ_QAT_MINW) void mcaq_qat_kernel(QatArgs a)
 // then each tile over its columns (short dependent chains: rows + columns,
 // not rows x columns).  fp32 sums in a different order than the reference's
 // upsample backward: grad_bits is checked to a tolerance.
-#ifndef MCAQ_FOLD_LDS
-#define MCAQ_FOLD_LDS 8192
-#endif
-constexpr int QAT_FOLD_LDS = MCAQ_FOLD_LDS;    // floats of pixel chunk
+constexpr int QAT_FOLD_LDS = 8192;    // floats of pixel chunk
 constexpr int QAT_FOLD_SL = 8;        // slices loaded together
 
 // first index i in [0, n) with nearest_src(i, in, n) >= v (n if none)
@@ -229,10 +223,6 @@ __global__ __launch_bounds__(256) void mcaq_qat_fold_kernel(QatArgs a) {
   const float* pf = S.work + (size_t)nsl * plane + (size_t)b * HW;
   const int rs = band_start(th, S.ht, H), re = band_start(th + 1, S.ht, H);
   const int rows_per_chunk = imax_(1, QAT_FOLD_LDS / W);
-#if defined(MCAQ_FOLD_EXP) && MCAQ_FOLD_EXP == 1
-  if (threadIdx.x < 1) S.gb[((size_t)b * S.ht + th) * wt] = (float)(re - rs);
-  return;
-#endif
   for (int w = threadIdx.x; w < W; w += 256) col[w] = 0.0f;
   for (int r0 = rs; r0 < re; r0 += rows_per_chunk) {
     const int r1 = imin_(re, r0 + rows_per_chunk);
@@ -260,9 +250,6 @@ __global__ __launch_bounds__(256) void mcaq_qat_fold_kernel(QatArgs a) {
     __syncthreads();
   }
   if (!S.gb) return;
-#if defined(MCAQ_FOLD_EXP) && MCAQ_FOLD_EXP == 2
-  return;
-#endif
   // tile tw: its columns, in order
   for (int tw = threadIdx.x; tw < wt; tw += 256) {
     const int cs = band_start(tw, wt, W), ce = band_start(tw + 1, wt, W);
@@ -358,9 +345,6 @@ int mcaq_qat_backward(const mcaq_qat_scale* scales, int nscales, hipStream_t str
   bool fold = false;
   for (int i = 0; i < nscales; ++i) fold = fold || scales[i].gm || scales[i].gb;
   if (fold) launch_k(mcaq::mcaq_qat_fold_kernel, dim3(blocks), dim3(256), 0, stream, a);
-#ifdef MCAQ_FOLD_TWICE
-  if (fold) launch_k(mcaq::mcaq_qat_fold_kernel, dim3(blocks), dim3(256), 0, stream, a);
-#endif
   return (int)hipGetLastError();
 }
 

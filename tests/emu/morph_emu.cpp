@@ -20,7 +20,8 @@ extern "C" int emu_morph(const mcaq_morph_scale* s) {
         Planes pl; Shared sh;
         carve_planes(planes.data(), s->Hc, s->Wc, pl);
         carve_shared(shm.data(), sh);
-        morph_edges(ctx, *s, b, role, pl, sh);
+        if (s->flags & F_CANNY_LEGACY) morph_edges<true>(ctx, *s, b, role, pl, sh);
+        else morph_edges<false>(ctx, *s, b, role, pl, sh);
       }
     }
     Shared sh2;
