@@ -55,13 +55,19 @@ constexpr int ST_LDS = 4096;  // floats of LDS (block sums; tail block sums)
 #ifndef MCAQ_STATS_MINW
 #define MCAQ_STATS_MINW 4
 #endif
+#ifndef MCAQ_STATS_PPL_R2   // pixels per lane when the channels take 2 rounds of blocks
+#define MCAQ_STATS_PPL_R2 2
+#endif
+#ifndef MCAQ_STATS_PPL_R4   // ... 3 or more rounds
+#define MCAQ_STATS_PPL_R4 1
+#endif
 #ifndef MCAQ_STATS_LANE_FLOATS   // x values a lane loads before reducing
 #define MCAQ_STATS_LANE_FLOATS 64
 #endif
 static inline int stats_ppl(int C, int HW) {
   const int nblk = (C + ST_CG - 1) / ST_CG;
   const int rounds = (nblk + ST_WAVES - 1) / ST_WAVES;
-  int ppl = rounds <= 1 ? 4 : (rounds == 2 ? 2 : 1);
+  int ppl = rounds <= 1 ? 4 : (rounds == 2 ? MCAQ_STATS_PPL_R2 : MCAQ_STATS_PPL_R4);
   if (ppl > MCAQ_STATS_MAXPPL) ppl = MCAQ_STATS_MAXPPL;
   while (ppl > 1 && HW % ppl) ppl >>= 1;
   return ppl;
@@ -441,6 +447,9 @@ constexpr int TILES_THREADS = 256;
 #ifndef MCAQ_MORPH_MINW     // min waves per SIMD of pass A: 4 -> <= 128 VGPRs
 #define MCAQ_MORPH_MINW 4
 #endif
+#ifndef MCAQ_MORPH_PRIO     // wave priority of passes A and B (0..3) against the streaming passes
+#define MCAQ_MORPH_PRIO 2
+#endif
 #ifndef MCAQ_TILES_MINW     // min waves per SIMD of pass B (register budget 512 / MINW)
 #define MCAQ_TILES_MINW 1
 #endif
@@ -469,7 +478,7 @@ __global__ __launch_bounds__(MORPH_THREADS, MCAQ_MORPH_MINW) void mcaq_morph_ker
   }
   // latency-bound per-image chain: win VALU / LDS issue arbitration against
   // co-resident streaming waves of other batches in flight
-  __builtin_amdgcn_s_setprio(2);
+  __builtin_amdgcn_s_setprio(MCAQ_MORPH_PRIO);
   int si = 0;
   while (si + 1 < a.nscales && (int)blockIdx.x >= a.wg_begin[si + 1]) ++si;
   const MorphScale& S = a.s[si];
@@ -498,7 +507,7 @@ __global__ __launch_bounds__(MORPH_THREADS, MCAQ_MORPH_MINW) void mcaq_morph_ker
 // past the batch end recomputes the last image (identical values written twice).
 __global__ __launch_bounds__(TILES_THREADS, MCAQ_TILES_MINW) void mcaq_tiles_kernel(MorphArgs a, int wlds) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  __builtin_amdgcn_s_setprio(2);
+  __builtin_amdgcn_s_setprio(MCAQ_MORPH_PRIO);
   int si = 0;
   while (si + 1 < a.nscales && (int)blockIdx.x >= a.twg_begin[si + 1]) ++si;
   const MorphScale& S = a.s[si];

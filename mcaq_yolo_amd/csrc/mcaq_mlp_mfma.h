@@ -36,9 +36,26 @@ enum : int {
   MMQ_SIZE = MMQ_W3 + 2048,
 };
 
-// keep the scheduler from hoisting every A-operand load of a layer at once
-// (that costs ~64 VGPRs and spills at 1024 threads / 128 VGPRs)
+// weight / folded-BN pointers of the tile MLPs: LDS-typed when the weights are
+// staged in the workgroup's LDS (ds_read, issued ahead of the MFMA chain; a
+// generic pointer compiles to flat loads that wait before every MFMA step)
+typedef const __attribute__((address_space(3))) float* lds_cf;
+
+// optional scheduling fence between groups of 8 k-steps (keeps the A-operand
+// loads of a layer from being hoisted at once); pass B's 256-thread workgroups
+// have the registers to hoist them, so it is off unless MCAQ_MLP_FENCE is set
+#if defined(MCAQ_MLP_FENCE)
 #define MLP_GROUP_FENCE __builtin_amdgcn_sched_barrier(0);
+#else
+#define MLP_GROUP_FENCE
+#endif
+
+// diagnostic build only (-DMCAQ_STAMPS): wave-level cycle stamps (no barrier)
+#if defined(MCAQ_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
+#define WSTAMP(on, k) do { if ((on) && (threadIdx.x & 63) == 0) g_mcaq_stamps[(k)] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define WSTAMP(on, k) do {} while (0)
+#endif
 
 __device__ __forceinline__ int d_neuron(int r, int half) { return (r & 3) + 8 * (r >> 2) + 4 * half; }
 
@@ -77,8 +94,8 @@ __device__ __forceinline__ float tree32(const f32x16& d) {
   return (u[0] + u[1]) + (u[2] + u[3]);
 }
 
-template <int NB>
-__device__ __forceinline__ void layernorm_d(f32x16* D, const float* g, const float* b, int half) {
+template <int NB, typename PT>
+__device__ __forceinline__ void layernorm_d(f32x16* D, PT g, PT b, int half) {
   float s = tree32(D[0]);
   if constexpr (NB == 2) s = s + tree32(D[1]);
   const float mean = s / (float)(32 * NB);
@@ -101,7 +118,8 @@ __device__ __forceinline__ void layernorm_d(f32x16* D, const float* g, const flo
 }
 
 // sequential dot over neurons 0..31 of one D block with w (N = 1 output layer)
-__device__ __forceinline__ float dot32_seq(const f32x16& d, const float* w, int half) {
+template <typename PT>
+__device__ __forceinline__ float dot32_seq(const f32x16& d, PT w, int half) {
   float other[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) other[r] = xhalf(d[r]);
@@ -124,7 +142,9 @@ __device__ __forceinline__ f32x16 zero16() {
 }
 
 // complexity MLP for the 32 tiles [t0, t0+32) of one image; writes T_CMLP
-__device__ void cmlp_block_mfma(const float* P, float* tiles, int NT, int t0, int lane) {
+template <typename PT>
+__device__ void cmlp_block_mfma(PT P, float* tiles, int NT, int t0, int lane, bool stamp = false) {
+  WSTAMP(stamp, 40);
   const int half = lane >> 5, col = lane & 31;
   const int t = t0 + col;
   const bool valid = t < NT;
@@ -142,11 +162,13 @@ __device__ void cmlp_block_mfma(const float* P, float* tiles, int NT, int t0, in
   for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
     for (int r = 0; r < 16; ++r) D1[nb][r] = D1[nb][r] + P[CM_B1 + 32 * nb + d_neuron(r, half)];
+  WSTAMP(stamp, 41);
   layernorm_d<2>(D1, P + CM_G1, P + CM_BE1, half);
 #pragma unroll
   for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
     for (int r = 0; r < 16; ++r) D1[nb][r] = fmax_(D1[nb][r], 0.0f);
+  WSTAMP(stamp, 42);
   // layer 2: 64 -> 32
   f32x16 D2[1] = {zero16()};
 #define CM_L2_STEP(S) D2[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(P[CMQ_W2 + (S) * 64 + lane], b_from_d<S>(D1, half), D2[0], 0, 0, 0);
@@ -157,16 +179,20 @@ __device__ void cmlp_block_mfma(const float* P, float* tiles, int NT, int t0, in
 #undef CM_L2_STEP
 #pragma unroll
   for (int r = 0; r < 16; ++r) D2[0][r] = D2[0][r] + P[CM_B2 + d_neuron(r, half)];
+  WSTAMP(stamp, 43);
   layernorm_d<1>(D2, P + CM_G2, P + CM_BE2, half);
+  WSTAMP(stamp, 44);
 #pragma unroll
   for (int r = 0; r < 16; ++r) D2[0][r] = fmax_(D2[0][r], 0.0f);
   // layer 3: 32 -> 1, sigmoid
   const float z = dot32_seq(D2[0], P + CM_W3, half) + P[CM_B3];
   if (valid && half == 0) tiles[t * TILE_FLOATS + T_CMLP] = 1.0f / (1.0f + cr_exp(-z));
+  WSTAMP(stamp, 45);
 }
 
 // BN eval on a D block with the folded per-neuron (alpha, beta), then ReLU
-__device__ __forceinline__ void bn_relu_d(f32x16& d, const float* alpha, const float* beta, int nb, int half) {
+template <typename PT>
+__device__ __forceinline__ void bn_relu_d(f32x16& d, PT alpha, PT beta, int nb, int half) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int j = 32 * nb + d_neuron(r, half);
@@ -177,8 +203,10 @@ __device__ __forceinline__ void bn_relu_d(f32x16& d, const float* alpha, const f
 // MLP bit mapper for the tiles [t0, t0+32): pre-temperature bits into T_AUX
 // ab: folded BN terms in LDS, alpha at [0,128) and beta at [128,256) for the
 // 32 + 64 + 32 neurons of BN1/BN2/BN3 (mcaq_morph.h, bn_fold)
-__device__ void mapper_block_mfma(const float* P, const float* ab, float* tiles, int NT, int t0, int lane,
-                                  int csrc, float min_bits, float max_bits) {
+template <typename PT>
+__device__ void mapper_block_mfma(PT P, PT ab, float* tiles, int NT, int t0, int lane,
+                                  int csrc, float min_bits, float max_bits, bool stamp = false) {
+  WSTAMP(stamp, 48);
   const int half = lane >> 5, col = lane & 31;
   const int t = t0 + col;
   const bool valid = t < NT;
@@ -186,6 +214,7 @@ __device__ void mapper_block_mfma(const float* P, const float* ab, float* tiles,
   c = clampf_(c, 0.0f, 1.0f);
   const float z0 = half == 0 ? c : c * c;              // k = 0, 1
   const float z1 = half == 0 ? cr_log1p(c) : 0.0f;     // k = 2, (3 = zero pad)
+  WSTAMP(stamp, 49);
   // layer 1: 3 -> 32
   f32x16 D1[1] = {zero16()};
   D1[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(P[MMQ_W1 + 0 * 64 + lane], z0, D1[0], 0, 0, 0);
@@ -193,6 +222,7 @@ __device__ void mapper_block_mfma(const float* P, const float* ab, float* tiles,
 #pragma unroll
   for (int r = 0; r < 16; ++r) D1[0][r] = D1[0][r] + P[MM_B1 + d_neuron(r, half)];
   bn_relu_d(D1[0], ab, ab + 128, 0, half);
+  WSTAMP(stamp, 50);
   // layer 2: 32 -> 64
   f32x16 D2[2] = {zero16(), zero16()};
 #define MM_L2_STEP(S)                                                                                  \
@@ -210,6 +240,7 @@ __device__ void mapper_block_mfma(const float* P, const float* ab, float* tiles,
     for (int r = 0; r < 16; ++r) D2[nb][r] = D2[nb][r] + P[MM_B2 + 32 * nb + d_neuron(r, half)];
     bn_relu_d(D2[nb], ab + 32, ab + 160, nb, half);
   }
+  WSTAMP(stamp, 51);
   // layer 3: 64 -> 32
   f32x16 D3[1] = {zero16()};
 #define MM_L3_STEP(S) D3[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(P[MMQ_W3 + (S) * 64 + lane], b_from_d<S>(D2, half), D3[0], 0, 0, 0);
@@ -221,10 +252,13 @@ __device__ void mapper_block_mfma(const float* P, const float* ab, float* tiles,
 #pragma unroll
   for (int r = 0; r < 16; ++r) D3[0][r] = D3[0][r] + P[MM_B3 + d_neuron(r, half)];
   bn_relu_d(D3[0], ab + 96, ab + 224, 0, half);
+  WSTAMP(stamp, 52);
   // layer 4: 32 -> 1, sigmoid, affine to [min_bits, max_bits]
   const float z = dot32_seq(D3[0], P + MM_W4, half) + P[MM_B4];
+  WSTAMP(stamp, 53);
   const float h = 1.0f / (1.0f + cr_exp(-z));
   if (valid && half == 0) tiles[t * TILE_FLOATS + T_AUX] = min_bits + (max_bits - min_bits) * h;
+  WSTAMP(stamp, 54);
 }
 
 }  // namespace mcaq

@@ -1449,8 +1449,11 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
   // -- complexity MLP + bilateral (morphology.py:959-968)
   if (S.flags & F_CMLP) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    for (int blk = ctx.tid >> 6; blk * 32 < NT; blk += ctx.nthr >> 6)
-      cmlp_block_mfma(Pc, tiles, NT, blk * 32, ctx.tid & 63);
+    for (int blk = ctx.tid >> 6; blk * 32 < NT; blk += ctx.nthr >> 6) {
+      const bool st = b == 0 && blk == 0 && ctx.nthr == 256;
+      if (wl) cmlp_block_mfma((lds_cf)Pc, tiles, NT, blk * 32, ctx.tid & 63, st);
+      else cmlp_block_mfma(Pc, tiles, NT, blk * 32, ctx.tid & 63, st);
+    }
     MSTAMP(28);
 #else
     MFOR(t, NT) {
@@ -1567,8 +1570,14 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
         ab[128 + j] = bn[n + jj] - (bn[2 * n + jj] * inv) * bn[jj];
       }
       MSYNC();
-      for (int blk = ctx.tid >> 6; blk * 32 < NT; blk += ctx.nthr >> 6)
-        mapper_block_mfma(Pmap, ab, tiles, NT, blk * 32, ctx.tid & 63, csrc, S.min_bits, S.max_bits);
+      MSTAMP(30);
+      for (int blk = ctx.tid >> 6; blk * 32 < NT; blk += ctx.nthr >> 6) {
+        const bool st = b == 0 && blk == 0 && ctx.nthr == 256;
+        if (wl) mapper_block_mfma((lds_cf)Pmap, (lds_cf)ab, tiles, NT, blk * 32, ctx.tid & 63, csrc, S.min_bits,
+                                  S.max_bits, st);
+        else mapper_block_mfma((const float*)Pmap, (const float*)ab, tiles, NT, blk * 32, ctx.tid & 63, csrc,
+                               S.min_bits, S.max_bits, st);
+      }
 #else
       MFOR(t, NT) tiles[t * TILE_FLOATS + T_AUX] =
           mapper_mlp_tile(Pmap, tiles[t * TILE_FLOATS + csrc], S.min_bits, S.max_bits);

@@ -7,18 +7,30 @@ export TMPDIR=/tmp
 L=mcaq_yolo_amd/lib/libmcaq_hip.so
 cp $L /tmp/base.so
 cp /tmp/base.so tools/probe/ab/base.so
-for v in base "$@"; do
+ok="base"
+for v in "$@"; do
   cp tools/probe/ab/$v.so $L
   timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "golden_case or packed or three_scales or bench_config" > gpurun_out/ab/$v.pytest.log 2>&1
   rc=$?; echo "$v pytest rc=$rc $(tail -1 gpurun_out/ab/$v.pytest.log)"
   if [ $rc -ne 0 ]; then grep -E "FAIL|assert" gpurun_out/ab/$v.pytest.log | head -5; continue; fi
-  for r in 1 2; do
-    timeout -k 10 120 python bench.py --no-cpu --no-e2e --steps 100 > gpurun_out/ab/$v.$r.json 2> gpurun_out/ab/$v.$r.err || { cp /tmp/base.so $L; tail -5 gpurun_out/ab/$v.$r.err; exit 1; }
+  ok="$ok $v"
+done
+# interleaved repetitions: base, v1, v2, ..., base, v1, v2, ...
+for r in 1 2 3; do
+  for v in $ok; do
+    cp tools/probe/ab/$v.so $L
+    timeout -k 10 120 python bench.py --no-cpu --no-e2e --steps 200 > gpurun_out/ab/$v.$r.json 2> gpurun_out/ab/$v.$r.err || { cp /tmp/base.so $L; tail -5 gpurun_out/ab/$v.$r.err; exit 1; }
   done
 done
 cp /tmp/base.so $L
 python - <<'PY'
-import json, glob
+import json, glob, collections
+agg = collections.defaultdict(list)
+for f in sorted(glob.glob("gpurun_out/ab/*.json")):
+    d = json.loads(open(f).read().strip().splitlines()[-1])
+    agg[f.split("/")[-1].split(".")[0]].append(d["value"])
+for k, v in sorted(agg.items()):
+    print("%-10s mean %8.0f img/s  runs %s" % (k, sum(v) / len(v), " ".join("%.0f" % x for x in v)))
 for f in sorted(glob.glob("gpurun_out/ab/*.json")):
     d = json.loads(open(f).read().strip().splitlines()[-1])
     k = d["kernels"]

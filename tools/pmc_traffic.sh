@@ -9,6 +9,6 @@ R=$GRAFT_REPO_ROOT
 mkdir -p $R/gpurun_out
 cd /tmp
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -s KILL 120 rocprofv3 --pmc $c --kernel-trace -d $R/gpurun_out/pmc_$c -o run --output-format csv -- python3 $R/bench.py --steps 8 --warmup 2 --pipeline 1 --eager --no-cpu > $R/gpurun_out/pmc_$c.log 2>&1 || { tail -5 $R/gpurun_out/pmc_$c.log; exit 1; }
+  timeout -s KILL 120 rocprofv3 --pmc $c --kernel-trace -d $R/gpurun_out/pmc_$c -o run --output-format csv -- python3 $R/bench.py --steps 8 --warmup 2 --pipeline 1 --eager --no-cpu --no-e2e > $R/gpurun_out/pmc_$c.log 2>&1 || { tail -5 $R/gpurun_out/pmc_$c.log; exit 1; }
 done
 cd $R && python tools/pmc_summary.py gpurun_out > gpurun_out/pmc_summary.json && cat gpurun_out/pmc_summary.json

@@ -32,6 +32,25 @@ __global__ __launch_bounds__(256) void copy4(const float4* __restrict__ x, float
   for (; i < n4; i += stride) y[i] = x[i];
 }
 
+
+// pass-1-shaped read: unit = 256 pixels x C channels of one image (C3 shape:
+// 64 x 80 x 80), wave w loads rows w, w+4, ... (ROWS per wave) as float4 per
+// lane, 1 KB per row; NWG_MIN = workgroups per CU requested
+template <int ROWS, int MINW>
+__global__ __launch_bounds__(256, MINW) void shape_read(const float* __restrict__ x, int C, int HW, float* out) {
+  const int upi = HW / 256;
+  const int b = blockIdx.x / upi, chunk = blockIdx.x - b * upi;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const float* xb = x + (size_t)b * C * HW + chunk * 256 + lane * 4;
+  float s = 0.0f;
+  float4 v[ROWS];
+#pragma unroll
+  for (int i = 0; i < ROWS; ++i) v[i] = *reinterpret_cast<const float4*>(xb + (size_t)(wv * ROWS + i) * HW);
+#pragma unroll
+  for (int i = 0; i < ROWS; ++i) s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  if (s == 12345.678f) out[0] = s;
+}
+
 int main() {
   // config 2: 32 x (64*6400 + 128*1600 + 256*400) floats; 3 input batches cycled
   const size_t n = (size_t)32 * (64 * 6400 + 128 * 1600 + 256 * 400);
@@ -67,6 +86,30 @@ int main() {
       const double us = tot * 1e3 / reps;
       const double bytes = (mode == 0 ? 4.0 : 8.0) * n;
       printf("%-8s grid %6d  %7.2f us  %7.1f GB/s\n", mode == 0 ? "read" : "copy", g, us, bytes / (us * 1e-6) / 1e9);
+    }
+  }
+
+  {
+    // C3 shape of config 2: B 32, C 64, 80 x 80 (52 MB)
+    const int B = 32, C = 64, HW = 6400;
+    const size_t bytes = (size_t)B * C * HW * 4;
+    const int grid = B * HW / 256;
+    for (int v = 0; v < 3; ++v) {
+      float tot = 0.0f;
+      const int reps = 30;
+      for (int r = 0; r < reps + 3; ++r) {
+        const float* xp = (const float*)x[r % nb];
+        if (v == 0) hipExtLaunchKernelGGL((shape_read<16, 4>), dim3(grid), dim3(256), 0, 0, e0, e1, 0, xp, C, HW, out);
+        if (v == 1) hipExtLaunchKernelGGL((shape_read<16, 2>), dim3(grid), dim3(256), 0, 0, e0, e1, 0, xp, C, HW, out);
+        if (v == 2) hipExtLaunchKernelGGL(read_sum, dim3(8192), dim3(256), 0, 0, e0, e1, 0, (const float4*)xp, bytes / 16, out);
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        if (r >= 3) tot += ms;
+      }
+      const double us = tot * 1e3 / reps;
+      printf("C3 %-22s %7.2f us  %7.1f GB/s\n", v == 0 ? "shape_read<16,4>" : (v == 1 ? "shape_read<16,2>" : "read_sum grid 8192"),
+             us, bytes / (us * 1e-6) / 1e9);
     }
   }
   return 0;
