@@ -33,6 +33,7 @@ bit_allocation.py:199-280 (phi itself is no-grad side information computed by
 the morph kernel, as in the reference).
 """
 import ctypes
+import functools
 from typing import Optional
 
 import torch
@@ -653,7 +654,7 @@ class LearnedSoftMask(nn.Module):
         bits_norm = ((bit_map.unsqueeze(1).float() - 2.0) / 6.0).clamp(0.0, 1.0)
         logits = self.net(torch.cat([bits_norm, act.float()], dim=1))
         m = torch.softmax(logits, dim=1)[:, :1]
-        m = F.interpolate(m, size=(H, W), mode="nearest")
+        m = _nearest_up(m, H, W)
         p = self.kernel_size // 2
         return F.conv2d(F.pad(m, (p, p, p, p), mode="replicate"), self.smooth_kernel)
 
@@ -661,6 +662,30 @@ class LearnedSoftMask(nn.Module):
         """m per tile before upsampling/smoothing (B, Ht, Wt); the quant pass
         turns it into m(p) on the fly."""
         return self._run(bit_map, x, absmean, plane=False)
+
+
+@functools.lru_cache(maxsize=None)
+def _block_nearest(n_in, n_out):
+    """True when ATen's nearest index floor(o * fp32(n_in / n_out)) is the block
+    index o // (n_out / n_in) for every output o (UpSampleKernel nearest_idx)."""
+    if n_out % n_in:
+        return False
+    s = n_out // n_in
+    sc = torch.tensor(n_in / n_out, dtype=torch.float32)
+    o = torch.arange(n_out, dtype=torch.float32)
+    return bool(torch.equal(torch.floor(o * sc).long(), torch.arange(n_out) // s))
+
+
+def _nearest_up(m, H, W):
+    """F.interpolate(m, (H, W), 'nearest') with the same values; on the GPU,
+    when the index map is a block map, as an expand whose backward is a
+    per-tile sum (ATen's upsample_nearest2d_backward kernel takes ~67 us per
+    call at config 5).  CPU tensors keep the reference op (bit-exact grads)."""
+    Ht, Wt = m.shape[-2:]
+    if m.is_cuda and _block_nearest(Ht, H) and _block_nearest(Wt, W):
+        B, C = m.shape[:2]
+        return m[:, :, :, None, :, None].expand(B, C, Ht, H // Ht, Wt, W // Wt).reshape(B, C, H, W)
+    return F.interpolate(m, size=(H, W), mode="nearest")
 
 
 class _SoftMaskFn(torch.autograd.Function):
