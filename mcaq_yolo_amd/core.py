@@ -108,20 +108,20 @@ _MFMA_IDX = {}
 
 def _mfma_a_operands(w):
     """Device version of params.mfma_a_operands: (N_out, K) weight -> A operands
-    of v_mfma_f32_32x32x2_f32 ([block][step][lane], lane l holds
-    W[32*block + (l & 31)][2*step + (l >> 5)], K zero-padded to even)."""
+    of v_mfma_f32_16x16x4_f32 ([block][step][lane], lane l holds
+    W[16*block + (l & 15)][4*step + (l >> 4)], K zero-padded to a multiple of 4)."""
     n, k = w.shape
-    kp = k + (k & 1)
-    nb = (n + 31) // 32
+    kp = (k + 3) // 4 * 4
+    nb = (n + 15) // 16
     key = (n, k, w.device)
     idx = _MFMA_IDX.get(key)
     if idx is None:
         b = torch.arange(nb).view(nb, 1, 1)
-        s = torch.arange(kp // 2).view(1, kp // 2, 1)
+        s = torch.arange(kp // 4).view(1, kp // 4, 1)
         lane = torch.arange(64).view(1, 1, 64)
-        idx = ((32 * b + (lane & 31)) * kp + 2 * s + (lane >> 5)).reshape(-1).to(w.device)
+        idx = ((16 * b + (lane & 15)) * kp + 4 * s + (lane >> 4)).reshape(-1).to(w.device)
         _MFMA_IDX[key] = idx
-    wp = torch.zeros(nb * 32, kp, device=w.device, dtype=torch.float32)
+    wp = torch.zeros(nb * 16, kp, device=w.device, dtype=torch.float32)
     wp[:n, :k] = w
     return wp.reshape(-1)[idx]
 

@@ -441,6 +441,7 @@ __global__ __launch_bounds__(256) void mcaq_finalize_kernel(FinalizeArgs a) {
 // morph pass B: one 256-thread workgroup per (scale, image), tile grid in LDS
 // ---------------------------------------------------------------------------
 constexpr int TILES_THREADS = 256;
+constexpr int TILES_SCRATCH_BYTES = 4 * (TILES_THREADS / 64) * MLP_SCRATCH_FLOATS;   // 34816
 #ifndef MCAQ_MORPH_THREADS
 #define MCAQ_MORPH_THREADS 1024
 #endif
@@ -515,11 +516,12 @@ __global__ __launch_bounds__(TILES_THREADS, MCAQ_TILES_MINW) void mcaq_tiles_ker
   const int g = (int)threadIdx.x / G;
   const int b = imin_(((int)blockIdx.x - a.twg_begin[si]) * ipw + g, S.B - 1);
   float* wl = wlds ? reinterpret_cast<float*>(smem) : nullptr;
-  char* base = smem + (wlds ? weights_lds_bytes() : 0) + (size_t)g * a.tgstride[si];
+  float* xs = reinterpret_cast<float*>(smem + (wlds ? weights_lds_bytes() : 0));   // MLP scratch, per wave
+  char* base = smem + (wlds ? weights_lds_bytes() : 0) + TILES_SCRATCH_BYTES + (size_t)g * a.tgstride[si];
   Ctx ctx{(int)threadIdx.x - g * G, G};
   Shared sh;
   carve_shared(base, sh);
-  morph_tiles(ctx, S, b, sh, wl, (int)threadIdx.x, TILES_THREADS);
+  morph_tiles(ctx, S, b, sh, wl, (int)threadIdx.x, TILES_THREADS, xs);
 }
 
 // ---------------------------------------------------------------------------
@@ -935,10 +937,10 @@ int mcaq_morph_finalize(const mcaq_morph_scale* scales, int nscales, const mcaq_
     }
     a.twg_begin[nscales] = twg;
     const int lim = MCAQ_MORPH_LDS_LIMIT - 1024;
-    if (per > lim) return (int)hipErrorInvalidValue;
-    // stage the weight blobs in LDS when they fit beside the tile arrays
-    const int wlds = per + weights_lds_bytes() <= lim;
-    const size_t tdyn = (size_t)per + (wlds ? weights_lds_bytes() : 0);
+    if (per + TILES_SCRATCH_BYTES > lim) return (int)hipErrorInvalidValue;
+    // stage the weight blobs in LDS when they fit beside the tile arrays and the MLP scratch
+    const int wlds = per + TILES_SCRATCH_BYTES + weights_lds_bytes() <= lim;
+    const size_t tdyn = (size_t)per + TILES_SCRATCH_BYTES + (wlds ? weights_lds_bytes() : 0);
     static int set_tiles = 0;
     if ((int)tdyn > set_tiles) {
       hipError_t ae = hipFuncSetAttribute((const void*)mcaq_tiles_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lim);

@@ -510,6 +510,12 @@ MCAQ_HD void sort_tiles(const Ctx& ctx, float* tiles, int NT, int src) {
 }
 
 }  // namespace mcaq
+// per-wave activation scratch of the MFMA tile MLPs (mcaq_mlp_mfma.h): 32 tiles
+// x MLP_XS floats (MLP_XS = 68: the B-operand reads of 16 tiles x 4 k-rows hit
+// 64 distinct banks)
+constexpr int MLP_XS = 68;
+constexpr int MLP_SCRATCH_FLOATS = 32 * MLP_XS;
+
 #if defined(__HIP_DEVICE_COMPILE__)
 #include "mcaq_mlp_mfma.h"   // fp32 MFMA versions of the tile MLPs (device only)
 #endif
@@ -1405,7 +1411,9 @@ MCAQ_HD int tiles_lds_bytes(int H, int W, int NT) {
   return fixed_bytes() + tile_bytes(NT) + extra_bytes(H, W, NT) + 100 * NT;
 }
 
-MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh, float* wl, int wtid, int wnthr) {
+// xs: the workgroup's MLP activation scratch (MLP_SCRATCH_FLOATS per wave), device only
+MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh, float* wl, int wtid, int wnthr,
+                         float* xs) {
   const int ht = S.ht, wt = S.wt, NT = ht * wt;
   float* tiles = sh.tiles;
   float* extra = tiles + NT * TILE_FLOATS;            // compact per-tile arrays / tables
@@ -1421,7 +1429,7 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
   if (wl && (S.flags & F_MAPPER) && !(S.flags & F_MAP_LINEAR)) Pmap = wl + WL_MM;
   if (wl && (S.flags & F_SOFTMASK)) Pm = wl + WL_SM;
 #else
-  (void)wl; (void)wtid; (void)wnthr;
+  (void)wl; (void)wtid; (void)wnthr; (void)xs;
   int S_ = 0;
   for (int s = 2; s <= S.tile; s *= 2) ++S_;
   const int NI = 20 + S_;
@@ -1451,8 +1459,9 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
 #if defined(__HIP_DEVICE_COMPILE__)
     for (int blk = ctx.tid >> 6; blk * 32 < NT; blk += ctx.nthr >> 6) {
       const bool st = b == 0 && blk == 0 && ctx.nthr == 256;
-      if (wl) cmlp_block_mfma((lds_cf)Pc, tiles, NT, blk * 32, ctx.tid & 63, st);
-      else cmlp_block_mfma(Pc, tiles, NT, blk * 32, ctx.tid & 63, st);
+      const lds_f xw = (lds_f)(xs + (threadIdx.x >> 6) * MLP_SCRATCH_FLOATS);
+      if (wl) cmlp_block_mfma((lds_cf)Pc, tiles, NT, blk * 32, ctx.tid & 63, xw, st);
+      else cmlp_block_mfma(Pc, tiles, NT, blk * 32, ctx.tid & 63, xw, st);
     }
     MSTAMP(28);
 #else
@@ -1573,10 +1582,11 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
       MSTAMP(30);
       for (int blk = ctx.tid >> 6; blk * 32 < NT; blk += ctx.nthr >> 6) {
         const bool st = b == 0 && blk == 0 && ctx.nthr == 256;
+        const lds_f xw = (lds_f)(xs + (threadIdx.x >> 6) * MLP_SCRATCH_FLOATS);
         if (wl) mapper_block_mfma((lds_cf)Pmap, (lds_cf)ab, tiles, NT, blk * 32, ctx.tid & 63, csrc, S.min_bits,
-                                  S.max_bits, st);
+                                  S.max_bits, xw, st);
         else mapper_block_mfma((const float*)Pmap, (const float*)ab, tiles, NT, blk * 32, ctx.tid & 63, csrc,
-                               S.min_bits, S.max_bits, st);
+                               S.min_bits, S.max_bits, xw, st);
       }
 #else
       MFOR(t, NT) tiles[t * TILE_FLOATS + T_AUX] =

@@ -27,20 +27,20 @@ def _f(a):
 
 
 def mfma_a_operands(Wm):
-    """Weight matrix (N_out, K) -> A operands of v_mfma_f32_32x32x2_f32 for the
+    """Weight matrix (N_out, K) -> A operands of v_mfma_f32_16x16x4_f32 for the
     transposed product D[neuron][tile]: [block][step][lane] with lane l holding
-    W[32*block + (l & 31)][2*step + (l >> 5)] (K zero-padded to even)."""
+    W[16*block + (l & 15)][4*step + (l >> 4)] (K zero-padded to a multiple of 4)."""
     Wm = np.asarray(Wm, np.float32)
     n, k = Wm.shape
-    kp = k + (k & 1)
-    nb = (n + 31) // 32
-    Wp = np.zeros((nb * 32, kp), np.float32)
+    kp = (k + 3) // 4 * 4
+    nb = (n + 15) // 16
+    Wp = np.zeros((nb * 16, kp), np.float32)
     Wp[:n, :k] = Wm
     lane = np.arange(64)
-    out = np.empty((nb, kp // 2, 64), np.float32)
+    out = np.empty((nb, kp // 4, 64), np.float32)
     for b in range(nb):
-        for s in range(kp // 2):
-            out[b, s] = Wp[32 * b + (lane & 31), 2 * s + (lane >> 5)]
+        for s in range(kp // 4):
+            out[b, s] = Wp[16 * b + (lane & 15), 4 * s + (lane >> 4)]
     return out.reshape(-1)
 
 

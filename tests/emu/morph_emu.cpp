@@ -26,7 +26,7 @@ extern "C" int emu_morph(const mcaq_morph_scale* s) {
     }
     Shared sh2;
     carve_shared(tshm.data(), sh2);
-    morph_tiles(ctx, *s, b, sh2, nullptr, 0, 1);
+    morph_tiles(ctx, *s, b, sh2, nullptr, 0, 1, nullptr);
   }
   return 0;
 }

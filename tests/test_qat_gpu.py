@@ -172,6 +172,59 @@ def test_hook_train_step_gradients():
     assert all(q.running_min is not None for q in h.quantizers.values())
 
 
+def test_hook_train_step_linear_mapper_gradients():
+    """with bit_mapping='linear' the bit map stays differentiable on
+    the GPU path too (bit_allocation.py:42-80): the quantizer's and the bit
+    loss's gradients reach the complexity MLP."""
+    from mcaq_yolo_amd.hooks import MCAQHooks
+    torch.manual_seed(0)
+    h = MCAQHooks(device=DEV, bit_mapping="linear").train()
+    gen = torch.Generator(device="cpu").manual_seed(6)
+    feats = [torch.nn.functional.silu(1.5 * torch.randn(2, c, s, s, generator=gen)).to(DEV).requires_grad_(True)
+             for c, s in ((64, 80), (128, 40), (256, 20))]
+    outs, aux = h.forward_features(feats, temperature=1.0)
+    loss = sum((o * o).mean() for o in outs) + (MCAQHooks.avg_bits(aux) - 4.0) ** 2
+    loss.backward()
+    gp = dict(h.named_parameters())["complexity_analyzer.complexity_mlp.0.weight"].grad
+    assert gp is not None and torch.isfinite(gp).all() and float(gp.abs().sum()) > 0
+
+
+def test_qat_misaligned_views_match_aligned():
+    """contiguous views whose storage offset is not a multiple of 16
+    bytes take the scalar kernels (the float4 ones need aligned x/y/g/gx);
+    results equal the aligned run."""
+    from mcaq_yolo_amd import core
+    B, C, H, W, ht, wt = 2, 40, 20, 20, 5, 5
+    gen = torch.Generator(device="cpu").manual_seed(12)
+    n = B * C * H * W
+    xs = torch.randn(n + 1, generator=gen).to(DEV)[1:].view(B, C, H, W)      # 4-byte offset
+    gs = torch.randn(n + 1, generator=gen).to(DEV)[1:].view(B, C, H, W)
+    assert xs.is_contiguous() and xs.data_ptr() % 16 != 0
+    bits = (torch.rand(B, ht, wt, generator=gen) * 6 + 2).to(DEV)
+    m = torch.rand(B, H, W, generator=gen).to(DEV)
+    mn, mx = core._channel_minmax(xs.clone())
+    y1 = core.qat_quantize(xs, bits, m, mn, mx)
+    y2 = core.qat_quantize(xs.clone(), bits, m, mn, mx)
+    assert torch.equal(y1, y2)
+    g1 = core.qat_quantize_backward(gs, xs, bits, m, mn, mx)
+    g2 = core.qat_quantize_backward(gs.clone(), xs.clone(), bits, m, mn, mx)
+    for a, b in zip(g1, g2):
+        assert torch.equal(a, b)
+
+
+def test_spatial_quantize_misaligned_view():
+    from mcaq_yolo_amd import mcaq_cuda_ops
+    B, C, H, W = 2, 16, 16, 16
+    gen = torch.Generator(device="cpu").manual_seed(13)
+    xs = torch.randn(B * C * H * W + 3, generator=gen).to(DEV)[3:].view(B, C, H, W)
+    assert xs.data_ptr() % 16 != 0
+    bits = torch.randint(2, 9, (B, 4, 4), generator=gen).float().to(DEV)
+    mn, mx = xs.amin(dim=(0, 2, 3)), xs.amax(dim=(0, 2, 3))
+    y1 = mcaq_cuda_ops.spatial_quantize(xs, bits, mn, mx, 4, 4)
+    y2 = mcaq_cuda_ops.spatial_quantize(xs.clone(), bits, mn, mx, 4, 4)
+    assert torch.equal(y1, y2)
+
+
 def _allclose_rel(got, ref, rtol, floor=1e-30):
     """max |got - ref| <= rtol * max(|ref|, floor).  `floor` covers gradients
     that are zero in exact arithmetic (a Linear bias feeding a train-mode
