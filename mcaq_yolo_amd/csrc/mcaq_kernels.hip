@@ -56,7 +56,7 @@ constexpr int ST_LDS = 4096;  // floats of LDS (block sums; tail block sums)
 #define MCAQ_STATS_MINW 4
 #endif
 #ifndef MCAQ_STATS_PPL_R2   // pixels per lane when the channels take 2 rounds of blocks
-#define MCAQ_STATS_PPL_R2 2
+#define MCAQ_STATS_PPL_R2 4
 #endif
 #ifndef MCAQ_STATS_PPL_R4   // ... 3 or more rounds
 #define MCAQ_STATS_PPL_R4 1

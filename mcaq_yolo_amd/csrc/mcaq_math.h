@@ -119,6 +119,15 @@ MCAQ_HD float aten_sum(int n, bool tail, Load load) {
 // Column index where ATen's tail (row_sum) order starts for M columns.
 MCAQ_HD int aten_tail_start(int M) { return (M / 32) * 32; }
 
+// a / b for 0 <= a < 2^24, b >= 1 without an integer division: the fp32
+// estimate is within one of the quotient, then corrected (exact)
+MCAQ_HD int div_small(int a, int b, float inv_b) {
+  int q = (int)((float)a * inv_b);
+  q -= (q * b > a) ? 1 : 0;
+  q += ((q + 1) * b <= a) ? 1 : 0;
+  return q;
+}
+
 // PyTorch upsample 'nearest' source index (UpSampleKernel nearest_idx).
 MCAQ_HD int nearest_src(int o, int in_size, int out_size) {
   if (out_size == in_size) return o;

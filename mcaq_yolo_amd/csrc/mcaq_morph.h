@@ -1138,18 +1138,20 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, P
     float* ttmp = S.tile_tmp + (size_t)b * NT * TT_STRIDE;
     const int nG = role ? (4 * NT + 63) & ~63 : (S_ * NT + 63) & ~63;
     const int nR = role ? 15 * NT : NT;
+    const float inv_nt = 1.0f / (float)NT, inv_wt = 1.0f / (float)wt;
     MFOR(u, nG + nR) {
       int it, t;
       if (u < nG) {
         const int nit = role ? 4 : S_;
         if (u >= nit * NT) continue;
-        it = (role ? 0 : 4) + u / NT; t = u - (u / NT) * NT;
+        const int kq = div_small(u, NT, inv_nt);
+        it = (role ? 0 : 4) + kq; t = u - kq * NT;
       } else {
-        const int v = u - nG, kk = v / NT;
+        const int v = u - nG, kk = div_small(v, NT, inv_nt);
         t = v - kk * NT;
         it = role ? (kk < 10 ? 4 + S_ + kk : 15 + S_ + (kk - 10)) : 14 + S_;
       }
-      const int th = t / wt, tw = t - (t / wt) * wt;
+      const int th = div_small(t, wt, inv_wt), tw = t - th * wt;
       const int h0 = th * T, w0 = tw * T;
       float val;
       if (it < 4) {
@@ -1415,6 +1417,7 @@ MCAQ_HD int tiles_lds_bytes(int H, int W, int NT) {
 MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh, float* wl, int wtid, int wnthr,
                          float* xs) {
   const int ht = S.ht, wt = S.wt, NT = ht * wt;
+  const float inv_wt = 1.0f / (float)wt;
   float* tiles = sh.tiles;
   float* extra = tiles + NT * TILE_FLOATS;            // compact per-tile arrays / tables
   float* wbuf = (float*)((char*)extra + extra_bytes(S.H, S.W, NT));
@@ -1485,7 +1488,7 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
       constexpr int BK = 12;
       auto wgt = [&](int u) {
         const int t = u / 25, k = u - (u / 25) * 25;
-        const int th = t / wt, tw = t - (t / wt) * wt;
+        const int th = div_small(t, wt, inv_wt), tw = t - th * wt;
         const int hh = imin_(imax_(th + k / 5 - 2, 0), ht - 1);
         const int ww = imin_(imax_(tw + k % 5 - 2, 0), wt - 1);
         const float d = extra[hh * wt + ww] - extra[t];
@@ -1494,9 +1497,10 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
       bcopy<BK>(ctx, NT * 25, wgt, [&](int u, float v) { wbuf[u] = v; });
       MSYNC();
     }
+    MSTAMP(29);
     const int cut = aten_tail_start(NT);
     MFOR(t, NT) {
-      const int th = t / wt, tw = t - (t / wt) * wt;
+      const int th = div_small(t, wt, inv_wt), tw = t - th * wt;
       // 25-row ATen outer sums of w*p and w: vector column = rows 0..15 folded,
       // then 16..24 in a0; tail column = 4 interleaved partials (rows 4i+q),
       // row 24 into partial 0.  Adding an exact +0 is an identity (sums never
@@ -1616,7 +1620,7 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
     const int KH = H / ht, KW = W / wt;
     const bool even = KH * ht == H && KW * wt == W && KH == KW;
     MFOR(t, NT) {
-      const int i = t / wt, j = t - (t / wt) * wt;
+      const int i = div_small(t, wt, inv_wt), j = t - i * wt;
       float a;
       if (even && KH == 4) a = (window_sum_t<4>(am, W, i * 4, j * 4) / 4.0f) / 4.0f;
       else if (even && KH == 8) a = (window_sum_t<8>(am, W, i * 8, j * 8) / 8.0f) / 8.0f;
@@ -1632,6 +1636,7 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
       lmx = fmax_(lmx, a);
     }
     const float amax = block_max(ctx, sh, lmx);
+    MSTAMP(31);
     const float den = amax + 1e-8f;
     // the two conv input features, compact: f0 = bits feature, f1 = activation
     float* f0a = extra;
@@ -1642,7 +1647,7 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
     }
     MSYNC();
     MFOR(t, NT) {
-      const int i = t / wt, j = t - (t / wt) * wt;
+      const int i = div_small(t, wt, inv_wt), j = t - i * wt;
       // 3x3 window (zero pad): (kh, kw) outer, ic inner, FMA from 0, + bias;
       // out-of-grid taps are skipped exactly as the reference's zero taps
       float f0[9], f1[9];
@@ -1673,8 +1678,11 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
         l0 = fmaf(Pm[SM_W2 + ic], hv, l0);
         l1 = fmaf(Pm[SM_W2 + 8 + ic], hv, l1);
       }
+      // softmax over 2: the larger logit's term is exp(+0) = 1 exactly
       const float mxl = fmax_(l0, l1);
-      const float e0 = cr_exp(l0 - mxl), e1 = cr_exp(l1 - mxl);
+      const bool first = l0 >= l1;
+      const float e = cr_exp((first ? l1 : l0) - mxl);
+      const float e0 = first ? 1.0f : e, e1 = first ? e : 1.0f;
       const float mtv = e0 / (e0 + e1);
       tiles[t * TILE_FLOATS + T_MT] = mtv;
       if (S.mt_out) S.mt_out[(size_t)b * NT + t] = mtv;

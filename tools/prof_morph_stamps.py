@@ -16,11 +16,11 @@ from mcaq_yolo_amd import abi  # noqa: E402
 STAGES = [(0, 1, "E gray+norm"), (1, 2, "E blur+hist"), (2, 3, "E otsu"), (3, 4, "E sobel255+dir"),
           (4, 5, "E nms"), (5, 6, "E hysteresis"), (8, 9, "E tile items"),
           (16, 17, "M gray+norm"), (17, 23, "M binarize"), (23, 24, "M sobel+lbp+planes"), (24, 25, "M tile items"),
-          (10, 26, "B stage loads"), (26, 27, "B assemble phi"), (27, 28, "B cmlp mfma"), (28, 11, "B cmlp out"), (11, 12, "B bilateral"), (12, 13, "B mapper"), (12, 30, "B  mapper: BN fold"), (30, 13, "B  mapper: MLP + finish"),
+          (10, 26, "B stage loads"), (26, 27, "B assemble phi"), (27, 28, "B cmlp mfma"), (28, 11, "B cmlp out"), (11, 12, "B bilateral"), (11, 29, "B  bilateral: weights (exp)"), (29, 12, "B  bilateral: 25-tap sums"), (12, 13, "B mapper"), (12, 30, "B  mapper: BN fold"), (30, 13, "B  mapper: MLP + finish"),
           (40, 41, "B  w0 cmlp L1"), (41, 42, "B  w0 cmlp LN1"), (42, 43, "B  w0 cmlp L2"), (43, 44, "B  w0 cmlp LN2"),
           (44, 45, "B  w0 cmlp L3+sigmoid"), (48, 49, "B  w0 map in (log1p)"), (49, 50, "B  w0 map L1+BN"),
           (50, 51, "B  w0 map L2+BN"), (51, 52, "B  w0 map L3+BN"), (52, 53, "B  w0 map L4 dot"), (53, 54, "B  w0 map sigmoid"),
-          (13, 14, "B softmask tiles"),
+          (13, 14, "B softmask tiles"), (13, 31, "B  softmask: pool |x| + max"), (31, 14, "B  softmask: net + softmax"),
           (14, 15, "B m plane")]
 
 
