@@ -440,8 +440,8 @@ __global__ __launch_bounds__(256) void mcaq_finalize_kernel(FinalizeArgs a) {
 // morph pass A: one 1024-thread workgroup per (scale, image), planes in LDS
 // morph pass B: one 256-thread workgroup per (scale, image), tile grid in LDS
 // ---------------------------------------------------------------------------
-constexpr int TILES_THREADS = 256;
-constexpr int TILES_SCRATCH_BYTES = 4 * (TILES_THREADS / 64) * MLP_SCRATCH_FLOATS;   // 34816
+constexpr int TILES_THREADS = MCAQ_TILES_THREADS;
+constexpr int TILES_SCRATCH_BYTES = 4 * (TILES_THREADS / 64) * MLP_SCRATCH_FLOATS;   // 34816 at 256 or 512
 #ifndef MCAQ_MORPH_THREADS
 #define MCAQ_MORPH_THREADS 1024
 #endif
@@ -920,8 +920,8 @@ int mcaq_morph_finalize(const mcaq_morph_scale* scales, int nscales, const mcaq_
     if (le != hipSuccess) return (int)le;
   }
   if (any_tiles) {
-    // pass B packing: one image per workgroup when it has more than 32 tiles
-    // (one MLP block per wave), else 4 images of one wave each
+    // pass B packing: the waves an image needs for one MLP block of MLP_TPW
+    // tiles each (at most the whole workgroup); small images share a workgroup
     int twg = 0, per = 0;
     for (int i = 0; i < nscales; ++i) {
       const MorphScale& S = a.s[i];
@@ -929,7 +929,7 @@ int mcaq_morph_finalize(const mcaq_morph_scale* scales, int nscales, const mcaq_
       a.tipw[i] = 1; a.tgstride[i] = 0;
       if (!(S.flags & (F_PHI | F_CMLP | F_MAPPER | F_SOFTMASK))) continue;
       const int NT = S.ht * S.wt;
-      const int G = imin_(TILES_THREADS, 64 * ((NT + 31) / 32));
+      const int G = imin_(TILES_THREADS, 64 * ((NT + MLP_TPW - 1) / MLP_TPW));
       a.tipw[i] = TILES_THREADS / G;
       a.tgstride[i] = (tiles_lds_bytes(S.H, S.W, NT) + 15) & ~15;
       per = imax_(per, a.tipw[i] * a.tgstride[i]);

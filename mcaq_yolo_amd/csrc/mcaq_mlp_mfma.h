@@ -5,7 +5,8 @@
 // chaining K/4 of them from C = 0 reproduces the oracle's Linear exactly:
 // sequential FMA over k = 0..K-1 from 0, then + bias.
 //
-// One wave owns a block of 32 tiles = two 16-tile halves h.  Layout
+// One wave owns a block of 16*NH tiles = NH 16-tile halves h (NH = 1 with
+// 512-thread pass B workgroups, 2 with 256).  Layout
 // (transposed product, M = neurons, N = tiles):
 //   A (16 neurons x 4 k): lane l holds W[16*mb + (l&15)][4s + (l>>4)]
 //   B (4 k x 16 tiles)  : lane l holds X[tile 16h + (l&15)][4s + (l>>4)]
@@ -66,12 +67,12 @@ __device__ __forceinline__ f32x4 mf16(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// D (two tile halves x NB neuron blocks) -> X[tile][neuron]
-template <int NB>
-__device__ __forceinline__ void d_store(lds_f xs, const f32x4 (&D)[2][NB], int j, int q) {
+// D (NH tile halves x NB neuron blocks) -> X[tile][neuron]
+template <int NH, int NB>
+__device__ __forceinline__ void d_store(lds_f xs, const f32x4 (&D)[NH][NB], int j, int q) {
   MLP_WAVE_FENCE();
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+  for (int h = 0; h < NH; ++h)
 #pragma unroll
     for (int mb = 0; mb < NB; ++mb)
 #pragma unroll
@@ -80,13 +81,13 @@ __device__ __forceinline__ void d_store(lds_f xs, const f32x4 (&D)[2][NB], int j
 }
 
 // Linear without bias, K inputs from X, 16*NB outputs: 2*NB chains of K/4 steps
-template <int K, int NB, typename PT>
-__device__ __forceinline__ void layer16(PT A, lds_f xs, f32x4 (&D)[2][NB], int lane) {
+template <int K, int NH, int NB, typename PT>
+__device__ __forceinline__ void layer16(PT A, lds_f xs, f32x4 (&D)[NH][NB], int lane) {
   constexpr int KS = K / 4;
   const int j = lane & 15, q = lane >> 4;
-  float bb[2][KS], aa[NB][KS];
+  float bb[NH][KS], aa[NB][KS];
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+  for (int h = 0; h < NH; ++h)
 #pragma unroll
     for (int s = 0; s < KS; ++s) bb[h][s] = xs[(16 * h + j) * MLP_XS + 4 * s + q];
 #pragma unroll
@@ -94,22 +95,22 @@ __device__ __forceinline__ void layer16(PT A, lds_f xs, f32x4 (&D)[2][NB], int l
 #pragma unroll
     for (int s = 0; s < KS; ++s) aa[mb][s] = A[(mb * KS + s) * 64 + lane];
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+  for (int h = 0; h < NH; ++h)
 #pragma unroll
     for (int mb = 0; mb < NB; ++mb) D[h][mb] = zero4();
 #pragma unroll
   for (int s = 0; s < KS; ++s)
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < NH; ++h)
 #pragma unroll
       for (int mb = 0; mb < NB; ++mb) D[h][mb] = mf16(aa[mb][s], bb[h][s], D[h][mb]);
 }
 
 // + bias per neuron
-template <int NB, typename PT>
-__device__ __forceinline__ void add_bias(f32x4 (&D)[2][NB], PT b, int q) {
+template <int NH, int NB, typename PT>
+__device__ __forceinline__ void add_bias(f32x4 (&D)[NH][NB], PT b, int q) {
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+  for (int h = 0; h < NH; ++h)
 #pragma unroll
     for (int mb = 0; mb < NB; ++mb)
 #pragma unroll
@@ -163,10 +164,10 @@ __device__ __forceinline__ void layernorm16(f32x4 (&d)[NB], PT g, PT b, int q) {
 }
 
 // BN eval with the folded per-neuron (alpha, beta), then ReLU
-template <int NB, typename PT>
-__device__ __forceinline__ void bn_relu16(f32x4 (&D)[2][NB], PT alpha, PT beta, int q) {
+template <int NH, int NB, typename PT>
+__device__ __forceinline__ void bn_relu16(f32x4 (&D)[NH][NB], PT alpha, PT beta, int q) {
 #pragma unroll
-  for (int h = 0; h < 2; ++h)
+  for (int h = 0; h < NH; ++h)
 #pragma unroll
     for (int mb = 0; mb < NB; ++mb)
 #pragma unroll
@@ -176,17 +177,17 @@ __device__ __forceinline__ void bn_relu16(f32x4 (&D)[2][NB], PT alpha, PT beta, 
       }
 }
 
-// complexity MLP for the 32 tiles [t0, t0+32) of one image; writes T_CMLP
-template <typename PT>
+// complexity MLP for the 16*NH tiles [t0, t0+16*NH) of one image; writes T_CMLP
+template <int NH, typename PT>
 __device__ void cmlp_block_mfma(PT P, float* tiles, int NT, int t0, int lane, lds_f xs, bool stamp = false) {
   const int j = lane & 15, q = lane >> 4;
   WSTAMP(stamp, 40);
   // layer 1: 8 -> 64 from phi (2 k-steps)
-  f32x4 D1[2][4];
+  f32x4 D1[NH][4];
   {
-    float bb[2][2], aa[4][2];
+    float bb[NH][2], aa[4][2];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < NH; ++h) {
       const int t = t0 + 16 * h + j;
       const float* tp = tiles + (t < NT ? t : 0) * TILE_FLOATS + T_PHI;
 #pragma unroll
@@ -197,39 +198,39 @@ __device__ void cmlp_block_mfma(PT P, float* tiles, int NT, int t0, int lane, ld
 #pragma unroll
       for (int s = 0; s < 2; ++s) aa[mb][s] = P[CMQ_W1 + (mb * 2 + s) * 64 + lane];
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < NH; ++h)
 #pragma unroll
       for (int mb = 0; mb < 4; ++mb) D1[h][mb] = zero4();
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
-      for (int h = 0; h < 2; ++h)
+      for (int h = 0; h < NH; ++h)
 #pragma unroll
         for (int mb = 0; mb < 4; ++mb) D1[h][mb] = mf16(aa[mb][s], bb[h][s], D1[h][mb]);
   }
-  add_bias<4>(D1, P + CM_B1, q);
+  add_bias<NH, 4>(D1, P + CM_B1, q);
   WSTAMP(stamp, 41);
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < NH; ++h) {
     layernorm16<4>(D1[h], P + CM_G1, P + CM_BE1, q);
 #pragma unroll
     for (int mb = 0; mb < 4; ++mb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) D1[h][mb][r] = fmax_(D1[h][mb][r], 0.0f);
   }
-  d_store<4>(xs, D1, j, q);
+  d_store<NH, 4>(xs, D1, j, q);
   WSTAMP(stamp, 42);
   // layer 2: 64 -> 32
-  f32x4 D2[2][2];
-  layer16<64, 2>(P + CMQ_W2, xs, D2, lane);
-  add_bias<2>(D2, P + CM_B2, q);
+  f32x4 D2[NH][2];
+  layer16<64, NH, 2>(P + CMQ_W2, xs, D2, lane);
+  add_bias<NH, 2>(D2, P + CM_B2, q);
   WSTAMP(stamp, 43);
 #pragma unroll
-  for (int h = 0; h < 2; ++h) layernorm16<2>(D2[h], P + CM_G2, P + CM_BE2, q);
-  d_store<2>(xs, D2, j, q);
+  for (int h = 0; h < NH; ++h) layernorm16<2>(D2[h], P + CM_G2, P + CM_BE2, q);
+  d_store<NH, 2>(xs, D2, j, q);
   WSTAMP(stamp, 44);
   // layer 3: 32 -> 1 (ReLU inside the sequential dot), sigmoid; lane = tile
-  if (lane < 32) {
+  if (lane < 16 * NH) {
     const int t = t0 + lane;
     float acc = 0.0f;
 #pragma unroll
@@ -240,25 +241,25 @@ __device__ void cmlp_block_mfma(PT P, float* tiles, int NT, int t0, int lane, ld
   WSTAMP(stamp, 45);
 }
 
-// MLP bit mapper for the tiles [t0, t0+32): pre-temperature bits into T_AUX
+// MLP bit mapper for the tiles [t0, t0+16*NH): pre-temperature bits into T_AUX
 // ab: folded BN terms in LDS, alpha at [0,128) and beta at [128,256) for the
 // 32 + 64 + 32 neurons of BN1/BN2/BN3 (mcaq_morph.h, bn fold)
-template <typename PT>
+template <int NH, typename PT>
 __device__ void mapper_block_mfma(PT P, PT ab, float* tiles, int NT, int t0, int lane, int csrc, float min_bits,
                                   float max_bits, lds_f xs, bool stamp = false) {
   const int j = lane & 15, q = lane >> 4;
   WSTAMP(stamp, 48);
   // layer 1: 3 -> 32, features (c, c^2, log1p c, 0) on k = q
-  f32x4 D1[2][2];
+  f32x4 D1[NH][2];
   {
-    // lane l < 32 evaluates log1p for tile l once; lanes (q = 2, j) of half h
-    // take it from lane 16h + j
-    const int tl = t0 + (lane & 31);
+    // lane l < 16*NH evaluates log1p for tile l once; lanes (q = 2, j) of
+    // half h take it from lane 16h + j
+    const int tl = t0 + (lane & (16 * NH - 1));
     const float cl = clampf_(tl < NT ? tiles[tl * TILE_FLOATS + csrc] : 0.0f, 0.0f, 1.0f);
-    const float lg = lane < 32 ? cr_log1p(cl) : 0.0f;
-    float bb[2];
+    const float lg = lane < 16 * NH ? cr_log1p(cl) : 0.0f;
+    float bb[NH];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < NH; ++h) {
       const int t = t0 + 16 * h + j;
       float c = t < NT ? tiles[t * TILE_FLOATS + csrc] : 0.0f;
       c = clampf_(c, 0.0f, 1.0f);
@@ -267,30 +268,30 @@ __device__ void mapper_block_mfma(PT P, PT ab, float* tiles, int NT, int t0, int
     }
     WSTAMP(stamp, 49);
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int h = 0; h < NH; ++h)
 #pragma unroll
       for (int mb = 0; mb < 2; ++mb) D1[h][mb] = mf16(P[MMQ_W1 + mb * 64 + lane], bb[h], zero4());
   }
-  add_bias<2>(D1, P + MM_B1, q);
-  bn_relu16<2>(D1, ab, ab + 128, q);
-  d_store<2>(xs, D1, j, q);
+  add_bias<NH, 2>(D1, P + MM_B1, q);
+  bn_relu16<NH, 2>(D1, ab, ab + 128, q);
+  d_store<NH, 2>(xs, D1, j, q);
   WSTAMP(stamp, 50);
   // layer 2: 32 -> 64
-  f32x4 D2[2][4];
-  layer16<32, 4>(P + MMQ_W2, xs, D2, lane);
-  add_bias<4>(D2, P + MM_B2, q);
-  bn_relu16<4>(D2, ab + 32, ab + 160, q);
-  d_store<4>(xs, D2, j, q);
+  f32x4 D2[NH][4];
+  layer16<32, NH, 4>(P + MMQ_W2, xs, D2, lane);
+  add_bias<NH, 4>(D2, P + MM_B2, q);
+  bn_relu16<NH, 4>(D2, ab + 32, ab + 160, q);
+  d_store<NH, 4>(xs, D2, j, q);
   WSTAMP(stamp, 51);
   // layer 3: 64 -> 32
-  f32x4 D3[2][2];
-  layer16<64, 2>(P + MMQ_W3, xs, D3, lane);
-  add_bias<2>(D3, P + MM_B3, q);
-  bn_relu16<2>(D3, ab + 96, ab + 224, q);
-  d_store<2>(xs, D3, j, q);
+  f32x4 D3[NH][2];
+  layer16<64, NH, 2>(P + MMQ_W3, xs, D3, lane);
+  add_bias<NH, 2>(D3, P + MM_B3, q);
+  bn_relu16<NH, 2>(D3, ab + 96, ab + 224, q);
+  d_store<NH, 2>(xs, D3, j, q);
   WSTAMP(stamp, 52);
   // layer 4: 32 -> 1 sequential dot, sigmoid, affine to [min_bits, max_bits]; lane = tile
-  if (lane < 32) {
+  if (lane < 16 * NH) {
     const int t = t0 + lane;
     float acc = 0.0f;
 #pragma unroll

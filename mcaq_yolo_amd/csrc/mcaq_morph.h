@@ -513,8 +513,15 @@ MCAQ_HD void sort_tiles(const Ctx& ctx, float* tiles, int NT, int src) {
 // per-wave activation scratch of the MFMA tile MLPs (mcaq_mlp_mfma.h): 32 tiles
 // x MLP_XS floats (MLP_XS = 68: the B-operand reads of 16 tiles x 4 k-rows hit
 // 64 distinct banks)
+#ifndef MCAQ_TILES_THREADS       // pass B workgroup size (256 or 512)
+#define MCAQ_TILES_THREADS 256
+#endif
 constexpr int MLP_XS = 68;
-constexpr int MLP_SCRATCH_FLOATS = 32 * MLP_XS;
+// tiles per wave block of the MFMA MLPs: 16 (one 16x16 half) at 512 threads,
+// 32 (two halves, more independent chains per wave) at 256
+constexpr int MLP_NH = MCAQ_TILES_THREADS >= 512 ? 1 : 2;
+constexpr int MLP_TPW = 16 * MLP_NH;
+constexpr int MLP_SCRATCH_FLOATS = MLP_TPW * MLP_XS;
 
 #if defined(__HIP_DEVICE_COMPILE__)
 #include "mcaq_mlp_mfma.h"   // fp32 MFMA versions of the tile MLPs (device only)
@@ -1460,11 +1467,11 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
   // -- complexity MLP + bilateral (morphology.py:959-968)
   if (S.flags & F_CMLP) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    for (int blk = ctx.tid >> 6; blk * 32 < NT; blk += ctx.nthr >> 6) {
-      const bool st = b == 0 && blk == 0 && ctx.nthr == 256;
+    for (int blk = ctx.tid >> 6; blk * MLP_TPW < NT; blk += ctx.nthr >> 6) {
+      const bool st = b == 0 && blk == 0 && ctx.nthr == MCAQ_TILES_THREADS;
       const lds_f xw = (lds_f)(xs + (threadIdx.x >> 6) * MLP_SCRATCH_FLOATS);
-      if (wl) cmlp_block_mfma((lds_cf)Pc, tiles, NT, blk * 32, ctx.tid & 63, xw, st);
-      else cmlp_block_mfma(Pc, tiles, NT, blk * 32, ctx.tid & 63, xw, st);
+      if (wl) cmlp_block_mfma<MLP_NH>((lds_cf)Pc, tiles, NT, blk * MLP_TPW, ctx.tid & 63, xw, st);
+      else cmlp_block_mfma<MLP_NH>(Pc, tiles, NT, blk * MLP_TPW, ctx.tid & 63, xw, st);
     }
     MSTAMP(28);
 #else
@@ -1584,12 +1591,12 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
       }
       MSYNC();
       MSTAMP(30);
-      for (int blk = ctx.tid >> 6; blk * 32 < NT; blk += ctx.nthr >> 6) {
-        const bool st = b == 0 && blk == 0 && ctx.nthr == 256;
+      for (int blk = ctx.tid >> 6; blk * MLP_TPW < NT; blk += ctx.nthr >> 6) {
+        const bool st = b == 0 && blk == 0 && ctx.nthr == MCAQ_TILES_THREADS;
         const lds_f xw = (lds_f)(xs + (threadIdx.x >> 6) * MLP_SCRATCH_FLOATS);
-        if (wl) mapper_block_mfma((lds_cf)Pmap, (lds_cf)ab, tiles, NT, blk * 32, ctx.tid & 63, csrc, S.min_bits,
+        if (wl) mapper_block_mfma<MLP_NH>((lds_cf)Pmap, (lds_cf)ab, tiles, NT, blk * MLP_TPW, ctx.tid & 63, csrc, S.min_bits,
                                   S.max_bits, xw, st);
-        else mapper_block_mfma((const float*)Pmap, (const float*)ab, tiles, NT, blk * 32, ctx.tid & 63, csrc,
+        else mapper_block_mfma<MLP_NH>((const float*)Pmap, (const float*)ab, tiles, NT, blk * MLP_TPW, ctx.tid & 63, csrc,
                                S.min_bits, S.max_bits, xw, st);
       }
 #else
