@@ -41,7 +41,7 @@ typedef void* hipEvent_t;
 extern "C" {
 #endif
 
-#define MCAQ_ABI_VERSION 5
+#define MCAQ_ABI_VERSION 6
 /* largest dynamic LDS request of the morph kernel (gfx950: 160 KiB per CU) */
 #define MCAQ_MORPH_LDS_LIMIT 163840
 
@@ -88,6 +88,8 @@ typedef struct {
   float* max_out;    /* (C) */
   int C, nunits, min_stride;
   int block_begin;   /* set by the launcher */
+  int per_tensor;    /* 1: ONE min/max over every channel, broadcast to the C
+                        outputs (per_channel=False, quantization.py:655-661) */
 } mcaq_finalize_scale;
 int mcaq_finalize(const mcaq_finalize_scale* scales, int nscales, hipStream_t stream);
 

@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libmcaq_hip.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -23,7 +23,7 @@ class StatsScale(ctypes.Structure):
 
 class FinalizeScale(ctypes.Structure):
     _fields_ = [("pmin", P), ("pmax", P), ("min_in", P), ("max_in", P), ("min_out", P), ("max_out", P),
-                ("C", I), ("nunits", I), ("min_stride", I), ("block_begin", I)]
+                ("C", I), ("nunits", I), ("min_stride", I), ("block_begin", I), ("per_tensor", I)]
 
 
 class MorphScale(ctypes.Structure):

@@ -395,6 +395,30 @@ __device__ __forceinline__ void finalize_body(const FinalizeArgs& a, int blk, fl
   while (si + 1 < a.nscales && blk >= a.s[si + 1].block_begin) ++si;
   const mcaq_finalize_scale& S = a.s[si];
   const int nthr = (int)blockDim.x, parts = nthr >> 6;
+  if (S.per_tensor) {   // one workgroup: every (unit, channel) partial, then broadcast
+    float mn = 3.402823466e38f, mx = -3.402823466e38f;
+    const int tid = (int)threadIdx.x;
+    if (S.pmin) {
+      const size_t n = (size_t)S.nunits * S.C;
+      for (size_t i = tid; i < n; i += nthr) { mn = fminf(mn, S.pmin[i]); mx = fmaxf(mx, S.pmax[i]); }
+    } else {
+      for (int c = tid; c < (S.min_stride ? S.C : 1); c += nthr) {
+        mn = fminf(mn, S.min_in[(size_t)S.min_stride * c]);
+        mx = fmaxf(mx, S.max_in[(size_t)S.min_stride * c]);
+      }
+    }
+    red[tid] = mn;
+    red[nthr + tid] = mx;
+    __syncthreads();
+    for (int h = nthr >> 1; h > 0; h >>= 1) {
+      if (tid < h) { red[tid] = fminf(red[tid], red[tid + h]); red[nthr + tid] = fmaxf(red[nthr + tid], red[nthr + tid + h]); }
+      __syncthreads();
+    }
+    mn = red[0];
+    mx = red[nthr];
+    for (int c = tid; c < S.C; c += nthr) { S.min_out[c] = mn; S.max_out[c] = mx; }
+    return;
+  }
   const int cl = threadIdx.x & 63, part = threadIdx.x >> 6;
   const int c = (blk - S.block_begin) * 64 + cl;
   const bool cv = c < S.C;
@@ -769,7 +793,7 @@ static int finalize_args(const mcaq_finalize_scale* scales, int nscales, Finaliz
     if (scales[i].C < 1 || !scales[i].min_out || !scales[i].max_out) return (int)hipErrorInvalidValue;
     if (scales[i].pmin ? (!scales[i].pmax || scales[i].nunits < 1) : (!scales[i].min_in || !scales[i].max_in))
       return (int)hipErrorInvalidValue;
-    blocks += (scales[i].C + 63) / 64;
+    blocks += scales[i].per_tensor ? 1 : (scales[i].C + 63) / 64;
   }
   a.nscales = nscales;
   a.nblocks = blocks;

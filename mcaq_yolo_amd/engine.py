@@ -114,10 +114,13 @@ class HookPlan:
 
     def prepare(self, feats, cmlp, mapper, smasks, temperature=1.0, mapper_kind="mlp", continuous=False,
                 normalize=False, minmax=None, batch_offset=0, batch_total=None, binarize_otsu=False,
-                contour_components=True, canny_legacy=False, min_bits=2.0, max_bits=8.0, quantize=True, hysteresis_iters=8):
+                contour_components=True, canny_legacy=False, min_bits=2.0, max_bits=8.0, quantize=True, hysteresis_iters=8,
+                per_tensor=False):
         """Validate inputs and build the launch descriptors (pointers are baked
         in: the tensors must stay alive and in place until the last launch).
-        minmax: optional per-scale (xmin, xmax) frozen calibration stats."""
+        minmax: optional per-scale (xmin, xmax) frozen calibration stats.
+        per_tensor: one batch min/max over all channels (per_channel=False,
+        quantization.py:655-661), broadcast to the C entries the kernel reads."""
         n = len(self.geoms)
         L = self.lib
         if len(feats) != n:
@@ -148,6 +151,7 @@ class HookPlan:
             for i, (g, b) in enumerate(zip(self.geoms, self.bufs)):
                 s = fz[i]
                 s.C, s.nunits, s.min_stride = g.C, b["units"], 1
+                s.per_tensor = 1 if per_tensor else 0
                 s.min_out, s.max_out = _p(b["xmin"]), _p(b["xmax"])
                 if minmax is not None and minmax[i] is not None:
                     lo, hi = minmax[i]

@@ -144,8 +144,6 @@ class MCAQHooks(nn.Module):
         minmax = None
         if quantizer._frozen() and quantizer.running_min is not None:
             minmax = [(quantizer.running_min.reshape(-1), quantizer.running_max.reshape(-1))]
-        elif not quantizer.per_channel:
-            raise NotImplementedError("per-tensor statistics on the fused hook path")
         an = self.complexity_analyzer
         sm = quantizer.soft_mask.blob() if (quantizer.smooth_transitions and quantizer.soft_mask is not None) \
             else None
@@ -154,7 +152,7 @@ class MCAQHooks(nn.Module):
                  mapper_kind=self.bit_mapping, normalize=self.normalize_complexity, minmax=minmax,
                  binarize_otsu=an.binarize_impl == "otsu", contour_components=an.contour_components,
                  canny_legacy=an.canny_impl == "legacy", min_bits=self.bit_mapper.min_bits, max_bits=self.bit_mapper.max_bits, quantize=quantize,
-                 process_group=self.process_group if minmax is None else None,
+                 per_tensor=not quantizer.per_channel, process_group=self.process_group if minmax is None else None,
                  batch_offset=self.batch_offset, batch_total=self.batch_total)
         feat_q = b["y"] if quantize else feat
         state.setdefault("aux", []).append({"layer": layer_idx, "complexity": b["complexity"],

@@ -12,6 +12,9 @@ Files written (DATA only; no reference source is copied):
   opt_<variant>_<shape>.npz      the analyzer switches the reference exposes
                                  (morphology.py:29-37): binarize_impl='otsu',
                                  contour_components=False, canny_impl='legacy'
+  pt_<shape>.npz                 per_channel=False quantizer (quantization.py:655-661):
+                                 one batch min/max over every channel; full y
+                                 (`python make_golden_r02.py pertensor` writes only these)
 """
 import os
 import sys
@@ -38,7 +41,7 @@ VARIANTS = {"otsu": {"binarize_impl": "otsu"}, "noeuler": {"contour_components":
             "legacy": {"canny_impl": "legacy"}}
 
 
-def modules(opts):
+def modules(opts, per_channel=True):
     w = np.load(os.path.join(HERE, "weights.npz"))
     sd = {k: torch.from_numpy(np.array(w[k])) for k in w.files}
 
@@ -48,7 +51,7 @@ def modules(opts):
     a.load_state_dict(sub("complexity_analyzer."))
     m = MLPMapper(2, 8)
     m.load_state_dict(sub("bit_mapper."))
-    q = SAQ(calibration_mode="minmax", smooth_transitions=True, per_channel=True)
+    q = SAQ(calibration_mode="minmax", smooth_transitions=True, per_channel=per_channel)
     q.soft_mask.load_state_dict(sub("soft_mask."))
     return a.eval(), m.eval(), q.eval()
 
@@ -87,7 +90,31 @@ def run_case(x, grid, opts, full_y):
     return out
 
 
+PT_SHAPES = {"p3": (2, 16, 80, 80, 8), "p5": (3, 32, 20, 20, 8), "odd": (2, 20, 44, 52, 8)}
+
+
+def per_tensor():
+    for si, (sname, (B, C, H, W, grid)) in enumerate(PT_SHAPES.items()):
+        x = synth_features(B, C, H, W, seed=99000 + si)
+        a, mapper, q = modules({}, per_channel=False)
+        a.grid_size = grid
+        out = dict(B=B, C=C, H=H, W=W, grid=grid, x=x.numpy().astype(np.float16))
+        with torch.no_grad():
+            comp = a(x)
+            out["complexity"] = comp.numpy()
+            for kind, mp in (("mlp", mapper), ("lin", LinMapper(2, 8))):
+                bm = mp(comp, 1.0)
+                out["bits_" + kind] = bm.numpy()
+                out["y_" + kind] = q(x, bm, training=False).numpy()
+        out["xmin"] = np.array(x.min().item(), np.float32)
+        out["xmax"] = np.array(x.max().item(), np.float32)
+        np.savez_compressed(os.path.join(HERE, "pt_%s.npz" % sname), **out)
+        print("pt", sname, "bits", np.unique(out["bits_mlp"]).astype(int).tolist())
+
+
 def main():
+    if sys.argv[1:] == ["pertensor"]:
+        return per_tensor()
     for i, (name, (B, C, H, W, grid)) in enumerate(LARGE.items()):
         x = synth_features(B, C, H, W, seed=77000 + i)
         out = run_case(x, grid, {}, full_y=False)
@@ -101,6 +128,7 @@ def main():
                 out["opt_" + k] = np.array(v)
             np.savez_compressed(os.path.join(HERE, "opt_%s_%s.npz" % (vname, sname)), **out)
             print(vname, sname, "bits", np.unique(out["bits_mlp"]).astype(int).tolist())
+    per_tensor()
 
 
 if __name__ == "__main__":

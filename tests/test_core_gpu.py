@@ -308,3 +308,22 @@ def test_gpu_equals_cpu_torch_path(mods, name):
         res[dev] = (outs[0].cpu(), aux[0]["bit_map"].cpu(), aux[0]["complexity"].cpu())
     assert torch.equal(res["cpu"][0], res[DEV][0]) and torch.equal(res["cpu"][1], res[DEV][1])
     np.testing.assert_allclose(res["cpu"][2].numpy(), res[DEV][2].numpy(), rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("name", ["pt_p3", "pt_p5", "pt_odd"])
+@pytest.mark.parametrize("mapping", ["mlp", "linear"])
+def test_per_tensor_hook_vs_reference(name, mapping):
+    """Fused hook with per_channel=False quantizers (the finalize reduces every
+    channel's partials to one min/max): bits and y bit-exact vs the reference
+    fixture (tests/golden/make_golden_r02.py pertensor)."""
+    import os
+    from conftest import GOLDEN
+    from test_fallback_cpu import hooks_per_tensor
+    d = np.load(os.path.join(GOLDEN, name + ".npz"))
+    h = hooks_per_tensor(DEV, int(d["grid"]), mapping)
+    x = torch.from_numpy(d["x"].astype(f32)).to(DEV)
+    with torch.no_grad():
+        outs, aux = h.forward_features([x])
+    key = "mlp" if mapping == "mlp" else "lin"
+    assert np.array_equal(aux[0]["bit_map"].cpu().numpy(), d["bits_" + key])
+    assert np.array_equal(outs[0].cpu().numpy(), d["y_" + key])
