@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libmcaq_hip.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -88,7 +88,7 @@ def _declare(lib):
     lib.mcaq_nms.restype = I
     lib.mcaq_nms.argtypes = [P, I, I, I, I, Fl, ctypes.c_double, I, I, Fl, I, P, P, P, P]
     lib.mcaq_nms_work_floats.restype = ctypes.c_size_t
-    lib.mcaq_nms_work_floats.argtypes = [I, I]
+    lib.mcaq_nms_work_floats.argtypes = [I, I, I]
     lib.mcaq_time_next_launch.restype = I
     lib.mcaq_time_next_launch.argtypes = [P, P]
     lib.mcaq_time_launch.restype = I

@@ -16,18 +16,22 @@
 //
 // One 1024-thread workgroup per image.  Phase 1 streams the (4+nc, N) slab of
 // the image once (coalesced over anchors), compacting candidates into a
-// 64-bit key array in LDS (ordered-score << 32 | anchor << 18 | cls).  Phase 2
-// bitonic-sorts the keys in LDS.  Phase 3 walks the sorted list in chunks of
-// 256: every candidate is tested against the boxes kept so far (4 threads per
-// candidate), a 256 x 256 chunk-local suppression bit matrix is built (one
-// 64-bit word per thread), then one lane resolves the chunk sequentially
-// with bit operations - exactly the greedy order of the CPU kernel.
+// 64-bit key array (ordered-score << 32 | anchor) and recording each
+// candidate's class in the workspace.  Up to NMS_LDS_KEYS candidates the keys
+// live in LDS; beyond that (large inputs, e.g. 1280x1280 = 33,600 anchors
+// at a low threshold) they are also written to a global key array sized
+// pow2(N) per image and sorted there.  Phase 2 bitonic-sorts the keys.
+// Phase 3 walks the sorted list in chunks of 256: every candidate is tested
+// against the boxes kept so far (4 threads per candidate), a 256 x 256
+// chunk-local suppression bit matrix is built (one 64-bit word per thread),
+// then one lane resolves the chunk sequentially with bit operations -
+// exactly the greedy order of the CPU kernel.
 #pragma once
 
 namespace mcaq {
 
 constexpr int NMS_THREADS = 1024;
-constexpr int NMS_MAX_ANCHORS = 16384;   // LDS key array (128 KiB)
+constexpr int NMS_LDS_KEYS = 16384;      // LDS key array (128 KiB); more candidates sort in global memory
 constexpr int NMS_CHUNK = 256;
 
 struct NmsArgs {
@@ -35,7 +39,9 @@ struct NmsArgs {
   float* out;          // (B, max_det, 6)
   int* counts;         // (B)
   float* kept;         // (B, max_det, 8) workspace: offset box + area
-  int B, no, N, nc, max_det, max_nms, agnostic;
+  int* cls;            // (B, N) workspace: class of each candidate anchor
+  unsigned long long* gkeys;   // (B, np2) workspace when N > NMS_LDS_KEYS, else unused
+  int B, no, N, np2N, nc, max_det, max_nms, agnostic;
   float conf, max_wh;
   double iou;
 };
@@ -63,46 +69,8 @@ __device__ __forceinline__ bool nms_iou_gt(float4 bi, float ai, float4 bj, float
   return (double)ovr > thr;
 }
 
-__global__ __launch_bounds__(NMS_THREADS) void mcaq_nms_kernel(NmsArgs a) {
-  __shared__ unsigned long long keys[NMS_MAX_ANCHORS];
-  __shared__ float4 cbox[NMS_CHUNK];        // offset boxes of the chunk
-  __shared__ float4 craw[NMS_CHUNK];        // xyxy boxes (output)
-  __shared__ float carea[NMS_CHUNK], cscore[NMS_CHUNK], ccls[NMS_CHUNK];
-  __shared__ int csup[NMS_CHUNK];
-  __shared__ unsigned long long cmask[NMS_CHUNK][4];
-  __shared__ int s_cnt, s_K;
-
-  const int b = blockIdx.x;
-  const int tid = threadIdx.x;
-  const int N = a.N;
-  const float* P = a.pred + (size_t)b * a.no * N;
-  float* kept = a.kept + (size_t)b * a.max_det * 8;
-  float* out = a.out + (size_t)b * a.max_det * 6;
-  if (tid == 0) { s_cnt = 0; s_K = 0; }
-  __syncthreads();
-
-  // ---- phase 1: candidates (max class score > conf), compacted into LDS
-  for (int ai = tid; ai < N; ai += NMS_THREADS) {
-    float best = P[(size_t)4 * N + ai];
-    int bj = 0;
-    for (int c = 1; c < a.nc; ++c) {
-      const float v = P[(size_t)(4 + c) * N + ai];
-      if (v > best) { best = v; bj = c; }
-    }
-    if (best > a.conf) {
-      const int slot = atomicAdd(&s_cnt, 1);
-      keys[slot] = ((unsigned long long)nms_score_key(best) << 32) |
-                   ((unsigned long long)ai << 18) | (unsigned long long)bj;
-    }
-  }
-  __syncthreads();
-  const int n = s_cnt;
-  int np2 = 1;
-  while (np2 < n) np2 <<= 1;
-  for (int i = n + tid; i < np2; i += NMS_THREADS) keys[i] = ~0ull;
-  __syncthreads();
-
-  // ---- phase 2: bitonic sort (ascending key = score desc, anchor asc)
+template <class KeyT>
+__device__ __forceinline__ void nms_bitonic(KeyT* keys, int np2, int tid) {
   for (int k = 2; k <= np2; k <<= 1) {
     for (int j = k >> 1; j > 0; j >>= 1) {
       for (int i = tid; i < np2; i += NMS_THREADS) {
@@ -116,15 +84,70 @@ __global__ __launch_bounds__(NMS_THREADS) void mcaq_nms_kernel(NmsArgs a) {
       __syncthreads();
     }
   }
+}
+
+__global__ __launch_bounds__(NMS_THREADS) void mcaq_nms_kernel(NmsArgs a) {
+  __shared__ unsigned long long lkeys[NMS_LDS_KEYS];
+  __shared__ float4 cbox[NMS_CHUNK];        // offset boxes of the chunk
+  __shared__ float4 craw[NMS_CHUNK];        // xyxy boxes (output)
+  __shared__ float carea[NMS_CHUNK], cscore[NMS_CHUNK], ccls[NMS_CHUNK];
+  __shared__ int csup[NMS_CHUNK];
+  __shared__ unsigned long long cmask[NMS_CHUNK][4];
+  __shared__ int s_cnt, s_K;
+
+  const int b = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int N = a.N;
+  const float* P = a.pred + (size_t)b * a.no * N;
+  float* kept = a.kept + (size_t)b * a.max_det * 8;
+  float* out = a.out + (size_t)b * a.max_det * 6;
+  int* ccl = a.cls + (size_t)b * N;
+  const bool big = N > NMS_LDS_KEYS;
+  unsigned long long* gk = big ? a.gkeys + (size_t)b * a.np2N : nullptr;
+  if (tid == 0) { s_cnt = 0; s_K = 0; }
+  __syncthreads();
+
+  // ---- phase 1: candidates (max class score > conf), compacted
+  for (int ai = tid; ai < N; ai += NMS_THREADS) {
+    float best = P[(size_t)4 * N + ai];
+    int bj = 0;
+    for (int c = 1; c < a.nc; ++c) {
+      const float v = P[(size_t)(4 + c) * N + ai];
+      if (v > best) { best = v; bj = c; }
+    }
+    if (best > a.conf) {
+      const int slot = atomicAdd(&s_cnt, 1);
+      const unsigned long long key = ((unsigned long long)nms_score_key(best) << 32) | (unsigned int)ai;
+      if (slot < NMS_LDS_KEYS) lkeys[slot] = key;
+      if (big) gk[slot] = key;
+      ccl[ai] = bj;
+    }
+  }
+  __syncthreads();
+  const int n = s_cnt;
+  int np2 = 1;
+  while (np2 < n) np2 <<= 1;
+  const bool inlds = n <= NMS_LDS_KEYS;
+
+  // ---- phase 2: bitonic sort (ascending key = score desc, anchor asc)
+  if (inlds) {
+    for (int i = n + tid; i < np2; i += NMS_THREADS) lkeys[i] = ~0ull;
+    __syncthreads();
+    nms_bitonic(lkeys, np2, tid);
+  } else {
+    for (int i = n + tid; i < np2; i += NMS_THREADS) gk[i] = ~0ull;
+    __syncthreads();
+    nms_bitonic(gk, np2, tid);
+  }
 
   // ---- phase 3: greedy suppression in chunks of 256 sorted candidates
   const int nproc = n < a.max_nms ? n : a.max_nms;
   for (int base = 0; base < nproc; base += NMS_CHUNK) {
     const int cn = (nproc - base) < NMS_CHUNK ? (nproc - base) : NMS_CHUNK;
     if (tid < cn) {
-      const unsigned long long key = keys[base + tid];
-      const int ai = (int)((key >> 18) & 0x3fffu);
-      const int cls = (int)(key & 0x3ffffu);
+      const unsigned long long key = inlds ? lkeys[base + tid] : gk[base + tid];
+      const int ai = (int)(unsigned int)key;
+      const int cls = ccl[ai];
       const float x = P[ai], y = P[(size_t)N + ai], w = P[(size_t)2 * N + ai], h = P[(size_t)3 * N + ai];
       const float hw = __fdiv_rn(w, 2.0f), hh = __fdiv_rn(h, 2.0f);   // xywh2xyxy
       const float4 r = make_float4(__fsub_rn(x, hw), __fsub_rn(y, hh), __fadd_rn(x, hw), __fadd_rn(y, hh));
@@ -201,19 +224,33 @@ __global__ __launch_bounds__(NMS_THREADS) void mcaq_nms_kernel(NmsArgs a) {
 
 extern "C" {
 
-size_t mcaq_nms_work_floats(int B, int max_det) {
-  return (size_t)(B > 0 ? B : 0) * (size_t)(max_det > 0 ? max_det : 0) * 8;
+static size_t nms_np2(int N) {
+  size_t p = 1;
+  while (p < (size_t)N) p <<= 1;
+  return p;
+}
+
+size_t mcaq_nms_work_floats(int B, int N, int max_det) {
+  if (B <= 0 || N < 0 || max_det <= 0) return 0;
+  size_t per = (size_t)max_det * 8 + (size_t)N;                     // kept boxes + candidate classes
+  if (N > mcaq::NMS_LDS_KEYS) per += 2 * nms_np2(N);                // global keys (u64)
+  return (size_t)B * per + 2;                                        // +2: 8-byte alignment of the keys
 }
 
 int mcaq_nms(const float* pred, int B, int no, int N, int nc, float conf_thres, double iou_thres, int max_det,
              int max_nms, float max_wh, int agnostic, float* out, int* counts, float* work, hipStream_t stream) {
-  if (B < 0 || nc < 1 || nc >= (1 << 18) || no != 4 + nc || N < 0 || N > mcaq::NMS_MAX_ANCHORS ||
-      max_det < 1 || max_nms < 1)
+  if (B < 0 || nc < 1 || no != 4 + nc || N < 0 || N > (1 << 30) || max_det < 1 || max_nms < 1)
     return (int)hipErrorInvalidValue;
   if (B == 0) return 0;
   if (!pred || !out || !counts || !work) return (int)hipErrorInvalidValue;
   mcaq::NmsArgs a;
   a.pred = pred; a.out = out; a.counts = counts; a.kept = work;
+  a.cls = reinterpret_cast<int*>(work + (size_t)B * max_det * 8);
+  {
+    const uintptr_t g = reinterpret_cast<uintptr_t>(work + (size_t)B * max_det * 8 + (size_t)B * N);
+    a.gkeys = reinterpret_cast<unsigned long long*>((g + 7) & ~(uintptr_t)7);
+  }
+  a.np2N = (int)nms_np2(N);
   a.B = B; a.no = no; a.N = N; a.nc = nc; a.max_det = max_det; a.max_nms = max_nms;
   a.agnostic = agnostic ? 1 : 0; a.conf = conf_thres; a.max_wh = max_wh; a.iou = iou_thres;
   hipLaunchKernelGGL(mcaq::mcaq_nms_kernel, dim3(B), dim3(mcaq::NMS_THREADS), 0, stream, a);

@@ -30,7 +30,7 @@ class NmsPlan:
         self.B, self.no, self.N, self.max_det = B, no, N, max_det
         self.out = torch.empty(B, max_det, 6, device=device)
         self.counts = torch.empty(B, device=device, dtype=torch.int32)
-        self.work = torch.empty(max(1, abi.lib().mcaq_nms_work_floats(B, max_det)), device=device)
+        self.work = torch.empty(max(1, abi.lib().mcaq_nms_work_floats(B, N, max_det)), device=device)
 
     def run(self, pred, conf_thres=0.25, iou_thres=0.45, agnostic=False, max_nms=30000, max_wh=7680):
         if not pred.is_cuda:

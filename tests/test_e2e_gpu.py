@@ -83,8 +83,20 @@ def test_nms_list_api_and_errors():
         non_max_suppression(torch.from_numpy(p).to(DEV), classes=[0])
     with pytest.raises(RuntimeError):
         non_max_suppression(torch.from_numpy(p), 0.25)
-    with pytest.raises(RuntimeError):                          # N > 16384 anchors
-        non_max_suppression(torch.zeros(1, 84, 16385, device=DEV))
+    with pytest.raises(RuntimeError):                          # no = 4 + nc violated
+        non_max_suppression(torch.zeros(1, 3, 100, device=DEV))
+
+
+@pytest.mark.parametrize("B,nc,N,seed,kw", [
+    (2, 80, 33600, 12, {}),                                   # 1280x1280 head: > 16,384 candidates, global keys
+    (1, 4, 33600, 13, {"conf": 0.0, "max_det": 1000}),        # every anchor a candidate, max_nms = 30000 cut
+    (2, 80, 16385, 14, {"conf": 0.0, "max_det": 1000}),       # every anchor a candidate: one past the LDS keys
+])
+def test_nms_large_inputs(B, nc, N, seed, kw):
+    """Anchor counts beyond the LDS key array (NMS_LDS_KEYS): candidates are
+    sorted in the global workspace; results still equal the restatement."""
+    cnt = _check(_synthetic_preds(B, nc, N, seed, dense=0.9), **kw)
+    assert cnt.min() > 0
 
 
 def _mcaq_yolo(mapper="mlp"):
