@@ -41,7 +41,7 @@ typedef void* hipEvent_t;
 extern "C" {
 #endif
 
-#define MCAQ_ABI_VERSION 7
+#define MCAQ_ABI_VERSION 8
 /* largest dynamic LDS request of the morph kernel (gfx950: 160 KiB per CU) */
 #define MCAQ_MORPH_LDS_LIMIT 163840
 
@@ -124,6 +124,9 @@ typedef struct {
   int flags, hyst_iters;
   float temperature, min_bits, max_bits;
   int block_begin;   /* set by the launcher */
+  int softmax_threads; /* torch.get_num_threads() of the reference CPU run the
+                          soft mask's channel softmax reproduces (its exp per
+                          tile depends on ATen's thread partition); <1 = 1 */
 } mcaq_morph_scale;
 int mcaq_morph(const mcaq_morph_scale* scales, int nscales, hipStream_t stream);
 /* mcaq_morph + mcaq_finalize in one launch: the channel min/max reduction

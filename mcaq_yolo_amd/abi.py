@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libmcaq_hip.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -32,7 +32,8 @@ class MorphScale(ctypes.Structure):
                 ("bits_out", P), ("m_out", P), ("mt_out", P), ("edge_out", P), ("bin_out", P), ("gscratch", P), ("tile_tmp", P),
                 ("B", I), ("H", I), ("W", I), ("Hc", I), ("Wc", I), ("tile", I), ("ht", I), ("wt", I),
                 ("batch_offset", I), ("batch_total", I), ("flags", I), ("hyst_iters", I),
-                ("temperature", Fl), ("min_bits", Fl), ("max_bits", Fl), ("block_begin", I)]
+                ("temperature", Fl), ("min_bits", Fl), ("max_bits", Fl), ("block_begin", I),
+                ("softmax_threads", I)]
 
 
 class QuantScale(ctypes.Structure):

@@ -196,6 +196,7 @@ def _morph_struct(B, H, W, tile, ht, wt, flags, **ptrs):
     s.flags = flags
     s.hyst_iters = 8
     s.temperature, s.min_bits, s.max_bits = 1.0, 2.0, 8.0
+    s.softmax_threads = torch.get_num_threads()   # the CPU reference's softmax partition
     return s
 
 

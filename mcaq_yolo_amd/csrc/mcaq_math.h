@@ -42,6 +42,50 @@ MCAQ_CR float cr_atan2(float y, float x) { return (float)atan2((double)y, (doubl
 MCAQ_HD float bits_as_float(uint32_t u) {
   union { uint32_t u; float f; } c; c.u = u; return c.f;
 }
+
+// exp as CPU ATen's vectorized float kernels evaluate it: SLEEF's
+// expf_u10 (AVX-512 build in libtorch_cpu: Cody-Waite reduction by ln2 with
+// two FMAs, degree-6 polynomial by FMA, 1 + s^2 u + s, scale by 2^(q>>1) and
+// 2^(q - q>>1)).  Not correctly rounded: it differs from exp() in the last bit
+// for ~9 % of arguments, which reaches the soft mask's softmax output
+// (quantization.py:231) in about one tile in 10^4.  Constants read from the
+// libtorch_cpu.so the fixtures were generated with.
+MCAQ_HD float sleef_expf(float d) {
+  const float qf = rintf(d * 1.44269502162933349609375f);
+  const int q = (int)qf;
+  float s = fmaf(qf, -0.693145751953125f, d);
+  s = fmaf(qf, -1.428606765330187045e-06f, s);
+  float u = 0.000198527617612853646278381f;
+  u = fmaf(u, s, 0.00139304355252534151077271f);
+  u = fmaf(u, s, 0.00833336077630519866943359f);
+  u = fmaf(u, s, 0.0416664853692054748535156f);
+  u = fmaf(u, s, 0.166666671633720397949219f);
+  u = fmaf(u, s, 0.5f);
+  u = 1.0f + fmaf(s * s, u, s);
+  const int a = q >> 1, b = q - a;
+  u = u * bits_as_float((uint32_t)(a + 127) << 23);
+  u = u * bits_as_float((uint32_t)(b + 127) << 23);
+  if (d < -104.0f) u = 0.0f;
+  if (d > 100.0f) u = __builtin_inff();
+  return u;
+}
+
+// Which exp ATen's channel softmax (dim=1 of (B, 2, ht, wt), SoftMaxKernel
+// _vec_softmax) applies to flattened position `flat` of N = B*NT: at::parallel_for
+// cuts [0, N) into ceil(N / T) chunks for T threads; within a chunk each
+// image's run is vectorized 16 lanes at a time (SLEEF) and its last < 16
+// positions go through scalar std::exp (glibc, correctly rounded).  T is the
+// reference process's torch.get_num_threads(); verified against torch.softmax
+// for T = 1..16 on batch / grid shapes of all three hook scales.
+MCAQ_HD bool aten_softmax_vec_lane(long long flat, long long N, int NT, int T) {
+  const long long nthr = T < 1 ? 1 : (T < N ? T : N);
+  const long long chunk = (N + nthr - 1) / nthr;
+  const long long cs = (flat / chunk) * chunk, ce = cs + chunk < N ? cs + chunk : N;
+  const long long img = flat / NT;
+  const long long ss = cs > img * NT ? cs : img * NT;
+  const long long se = ce < (img + 1) * NT ? ce : (img + 1) * NT;
+  return flat < ss + ((se - ss) / 16) * 16;
+}
 MCAQ_HD uint32_t float_as_bits(float f) {
   union { uint32_t u; float f; } c; c.f = f; return c.u;
 }

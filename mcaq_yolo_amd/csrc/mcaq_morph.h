@@ -1685,10 +1685,14 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
         l0 = fmaf(Pm[SM_W2 + ic], hv, l0);
         l1 = fmaf(Pm[SM_W2 + 8 + ic], hv, l1);
       }
-      // softmax over 2: the larger logit's term is exp(+0) = 1 exactly
+      // softmax over 2: the larger logit's term is exp(+0) = 1 exactly (both
+      // exps); the other is SLEEF's or glibc's by ATen's lane of this tile
       const float mxl = fmax_(l0, l1);
       const bool first = l0 >= l1;
-      const float e = cr_exp((first ? l1 : l0) - mxl);
+      const float ea = (first ? l1 : l0) - mxl;
+      const bool vl = aten_softmax_vec_lane((long long)(S.batch_offset + b) * NT + t,
+                                            (long long)S.batch_total * NT, NT, S.softmax_threads);
+      const float e = vl ? sleef_expf(ea) : cr_exp(ea);
       const float e0 = first ? 1.0f : e, e1 = first ? e : 1.0f;
       const float mtv = e0 / (e0 + e1);
       tiles[t * TILE_FLOATS + T_MT] = mtv;

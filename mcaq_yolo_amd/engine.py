@@ -115,12 +115,15 @@ class HookPlan:
     def prepare(self, feats, cmlp, mapper, smasks, temperature=1.0, mapper_kind="mlp", continuous=False,
                 normalize=False, minmax=None, batch_offset=0, batch_total=None, binarize_otsu=False,
                 contour_components=True, canny_legacy=False, min_bits=2.0, max_bits=8.0, quantize=True, hysteresis_iters=8,
-                per_tensor=False):
+                per_tensor=False, softmax_threads=None):
         """Validate inputs and build the launch descriptors (pointers are baked
         in: the tensors must stay alive and in place until the last launch).
         minmax: optional per-scale (xmin, xmax) frozen calibration stats.
         per_tensor: one batch min/max over all channels (per_channel=False,
-        quantization.py:655-661), broadcast to the C entries the kernel reads."""
+        quantization.py:655-661), broadcast to the C entries the kernel reads.
+        softmax_threads: thread count of the CPU reference whose soft-mask
+        softmax is reproduced bit for bit (ATen picks SLEEF or glibc exp per
+        tile by its thread partition); default torch.get_num_threads()."""
         n = len(self.geoms)
         L = self.lib
         if len(feats) != n:
@@ -199,6 +202,7 @@ class HookPlan:
             s.batch_total = batch_total if batch_total is not None else g.B
             s.flags = flags | (abi.F_SOFTMASK if (with_mask[i] and quantize) else 0)
             s.hyst_iters = hysteresis_iters
+            s.softmax_threads = int(softmax_threads) if softmax_threads else torch.get_num_threads()
             s.temperature, s.min_bits, s.max_bits = T, float(min_bits), float(max_bits)
         self._mo = mo
         # ---- pass 2

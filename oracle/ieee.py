@@ -131,3 +131,49 @@ def seq_sum(rows):
 def rint32(v):
     """torch.round: round half to even."""
     return np.rint(np.asarray(v, f32)).astype(f32)
+
+
+def sleef_expf32(d):
+    """SLEEF expf_u10 as libtorch_cpu's AVX-512 build evaluates it (the exp of
+    ATen's vectorized float kernels): q = rint(d * log2(e)), two-FMA Cody-Waite
+    reduction, degree-6 FMA polynomial, 1 + s*s*u + s, scaled by 2^(q>>1) and
+    2^(q - q>>1).  Constants read from the libtorch_cpu.so that generated the
+    golden fixtures."""
+    d = np.asarray(d, f32)
+    qf = np.rint((d * f32(1.44269502162933349609375)).astype(f32)).astype(f32)
+    q = qf.astype(np.int64)
+    s = fma32(qf, f32(-0.693145751953125), d)
+    s = fma32(qf, f32(-1.428606765330187045e-06), s)
+    u = np.full(d.shape, f32(0.000198527617612853646278381), f32)
+    for c in (0.00139304355252534151077271, 0.00833336077630519866943359, 0.0416664853692054748535156,
+              0.166666671633720397949219, 0.5):
+        u = fma32(u, s, f32(c))
+    u = (f32(1.0) + fma32((s * s).astype(f32), u, s)).astype(f32)
+    a = q >> 1
+    b = q - a
+    u = (u * ((a + 127).astype(np.uint32) << 23).view(f32)).astype(f32)
+    u = (u * ((b + 127).astype(np.uint32) << 23).view(f32)).astype(f32)
+    u = np.where(d < f32(-104.0), f32(0.0), u)
+    return np.where(d > f32(100.0), f32(np.inf), u).astype(f32)
+
+
+def aten_softmax_vec_lanes(B, NT, threads, batch_offset=0, batch_total=None):
+    """(B, NT) bool: True where ATen's dim-1 softmax of a (batch_total, 2, ht, wt)
+    tensor evaluates exp vectorized (SLEEF), False where the scalar tail (glibc
+    expf, correctly rounded) does.  at::parallel_for cuts the flattened
+    (image, tile) range into ceil(N / T) chunks; inside a chunk each image's
+    run is vectorized 16 lanes at a time and its last < 16 positions are
+    scalar.  Checked against torch.softmax for T = 1..16 (tests/test_oracle_cpu.py)."""
+    bt = B if batch_total is None else batch_total
+    N = bt * NT
+    nthr = max(1, min(int(threads), N))
+    chunk = -(-N // nthr)
+    lanes = np.zeros(N, bool)
+    for cs in range(0, N, chunk):
+        ce = min(N, cs + chunk)
+        img = cs // NT
+        while img * NT < ce:
+            ss, se = max(cs, img * NT), min(ce, (img + 1) * NT)
+            lanes[ss:ss + ((se - ss) // 16) * 16] = True
+            img += 1
+    return lanes[batch_offset * NT:(batch_offset + B) * NT].reshape(B, NT)

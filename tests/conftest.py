@@ -11,6 +11,13 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP) GPU and the built libmcaq_hip.so")
+    # the golden fixtures were generated with 8 torch threads, and the soft
+    # mask's softmax exp per tile follows ATen's thread partition
+    # (oracle.mcaq_oracle.REF_THREADS): the CPU path and the HIP path
+    # (softmax_threads default = torch.get_num_threads()) reproduce that run
+    import torch
+    from oracle.mcaq_oracle import REF_THREADS
+    torch.set_num_threads(REF_THREADS)
 
 
 def pytest_collection_modifyitems(config, items):

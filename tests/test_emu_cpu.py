@@ -58,6 +58,7 @@ def run_emu(emu, x, grid, flags, T=1.0, c_in=None, bits_in=None):
     s.batch_offset, s.batch_total = 0, B
     s.flags = flags
     s.hyst_iters = 8
+    s.softmax_threads = O.REF_THREADS
     s.temperature, s.min_bits, s.max_bits = max(T, 0.1), 2.0, 8.0
     lib.emu_morph(ctypes.byref(s))
     return out

@@ -191,3 +191,41 @@ def test_option_and_yolov8m_fixtures(name):
     assert rel(C, d["complexity"]) < 1e-6
     assert np.array_equal(O.mlp_mapper(C, W, 1.0), d["bits_mlp"])
     assert np.array_equal(O.linear_mapper(C, 1.0), d["bits_lin"])
+
+
+def test_softmax_exp_partition_matches_aten():
+    """ATen's dim-1 softmax of (B, 2, ht, wt): SLEEF expf on vectorized lanes,
+    glibc on scalar tails, by at::parallel_for's partition for T threads
+    (oracle/ieee.py); bit-exact vs torch.softmax for T = 1, 3, 8, 16 on hook
+    tile grids.  Plain cr-exp everywhere differs from torch on ~1 % of tiles."""
+    import torch
+    from oracle.ieee import aten_softmax_vec_lanes, cr32, sleef_expf32
+    rng = np.random.default_rng(11)
+    old = torch.get_num_threads()
+    try:
+        for T in (1, 3, 8, 16):
+            torch.set_num_threads(T)
+            for B, ht, wt in ((1, 10, 10), (3, 11, 13), (32, 10, 10), (32, 5, 5), (16, 20, 20), (2, 37, 41)):
+                lg = (rng.standard_normal((B, 2, ht, wt)) * 3).astype(np.float32)
+                ref = torch.softmax(torch.from_numpy(lg), 1)[:, 0].numpy()
+                vl = aten_softmax_vec_lanes(B, ht * wt, T).reshape(B, ht, wt)
+                mx = np.maximum(lg[:, 0], lg[:, 1])
+                a0, a1 = (lg[:, 0] - mx).astype(np.float32), (lg[:, 1] - mx).astype(np.float32)
+                e0 = np.where(vl, sleef_expf32(a0), cr32(np.exp, a0))
+                e1 = np.where(vl, sleef_expf32(a1), cr32(np.exp, a1))
+                m = (e0 / (e0 + e1).astype(np.float32)).astype(np.float32)
+                assert np.array_equal(m, ref), (T, B, ht, wt, int((m != ref).sum()))
+    finally:
+        torch.set_num_threads(old)
+
+
+def test_sleef_expf_restatement():
+    """sleef_expf32 on a sweep of arguments: finite, within 1 ulp of the
+    correctly rounded exp, exactly 1 at 0, 0 below -104."""
+    from oracle.ieee import cr32, sleef_expf32
+    x = np.linspace(-103.0, 88.0, 200001).astype(np.float32)
+    e = sleef_expf32(x)
+    c = cr32(np.exp, x)
+    ulp = np.abs(e.view(np.int32).astype(np.int64) - c.view(np.int32).astype(np.int64))
+    assert ulp.max() <= 1 and 0.01 < (ulp == 1).mean() < 0.3
+    assert sleef_expf32(np.float32(0.0)) == 1.0 and sleef_expf32(np.float32(-105.0)) == 0.0
