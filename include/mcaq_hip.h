@@ -213,5 +213,17 @@ int mcaq_abi_version(void);
 
 #ifdef __cplusplus
 }
+
+/* C++-linkage entry with the reference's exact declaration
+ * (mcaq_yolo/engine/MCAQPlugin.cpp:15-23, mcaq_yolo/ops/src/mcaq_ops.cpp:7-16;
+ * cudaStream_t -> hipStream_t): a plugin or extension compiled against that
+ * declaration links against libmcaq_hip.so unchanged.  Errors are left for
+ * hipGetLastError(), as the reference's void launcher leaves them for
+ * cudaGetLastError(). */
+void launch_spatial_quantization(const float* input, const float* bit_map,
+                                 const float* min_vals, const float* max_vals,
+                                 const float* mask, float* output,
+                                 int N, int C, int H, int W, int tile_h, int tile_w,
+                                 int n_tiles_h, int n_tiles_w, hipStream_t stream);
 #endif
 #endif /* MCAQ_HIP_H_ */

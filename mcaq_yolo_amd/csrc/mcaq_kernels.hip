@@ -920,6 +920,9 @@ int mcaq_morph_finalize(const mcaq_morph_scale* scales, int nscales, const mcaq_
     }
     a.wg_begin[nscales] = wg;
     if (fa.nblocks > 0 && dyn < (size_t)(8 * MORPH_THREADS)) dyn = 8 * MORPH_THREADS;  // finalize_body's LDS
+#ifdef MCAQ_MORPH_EXCL
+    dyn = (size_t)limit;   // A/B: one pass-A workgroup per CU (no streaming waves beside it)
+#endif
     const int grid = wg + fa.nblocks;
     // canny_impl='legacy' is an analyzer option: one value for every scale of a launch
     const int leg = (a.s[0].flags & F_CANNY_LEGACY) ? 1 : 0;
@@ -964,7 +967,11 @@ int mcaq_morph_finalize(const mcaq_morph_scale* scales, int nscales, const mcaq_
     if (per + TILES_SCRATCH_BYTES > lim) return (int)hipErrorInvalidValue;
     // stage the weight blobs in LDS when they fit beside the tile arrays and the MLP scratch
     const int wlds = per + TILES_SCRATCH_BYTES + weights_lds_bytes() <= lim;
+#ifdef MCAQ_TILES_EXCL
+    const size_t tdyn = (size_t)lim;   // A/B: one pass-B workgroup per CU (no streaming waves beside it)
+#else
     const size_t tdyn = (size_t)per + TILES_SCRATCH_BYTES + (wlds ? weights_lds_bytes() : 0);
+#endif
     static int set_tiles = 0;
     if ((int)tdyn > set_tiles) {
       hipError_t ae = hipFuncSetAttribute((const void*)mcaq_tiles_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
@@ -1033,3 +1040,15 @@ int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream) 
 
 #include "mcaq_qat.h"
 #include "mcaq_nms.h"
+
+// C++-linkage drop-in for the reference's declaration (include/mcaq_hip.h):
+// same name, argument list and void return as MCAQPlugin.cpp:15-23.  An
+// argument error launches nothing and is reported on stderr (the reference
+// would launch with the bad sizes).
+void launch_spatial_quantization(const float* input, const float* bit_map, const float* min_vals,
+                                 const float* max_vals, const float* mask, float* output, int N, int C, int H,
+                                 int W, int tile_h, int tile_w, int n_tiles_h, int n_tiles_w, hipStream_t stream) {
+  const int e = mcaq_launch_spatial_quantization(input, bit_map, min_vals, max_vals, mask, output, N, C, H, W, tile_h,
+                                                 tile_w, n_tiles_h, n_tiles_w, stream);
+  if (e) fprintf(stderr, "launch_spatial_quantization: error %d (%s)\n", e, hipGetErrorString((hipError_t)e));
+}

@@ -58,3 +58,14 @@ def test_invalid_args_rejected_without_gpu():
     s.tile = 3
     assert lib.mcaq_morph(ctypes.byref(s), 1, None) != 0
     assert lib.mcaq_stats(ctypes.byref(abi.StatsScale()), 0, None) != 0
+
+
+def test_reference_cpp_linkage_symbol_exported():
+    """launch_spatial_quantization with the reference's C++ declaration
+    (MCAQPlugin.cpp:15-23, hipStream_t for cudaStream_t) is exported under its
+    Itanium-mangled name, so a caller compiled against that declaration links."""
+    if not os.path.exists(abi.LIB_PATH):
+        pytest.skip("library not built (run __graft_entry__.build())")
+    lib = ctypes.CDLL(abi.LIB_PATH)
+    mangled = "_Z27launch_spatial_quantizationPKfS0_S0_S0_S0_PfiiiiiiiiP12ihipStream_t"
+    assert hasattr(lib, mangled)

@@ -20,13 +20,16 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
          "-ffp-contract=off", "-fno-fast-math", "-Wall", "-Wno-unused-result"]
 
 
-def build(force=False, verbose=True, stamps=False):
-    out = OUT.replace(".so", "_stamps.so") if stamps else OUT
-    if not force and os.path.exists(out) and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in DEPS):
+def build(force=False, verbose=True, stamps=False, defines=(), out=None):
+    """defines / out: A/B variant builds (tools/gpu_ab.sh), e.g.
+    python tools/build.py --variant tools/probe/ab/x.so -DMCAQ_TILES_EXCL"""
+    out = out or (OUT.replace(".so", "_stamps.so") if stamps else OUT)
+    if not force and not defines and os.path.exists(out) and \
+            all(os.path.getmtime(out) >= os.path.getmtime(d) for d in DEPS):
         return out
     os.makedirs(os.path.dirname(out), exist_ok=True)
     tmp = out + ".tmp"
-    cmd = [HIPCC] + FLAGS + (["-DMCAQ_STAMPS"] if stamps else []) + ["-o", tmp] + SRCS
+    cmd = [HIPCC] + FLAGS + (["-DMCAQ_STAMPS"] if stamps else []) + list(defines) + ["-o", tmp] + SRCS
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
@@ -35,4 +38,7 @@ def build(force=False, verbose=True, stamps=False):
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, stamps="--stamps" in sys.argv))
+    a = sys.argv[1:]
+    out = a[a.index("--variant") + 1] if "--variant" in a else None
+    print(build(force="--force" in a, stamps="--stamps" in a, out=out,
+                defines=[x for x in a if x.startswith("-D")]))
