@@ -41,7 +41,7 @@ typedef void* hipEvent_t;
 extern "C" {
 #endif
 
-#define MCAQ_ABI_VERSION 8
+#define MCAQ_ABI_VERSION 9
 /* largest dynamic LDS request of the morph kernel (gfx950: 160 KiB per CU) */
 #define MCAQ_MORPH_LDS_LIMIT 163840
 
@@ -187,6 +187,10 @@ typedef struct {
   const float* xmax;   /* (C) */
   int B, C, H, W, ht, wt;
   int unit_begin, block_begin;  /* set by the launcher */
+  int* arrive;         /* (B) zero-initialised arrival counters (left zeroed):
+                          the last backward unit of an image folds that
+                          image's partials into gm / gb inside the same
+                          launch; NULL: a separate fold kernel does it */
 } mcaq_qat_scale;
 int mcaq_qat_forward(const mcaq_qat_scale* scales, int nscales, hipStream_t stream);
 int mcaq_qat_backward(const mcaq_qat_scale* scales, int nscales, hipStream_t stream);

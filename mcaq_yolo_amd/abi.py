@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libmcaq_hip.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -46,7 +46,7 @@ class QatScale(ctypes.Structure):
     _fields_ = [("x", P), ("g", P), ("y", P), ("gx", P), ("gm", P), ("gb", P), ("work", P),
                 ("bits", P), ("m", P), ("xmin", P), ("xmax", P),
                 ("B", I), ("C", I), ("H", I), ("W", I), ("ht", I), ("wt", I),
-                ("unit_begin", I), ("block_begin", I)]
+                ("unit_begin", I), ("block_begin", I), ("arrive", P)]
 
 
 # morph stage flags (mcaq_morph.h)

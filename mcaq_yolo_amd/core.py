@@ -736,6 +736,26 @@ def qat_quantize(x, bits, m, xmin, xmax):
     return y
 
 
+_ARRIVE = {}
+
+
+def _arrive_counters(B, device):
+    """Zeroed per-image arrival counters for the in-launch fold of
+    mcaq_qat_backward (the kernel leaves them zeroed): one persistent int32
+    buffer per device, created outside graph capture.  While a HIP graph is
+    being captured and none exists yet, a fresh zeroed buffer is captured
+    (its fill node re-zeroes it on each replay)."""
+    key = torch.device(device)
+    buf = _ARRIVE.get(key)
+    if buf is not None and buf.numel() >= B:
+        return buf
+    if torch.cuda.is_current_stream_capturing():
+        return torch.zeros(B, dtype=torch.int32, device=device)
+    buf = torch.zeros(max(B, 1024), dtype=torch.int32, device=device)
+    _ARRIVE[key] = buf
+    return buf
+
+
 def qat_quantize_backward(g, x, bits, m, xmin, xmax, want_gm=True, want_gb=True):
     """Straight-through backward (quantization.py:94-118 + the autograd graph of
     :699-737): (grad_x, grad_bits (B,ht,wt) or None, grad_m (B,H,W) or None)."""
@@ -747,6 +767,8 @@ def qat_quantize_backward(g, x, bits, m, xmin, xmax, want_gm=True, want_gb=True)
     work = torch.empty(L.mcaq_qat_work_floats(B, C, H, W), device=x.device)
     q = _qat_struct(x, bits, m, xmin, xmax)
     q.g, q.gx, q.gm, q.gb, q.work = _p(g), _p(gx), _p(gm), _p(gb), _p(work)
+    if (gm is not None or gb is not None) and W <= 2048:
+        q.arrive = _p(_arrive_counters(B, x.device))   # fold inside the backward launch
     abi.check(L.mcaq_qat_backward(ctypes.byref(q), 1, _stream()), "mcaq_qat_backward")
     return gx, gb, gm
 

@@ -32,6 +32,106 @@ struct QatArgs {
 constexpr int QAT_LO = 1;   // table widths QAT_LO .. 8 (the reference's bc_int <= 8)
 constexpr int QAT_NB = 8;
 
+// one workgroup per (scale, image, tile row): the band of pixel rows whose
+// nearest tile row is th (binary search: nearest_src is monotone).  The
+// per-slice channel partials of the backward kernel are summed per pixel,
+// slices in order, the slice loads of a pixel issued together -> grad_m and
+// an LDS chunk of the band; each pixel column is summed over the band's rows,
+// then each tile over its columns (short dependent chains: rows + columns,
+// not rows x columns).  fp32 sums in a different order than the reference's
+// upsample backward: grad_bits is checked to a tolerance.
+constexpr int QAT_FOLD_LDS = 8192;    // floats of pixel chunk
+constexpr int QAT_FOLD_SL = 8;        // slices loaded together
+
+// first index i in [0, n) with nearest_src(i, in, n) >= v (n if none)
+__device__ __forceinline__ int band_start(int v, int in, int n) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (nearest_src(mid, in, n) >= v) hi = mid; else lo = mid + 1;
+  }
+  return lo;
+}
+
+constexpr int QAT_FOLD_PX = 4;        // pixels per thread per round
+
+// per thread: pixels i0 + 256 j (j < QAT_FOLD_PX, i < np) of the chunk at p0;
+// all slice loads of a round issued before the first add, slices summed in order
+__device__ __forceinline__ void slice_sums(const float* pm, const float* pf, size_t plane, int nsl, int p0,
+                                           int i0, int np, float (&am)[QAT_FOLD_PX], float (&af)[QAT_FOLD_PX]) {
+  for (int s0 = 0; s0 < nsl; s0 += QAT_FOLD_SL) {
+    float vm[QAT_FOLD_PX][QAT_FOLD_SL], vf[QAT_FOLD_PX][QAT_FOLD_SL];
+#pragma unroll
+    for (int j = 0; j < QAT_FOLD_PX; ++j) {
+      const int p = p0 + imin_(i0 + 256 * j, np - 1);
+#pragma unroll
+      for (int k = 0; k < QAT_FOLD_SL; ++k) {
+        const size_t o = (size_t)imin_(s0 + k, nsl - 1) * plane + p;
+        vm[j][k] = pm[o];
+        vf[j][k] = pf[o];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < QAT_FOLD_PX; ++j)
+#pragma unroll
+      for (int k = 0; k < QAT_FOLD_SL; ++k)
+        if (s0 + k < nsl) {
+          am[j] = (s0 + k == 0) ? vm[j][k] : am[j] + vm[j][k];
+          af[j] = (s0 + k == 0) ? vf[j][k] : af[j] + vf[j][k];
+        }
+  }
+}
+
+// The whole fold of image b by one workgroup (the last backward unit of the
+// image to finish, inside the backward launch): per pixel the slice partials
+// in slice order -> grad_m and the per-pixel f-sum (kept in the slice-0
+// f plane), then per (tile row, pixel column) the band's rows in order, then
+// per tile its columns in order - the separate fold kernel's order.  buf:
+// 2048 floats of LDS; needs W <= 2048.
+constexpr int QAT_FUSED_BUF = 2048;
+__device__ void qat_fold_image(const mcaq_qat_scale& S, int b, float* buf) {
+  const int tid = threadIdx.x;
+  const int H = S.H, W = S.W, HW = H * W, ht = S.ht, wt = S.wt;
+  const int nsl = (S.C + 31) / 32;
+  const size_t plane = (size_t)S.B * HW;
+  const float* pm = S.work + (size_t)b * HW;
+  float* pf = S.work + (size_t)nsl * plane + (size_t)b * HW;
+  for (int i0 = tid; i0 < HW; i0 += 256 * QAT_FOLD_PX) {
+    float am[QAT_FOLD_PX], af[QAT_FOLD_PX];
+    slice_sums(pm, pf, plane, nsl, 0, i0, HW, am, af);
+#pragma unroll
+    for (int j = 0; j < QAT_FOLD_PX; ++j) {
+      const int i = i0 + 256 * j;
+      if (i < HW) {
+        if (S.gm) S.gm[(size_t)b * HW + i] = am[j];
+        pf[i] = af[j];   // this thread read every slice of pixel i above
+      }
+    }
+  }
+  if (!S.gb) return;
+  __syncthreads();   // pf of the whole image written (one CU: its L1 is shared)
+  const int rows_per = imax_(1, QAT_FUSED_BUF / W);
+  for (int th0 = 0; th0 < ht; th0 += rows_per) {
+    const int nr = imin_(ht - th0, rows_per);
+    for (int it = tid; it < nr * W; it += 256) {
+      const int r = it / W, w = it - r * W;
+      const int rs = band_start(th0 + r, ht, H), re = band_start(th0 + r + 1, ht, H);
+      float t = 0.0f;
+      for (int h = rs; h < re; ++h) t += pf[h * W + w];
+      buf[r * W + w] = t;
+    }
+    __syncthreads();
+    for (int it = tid; it < nr * wt; it += 256) {
+      const int r = it / wt, tw = it - r * wt;
+      const int cs = band_start(tw, wt, W), ce = band_start(tw + 1, wt, W);
+      float t = 0.0f;
+      for (int w = cs; w < ce; ++w) t += buf[r * W + w];
+      S.gb[((size_t)b * ht + th0 + r) * wt + tw] = t;
+    }
+    __syncthreads();
+  }
+}
+
 // unit = 256 pixels x 32 channels of one image (the pass-2 layout): lane l of
 // wave w owns pixels 4l..4l+3 and channels 8w..8w+7 of the slice (channel
 // loop fully unrolled: the compiler schedules the loads).  Measured slower at
@@ -42,6 +142,7 @@ template <bool kBwd, bool kVec>
 __global__ __launch_bounds__(256, MCAQ_QAT_MINW) void mcaq_qat_kernel(QatArgs a) {
   __shared__ float2 qt[32 * QAT_NB];
   __shared__ float red[2][4][256];
+  __shared__ int s_last;
   const int unit = blockIdx.x;
   int si = 0;
   while (si + 1 < a.nscales && unit >= a.s[si + 1].unit_begin) ++si;
@@ -155,56 +256,17 @@ __global__ __launch_bounds__(256, MCAQ_QAT_MINW) void mcaq_qat_kernel(QatArgs a)
     S.work[o] = tm;
     S.work[(size_t)nsl * plane + o] = tf;
   }
-}
-
-// one workgroup per (scale, image, tile row): the band of pixel rows whose
-// nearest tile row is th (binary search: nearest_src is monotone).  The
-// per-slice channel partials of the backward kernel are summed per pixel,
-// slices in order, the slice loads of a pixel issued together -> grad_m and
-// an LDS chunk of the band; each pixel column is summed over the band's rows,
-// then each tile over its columns (short dependent chains: rows + columns,
-// not rows x columns).  fp32 sums in a different order than the reference's
-// upsample backward: grad_bits is checked to a tolerance.
-constexpr int QAT_FOLD_LDS = 8192;    // floats of pixel chunk
-constexpr int QAT_FOLD_SL = 8;        // slices loaded together
-
-// first index i in [0, n) with nearest_src(i, in, n) >= v (n if none)
-__device__ __forceinline__ int band_start(int v, int in, int n) {
-  int lo = 0, hi = n;
-  while (lo < hi) {
-    const int mid = (lo + hi) >> 1;
-    if (nearest_src(mid, in, n) >= v) hi = mid; else lo = mid + 1;
-  }
-  return lo;
-}
-
-constexpr int QAT_FOLD_PX = 4;        // pixels per thread per round
-
-// per thread: pixels i0 + 256 j (j < QAT_FOLD_PX, i < np) of the chunk at p0;
-// all slice loads of a round issued before the first add, slices summed in order
-__device__ __forceinline__ void slice_sums(const float* pm, const float* pf, size_t plane, int nsl, int p0,
-                                           int i0, int np, float (&am)[QAT_FOLD_PX], float (&af)[QAT_FOLD_PX]) {
-  for (int s0 = 0; s0 < nsl; s0 += QAT_FOLD_SL) {
-    float vm[QAT_FOLD_PX][QAT_FOLD_SL], vf[QAT_FOLD_PX][QAT_FOLD_SL];
-#pragma unroll
-    for (int j = 0; j < QAT_FOLD_PX; ++j) {
-      const int p = p0 + imin_(i0 + 256 * j, np - 1);
-#pragma unroll
-      for (int k = 0; k < QAT_FOLD_SL; ++k) {
-        const size_t o = (size_t)imin_(s0 + k, nsl - 1) * plane + p;
-        vm[j][k] = pm[o];
-        vf[j][k] = pf[o];
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < QAT_FOLD_PX; ++j)
-#pragma unroll
-      for (int k = 0; k < QAT_FOLD_SL; ++k)
-        if (s0 + k < nsl) {
-          am[j] = (s0 + k == 0) ? vm[j][k] : am[j] + vm[j][k];
-          af[j] = (s0 + k == 0) ? vf[j][k] : af[j] + vf[j][k];
-        }
-  }
+  if (!S.arrive || (!S.gm && !S.gb)) return;
+  // last-arriver fold: release this unit's partials, count it in; the unit
+  // that completes image b acquires every partial of b and folds them
+  __threadfence();
+  __syncthreads();
+  if (tid == 0) s_last = atomicAdd(S.arrive + b, 1) == upi * nsl - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  qat_fold_image(S, b, &red[0][0][0]);
+  if (tid == 0) atomicExch(S.arrive + b, 0);   // zeroed for the next launch
 }
 
 __global__ __launch_bounds__(256) void mcaq_qat_fold_kernel(QatArgs a) {
@@ -214,6 +276,7 @@ __global__ __launch_bounds__(256) void mcaq_qat_fold_kernel(QatArgs a) {
   int si = 0;
   while (si + 1 < a.nscales && blk >= a.s[si + 1].block_begin) ++si;
   const mcaq_qat_scale S = si == 0 ? a.s[0] : si == 1 ? a.s[1] : a.s[2];
+  if (S.arrive) return;   // folded inside the backward launch
   const int lb = blk - S.block_begin;
   const int b = lb / S.ht, th = lb - (lb / S.ht) * S.ht;
   const int H = S.H, W = S.W, HW = H * W, wt = S.wt;
@@ -302,6 +365,7 @@ static int qat_args(const mcaq_qat_scale* scales, int nscales, bool bwd, mcaq::Q
         !s.x || !s.bits || !s.xmin || !s.xmax)
       return (int)hipErrorInvalidValue;
     if (bwd ? (!s.g || !s.gx || !s.work) : !s.y) return (int)hipErrorInvalidValue;
+    if (bwd && s.arrive && s.W > QAT_FUSED_BUF) return (int)hipErrorInvalidValue;
     a.s[i] = s;
     a.s[i].unit_begin = units;
     a.s[i].block_begin = blocks;
@@ -342,8 +406,9 @@ int mcaq_qat_backward(const mcaq_qat_scale* scales, int nscales, hipStream_t str
     launch_k((mcaq::mcaq_qat_kernel<true, false>), dim3(a.units_total), dim3(256), 0, stream, a);
   hipError_t le = hipGetLastError();
   if (le != hipSuccess) return (int)le;
+  // the separate fold only for scales without arrival counters
   bool fold = false;
-  for (int i = 0; i < nscales; ++i) fold = fold || scales[i].gm || scales[i].gb;
+  for (int i = 0; i < nscales; ++i) fold = fold || ((scales[i].gm || scales[i].gb) && !a.s[i].arrive);
   if (fold) launch_k(mcaq::mcaq_qat_fold_kernel, dim3(blocks), dim3(256), 0, stream, a);
   return (int)hipGetLastError();
 }

@@ -283,3 +283,39 @@ def test_mapper_train_mode_vs_reference(temp):
     for n, b in m.mapping_network.named_buffers():
         if b.dtype.is_floating_point:
             _allclose_rel(N(b), d[t + ".buf.mapping_network." + n], 1e-5)
+
+
+@pytest.mark.parametrize("shape", [(16, 64, 80, 80, 10, 10), (3, 40, 13, 17, 3, 4), (2, 256, 20, 20, 5, 5)])
+def test_qat_fold_in_launch_equals_fold_kernel(shape):
+    """The backward's in-launch fold (last unit of each image, arrival
+    counters) gives grad_m / grad_bits bit-identical to the separate fold
+    kernel (same summation order), leaves the counters zeroed, and repeated
+    launches (three scales in one launch, replayed) give the same bits."""
+    from mcaq_yolo_amd import abi, core
+    B, C, H, W, ht, wt = shape
+    rng = np.random.default_rng(7 + sum(shape))
+    x = T((rng.standard_normal((B, C, H, W)) * 1.5).astype(f32))
+    g = T(rng.standard_normal((B, C, H, W)).astype(f32))
+    bits = T(rng.uniform(2.0, 8.0, (B, ht, wt)).astype(f32))
+    m = T(rng.uniform(0.5, 1.0, (B, H, W)).astype(f32))
+    mn, mx = core._channel_minmax(x)
+    L = abi.lib()
+    outs = {}
+    arrive = torch.zeros(B, dtype=torch.int32, device=DEV)
+    for fused in (False, True, True):
+        gx = torch.empty_like(x)
+        gm = torch.empty(B, H, W, device=DEV)
+        gb = torch.empty(B, ht, wt, device=DEV)
+        work = torch.full((L.mcaq_qat_work_floats(B, C, H, W),), float("nan"), device=DEV)
+        q = core._qat_struct(x, bits, m, mn, mx)
+        q.g, q.gx, q.gm, q.gb, q.work = core._p(g), core._p(gx), core._p(gm), core._p(gb), core._p(work)
+        if fused:
+            q.arrive = core._p(arrive)
+        abi.check(L.mcaq_qat_backward(abi.ctypes.byref(q), 1, core._stream()), "mcaq_qat_backward")
+        torch.cuda.synchronize()
+        outs.setdefault(fused, []).append((N(gx), N(gm), N(gb)))
+    assert int(arrive.abs().sum()) == 0
+    ref = outs[False][0]
+    for got in outs[True]:
+        for a, b in zip(got, ref):
+            assert np.array_equal(a, b)
