@@ -253,20 +253,33 @@ __global__ __launch_bounds__(256, MCAQ_QAT_MINW) void mcaq_qat_kernel(QatArgs a)
     const float tf = ((red[1][0][tid] + red[1][1][tid]) + red[1][2][tid]) + red[1][3][tid];
     const size_t plane = (size_t)S.B * HW;
     const size_t o = ((size_t)slice * S.B + b) * HW + p;
-    S.work[o] = tm;
-    S.work[(size_t)nsl * plane + o] = tf;
+    if (S.arrive) {
+      // handed to the image's last unit inside this launch: write-through
+      // (sc1) stores, no release fence (cdna_hip_programming.md Guideline 16)
+      __hip_atomic_store(S.work + o, tm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(S.work + (size_t)nsl * plane + o, tf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      S.work[o] = tm;
+      S.work[(size_t)nsl * plane + o] = tf;
+    }
   }
   if (!S.arrive || (!S.gm && !S.gb)) return;
-  // last-arriver fold: release this unit's partials, count it in; the unit
-  // that completes image b acquires every partial of b and folds them
-  __threadfence();
+  // last-arriver fold: every storing wave drains its sc1 stores, then one
+  // lane counts the unit in; the unit that completes image b takes ONE
+  // agent-scope acquire and folds every partial of b
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (tid == 0) s_last = atomicAdd(S.arrive + b, 1) == upi * nsl - 1;
+  if (tid == 0)
+    s_last = __hip_atomic_fetch_add(S.arrive + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == upi * nsl - 1;
   __syncthreads();
   if (!s_last) return;
-  __threadfence();
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
   qat_fold_image(S, b, &red[0][0][0]);
-  if (tid == 0) atomicExch(S.arrive + b, 0);   // zeroed for the next launch
+  if (tid == 0) __hip_atomic_store(S.arrive + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // for the next launch
 }
 
 __global__ __launch_bounds__(256) void mcaq_qat_fold_kernel(QatArgs a) {
