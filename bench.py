@@ -196,7 +196,7 @@ def main_qat(args, world, rank, dev, pg):
     gms = [torch.empty(B, hh, ww, device=dev) for (hh, ww) in SIZES]
     gbs = [torch.empty_like(b) for b in bits]
     works = [torch.empty(L.mcaq_qat_work_floats(*x.shape), device=dev) for x in xs]
-    arrive = torch.zeros(3, B, dtype=torch.int32, device=dev)
+    arrive = torch.zeros(3, B * max(hh // grid for (hh, _) in SIZES), dtype=torch.int32, device=dev)
     arr, arr_u = (abi.QatScale * 3)(), (abi.QatScale * 3)()
     for i in range(3):
         q = core._qat_struct(xs[i], bits[i], ms[i], mm[i][0], mm[i][1])

@@ -187,10 +187,11 @@ typedef struct {
   const float* xmax;   /* (C) */
   int B, C, H, W, ht, wt;
   int unit_begin, block_begin;  /* set by the launcher */
-  int* arrive;         /* (B) zero-initialised arrival counters (left zeroed):
-                          the last backward unit of an image folds that
-                          image's partials into gm / gb inside the same
-                          launch; NULL: a separate fold kernel does it */
+  int* arrive;         /* (B, ht) zero-initialised arrival counters (left
+                          zeroed), 16 <= W <= 512: the last backward unit to
+                          finish a (image, tile row) band folds that band's
+                          partials into gm / gb inside the same launch;
+                          NULL: a separate fold kernel does it */
 } mcaq_qat_scale;
 int mcaq_qat_forward(const mcaq_qat_scale* scales, int nscales, hipStream_t stream);
 int mcaq_qat_backward(const mcaq_qat_scale* scales, int nscales, hipStream_t stream);

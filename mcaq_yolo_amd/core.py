@@ -767,8 +767,8 @@ def qat_quantize_backward(g, x, bits, m, xmin, xmax, want_gm=True, want_gb=True)
     work = torch.empty(L.mcaq_qat_work_floats(B, C, H, W), device=x.device)
     q = _qat_struct(x, bits, m, xmin, xmax)
     q.g, q.gx, q.gm, q.gb, q.work = _p(g), _p(gx), _p(gm), _p(gb), _p(work)
-    if (gm is not None or gb is not None) and W <= 2048:
-        q.arrive = _p(_arrive_counters(B, x.device))   # fold inside the backward launch
+    if (gm is not None or gb is not None) and 16 <= W <= 512:
+        q.arrive = _p(_arrive_counters(B * bits.shape[-2], x.device))   # fold inside the backward launch
     abi.check(L.mcaq_qat_backward(ctypes.byref(q), 1, _stream()), "mcaq_qat_backward")
     return gx, gb, gm
 

@@ -82,55 +82,59 @@ __device__ __forceinline__ void slice_sums(const float* pm, const float* pf, siz
   }
 }
 
-// The whole fold of image b by one workgroup (the last backward unit of the
-// image to finish, inside the backward launch): per pixel the slice partials
-// in slice order -> grad_m and the per-pixel f-sum (kept in the slice-0
-// f plane), then per (tile row, pixel column) the band's rows in order, then
-// per tile its columns in order - the separate fold kernel's order.  buf:
-// 2048 floats of LDS; needs W <= 2048.
-constexpr int QAT_FUSED_BUF = 2048;
-__device__ void qat_fold_image(const mcaq_qat_scale& S, int b, float* buf) {
-  const int tid = threadIdx.x;
-  const int H = S.H, W = S.W, HW = H * W, ht = S.ht, wt = S.wt;
+// Fold of one (image b, tile row th) band by one 256-thread workgroup: the
+// band's pixel rows in chunks of `cap` pixels (pl); per pixel the slice
+// partials in slice order -> grad_m and pl; per pixel column the band's rows
+// in order (col, W floats); per tile its columns in order -> grad_bits.  The
+// separate fold kernel runs it per block; the backward kernel's last unit of
+// a band runs it inside its own launch.
+__device__ void qat_fold_band(const mcaq_qat_scale& S, int b, int th, float* pl, float* col, int cap) {
+  const int H = S.H, W = S.W, HW = H * W, wt = S.wt;
   const int nsl = (S.C + 31) / 32;
   const size_t plane = (size_t)S.B * HW;
   const float* pm = S.work + (size_t)b * HW;
-  float* pf = S.work + (size_t)nsl * plane + (size_t)b * HW;
-  for (int i0 = tid; i0 < HW; i0 += 256 * QAT_FOLD_PX) {
-    float am[QAT_FOLD_PX], af[QAT_FOLD_PX];
-    slice_sums(pm, pf, plane, nsl, 0, i0, HW, am, af);
+  const float* pf = S.work + (size_t)nsl * plane + (size_t)b * HW;
+  const int rs = band_start(th, S.ht, H), re = band_start(th + 1, S.ht, H);
+  const int rows_per_chunk = imax_(1, cap / W);
+  for (int w = threadIdx.x; w < W; w += 256) col[w] = 0.0f;
+  for (int r0 = rs; r0 < re; r0 += rows_per_chunk) {
+    const int r1 = imin_(re, r0 + rows_per_chunk);
+    const int p0 = r0 * W, np = (r1 - r0) * W;
+    for (int i0 = threadIdx.x; i0 < np; i0 += 256 * QAT_FOLD_PX) {
+      float am[QAT_FOLD_PX], af[QAT_FOLD_PX];
+      slice_sums(pm, pf, plane, nsl, p0, i0, np, am, af);
 #pragma unroll
-    for (int j = 0; j < QAT_FOLD_PX; ++j) {
-      const int i = i0 + 256 * j;
-      if (i < HW) {
-        if (S.gm) S.gm[(size_t)b * HW + i] = am[j];
-        pf[i] = af[j];   // this thread read every slice of pixel i above
+      for (int j = 0; j < QAT_FOLD_PX; ++j) {
+        const int i = i0 + 256 * j;
+        if (i < np) {
+          if (S.gm) S.gm[(size_t)b * HW + p0 + i] = am[j];
+          pl[i] = af[j];
+        }
       }
     }
+    __syncthreads();
+    // per pixel column: the band's rows of this chunk, in order
+    if (S.gb)
+      for (int w = threadIdx.x; w < W; w += 256) {
+        float t = col[w];
+        for (int r = 0; r < r1 - r0; ++r) t += pl[r * W + w];
+        col[w] = t;
+      }
+    __syncthreads();
   }
   if (!S.gb) return;
-  __syncthreads();   // pf of the whole image written (one CU: its L1 is shared)
-  const int rows_per = imax_(1, QAT_FUSED_BUF / W);
-  for (int th0 = 0; th0 < ht; th0 += rows_per) {
-    const int nr = imin_(ht - th0, rows_per);
-    for (int it = tid; it < nr * W; it += 256) {
-      const int r = it / W, w = it - r * W;
-      const int rs = band_start(th0 + r, ht, H), re = band_start(th0 + r + 1, ht, H);
-      float t = 0.0f;
-      for (int h = rs; h < re; ++h) t += pf[h * W + w];
-      buf[r * W + w] = t;
-    }
-    __syncthreads();
-    for (int it = tid; it < nr * wt; it += 256) {
-      const int r = it / wt, tw = it - r * wt;
-      const int cs = band_start(tw, wt, W), ce = band_start(tw + 1, wt, W);
-      float t = 0.0f;
-      for (int w = cs; w < ce; ++w) t += buf[r * W + w];
-      S.gb[((size_t)b * ht + th0 + r) * wt + tw] = t;
-    }
-    __syncthreads();
+  // tile tw: its columns, in order
+  for (int tw = threadIdx.x; tw < wt; tw += 256) {
+    const int cs = band_start(tw, wt, W), ce = band_start(tw + 1, wt, W);
+    float t = 0.0f;
+    for (int w = cs; w < ce; ++w) t += col[w];
+    S.gb[((size_t)b * S.ht + th) * wt + tw] = t;
   }
 }
+
+// in-launch fold: the backward kernel's LDS lent to the band fold
+constexpr int QAT_FUSED_BUF = 2048;   // floats: col (QAT_FUSED_MAXW) + pixel chunk
+constexpr int QAT_FUSED_MAXW = 512;
 
 // unit = 256 pixels x 32 channels of one image (the pass-2 layout): lane l of
 // wave w owns pixels 4l..4l+3 and channels 8w..8w+7 of the slice (channel
@@ -142,7 +146,7 @@ template <bool kBwd, bool kVec>
 __global__ __launch_bounds__(256, MCAQ_QAT_MINW) void mcaq_qat_kernel(QatArgs a) {
   __shared__ float2 qt[32 * QAT_NB];
   __shared__ float red[2][4][256];
-  __shared__ int s_last;
+  __shared__ int s_last;   // bands completed by this unit (bit per band)
   const int unit = blockIdx.x;
   int si = 0;
   while (si + 1 < a.nscales && unit >= a.s[si + 1].unit_begin) ++si;
@@ -264,22 +268,40 @@ __global__ __launch_bounds__(256, MCAQ_QAT_MINW) void mcaq_qat_kernel(QatArgs a)
     }
   }
   if (!S.arrive || (!S.gm && !S.gb)) return;
-  // last-arriver fold: every storing wave drains its sc1 stores, then one
-  // lane counts the unit in; the unit that completes image b takes ONE
-  // agent-scope acquire and folds every partial of b
+  // last-arriver fold per (image, tile row): every storing wave drains its
+  // sc1 stores; one lane per tile-row band this unit's pixels touch counts
+  // the unit in (a band is complete after nsl x the chunks overlapping it);
+  // a unit that completes a band takes ONE agent-scope acquire and folds it
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (tid == 0)
-    s_last = __hip_atomic_fetch_add(S.arrive + b, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == upi * nsl - 1;
+  const int plo = chunk * 256, phi = imin_(HW, plo + 256) - 1;
+  const int thA = nearest_src(plo / S.W, S.ht, S.H), thB = nearest_src(phi / S.W, S.ht, S.H);
+  if (tid == 0) s_last = 0;
   __syncthreads();
-  if (!s_last) return;
+  if (tid <= thB - thA) {
+    const int th = thA + tid;
+    const int rs = band_start(th, S.ht, S.H), re = band_start(th + 1, S.ht, S.H);
+    const int need = nsl * ((re * S.W + 255) / 256 - (rs * S.W) / 256);
+    const int old = __hip_atomic_fetch_add(S.arrive + (size_t)b * S.ht + th, 1, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+    if (old == need - 1) atomicOr(&s_last, 1 << tid);
+  }
+  __syncthreads();
+  const int done = s_last;
+  if (!done) return;
   if (tid == 0) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  qat_fold_image(S, b, &red[0][0][0]);
-  if (tid == 0) __hip_atomic_store(S.arrive + b, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // for the next launch
+  float* buf = &red[0][0][0];
+  for (int k = 0; k <= thB - thA; ++k)
+    if (done & (1 << k)) {
+      qat_fold_band(S, b, thA + k, buf + QAT_FUSED_MAXW, buf, QAT_FUSED_BUF - QAT_FUSED_MAXW);
+      __syncthreads();
+      if (tid == 0)   // zeroed for the next launch
+        __hip_atomic_store(S.arrive + (size_t)b * S.ht + thA + k, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 }
 
 __global__ __launch_bounds__(256) void mcaq_qat_fold_kernel(QatArgs a) {
@@ -292,47 +314,7 @@ __global__ __launch_bounds__(256) void mcaq_qat_fold_kernel(QatArgs a) {
   if (S.arrive) return;   // folded inside the backward launch
   const int lb = blk - S.block_begin;
   const int b = lb / S.ht, th = lb - (lb / S.ht) * S.ht;
-  const int H = S.H, W = S.W, HW = H * W, wt = S.wt;
-  const int nsl = (S.C + 31) / 32;
-  const size_t plane = (size_t)S.B * HW;
-  const float* pm = S.work + (size_t)b * HW;
-  const float* pf = S.work + (size_t)nsl * plane + (size_t)b * HW;
-  const int rs = band_start(th, S.ht, H), re = band_start(th + 1, S.ht, H);
-  const int rows_per_chunk = imax_(1, QAT_FOLD_LDS / W);
-  for (int w = threadIdx.x; w < W; w += 256) col[w] = 0.0f;
-  for (int r0 = rs; r0 < re; r0 += rows_per_chunk) {
-    const int r1 = imin_(re, r0 + rows_per_chunk);
-    const int p0 = r0 * W, np = (r1 - r0) * W;
-    for (int i0 = threadIdx.x; i0 < np; i0 += 256 * QAT_FOLD_PX) {
-      float am[QAT_FOLD_PX], af[QAT_FOLD_PX];
-      slice_sums(pm, pf, plane, nsl, p0, i0, np, am, af);
-#pragma unroll
-      for (int j = 0; j < QAT_FOLD_PX; ++j) {
-        const int i = i0 + 256 * j;
-        if (i < np) {
-          if (S.gm) S.gm[(size_t)b * HW + p0 + i] = am[j];
-          pl[i] = af[j];
-        }
-      }
-    }
-    __syncthreads();
-    // per pixel column: the band's rows of this chunk, in order
-    if (S.gb)
-      for (int w = threadIdx.x; w < W; w += 256) {
-        float t = col[w];
-        for (int r = 0; r < r1 - r0; ++r) t += pl[r * W + w];
-        col[w] = t;
-      }
-    __syncthreads();
-  }
-  if (!S.gb) return;
-  // tile tw: its columns, in order
-  for (int tw = threadIdx.x; tw < wt; tw += 256) {
-    const int cs = band_start(tw, wt, W), ce = band_start(tw + 1, wt, W);
-    float t = 0.0f;
-    for (int w = cs; w < ce; ++w) t += col[w];
-    S.gb[((size_t)b * S.ht + th) * wt + tw] = t;
-  }
+  qat_fold_band(S, b, th, pl, col, QAT_FOLD_LDS);
 }
 
 // running <- a * running + c * batch (first batch: running <- batch),
@@ -378,7 +360,8 @@ static int qat_args(const mcaq_qat_scale* scales, int nscales, bool bwd, mcaq::Q
         !s.x || !s.bits || !s.xmin || !s.xmax)
       return (int)hipErrorInvalidValue;
     if (bwd ? (!s.g || !s.gx || !s.work) : !s.y) return (int)hipErrorInvalidValue;
-    if (bwd && s.arrive && s.W > QAT_FUSED_BUF) return (int)hipErrorInvalidValue;
+    // in-launch fold: col fits the lent LDS, and a 256-pixel unit touches < 32 bands
+    if (bwd && s.arrive && (s.W > QAT_FUSED_MAXW || s.W < 16)) return (int)hipErrorInvalidValue;
     a.s[i] = s;
     a.s[i].unit_begin = units;
     a.s[i].block_begin = blocks;

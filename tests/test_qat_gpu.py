@@ -285,7 +285,8 @@ def test_mapper_train_mode_vs_reference(temp):
             _allclose_rel(N(b), d[t + ".buf.mapping_network." + n], 1e-5)
 
 
-@pytest.mark.parametrize("shape", [(16, 64, 80, 80, 10, 10), (3, 40, 13, 17, 3, 4), (2, 256, 20, 20, 5, 5)])
+@pytest.mark.parametrize("shape", [(16, 64, 80, 80, 10, 10), (3, 40, 19, 17, 3, 4), (2, 256, 20, 20, 5, 5),
+                                   (2, 32, 44, 52, 11, 13)])
 def test_qat_fold_in_launch_equals_fold_kernel(shape):
     """The backward's in-launch fold (last unit of each image, arrival
     counters) gives grad_m / grad_bits bit-identical to the separate fold
@@ -301,7 +302,7 @@ def test_qat_fold_in_launch_equals_fold_kernel(shape):
     mn, mx = core._channel_minmax(x)
     L = abi.lib()
     outs = {}
-    arrive = torch.zeros(B, dtype=torch.int32, device=DEV)
+    arrive = torch.zeros(B * ht, dtype=torch.int32, device=DEV)
     for fused in (False, True, True):
         gx = torch.empty_like(x)
         gm = torch.empty(B, H, W, device=DEV)
