@@ -736,6 +736,11 @@ def qat_quantize(x, bits, m, xmin, xmax):
     return y
 
 
+# The backward's in-launch fold (arrival counters, last unit of each tile-row
+# band folds it) measured slower than backward kernel + fold kernel at config
+# 5 (46.4 vs 32.1 + 8.5 us: every unit drains its stores before counting in),
+# so the two-kernel form is the default; the in-launch form stays selectable.
+FOLD_IN_LAUNCH = False
 _ARRIVE = {}
 
 
@@ -767,7 +772,7 @@ def qat_quantize_backward(g, x, bits, m, xmin, xmax, want_gm=True, want_gb=True)
     work = torch.empty(L.mcaq_qat_work_floats(B, C, H, W), device=x.device)
     q = _qat_struct(x, bits, m, xmin, xmax)
     q.g, q.gx, q.gm, q.gb, q.work = _p(g), _p(gx), _p(gm), _p(gb), _p(work)
-    if (gm is not None or gb is not None) and 16 <= W <= 512:
+    if FOLD_IN_LAUNCH and (gm is not None or gb is not None) and 16 <= W <= 512:
         q.arrive = _p(_arrive_counters(B * bits.shape[-2], x.device))   # fold inside the backward launch
     abi.check(L.mcaq_qat_backward(ctypes.byref(q), 1, _stream()), "mcaq_qat_backward")
     return gx, gb, gm
