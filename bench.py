@@ -492,6 +492,54 @@ class Runner:
             torch.cuda.current_stream().wait_stream(st)
 
 
+class SplitRunner:
+    """--schedule split (N = 1, eager): the HBM passes of every batch on ONE
+    streaming stream, back to back (stats(j + L), then quant(j)), the
+    per-image morphology of each batch on one of two high-priority streams
+    between them (after stats(j) via an event; quant(j) waits for its tiles
+    pass).  L batches of look-ahead cover the morphology chain; plan buffers
+    are reused every len(plans) >= L + 1 batches, and every reuse hazard is
+    ordered by the streaming stream's program order."""
+
+    def __init__(self, plans, lookahead):
+        if len(plans) < lookahead + 1:
+            raise ValueError("split schedule needs >= lookahead + 1 input batches")
+        self.plans, self.L = plans, lookahead
+        self.S = torch.cuda.Stream(priority=0)
+        lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") else (0, -1)
+        self.M = [torch.cuda.Stream(priority=hi) for _ in range(2)]
+        self.ev_s, self.ev_t = {}, {}
+        self.i = 0
+        for j in range(lookahead):
+            self._front(j)
+
+    def _front(self, j):
+        plan = self.plans[j % len(self.plans)]
+        with torch.cuda.stream(self.S):
+            plan.launch_stats(self.S)
+            e = torch.cuda.Event()
+            e.record(self.S)
+        M = self.M[j % 2]
+        M.wait_event(e)
+        with torch.cuda.stream(M):
+            plan.launch_morph(M)
+            t = torch.cuda.Event()
+            t.record(M)
+        self.ev_t[j] = t
+
+    def step(self):
+        j = self.i
+        self.i += 1
+        self._front(j + self.L)
+        self.S.wait_event(self.ev_t.pop(j))
+        with torch.cuda.stream(self.S):
+            self.plans[j % len(self.plans)].launch_quant(self.S)
+
+    def sync(self):
+        for st in [self.S] + self.M:
+            torch.cuda.current_stream().wait_stream(st)
+
+
 def kernel_timing(plan, reps=20):
     """Per-launch device time of each kernel of a step, in sequence: `reps`
     single-batch steps on one stream.  Pass 1 and pass 2 are launched through
@@ -535,6 +583,10 @@ def main():
     ap.add_argument("--e2e", action="store_true", help="only the end-to-end line (run_e2e)")
     ap.add_argument("--amp", action="store_true", help="--e2e: network under bf16 autocast (hooks stay fp32)")
     ap.add_argument("--eager", action="store_true", help="no HIP graphs")
+    ap.add_argument("--schedule", choices=("streams", "split"), default="streams",
+                    help="streams: --pipeline batches in flight, one HIP graph each (default); split: HBM passes "
+                         "on one stream, morphology on two (SplitRunner, eager, N = 1)")
+    ap.add_argument("--lookahead", type=int, default=3, help="--schedule split: batches of look-ahead")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -567,7 +619,10 @@ def main():
     cm, mm, sm = load_blobs(dev)
     geoms = [ScaleGeom(B, c, h, w, grid) for c, (h, w) in zip(chans, SIZES)]
     plans = []
-    for p in range(max(args.inputs or max(3, depth), depth)):
+    nin = max(args.inputs or max(3, depth), depth)
+    if args.schedule == "split":
+        nin = max(nin, args.lookahead + 1)
+    for p in range(nin):
         # each batch in flight has its own synthetic input (seeded per rank and slot)
         feats = [synth_features(B, c, h, w, 1000 * args.config + i + 7919 * rank + 104729 * p, dev)
                  for i, (c, (h, w)) in enumerate(zip(chans, SIZES))]
@@ -578,8 +633,13 @@ def main():
         plans.append(plan)
     torch.cuda.synchronize()
 
-    use_graph = not args.eager
-    runner = Runner(plans, pg, use_graph, depth)
+    use_graph = not args.eager and args.schedule == "streams"
+    if args.schedule == "split":
+        if pg is not None:
+            raise SystemExit("--schedule split is a single-GPU experiment")
+        runner = SplitRunner(plans, args.lookahead)
+    else:
+        runner = Runner(plans, pg, use_graph, depth)
     for _ in range(max(args.warmup, 1)):
         runner.step()
     runner.sync()
@@ -661,7 +721,7 @@ def main():
                                    "quant/dequant; YOLOv8 network excluded (see e2e)" % (name, B, grid, mapper),
                        "global_batch": world * B, "grid_size": grid, "mapper": mapper,
                        "parallelism": "dp%d" % world, "hip_graph": use_graph,
-                       "batches_in_flight": depth, "input_batches": len(plans),
+                       "batches_in_flight": depth, "schedule": args.schedule if args.schedule == "streams" else "split (look-ahead %d)" % args.lookahead, "input_batches": len(plans),
                        "latency_ms_single_batch": round(latency_ms, 4),
                        "host_enqueue_us_per_step": round(t_enq / args.steps * 1e6, 1)},
             # north star: the whole fused complexity + quant path,
