@@ -313,7 +313,7 @@ def _shift_class_bias(m, imgs, target=E2E_TARGET_CANDIDATES):
     return delta
 
 
-def run_e2e(cfg, steps, warmup, world, rank, dev, pg, amp=False, eager=False):
+def run_e2e(cfg, steps, warmup, world, rank, dev, pg, amp=False, eager=False, fuse=True, channels_last=False):
     """End-to-end MCAQ inference: YOLOv8 (MIOpen
     convolutions, seeded weights) with the MCAQ hooks at C3/C4/C5 on the HIP
     kernels, Detect decode, batched HIP NMS; N > 1: each rank its batch shard,
@@ -326,10 +326,15 @@ def run_e2e(cfg, steps, warmup, world, rank, dev, pg, amp=False, eager=False):
     m = MCAQYOLO(name, grid_size=grid, bit_mapping=mapper, device=dev)
     m.load_state_dict(hook_state_dict(dev), strict=False)
     m.eval()
+    if fuse:
+        m.fuse()        # Conv + BN folded, as the reference's ultralytics predictor does
     if pg is not None:
         m.process_group, m.batch_offset, m.batch_total = pg, rank * B, world * B
     g = torch.Generator(device="cpu").manual_seed(1000 * cfg + rank)
     imgs = torch.rand(B, 3, 640, 640, generator=g).to(dev)
+    if channels_last:
+        m.model.to(memory_format=torch.channels_last)
+        imgs = imgs.contiguous(memory_format=torch.channels_last)
     delta = _shift_class_bias(m, imgs)
 
     def step(hooks=True):
@@ -395,6 +400,7 @@ def run_e2e(cfg, steps, warmup, world, rank, dev, pg, amp=False, eager=False):
                                   " + RCCL detection all-gather" if pg is not None else ""),
                    "global_batch": world * B, "grid_size": grid, "mapper": mapper,
                    "parallelism": "dp%d" % world, "hip_graph": pg is None and not eager,
+                   "conv_bn_fused": fuse, "channels_last": channels_last,
                    "network_only_ms_per_step": round(net_s * 1e3, 4),
                    "mcaq_hooks_and_nms_ms_per_step": round((step_s - net_s) * 1e3, 4),
                    "detections_per_image": round(float(cnt.float().mean()), 2)},
@@ -402,7 +408,10 @@ def run_e2e(cfg, steps, warmup, world, rank, dev, pg, amp=False, eager=False):
 
 
 def main_e2e(args, world, rank, dev, pg):
-    out = run_e2e(args.config, args.steps, args.warmup, world, rank, dev, pg, args.amp, args.eager)
+    if args.find:
+        torch.backends.cudnn.benchmark = True
+    out = run_e2e(args.config, args.steps, args.warmup, world, rank, dev, pg, args.amp, args.eager,
+                  not args.no_fuse, args.channels_last)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if pg is not None:
@@ -582,6 +591,9 @@ def main():
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (YOLOv8 + hooks + NMS) leg")
     ap.add_argument("--e2e", action="store_true", help="only the end-to-end line (run_e2e)")
     ap.add_argument("--amp", action="store_true", help="--e2e: network under bf16 autocast (hooks stay fp32)")
+    ap.add_argument("--no-fuse", action="store_true", help="--e2e: keep Conv and BatchNorm separate")
+    ap.add_argument("--channels-last", action="store_true", help="--e2e: NHWC network (experiment)")
+    ap.add_argument("--find", action="store_true", help="--e2e: MIOpen Find (torch.backends.cudnn.benchmark)")
     ap.add_argument("--eager", action="store_true", help="no HIP graphs")
     ap.add_argument("--schedule", choices=("streams", "split"), default="streams",
                     help="streams: --pipeline batches in flight, one HIP graph each (default); split: HBM passes "

@@ -208,8 +208,10 @@ int mcaq_ema_stats(const float* batch_min, const float* batch_max, float* runnin
  * (agnostic: none), greedy IoU > iou_thres suppression (torchvision CPU
  * arithmetic), first max_det kept.  out (B, max_det, 6) = x1 y1 x2 y2 conf
  * cls (rows past counts[b] zeroed), counts (B) int32.  work:
- * mcaq_nms_work_floats(B, N, max_det) floats (kept boxes, candidate classes and,
- * above 16,384 anchors, a pow2(N) global key array per image). */
+ * mcaq_nms_work_floats(B, N, max_det) floats (kept boxes, candidate classes,
+ * candidate counts and a pow2(N) key array per image).  Two kernels and a
+ * 4*B-byte memset: a scan over B x ceil(N/256) workgroups, then one
+ * workgroup per image. */
 int mcaq_nms(const float* pred, int B, int no, int N, int nc, float conf_thres, double iou_thres, int max_det,
              int max_nms, float max_wh, int agnostic, float* out, int* counts, float* work, hipStream_t stream);
 size_t mcaq_nms_work_floats(int B, int N, int max_det);

@@ -14,18 +14,19 @@
 //              for an earlier kept box, IoU = inter / (area_k + area_c - inter)
 //              in fp32, compared in double; the first max_det kept boxes.
 //
-// One 1024-thread workgroup per image.  Phase 1 streams the (4+nc, N) slab of
-// the image once (coalesced over anchors), compacting candidates into a
-// 64-bit key array (ordered-score << 32 | anchor) and recording each
-// candidate's class in the workspace.  Up to NMS_LDS_KEYS candidates the keys
-// live in LDS; beyond that (large inputs, e.g. 1280x1280 = 33,600 anchors
-// at a low threshold) they are also written to a global key array sized
-// pow2(N) per image and sorted there.  Phase 2 bitonic-sorts the keys.
-// Phase 3 walks the sorted list in chunks of 256: every candidate is tested
-// against the boxes kept so far (4 threads per candidate), a 256 x 256
-// chunk-local suppression bit matrix is built (one 64-bit word per thread),
-// then one lane resolves the chunk sequentially with bit operations -
-// exactly the greedy order of the CPU kernel.
+// Two launches.  The scan kernel spreads the (4+nc, N) slab of every image
+// over B x ceil(N/256) workgroups (one anchor per thread, class rows read
+// coalesced over anchors): the best class score and first argmax per anchor,
+// candidates (score > conf) compacted per image with one atomic per wave into
+// a 64-bit key array (ordered-score << 32 | anchor) in the workspace, each
+// candidate's class recorded.  The NMS kernel (one 1024-thread workgroup per
+// image) then sorts the image's keys - in LDS up to NMS_LDS_KEYS candidates,
+// in the global key array beyond (large inputs, e.g. 1280x1280 = 33,600
+// anchors at a low threshold) - and walks them in chunks of 256: every
+// candidate is tested against the boxes kept so far (4 threads per
+// candidate), a 256 x 256 chunk-local suppression bit matrix is built (one
+// 64-bit word per thread), then one lane resolves the chunk sequentially with
+// bit operations - exactly the greedy order of the CPU kernel.
 #pragma once
 
 namespace mcaq {
@@ -40,7 +41,8 @@ struct NmsArgs {
   int* counts;         // (B)
   float* kept;         // (B, max_det, 8) workspace: offset box + area
   int* cls;            // (B, N) workspace: class of each candidate anchor
-  unsigned long long* gkeys;   // (B, np2) workspace when N > NMS_LDS_KEYS, else unused
+  int* ncand;          // (B) candidate counts (zeroed before the scan)
+  unsigned long long* gkeys;   // (B, pow2(N)) candidate keys
   int B, no, N, np2N, nc, max_det, max_nms, agnostic;
   float conf, max_wh;
   double iou;
@@ -86,6 +88,39 @@ __device__ __forceinline__ void nms_bitonic(KeyT* keys, int np2, int tid) {
   }
 }
 
+constexpr int NMS_SCAN_THREADS = 256;
+
+__global__ __launch_bounds__(NMS_SCAN_THREADS) void mcaq_nms_scan_kernel(NmsArgs a) {
+  const int b = blockIdx.y;
+  const int N = a.N;
+  const int ai = blockIdx.x * NMS_SCAN_THREADS + threadIdx.x;
+  const float* P = a.pred + (size_t)b * a.no * N;
+  bool cand = false;
+  float best = 0.0f;
+  int bj = 0;
+  if (ai < N) {
+    best = P[(size_t)4 * N + ai];
+    for (int c = 1; c < a.nc; ++c) {
+      const float v = P[(size_t)(4 + c) * N + ai];
+      if (v > best) { best = v; bj = c; }
+    }
+    cand = best > a.conf;
+  }
+  // one atomic per wave: slots in lane order
+  const unsigned long long mask = __ballot(cand);
+  if (!mask) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((long long)mask) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(a.ncand + b, __popcll(mask));
+  base = __shfl(base, leader);
+  if (cand) {
+    const int slot = base + __popcll(mask & ((1ull << lane) - 1));
+    a.gkeys[(size_t)b * a.np2N + slot] = ((unsigned long long)nms_score_key(best) << 32) | (unsigned int)ai;
+    a.cls[(size_t)b * N + ai] = bj;
+  }
+}
+
 __global__ __launch_bounds__(NMS_THREADS) void mcaq_nms_kernel(NmsArgs a) {
   __shared__ unsigned long long lkeys[NMS_LDS_KEYS];
   __shared__ float4 cbox[NMS_CHUNK];        // offset boxes of the chunk
@@ -93,7 +128,7 @@ __global__ __launch_bounds__(NMS_THREADS) void mcaq_nms_kernel(NmsArgs a) {
   __shared__ float carea[NMS_CHUNK], cscore[NMS_CHUNK], ccls[NMS_CHUNK];
   __shared__ int csup[NMS_CHUNK];
   __shared__ unsigned long long cmask[NMS_CHUNK][4];
-  __shared__ int s_cnt, s_K;
+  __shared__ int s_K;
 
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
@@ -101,37 +136,17 @@ __global__ __launch_bounds__(NMS_THREADS) void mcaq_nms_kernel(NmsArgs a) {
   const float* P = a.pred + (size_t)b * a.no * N;
   float* kept = a.kept + (size_t)b * a.max_det * 8;
   float* out = a.out + (size_t)b * a.max_det * 6;
-  int* ccl = a.cls + (size_t)b * N;
-  const bool big = N > NMS_LDS_KEYS;
-  unsigned long long* gk = big ? a.gkeys + (size_t)b * a.np2N : nullptr;
-  if (tid == 0) { s_cnt = 0; s_K = 0; }
-  __syncthreads();
-
-  // ---- phase 1: candidates (max class score > conf), compacted
-  for (int ai = tid; ai < N; ai += NMS_THREADS) {
-    float best = P[(size_t)4 * N + ai];
-    int bj = 0;
-    for (int c = 1; c < a.nc; ++c) {
-      const float v = P[(size_t)(4 + c) * N + ai];
-      if (v > best) { best = v; bj = c; }
-    }
-    if (best > a.conf) {
-      const int slot = atomicAdd(&s_cnt, 1);
-      const unsigned long long key = ((unsigned long long)nms_score_key(best) << 32) | (unsigned int)ai;
-      if (slot < NMS_LDS_KEYS) lkeys[slot] = key;
-      if (big) gk[slot] = key;
-      ccl[ai] = bj;
-    }
-  }
-  __syncthreads();
-  const int n = s_cnt;
+  const int* ccl = a.cls + (size_t)b * N;
+  unsigned long long* gk = a.gkeys + (size_t)b * a.np2N;
+  const int n = a.ncand[b];
+  if (tid == 0) s_K = 0;
   int np2 = 1;
   while (np2 < n) np2 <<= 1;
   const bool inlds = n <= NMS_LDS_KEYS;
 
-  // ---- phase 2: bitonic sort (ascending key = score desc, anchor asc)
+  // ---- bitonic sort of the scan's keys (ascending key = score desc, anchor asc)
   if (inlds) {
-    for (int i = n + tid; i < np2; i += NMS_THREADS) lkeys[i] = ~0ull;
+    for (int i = tid; i < np2; i += NMS_THREADS) lkeys[i] = i < n ? gk[i] : ~0ull;
     __syncthreads();
     nms_bitonic(lkeys, np2, tid);
   } else {
@@ -232,9 +247,8 @@ static size_t nms_np2(int N) {
 
 size_t mcaq_nms_work_floats(int B, int N, int max_det) {
   if (B <= 0 || N < 0 || max_det <= 0) return 0;
-  size_t per = (size_t)max_det * 8 + (size_t)N;                     // kept boxes + candidate classes
-  if (N > mcaq::NMS_LDS_KEYS) per += 2 * nms_np2(N);                // global keys (u64)
-  return (size_t)B * per + 2;                                        // +2: 8-byte alignment of the keys
+  // kept boxes + candidate classes + counts, then the pow2(N) key arrays (u64)
+  return (size_t)B * ((size_t)max_det * 8 + (size_t)N + 1) + 2 + (size_t)B * 2 * nms_np2(N);
 }
 
 int mcaq_nms(const float* pred, int B, int no, int N, int nc, float conf_thres, double iou_thres, int max_det,
@@ -246,13 +260,22 @@ int mcaq_nms(const float* pred, int B, int no, int N, int nc, float conf_thres, 
   mcaq::NmsArgs a;
   a.pred = pred; a.out = out; a.counts = counts; a.kept = work;
   a.cls = reinterpret_cast<int*>(work + (size_t)B * max_det * 8);
+  a.ncand = a.cls + (size_t)B * N;
   {
-    const uintptr_t g = reinterpret_cast<uintptr_t>(work + (size_t)B * max_det * 8 + (size_t)B * N);
+    const uintptr_t g = reinterpret_cast<uintptr_t>(a.ncand + B);
     a.gkeys = reinterpret_cast<unsigned long long*>((g + 7) & ~(uintptr_t)7);
   }
   a.np2N = (int)nms_np2(N);
   a.B = B; a.no = no; a.N = N; a.nc = nc; a.max_det = max_det; a.max_nms = max_nms;
   a.agnostic = agnostic ? 1 : 0; a.conf = conf_thres; a.max_wh = max_wh; a.iou = iou_thres;
+  hipError_t e = hipMemsetAsync(a.ncand, 0, sizeof(int) * (size_t)B, stream);
+  if (e != hipSuccess) return (int)e;
+  if (N > 0) {
+    hipLaunchKernelGGL(mcaq::mcaq_nms_scan_kernel, dim3((N + mcaq::NMS_SCAN_THREADS - 1) / mcaq::NMS_SCAN_THREADS, B),
+                       dim3(mcaq::NMS_SCAN_THREADS), 0, stream, a);
+    e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+  }
   hipLaunchKernelGGL(mcaq::mcaq_nms_kernel, dim3(B), dim3(mcaq::NMS_THREADS), 0, stream, a);
   return (int)hipGetLastError();
 }

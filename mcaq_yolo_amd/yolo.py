@@ -73,6 +73,22 @@ class Conv(nn.Module):
     def forward(self, x):
         return self.act(self.bn(self.conv(x)))
 
+    @torch.no_grad()
+    def fuse(self):
+        """Fold the (eval) BatchNorm into the convolution, as ultralytics'
+        inference AutoBackend does by default (fuse_conv_and_bn): w' = w * g /
+        sqrt(var + eps), b' = beta - mean * g / sqrt(var + eps)."""
+        if isinstance(self.bn, nn.Identity):
+            return self
+        bn, conv = self.bn, self.conv
+        scale = bn.weight / torch.sqrt(bn.running_var + bn.eps)
+        fused = nn.Conv2d(conv.in_channels, conv.out_channels, conv.kernel_size, conv.stride, conv.padding,
+                          groups=conv.groups, bias=True).to(conv.weight.device)
+        fused.weight.copy_(conv.weight * scale.reshape(-1, 1, 1, 1))
+        fused.bias.copy_(bn.bias - bn.running_mean * scale)
+        self.conv, self.bn = fused, nn.Identity()
+        return self
+
 
 class Bottleneck(nn.Module):
     def __init__(self, c1, c2, shortcut=True, g=1, k=(3, 3), e=0.5):
@@ -245,6 +261,13 @@ class DetectionModel(nn.Module):
         self.stride = det.stride
         det.bias_init()
 
+    def fuse(self):
+        """Conv + BatchNorm folding for inference (ultralytics DetectionModel.fuse)."""
+        for mod in self.modules():
+            if isinstance(mod, Conv):
+                mod.fuse()
+        return self
+
     def forward(self, x):
         y = []
         for m in self.model:
@@ -311,6 +334,13 @@ class MCAQYOLO(MCAQHooks):
         if str(device).startswith("cuda") and torch.cuda.is_available():
             self.to(device)
         self.register(self.model.model)
+
+    def fuse(self):
+        """Fold every Conv's BatchNorm into its convolution for inference (what
+        the reference's ultralytics Predictor does through AutoBackend(fuse=True));
+        the hooks stay registered on the same layers."""
+        self.model.fuse()
+        return self
 
     def load_checkpoint(self, sd):
         """Load a reference MCAQYOLO state_dict ('model.model.<i>...', hook

@@ -98,3 +98,26 @@ def test_checkpoint_loading_checks_keys(tmp_path):
     partial = {kk: v for kk, v in src.state_dict().items() if not kk.startswith("model.model.22")}
     with pytest.raises(RuntimeError, match="unloaded"):
         dst.load_checkpoint(partial)
+
+
+def test_conv_bn_fuse_matches_unfused():
+    """DetectionModel.fuse() (Conv + eval BatchNorm folded, ultralytics'
+    inference default) gives the same detections head output to fp32
+    rounding, and leaves no BatchNorm in the network."""
+    import torch
+    from mcaq_yolo_amd.yolo import DetectionModel
+    torch.manual_seed(0)
+    m = DetectionModel("yolov8n").eval()
+    for mod in m.modules():                    # non-trivial BN statistics
+        if isinstance(mod, torch.nn.BatchNorm2d):
+            mod.running_mean.uniform_(-0.5, 0.5)
+            mod.running_var.uniform_(0.5, 2.0)
+            mod.weight.data.uniform_(0.5, 1.5)
+            mod.bias.data.uniform_(-0.2, 0.2)
+    x = torch.rand(1, 3, 64, 64)
+    with torch.no_grad():
+        y0 = m(x)[0].clone()
+        m.fuse()
+        y1 = m(x)[0]
+    assert not any(isinstance(mod, torch.nn.BatchNorm2d) for mod in m.modules())
+    torch.testing.assert_close(y1, y0, rtol=1e-4, atol=1e-3)
