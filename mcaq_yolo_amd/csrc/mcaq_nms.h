@@ -32,7 +32,8 @@
 namespace mcaq {
 
 constexpr int NMS_THREADS = 1024;
-constexpr int NMS_LDS_KEYS = 16384;      // LDS key array (128 KiB); more candidates sort in global memory
+constexpr int NMS_LDS_KEYS = 8192;       // LDS key array (64 KiB); more candidates sort in global memory
+constexpr int NMS_LDS_KEPT = 1024;       // kept boxes cached in LDS (more: read from the workspace)
 constexpr int NMS_CHUNK = 256;
 
 struct NmsArgs {
@@ -100,7 +101,15 @@ __global__ __launch_bounds__(NMS_SCAN_THREADS) void mcaq_nms_scan_kernel(NmsArgs
   int bj = 0;
   if (ai < N) {
     best = P[(size_t)4 * N + ai];
-    for (int c = 1; c < a.nc; ++c) {
+    int c = 1;
+    for (; c + 8 <= a.nc; c += 8) {      // 8 class rows in flight, compared in class order
+      float v[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = P[(size_t)(4 + c + k) * N + ai];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) if (v[k] > best) { best = v[k]; bj = c + k; }
+    }
+    for (; c < a.nc; ++c) {
       const float v = P[(size_t)(4 + c) * N + ai];
       if (v > best) { best = v; bj = c; }
     }
@@ -128,6 +137,8 @@ __global__ __launch_bounds__(NMS_THREADS) void mcaq_nms_kernel(NmsArgs a) {
   __shared__ float carea[NMS_CHUNK], cscore[NMS_CHUNK], ccls[NMS_CHUNK];
   __shared__ int csup[NMS_CHUNK];
   __shared__ unsigned long long cmask[NMS_CHUNK][4];
+  __shared__ float4 kbox[NMS_LDS_KEPT];     // offset boxes kept so far (first NMS_LDS_KEPT)
+  __shared__ float karea[NMS_LDS_KEPT];
   __shared__ int s_K;
 
   const int b = blockIdx.x;
@@ -185,7 +196,9 @@ __global__ __launch_bounds__(NMS_THREADS) void mcaq_nms_kernel(NmsArgs a) {
         const float4 bj = cbox[t];
         const float aj = carea[t];
         bool s = false;
-        for (int k = g; k < K && !s; k += 4) {
+        const int KL = K < NMS_LDS_KEPT ? K : NMS_LDS_KEPT;
+        for (int k = g; k < KL && !s; k += 4) s = nms_iou_gt(kbox[k], karea[k], bj, aj, a.iou);
+        for (int k = KL + g; k < K && !s; k += 4) {
           const float4 bk = *reinterpret_cast<const float4*>(kept + (size_t)k * 8);
           const float ak = kept[(size_t)k * 8 + 4];
           s = nms_iou_gt(bk, ak, bj, aj, a.iou);
@@ -216,8 +229,13 @@ __global__ __launch_bounds__(NMS_THREADS) void mcaq_nms_kernel(NmsArgs a) {
         const unsigned long long wsel = (r < 64) ? rm0 : (r < 128) ? rm1 : (r < 192) ? rm2 : rm3;
         if (csup[r] || ((wsel >> (r & 63)) & 1ull)) continue;
         const float4 o = cbox[r];
-        float* kp = kept + (size_t)Kc * 8;
-        kp[0] = o.x; kp[1] = o.y; kp[2] = o.z; kp[3] = o.w; kp[4] = carea[r];
+        if (Kc < NMS_LDS_KEPT) {
+          kbox[Kc] = o;
+          karea[Kc] = carea[r];
+        } else {
+          float* kp = kept + (size_t)Kc * 8;
+          kp[0] = o.x; kp[1] = o.y; kp[2] = o.z; kp[3] = o.w; kp[4] = carea[r];
+        }
         const float4 rr = craw[r];
         float* op = out + (size_t)Kc * 6;
         op[0] = rr.x; op[1] = rr.y; op[2] = rr.z; op[3] = rr.w; op[4] = cscore[r]; op[5] = ccls[r];
