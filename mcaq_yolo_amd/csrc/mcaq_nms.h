@@ -139,6 +139,7 @@ __global__ __launch_bounds__(NMS_THREADS) void mcaq_nms_kernel(NmsArgs a) {
   __shared__ unsigned long long cmask[NMS_CHUNK][4];
   __shared__ float4 kbox[NMS_LDS_KEPT];     // offset boxes kept so far (first NMS_LDS_KEPT)
   __shared__ float karea[NMS_LDS_KEPT];
+  __shared__ unsigned long long alive0[4];
   __shared__ int s_K;
 
   const int b = blockIdx.x;
@@ -206,41 +207,60 @@ __global__ __launch_bounds__(NMS_THREADS) void mcaq_nms_kernel(NmsArgs a) {
         if (s) csup[t] = 1;
       }
     }
-    // chunk-local matrix: row r, word w covers columns 64w..64w+63 (> r)
+    __syncthreads();
+    // the chunk's survivors of the kept boxes as bit words (wave 0, one ballot per word)
+    if (tid < 64) {
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        const int t = w * 64 + tid;
+        const unsigned long long m = __ballot(t < cn && !csup[t]);
+        if (tid == 0) alive0[w] = m;
+      }
+    }
+    // chunk-local matrix: row r, word w covers columns 64w..64w+63 (> r);
+    // rows and columns already suppressed by a kept box are never consulted
     {
       const int r = tid >> 2, w = tid & 3;
       unsigned long long bits = 0;
-      if (r < cn) {
+      if (r < cn && !csup[r]) {
         const float4 br = cbox[r];
         const float ar = carea[r];
         const int c0 = w * 64;
         for (int q = 0; q < 64; ++q) {
           const int c = c0 + q;
-          if (c > r && c < cn && nms_iou_gt(br, ar, cbox[c], carea[c], a.iou)) bits |= 1ull << q;
+          if (c > r && c < cn && !csup[c] && nms_iou_gt(br, ar, cbox[c], carea[c], a.iou)) bits |= 1ull << q;
         }
       }
       cmask[r][w] = bits;
     }
     __syncthreads();
     if (tid == 0) {
-      unsigned long long rm0 = 0, rm1 = 0, rm2 = 0, rm3 = 0;
+      // greedy in candidate order, visiting only live candidates: alive =
+      // not suppressed by a kept box nor by an earlier kept one of the chunk
+      unsigned long long rm[4] = {0ull, 0ull, 0ull, 0ull};
       int Kc = K;
-      for (int r = 0; r < cn && Kc < a.max_det; ++r) {
-        const unsigned long long wsel = (r < 64) ? rm0 : (r < 128) ? rm1 : (r < 192) ? rm2 : rm3;
-        if (csup[r] || ((wsel >> (r & 63)) & 1ull)) continue;
-        const float4 o = cbox[r];
-        if (Kc < NMS_LDS_KEPT) {
-          kbox[Kc] = o;
-          karea[Kc] = carea[r];
-        } else {
-          float* kp = kept + (size_t)Kc * 8;
-          kp[0] = o.x; kp[1] = o.y; kp[2] = o.z; kp[3] = o.w; kp[4] = carea[r];
+#pragma unroll
+      for (int w = 0; w < 4; ++w) {
+        unsigned long long live = alive0[w] & ~rm[w];
+        while (live && Kc < a.max_det) {
+          const int q = __ffsll((long long)live) - 1;
+          const int r = w * 64 + q;
+          const float4 o = cbox[r];
+          if (Kc < NMS_LDS_KEPT) {
+            kbox[Kc] = o;
+            karea[Kc] = carea[r];
+          } else {
+            float* kp = kept + (size_t)Kc * 8;
+            kp[0] = o.x; kp[1] = o.y; kp[2] = o.z; kp[3] = o.w; kp[4] = carea[r];
+          }
+          const float4 rr = craw[r];
+          float* op = out + (size_t)Kc * 6;
+          op[0] = rr.x; op[1] = rr.y; op[2] = rr.z; op[3] = rr.w; op[4] = cscore[r]; op[5] = ccls[r];
+          ++Kc;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) rm[j] |= cmask[r][j];
+          live = alive0[w] & ~rm[w] & ~((2ull << q) - 1ull);   // bits above q (q = 63: none)
         }
-        const float4 rr = craw[r];
-        float* op = out + (size_t)Kc * 6;
-        op[0] = rr.x; op[1] = rr.y; op[2] = rr.z; op[3] = rr.w; op[4] = cscore[r]; op[5] = ccls[r];
-        ++Kc;
-        rm0 |= cmask[r][0]; rm1 |= cmask[r][1]; rm2 |= cmask[r][2]; rm3 |= cmask[r][3];
       }
       s_K = Kc;
     }
