@@ -549,7 +549,7 @@ class SplitRunner:
             torch.cuda.current_stream().wait_stream(st)
 
 
-def kernel_timing(plan, reps=20):
+def kernel_timing(plan, reps=40):
     """Per-launch device time of each kernel of a step, in sequence: `reps`
     single-batch steps on one stream.  Pass 1 and pass 2 are launched through
     hipExtLaunchKernel with start/stop events (mcaq_time_next_launch: the
@@ -573,7 +573,9 @@ def kernel_timing(plan, reps=20):
         plan.launch_quant(st)
     torch.cuda.synchronize()
     pairs = ((0, 1), (2, 3), (4, 5))
-    return {k: sum(e[a].elapsed_time(e[b]) for e in ev) * 1e3 / reps for k, (a, b) in zip(names, pairs)}
+    # median over the launches (a kernel trace's per-dispatch durations have a
+    # long upper tail: profiles/r02_v6 p1 trace, quant mean 36.5 / median 36.1 us)
+    return {k: sorted(e[a].elapsed_time(e[b]) for e in ev)[reps // 2] * 1e3 for k, (a, b) in zip(names, pairs)}
 
 
 def main():
@@ -706,8 +708,8 @@ def main():
     out = None
     if rank == 0:
         q_gbs = 8 * elems / (quant_us * 1e-6) / 1e9
-        seq = "hipExtLaunchKernel start/stop events of each launch, 20 single-batch steps in sequence on one stream " \
-              "(the --pipeline 1 context of profiles/*_kernel_stats_pipeline1.csv)"
+        seq = "hipExtLaunchKernel start/stop events of each launch, median of 40 single-batch steps in sequence on " \
+              "one stream (the --pipeline 1 context of profiles/*_kernel_stats_pipeline1.csv)"
         kern = {"quant": {"us": round(quant_us, 2), "alg_bytes": 8 * elems, "GB/s": round(q_gbs, 1),
                           "frac": round(q_gbs / HBM_PEAK_GBS, 4), "timing": seq}}
         gbs = 4 * elems / (kt["stats"] * 1e-6) / 1e9
