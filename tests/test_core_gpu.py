@@ -327,3 +327,30 @@ def test_per_tensor_hook_vs_reference(name, mapping):
     key = "mlp" if mapping == "mlp" else "lin"
     assert np.array_equal(aux[0]["bit_map"].cpu().numpy(), d["bits_" + key])
     assert np.array_equal(outs[0].cpu().numpy(), d["y_" + key])
+
+
+def test_per_tensor_calibrated_frozen_hook_equals_cpu_path():
+    """per_channel=False with calibration then freeze_calibration: the fused
+    hook reads the scalar running statistics (min_stride 0) and gives the same
+    bits and y as the pure-PyTorch CPU path with the same state."""
+    import os
+    from conftest import GOLDEN
+    from test_fallback_cpu import hooks_per_tensor
+    d = np.load(os.path.join(GOLDEN, "pt_p5.npz"))
+    x = torch.from_numpy(d["x"].astype(f32))
+    res = {}
+    for dev in ("cpu", DEV):
+        h = hooks_per_tensor(dev, int(d["grid"]), "mlp")
+        q = h.quantizers["4"]
+        with torch.no_grad():
+            for k in range(3):      # calibration passes (EMA of the batch min/max)
+                h.begin(calibrating=True)
+                h.run_scale(4, (x * (1.0 + 0.1 * k)).to(dev), h._mcaq_state)
+                h.end()
+            q.freeze_calibration()
+            assert q.running_min.numel() == 1
+            outs, aux = h.forward_features([x.to(dev)])
+        res[dev] = (outs[0].cpu().numpy(), aux[0]["bit_map"].cpu().numpy(), float(q.running_min), float(q.running_max))
+    assert res["cpu"][2:] == res[DEV][2:]
+    assert np.array_equal(res["cpu"][1], res[DEV][1])
+    assert np.array_equal(res["cpu"][0], res[DEV][0])
