@@ -212,10 +212,10 @@ def main_qat(args, world, rank, dev, pg):
     # two-kernel form (no counters) is timed beside it for comparison.
     kt = {}
     reps = 20
-    for k, fn, skip in (("qat_forward", lambda: L.mcaq_qat_forward(arr, 3, sh), 0),
-                        ("qat_backward", lambda: L.mcaq_qat_backward(arr, 3, sh), 0),
-                        ("qat_backward_kernel_unfused", lambda: L.mcaq_qat_backward(arr_u, 3, sh), 0),
-                        ("qat_fold_unfused", lambda: L.mcaq_qat_backward(arr_u, 3, sh), 1)):
+    for k, fn, skip in (("qat_forward", lambda: L.mcaq_qat_forward(arr_u, 3, sh), 0),
+                        ("qat_backward_kernel", lambda: L.mcaq_qat_backward(arr_u, 3, sh), 0),
+                        ("qat_fold", lambda: L.mcaq_qat_backward(arr_u, 3, sh), 1),
+                        ("qat_backward_fold_in_launch", lambda: L.mcaq_qat_backward(arr, 3, sh), 0)):
         abi.check(fn(), k)
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
         for a_, b_ in ev:
@@ -227,7 +227,7 @@ def main_qat(args, world, rank, dev, pg):
             fn()
         torch.cuda.synchronize()
         kt[k] = sum(a_.elapsed_time(b_) for a_, b_ in ev) * 1e3 / reps
-    kt["qat_backward_unfused"] = kt["qat_backward_kernel_unfused"] + kt["qat_fold_unfused"]
+    kt["qat_backward"] = kt["qat_backward_kernel"] + kt["qat_fold"]    # the product's two-kernel form
 
     if pg is not None:
         import torch.distributed as dist
@@ -250,9 +250,9 @@ def main_qat(args, world, rank, dev, pg):
         # fold: reads the 2 x ceil(C/32) partial planes (the work buffer), writes grad_m + grad_bits
         pix = sum(B * hh * ww for (hh, ww) in SIZES)
         fold_b = sum(4 * 2 * ((c + 31) // 32) * B * hh * ww for c, (hh, ww) in zip(chans, SIZES)) + 4 * pix
-        for k, nb in (("qat_forward", 8 * elems + 4 * pix), ("qat_backward", 12 * elems + 4 * pix),
-                      ("qat_backward_kernel_unfused", 12 * elems + 4 * pix), ("qat_fold_unfused", fold_b),
-                      ("qat_backward_unfused", 12 * elems + 4 * pix)):
+        for k, nb in (("qat_forward", 8 * elems + 4 * pix), ("qat_backward_kernel", 12 * elems + 4 * pix),
+                      ("qat_fold", fold_b), ("qat_backward", 12 * elems + 4 * pix),
+                      ("qat_backward_fold_in_launch", 12 * elems + 4 * pix)):
             gbs_ = nb / (kt[k] * 1e-6) / 1e9
             kern[k] = {"us": round(kt[k], 2), "alg_bytes": nb, "GB/s": round(gbs_, 1),
                        "frac": round(gbs_ / HBM_PEAK_GBS, 4)}
@@ -267,12 +267,12 @@ def main_qat(args, world, rank, dev, pg):
                                    "continuous bits, STE, stage-3 temperature 1); YOLOv8 network excluded"
                                    % (name, B, grid, mapper),
                        "global_batch": world * B, "parallelism": "dp%d" % world, "hip_graph": use_graph},
-            "roofline": {"bound": "hbm", "achieved": kern["qat_backward"]["GB/s"], "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": kern["qat_backward"]["frac"], "traffic": None,
-                         "kernel": "mcaq_qat_kernel<bwd> with the grad_m / grad_bits fold inside the launch "
-                                   "(read g, x + write grad_x: 12 B per element, + 4 B per pixel of mask)",
-                         "alg_bytes_per_launch": kern["qat_backward"]["alg_bytes"],
-                         "us_per_launch": kern["qat_backward"]["us"]},
+            "roofline": {"bound": "hbm", "achieved": kern["qat_backward_kernel"]["GB/s"], "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": kern["qat_backward_kernel"]["frac"], "traffic": None,
+                         "kernel": "mcaq_qat_kernel<bwd> (read g, x + write grad_x: 12 B per element, + 4 B per "
+                                   "pixel of mask); its fold kernel is kernels.qat_fold",
+                         "alg_bytes_per_launch": kern["qat_backward_kernel"]["alg_bytes"],
+                         "us_per_launch": kern["qat_backward_kernel"]["us"]},
             "step_roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                               "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                               "kernel": "whole QAT step, 24 B per feature element (fwd 12 + bwd 12)",
