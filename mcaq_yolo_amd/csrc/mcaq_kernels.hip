@@ -185,7 +185,11 @@ __device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, fl
   const int C = S.C;
   const float* xb = S.x + (size_t)b * C * HW;
   const bool cropped = (S.Hc != S.H) || (S.Wc != S.W);
+#ifdef MCAQ_PROBE_STATS_NO_MINMAX   // timing probe only (no min/max partials)
+  const bool want_g = S.gray != nullptr, want_a = S.absmean != nullptr, want_m = false;
+#else
   const bool want_g = S.gray != nullptr, want_a = S.absmean != nullptr, want_m = S.pmin != nullptr;
+#endif
   const int base = chunk * UPIX;
   const int q0 = base + lane * PPL;                    // first pixel of this lane
   bool pv[PPL];
@@ -291,7 +295,11 @@ __device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, fl
   const int ntail = tend - tstart;
   const int nilp = C >> 2;                        // rows per interleaved cascade
   const int nbt = (nilp + 15) >> 4;               // 16-row blocks per cascade
+#ifdef MCAQ_PROBE_STATS_NO_TAIL   // timing probe only (wrong tail sums): tools/probe/stats_probe.sh
+  const bool need_tail = false;
+#else
   const bool need_tail = ntail > 0 && (want_a || (want_g && !cropped));
+#endif
   const bool coop = nbt <= 16;                    // 31 px x 4 x 16 x 2 floats fit the LDS
   float tg = 0.0f, ta = 0.0f;
   if (need_tail && coop) {
