@@ -257,14 +257,19 @@ __device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, fl
 #pragma unroll
         for (int k = 0; k < PPL; ++k) { bsg[wv][lane * PPL + k] = gb[k]; bsa[wv][lane * PPL + k] = ab[k]; }
         if (want_m) {
+          // no valid-pixel masking: PPL divides HW, so a lane's pixels are all
+          // in the image or the lane loaded pixels 0.. of the same channel row
+          // (qa = 0 / clamped index) - genuine values, which cannot move a min
+          // or max over the batch (r02 probe: the masks were ~1/3 of pass 1's
+          // min/max VALU work, tools/probe/stats_probe.sh)
           float mn[ST_CG], mx[ST_CG];
 #pragma unroll
           for (int i = 0; i < ST_CG; ++i) {
-            float lo = 3.402823466e38f, hi = -3.402823466e38f;
+            float lo = v[rr][i][0], hi = v[rr][i][0];
 #pragma unroll
-            for (int k = 0; k < PPL; ++k) {
-              lo = fminf(lo, pv[k] ? v[rr][i][k] : 3.402823466e38f);
-              hi = fmaxf(hi, pv[k] ? v[rr][i][k] : -3.402823466e38f);
+            for (int k = 1; k < PPL; ++k) {
+              lo = fminf(lo, v[rr][i][k]);
+              hi = fmaxf(hi, v[rr][i][k]);
             }
             mn[i] = lo; mx[i] = hi;
           }
