@@ -583,7 +583,7 @@ constexpr int QMAXNT = 1024;   // max tiles per image whose m values are staged 
 // QuantizationParameters computes them).
 template <bool kVec, bool kNTL, bool kNTS, bool kMtLds>
 __global__ __launch_bounds__(256) void mcaq_quant_kernel(QuantArgs a) {
-  __shared__ float2 qt[QSLICE * QMAXBITS];
+  __shared__ float4 qt[QSLICE * QMAXBITS];   // scale, zp, 1/scale
   __shared__ float mts[QMAXNT];
   __shared__ float mq[256];
   const int unit = blockIdx.x;
@@ -604,7 +604,7 @@ __global__ __launch_bounds__(256) void mcaq_quant_kernel(QuantArgs a) {
   for (int i = tid; i < nc * NB; i += 256) {
     const int c = i / NB, k = i - (i / NB) * NB;
     const QParam q = qparam(S.xmin[c0 + c], S.xmax[c0 + c], S.bits_lo + k);
-    qt[i] = make_float2(q.scale, q.zp);
+    qt[i] = make_float4(q.scale, q.zp, q.rs, 0.0f);
   }
   const int NTq = S.ht * S.wt;
   if (kMtLds && S.mt)
@@ -695,9 +695,9 @@ __global__ __launch_bounds__(256) void mcaq_quant_kernel(QuantArgs a) {
     float o[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const float2 sz = qt[(cw + c) * NB + kb[k]];
+      const float4 sz = qt[(cw + c) * NB + kb[k]];
       QParam q;
-      q.scale = sz.x; q.zp = sz.y; q.qmin = qlo[k]; q.qmax = qhi[k];
+      q.scale = sz.x; q.zp = sz.y; q.rs = sz.z; q.qmin = qlo[k]; q.qmax = qhi[k];
       float d = quant_dequant(v[c][k], q);
       if (has_m) d = d * mv[k];
       o[k] = d;

@@ -144,7 +144,7 @@ constexpr int QAT_FUSED_MAXW = 512;
 // workgroups walking all 32 channels of a slice (every unit resident at once).
 template <bool kBwd, bool kVec>
 __global__ __launch_bounds__(256, MCAQ_QAT_MINW) void mcaq_qat_kernel(QatArgs a) {
-  __shared__ float2 qt[32 * QAT_NB];
+  __shared__ float4 qt[32 * QAT_NB];   // scale, zp, 1/scale
   __shared__ float red[2][4][256];
   __shared__ int s_last;   // bands completed by this unit (bit per band)
   const int unit = blockIdx.x;
@@ -164,7 +164,7 @@ __global__ __launch_bounds__(256, MCAQ_QAT_MINW) void mcaq_qat_kernel(QatArgs a)
   for (int i = tid; i < nc * QAT_NB; i += 256) {
     const int c = i / QAT_NB, k = i - c * QAT_NB;
     const QParam q = qparam(S.xmin[c0 + c], S.xmax[c0 + c], QAT_LO + k);
-    qt[i] = make_float2(q.scale, q.zp);
+    qt[i] = make_float4(q.scale, q.zp, q.rs, 0.0f);
   }
   const int q0 = chunk * 256 + lane * 4;
   bool pv[4];
@@ -215,13 +215,13 @@ __global__ __launch_bounds__(256, MCAQ_QAT_MINW) void mcaq_qat_kernel(QatArgs a)
     float o[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      const float2 zl = qt[(cw + c) * QAT_NB + kl[k]];
-      const float2 zh = qt[(cw + c) * QAT_NB + kh[k]];
+      const float4 zl = qt[(cw + c) * QAT_NB + kl[k]];
+      const float4 zh = qt[(cw + c) * QAT_NB + kh[k]];
       const int lo = kl[k] + QAT_LO, hi = kh[k] + QAT_LO;
       QParam L, Hq;
-      L.scale = zl.x; L.zp = zl.y;
+      L.scale = zl.x; L.zp = zl.y; L.rs = zl.z;
       L.qmin = (float)(-(1 << (lo - 1))); L.qmax = (float)((1 << (lo - 1)) - 1);
-      Hq.scale = zh.x; Hq.zp = zh.y;
+      Hq.scale = zh.x; Hq.zp = zh.y; Hq.rs = zh.z;
       Hq.qmin = (float)(-(1 << (hi - 1))); Hq.qmax = (float)((1 << (hi - 1)) - 1);
       const float ql = quant_dequant(v[k], L);
       const float qh = quant_dequant(v[k], Hq);

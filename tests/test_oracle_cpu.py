@@ -229,3 +229,24 @@ def test_sleef_expf_restatement():
     ulp = np.abs(e.view(np.int32).astype(np.int64) - c.view(np.int32).astype(np.int64))
     assert ulp.max() <= 1 and 0.01 < (ulp == 1).mean() < 0.3
     assert sleef_expf32(np.float32(0.0)) == 1.0 and sleef_expf32(np.float32(-105.0)) == 0.0
+
+
+def test_reciprocal_division_is_correctly_rounded():
+    """The kernels' x / s (mcaq_math.h div_by): q0 = RN(x * RN(1/s)),
+    r = x - q0 s exactly (FMA), RN(q0 + r RN(1/s)) equals IEEE x / s on
+    qparam-shaped scales and on divisors with adversarial mantissas."""
+    from oracle.ieee import fma32
+    f32 = np.float32
+    rng = np.random.default_rng(3)
+    n = 400000
+    rngv = np.exp(rng.uniform(np.log(1e-8), np.log(50.0), n)).astype(f32)
+    s = (rngv / (2.0 ** rng.integers(1, 16, n) - 1).astype(f32)).astype(f32)
+    x = (rng.standard_normal(n) * np.exp(rng.uniform(-8, 5, n))).astype(f32)
+    mant = np.array([0x7fffff, 0x7ffffe, 0x000001, 0x400000, 0x555555], np.uint32)
+    adv = ((np.arange(110, 135, dtype=np.uint32)[:, None] << 23) | mant[None, :]).ravel().view(f32)
+    s = np.concatenate([s, np.repeat(adv, 2000)])
+    x = np.concatenate([x, rng.uniform(-1000, 1000, adv.size * 2000).astype(f32)])
+    y = (f32(1.0) / s).astype(f32)
+    q0 = (x * y).astype(f32)
+    q1 = fma32(fma32(-q0, s, x), y, q0)
+    assert np.array_equal(q1, (x / s).astype(f32))
