@@ -215,10 +215,20 @@ MCAQ_HD float div_by(float x, float s, float rs) {
 #endif
 }
 
+// clamp of a finite value into [lo, hi] (lo <= hi): one v_med3_f32 on the
+// device instead of two compare + select pairs
+MCAQ_HD float clamp_med3(float x, float lo, float hi) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_fmed3f(x, lo, hi);
+#else
+  return clampf_(x, lo, hi);
+#endif
+}
+
 // y = (clamp(rint(x/s + zp)) - zp) * s     (quantization.py:597-600)
 MCAQ_HD float quant_dequant(float x, const QParam& q) {
   float t = div_by(x, q.scale, q.rs) + q.zp;
-  float r = clampf_(rintf(t), q.qmin, q.qmax);
+  float r = clamp_med3(rintf(t), q.qmin, q.qmax);
   return (r - q.zp) * q.scale;
 }
 
