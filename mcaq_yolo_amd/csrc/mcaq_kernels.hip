@@ -613,6 +613,7 @@ __global__ __launch_bounds__(256) void mcaq_quant_kernel(QuantArgs a) {
   const float* mtab = kMtLds ? mts : (S.mt ? S.mt + (size_t)b * NTq : nullptr);
 
   const int q0 = chunk * 256 + lane * 4;
+  const NearestMap nmh = nearest_map(S.ht, S.H), nmw = nearest_map(S.wt, S.W);
   bool pv[4];
   int kb[4];
   float mv[4];
@@ -626,8 +627,8 @@ __global__ __launch_bounds__(256) void mcaq_quant_kernel(QuantArgs a) {
       th = imin_(h / S.compat_tile_h, S.ht - 1);
       tw = imin_(w / S.compat_tile_w, S.wt - 1);
     } else {                     // PyTorch path: nearest upsample of the bit map
-      th = nearest_src(h, S.ht, S.H);
-      tw = nearest_src(w, S.wt, S.W);
+      th = nearest_apply(nmh, h);
+      tw = nearest_apply(nmw, w);
     }
     const float bv = S.bits[((size_t)b * S.ht + th) * S.wt + tw];
     kb[k] = imin_(imax_((int)rintf(bv), S.bits_lo), S.bits_lo + NB - 1) - S.bits_lo;
@@ -674,11 +675,11 @@ __global__ __launch_bounds__(256) void mcaq_quant_kernel(QuantArgs a) {
       const int h = p / S.W, w = p - (p / S.W) * S.W;
       int cs[5];
 #pragma unroll
-      for (int j = 0; j < 5; ++j) cs[j] = nearest_src(imin_(imax_(w + j - 2, 0), S.W - 1), S.wt, S.W);
+      for (int j = 0; j < 5; ++j) cs[j] = nearest_apply(nmw, imin_(imax_(w + j - 2, 0), S.W - 1));
       float acc = 0.0f;
 #pragma unroll
       for (int i = 0; i < 5; ++i) {
-        const int rb = nearest_src(imin_(imax_(h + i - 2, 0), S.H - 1), S.ht, S.H) * S.wt;
+        const int rb = nearest_apply(nmh, imin_(imax_(h + i - 2, 0), S.H - 1)) * S.wt;
 #pragma unroll
         for (int j = 0; j < 5; ++j) acc = fmaf(bits_as_float(k_smooth5_bits[i * 5 + j]), mtab[rb + cs[j]], acc);
       }

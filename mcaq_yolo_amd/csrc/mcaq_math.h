@@ -181,6 +181,22 @@ MCAQ_HD int nearest_src(int o, int in_size, int out_size) {
   return s < in_size - 1 ? s : in_size - 1;
 }
 
+// nearest_src with the ratio resolved once (per workgroup): when out = in *
+// 2^k (a whole number of power-of-two tiles, the usual hook case) the source
+// index is o >> k exactly (in/out = 2^-k is exact in fp32), else nearest_src.
+struct NearestMap { int in, out, shift; };
+MCAQ_HD NearestMap nearest_map(int in_size, int out_size) {
+  NearestMap m{in_size, out_size, -1};
+  if (in_size > 0 && out_size % in_size == 0) {
+    const int r = out_size / in_size;
+    if ((r & (r - 1)) == 0) { int k = 0; while ((1 << k) < r) ++k; m.shift = k; }
+  }
+  return m;
+}
+MCAQ_HD int nearest_apply(const NearestMap& m, int o) {
+  return m.shift >= 0 ? (o >> m.shift) : nearest_src(o, m.in, m.out);
+}
+
 // Quantization parameters (quantization.py:26-66) for integer bits b.
 struct QParam { float scale, zp, qmin, qmax, rs; };   // rs = RN(1 / scale)
 MCAQ_HD QParam qparam(float xmin, float xmax, int b) {

@@ -167,6 +167,7 @@ __global__ __launch_bounds__(256, MCAQ_QAT_MINW) void mcaq_qat_kernel(QatArgs a)
     qt[i] = make_float4(q.scale, q.zp, q.rs, 0.0f);
   }
   const int q0 = chunk * 256 + lane * 4;
+  const NearestMap nmh = nearest_map(S.ht, S.H), nmw = nearest_map(S.wt, S.W);
   bool pv[4];
   int kl[4], kh[4];
   float fu[4], omf[4], mv[4];
@@ -175,7 +176,7 @@ __global__ __launch_bounds__(256, MCAQ_QAT_MINW) void mcaq_qat_kernel(QatArgs a)
     const int p = imin_(q0 + k, HW - 1);
     pv[k] = q0 + k < HW;
     const int h = p / S.W, w = p - (p / S.W) * S.W;
-    const float bv = S.bits[((size_t)b * S.ht + nearest_src(h, S.ht, S.H)) * S.wt + nearest_src(w, S.wt, S.W)];
+    const float bv = S.bits[((size_t)b * S.ht + nearest_apply(nmh, h)) * S.wt + nearest_apply(nmw, w)];
     const float fl = floorf(bv);
     fu[k] = bv - fl;                 // exact (Sterbenz) for b >= 1
     omf[k] = 1.0f - fu[k];
