@@ -558,7 +558,7 @@ __global__ __launch_bounds__(TILES_THREADS, MCAQ_TILES_MINW) void mcaq_tiles_ker
   Ctx ctx{(int)threadIdx.x - g * G, G};
   Shared sh;
   carve_shared(base, sh);
-  morph_tiles(ctx, S, b, sh, wl, (int)threadIdx.x, TILES_THREADS, xs, a.tpairs != 0);
+  morph_tiles(ctx, S, b, sh, wl, (int)threadIdx.x, TILES_THREADS, xs);
 }
 
 // ---------------------------------------------------------------------------
@@ -978,24 +978,6 @@ int mcaq_morph_finalize(const mcaq_morph_scale* scales, int nscales, const mcaq_
     }
     a.twg_begin[nscales] = twg;
     const int lim = MCAQ_MORPH_LDS_LIMIT - 1024;
-    // the bilateral pair-exp table where every scale's image groups have room for it
-    {
-      int perp = 0;
-      for (int i = 0; i < nscales; ++i) {
-        const MorphScale& S = a.s[i];
-        if (!(S.flags & (F_PHI | F_CMLP | F_MAPPER | F_SOFTMASK))) continue;
-        const int NT = S.ht * S.wt;
-        perp = imax_(perp, a.tipw[i] * ((tiles_lds_bytes(S.H, S.W, NT) + tiles_pair_bytes(NT) + 15) & ~15));
-      }
-      a.tpairs = perp + TILES_SCRATCH_BYTES <= lim ? 1 : 0;
-      if (a.tpairs) {
-        per = perp;
-        for (int i = 0; i < nscales; ++i)
-          if (a.s[i].flags & (F_PHI | F_CMLP | F_MAPPER | F_SOFTMASK))
-            a.tgstride[i] = (tiles_lds_bytes(a.s[i].H, a.s[i].W, a.s[i].ht * a.s[i].wt) +
-                             tiles_pair_bytes(a.s[i].ht * a.s[i].wt) + 15) & ~15;
-      }
-    }
     if (per + TILES_SCRATCH_BYTES > lim) return (int)hipErrorInvalidValue;
     // stage the weight blobs in LDS when they fit beside the tile arrays and the MLP scratch
     const int wlds = per + TILES_SCRATCH_BYTES + weights_lds_bytes() <= lim;

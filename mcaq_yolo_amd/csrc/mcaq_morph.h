@@ -69,10 +69,8 @@ struct MorphArgs {
   // image group (planes + shared, or shared only), plane bytes per image, and
   // the first workgroup of each scale (wg_begin[nscales] = pass A workgroups)
   int ipw[3], gstride[3], pstride[3], wg_begin[4];
-  // pass B packing: images per workgroup, LDS bytes per image, first
-  // workgroup; whether the bilateral pair-exp table fits (tiles_pair_bytes)
+  // pass B packing: images per workgroup, LDS bytes per image, first workgroup
   int tipw[3], tgstride[3], twg_begin[4];
-  int tpairs;
 };
 
 // bit planes
@@ -1416,17 +1414,15 @@ MCAQ_HD void stage_tiles(const Ctx& ctx, const MorphScale& S, int b, float* tile
 // images share a workgroup): phi assembly, complexity MLP, bilateral,
 // normalisation, bit mapper, soft mask (tile values; the m plane itself only
 // on request).  LDS per image: Shared (fixed + tiles) | extra | bilateral
-// weights (25 NT floats) [| bilateral pair exps (12 NT floats), `pairs`]; the
-// staged weight blobs `wl` (or null) belong to the workgroup.
+// weights (25 NT floats) | bilateral range exps (12 NT floats); the staged
+// weight blobs `wl` (or null) belong to the workgroup.
 MCAQ_HD int tiles_lds_bytes(int H, int W, int NT) {
-  return fixed_bytes() + tile_bytes(NT) + extra_bytes(H, W, NT) + 100 * NT;
+  return fixed_bytes() + tile_bytes(NT) + extra_bytes(H, W, NT) + 100 * NT + 48 * NT;
 }
-// + the bilateral pair-exp table (12 NT floats) when the launch has room for it
-MCAQ_HD int tiles_pair_bytes(int NT) { return 48 * NT; }
 
 // xs: the workgroup's MLP activation scratch (MLP_SCRATCH_FLOATS per wave), device only
 MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh, float* wl, int wtid, int wnthr,
-                         float* xs, bool pairs) {
+                         float* xs) {
   const int ht = S.ht, wt = S.wt, NT = ht * wt;
   const float inv_wt = 1.0f / (float)wt;
   float* tiles = sh.tiles;
@@ -1499,18 +1495,7 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
     // most 2 apart - 12 "forward" offsets (0,1) (0,2) (1,-2..2) (2,-2..2) per
     // tile, up to BK per thread in flight - and the 25 taps (replicate-
     // clamped neighbours) gather them: ~12 exps per tile instead of 25.
-    if (!pairs) {   // no LDS for the pair table (very large tile grids): 25 exps per tile
-      auto wgt = [&](int u) {
-        const int t = u / 25, k = u - (u / 25) * 25;
-        const int th = div_small(t, wt, inv_wt), tw = t - th * wt;
-        const int hh = imin_(imax_(th + k / 5 - 2, 0), ht - 1);
-        const int ww = imin_(imax_(tw + k % 5 - 2, 0), wt - 1);
-        const float d = extra[hh * wt + ww] - extra[t];
-        return bits_as_float(k_bilat_sp_bits[k]) * cr_exp((-(d * d)) / 0.02f);
-      };
-      bcopy<12>(ctx, NT * 25, wgt, [&](int u, float v) { wbuf[u] = v; });
-      MSYNC();
-    } else {
+    {
       constexpr int BK = 12;
       float* ebuf = wbuf + 25 * NT;
       auto fexp = [&](int u) {

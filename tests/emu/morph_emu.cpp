@@ -12,7 +12,7 @@ extern "C" int emu_morph(const mcaq_morph_scale* s) {
   using namespace mcaq;
   const int NT = s->ht * s->wt;
   std::vector<char> planes(plane_bytes(s->Hc, s->Wc) + 64), shm(fixed_bytes() + tile_bytes(NT) + 64);
-  std::vector<char> tshm(tiles_lds_bytes(s->H, s->W, NT) + tiles_pair_bytes(NT) + 64);
+  std::vector<char> tshm(tiles_lds_bytes(s->H, s->W, NT) + 64);
   for (int b = 0; b < s->B; ++b) {
     Ctx ctx{0, 1};
     if (s->flags & F_PHI) {
@@ -26,7 +26,7 @@ extern "C" int emu_morph(const mcaq_morph_scale* s) {
     }
     Shared sh2;
     carve_shared(tshm.data(), sh2);
-    morph_tiles(ctx, *s, b, sh2, nullptr, 0, 1, nullptr, (b & 1) == 0);   // both bilateral forms
+    morph_tiles(ctx, *s, b, sh2, nullptr, 0, 1, nullptr);
   }
   return 0;
 }
