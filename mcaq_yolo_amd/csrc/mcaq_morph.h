@@ -1414,10 +1414,10 @@ MCAQ_HD void stage_tiles(const Ctx& ctx, const MorphScale& S, int b, float* tile
 // images share a workgroup): phi assembly, complexity MLP, bilateral,
 // normalisation, bit mapper, soft mask (tile values; the m plane itself only
 // on request).  LDS per image: Shared (fixed + tiles) | extra | bilateral
-// weights (25 NT floats) | bilateral range exps (12 NT floats); the staged
-// weight blobs `wl` (or null) belong to the workgroup.
+// weights (25 NT floats); the staged weight blobs `wl` (or null) belong to the
+// workgroup.
 MCAQ_HD int tiles_lds_bytes(int H, int W, int NT) {
-  return fixed_bytes() + tile_bytes(NT) + extra_bytes(H, W, NT) + 100 * NT + 48 * NT;
+  return fixed_bytes() + tile_bytes(NT) + extra_bytes(H, W, NT) + 100 * NT;
 }
 
 // xs: the workgroup's MLP activation scratch (MLP_SCRATCH_FLOATS per wave), device only
@@ -1489,43 +1489,19 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
     }
     MSYNC();
     MSTAMP(11);
-    // range weights w = spatial * exp(-(d^2)/0.02).  exp(-(d^2)/0.02) is the
-    // same for the pair (t, n) seen from either tile ((-d)^2 = d^2 exactly) and
-    // is 1 for n = t, so it is evaluated once per unordered pair of tiles at
-    // most 2 apart - 12 "forward" offsets (0,1) (0,2) (1,-2..2) (2,-2..2) per
-    // tile, up to BK per thread in flight - and the 25 taps (replicate-
-    // clamped neighbours) gather them: ~12 exps per tile instead of 25.
+    // range weights w = spatial * exp(-(d^2)/0.02), one thread per (tile, tap),
+    // up to BK items per thread with their exps in flight together
     {
       constexpr int BK = 12;
-      float* ebuf = wbuf + 25 * NT;
-      auto fexp = [&](int u) {
-        const int t = u / 12, o = u - (u / 12) * 12;
-        const int th = div_small(t, wt, inv_wt), tw = t - th * wt;
-        const int di = o < 2 ? 0 : (o < 7 ? 1 : 2);
-        const int dj = o < 2 ? o + 1 : (o < 7 ? o - 4 : o - 9);
-        const int nh = th + di, nw = tw + dj;
-        if (nh >= ht || nw < 0 || nw >= wt) return 0.0f;   // no such pair
-        const float d = extra[nh * wt + nw] - extra[t];
-        return cr_exp((-(d * d)) / 0.02f);
-      };
-      bcopy<BK>(ctx, NT * 12, fexp, [&](int u, float v) { ebuf[u] = v; });
-      MSYNC();
-      MFOR(u, NT * 25) {
+      auto wgt = [&](int u) {
         const int t = u / 25, k = u - (u / 25) * 25;
         const int th = div_small(t, wt, inv_wt), tw = t - th * wt;
         const int hh = imin_(imax_(th + k / 5 - 2, 0), ht - 1);
         const int ww = imin_(imax_(tw + k % 5 - 2, 0), wt - 1);
-        const int di = hh - th, dj = ww - tw;
-        float e = 1.0f;                                      // n = t: exp(-0) = 1
-        if (di != 0 || dj != 0) {
-          const bool fwd = di > 0 || (di == 0 && dj > 0);
-          const int a = fwd ? t : hh * wt + ww;
-          const int fi = fwd ? di : -di, fj = fwd ? dj : -dj;
-          const int o = fi == 0 ? fj - 1 : (fi == 1 ? fj + 4 : fj + 9);
-          e = ebuf[a * 12 + o];
-        }
-        wbuf[u] = bits_as_float(k_bilat_sp_bits[k]) * e;
-      }
+        const float d = extra[hh * wt + ww] - extra[t];
+        return bits_as_float(k_bilat_sp_bits[k]) * cr_exp((-(d * d)) / 0.02f);
+      };
+      bcopy<BK>(ctx, NT * 25, wgt, [&](int u, float v) { wbuf[u] = v; });
       MSYNC();
     }
     MSTAMP(29);
