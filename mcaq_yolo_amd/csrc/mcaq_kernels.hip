@@ -690,34 +690,18 @@ __global__ __launch_bounds__(256) void mcaq_quant_kernel(QuantArgs a) {
     for (int k = 0; k < 4; ++k) mv[k] = mq[lane * 4 + k];
   }
   if (ncw <= 0) return;
-  // a lane's 4 pixels lie in one tile whenever the tile grid is a whole number
-  // of >= 4-pixel tiles (the hook shapes): then one table entry per channel
-  // serves all 4 (a quarter of the LDS reads; wave-uniform test)
-  const bool quad1 = __all(kb[0] == kb[1] && kb[1] == kb[2] && kb[2] == kb[3]);
 #pragma unroll
   for (int c = 0; c < QCW; ++c) {
     if (c >= ncw) break;
     float o[4];
-    if (quad1) {
-      const float4 sz = qt[(cw + c) * NB + kb[0]];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float4 sz = qt[(cw + c) * NB + kb[k]];
       QParam q;
-      q.scale = sz.x; q.zp = sz.y; q.rs = sz.z; q.qmin = qlo[0]; q.qmax = qhi[0];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float d = quant_dequant(v[c][k], q);
-        if (has_m) d = d * mv[k];
-        o[k] = d;
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const float4 sz = qt[(cw + c) * NB + kb[k]];
-        QParam q;
-        q.scale = sz.x; q.zp = sz.y; q.rs = sz.z; q.qmin = qlo[k]; q.qmax = qhi[k];
-        float d = quant_dequant(v[c][k], q);
-        if (has_m) d = d * mv[k];
-        o[k] = d;
-      }
+      q.scale = sz.x; q.zp = sz.y; q.rs = sz.z; q.qmin = qlo[k]; q.qmax = qhi[k];
+      float d = quant_dequant(v[c][k], q);
+      if (has_m) d = d * mv[k];
+      o[k] = d;
     }
     float* orow = yb + (size_t)c * HW;
     if (kVec) {
