@@ -50,6 +50,11 @@ class MCAQHooks(nn.Module):
         # regression's reduction order follows the image's global batch index
         self.process_group = None
         self.batch_offset, self.batch_total = 0, None
+        # thread count of the CPU reference run whose soft-mask softmax the
+        # kernels reproduce bit for bit (ATen's exp per tile follows its thread
+        # partition); None = torch.get_num_threads() at each call,
+        # an int pins it (results then independent of this process's threads)
+        self.softmax_threads = None
         self._handles = []
         self._plans = {}
         if str(device).startswith("cuda") and torch.cuda.is_available():
@@ -152,7 +157,7 @@ class MCAQHooks(nn.Module):
                  mapper_kind=self.bit_mapping, normalize=self.normalize_complexity, minmax=minmax,
                  binarize_otsu=an.binarize_impl == "otsu", contour_components=an.contour_components,
                  canny_legacy=an.canny_impl == "legacy", min_bits=self.bit_mapper.min_bits, max_bits=self.bit_mapper.max_bits, quantize=quantize,
-                 per_tensor=not quantizer.per_channel, process_group=self.process_group if minmax is None else None,
+                 per_tensor=not quantizer.per_channel, softmax_threads=self.softmax_threads, process_group=self.process_group if minmax is None else None,
                  batch_offset=self.batch_offset, batch_total=self.batch_total)
         feat_q = b["y"] if quantize else feat
         state.setdefault("aux", []).append({"layer": layer_idx, "complexity": b["complexity"],

@@ -354,3 +354,31 @@ def test_per_tensor_calibrated_frozen_hook_equals_cpu_path():
     assert res["cpu"][2:] == res[DEV][2:]
     assert np.array_equal(res["cpu"][1], res[DEV][1])
     assert np.array_equal(res["cpu"][0], res[DEV][0])
+
+
+def test_hooks_softmax_threads_pinned():
+    """MCAQHooks.softmax_threads pins the ATen thread partition the soft mask
+    reproduces: the fused hook at softmax_threads=T equals the oracle at T,
+    whatever torch.get_num_threads() is in this process."""
+    from mcaq_yolo_amd.hooks import MCAQHooks
+    d = load_case("odd_c20")
+    x = d["x"].astype(f32)
+    W = load_weights()
+    h = MCAQHooks(grid_size=int(d["grid"]), device=DEV, indices=(4,))
+    sd = {k: v for k, v in _sd("").items() if k.startswith(("complexity_analyzer.", "bit_mapper."))}
+    sd.update({"quantizers.4." + k: v for k, v in _sd("").items() if k.startswith("soft_mask.")})
+    h.load_state_dict(sd, strict=False)
+    h.eval()
+    old = torch.get_num_threads()
+    try:
+        torch.set_num_threads(3)
+        for T in (1, 8):
+            h.softmax_threads = T
+            with torch.no_grad():
+                outs, aux = h.forward_features([torch.from_numpy(x).to(DEV)])
+            bits = aux[0]["bit_map"].cpu().numpy()
+            m = O.soft_mask(bits, x, W, threads=T)
+            y = O.quantize(x, bits, m, x.min(axis=(0, 2, 3)), x.max(axis=(0, 2, 3)))
+            assert np.array_equal(outs[0].cpu().numpy(), y), T
+    finally:
+        torch.set_num_threads(old)
