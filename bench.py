@@ -581,8 +581,8 @@ def kernel_timing(plan, reps=40):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=400, help="timed steps (400 x ~65 us: the pipeline fill / drain is < 0.5 %% of the window)")
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS) + [5],
                     help="2/3/4: inference hook path; 5: QAT hook training step")
     ap.add_argument("--pipeline", type=int, default=3, help="batches in flight (HIP streams)")
