@@ -601,6 +601,8 @@ def main():
                     help="streams: --pipeline batches in flight, one HIP graph each (default); split: HBM passes "
                          "on one stream, morphology on two (SplitRunner, eager, N = 1)")
     ap.add_argument("--lookahead", type=int, default=3, help="--schedule split: batches of look-ahead")
+    ap.add_argument("--m-plane", action="store_true",
+                    help="pass B writes the m(p) plane and pass 2 reads it (instead of regenerating m per slice)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -642,7 +644,7 @@ def main():
                  for i, (c, (h, w)) in enumerate(zip(chans, SIZES))]
         plan = HookPlan(geoms, dev)
         plan.prepare(feats, cm, mm, [sm, sm, sm], temperature=1.0, mapper_kind=mapper,
-                     batch_offset=rank * B, batch_total=world * B)
+                     batch_offset=rank * B, batch_total=world * B, m_plane=args.m_plane)
         plan.feats = feats
         plans.append(plan)
     torch.cuda.synchronize()

@@ -115,7 +115,7 @@ class HookPlan:
     def prepare(self, feats, cmlp, mapper, smasks, temperature=1.0, mapper_kind="mlp", continuous=False,
                 normalize=False, minmax=None, batch_offset=0, batch_total=None, binarize_otsu=False,
                 contour_components=True, canny_legacy=False, min_bits=2.0, max_bits=8.0, quantize=True, hysteresis_iters=8,
-                per_tensor=False, softmax_threads=None):
+                per_tensor=False, softmax_threads=None, m_plane=False):
         """Validate inputs and build the launch descriptors (pointers are baked
         in: the tensors must stay alive and in place until the last launch).
         minmax: optional per-scale (xmin, xmax) frozen calibration stats.
@@ -123,9 +123,16 @@ class HookPlan:
         quantization.py:655-661), broadcast to the C entries the kernel reads.
         softmax_threads: thread count of the CPU reference whose soft-mask
         softmax is reproduced bit for bit (ATen picks SLEEF or glibc exp per
-        tile by its thread partition); default torch.get_num_threads()."""
+        tile by its thread partition); default torch.get_num_threads().
+        m_plane: pass B writes the soft-mask plane m(p) and pass 2 reads it,
+        instead of pass 2 regenerating m(p) from the tile values per channel
+        slice (+4 B per pixel written, +4 B per pixel per slice read)."""
         n = len(self.geoms)
         L = self.lib
+        if m_plane:
+            for g, b in zip(self.geoms, self.bufs):
+                if b["m"] is None:
+                    b["m"] = torch.empty(g.B, 1, g.H, g.W, device=self.device)
         if len(feats) != n:
             raise ValueError("expected %d feature maps" % n)
         for f, g in zip(feats, self.geoms):
@@ -213,7 +220,10 @@ class HookPlan:
             for i, (f, g, b) in enumerate(zip(feats, self.geoms, self.bufs)):
                 s = qs[i]
                 s.x, s.y, s.bits = _p(f), _p(b["y"]), _p(b["bits"])
-                s.mt = _p(b["mt"]) if with_mask[i] else None   # m(p) generated in the quant pass
+                if with_mask[i] and m_plane:
+                    s.m = _p(b["m"])                              # m(p) plane written by pass B
+                else:
+                    s.mt = _p(b["mt"]) if with_mask[i] else None  # m(p) generated in the quant pass
                 s.xmin, s.xmax = _p(b["xmin"]), _p(b["xmax"])
                 s.B, s.C, s.H, s.W, s.ht, s.wt = g.B, g.C, g.H, g.W, g.ht, g.wt
                 s.bits_lo, s.nbits = lo_b, nb

@@ -319,3 +319,14 @@ def test_config4_yolov8m_slice_properties(dev, blobs):
     384 x 40^2, 576 x 20^2, grid 8) at full size."""
     seen = _full_size_properties(dev, blobs, [(32, 192, 80, 80), (32, 384, 40, 40), (32, 576, 20, 20)], 8, 4)
     assert len(seen) >= 2
+
+
+def test_m_plane_option_same_y(dev, blobs):
+    """m_plane=True (pass B writes m(p), pass 2 reads it) gives the y of the
+    default (pass 2 regenerates m(p) from the tile values): same FMA order."""
+    xs = [load_case(n)["x"].astype(f32) for n in ("full_p3", "full_p4", "full_p5")]
+    a = run_plan(dev, blobs, xs, 8, "mlp")
+    b = run_plan(dev, blobs, xs, 8, "mlp", m_plane=True)
+    for oa, ob, x in zip(a, b, xs):
+        assert np.array_equal(oa["y"], ob["y"])
+        check_against_oracle(ob, x, blobs[0], 8, "mlp")
