@@ -198,37 +198,6 @@ __device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, fl
   const int nblk = (C + ST_CG - 1) / ST_CG;
   const int rounds = (nblk + ST_WAVES - 1) / ST_WAVES;
 
-  // ---- tail columns (ATen row_sum order, < 32 pixels, the image's last unit):
-  // when their 4 x ceil(C/64) 16-row block items fit one per thread, the
-  // items' loads are issued here, ahead of the main loads, so they ride on
-  // the same memory round trip (r02 probe: the tail's own round trip was
-  // ~0.85 us of pass 1 at config 2); the sums are taken after the main loop
-  const int tstart = imax_(aten_tail_start(HW), base);
-  const int tend = imin_(HW, base + UPIX);
-  const int ntail = tend - tstart;
-  const int nilp = C >> 2;                        // rows per interleaved cascade
-  const int nbt = (nilp + 15) >> 4;               // 16-row blocks per cascade
-#ifdef MCAQ_PROBE_STATS_NO_TAIL   // timing probe only (wrong tail sums): tools/probe/stats_probe.sh
-  const bool need_tail = false;
-#else
-  const bool need_tail = ntail > 0 && (want_a || (want_g && !cropped));
-#endif
-  const bool coop = nbt <= 16;                    // 31 px x 4 x 16 x 2 floats fit the LDS
-  const int titems = ntail * 4 * nbt;
-  // (one-pixel-per-lane units only: the C5-shaped scales with a tail; the
-  // 16 extra registers would spill the 2/4-pixel instantiations)
-  const bool tpre = PPL == 1 && need_tail && coop && titems <= 256;
-  float tv[16];
-  int tn = 0;
-  if (tpre && tid < titems) {
-    const int i = tid / (4 * nbt), rem = tid - i * (4 * nbt);
-    const int k = rem / nbt, j = rem - k * nbt;
-    const int r0 = 16 * j;
-    tn = imin_(16, nilp - r0);
-#pragma unroll
-    for (int e = 0; e < 16; ++e) tv[e] = xb[(size_t)(4 * (r0 + (e < tn ? e : 0)) + k) * HW + tstart + i];
-  }
-
   Fold fg, fa;   // pixel `tid` (tid < UPIX)
   fg.init(); fa.init();
   // MR rounds of 16-row blocks are loaded before the first is reduced (MR * 16
@@ -325,33 +294,35 @@ __device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, fl
     }
   }
 
-  // ---- tail columns: block sums of the prefetched items (or loaded here)
+  // ---- tail columns (row_sum order), all in the image's last unit
+  const int tstart = imax_(aten_tail_start(HW), base);
+  const int tend = imin_(HW, base + UPIX);
+  const int ntail = tend - tstart;
+  const int nilp = C >> 2;                        // rows per interleaved cascade
+  const int nbt = (nilp + 15) >> 4;               // 16-row blocks per cascade
+#ifdef MCAQ_PROBE_STATS_NO_TAIL   // timing probe only (wrong tail sums): tools/probe/stats_probe.sh
+  const bool need_tail = false;
+#else
+  const bool need_tail = ntail > 0 && (want_a || (want_g && !cropped));
+#endif
+  const bool coop = nbt <= 16;                    // 31 px x 4 x 16 x 2 floats fit the LDS
   float tg = 0.0f, ta = 0.0f;
   if (need_tail && coop) {
     float* tsg = lds;                             // [px][k][j]
     float* tsa = lds + ST_LDS / 2;
-    const int items = titems;
-    if (tpre) {
-      if (tid < items) {
-        float sg = 0.0f, sa = 0.0f;
+    const int items = ntail * 4 * nbt;
+    for (int it = tid; it < items; it += 256) {
+      const int i = it / (4 * nbt), rem = it - i * (4 * nbt);
+      const int k = rem / nbt, j = rem - k * nbt;
+      const int p = tstart + i;
+      const int r0 = 16 * j, n = imin_(16, nilp - r0);
+      float v[16];
 #pragma unroll
-        for (int e = 0; e < 16; ++e) if (e < tn) { sg = sg + tv[e]; sa = sa + fabsf(tv[e]); }
-        tsg[tid] = sg; tsa[tid] = sa;
-      }
-    } else {
-      for (int it = tid; it < items; it += 256) {
-        const int i = it / (4 * nbt), rem = it - i * (4 * nbt);
-        const int k = rem / nbt, j = rem - k * nbt;
-        const int p = tstart + i;
-        const int r0 = 16 * j, n = imin_(16, nilp - r0);
-        float v[16];
+      for (int e = 0; e < 16; ++e) v[e] = xb[(size_t)(4 * (r0 + (e < n ? e : 0)) + k) * HW + p];
+      float sg = 0.0f, sa = 0.0f;
 #pragma unroll
-        for (int e = 0; e < 16; ++e) v[e] = xb[(size_t)(4 * (r0 + (e < n ? e : 0)) + k) * HW + p];
-        float sg = 0.0f, sa = 0.0f;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) if (e < n) { sg = sg + v[e]; sa = sa + fabsf(v[e]); }
-        tsg[it] = sg; tsa[it] = sa;
-      }
+      for (int e = 0; e < 16; ++e) if (e < n) { sg = sg + v[e]; sa = sa + fabsf(v[e]); }
+      tsg[it] = sg; tsa[it] = sa;
     }
     __syncthreads();
     const int i = tid - (tstart - base);
