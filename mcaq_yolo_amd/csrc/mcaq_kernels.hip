@@ -592,30 +592,12 @@ __global__ __launch_bounds__(256) void mcaq_quant_kernel(QuantArgs a) {
   const mcaq_quant_scale& S = a.s[si];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int HW = S.H * S.W;
+  const int upi = (HW + 255) / 256;
   const int nsl = (S.C + QSLICE - 1) / QSLICE;
   int lu = unit - S.unit_begin;
   const int slice = lu % nsl; lu /= nsl;
-  // kVec (HW % 4 == 0): units tile the batch's flattened pixel range, so the
-  // last chunk of an image continues into the next image and no unit runs
-  // part-empty (C4 / C5 at config 2: 89 % / 78 % of the lanes busy with
-  // per-image chunks); a lane's 4 pixels stay in one image.  Scalar path:
-  // per-image chunks.
-  int b, q0, b_first, nimg;
-  if (kVec) {
-    const int f0 = lu * 256 + lane * 4;
-    const int ftot = S.B * HW;
-    b = imin_(f0, ftot - 1) / HW;
-    q0 = f0 < ftot ? f0 - b * HW : HW;       // past the batch: an invalid quad
-    b_first = (lu * 256) / HW;
-    nimg = imin_(S.B - 1, imin_(lu * 256 + 255, ftot - 1) / HW) - b_first + 1;
-  } else {
-    const int upi = (HW + 255) / 256;
-    const int chunk = lu % upi;
-    b = lu / upi;
-    q0 = chunk * 256 + lane * 4;
-    b_first = b;
-    nimg = 1;
-  }
+  const int chunk = lu % upi;
+  const int b = lu / upi;
   const int c0 = slice * QSLICE;
   const int nc = imin_(QSLICE, S.C - c0);
   const int NB = S.nbits;
@@ -625,12 +607,12 @@ __global__ __launch_bounds__(256) void mcaq_quant_kernel(QuantArgs a) {
     qt[i] = make_float4(q.scale, q.zp, q.rs, 0.0f);
   }
   const int NTq = S.ht * S.wt;
-  // the unit's images' m(tile) values in LDS when they fit, else read through L2
-  const bool mlds = kMtLds && nimg * NTq <= QMAXNT;
-  if (mlds && S.mt)
-    for (int i = tid; i < nimg * NTq; i += 256) mts[i] = S.mt[(size_t)b_first * NTq + i];
-  const float* mtab = mlds ? mts + (size_t)(b - b_first) * NTq : (S.mt ? S.mt + (size_t)b * NTq : nullptr);
+  if (kMtLds && S.mt)
+    for (int i = tid; i < NTq; i += 256) mts[i] = S.mt[(size_t)b * NTq + i];
+  // tile grids with more than QMAXNT tiles read their m values through L2
+  const float* mtab = kMtLds ? mts : (S.mt ? S.mt + (size_t)b * NTq : nullptr);
 
+  const int q0 = chunk * 256 + lane * 4;
   const NearestMap nmh = nearest_map(S.ht, S.H), nmw = nearest_map(S.wt, S.W);
   bool pv[4];
   int kb[4];
@@ -1018,27 +1000,25 @@ int mcaq_morph_finalize(const mcaq_morph_scale* scales, int nscales, const mcaq_
 int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream) {
   if (nscales < 1 || nscales > 3) return (int)hipErrorInvalidValue;
   QuantArgs a;
-  // 16-byte rows: HW % 4 == 0 and 16-byte aligned x / y bases (a contiguous
-  // view may start at any float offset), else the scalar kernel
-  bool vec = true;
-  for (int i = 0; i < nscales; ++i)
-    vec = vec && ((scales[i].H * scales[i].W) & 3) == 0 && (((uintptr_t)scales[i].x | (uintptr_t)scales[i].y) & 15) == 0;
   int units = 0;
   for (int i = 0; i < nscales; ++i) {
     a.s[i] = scales[i];
     a.s[i].unit_begin = units;
     const int HW = scales[i].H * scales[i].W;
     if (scales[i].nbits < 1 || scales[i].nbits > QMAXBITS || scales[i].bits_lo < 1 ||
-        scales[i].bits_lo + scales[i].nbits - 1 > 16 || HW < 1 || scales[i].C < 1 || scales[i].B < 1 ||
+        scales[i].bits_lo + scales[i].nbits - 1 > 16 || HW < 1 || scales[i].C < 1 ||
         scales[i].ht < 1 || scales[i].wt < 1 || !scales[i].x || !scales[i].y || !scales[i].bits ||
         !scales[i].xmin || !scales[i].xmax)
       return (int)hipErrorInvalidValue;
-    // vector kernel: 256-pixel units over the batch's flattened pixels; scalar: per image
-    const long long chunks = vec ? ((long long)scales[i].B * HW + 255) / 256 : (long long)scales[i].B * ((HW + 255) / 256);
-    units += (int)(chunks * ((scales[i].C + QSLICE - 1) / QSLICE));
+    units += scales[i].B * ((HW + 255) / 256) * ((scales[i].C + QSLICE - 1) / QSLICE);
   }
   a.nscales = nscales;
   a.units_total = units;
+  // 16-byte rows: HW % 4 == 0 and 16-byte aligned x / y bases (a contiguous
+  // view may start at any float offset), else the scalar kernel
+  bool vec = true;
+  for (int i = 0; i < nscales; ++i)
+    vec = vec && ((scales[i].H * scales[i].W) & 3) == 0 && (((uintptr_t)scales[i].x | (uintptr_t)scales[i].y) & 15) == 0;
   // nontemporal policy (measured): bit 0 = streaming stores of
   // y, bit 1 = nontemporal loads of x.  NT stores always; NT loads only when
   // the launch reads > 256 MB of x (config 3), where nothing of x survives in
