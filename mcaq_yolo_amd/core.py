@@ -290,7 +290,7 @@ class MorphologicalComplexityAnalyzer(nn.Module):
         B, C, H, W = x.shape
         T = tile_size(H, self.grid_size)
         ht, wt = H // T, W // T
-        if ht < 1 or wt < 1 or T > 64:
+        if ht < 1 or wt < 1 or T > 128:
             raise ValueError("feature map %dx%d: tile %d unsupported" % (H, W, T))
         dev = x.device
         gray = torch.empty(B, ht * T, wt * T, device=dev)

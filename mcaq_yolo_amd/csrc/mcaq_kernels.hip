@@ -893,7 +893,7 @@ int mcaq_morph_finalize(const mcaq_morph_scale* scales, int nscales, const mcaq_
     memcpy(&a.s[i], &scales[i], sizeof(MorphScale));
     MorphScale& S = a.s[i];
     if (S.B < 1 || S.ht < 1 || S.wt < 1) return (int)hipErrorInvalidValue;
-    if (S.tile < 4 || (S.tile & (S.tile - 1)) || S.tile > 64) return (int)hipErrorInvalidValue;
+    if (S.tile < 4 || (S.tile & (S.tile - 1)) || S.tile > 128) return (int)hipErrorInvalidValue;
     if (S.Hc != S.ht * S.tile || S.Wc != S.wt * S.tile || S.Hc > S.H || S.Wc > S.W) return (int)hipErrorInvalidValue;
     // tile_tmp carries the per-tile partials from pass A to pass B; without
     // F_PHI the complexity MLP reads phi from phi_out

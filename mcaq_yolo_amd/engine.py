@@ -51,8 +51,8 @@ class ScaleGeom:
         self.Hc, self.Wc = self.ht * self.tile, self.wt * self.tile
         if self.ht < 1 or self.wt < 1:
             raise ValueError("feature map %dx%d smaller than one %d-pixel tile" % (H, W, self.tile))
-        if self.tile > 64:
-            raise ValueError("tile %d > 64 not supported (H=%d, grid=%d)" % (self.tile, H, grid_size))
+        if self.tile > 128:
+            raise ValueError("tile %d > 128 not supported (H=%d, grid=%d)" % (self.tile, H, grid_size))
 
     @property
     def key(self):

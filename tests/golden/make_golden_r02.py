@@ -15,6 +15,9 @@ Files written (DATA only; no reference source is copied):
   pt_<shape>.npz                 per_channel=False quantizer (quantization.py:655-661):
                                  one batch min/max over every channel; full y
                                  (`python make_golden_r02.py pertensor` writes only these)
+  case_t128_c1.npz               1 x 1 x 1024^2 at grid 8: tile 128, the largest tile the
+                                 analyzer kernel takes (`python make_golden_r02.py t128`
+                                 writes only this); y as channel sums
 """
 import os
 import sys
@@ -112,9 +115,18 @@ def per_tensor():
         print("pt", sname, "bits", np.unique(out["bits_mlp"]).astype(int).tolist())
 
 
+def t128():
+    x = synth_features(1, 1, 1024, 1024, seed=66000)
+    out = run_case(x, 8, {}, full_y=None)
+    np.savez_compressed(os.path.join(HERE, "case_t128_c1.npz"), **out)
+    print("t128_c1 tile", out["tile"], "bits", np.unique(out["bits_mlp"]).astype(int).tolist())
+
+
 def main():
     if sys.argv[1:] == ["pertensor"]:
         return per_tensor()
+    if sys.argv[1:] == ["t128"]:
+        return t128()
     for i, (name, (B, C, H, W, grid)) in enumerate(LARGE.items()):
         x = synth_features(B, C, H, W, seed=77000 + i)
         out = run_case(x, grid, {}, full_y=False)
@@ -129,6 +141,7 @@ def main():
             np.savez_compressed(os.path.join(HERE, "opt_%s_%s.npz" % (vname, sname)), **out)
             print(vname, sname, "bits", np.unique(out["bits_mlp"]).astype(int).tolist())
     per_tensor()
+    t128()
 
 
 if __name__ == "__main__":

@@ -31,7 +31,7 @@ def mods():
 
 
 # ---- test_smoke.py restated -------------------------------------------------
-@pytest.mark.parametrize("H", [640, 80, 40, 20])
+@pytest.mark.parametrize("H", [1024, 640, 80, 40, 20])
 def test_phi_tiles_shapes(H):
     """test_smoke.py:33-47"""
     from mcaq_yolo_amd.core import MorphologicalComplexityAnalyzer
@@ -44,6 +44,22 @@ def test_phi_tiles_shapes(H):
     assert set(detailed) == {"fractal", "texture", "gradient", "edge", "contour"}
     assert tile >= 4 and (tile & (tile - 1)) == 0
     assert float(phi.min()) >= 0.0 and float(phi.max()) <= 1.0 + 1e-5
+
+
+def test_analyzer_tile128_vs_reference(mods):
+    """1024^2 image at grid 8 -> tile 128 (curriculum scoring of large
+    inputs): phi bit-exact, C within 1e-6 and bits exact vs the reference
+    fixture case_t128_c1."""
+    a, m, _ = mods
+    d = load_case("t128_c1")
+    x = torch.from_numpy(d["x"].astype(f32)).to(DEV)
+    with torch.no_grad():
+        phi, _ = a.compute_phi_tiles(x)
+        c = a(x)
+        assert np.array_equal(phi.cpu().numpy(), d["phi"])
+        cc = c.cpu().numpy()
+        assert np.max(np.abs(cc - d["complexity"]) / np.abs(d["complexity"])) < 1e-6
+        assert np.array_equal(m(c, 1.0).cpu().numpy(), d["bits_mlp"])
 
 
 def test_analyzer_forward_range():

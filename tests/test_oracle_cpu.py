@@ -16,7 +16,7 @@ from conftest import GOLDEN, case_names, load_case, load_weights
 from oracle import mcaq_oracle as O
 from oracle.ieee import aten_sum, fma32
 
-FAST = [c for c in case_names() if c not in ("t64_c1", "t32_c4", "m_p3", "m_p4")]   # m_*: test_option_and_yolov8m_fixtures
+FAST = [c for c in case_names() if c not in ("t64_c1", "t32_c4", "t128_c1", "m_p3", "m_p4")]   # m_*: test_option_and_yolov8m_fixtures
 
 
 def rel(a, b):
@@ -112,6 +112,23 @@ def test_complexity_bits_mask_y(name):
         assert np.allclose(y.astype(np.float64).sum(axis=(2, 3)), d["y_mlp_sum"], rtol=1e-9, atol=1e-6)
 
 
+def test_tile128_fixture():
+    """case_t128_c1 (1x1x1024^2, grid 8 -> tile 128, the largest tile the
+    analyzer kernel takes): edge / mask / phi1..phi8 bit-exact, bits exact."""
+    d = load_case("t128_c1")
+    assert int(d["tile"]) == 128
+    x = d["x"].astype(np.float32)
+    W = load_weights()
+    phi, I = O.phi_tiles(x, 8, internals=True)
+    assert np.array_equal(I["edge"], d["edge"]) and np.array_equal(I["binmask"], d["binmask"])
+    assert np.array_equal(phi, d["phi"])
+    c = O.complexity_mlp(phi.reshape(-1, 8), W).reshape(phi.shape[:3])
+    C = np.clip(O.bilateral(c), np.float32(0.0), np.float32(1.0)).astype(np.float32)
+    assert rel(C, d["complexity"]) < 1e-6
+    assert np.array_equal(O.mlp_mapper(C, W, 1.0), d["bits_mlp"])
+    assert np.array_equal(O.linear_mapper(C, 1.0), d["bits_lin"])
+
+
 # ---- the reference's own known-answer tests (tests/test_smoke.py) ----------
 
 def test_euler_component_kat():
@@ -147,7 +164,7 @@ def test_tile_size_and_ranges(H):
 
 def test_log2_overrides_match_torch():
     torch = pytest.importorskip("torch")
-    for T in (4, 8, 16, 32, 64):
+    for T in (4, 8, 16, 32, 64, 128):
         p = (np.arange(T * T + 1, dtype=np.float32) / np.float32(T * T)).astype(np.float32)
         a = (p + np.float32(1e-10)).astype(np.float32)
         assert np.array_equal(torch.log2(torch.from_numpy(a)).numpy(), O.log2_torch(a))

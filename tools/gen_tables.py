@@ -25,12 +25,13 @@ def table(name, arr):
 def fractal_constants():
     """Box-counting regression terms that depend only on the number of scales
     S = log2(tile) (morphology.py:596-617, oracle.fractal_tiles): x = log(s),
-    w = exp(-0.1 i), and per S the scalars w_sum, x_mean, var."""
+    w = exp(-0.1 i), and per S the scalars w_sum, x_mean, var; S <= 8 (the
+    kernel's register arrays), tile <= 128 used."""
     f32 = np.float32
-    x = cr32(np.log, np.array([2.0 ** (i + 1) for i in range(6)], f32))
-    w = cr32(np.exp, (f32(-0.1) * np.arange(6, dtype=f32)).astype(f32))
-    st = np.zeros((7, 4), f32)
-    for S in range(2, 7):
+    x = cr32(np.log, np.array([2.0 ** (i + 1) for i in range(8)], f32))
+    w = cr32(np.exp, (f32(-0.1) * np.arange(8, dtype=f32)).astype(f32))
+    st = np.zeros((9, 4), f32)
+    for S in range(2, 9):
         ws, xs = w[:S], x[:S]
         w_sum = aten_sum(ws[:, None])[0]
         x_mean = (aten_sum((ws * xs).astype(f32)[:, None])[0] / w_sum).astype(f32)
