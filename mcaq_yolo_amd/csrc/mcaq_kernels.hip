@@ -79,6 +79,12 @@ static inline int stats_ppl(int C, int HW) {
 // bits picked before, so lane l ends with one channel reduced over all 16
 // lanes of its row), then two cross-row exchanges.  Min and max are exact in
 // any order.
+// NaN-propagating min / max (v_minimum3_f32 / v_maximum3_f32 on gfx950, as
+// ATen's amin/amax propagate NaN): unlike fminf/fmaxf in IEEE mode they need
+// no v_max_f32 canonicalisation of loaded or DPP-moved operands, which was a
+// third of pass 1's min/max VALU work.  Exact in any order.
+__device__ __forceinline__ float vmin_(float a, float b) { return __builtin_elementwise_minimum(a, b); }
+__device__ __forceinline__ float vmax_(float a, float b) { return __builtin_elementwise_maximum(a, b); }
 template <int CTRL>
 __device__ __forceinline__ float dpp_f(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
@@ -89,8 +95,8 @@ __device__ __forceinline__ void rs_step(float (&mn)[16], float (&mx)[16], bool u
   for (int i = 0; i < H; ++i) {
     const float smn = up ? mn[i] : mn[i + H], kmn = up ? mn[i + H] : mn[i];
     const float smx = up ? mx[i] : mx[i + H], kmx = up ? mx[i + H] : mx[i];
-    mn[i] = fminf(kmn, dpp_f<CTRL>(smn));
-    mx[i] = fmaxf(kmx, dpp_f<CTRL>(smx));
+    mn[i] = vmin_(kmn, dpp_f<CTRL>(smn));
+    mx[i] = vmax_(kmx, dpp_f<CTRL>(smx));
   }
 }
 // returns channel c(l) = 8*b3 + 4*b2 + 2*b1 + b0 of lane l (b = bits of l & 15)
@@ -100,8 +106,8 @@ __device__ __forceinline__ void wave_minmax16(float (&mn)[ST_CG], float (&mx)[ST
   rs_step<2, 0x4E>(mn, mx, (lane & 2) != 0);    // quad_perm 2301 (l ^ 2)
   rs_step<1, 0xB1>(mn, mx, (lane & 1) != 0);    // quad_perm 1032 (l ^ 1)
   float a = mn[0], b = mx[0];
-  a = fminf(a, __shfl_xor(a, 16, 64)); b = fmaxf(b, __shfl_xor(b, 16, 64));
-  a = fminf(a, __shfl_xor(a, 32, 64)); b = fmaxf(b, __shfl_xor(b, 32, 64));
+  a = vmin_(a, __shfl_xor(a, 16, 64)); b = vmax_(b, __shfl_xor(b, 16, 64));
+  a = vmin_(a, __shfl_xor(a, 32, 64)); b = vmax_(b, __shfl_xor(b, 32, 64));
   omn = a; omx = b;
 }
 
@@ -268,8 +274,8 @@ __device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, fl
             float lo = v[rr][i][0], hi = v[rr][i][0];
 #pragma unroll
             for (int k = 1; k < PPL; ++k) {
-              lo = fminf(lo, v[rr][i][k]);
-              hi = fmaxf(hi, v[rr][i][k]);
+              lo = vmin_(lo, v[rr][i][k]);
+              hi = vmax_(hi, v[rr][i][k]);
             }
             mn[i] = lo; mx[i] = hi;
           }
