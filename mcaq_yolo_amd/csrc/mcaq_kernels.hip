@@ -415,22 +415,22 @@ __device__ __forceinline__ void finalize_body(const FinalizeArgs& a, int blk, fl
   const mcaq_finalize_scale& S = a.s[si];
   const int nthr = (int)blockDim.x, parts = nthr >> 6;
   if (S.per_tensor) {   // one workgroup: every (unit, channel) partial, then broadcast
-    float mn = 3.402823466e38f, mx = -3.402823466e38f;
+    float mn = __builtin_huge_valf(), mx = -__builtin_huge_valf();
     const int tid = (int)threadIdx.x;
     if (S.pmin) {
       const size_t n = (size_t)S.nunits * S.C;
-      for (size_t i = tid; i < n; i += nthr) { mn = fminf(mn, S.pmin[i]); mx = fmaxf(mx, S.pmax[i]); }
+      for (size_t i = tid; i < n; i += nthr) { mn = vmin_(mn, S.pmin[i]); mx = vmax_(mx, S.pmax[i]); }
     } else {
       for (int c = tid; c < (S.min_stride ? S.C : 1); c += nthr) {
-        mn = fminf(mn, S.min_in[(size_t)S.min_stride * c]);
-        mx = fmaxf(mx, S.max_in[(size_t)S.min_stride * c]);
+        mn = vmin_(mn, S.min_in[(size_t)S.min_stride * c]);
+        mx = vmax_(mx, S.max_in[(size_t)S.min_stride * c]);
       }
     }
     red[tid] = mn;
     red[nthr + tid] = mx;
     __syncthreads();
     for (int h = nthr >> 1; h > 0; h >>= 1) {
-      if (tid < h) { red[tid] = fminf(red[tid], red[tid + h]); red[nthr + tid] = fmaxf(red[nthr + tid], red[nthr + tid + h]); }
+      if (tid < h) { red[tid] = vmin_(red[tid], red[tid + h]); red[nthr + tid] = vmax_(red[nthr + tid], red[nthr + tid + h]); }
       __syncthreads();
     }
     mn = red[0];
@@ -441,7 +441,7 @@ __device__ __forceinline__ void finalize_body(const FinalizeArgs& a, int blk, fl
   const int cl = threadIdx.x & 63, part = threadIdx.x >> 6;
   const int c = (blk - S.block_begin) * 64 + cl;
   const bool cv = c < S.C;
-  float mn = 3.402823466e38f, mx = -3.402823466e38f;
+  float mn = __builtin_huge_valf(), mx = -__builtin_huge_valf();
   if (cv) {
     if (S.pmin) {
       const float* pn = S.pmin + c;
@@ -452,12 +452,12 @@ __device__ __forceinline__ void finalize_body(const FinalizeArgs& a, int blk, fl
         const size_t o = (size_t)u * S.C;
         const float m0 = pn[o], m1 = pn[o + st], m2 = pn[o + 2 * st], m3 = pn[o + 3 * st];
         const float x0 = px[o], x1 = px[o + st], x2 = px[o + 2 * st], x3 = px[o + 3 * st];
-        mn = fminf(mn, fminf(fminf(m0, m1), fminf(m2, m3)));
-        mx = fmaxf(mx, fmaxf(fmaxf(x0, x1), fmaxf(x2, x3)));
+        mn = vmin_(mn, vmin_(vmin_(m0, m1), vmin_(m2, m3)));
+        mx = vmax_(mx, vmax_(vmax_(x0, x1), vmax_(x2, x3)));
       }
       for (; u < S.nunits; u += parts) {
-        mn = fminf(mn, pn[(size_t)u * S.C]);
-        mx = fmaxf(mx, px[(size_t)u * S.C]);
+        mn = vmin_(mn, pn[(size_t)u * S.C]);
+        mx = vmax_(mx, px[(size_t)u * S.C]);
       }
     } else if (part == 0) {
       mn = S.min_in[(size_t)S.min_stride * c];
@@ -468,7 +468,7 @@ __device__ __forceinline__ void finalize_body(const FinalizeArgs& a, int blk, fl
   red[nthr + part * 64 + cl] = mx;
   __syncthreads();
   if (part == 0 && cv) {
-    for (int k = 1; k < parts; ++k) { mn = fminf(mn, red[k * 64 + cl]); mx = fmaxf(mx, red[nthr + k * 64 + cl]); }
+    for (int k = 1; k < parts; ++k) { mn = vmin_(mn, red[k * 64 + cl]); mx = vmax_(mx, red[nthr + k * 64 + cl]); }
     S.min_out[c] = mn;
     S.max_out[c] = mx;
   }

@@ -398,3 +398,22 @@ def test_hooks_softmax_threads_pinned():
             assert np.array_equal(outs[0].cpu().numpy(), y), T
     finally:
         torch.set_num_threads(old)
+
+
+@pytest.mark.parametrize("shape", [(2, 24, 40, 40), (3, 20, 13, 11), (2, 256, 20, 20)])
+def test_channel_minmax_nonfinite_like_aten(shape):
+    """Pass 1 + finalize channel min/max propagate NaN and keep +-inf, as
+    ATen's amin/amax (quantization.py:650-654) do."""
+    from mcaq_yolo_amd import core
+    g = torch.Generator().manual_seed(sum(shape))
+    x = torch.randn(*shape, generator=g)
+    B, C, H, W = shape
+    x[1, 2, H // 2, W // 3] = float("nan")
+    x[0, 3, H - 1, W - 1] = float("inf")
+    x[-1, 4, 0, 0] = float("-inf")
+    x[:, 5] = float("inf")
+    x[:, 6] = -0.0
+    mn, mx = core._channel_minmax(x.to(DEV))
+    rmn, rmx = x.amin(dim=(0, 2, 3)), x.amax(dim=(0, 2, 3))
+    torch.testing.assert_close(mn.cpu(), rmn, rtol=0, atol=0, equal_nan=True)
+    torch.testing.assert_close(mx.cpu(), rmx, rtol=0, atol=0, equal_nan=True)
