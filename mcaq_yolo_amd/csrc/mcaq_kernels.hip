@@ -607,22 +607,23 @@ __global__ __launch_bounds__(256) void mcaq_quant_kernel(QuantArgs a) {
   const int c0 = slice * QSLICE;
   const int nc = imin_(QSLICE, S.C - c0);
   const int NB = S.nbits;
-  for (int i = tid; i < nc * NB; i += 256) {
-    const int c = i / NB, k = i - (i / NB) * NB;
-    const QParam q = qparam(S.xmin[c0 + c], S.xmax[c0 + c], S.bits_lo + k);
-    qt[i] = make_float4(q.scale, q.zp, q.rs, 0.0f);
-  }
   const int NTq = S.ht * S.wt;
-  if (kMtLds && S.mt)
-    for (int i = tid; i < NTq; i += 256) mts[i] = S.mt[(size_t)b * NTq + i];
+  // Issue order: the small operands (this thread's first table entry's
+  // min/max, first m(tile) value, the lanes' tile bits), then the x rows;
+  // the table and the staged m values are built while x is in flight (one
+  // memory round trip before compute instead of three in sequence).
+  const int ntab = nc * NB;
+  float tmn = 0.0f, tmx = 0.0f;
+  if (tid < ntab) { const int c = tid / NB; tmn = S.xmin[c0 + c]; tmx = S.xmax[c0 + c]; }
+  const bool mt0 = kMtLds && S.mt && tid < NTq;
+  const float mtv = mt0 ? S.mt[(size_t)b * NTq + tid] : 0.0f;
   // tile grids with more than QMAXNT tiles read their m values through L2
   const float* mtab = kMtLds ? mts : (S.mt ? S.mt + (size_t)b * NTq : nullptr);
 
   const int q0 = chunk * 256 + lane * 4;
   const NearestMap nmh = nearest_map(S.ht, S.H), nmw = nearest_map(S.wt, S.W);
   bool pv[4];
-  int kb[4];
-  float mv[4];
+  float bv[4], mv[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int p = imin_(q0 + k, HW - 1);
@@ -636,18 +637,10 @@ __global__ __launch_bounds__(256) void mcaq_quant_kernel(QuantArgs a) {
       th = nearest_apply(nmh, h);
       tw = nearest_apply(nmw, w);
     }
-    const float bv = S.bits[((size_t)b * S.ht + th) * S.wt + tw];
-    kb[k] = imin_(imax_((int)rintf(bv), S.bits_lo), S.bits_lo + NB - 1) - S.bits_lo;
+    bv[k] = S.bits[((size_t)b * S.ht + th) * S.wt + tw];
     mv[k] = (S.m && !S.mt) ? S.m[(size_t)b * HW + p] : 1.0f;
   }
   const bool has_m = S.m != nullptr || S.mt != nullptr;
-  float qlo[4], qhi[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int bb = S.bits_lo + kb[k];
-    qlo[k] = (float)(-(1 << (bb - 1)));
-    qhi[k] = (float)((1 << (bb - 1)) - 1);
-  }
   const int cw = wv * QCW;                 // first channel of this wave in the slice
   const int ncw = imin_(QCW, nc - cw);     // may be <= 0 for a short last slice
   const size_t rowbase = ((size_t)b * S.C + c0 + cw) * HW;
@@ -669,6 +662,27 @@ __global__ __launch_bounds__(256) void mcaq_quant_kernel(QuantArgs a) {
         for (int k = 0; k < 4; ++k) v[c][k] = row[imin_(q0 + k, HW - 1)];
       }
     }
+  }
+  if (tid < ntab) {
+    const QParam q = qparam(tmn, tmx, S.bits_lo + (tid - (tid / NB) * NB));
+    qt[tid] = make_float4(q.scale, q.zp, q.rs, 0.0f);
+  }
+  for (int i = tid + 256; i < ntab; i += 256) {   // > 256 entries: continuous bit ranges
+    const int c = i / NB, k = i - (i / NB) * NB;
+    const QParam q = qparam(S.xmin[c0 + c], S.xmax[c0 + c], S.bits_lo + k);
+    qt[i] = make_float4(q.scale, q.zp, q.rs, 0.0f);
+  }
+  if (mt0) mts[tid] = mtv;
+  if (kMtLds && S.mt)
+    for (int i = tid + 256; i < NTq; i += 256) mts[i] = S.mt[(size_t)b * NTq + i];
+  int kb[4];
+  float qlo[4], qhi[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    kb[k] = imin_(imax_((int)rintf(bv[k]), S.bits_lo), S.bits_lo + NB - 1) - S.bits_lo;
+    const int bb = S.bits_lo + kb[k];
+    qlo[k] = (float)(-(1 << (bb - 1)));
+    qhi[k] = (float)((1 << (bb - 1)) - 1);
   }
   __syncthreads();   // qt, mts ready
   if (S.mt) {
