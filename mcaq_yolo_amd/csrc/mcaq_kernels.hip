@@ -587,8 +587,13 @@ constexpr int QMAXNT = 1024;   // max tiles per image whose m values are staged 
 // soft-mask value are fetched once; per-(channel, bits) scale / zero-point
 // come from an LDS table built by the workgroup (IEEE divisions, as
 // QuantizationParameters computes them).
+#ifdef MCAQ_QUANT_MINW   // A/B builds: minimum resident workgroups per CU
+#define MCAQ_QUANT_LB __launch_bounds__(256, MCAQ_QUANT_MINW)
+#else
+#define MCAQ_QUANT_LB __launch_bounds__(256)
+#endif
 template <bool kVec, bool kNTL, bool kNTS, bool kMtLds>
-__global__ __launch_bounds__(256) void mcaq_quant_kernel(QuantArgs a) {
+__global__ MCAQ_QUANT_LB void mcaq_quant_kernel(QuantArgs a) {
   __shared__ float4 qt[QSLICE * QMAXBITS];   // scale, zp, 1/scale
   __shared__ float mts[QMAXNT];
   __shared__ float mq[256];
