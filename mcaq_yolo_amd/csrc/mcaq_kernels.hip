@@ -587,11 +587,14 @@ constexpr int QMAXNT = 1024;   // max tiles per image whose m values are staged 
 // soft-mask value are fetched once; per-(channel, bits) scale / zero-point
 // come from an LDS table built by the workgroup (IEEE divisions, as
 // QuantizationParameters computes them).
-#ifdef MCAQ_QUANT_MINW   // A/B builds: minimum resident workgroups per CU
-#define MCAQ_QUANT_LB __launch_bounds__(256, MCAQ_QUANT_MINW)
-#else
-#define MCAQ_QUANT_LB __launch_bounds__(256)
+// 6 resident workgroups per CU (79 VGPRs, no spills): the prologue's early
+// loads raised the unbounded kernel to 91 VGPRs / 5 workgroups; r02 A/B
+// 29.7 vs 30.4-30.6 us back to back (profiles/r02_probes/ab_round2_late.txt);
+// 7 spills 16 VGPRs
+#ifndef MCAQ_QUANT_MINW
+#define MCAQ_QUANT_MINW 6
 #endif
+#define MCAQ_QUANT_LB __launch_bounds__(256, MCAQ_QUANT_MINW)
 template <bool kVec, bool kNTL, bool kNTS, bool kMtLds>
 __global__ MCAQ_QUANT_LB void mcaq_quant_kernel(QuantArgs a) {
   __shared__ float4 qt[QSLICE * QMAXBITS];   // scale, zp, 1/scale
