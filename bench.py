@@ -549,26 +549,68 @@ class SplitRunner:
             torch.cuda.current_stream().wait_stream(st)
 
 
-def kernel_timing(plan, reps=40):
+class StagedRunner:
+    """--schedule staged (default): the software-pipelined step of
+    engine.HookPipeline - pass 1 of batch i + pass 2 of batch i-3 on one
+    stream, morph pass A of batch i-1 and pass B of batch i-2 on two more;
+    one native call per step.  After the first 3 (filling) steps every step
+    carries one batch's worth of every stage, and a step's pieces depend only
+    on the previous step's, so synchronising before the timed window does
+    not drain the pipeline: the first timed step already runs all four."""
+
+    def __init__(self, plans, pg, cu_masks=None):
+        from mcaq_yolo_amd.engine import HookPipeline
+        self.pipe = HookPipeline(plans, cu_masks=cu_masks, process_group=pg)
+
+    def step(self):
+        self.pipe.submit()
+
+    def sync(self):
+        self.pipe.join(torch.cuda.current_stream())
+
+
+def cu_masks_for(n_morph, ncus=256):
+    """CU masks: n_morph CUs (spread evenly over the chip) for the two morph
+    streams, the rest for the streaming stream; 0 = no masks."""
+    if n_morph <= 0:
+        return None
+    step = ncus / float(n_morph)
+    morph = sorted({int(k * step) for k in range(n_morph)})
+    stream = [c for c in range(ncus) if c not in set(morph)]
+    return [stream, morph, morph]
+
+
+def kernel_timing(plans, reps=40, evict=None):
     """Per-launch device time of each kernel of a step, in sequence: `reps`
-    single-batch steps on one stream.  Pass 1 and pass 2 are launched through
-    hipExtLaunchKernel with start/stop events (mcaq_time_next_launch: the
-    dispatch's own start and end, as a kernel trace reports them); the
-    morphology launch (two kernels + finalize) by events around it."""
+    single-batch steps on one stream, cycling the plans (>= 4 input batches:
+    367 MB of x at config 2, more than the 256 MiB Infinity Cache).  Pass 1
+    and pass 2 are launched through hipExtLaunchKernel with start/stop events
+    (mcaq_time_next_launch: the dispatch's own start and end, as a kernel
+    trace reports them); the morphology launch (two kernels + finalize) by
+    events around it.  evict: a tensor > 256 MiB read by a torch reduction
+    right before each timed pass-1 and pass-2 dispatch, so neither finds x in
+    the Infinity Cache (pass 2 otherwise re-reads the x that pass 1 of the
+    same batch has just read); read-only, so the timed dispatch does not pay
+    for the write-back of the sweep's own lines."""
     st = torch.cuda.current_stream()
-    L = plan.lib
+    L = plans[0].lib
     names = ("stats", "morph_finalize", "quant")
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(6)] for _ in range(reps)]
     for e in ev:            # create the HIP events (lazily created on first record)
         for x in e:
             x.record(st)
     torch.cuda.synchronize()
-    for e in ev:
+    for r, e in enumerate(ev):
+        plan = plans[r % len(plans)]
+        if evict is not None:
+            torch.sum(evict)
         L.mcaq_time_next_launch(ctypes.c_void_p(e[0].cuda_event), ctypes.c_void_p(e[1].cuda_event))
         plan.launch_stats(st)
         e[2].record(st)
         plan.launch_morph(st)
         e[3].record(st)
+        if evict is not None:
+            torch.sum(evict)
         L.mcaq_time_next_launch(ctypes.c_void_p(e[4].cuda_event), ctypes.c_void_p(e[5].cuda_event))
         plan.launch_quant(st)
     torch.cuda.synchronize()
@@ -597,9 +639,12 @@ def main():
     ap.add_argument("--channels-last", action="store_true", help="--e2e: NHWC network (experiment)")
     ap.add_argument("--find", action="store_true", help="--e2e: MIOpen Find (torch.backends.cudnn.benchmark)")
     ap.add_argument("--eager", action="store_true", help="no HIP graphs")
-    ap.add_argument("--schedule", choices=("streams", "split"), default="streams",
-                    help="streams: --pipeline batches in flight, one HIP graph each (default); split: HBM passes "
-                         "on one stream, morphology on two (SplitRunner, eager, N = 1)")
+    ap.add_argument("--schedule", choices=("staged", "streams", "split"), default="staged",
+                    help="staged: software pipeline, pass 1 (i) + pass 2 (i-3) | pass A (i-1) | pass B (i-2) "
+                         "on three streams (default); streams: --pipeline batches in flight, one HIP graph "
+                         "each; split: HBM passes on one stream, morphology on two (SplitRunner, eager, N = 1)")
+    ap.add_argument("--morph-cus", type=int, default=0,
+                    help="--schedule staged: pin the morph streams to this many CUs (0: no CU masks)")
     ap.add_argument("--lookahead", type=int, default=3, help="--schedule split: batches of look-ahead")
     ap.add_argument("--m-plane", action="store_true",
                     help="pass B writes the m(p) plane and pass 2 reads it (instead of regenerating m per slice)")
@@ -636,6 +681,8 @@ def main():
     geoms = [ScaleGeom(B, c, h, w, grid) for c, (h, w) in zip(chans, SIZES)]
     plans = []
     nin = max(args.inputs or max(3, depth), depth)
+    if args.schedule == "staged":
+        nin = max(nin, 4)
     if args.schedule == "split":
         nin = max(nin, args.lookahead + 1)
     for p in range(nin):
@@ -650,7 +697,9 @@ def main():
     torch.cuda.synchronize()
 
     use_graph = not args.eager and args.schedule == "streams"
-    if args.schedule == "split":
+    if args.schedule == "staged":
+        runner = StagedRunner(plans, pg, cu_masks_for(args.morph_cus))
+    elif args.schedule == "split":
         if pg is not None:
             raise SystemExit("--schedule split is a single-GPU experiment")
         runner = SplitRunner(plans, args.lookahead)
@@ -661,17 +710,25 @@ def main():
     runner.sync()
     torch.cuda.synchronize()
 
-    kt = kernel_timing(plans[0])
-    # single-batch latency: one step at a time, nothing in flight beside it
+    # per-kernel device times: in sequence (pass 2 right behind its own pass 1
+    # and morphology) and with x evicted from the Infinity Cache before each
+    # timed HBM pass (the roofline figure)
+    kt_seq = kernel_timing(plans)
+    sweep = torch.ones(96 << 20, device=dev)         # 384 MiB
+    kt = kernel_timing(plans, evict=sweep)
+    del sweep
+    # single-batch latency: one batch through its chain with nothing in flight
+    # beside it (the plan's own launch sequence on one stream)
     lat = []
     for _ in range(10):
         torch.cuda.synchronize()
         t1 = time.perf_counter()
-        runner.step()
-        runner.sync()
+        plans[0].launch(torch.cuda.current_stream())
         torch.cuda.synchronize()
         lat.append(time.perf_counter() - t1)
     latency_ms = sorted(lat)[len(lat) // 2] * 1e3
+    runner.step()         # plans[0] was re-run alone: one more step to be safe, then settle
+    runner.sync()
 
     # ---- timed region: K steps, `depth` batches in flight
     if pg is not None:
@@ -711,14 +768,17 @@ def main():
     if rank == 0:
         q_gbs = 8 * elems / (quant_us * 1e-6) / 1e9
         seq = "hipExtLaunchKernel start/stop events of each launch, median of 40 single-batch steps in sequence on " \
-              "one stream (the --pipeline 1 context of profiles/*_kernel_stats_pipeline1.csv)"
+              "one stream over %d input batches, x evicted from the Infinity Cache (384 MiB sweep) before each " \
+              "timed pass" % len(plans)
         kern = {"quant": {"us": round(quant_us, 2), "alg_bytes": 8 * elems, "GB/s": round(q_gbs, 1),
-                          "frac": round(q_gbs / HBM_PEAK_GBS, 4), "timing": seq}}
+                          "frac": round(q_gbs / HBM_PEAK_GBS, 4), "timing": seq,
+                          "us_in_sequence": round(kt_seq["quant"], 2)}}
         gbs = 4 * elems / (kt["stats"] * 1e-6) / 1e9
         kern["stats"] = {"us": round(kt["stats"], 2), "alg_bytes": 4 * elems, "GB/s": round(gbs, 1),
-                         "frac": round(gbs / HBM_PEAK_GBS, 4), "timing": seq}
-        kern["morph_finalize"] = {"us": round(kt["morph_finalize"], 2), "bound": "latency (per-image chain)",
-                                  "timing": seq}
+                         "frac": round(gbs / HBM_PEAK_GBS, 4), "timing": seq,
+                         "us_in_sequence": round(kt_seq["stats"], 2)}
+        kern["morph_finalize"] = {"us": round(kt_seq["morph_finalize"], 2), "bound": "latency (per-image chain)",
+                                  "timing": "events around the launch, in sequence"}
         out = {
             "metric": HOOK_METRIC,
             "value": round(value, 2),
@@ -737,7 +797,14 @@ def main():
                                    "quant/dequant; YOLOv8 network excluded (see e2e)" % (name, B, grid, mapper),
                        "global_batch": world * B, "grid_size": grid, "mapper": mapper,
                        "parallelism": "dp%d" % world, "hip_graph": use_graph,
-                       "batches_in_flight": depth, "schedule": args.schedule if args.schedule == "streams" else "split (look-ahead %d)" % args.lookahead, "input_batches": len(plans),
+                       "batches_in_flight": 4 if args.schedule == "staged" else depth,
+                       "schedule": {"staged": "staged: pass 1 (i) + pass 2 (i-3) | pass A (i-1) | pass B (i-2), "
+                                              "3 streams, events%s" % (", morph on %d CUs" % args.morph_cus
+                                                                       if args.morph_cus else ""),
+                                    "streams": "streams: %d batch chains on %d streams, one HIP graph each"
+                                               % (depth, depth),
+                                    "split": "split (look-ahead %d)" % args.lookahead}[args.schedule],
+                       "input_batches": len(plans),
                        "latency_ms_single_batch": round(latency_ms, 4),
                        "host_enqueue_us_per_step": round(t_enq / args.steps * 1e6, 1)},
             # north star: the whole fused complexity + quant path,

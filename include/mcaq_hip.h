@@ -41,7 +41,7 @@ typedef void* hipEvent_t;
 extern "C" {
 #endif
 
-#define MCAQ_ABI_VERSION 9
+#define MCAQ_ABI_VERSION 10
 /* largest dynamic LDS request of the morph kernel (gfx950: 160 KiB per CU) */
 #define MCAQ_MORPH_LDS_LIMIT 163840
 
@@ -151,8 +151,41 @@ typedef struct {
   int bits_lo, nbits;  /* supported widths [bits_lo, bits_lo + nbits - 1] */
   int compat_tile_h, compat_tile_w; /* >0: spatial_quantize tile indexing */
   int unit_begin;      /* set by the launcher */
+  int stats_cover_x;   /* 1: xmin / xmax are the min / max of this x itself (the
+                          batch statistics of pass 1, all-reduced or not):
+                          channels whose statistics are finite hold only
+                          finite x and take the shorter arithmetic; 0: any x
+                          (frozen / external statistics) */
 } mcaq_quant_scale;
 int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream);
+
+/* mcaq_morph_finalize with a choice of passes: bit 0 = pass A (the per-image
+ * pixel chain -> tile partials, + the channel min/max workgroups), bit 1 =
+ * pass B (tile chain: phi, complexity MLP, bilateral, mapper, soft mask).
+ * Pass B reads what pass A wrote (tile_tmp). */
+int mcaq_morph_pass(const mcaq_morph_scale* scales, int nscales,
+                    const mcaq_finalize_scale* fscales, int nfscales, int passes, hipStream_t stream);
+
+/* ---- software-pipelined hook path (batched throughput) --------------------
+ * Step i issues pass 1 of batch i and pass 2 of batch i-3 on stream 0, morph
+ * pass A (+ channel min/max) of batch i-1 on stream 1, pass B of batch i-2 on
+ * stream 2; each piece waits only for the previous step's piece it reads
+ * (events), so the morphology runs beside the HBM passes.  Callers cycle >= 4
+ * buffer sets.  cu_masks: NULL, or 3 x mask_words CU bit masks (stream 0, 1,
+ * 2; an all-zero mask = no mask).  hold_a: leave stream 1's end-of-step event
+ * unrecorded until mcaq_pipeline_release_a (the caller enqueues the RCCL
+ * min/max all-reduce of batch i-1 on mcaq_pipeline_stream(p, 1) first). */
+typedef struct mcaq_pipeline mcaq_pipeline;
+int mcaq_pipeline_create(const uint32_t* cu_masks, int mask_words, mcaq_pipeline** out);
+int mcaq_pipeline_destroy(mcaq_pipeline* p);
+void* mcaq_pipeline_stream(mcaq_pipeline* p, int k);
+int mcaq_pipeline_step(mcaq_pipeline* p,
+                       const mcaq_stats_scale* st, int nst,
+                       const mcaq_morph_scale* ma, int nma, const mcaq_finalize_scale* fz, int nfz,
+                       const mcaq_morph_scale* mb, int nmb,
+                       const mcaq_quant_scale* qs, int nq, int hold_a);
+int mcaq_pipeline_release_a(mcaq_pipeline* p);
+int mcaq_pipeline_join(mcaq_pipeline* p, hipStream_t stream);
 
 /* Measurement: the calling thread's NEXT mcaq_stats / mcaq_quant launch is
  * issued through hipExtLaunchKernel with these start/stop events (either may

@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libmcaq_hip.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -39,7 +39,8 @@ class MorphScale(ctypes.Structure):
 class QuantScale(ctypes.Structure):
     _fields_ = [("x", P), ("y", P), ("bits", P), ("m", P), ("mt", P), ("xmin", P), ("xmax", P),
                 ("B", I), ("C", I), ("H", I), ("W", I), ("ht", I), ("wt", I),
-                ("bits_lo", I), ("nbits", I), ("compat_tile_h", I), ("compat_tile_w", I), ("unit_begin", I)]
+                ("bits_lo", I), ("nbits", I), ("compat_tile_h", I), ("compat_tile_w", I), ("unit_begin", I),
+                ("stats_cover_x", I)]
 
 
 class QatScale(ctypes.Structure):
@@ -57,7 +58,9 @@ F_BIN_OTSU, F_NO_EULER, F_CANNY_LEGACY = 256, 512, 1024
 EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats", "mcaq_stats_units",
            "mcaq_finalize", "mcaq_morph", "mcaq_morph_finalize", "mcaq_morph_scratch_bytes", "mcaq_quant",
            "mcaq_qat_forward", "mcaq_qat_backward", "mcaq_qat_work_floats", "mcaq_ema_stats",
-           "mcaq_nms", "mcaq_nms_work_floats", "mcaq_time_next_launch", "mcaq_time_launch")
+           "mcaq_nms", "mcaq_nms_work_floats", "mcaq_time_next_launch", "mcaq_time_launch",
+           "mcaq_morph_pass", "mcaq_pipeline_create", "mcaq_pipeline_destroy", "mcaq_pipeline_stream",
+           "mcaq_pipeline_step", "mcaq_pipeline_release_a", "mcaq_pipeline_join")
 
 _LIB = None
 
@@ -78,6 +81,22 @@ def _declare(lib):
         f.argtypes = [ctypes.POINTER(st), I, P]
     lib.mcaq_morph_finalize.restype = I
     lib.mcaq_morph_finalize.argtypes = [ctypes.POINTER(MorphScale), I, ctypes.POINTER(FinalizeScale), I, P]
+    lib.mcaq_morph_pass.restype = I
+    lib.mcaq_morph_pass.argtypes = [ctypes.POINTER(MorphScale), I, ctypes.POINTER(FinalizeScale), I, I, P]
+    lib.mcaq_pipeline_create.restype = I
+    lib.mcaq_pipeline_create.argtypes = [ctypes.POINTER(ctypes.c_uint32), I, ctypes.POINTER(P)]
+    lib.mcaq_pipeline_destroy.restype = I
+    lib.mcaq_pipeline_destroy.argtypes = [P]
+    lib.mcaq_pipeline_stream.restype = P
+    lib.mcaq_pipeline_stream.argtypes = [P, I]
+    lib.mcaq_pipeline_step.restype = I
+    lib.mcaq_pipeline_step.argtypes = [P, ctypes.POINTER(StatsScale), I, ctypes.POINTER(MorphScale), I,
+                                       ctypes.POINTER(FinalizeScale), I, ctypes.POINTER(MorphScale), I,
+                                       ctypes.POINTER(QuantScale), I, I]
+    lib.mcaq_pipeline_release_a.restype = I
+    lib.mcaq_pipeline_release_a.argtypes = [P]
+    lib.mcaq_pipeline_join.restype = I
+    lib.mcaq_pipeline_join.argtypes = [P, P]
     lib.mcaq_stats_units.restype = I
     lib.mcaq_stats_units.argtypes = [I, I, I, I]
     lib.mcaq_morph_scratch_bytes.restype = ctypes.c_size_t

@@ -747,10 +747,13 @@ _ARRIVE = {}
 def _arrive_counters(B, device):
     """Zeroed per-image arrival counters for the in-launch fold of
     mcaq_qat_backward (the kernel leaves them zeroed): one persistent int32
-    buffer per device, created outside graph capture.  While a HIP graph is
-    being captured and none exists yet, a fresh zeroed buffer is captured
-    (its fill node re-zeroes it on each replay)."""
-    key = torch.device(device)
+    buffer per (device, stream), created outside graph capture.  Launches on
+    one stream run one after another, and each leaves the counters zeroed, so
+    the scales of a step may share a buffer; launches on different streams
+    (batches in flight) get different buffers.  While a HIP graph is being
+    captured and none exists yet, a fresh zeroed buffer is captured (its fill
+    node re-zeroes it on each replay)."""
+    key = (torch.device(device), torch.cuda.current_stream(device).cuda_stream)
     buf = _ARRIVE.get(key)
     if buf is not None and buf.numel() >= B:
         return buf
@@ -1006,7 +1009,8 @@ class SpatialAdaptiveQuantization(nn.Module):
         _, ht, wt = bits.shape
         want_m = self.smooth_transitions and self.soft_mask is not None
         absmean = torch.empty(B, H, W, device=xf.device) if want_m else None
-        if bool(self.stats_frozen) and self.running_min is not None:
+        frozen = bool(self.stats_frozen) and self.running_min is not None
+        if frozen:
             xmin = self.running_min.reshape(-1).float().expand(C).contiguous() \
                 if self.running_min.numel() == 1 else self.running_min.reshape(-1).float().contiguous()
             xmax = self.running_max.reshape(-1).float().expand(C).contiguous() \
@@ -1021,6 +1025,7 @@ class SpatialAdaptiveQuantization(nn.Module):
         q.x, q.y, q.bits, q.mt, q.xmin, q.xmax = _p(xf), _p(y), _p(bits), _p(mt), _p(xmin), _p(xmax)
         q.B, q.C, q.H, q.W, q.ht, q.wt = B, C, H, W, ht, wt
         q.bits_lo, q.nbits = 2, 7
+        q.stats_cover_x = 0 if frozen else 1
         abi.check(abi.lib().mcaq_quant(ctypes.byref(q), 1, _stream()), "mcaq_quant")
         return y
 

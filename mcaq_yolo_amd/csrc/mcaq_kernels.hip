@@ -600,6 +600,7 @@ __global__ MCAQ_QUANT_LB void mcaq_quant_kernel(QuantArgs a) {
   __shared__ float4 qt[QSLICE * QMAXBITS];   // scale, zp, 1/scale
   __shared__ float mts[QMAXNT];
   __shared__ float mq[256];
+  __shared__ int qany[QSLICE];               // channel needs quant_dequant_any
   const int unit = blockIdx.x;
   int si = 0;
   while (si + 1 < a.nscales && unit >= a.s[si + 1].unit_begin) ++si;
@@ -672,13 +673,16 @@ __global__ MCAQ_QUANT_LB void mcaq_quant_kernel(QuantArgs a) {
     }
   }
   if (tid < ntab) {
-    const QParam q = qparam(tmn, tmx, S.bits_lo + (tid - (tid / NB) * NB));
+    const int kq = tid - (tid / NB) * NB;
+    const QParam q = qparam(tmn, tmx, S.bits_lo + kq);
     qt[tid] = make_float4(q.scale, q.zp, q.rs, 0.0f);
+    if (kq == 0) qany[tid / NB] = (!S.stats_cover_x || stats_need_any(tmn, tmx)) ? 1 : 0;
   }
   for (int i = tid + 256; i < ntab; i += 256) {   // > 256 entries: continuous bit ranges
     const int c = i / NB, k = i - (i / NB) * NB;
     const QParam q = qparam(S.xmin[c0 + c], S.xmax[c0 + c], S.bits_lo + k);
     qt[i] = make_float4(q.scale, q.zp, q.rs, 0.0f);
+    if (k == 0) qany[c] = (!S.stats_cover_x || stats_need_any(S.xmin[c0 + c], S.xmax[c0 + c])) ? 1 : 0;
   }
   if (mt0) mts[tid] = mtv;
   if (kMtLds && S.mt)
@@ -718,6 +722,12 @@ __global__ MCAQ_QUANT_LB void mcaq_quant_kernel(QuantArgs a) {
     for (int k = 0; k < 4; ++k) mv[k] = mq[lane * 4 + k];
   }
   if (ncw <= 0) return;
+  // one wave-uniform choice for the wave's channels: the short arithmetic
+  // unless a channel's statistics do not cover x or are not finite
+  int anyc = 0;
+#pragma unroll
+  for (int c = 0; c < QCW; ++c) anyc |= c < ncw ? qany[cw + c] : 0;
+  const bool any_x = __builtin_amdgcn_readfirstlane(anyc) != 0;
 #pragma unroll
   for (int c = 0; c < QCW; ++c) {
     if (c >= ncw) break;
@@ -727,7 +737,7 @@ __global__ MCAQ_QUANT_LB void mcaq_quant_kernel(QuantArgs a) {
       const float4 sz = qt[(cw + c) * NB + kb[k]];
       QParam q;
       q.scale = sz.x; q.zp = sz.y; q.rs = sz.z; q.qmin = qlo[k]; q.qmax = qhi[k];
-      float d = quant_dequant(v[c][k], q);
+      float d = any_x ? quant_dequant_any(v[c][k], q) : quant_dequant(v[c][k], q);
       if (has_m) d = d * mv[k];
       o[k] = d;
     }
@@ -907,15 +917,30 @@ int mcaq_morph(const mcaq_morph_scale* scales, int nscales, hipStream_t stream) 
   return mcaq_morph_finalize(scales, nscales, nullptr, 0, stream);
 }
 
-int mcaq_morph_finalize(const mcaq_morph_scale* scales, int nscales, const mcaq_finalize_scale* fscales,
-                        int nfscales, hipStream_t stream) {
+}  // extern "C"
+
+// Launch configuration of the morph passes for a set of scales (validated):
+// pass A (+ the channel min/max workgroups riding along) and pass B.
+struct MorphLaunch {
+  MorphArgs a;
+  FinalizeArgs fa;
+  int any_phi, any_tiles;
+  int grid_a, var_a;       // pass A grid (0: no pass A) and kernel variant (2 * legacy + lds mode)
+  size_t dyn_a;
+  int grid_b, wlds;        // pass B grid (0: no pass B), weights staged in LDS
+  size_t dyn_b;
+};
+
+static int morph_launch_config(const mcaq_morph_scale* scales, int nscales, const mcaq_finalize_scale* fscales,
+                               int nfscales, MorphLaunch& L) {
   if (nscales < 1 || nscales > 3) return (int)hipErrorInvalidValue;
-  FinalizeArgs fa{};
+  FinalizeArgs& fa = L.fa;
+  fa = FinalizeArgs{};
   if (nfscales > 0) {
     const int fe = finalize_args(fscales, nfscales, fa);
     if (fe) return fe;
   }
-  MorphArgs a;
+  MorphArgs& a = L.a;
   int blocks = 0, any_phi = 0, any_tiles = 0;
   for (int i = 0; i < nscales; ++i) {
     memcpy(&a.s[i], &scales[i], sizeof(MorphScale));
@@ -935,11 +960,9 @@ int mcaq_morph_finalize(const mcaq_morph_scale* scales, int nscales, const mcaq_
     any_tiles |= tf != 0;
   }
   a.nscales = nscales;
-  if (!any_phi && fa.nblocks > 0) {   // nothing to ride along with
-    hipLaunchKernelGGL(mcaq_finalize_kernel, dim3(fa.nblocks), dim3(256), 0, stream, fa);
-    const hipError_t fe = hipGetLastError();
-    if (fe != hipSuccess) return (int)fe;
-  }
+  L.any_phi = any_phi;
+  L.any_tiles = any_tiles;
+  L.grid_a = 0; L.grid_b = 0; L.dyn_a = 0; L.dyn_b = 0; L.var_a = 0; L.wlds = 0;
   if (any_phi) {
     int mode, stride; size_t dyn;
     int e = morph_plan(a.s, nscales, &mode, &stride, &dyn);
@@ -965,28 +988,13 @@ int mcaq_morph_finalize(const mcaq_morph_scale* scales, int nscales, const mcaq_
 #ifdef MCAQ_MORPH_EXCL
     dyn = (size_t)limit;   // A/B: one pass-A workgroup per CU (no streaming waves beside it)
 #endif
-    const int grid = wg + fa.nblocks;
     // canny_impl='legacy' is an analyzer option: one value for every scale of a launch
     const int leg = (a.s[0].flags & F_CANNY_LEGACY) ? 1 : 0;
     for (int i = 1; i < nscales; ++i)
       if (((a.s[i].flags & F_CANNY_LEGACY) ? 1 : 0) != leg) return (int)hipErrorInvalidValue;
-    static int set[4] = {0, 0, 0, 0};  // raise the dynamic LDS limit once (not during graph capture)
-    const int var = 2 * leg + mode;
-    const void* fns[4] = {(const void*)mcaq_morph_kernel<false>, (const void*)mcaq_morph_kernel<true>,
-                          (const void*)mcaq_morph_kernel<false, true>, (const void*)mcaq_morph_kernel<true, true>};
-    if ((int)dyn > set[var]) {
-      hipError_t ae = hipFuncSetAttribute(fns[var], hipFuncAttributeMaxDynamicSharedMemorySize, limit);
-      if (ae != hipSuccess) return (int)ae;
-      set[var] = limit;
-    }
-    switch (var) {
-      case 0: hipLaunchKernelGGL((mcaq_morph_kernel<false>), dim3(grid), dim3(MORPH_THREADS), dyn, stream, a, fa); break;
-      case 1: hipLaunchKernelGGL((mcaq_morph_kernel<true>), dim3(grid), dim3(MORPH_THREADS), dyn, stream, a, fa); break;
-      case 2: hipLaunchKernelGGL((mcaq_morph_kernel<false, true>), dim3(grid), dim3(MORPH_THREADS), dyn, stream, a, fa); break;
-      default: hipLaunchKernelGGL((mcaq_morph_kernel<true, true>), dim3(grid), dim3(MORPH_THREADS), dyn, stream, a, fa); break;
-    }
-    hipError_t le = hipGetLastError();
-    if (le != hipSuccess) return (int)le;
+    L.grid_a = wg + fa.nblocks;
+    L.var_a = 2 * leg + mode;
+    L.dyn_a = dyn;
   }
   if (any_tiles) {
     // pass B packing: the waves an image needs for one MLP block of MLP_TPW
@@ -1008,21 +1016,74 @@ int mcaq_morph_finalize(const mcaq_morph_scale* scales, int nscales, const mcaq_
     const int lim = MCAQ_MORPH_LDS_LIMIT - 1024;
     if (per + TILES_SCRATCH_BYTES > lim) return (int)hipErrorInvalidValue;
     // stage the weight blobs in LDS when they fit beside the tile arrays and the MLP scratch
-    const int wlds = per + TILES_SCRATCH_BYTES + weights_lds_bytes() <= lim;
+    L.wlds = per + TILES_SCRATCH_BYTES + weights_lds_bytes() <= lim;
 #ifdef MCAQ_TILES_EXCL
-    const size_t tdyn = (size_t)lim;   // A/B: one pass-B workgroup per CU (no streaming waves beside it)
+    L.dyn_b = (size_t)lim;   // A/B: one pass-B workgroup per CU (no streaming waves beside it)
 #else
-    const size_t tdyn = (size_t)per + TILES_SCRATCH_BYTES + (wlds ? weights_lds_bytes() : 0);
+    L.dyn_b = (size_t)per + TILES_SCRATCH_BYTES + (L.wlds ? weights_lds_bytes() : 0);
 #endif
+    L.grid_b = twg;
+  }
+  return 0;
+}
+
+// passes: bit 0 = pass A (+ channel min/max workgroups), bit 1 = pass B
+static int morph_launch(const MorphLaunch& L, int passes, hipStream_t stream) {
+  const MorphArgs& a = L.a;
+  const FinalizeArgs& fa = L.fa;
+  if ((passes & 1) && !L.any_phi && fa.nblocks > 0) {   // nothing to ride along with
+    hipLaunchKernelGGL(mcaq_finalize_kernel, dim3(fa.nblocks), dim3(256), 0, stream, fa);
+    const hipError_t fe = hipGetLastError();
+    if (fe != hipSuccess) return (int)fe;
+  }
+  if ((passes & 1) && L.grid_a > 0) {
+    const int limit = morph_lds_budget();
+    static int set[4] = {0, 0, 0, 0};  // raise the dynamic LDS limit once (not during graph capture)
+    const int var = L.var_a;
+    const void* fns[4] = {(const void*)mcaq_morph_kernel<false>, (const void*)mcaq_morph_kernel<true>,
+                          (const void*)mcaq_morph_kernel<false, true>, (const void*)mcaq_morph_kernel<true, true>};
+    if ((int)L.dyn_a > set[var]) {
+      hipError_t ae = hipFuncSetAttribute(fns[var], hipFuncAttributeMaxDynamicSharedMemorySize, limit);
+      if (ae != hipSuccess) return (int)ae;
+      set[var] = limit;
+    }
+    const dim3 g(L.grid_a), t(MORPH_THREADS);
+    switch (var) {
+      case 0: hipLaunchKernelGGL((mcaq_morph_kernel<false>), g, t, L.dyn_a, stream, a, fa); break;
+      case 1: hipLaunchKernelGGL((mcaq_morph_kernel<true>), g, t, L.dyn_a, stream, a, fa); break;
+      case 2: hipLaunchKernelGGL((mcaq_morph_kernel<false, true>), g, t, L.dyn_a, stream, a, fa); break;
+      default: hipLaunchKernelGGL((mcaq_morph_kernel<true, true>), g, t, L.dyn_a, stream, a, fa); break;
+    }
+    hipError_t le = hipGetLastError();
+    if (le != hipSuccess) return (int)le;
+  }
+  if ((passes & 2) && L.grid_b > 0) {
+    const int lim = MCAQ_MORPH_LDS_LIMIT - 1024;
     static int set_tiles = 0;
-    if ((int)tdyn > set_tiles) {
+    if ((int)L.dyn_b > set_tiles) {
       hipError_t ae = hipFuncSetAttribute((const void*)mcaq_tiles_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
       if (ae != hipSuccess) return (int)ae;
       set_tiles = lim;
     }
-    hipLaunchKernelGGL(mcaq_tiles_kernel, dim3(twg), dim3(TILES_THREADS), tdyn, stream, a, wlds);
+    hipLaunchKernelGGL(mcaq_tiles_kernel, dim3(L.grid_b), dim3(TILES_THREADS), L.dyn_b, stream, a, L.wlds);
   }
   return (int)hipGetLastError();
+}
+
+extern "C" {
+
+int mcaq_morph_finalize(const mcaq_morph_scale* scales, int nscales, const mcaq_finalize_scale* fscales,
+                        int nfscales, hipStream_t stream) {
+  return mcaq_morph_pass(scales, nscales, fscales, nfscales, 3, stream);
+}
+
+int mcaq_morph_pass(const mcaq_morph_scale* scales, int nscales, const mcaq_finalize_scale* fscales,
+                    int nfscales, int passes, hipStream_t stream) {
+  if (passes < 1 || passes > 3) return (int)hipErrorInvalidValue;
+  MorphLaunch L;
+  const int e = morph_launch_config(scales, nscales, fscales, nfscales, L);
+  if (e) return e;
+  return morph_launch(L, passes, stream);
 }
 
 int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream) {
@@ -1082,6 +1143,7 @@ int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream) 
 
 #include "mcaq_qat.h"
 #include "mcaq_nms.h"
+#include "mcaq_pipeline.h"
 
 // C++-linkage drop-in for the reference's declaration (include/mcaq_hip.h):
 // same name, argument list and void return as MCAQPlugin.cpp:15-23.  An

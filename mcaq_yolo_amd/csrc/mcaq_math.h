@@ -110,6 +110,22 @@ MCAQ_HD float log2_ref(float a) {
 }
 
 MCAQ_HD float fmax_(float a, float b) { return a > b ? a : b; }
+// NaN-propagating max / ReLU (torch.amax, torch.relu keep NaN)
+MCAQ_HD float fmaxp(float a, float b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_elementwise_maximum(a, b);
+#else
+  return a != a ? a : (b != b ? b : (a > b ? a : b));
+#endif
+}
+MCAQ_HD float fminp(float a, float b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_elementwise_minimum(a, b);
+#else
+  return a != a ? a : (b != b ? b : (a < b ? a : b));
+#endif
+}
+MCAQ_HD float relu_nan(float x) { return (x > 0.0f || x != x) ? x : 0.0f; }
 MCAQ_HD float fmin_(float a, float b) { return a < b ? a : b; }
 MCAQ_HD float clampf_(float v, float lo, float hi) { return v < lo ? lo : (v > hi ? hi : v); }
 MCAQ_HD int imin_(int a, int b) { return a < b ? a : b; }
@@ -220,6 +236,8 @@ MCAQ_HD QParam qparam(float xmin, float xmax, int b) {
 // it can differ - subnormal x, the sign of a zero quotient - the quotient
 // is < 1e-20 and the + zp that follows (0 or |zp| >= 6e-8) absorbs it, so
 // quant_dequant is unchanged.  MCAQ_TRUE_DIV builds keep the IEEE division.
+// x / s, correctly rounded, for |x rs| < FLT_MAX (finite statistics cover x:
+// the fast path of pass 2)
 MCAQ_HD float div_by(float x, float s, float rs) {
 #ifdef MCAQ_TRUE_DIV
   (void)rs;
@@ -227,6 +245,29 @@ MCAQ_HD float div_by(float x, float s, float rs) {
 #else
   const float q0 = x * rs;
   const float r = fmaf(-q0, s, x);
+  return fmaf(r, rs, q0);
+#endif
+}
+
+// The same for any x: when q0 = x rs is +-inf (x = +-inf, or an overflowing
+// product) the remainder fma(-q0, s, x) is NaN; it is mapped to -FLT_MAX
+// (v_med3_f32 returns its smallest operand when one is NaN), so the result is
+// q0 = +-inf = x / s, as the reference's IEEE division gives.  NaN x stays NaN
+// (q0 is NaN).  Finite remainders pass unchanged.
+MCAQ_HD float rem_finite(float r) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_fmed3f(r, -3.40282347e38f, 3.40282347e38f);
+#else
+  return r != r ? -3.40282347e38f : clampf_(r, -3.40282347e38f, 3.40282347e38f);
+#endif
+}
+MCAQ_HD float div_by_any(float x, float s, float rs) {
+#ifdef MCAQ_TRUE_DIV
+  (void)rs;
+  return x / s;
+#else
+  const float q0 = x * rs;
+  const float r = rem_finite(fmaf(-q0, s, x));
   return fmaf(r, rs, q0);
 #endif
 }
@@ -241,11 +282,40 @@ MCAQ_HD float clamp_med3(float x, float lo, float hi) {
 #endif
 }
 
-// y = (clamp(rint(x/s + zp)) - zp) * s     (quantization.py:597-600)
+// torch.clamp(v, lo, hi) (lo <= hi): +-inf clamp to a bound, NaN stays NaN.
+// On the device v_maximum_f32 / v_minimum_f32 (gfx950, NaN-propagating); a
+// single v_med3_f32 would turn NaN into lo (it returns min3 when an operand
+// is NaN).
+MCAQ_HD float clamp_nan(float x, float lo, float hi) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_elementwise_minimum(__builtin_elementwise_maximum(x, lo), hi);
+#else
+  return clampf_(x, lo, hi);
+#endif
+}
+
+// y = (clamp(rint(x/s + zp)) - zp) * s     (quantization.py:597-600), for
+// finite x with |x / s| well inside the fp32 range: the fast path, taken by
+// the kernels where the channel's own batch min/max are finite and < 1e20
+// in magnitude (then every x of the channel is, and |x rs| < 3e30)
 MCAQ_HD float quant_dequant(float x, const QParam& q) {
   float t = div_by(x, q.scale, q.rs) + q.zp;
   float r = clamp_med3(rintf(t), q.qmin, q.qmax);
   return (r - q.zp) * q.scale;
+}
+
+// the same for any x, with the reference's non-finite behaviour: x = +-inf
+// -> the qmax / qmin level, x = NaN -> NaN (2 more VALU operations)
+MCAQ_HD float quant_dequant_any(float x, const QParam& q) {
+  float t = div_by_any(x, q.scale, q.rs) + q.zp;
+  float r = clamp_nan(rintf(t), q.qmin, q.qmax);
+  return (r - q.zp) * q.scale;
+}
+
+// true when a channel with batch statistics [xmin, xmax] needs
+// quant_dequant_any (a NaN or +-inf in the channel, or huge magnitudes)
+MCAQ_HD bool stats_need_any(float xmin, float xmax) {
+  return !(fabsf(xmin) < 1e20f && fabsf(xmax) < 1e20f);
 }
 
 }  // namespace mcaq

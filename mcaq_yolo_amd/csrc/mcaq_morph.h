@@ -178,12 +178,13 @@ MCAQ_HD void carve_shared(char* base, Shared& sh) {
 // ---- reductions (exact operations only: min / max / integer / exact double) --
 MCAQ_HD void block_minmax(const Ctx& ctx, Shared& sh, float lmn, float lmx, float& mn, float& mx) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  for (int o = 32; o > 0; o >>= 1) { lmn = fminf(lmn, __shfl_xor(lmn, o, 64)); lmx = fmaxf(lmx, __shfl_xor(lmx, o, 64)); }
+  // NaN-propagating, as torch.amin / amax
+  for (int o = 32; o > 0; o >>= 1) { lmn = fminp(lmn, __shfl_xor(lmn, o, 64)); lmx = fmaxp(lmx, __shfl_xor(lmx, o, 64)); }
   const int nw = ctx.nthr >> 6;
   if ((ctx.tid & 63) == 0) { sh.redf[ctx.tid >> 6] = lmn; sh.redf[32 + (ctx.tid >> 6)] = lmx; }
   MSYNC();
   mn = sh.redf[0]; mx = sh.redf[32];
-  for (int w = 1; w < nw; ++w) { mn = fminf(mn, sh.redf[w]); mx = fmaxf(mx, sh.redf[32 + w]); }
+  for (int w = 1; w < nw; ++w) { mn = fminp(mn, sh.redf[w]); mx = fmaxp(mx, sh.redf[32 + w]); }
   MSYNC();
 #else
   (void)ctx; (void)sh;
@@ -731,10 +732,10 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, P
       for (int i = 0; i < GPT; ++i) {
         const int p = ctx.tid + i * ctx.nthr;
         gv[i] = gin[p < P ? p : 0];
-        if (p < P) { lmn = fmin_(lmn, gv[i]); lmx = fmax_(lmx, gv[i]); }
+        if (p < P) { lmn = fminp(lmn, gv[i]); lmx = fmaxp(lmx, gv[i]); }
       }
     } else {
-      MFOR(p, P) { const float v = gin[p]; pl.G[p] = v; lmn = fmin_(lmn, v); lmx = fmax_(lmx, v); }
+      MFOR(p, P) { const float v = gin[p]; pl.G[p] = v; lmn = fminp(lmn, v); lmx = fmaxp(lmx, v); }
     }
     float mn, mx;
     block_minmax(ctx, sh, lmn, lmx, mn, mx);
@@ -868,7 +869,7 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, P
         const int h2 = imin_(imax_(h - dy1, 0), Hc - 1), w2 = imin_(imax_(w - dx1, 0), Wc - 1);
         const float nms = (m >= pl.Bf[h1 * Wc + w1] && m >= pl.Bf[h2 * Wc + w2]) ? m : 0.0f;
         pl.A[p] = nms;
-        lmn = fmin_(lmn, nms); lmx = fmax_(lmx, nms);
+        lmn = fminp(lmn, nms); lmx = fmaxp(lmx, nms);
       }
       float mn, mx;
       block_minmax(ctx, sh, lmn, lmx, mn, mx);
@@ -1640,7 +1641,7 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
         a = (s / (float)(hb - ha)) / (float)(wb - wa);
       }
       tiles[t * TILE_FLOATS + T_ACT] = a;
-      lmx = fmax_(lmx, a);
+      lmx = fmaxp(lmx, a);          // torch.amax: a NaN activation makes the image's max NaN
     }
     const float amax = block_max(ctx, sh, lmx);
     MSTAMP(31);
@@ -1681,7 +1682,7 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
       float l0 = Pm[SM_B2 + 0], l1 = Pm[SM_B2 + 1];
 #pragma unroll
       for (int ic = 0; ic < 8; ++ic) {
-        const float hv = fmax_(hid[ic] + Pm[SM_B1 + ic], 0.0f);
+        const float hv = relu_nan(hid[ic] + Pm[SM_B1 + ic]);
         l0 = fmaf(Pm[SM_W2 + ic], hv, l0);
         l1 = fmaf(Pm[SM_W2 + 8 + ic], hv, l1);
       }

@@ -224,8 +224,8 @@ __global__ __launch_bounds__(256, MCAQ_QAT_MINW) void mcaq_qat_kernel(QatArgs a)
       L.qmin = (float)(-(1 << (lo - 1))); L.qmax = (float)((1 << (lo - 1)) - 1);
       Hq.scale = zh.x; Hq.zp = zh.y; Hq.rs = zh.z;
       Hq.qmin = (float)(-(1 << (hi - 1))); Hq.qmax = (float)((1 << (hi - 1)) - 1);
-      const float ql = quant_dequant(v[k], L);
-      const float qh = quant_dequant(v[k], Hq);
+      const float ql = quant_dequant_any(v[k], L);
+      const float qh = quant_dequant_any(v[k], Hq);
       const float xq = omf[k] * ql + fu[k] * qh;      // two rounded products, one rounded add
       if (!kBwd) {
         o[k] = has_m ? xq * mv[k] : xq;

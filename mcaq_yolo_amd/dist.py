@@ -35,19 +35,24 @@ class GroupBatchNorm1d(nn.BatchNorm1d):
     def from_bn(cls, bn, process_group):
         new = cls(bn.num_features, bn.eps, bn.momentum, bn.affine, bn.track_running_stats, process_group)
         new.load_state_dict(bn.state_dict())
+        new.train(bn.training)      # a swapped-in eval-mode layer stays in eval mode
         return new.to(bn.weight.device if bn.affine else bn.running_mean.device)
 
     def forward(self, x):
         if not self.training or self.process_group is None:
             return super().forward(x)
         from torch.distributed.nn.functional import all_reduce
+        # two passes, as a single-process BatchNorm1d over the global batch:
+        # the global mean first (sum and count in one all-reduce), then the
+        # sum of squared deviations from it - no E[x^2] - mean^2 cancellation
+        # when |mean| >> std
         n_local = torch.tensor([float(x.shape[0])], device=x.device, dtype=x.dtype)
-        stats = torch.cat([x.sum(dim=0), (x * x).sum(dim=0), n_local])
-        stats = all_reduce(stats, group=self.process_group)
         C = x.shape[1]
-        n = stats[2 * C]
-        mean = stats[:C] / n
-        var = (stats[C:2 * C] / n - mean * mean).clamp(min=0.0)
+        s1 = all_reduce(torch.cat([x.sum(dim=0), n_local]), group=self.process_group)
+        n = s1[C]
+        mean = s1[:C] / n
+        d = x - mean
+        var = all_reduce((d * d).sum(dim=0), group=self.process_group) / n
         if self.track_running_stats:
             with torch.no_grad():
                 self.num_batches_tracked += 1
@@ -55,7 +60,7 @@ class GroupBatchNorm1d(nn.BatchNorm1d):
                 unbiased = var.detach() * (n / (n - 1).clamp(min=1.0))
                 self.running_mean.mul_(1 - m).add_(m * mean.detach())
                 self.running_var.mul_(1 - m).add_(m * unbiased)
-        y = (x - mean) / torch.sqrt(var + self.eps)
+        y = d / torch.sqrt(var + self.eps)
         return y * self.weight + self.bias if self.affine else y
 
 
@@ -75,20 +80,27 @@ def sync_mapper_batchnorm(mapper, process_group):
 
 def allreduce_gradients(params, process_group, average=True):
     """Average the gradients of `params` over the group with ONE collective:
-    flatten into a single bucket, all_reduce, copy back (None grads count as
-    zeros and stay None)."""
+    every parameter that requires grad goes into a single flat bucket in the
+    order given (a None grad contributes zeros), so every rank reduces
+    buffers of the same length and layout even when ranks disagree on which
+    grads are None; afterwards every such parameter holds the averaged
+    gradient (as DDP leaves it)."""
     import torch.distributed as dist
-    ps = [p for p in params if p.grad is not None]
+    ps = [p for p in params if p.requires_grad]
     if not ps:
         return
-    flat = torch.cat([p.grad.reshape(-1) for p in ps])
+    flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in ps])
     dist.all_reduce(flat, group=process_group)
     if average:
         flat /= dist.get_world_size(process_group)
     o = 0
     for p in ps:
         n = p.numel()
-        p.grad.copy_(flat[o:o + n].view_as(p.grad))
+        g = flat[o:o + n].view_as(p)
+        if p.grad is None:
+            p.grad = g.clone()
+        else:
+            p.grad.copy_(g)
         o += n
 
 

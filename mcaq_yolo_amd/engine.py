@@ -11,7 +11,12 @@ HIP stream:
 
 All buffers of a `HookPlan` are allocated once, so `HookPlan.run` only
 enqueues launches and can be captured into a HIP graph (torch.cuda.CUDAGraph).
-There is no CPU path: non-CUDA tensors or a missing library raise.
+`HookPipeline` runs many batches software-pipelined over three streams
+(mcaq_pipeline.h) for batched throughput.
+
+This module is the HIP path only: non-CUDA tensors or a missing library
+raise here.  CPU tensors take the pure-PyTorch path (fallback.py), which the
+modules in core.py / hooks.py dispatch to, as the reference does.
 """
 import ctypes
 
@@ -227,6 +232,8 @@ class HookPlan:
                 s.xmin, s.xmax = _p(b["xmin"]), _p(b["xmax"])
                 s.B, s.C, s.H, s.W, s.ht, s.wt = g.B, g.C, g.H, g.W, g.ht, g.wt
                 s.bits_lo, s.nbits = lo_b, nb
+                # batch statistics of this x (pass 1 + finalize, all-reduced or not)
+                s.stats_cover_x = 1 if (minmax is None or minmax[i] is None) else 0
             self._qs = qs
         self._n = n
 
@@ -285,3 +292,90 @@ def sync_channel_minmax(bufs, process_group):
         b["xmin"].copy_(-vec[o:o + C])
         b["xmax"].copy_(vec[o + C:o + 2 * C])
         o += 2 * C
+
+
+class HookPipeline:
+    """Software-pipelined hook path for batched throughput (mcaq_pipeline.h):
+    step i runs pass 1 of batch i and pass 2 of batch i-3 on a streaming
+    stream, morph pass A (+ channel min/max) of batch i-1 and pass B of batch
+    i-2 on two more streams, each piece waiting only for the previous step's
+    piece it reads.  `plans` (>= 4 prepared HookPlans of the same shapes) are
+    cycled: batch j uses plans[j % len(plans)].  `submit()` issues one step
+    and returns the plan whose pass 2 it issued (None while filling).
+    cu_masks: None, or three lists of CU indices (streaming, pass A, pass B)
+    to pin the streams' workgroups to (hipExtStreamCreateWithCUMask).
+    process_group (N > 1): the channel min/max of batch i-1 is all-reduced on
+    the pass-A stream right after its finalize, before pass 2 reads it."""
+
+    def __init__(self, plans, cu_masks=None, process_group=None, ncus=256):
+        if len(plans) < 4:
+            raise ValueError("the 4-stage pipeline needs >= 4 independent HookPlans")
+        self.plans = list(plans)
+        self.lib = plans[0].lib
+        self.pg = process_group
+        h = ctypes.c_void_p()
+        if cu_masks is None:
+            abi.check(self.lib.mcaq_pipeline_create(None, 0, ctypes.byref(h)), "mcaq_pipeline_create")
+        else:
+            words = (ncus + 31) // 32
+            arr = (ctypes.c_uint32 * (3 * words))()
+            for k, cus in enumerate(cu_masks):
+                for c in (cus or ()):
+                    arr[k * words + c // 32] |= 1 << (c % 32)
+            abi.check(self.lib.mcaq_pipeline_create(arr, words, ctypes.byref(h)), "mcaq_pipeline_create")
+        self.handle = h
+        self.i = 0
+        self.last = None      # drain(): no new batches from this index on
+        self._a_stream = None
+        if process_group is not None:
+            self._a_stream = torch.cuda.ExternalStream(self.lib.mcaq_pipeline_stream(h, 1))
+
+    def _piece(self, j, attr):
+        if j < 0 or (self.last is not None and j >= self.last):
+            return None, 0
+        p = self.plans[j % len(self.plans)]
+        v = getattr(p, attr)
+        return v, (p._n if v is not None else 0)
+
+    def submit(self):
+        i = self.i
+        st, nst = self._piece(i, "_st")
+        ma, nma = self._piece(i - 1, "_mo")
+        fz, nfz = self._piece(i - 1, "_fz")
+        mb, nmb = self._piece(i - 2, "_mo")
+        qs, nq = self._piece(i - 3, "_qs")
+        hold = 1 if (self.pg is not None and nma > 0 and fz is not None) else 0
+        abi.check(self.lib.mcaq_pipeline_step(self.handle, st, nst, ma, nma, fz, nfz, mb, nmb, qs, nq, hold),
+                  "mcaq_pipeline_step")
+        if hold:
+            with torch.cuda.stream(self._a_stream):
+                sync_channel_minmax(self.plans[(i - 1) % len(self.plans)].bufs, self.pg)
+            abi.check(self.lib.mcaq_pipeline_release_a(self.handle), "mcaq_pipeline_release_a")
+        self.i += 1
+        return self.plans[(i - 3) % len(self.plans)] if qs is not None else None
+
+    def drain(self):
+        """Finish every submitted batch: three more steps that start no new
+        batch.  Returns the plans completed by them, in batch order."""
+        self.last = self.i
+        done = []
+        for _ in range(3):
+            p = self.submit()
+            if p is not None:
+                done.append(p)
+        return done
+
+    def join(self, stream=None):
+        """Order `stream` (default: the current one) after everything submitted."""
+        abi.check(self.lib.mcaq_pipeline_join(self.handle, _stream_handle(stream)), "mcaq_pipeline_join")
+
+    def close(self):
+        if self.handle is not None:
+            self.lib.mcaq_pipeline_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

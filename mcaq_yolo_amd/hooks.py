@@ -118,6 +118,10 @@ class MCAQHooks(nn.Module):
         continuous bits from the train-mode mapper, fractional-bit STE
         quantizer on the HIP kernels) and every CPU tensor (the pure-PyTorch
         path, BASELINE config 1)."""
+        B = feat.shape[0]
+        bt = self.batch_total
+        if not self.training and not feat.is_cuda and bt is not None and bt > B:
+            return self._run_scale_shard_cpu(layer_idx, feat, state)
         complexity = self.complexity_analyzer(feat)
         if self.normalize_complexity:
             B = complexity.shape[0]
@@ -133,6 +137,41 @@ class MCAQHooks(nn.Module):
         state.setdefault("aux", []).append({"layer": layer_idx, "complexity": complexity,
                                             "bit_map": bit_map, "features_q": feat_q})
         return feat_q if quantize else None
+
+    def _run_scale_shard_cpu(self, layer_idx, feat, state):
+        """A batch shard on the pure-PyTorch path (inference / calibration).
+        Several CPU ATen results depend on a value's position in the WHOLE
+        batch, not only on the image: the fractal regression's outer sums
+        over the scales (a tile's global column picks the vectorised or the
+        row_sum order, morphology.py:614-620), the vector-body / scalar-tail
+        split of SLEEF log / log2 / exp and the softmax thread partition
+        (SURVEY App. A.1, A.6), and oneDNN vs MKL for single-image 3x3
+        convolutions (A.2).  So the shard runs on a tensor of the global batch
+        shape: rows batch_offset .. batch_offset + B - 1 hold this shard's
+        images and the other rows repeat them (which leaves the shard's
+        channel min/max unchanged; the process group's all-reduce then makes
+        it global).  The shard's rows of every output are exactly those of
+        the single-process run on the global batch, at world_size x the CPU
+        work of the shard."""
+        B = feat.shape[0]
+        off, bt = self.batch_offset, self.batch_total
+        if not 0 <= off <= bt - B:
+            raise ValueError("batch_offset %d + shard %d exceeds batch_total %d" % (off, B, bt))
+        rows = (torch.arange(bt) - off) % B
+        sub = {"temperature": state.get("temperature", 1.0), "quantize": state.get("quantize", True),
+               "calibrating": state.get("calibrating", False), "aux": []}
+        saved = self.batch_total
+        self.batch_total = None
+        try:
+            out = self._run_scale_modules(layer_idx, feat.index_select(0, rows.to(feat.device)), sub)
+        finally:
+            self.batch_total = saved
+        a = sub["aux"][0]
+        sl = slice(off, off + B)
+        feat_q = a["features_q"][sl] if state.get("quantize", True) else feat
+        state.setdefault("aux", []).append({"layer": layer_idx, "complexity": a["complexity"][sl],
+                                            "bit_map": a["bit_map"][sl], "features_q": feat_q})
+        return feat_q if out is not None else None
 
     def run_scale(self, layer_idx, feat, state):
         if self.training or not feat.is_cuda:

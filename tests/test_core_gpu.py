@@ -417,3 +417,42 @@ def test_channel_minmax_nonfinite_like_aten(shape):
     rmn, rmx = x.amin(dim=(0, 2, 3)), x.amax(dim=(0, 2, 3))
     torch.testing.assert_close(mn.cpu(), rmn, rtol=0, atol=0, equal_nan=True)
     torch.testing.assert_close(mx.cpu(), rmx, rtol=0, atol=0, equal_nan=True)
+
+
+@pytest.mark.parametrize("smooth", [False, True])
+def test_frozen_quant_nonfinite_like_reference(smooth):
+    """Pass 2 with frozen calibration statistics on inputs holding +-inf and
+    NaN: +inf -> the qmax level, -inf -> the qmin level, NaN stays NaN, as the
+    reference's torch.round / torch.clamp quantizer (quantization.py:592-600)
+    gives -- the CPU module (the reference algorithm), the HIP module and the
+    extension op agree bit for bit, NaN positions included."""
+    from mcaq_yolo_amd import mcaq_cuda_ops
+    from mcaq_yolo_amd.core import SpatialAdaptiveQuantization
+    g = torch.Generator().manual_seed(11)
+    B, C, H, W = 2, 12, 16, 16
+    x = torch.randn(B, C, H, W, generator=g)
+    rmin, rmax = x.amin(dim=(0, 2, 3), keepdim=True), x.amax(dim=(0, 2, 3), keepdim=True)
+    x[0, 1, 3, 4] = float("inf")
+    x[1, 2, 5, 6] = float("-inf")
+    x[0, 3, 7, 8] = float("nan")
+    x[1, 4, :, 0] = float("inf")
+    x[0, 5, 0, :] = float("nan")
+    bit_map = torch.randint(2, 9, (B, 4, 4), generator=g).float()
+    outs = {}
+    for dev in ("cpu", DEV):
+        q = SpatialAdaptiveQuantization(smooth_transitions=smooth)
+        if smooth:
+            q.soft_mask.load_state_dict(_sd("soft_mask."))
+        q = q.to(dev).eval()
+        q.running_min, q.running_max = rmin.to(dev), rmax.to(dev)
+        q.freeze_calibration()
+        with torch.no_grad():
+            outs[dev] = q(x.to(dev), bit_map.to(dev)).cpu()
+    torch.testing.assert_close(outs[DEV], outs["cpu"], rtol=0, atol=0, equal_nan=True)
+    y = outs[DEV]
+    assert torch.isnan(y[0, 3, 7, 8]) and torch.isnan(y[0, 5, 0]).all()
+    assert torch.isfinite(y[0, 1, 3, 4]) and torch.isfinite(y[1, 2, 5, 6]) and torch.isfinite(y[1, 4, :, 0]).all()
+    if not smooth:
+        # extension op, same statistics
+        y2 = mcaq_cuda_ops.spatial_quantize(x.to(DEV).contiguous(), bit_map.to(DEV), rmin.to(DEV), rmax.to(DEV), 4, 4)
+        torch.testing.assert_close(y2.cpu(), outs["cpu"], rtol=0, atol=0, equal_nan=True)

@@ -172,3 +172,53 @@ def test_mapper_sync_batchnorm_and_grad_allreduce_two_ranks():
             np.testing.assert_allclose(rg[k], v, rtol=1e-4, atol=1e-4 * gmax, err_msg=k)
         for k, v in bufs.items():
             np.testing.assert_allclose(rbuf[k], v, rtol=1e-5, atol=1e-6, err_msg=k)
+
+
+# ---------------------------------------------------------------------------
+def _none_grad_worker(rank, world):
+    from mcaq_yolo_amd import dist as mdist
+    a = torch.nn.Parameter(torch.zeros(3))
+    b = torch.nn.Parameter(torch.zeros(5))
+    c = torch.nn.Parameter(torch.zeros(2))
+    # rank 0 leaves b's grad None, rank 1 leaves a's: the buckets still line up
+    if rank == 0:
+        a.grad, c.grad = torch.full((3,), 1.0), torch.full((2,), 10.0)
+    else:
+        b.grad, c.grad = torch.full((5,), 2.0), torch.full((2,), 20.0)
+    mdist.allreduce_gradients([a, b, c], dist.group.WORLD)
+    return a.grad.numpy(), b.grad.numpy(), c.grad.numpy()
+
+
+def test_allreduce_gradients_ranks_disagree_on_none():
+    res = _run("_none_grad_worker")
+    for r in range(2):
+        a, b, c = res[r]
+        assert np.array_equal(a, np.full(3, 0.5, np.float32))
+        assert np.array_equal(b, np.full(5, 1.0, np.float32))
+        assert np.array_equal(c, np.full(2, 15.0, np.float32))
+
+
+def _bn_large_mean_worker(rank, world):
+    from mcaq_yolo_amd.dist import GroupBatchNorm1d
+    x = _bn_large_mean_case()
+    n = x.shape[0] // world
+    bn = GroupBatchNorm1d(x.shape[1], process_group=dist.group.WORLD).train()
+    y = bn(x[rank * n:(rank + 1) * n])
+    return y.detach().numpy(), bn.running_var.numpy()
+
+
+def _bn_large_mean_case():
+    g = torch.Generator().manual_seed(5)
+    return 1e4 + 0.5 * torch.randn(64, 6, generator=g)     # |mean| >> std
+
+
+def test_group_batchnorm_large_mean_two_ranks():
+    """|mean| = 1e4, std 0.5: E[x^2] - mean^2 in fp32 loses the variance; the
+    two-pass global statistics match the single-process BatchNorm1d."""
+    x = _bn_large_mean_case()
+    bn = torch.nn.BatchNorm1d(6).train()
+    y = bn(x).detach().numpy()
+    res = _run("_bn_large_mean_worker")
+    for r in range(2):
+        np.testing.assert_allclose(res[r][0], y[r * 32:(r + 1) * 32], rtol=1e-3, atol=2e-3)
+        np.testing.assert_allclose(res[r][1], bn.running_var.numpy(), rtol=1e-3)
