@@ -550,7 +550,7 @@ class SplitRunner:
 
 
 class StagedRunner:
-    """--schedule staged (default): the software-pipelined step of
+    """--schedule staged: the software-pipelined step of
     engine.HookPipeline - pass 1 of batch i + pass 2 of batch i-3 on one
     stream, morph pass A of batch i-1 and pass B of batch i-2 on two more;
     one native call per step.  After the first 3 (filling) steps every step
@@ -639,10 +639,11 @@ def main():
     ap.add_argument("--channels-last", action="store_true", help="--e2e: NHWC network (experiment)")
     ap.add_argument("--find", action="store_true", help="--e2e: MIOpen Find (torch.backends.cudnn.benchmark)")
     ap.add_argument("--eager", action="store_true", help="no HIP graphs")
-    ap.add_argument("--schedule", choices=("staged", "streams", "split"), default="staged",
-                    help="staged: software pipeline, pass 1 (i) + pass 2 (i-3) | pass A (i-1) | pass B (i-2) "
-                         "on three streams (default); streams: --pipeline batches in flight, one HIP graph "
-                         "each; split: HBM passes on one stream, morphology on two (SplitRunner, eager, N = 1)")
+    ap.add_argument("--schedule", choices=("staged", "streams", "split"), default="streams",
+                    help="streams (default): --pipeline batches in flight, one HIP graph each; staged: software "
+                         "pipeline, pass 1 (i) + pass 2 (i-3) | pass A (i-1) | pass B (i-2) on three streams "
+                         "(eager, host-enqueue bound: 77 vs 64 us per step, profiles/r03_base); split: HBM "
+                         "passes on one stream, morphology on two (SplitRunner, eager, N = 1)")
     ap.add_argument("--morph-cus", type=int, default=0,
                     help="--schedule staged: pin the morph streams to this many CUs (0: no CU masks)")
     ap.add_argument("--lookahead", type=int, default=3, help="--schedule split: batches of look-ahead")
