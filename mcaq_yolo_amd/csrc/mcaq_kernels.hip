@@ -576,8 +576,11 @@ struct QuantArgs {
   int units_total;
 };
 
-constexpr int QSLICE = 32;     // channels per unit (8 per wave)
-constexpr int QCW = 8;         // channels per wave
+#ifndef MCAQ_QSLICE
+#define MCAQ_QSLICE 32
+#endif
+constexpr int QSLICE = MCAQ_QSLICE;   // channels per unit (8 per wave)
+constexpr int QCW = QSLICE / 4;       // channels per wave
 constexpr int QMAXBITS = 15;   // max entries per channel in the LDS table
 constexpr int QMAXNT = 1024;   // max tiles per image whose m values are staged in LDS (more: read from L2)
 
@@ -595,10 +598,26 @@ constexpr int QMAXNT = 1024;   // max tiles per image whose m values are staged 
 #define MCAQ_QUANT_MINW 6
 #endif
 #define MCAQ_QUANT_LB __launch_bounds__(256, MCAQ_QUANT_MINW)
-template <bool kVec, bool kNTL, bool kNTS, bool kMtLds>
+// m(p) source of a pass-2 instantiation (compile time, so that no load sits
+// behind a runtime branch: the compiler's wait counts then stay exact and the
+// x rows stay in flight through the prologue -- with the loads behind
+// branches it waited for every x row before the first barrier, r03)
+enum : int { QM_NONE = 0, QM_MT_LDS = 1, QM_MT_L2 = 2, QM_PLANE = 3 };
+
+// pixel -> tile row / column: the reference's nearest source index
+// floor(o * fp32(in / out)), clamped (exact for the o >> k and o >> 1 special
+// cases of ATen's nearest_idx too: in / out is then a power of two), or the
+// spatial_quantize contract o / tile, clamped; branch-free
+__device__ __forceinline__ int q_tile_of(int o, int in, float sc, int compat_tile) {
+  const int ns = imin_((int)floorf((float)o * sc), in - 1);
+  const int ct = imin_(o / imax_(compat_tile, 1), in - 1);
+  return compat_tile > 0 ? ct : ns;
+}
+
+template <bool kVec, bool kNTL, bool kNTS, int kM, bool kBig>
 __global__ MCAQ_QUANT_LB void mcaq_quant_kernel(QuantArgs a) {
   __shared__ float4 qt[QSLICE * QMAXBITS];   // scale, zp, 1/scale
-  __shared__ float mts[QMAXNT];
+  __shared__ float mts[kM == QM_MT_LDS ? QMAXNT : 1];
   __shared__ float mq[256];
   __shared__ int qany[QSLICE];               // channel needs quant_dequant_any
   const int unit = blockIdx.x;
@@ -617,76 +636,73 @@ __global__ MCAQ_QUANT_LB void mcaq_quant_kernel(QuantArgs a) {
   const int nc = imin_(QSLICE, S.C - c0);
   const int NB = S.nbits;
   const int NTq = S.ht * S.wt;
-  // Issue order: the small operands (this thread's first table entry's
-  // min/max, first m(tile) value, the lanes' tile bits), then the x rows;
-  // the table and the staged m values are built while x is in flight (one
-  // memory round trip before compute instead of three in sequence).
   const int ntab = nc * NB;
-  float tmn = 0.0f, tmx = 0.0f;
-  if (tid < ntab) { const int c = tid / NB; tmn = S.xmin[c0 + c]; tmx = S.xmax[c0 + c]; }
-  const bool mt0 = kMtLds && S.mt && tid < NTq;
-  const float mtv = mt0 ? S.mt[(size_t)b * NTq + tid] : 0.0f;
-  // tile grids with more than QMAXNT tiles read their m values through L2
-  const float* mtab = kMtLds ? mts : (S.mt ? S.mt + (size_t)b * NTq : nullptr);
-
+  // ---- 1. small operands, unconditional (clamped indices): this thread's
+  // table entry's min / max, its m(tile) value, the lane's 4 tile bits (and
+  // m(p) values when the plane is given)
+  const int tc = imin_(tid / NB, nc - 1);
+  const float tmn = S.xmin[c0 + tc], tmx = S.xmax[c0 + tc];
+  float mtv = 0.0f;
+  if (kM == QM_MT_LDS) mtv = S.mt[(size_t)b * NTq + imin_(tid, NTq - 1)];
   const int q0 = chunk * 256 + lane * 4;
-  const NearestMap nmh = nearest_map(S.ht, S.H), nmw = nearest_map(S.wt, S.W);
+  const float sch = (float)S.ht / (float)S.H, scw = (float)S.wt / (float)S.W;
   bool pv[4];
   float bv[4], mv[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int p = imin_(q0 + k, HW - 1);
     pv[k] = q0 + k < HW;
-    const int h = p / S.W, w = p - (p / S.W) * S.W;
-    int th, tw;
-    if (S.compat_tile_h > 0) {   // spatial_quantize contract: h / tile_h, clamped
-      th = imin_(h / S.compat_tile_h, S.ht - 1);
-      tw = imin_(w / S.compat_tile_w, S.wt - 1);
-    } else {                     // PyTorch path: nearest upsample of the bit map
-      th = nearest_apply(nmh, h);
-      tw = nearest_apply(nmw, w);
-    }
+    const int h = p / S.W, w = p - h * S.W;
+    const int th = q_tile_of(h, S.ht, sch, S.compat_tile_h);
+    const int tw = q_tile_of(w, S.wt, scw, S.compat_tile_w);
     bv[k] = S.bits[((size_t)b * S.ht + th) * S.wt + tw];
-    mv[k] = (S.m && !S.mt) ? S.m[(size_t)b * HW + p] : 1.0f;
+    mv[k] = kM == QM_PLANE ? S.m[(size_t)b * HW + p] : 1.0f;
   }
-  const bool has_m = S.m != nullptr || S.mt != nullptr;
+  // ---- 2. the x rows (8 x 16 B per lane), in flight through the prologue
   const int cw = wv * QCW;                 // first channel of this wave in the slice
   const int ncw = imin_(QCW, nc - cw);     // may be <= 0 for a short last slice
-  const size_t rowbase = ((size_t)b * S.C + c0 + cw) * HW;
+  const size_t rowbase = ((size_t)b * S.C + c0 + imax_(imin_(cw, nc - 1), 0)) * HW;
   const float* xb = S.x + rowbase;
   float* yb = S.y + rowbase;
   float v[QCW][4];
   const int qa = pv[0] ? q0 : 0;
-  if (ncw > 0) {
 #pragma unroll
-    for (int c = 0; c < QCW; ++c) {
-      const float* row = xb + (size_t)(c < ncw ? c : 0) * HW;
-      if (kVec) {
-        typedef float f4v __attribute__((ext_vector_type(4)));
-        const f4v t = kNTL ? __builtin_nontemporal_load(reinterpret_cast<const f4v*>(row + qa))
-                          : *reinterpret_cast<const f4v*>(row + qa);
-        v[c][0] = t.x; v[c][1] = t.y; v[c][2] = t.z; v[c][3] = t.w;
-      } else {
+  for (int c = 0; c < QCW; ++c) {
+    const float* row = xb + (size_t)imin_(c, imax_(ncw - 1, 0)) * HW;
+    if (kVec) {
+      typedef float f4v __attribute__((ext_vector_type(4)));
+      const f4v t = kNTL ? __builtin_nontemporal_load(reinterpret_cast<const f4v*>(row + qa))
+                        : *reinterpret_cast<const f4v*>(row + qa);
+      v[c][0] = t.x; v[c][1] = t.y; v[c][2] = t.z; v[c][3] = t.w;
+    } else {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[c][k] = row[imin_(q0 + k, HW - 1)];
-      }
+      for (int k = 0; k < 4; ++k) v[c][k] = row[imin_(q0 + k, HW - 1)];
     }
   }
-  if (tid < ntab) {
-    const int kq = tid - (tid / NB) * NB;
+  // ---- 3. scale / zero-point table and staged m values (no global loads
+  // behind a branch on the common path; > 256 entries only in kBig builds)
+  {
+    // every thread computes an entry (tid >= ntab: an unused slot of the
+    // 480-entry table), so the min / max loads have an unconditional use and
+    // are not sunk into a branch behind the x rows
+    const int kq = imin_(tid - tc * NB, QMAXBITS - 1);
     const QParam q = qparam(tmn, tmx, S.bits_lo + kq);
     qt[tid] = make_float4(q.scale, q.zp, q.rs, 0.0f);
-    if (kq == 0) qany[tid / NB] = (!S.stats_cover_x || stats_need_any(tmn, tmx)) ? 1 : 0;
+    if (kq == 0) qany[tc] = (!S.stats_cover_x || stats_need_any(tmn, tmx)) ? 1 : 0;
   }
-  for (int i = tid + 256; i < ntab; i += 256) {   // > 256 entries: continuous bit ranges
-    const int c = i / NB, k = i - (i / NB) * NB;
-    const QParam q = qparam(S.xmin[c0 + c], S.xmax[c0 + c], S.bits_lo + k);
-    qt[i] = make_float4(q.scale, q.zp, q.rs, 0.0f);
-    if (k == 0) qany[c] = (!S.stats_cover_x || stats_need_any(S.xmin[c0 + c], S.xmax[c0 + c])) ? 1 : 0;
+  if (kBig) {
+    for (int i = tid + 256; i < ntab; i += 256) {   // > 256 entries: continuous bit ranges
+      const int c = i / NB, k = i - (i / NB) * NB;
+      const QParam q = qparam(S.xmin[c0 + c], S.xmax[c0 + c], S.bits_lo + k);
+      qt[i] = make_float4(q.scale, q.zp, q.rs, 0.0f);
+      if (k == 0) qany[c] = (!S.stats_cover_x || stats_need_any(S.xmin[c0 + c], S.xmax[c0 + c])) ? 1 : 0;
+    }
   }
-  if (mt0) mts[tid] = mtv;
-  if (kMtLds && S.mt)
-    for (int i = tid + 256; i < NTq; i += 256) mts[i] = S.mt[(size_t)b * NTq + i];
+  if (kM == QM_MT_LDS) {
+    if (tid < NTq) mts[tid] = mtv;
+    if (kBig)
+      for (int i = tid + 256; i < NTq; i += 256) mts[i] = S.mt[(size_t)b * NTq + i];
+  }
   int kb[4];
   float qlo[4], qhi[4];
 #pragma unroll
@@ -697,21 +713,26 @@ __global__ MCAQ_QUANT_LB void mcaq_quant_kernel(QuantArgs a) {
     qhi[k] = (float)((1 << (bb - 1)) - 1);
   }
   __syncthreads();   // qt, mts ready
-  if (S.mt) {
+#ifndef MCAQ_PROBE_Q_NOM
+  if (kM == QM_MT_LDS || kM == QM_MT_L2) {
+#else
+  if (false) {
+#endif
     // m(p) = 5x5 Gaussian (replicate pad) of the nearest-upsampled tile values,
     // taps row-major from 0 - the m plane LearnedSoftMask produces
     // (quantization.py:235-238), generated here instead of read from HBM.
     // Wave w computes pixel w of every lane's quad; the quads meet in LDS.
+    const float* mtab = kM == QM_MT_LDS ? mts : S.mt + (size_t)b * NTq;
     {
       const int p = imin_(q0 + wv, HW - 1);
-      const int h = p / S.W, w = p - (p / S.W) * S.W;
+      const int h = p / S.W, w = p - h * S.W;
       int cs[5];
 #pragma unroll
-      for (int j = 0; j < 5; ++j) cs[j] = nearest_apply(nmw, imin_(imax_(w + j - 2, 0), S.W - 1));
+      for (int j = 0; j < 5; ++j) cs[j] = q_tile_of(imin_(imax_(w + j - 2, 0), S.W - 1), S.wt, scw, 0);
       float acc = 0.0f;
 #pragma unroll
       for (int i = 0; i < 5; ++i) {
-        const int rb = nearest_apply(nmh, imin_(imax_(h + i - 2, 0), S.H - 1)) * S.wt;
+        const int rb = q_tile_of(imin_(imax_(h + i - 2, 0), S.H - 1), S.ht, sch, 0) * S.wt;
 #pragma unroll
         for (int j = 0; j < 5; ++j) acc = fmaf(bits_as_float(k_smooth5_bits[i * 5 + j]), mtab[rb + cs[j]], acc);
       }
@@ -737,8 +758,12 @@ __global__ MCAQ_QUANT_LB void mcaq_quant_kernel(QuantArgs a) {
       const float4 sz = qt[(cw + c) * NB + kb[k]];
       QParam q;
       q.scale = sz.x; q.zp = sz.y; q.rs = sz.z; q.qmin = qlo[k]; q.qmax = qhi[k];
+#ifdef MCAQ_PROBE_Q_NOQ
+      float d = v[c][k] * q.scale;
+#else
       float d = any_x ? quant_dequant_any(v[c][k], q) : quant_dequant(v[c][k], q);
-      if (has_m) d = d * mv[k];
+#endif
+      if (kM != QM_NONE) d = d * mv[k];
       o[k] = d;
     }
     float* orow = yb + (size_t)c * HW;
@@ -1120,22 +1145,44 @@ int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream) 
     xbytes += (size_t)scales[i].B * scales[i].C * scales[i].H * scales[i].W * sizeof(float);
   const int nt = xbytes > ((size_t)256 << 20) ? 3 : 1;
 #endif
-  bool mt_lds = true;
-  for (int i = 0; i < nscales; ++i) mt_lds = mt_lds && (!scales[i].mt || scales[i].ht * scales[i].wt <= QMAXNT);
+  // m(p) source: one kind for every scale of the launch (the hook always
+  // passes m(tile) values or nothing; the reference op a plane or nothing)
+  int kind = -1;
+  bool big = false;
+  for (int i = 0; i < nscales; ++i) {
+    const mcaq_quant_scale& q = scales[i];
+    const int NT = q.ht * q.wt;
+    const int k = q.mt ? (NT <= QMAXNT ? QM_MT_LDS : QM_MT_L2) : (q.m ? QM_PLANE : QM_NONE);
+    if (kind >= 0 && k != kind) {
+      // mixed kinds: one launch per scale
+      for (int j = 0; j < nscales; ++j) {
+        const int e = mcaq_quant(&scales[j], 1, stream);
+        if (e) return e;
+      }
+      return 0;
+    }
+    kind = k;
+    big = big || imin_(QSLICE, q.C) * q.nbits > 256 || (k == QM_MT_LDS && NT > 256);
+  }
   const dim3 g(units), t(256);
-  if (!mt_lds) {
-    if (vec) launch_k((mcaq_quant_kernel<true, false, true, false>), g, t, 0, stream, a);
-    else launch_k((mcaq_quant_kernel<false, false, false, false>), g, t, 0, stream, a);
-  } else if (!vec)
-    launch_k((mcaq_quant_kernel<false, false, false, true>), g, t, 0, stream, a);
-  else if (nt == 3)
-    launch_k((mcaq_quant_kernel<true, true, true, true>), g, t, 0, stream, a);
-  else if (nt == 2)
-    launch_k((mcaq_quant_kernel<true, true, false, true>), g, t, 0, stream, a);
-  else if (nt == 1)
-    launch_k((mcaq_quant_kernel<true, false, true, true>), g, t, 0, stream, a);
-  else
-    launch_k((mcaq_quant_kernel<true, false, false, true>), g, t, 0, stream, a);
+#define MCAQ_Q_LAUNCH(V, L, S_)                                                                              \
+  do {                                                                                                       \
+    switch (kind * 2 + (big ? 1 : 0)) {                                                                      \
+      case 0: launch_k((mcaq_quant_kernel<V, L, S_, QM_NONE, false>), g, t, 0, stream, a); break;           \
+      case 1: launch_k((mcaq_quant_kernel<V, L, S_, QM_NONE, true>), g, t, 0, stream, a); break;            \
+      case 2: launch_k((mcaq_quant_kernel<V, L, S_, QM_MT_LDS, false>), g, t, 0, stream, a); break;         \
+      case 3: launch_k((mcaq_quant_kernel<V, L, S_, QM_MT_LDS, true>), g, t, 0, stream, a); break;          \
+      case 4: case 5: launch_k((mcaq_quant_kernel<V, L, S_, QM_MT_L2, true>), g, t, 0, stream, a); break;  \
+      case 6: launch_k((mcaq_quant_kernel<V, L, S_, QM_PLANE, false>), g, t, 0, stream, a); break;          \
+      default: launch_k((mcaq_quant_kernel<V, L, S_, QM_PLANE, true>), g, t, 0, stream, a); break;          \
+    }                                                                                                        \
+  } while (0)
+  if (!vec) MCAQ_Q_LAUNCH(false, false, false);
+  else if (nt == 3) MCAQ_Q_LAUNCH(true, true, true);
+  else if (nt == 1) MCAQ_Q_LAUNCH(true, false, true);
+  else if (nt == 2) MCAQ_Q_LAUNCH(true, true, false);
+  else MCAQ_Q_LAUNCH(true, false, false);
+#undef MCAQ_Q_LAUNCH
   return (int)hipGetLastError();
 }
 
