@@ -41,7 +41,7 @@ typedef void* hipEvent_t;
 extern "C" {
 #endif
 
-#define MCAQ_ABI_VERSION 10
+#define MCAQ_ABI_VERSION 11
 /* largest dynamic LDS request of the morph kernel (gfx950: 160 KiB per CU) */
 #define MCAQ_MORPH_LDS_LIMIT 163840
 
@@ -248,6 +248,62 @@ int mcaq_ema_stats(const float* batch_min, const float* batch_max, float* runnin
 int mcaq_nms(const float* pred, int B, int no, int N, int nc, float conf_thres, double iou_thres, int max_det,
              int max_nms, float max_wh, int agnostic, float* out, int* counts, float* work, hipStream_t stream);
 size_t mcaq_nms_work_floats(int B, int N, int max_det);
+
+/* ---- train-mode (QAT) tile networks: fused forward / backward ------------
+ * Replace the autograd glue of the train-mode hook (DESIGN s.8): the bit
+ * mapper with batch-statistics BatchNorm (bit_allocation.py:218-280,
+ * 120-130), the analyzer head (complexity MLP + bilateral + clamp,
+ * morphology.py:81-97, 309-354, 959-968) and the soft-mask net
+ * (quantization.py:213-239).  Parameters are the modules' own fp32 tensors
+ * (torch layouts); gradients come back as one flat vector in the modules'
+ * parameters() order.  gpart: per-workgroup partial sums (sizes below). */
+typedef struct {
+  const float *w1, *b1, *g1, *be1;   /* Linear(3,32), BatchNorm1d(32) */
+  float *rm1, *rv1;                  /* running mean / var (updated by the forward) */
+  long long* nbt1;                   /* num_batches_tracked, or NULL */
+  const float *w2, *b2, *g2, *be2;   /* Linear(32,64), BatchNorm1d(64) */
+  float *rm2, *rv2;
+  long long* nbt2;
+  const float *w3, *b3, *g3, *be3;   /* Linear(64,32), BatchNorm1d(32) */
+  float *rm3, *rv3;
+  long long* nbt3;
+  const float *w4, *b4;              /* Linear(32,1) */
+} mcaq_mapper_params;
+typedef struct {
+  const float *w1, *b1, *g1, *be1;   /* Linear(8,64), LayerNorm(64) */
+  const float *w2, *b2, *g2, *be2;   /* Linear(64,32), LayerNorm(32) */
+  const float *w3, *b3;              /* Linear(32,1) */
+} mcaq_cmlp_params;
+typedef struct {
+  const float *w1, *b1;              /* Conv2d(2,8,3,pad 1) */
+  const float *w2, *b2;              /* Conv2d(8,2,1) */
+} mcaq_smask_params;
+
+/* bits (n) = train-mode mapper of c (n): 4 launches; work keeps the
+ * activations and batch statistics for the backward (temperature <= 0:
+ * none; round_bits: straight-through round; update_stats: BN running stats
+ * with `momentum`, num_batches_tracked += 1) */
+size_t mcaq_mapper_work_floats(int n);
+int mcaq_mapper_train_forward(const mcaq_mapper_params* P, const float* c, int n, float min_bits, float max_bits,
+                              float temperature, float momentum, int round_bits, int update_stats, float* bits,
+                              float* work, hipStream_t stream);
+/* gc (n), gparams (4609: mapping_network parameters() order); 5 launches */
+size_t mcaq_mapper_gpart_floats(int n);
+int mcaq_mapper_train_backward(const mcaq_mapper_params* P, const float* c, int n, const float* gbits,
+                               float min_bits, float max_bits, float temperature, float* work, float* gc,
+                               float* gparams, float* gpart, hipStream_t stream);
+/* analyzer head: gC (B, ht, wt) -> gcraw (B, ht, wt) work, gparams (2881:
+ * complexity_mlp parameters() order); phi (B*ht*wt, 8), craw = the MLP output
+ * before the bilateral; 3 launches */
+size_t mcaq_head_gpart_floats(int n);
+int mcaq_head_train_backward(const mcaq_cmlp_params* P, const float* phi, const float* craw, const float* gC, int B,
+                             int ht, int wt, float* gcraw, float* gparams, float* gpart, hipStream_t stream);
+/* soft mask: gm (B, H, W) -> gbits (B, ht, wt) (accumulate != 0: added),
+ * gparams (170: net parameters() order); 2 launches */
+size_t mcaq_smask_gpart_floats(int B);
+int mcaq_smask_train_backward(const mcaq_smask_params* P, const float* bits, const float* absmean, const float* gm,
+                              int B, int H, int W, int ht, int wt, float* gbits, int accumulate, float* gparams,
+                              float* gpart, hipStream_t stream);
 
 int mcaq_abi_version(void);
 

@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libmcaq_hip.so")
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -50,6 +50,20 @@ class QatScale(ctypes.Structure):
                 ("unit_begin", I), ("block_begin", I), ("arrive", P)]
 
 
+class MapperParams(ctypes.Structure):
+    """mcaq_mapper_params: the train-mode mapper's tensors (torch layouts)."""
+    _fields_ = [(n, P) for n in ("w1", "b1", "g1", "be1", "rm1", "rv1", "nbt1", "w2", "b2", "g2", "be2", "rm2",
+                                 "rv2", "nbt2", "w3", "b3", "g3", "be3", "rm3", "rv3", "nbt3", "w4", "b4")]
+
+
+class CmlpParams(ctypes.Structure):
+    _fields_ = [(n, P) for n in ("w1", "b1", "g1", "be1", "w2", "b2", "g2", "be2", "w3", "b3")]
+
+
+class SmaskParams(ctypes.Structure):
+    _fields_ = [(n, P) for n in ("w1", "b1", "w2", "b2")]
+
+
 # morph stage flags (mcaq_morph.h)
 F_PHI, F_CMLP, F_MAPPER, F_SOFTMASK = 1, 2, 4, 8
 F_CONT, F_HAS_T, F_NORM_C, F_MAP_LINEAR = 16, 32, 64, 128
@@ -60,7 +74,10 @@ EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats",
            "mcaq_qat_forward", "mcaq_qat_backward", "mcaq_qat_work_floats", "mcaq_ema_stats",
            "mcaq_nms", "mcaq_nms_work_floats", "mcaq_time_next_launch", "mcaq_time_launch",
            "mcaq_morph_pass", "mcaq_pipeline_create", "mcaq_pipeline_destroy", "mcaq_pipeline_stream",
-           "mcaq_pipeline_step", "mcaq_pipeline_release_a", "mcaq_pipeline_join")
+           "mcaq_pipeline_step", "mcaq_pipeline_release_a", "mcaq_pipeline_join",
+           "mcaq_mapper_work_floats", "mcaq_mapper_train_forward", "mcaq_mapper_gpart_floats",
+           "mcaq_mapper_train_backward", "mcaq_head_gpart_floats", "mcaq_head_train_backward",
+           "mcaq_smask_gpart_floats", "mcaq_smask_train_backward")
 
 _LIB = None
 
@@ -113,6 +130,19 @@ def _declare(lib):
     lib.mcaq_time_next_launch.argtypes = [P, P]
     lib.mcaq_time_launch.restype = I
     lib.mcaq_time_launch.argtypes = [I, P, P]
+    SZ = ctypes.c_size_t
+    for n in ("mcaq_mapper_work_floats", "mcaq_mapper_gpart_floats", "mcaq_head_gpart_floats",
+              "mcaq_smask_gpart_floats"):
+        getattr(lib, n).restype = SZ
+        getattr(lib, n).argtypes = [I]
+    lib.mcaq_mapper_train_forward.restype = I
+    lib.mcaq_mapper_train_forward.argtypes = [ctypes.POINTER(MapperParams), P, I, Fl, Fl, Fl, Fl, I, I, P, P, P]
+    lib.mcaq_mapper_train_backward.restype = I
+    lib.mcaq_mapper_train_backward.argtypes = [ctypes.POINTER(MapperParams), P, I, P, Fl, Fl, Fl, P, P, P, P, P]
+    lib.mcaq_head_train_backward.restype = I
+    lib.mcaq_head_train_backward.argtypes = [ctypes.POINTER(CmlpParams), P, P, P, I, I, I, P, P, P, P]
+    lib.mcaq_smask_train_backward.restype = I
+    lib.mcaq_smask_train_backward.argtypes = [ctypes.POINTER(SmaskParams), P, P, P, I, I, I, I, I, P, I, P, P, P]
     return lib
 
 

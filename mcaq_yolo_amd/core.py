@@ -282,7 +282,7 @@ class MorphologicalComplexityAnalyzer(nn.Module):
         ps = [p for p in self.complexity_mlp.parameters()]
         return self._blob.get(ps, lambda: _pack_cmlp(self.complexity_mlp))
 
-    def _run(self, features, want_c):
+    def _run(self, features, want_c, want_craw=False):
         _need_cuda(features, "features")
         if features.dim() != 4:
             raise ValueError("features must be (B, C, H, W)")
@@ -303,11 +303,15 @@ class MorphologicalComplexityAnalyzer(nn.Module):
             flags |= abi.F_CMLP
             ptrs["cmlp"] = self.cmlp_blob()
             ptrs["c_out"] = torch.empty(B, ht, wt, device=dev)
+            if want_craw:
+                ptrs["cmlp_out"] = torch.empty(B, ht, wt, device=dev)
         scratch = L.mcaq_morph_scratch_bytes(B, ht * T, wt * T, ht, wt)
         if scratch:
             ptrs["gscratch"] = torch.empty(scratch, device=dev, dtype=torch.uint8)
         s = _morph_struct(B, H, W, T, ht, wt, flags, **ptrs)
         abi.check(L.mcaq_morph(ctypes.byref(s), 1, _stream()), "mcaq_morph")
+        if want_craw:
+            return phi, ptrs.get("c_out"), ptrs.get("cmlp_out")
         return phi, ptrs.get("c_out")
 
     @staticmethod
@@ -401,10 +405,16 @@ class MorphologicalComplexityAnalyzer(nn.Module):
             c = self._head(phi)
         elif _wants_grad((), self.complexity_mlp.parameters()):
             # phi is no-grad side information (morph kernel); C is the kernel's
-            # value and its gradient reaches complexity_mlp through the torch
-            # restatement of the MLP + bilateral
-            phi, ck = self._run(features, want_c=True)
-            c = _kernel_value(lambda p: ck, self._head, [phi], list(self.complexity_mlp.parameters()))
+            # value and its gradient reaches complexity_mlp through the fused
+            # head backward (mcaq_head_train_backward) or, FUSED_TRAIN off, the
+            # torch restatement of the MLP + bilateral
+            if FUSED_TRAIN:
+                out = _HeadTrainFn.apply(self, features, *self.complexity_mlp.parameters())
+                phi, c = self._last_phi, out
+                self._last_phi = None
+            else:
+                phi, ck = self._run(features, want_c=True)
+                c = _kernel_value(lambda p: ck, self._head, [phi], list(self.complexity_mlp.parameters()))
         else:
             phi, c = self._run(features, want_c=True)
         if return_detailed:
@@ -557,6 +567,14 @@ class ComplexityToBitMappingNetwork(nn.Module):
         bit_map = (self.min_bits + (self.max_bits - self.min_bits) * h).reshape(B, H, W)
         return _finish_bits(bit_map, self.min_bits, self.max_bits, temperature, return_continuous)
 
+    def _fusable(self):
+        """The fused train-mode kernels take the reference stack with plain
+        BatchNorm1d layers (a process-group BatchNorm, dist.GroupBatchNorm1d,
+        keeps the torch path: its statistics span the ranks)."""
+        net = self.mapping_network
+        return all(type(net[i]) is nn.BatchNorm1d and net[i].track_running_stats and net[i].momentum is not None
+                   and net[i].affine for i in (1, 4, 7))
+
     def mapper_blob(self):
         net = self.mapping_network
         ts = list(net.parameters()) + [net[i].running_mean for i in (1, 4, 7)] + \
@@ -566,6 +584,8 @@ class ComplexityToBitMappingNetwork(nn.Module):
     def forward(self, complexity: torch.Tensor, temperature: Optional[float] = None,
                 return_continuous: bool = False) -> torch.Tensor:
         c = _normalize_complexity_shape(complexity)
+        if self.training and c.is_cuda and FUSED_TRAIN and self._fusable():
+            return _MapperTrainFn.apply(self, c, temperature, return_continuous, *self.mapping_network.parameters())
         if self.training or not c.is_cuda:
             return self._forward_torch(c, temperature, return_continuous)
 
@@ -706,6 +726,8 @@ class _SoftMaskFn(torch.autograd.Function):
         bit_map, absmean = ctx.saved_tensors
         mod = ctx.mod
         params = list(mod.net.parameters())
+        if FUSED_TRAIN:
+            return _smask_backward_fused(ctx, mod, bit_map, absmean, gm, params)
         with torch.enable_grad():
             b = bit_map.detach().requires_grad_(ctx.needs_input_grad[0])
             m = mod._torch_forward(b, absmean)
@@ -715,6 +737,120 @@ class _SoftMaskFn(torch.autograd.Function):
         gb = next(it) if ctx.needs_input_grad[0] else None
         gp = [next(it) if p.requires_grad else None for p in params]
         return (gb, None, None) + tuple(gp)
+
+
+# ---------------------------------------------------------------------------
+# train-mode tile networks on the fused kernels (csrc/mcaq_train.h)
+# ---------------------------------------------------------------------------
+# False: the torch autograd restatement of the analyzer head, the train-mode
+# mapper and the soft-mask backward (the r02 path; A/B and cross-check)
+FUSED_TRAIN = True
+
+
+def _split_flat(flat, params):
+    out, o = [], 0
+    for p in params:
+        n = p.numel()
+        out.append(flat[o:o + n].view_as(p))
+        o += n
+    return out
+
+
+class _HeadTrainFn(torch.autograd.Function):
+    """Analyzer in train mode: phi, C (= clamp(bilateral(MLP(phi)))) and the
+    MLP output from the morph kernel (bit-exact forward); the backward is the
+    fused bilateral adjoint + complexity MLP backward."""
+
+    @staticmethod
+    def forward(ctx, mod, features, *params):
+        phi, c, craw = mod._run(features, want_c=True, want_craw=True)
+        mod._last_phi = phi
+        ctx.mod = mod
+        ctx.save_for_backward(phi, craw, *params)
+        return c
+
+    @staticmethod
+    def backward(ctx, gc):
+        phi, craw = ctx.saved_tensors[:2]
+        params = ctx.saved_tensors[2:]
+        B, ht, wt = craw.shape
+        n = B * ht * wt
+        L = abi.lib()
+        q = abi.CmlpParams(*[_p(p.detach()) for p in params])
+        gcraw = torch.empty(n, device=craw.device)
+        gflat = torch.empty(_CM_SIZE, device=craw.device)
+        gpart = torch.empty(L.mcaq_head_gpart_floats(n), device=craw.device)
+        abi.check(L.mcaq_head_train_backward(ctypes.byref(q), _p(phi), _p(craw), _p(_f32c(gc)), B, ht, wt, _p(gcraw),
+                                             _p(gflat), _p(gpart), _stream()), "mcaq_head_train_backward")
+        return (None, None) + tuple(_split_flat(gflat, params))
+
+
+class _MapperTrainFn(torch.autograd.Function):
+    """ComplexityToBitMappingNetwork in train mode (batch-statistics
+    BatchNorm, running stats updated, straight-through clamp / round) on the
+    fused kernels: 4 forward launches, 5 backward launches."""
+
+    @staticmethod
+    def forward(ctx, mod, c, temperature, return_continuous, *params):
+        net = mod.mapping_network
+        cf = _f32c(c).reshape(-1)
+        n = cf.numel()
+        L = abi.lib()
+        bns = [net[i] for i in (1, 4, 7)]
+        q = abi.MapperParams()
+        for k, t in zip(("w1", "b1", "w2", "b2", "w3", "b3", "w4", "b4"),
+                        (net[0].weight, net[0].bias, net[3].weight, net[3].bias, net[6].weight, net[6].bias,
+                         net[9].weight, net[9].bias)):
+            setattr(q, k, _p(t.detach()))
+        for i, bn in enumerate(bns, 1):
+            for k, t in (("g", bn.weight), ("be", bn.bias), ("rm", bn.running_mean), ("rv", bn.running_var),
+                         ("nbt", bn.num_batches_tracked)):
+                setattr(q, "%s%d" % (k, i), _p(t.detach()) if t is not None else None)
+        T = max(float(temperature), 0.1) if temperature is not None else 0.0
+        work = torch.empty(L.mcaq_mapper_work_floats(n), device=c.device)
+        bits = torch.empty(n, device=c.device)
+        abi.check(L.mcaq_mapper_train_forward(ctypes.byref(q), _p(cf), n, mod.min_bits, mod.max_bits, T,
+                                              float(bns[0].momentum), 0 if return_continuous else 1, 1, _p(bits),
+                                              _p(work), _stream()), "mcaq_mapper_train_forward")
+        ctx.q, ctx.T, ctx.mod = q, T, mod
+        ctx.save_for_backward(cf, work, *params)
+        return bits.view(c.shape)
+
+    @staticmethod
+    def backward(ctx, gbits):
+        cf, work = ctx.saved_tensors[:2]
+        params = ctx.saved_tensors[2:]
+        n = cf.numel()
+        L = abi.lib()
+        mod = ctx.mod
+        gc = torch.empty(n, device=cf.device)
+        gflat = torch.empty(_MAPPER_G_SIZE, device=cf.device)
+        gpart = torch.empty(L.mcaq_mapper_gpart_floats(n), device=cf.device)
+        abi.check(L.mcaq_mapper_train_backward(ctypes.byref(ctx.q), _p(cf), n, _p(_f32c(gbits)), mod.min_bits,
+                                               mod.max_bits, ctx.T, _p(work), _p(gc), _p(gflat), _p(gpart),
+                                               _stream()), "mcaq_mapper_train_backward")
+        return (None, gc.view(gbits.shape), None, None) + tuple(_split_flat(gflat, params))
+
+
+_MAPPER_G_SIZE = 4609
+
+
+def _smask_backward_fused(ctx, mod, bit_map, absmean, gm, params):
+    """LearnedSoftMask backward on the fused kernel: grads of the bit map and
+    of the net's parameters from the m(p) gradient."""
+    B, H, W = absmean.shape
+    _, ht, wt = bit_map.shape
+    L = abi.lib()
+    q = abi.SmaskParams(*[_p(p.detach()) for p in params])
+    gb = torch.empty(B, ht, wt, device=absmean.device)
+    gflat = torch.empty(_SM_SIZE, device=absmean.device)
+    gpart = torch.empty(L.mcaq_smask_gpart_floats(B), device=absmean.device)
+    abi.check(L.mcaq_smask_train_backward(ctypes.byref(q), _p(_f32c(bit_map)), _p(absmean), _p(_f32c(gm)), B, H, W,
+                                          ht, wt, _p(gb), 0, _p(gflat), _p(gpart), _stream()),
+              "mcaq_smask_train_backward")
+    gp = _split_flat(gflat, params)
+    return (gb if ctx.needs_input_grad[0] else None, None, None) + tuple(
+        g if p.requires_grad else None for g, p in zip(gp, params))
 
 
 def _qat_struct(x, bits, m, xmin, xmax):

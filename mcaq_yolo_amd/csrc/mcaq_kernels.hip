@@ -1191,6 +1191,7 @@ int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream) 
 #include "mcaq_qat.h"
 #include "mcaq_nms.h"
 #include "mcaq_pipeline.h"
+#include "mcaq_train.h"
 
 // C++-linkage drop-in for the reference's declaration (include/mcaq_hip.h):
 // same name, argument list and void return as MCAQPlugin.cpp:15-23.  An

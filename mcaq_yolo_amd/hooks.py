@@ -57,6 +57,10 @@ class MCAQHooks(nn.Module):
         self.softmax_threads = None
         self._handles = []
         self._plans = {}
+        # buffer set of the per-shape HookPlans: steps captured into HIP graphs
+        # that run concurrently (batches in flight on several streams) each
+        # take their own slot, so they never share the hook's device buffers
+        self.plan_slot = 0
         if str(device).startswith("cuda") and torch.cuda.is_available():
             self.to(device)
 
@@ -105,7 +109,7 @@ class MCAQHooks(nn.Module):
         return hook
 
     def _plan(self, feat):
-        key = (tuple(feat.shape), feat.device, self.complexity_analyzer.grid_size)
+        key = (tuple(feat.shape), feat.device, self.complexity_analyzer.grid_size, self.plan_slot)
         plan = self._plans.get(key)
         if plan is None:
             plan = HookPlan([ScaleGeom(*feat.shape, self.complexity_analyzer.grid_size)], feat.device)

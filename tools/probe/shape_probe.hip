@@ -88,6 +88,30 @@ __global__ __launch_bounds__(256, 4) void read_units(Args a) {
   if (acc == 12345.678f) a.sink[0] = acc;
 }
 
+// pass-1 shape, channel-split: unit = (image, 256-px chunk, group of 64
+// channels); wave w reads the 16-row block 4 * group + w (one round)
+__global__ __launch_bounds__(256, 4) void read_units_split(Args a) {
+  const int u = blockIdx.x;
+  const int si = scale_of(a, u);
+  const Scale& S = a.s[si];
+  const int lu = u - S.begin;
+  const int upi = (S.HW + 255) / 256;
+  const int ngr = S.C / 64;
+  const int grp = lu % ngr, chunk = (lu / ngr) % upi, b = lu / (ngr * upi);
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int blk = grp * 4 + wv;
+  const int p = chunk * 256 + lane * 4;
+  const int pc = p < S.HW ? p : 0;
+  f4v v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    v[i] = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(S.x + ((size_t)b * S.C + blk * 16 + i) * S.HW + pc));
+  float acc = 0.0f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  if (acc == 12345.678f) a.sink[0] = acc;
+}
+
 __global__ void fill(float* p, size_t n, unsigned seed) {
   for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
     unsigned h = (unsigned)i * 2654435761u ^ seed;
@@ -186,5 +210,12 @@ int main() {
       hipExtLaunchKernelGGL(read_units, dim3(a.units), dim3(256), 0, 0, e0, e1, 0, a);
     });
   }
+  run("read units split (256 px x 64 ch, 1 round)", MB * 1e6, [&](int k) {
+    Args a = mkargs(k, 256, 0, 0, true);
+    int units = 0;
+    for (int i = 0; i < 3; ++i) { a.s[i].units = B * ((HWs[i] + 255) / 256) * (Cs[i] / 64); a.s[i].begin = units; units += a.s[i].units; }
+    a.units = units;
+    hipExtLaunchKernelGGL(read_units_split, dim3(units), dim3(256), 0, 0, e0, e1, 0, a);
+  });
   return 0;
 }

@@ -23,7 +23,7 @@ for f in sorted(glob.glob(d + "/b*.json")):
     if j.get("cpu_baseline"):
         print("   cpu_baseline", j["cpu_baseline"]["value"], j["cpu_baseline"]["cores"])
     if j.get("e2e"):
-        print("   e2e", {k_: j["e2e"].get(k_) for k_ in ("value", "ms_per_step")}, j["e2e"].get("config", {}).get("mcaq_hooks_and_nms_ms_per_step"))
+        print("   e2e", {k_: j["e2e"].get(k_) for k_ in ("value", "ms_per_step")}, j["e2e"].get("config", {}).get("mcaq_hooks_ms_per_step"))
 for f in sorted(glob.glob(d + "/**/*kernel_stats.csv", recursive=True)):
     print(f)
     for r in csv.DictReader(open(f)):
