@@ -137,8 +137,8 @@ def test_fused_mapper_vs_reference_fixture():
         for n, b in m.mapping_network.named_buffers():
             if b.dtype.is_floating_point:
                 _rel(b, torch.from_numpy(d[t + ".buf.mapping_network." + n]), 1e-5)
-            else:   # num_batches_tracked: one train-mode forward from a fresh module
-                assert int(b) == 1, n
+            else:   # num_batches_tracked: the loaded count + one train-mode forward
+                assert int(b) == int(np.asarray(W["bit_mapper.mapping_network." + n])) + 1, n
 
 
 def test_fused_softmask_backward_vs_autograd():
