@@ -489,7 +489,16 @@ def cpu_baseline(cfg_id, budget_s=10.0):
                       % (n, B, name, "x".join(map(str, chans)), grid, mapper, torch.get_num_threads(), dt)}
 
 
-class Runner:
+class _RunMixin:
+    def run(self, steps):
+        for _ in range(steps):
+            self.step()
+
+    def prepare(self, steps):
+        pass
+
+
+class Runner(_RunMixin):
     """Issues hook-path steps.  Independent HookPlans (own inputs and
     buffers) cycled over `depth` HIP streams: step i runs plan i % len(plans)
     on stream i % depth, so the per-image morphology of one batch
@@ -541,7 +550,7 @@ class Runner:
             torch.cuda.current_stream().wait_stream(st)
 
 
-class SplitRunner:
+class SplitRunner(_RunMixin):
     """--schedule split (N = 1, eager): the HBM passes of every batch on ONE
     streaming stream, back to back (stats(j + L), then quant(j)), the
     per-image morphology of each batch on one of two high-priority streams
@@ -591,33 +600,78 @@ class SplitRunner:
 
 class StagedRunner:
     """--schedule staged: the software-pipelined step of
-    engine.HookPipeline - pass 1 of batch i + pass 2 of batch i-3 on one
-    stream, morph pass A of batch i-1 and pass B of batch i-2 on two more;
-    one native call per step.  After the first 3 (filling) steps every step
+    engine.HookPipeline - pass 1 of batch i, morph pass A of batch i-1, pass
+    B of batch i-2 and pass 2 of batch i-3, each on its own stream, every
+    piece waiting only for the earlier steps' pieces it depends on.  N = 1:
+    runs of `group` steps are captured as HIP graphs (the four streams as
+    parallel branches, event edges between them; one graph per buffer-set
+    phase) and replayed, so no host work or cross-stream event round trip is
+    paid per launch.  N > 1 (the RCCL min/max all-reduce of each batch on the
+    pass-A stream): eager steps.  After the first 3 (filling) steps every step
     carries one batch's worth of every stage, and a step's pieces depend only
-    on the previous step's, so synchronising before the timed window does
-    not drain the pipeline: the first timed step already runs all four."""
+    on earlier steps', so synchronising before the timed window does not
+    drain the pipeline: the first timed step already runs all four."""
 
-    def __init__(self, plans, pg, cu_masks=None):
+    def __init__(self, plans, pg, cu_masks=None, group=4):
         from mcaq_yolo_amd.engine import HookPipeline
         self.pipe = HookPipeline(plans, cu_masks=cu_masks, process_group=pg)
+        self.graphs = {}
+        self.group = group
+        self.use_graph = pg is None
+        self.stream = torch.cuda.Stream()
+        if self.use_graph:
+            for _ in range(3):                    # fill eagerly
+                self.pipe.submit()
+            self.pipe.join(self.stream)
+
+    def _plan_runs(self, steps):
+        n, i, out = len(self.pipe.plans), self.pipe.i, []
+        while steps > 0:
+            k = min(self.group, steps)
+            out.append((i % n, k))
+            i += k
+            steps -= k
+        return out
+
+    def prepare(self, steps):
+        """Capture every graph a `steps` window needs (before timing)."""
+        if not self.use_graph:
+            return
+        i = self.pipe.i
+        for ph, k in self._plan_runs(steps):
+            if (ph, k) not in self.graphs:
+                self.graphs[(ph, k)] = self.pipe.capture(k, self.stream, at=i)
+            i += k
+
+    def run(self, steps):
+        """Issue exactly `steps` steps."""
+        if not self.use_graph:
+            for _ in range(steps):
+                self.pipe.submit()
+            return
+        self.prepare(steps)
+        for key in self._plan_runs(steps):
+            self.pipe.replay(self.graphs[key], self.stream)
 
     def step(self):
-        self.pipe.submit()
+        self.run(1)
 
     def sync(self):
-        self.pipe.join(torch.cuda.current_stream())
+        if self.use_graph:
+            torch.cuda.current_stream().wait_stream(self.stream)
+        else:
+            self.pipe.join(torch.cuda.current_stream())
 
 
 def cu_masks_for(n_morph, ncus=256):
     """CU masks: n_morph CUs (spread evenly over the chip) for the two morph
-    streams, the rest for the streaming stream; 0 = no masks."""
+    streams, the rest for the two streaming streams; 0 = no masks."""
     if n_morph <= 0:
         return None
     step = ncus / float(n_morph)
     morph = sorted({int(k * step) for k in range(n_morph)})
     stream = [c for c in range(ncus) if c not in set(morph)]
-    return [stream, morph, morph]
+    return [stream, morph, morph, stream]
 
 
 def kernel_timing(plans, reps=40, evict=None):
@@ -689,6 +743,11 @@ def main():
     ap.add_argument("--morph-cus", type=int, default=0,
                     help="--schedule staged: pin the morph streams to this many CUs (0: no CU masks)")
     ap.add_argument("--lookahead", type=int, default=3, help="--schedule split: batches of look-ahead")
+    ap.add_argument("--staged-plans", type=int, default=8,
+                    help="--schedule staged: buffer sets / input batches cycled (>= 4)")
+    ap.add_argument("--graph-steps", type=int, default=4,
+                    help="--schedule staged, N = 1: steps per captured HIP graph (<= --staged-plans - 4 keeps the "
+                         "buffer-reuse edges between graphs)")
     ap.add_argument("--m-plane", action="store_true",
                     help="pass B writes the m(p) plane and pass 2 reads it (instead of regenerating m per slice)")
     args = ap.parse_args()
@@ -725,7 +784,7 @@ def main():
     plans = []
     nin = max(args.inputs or max(3, depth), depth)
     if args.schedule == "staged":
-        nin = max(nin, 4)
+        nin = max(nin, args.staged_plans)
     if args.schedule == "split":
         nin = max(nin, args.lookahead + 1)
     for p in range(nin):
@@ -741,15 +800,14 @@ def main():
 
     use_graph = not args.eager and args.schedule == "streams"
     if args.schedule == "staged":
-        runner = StagedRunner(plans, pg, cu_masks_for(args.morph_cus))
+        runner = StagedRunner(plans, pg, cu_masks_for(args.morph_cus), group=args.graph_steps)
     elif args.schedule == "split":
         if pg is not None:
             raise SystemExit("--schedule split is a single-GPU experiment")
         runner = SplitRunner(plans, args.lookahead)
     else:
         runner = Runner(plans, pg, use_graph, depth)
-    for _ in range(max(args.warmup, 1)):
-        runner.step()
+    runner.run(max(args.warmup, 1))
     runner.sync()
     torch.cuda.synchronize()
 
@@ -770,7 +828,8 @@ def main():
         torch.cuda.synchronize()
         lat.append(time.perf_counter() - t1)
     latency_ms = sorted(lat)[len(lat) // 2] * 1e3
-    runner.step()         # plans[0] was re-run alone: one more step to be safe, then settle
+    runner.run(4)         # plans[0] was re-run alone: a few more steps to be safe, then settle
+    runner.prepare(args.steps)
     runner.sync()
 
     # ---- timed region: K steps, `depth` batches in flight
@@ -779,8 +838,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        runner.step()
+    runner.run(args.steps)
     t_enq = time.perf_counter() - t0
     runner.sync()
     torch.cuda.synchronize()
@@ -839,11 +897,14 @@ def main():
                                    "stats, phi1..5, complexity MLP, bilateral, bit mapper, soft mask, 2-8 bit "
                                    "quant/dequant; YOLOv8 network excluded (see e2e)" % (name, B, grid, mapper),
                        "global_batch": world * B, "grid_size": grid, "mapper": mapper,
-                       "parallelism": "dp%d" % world, "hip_graph": use_graph,
+                       "parallelism": "dp%d" % world,
+                       "hip_graph": use_graph or getattr(runner, "use_graph", False),
                        "batches_in_flight": 4 if args.schedule == "staged" else depth,
-                       "schedule": {"staged": "staged: pass 1 (i) + pass 2 (i-3) | pass A (i-1) | pass B (i-2), "
-                                              "3 streams, events%s" % (", morph on %d CUs" % args.morph_cus
-                                                                       if args.morph_cus else ""),
+                       "schedule": {"staged": "staged: pass 1 (i) | pass A (i-1) | pass B (i-2) | pass 2 (i-3) on 4 "
+                                              "streams, event edges%s%s" % (
+                                                  ", %d steps per HIP graph" % args.graph_steps
+                                                  if getattr(runner, "use_graph", False) else ", eager",
+                                                  ", morph on %d CUs" % args.morph_cus if args.morph_cus else ""),
                                     "streams": "streams: %d batch chains on %d streams, one HIP graph each"
                                                % (depth, depth),
                                     "split": "split (look-ahead %d)" % args.lookahead}[args.schedule],

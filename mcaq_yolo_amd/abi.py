@@ -74,7 +74,8 @@ EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats",
            "mcaq_qat_forward", "mcaq_qat_backward", "mcaq_qat_work_floats", "mcaq_ema_stats",
            "mcaq_nms", "mcaq_nms_work_floats", "mcaq_time_next_launch", "mcaq_time_launch",
            "mcaq_morph_pass", "mcaq_pipeline_create", "mcaq_pipeline_destroy", "mcaq_pipeline_stream",
-           "mcaq_pipeline_step", "mcaq_pipeline_release_a", "mcaq_pipeline_join",
+           "mcaq_pipeline_step", "mcaq_pipeline_release_a", "mcaq_pipeline_join", "mcaq_pipeline_fork",
+           "mcaq_pipeline_get_step", "mcaq_pipeline_set_step",
            "mcaq_mapper_work_floats", "mcaq_mapper_train_forward", "mcaq_mapper_gpart_floats",
            "mcaq_mapper_train_backward", "mcaq_head_gpart_floats", "mcaq_head_train_backward",
            "mcaq_smask_gpart_floats", "mcaq_smask_train_backward")
@@ -101,7 +102,7 @@ def _declare(lib):
     lib.mcaq_morph_pass.restype = I
     lib.mcaq_morph_pass.argtypes = [ctypes.POINTER(MorphScale), I, ctypes.POINTER(FinalizeScale), I, I, P]
     lib.mcaq_pipeline_create.restype = I
-    lib.mcaq_pipeline_create.argtypes = [ctypes.POINTER(ctypes.c_uint32), I, ctypes.POINTER(P)]
+    lib.mcaq_pipeline_create.argtypes = [ctypes.POINTER(ctypes.c_uint32), I, I, ctypes.POINTER(P)]
     lib.mcaq_pipeline_destroy.restype = I
     lib.mcaq_pipeline_destroy.argtypes = [P]
     lib.mcaq_pipeline_stream.restype = P
@@ -114,6 +115,12 @@ def _declare(lib):
     lib.mcaq_pipeline_release_a.argtypes = [P]
     lib.mcaq_pipeline_join.restype = I
     lib.mcaq_pipeline_join.argtypes = [P, P]
+    lib.mcaq_pipeline_fork.restype = I
+    lib.mcaq_pipeline_fork.argtypes = [P, P]
+    lib.mcaq_pipeline_get_step.restype = ctypes.c_longlong
+    lib.mcaq_pipeline_get_step.argtypes = [P]
+    lib.mcaq_pipeline_set_step.restype = I
+    lib.mcaq_pipeline_set_step.argtypes = [P, ctypes.c_longlong]
     lib.mcaq_stats_units.restype = I
     lib.mcaq_stats_units.argtypes = [I, I, I, I]
     lib.mcaq_morph_scratch_bytes.restype = ctypes.c_size_t

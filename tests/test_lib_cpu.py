@@ -14,7 +14,7 @@ HDR = os.path.join(ROOT, "include", "mcaq_hip.h")
 
 def declared_functions():
     src = open(HDR).read()
-    return sorted(set(re.findall(r"^(?:int|size_t|void\*)\s+(mcaq_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^(?:int|size_t|void\*|long long)\s+(mcaq_\w+)\s*\(", src, re.M)))
 
 
 def test_library_built_and_exports_header_symbols():

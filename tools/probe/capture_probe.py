@@ -1,0 +1,167 @@
+"""Probe: multi-stream HIP stream capture through torch.cuda.graph on this
+ROCm, in increasing complexity; prints a line after each case (a crash names
+the case that broke).  Cases:
+  A  fork origin -> s1, s2 (events), kernels, join
+  B  side-to-side edge: s2 waits for an event recorded on s1
+  C  one event recorded twice inside the capture (ring reuse)
+  D  HookPipeline.capture(n) for n = 1, 2, 4, 8 (no pre/post)
+  E  HookPipeline.capture(8) with pre/post copies"""
+import ctypes
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+hip = ctypes.CDLL("libamdhip64.so")
+V = ctypes.c_void_p
+
+
+def say(*a):
+    print(*a, flush=True)
+
+
+def hstream(flags=1):
+    s = V()
+    assert hip.hipStreamCreateWithFlags(ctypes.byref(s), flags) == 0
+    return s, torch.cuda.ExternalStream(s.value)
+
+
+def hevent():
+    e = V()
+    assert hip.hipEventCreateWithFlags(ctypes.byref(e), 2) == 0   # disable timing
+    return e
+
+
+x = torch.randn(1 << 20, device="cuda")
+y = torch.empty_like(x)
+z = torch.empty_like(x)
+cap = torch.cuda.Stream()
+(h1, s1), (h2, s2) = hstream(), hstream()
+ef, e1, e2, ej1, ej2 = (hevent() for _ in range(5))
+
+
+def run_case(name, body):
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=cap):
+        hc = V(cap.cuda_stream)
+        body(hc)
+    g.replay()
+    torch.cuda.synchronize()
+    say("case", name, "ok", float(y.sum()), float(z.sum()))
+
+
+def fork(hc):
+    assert hip.hipEventRecord(ef, hc) == 0
+    assert hip.hipStreamWaitEvent(h1, ef, 0) == 0
+    assert hip.hipStreamWaitEvent(h2, ef, 0) == 0
+
+
+def join(hc):
+    assert hip.hipEventRecord(ej1, h1) == 0
+    assert hip.hipEventRecord(ej2, h2) == 0
+    assert hip.hipStreamWaitEvent(hc, ej1, 0) == 0
+    assert hip.hipStreamWaitEvent(hc, ej2, 0) == 0
+
+
+def case_a(hc):
+    fork(hc)
+    with torch.cuda.stream(s1):
+        y.copy_(x)
+    with torch.cuda.stream(s2):
+        z.copy_(x)
+    join(hc)
+
+
+def case_b(hc):
+    fork(hc)
+    with torch.cuda.stream(s1):
+        y.copy_(x)
+    assert hip.hipEventRecord(e1, h1) == 0
+    assert hip.hipStreamWaitEvent(h2, e1, 0) == 0
+    with torch.cuda.stream(s2):
+        z.copy_(y)
+    join(hc)
+
+
+def case_c(hc):
+    fork(hc)
+    for _ in range(2):
+        with torch.cuda.stream(s1):
+            y.add_(1.0)
+        assert hip.hipEventRecord(e1, h1) == 0
+        assert hip.hipStreamWaitEvent(h2, e1, 0) == 0
+        with torch.cuda.stream(s2):
+            z.copy_(y)
+        assert hip.hipEventRecord(e2, h2) == 0
+        assert hip.hipStreamWaitEvent(h1, e2, 0) == 0
+    join(hc)
+
+
+def case_c1(hc):            # one event re-recorded, one direction only
+    fork(hc)
+    for _ in range(2):
+        with torch.cuda.stream(s1):
+            y.add_(1.0)
+        assert hip.hipEventRecord(e1, h1) == 0
+        assert hip.hipStreamWaitEvent(h2, e1, 0) == 0
+        with torch.cuda.stream(s2):
+            z.copy_(y)
+    join(hc)
+
+
+def case_c2(hc):            # both directions, distinct events, no re-record
+    fork(hc)
+    with torch.cuda.stream(s1):
+        y.add_(1.0)
+    assert hip.hipEventRecord(e1, h1) == 0
+    assert hip.hipStreamWaitEvent(h2, e1, 0) == 0
+    with torch.cuda.stream(s2):
+        z.copy_(y)
+    assert hip.hipEventRecord(e2, h2) == 0
+    assert hip.hipStreamWaitEvent(h1, e2, 0) == 0
+    with torch.cuda.stream(s1):
+        y.add_(1.0)
+    join(hc)
+
+
+say("torch", torch.__version__, "hip", torch.version.hip)
+run_case("A", case_a)
+run_case("B", case_b)
+
+# D: the bench's staged runner (config 2, 8 buffer sets, 4-step graphs) vs streams
+import time  # noqa: E402
+import bench  # noqa: E402
+from mcaq_yolo_amd.engine import HookPlan, ScaleGeom  # noqa: E402
+dev = torch.device("cuda:0")
+name, B, chans, grid, mapper = bench.CONFIGS[2]
+cm, mm, sm = bench.load_blobs(dev)
+geoms = [ScaleGeom(B, c, h, w, grid) for c, (h, w) in zip(chans, bench.SIZES)]
+plans = []
+for p in range(8):
+    feats = [bench.synth_features(B, c, h, w, 2000 + i + 104729 * p, dev) for i, (c, (h, w)) in enumerate(zip(chans, bench.SIZES))]
+    plan = HookPlan(geoms, dev)
+    plan.prepare(feats, cm, mm, [sm] * 3, mapper_kind=mapper)
+    plan.feats = feats
+    plans.append(plan)
+torch.cuda.synchronize()
+for G in (4, 2, 1):
+    r = bench.StagedRunner(plans, None, group=G)
+    r.run(40); r.sync(); torch.cuda.synchronize()
+    for K in (20, 400, 20, 400):
+        r.prepare(K); r.sync(); torch.cuda.synchronize()
+        t0 = time.perf_counter(); r.run(K); te = time.perf_counter() - t0; r.sync(); torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        say("D staged graph G=%d K=%d: %.2f us/step (enqueue %.1f us/step)" % (G, K, dt / K * 1e6, te / K * 1e6))
+    r.pipe.close()
+r = bench.Runner(plans[:3], None, True, 3)
+for K in (20, 400, 20, 400):
+    r.run(20); r.sync(); torch.cuda.synchronize()
+    t0 = time.perf_counter(); r.run(K); r.sync(); torch.cuda.synchronize()
+    say("D streams K=%d: %.2f us/step" % (K, (time.perf_counter() - t0) / K * 1e6))
+run_case("C1", case_c1)
+run_case("C2", case_c2)
+run_case("C", case_c)
+say("all ok")
