@@ -244,6 +244,12 @@ size_t mcaq_qat_work_floats(int B, int C, int H, int W);
  * (first != 0: running <- batch), in place. */
 int mcaq_ema_stats(const float* batch_min, const float* batch_max, float* running_min, float* running_max,
                    int C, double momentum, int first, hipStream_t stream);
+/* The same, plus copies of the updated statistics (copy_min / copy_max, the
+ * values this step's quantizer uses, or NULL) and num_batches_tracked += 1
+ * (num_batches, int64, or NULL) in the same launch. */
+int mcaq_ema_stats_ex(const float* batch_min, const float* batch_max, float* running_min, float* running_max,
+                      int C, double momentum, int first, float* copy_min, float* copy_max, long long* num_batches,
+                      hipStream_t stream);
 
 /* ---- batched NMS of YOLOv8 Detect outputs ----------------------------------
  * pred (B, no, N) fp32 with no = 4 + nc rows (cx, cy, w, h, class scores);
@@ -302,19 +308,34 @@ int mcaq_mapper_train_forward(const mcaq_mapper_params* P, const float* c, int n
 size_t mcaq_mapper_gpart_floats(int n);
 int mcaq_mapper_train_backward(const mcaq_mapper_params* P, const float* c, int n, const float* gbits,
                                float min_bits, float max_bits, float temperature, float* work, float* gc,
-                               float* gparams, float* gpart, hipStream_t stream);
+                               float* gparams, float* gpart, int accumulate, hipStream_t stream);
 /* analyzer head: gC (B, ht, wt) -> gcraw (B, ht, wt) work, gparams (2881:
  * complexity_mlp parameters() order); phi (B*ht*wt, 8), craw = the MLP output
  * before the bilateral; 3 launches */
 size_t mcaq_head_gpart_floats(int n);
 int mcaq_head_train_backward(const mcaq_cmlp_params* P, const float* phi, const float* craw, const float* gC, int B,
-                             int ht, int wt, float* gcraw, float* gparams, float* gpart, hipStream_t stream);
+                             int ht, int wt, float* gcraw, float* gparams, float* gpart, int accumulate,
+                             hipStream_t stream);
 /* soft mask: gm (B, H, W) -> gbits (B, ht, wt) (accumulate != 0: added),
  * gparams (170: net parameters() order); 2 launches */
 size_t mcaq_smask_gpart_floats(int B);
 int mcaq_smask_train_backward(const mcaq_smask_params* P, const float* bits, const float* absmean, const float* gm,
                               int B, int H, int W, int ht, int wt, float* gbits, int accumulate, float* gparams,
                               float* gpart, hipStream_t stream);
+/* gparams of the mapper / head backward: accumulate != 0 adds to gparams
+ * (the parameters' persistent gradient storage), 0 overwrites it. */
+
+/* ---- device packing of parameter blobs (the kernels' weight layouts) -------
+ * Segment i fills out[dst .. dst + len): mode 0 copies n floats from src;
+ * mode 1 writes the v_mfma_f32_16x16x4_f32 A operands of an (n, k) row-major
+ * weight (ceil(n/16) blocks x ceil(k/4) steps x 64 lanes, zero padded);
+ * out[0 .. total) not covered by a segment is zeroed.  One launch. */
+#define MCAQ_PACK_MAXSEG 16
+typedef struct {
+  const float* src;
+  int n, k, mode, dst;
+} mcaq_pack_seg;
+int mcaq_pack(const mcaq_pack_seg* segs, int nseg, float* out, int total, hipStream_t stream);
 
 int mcaq_abi_version(void);
 

@@ -60,6 +60,14 @@ class CmlpParams(ctypes.Structure):
     _fields_ = [(n, P) for n in ("w1", "b1", "g1", "be1", "w2", "b2", "g2", "be2", "w3", "b3")]
 
 
+MCAQ_PACK_MAXSEG = 16
+
+
+class PackSeg(ctypes.Structure):
+    """mcaq_pack_seg."""
+    _fields_ = [("src", P), ("n", I), ("k", I), ("mode", I), ("dst", I)]
+
+
 class SmaskParams(ctypes.Structure):
     _fields_ = [(n, P) for n in ("w1", "b1", "w2", "b2")]
 
@@ -78,7 +86,7 @@ EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats",
            "mcaq_pipeline_get_step", "mcaq_pipeline_set_step",
            "mcaq_mapper_work_floats", "mcaq_mapper_train_forward", "mcaq_mapper_gpart_floats",
            "mcaq_mapper_train_backward", "mcaq_head_gpart_floats", "mcaq_head_train_backward",
-           "mcaq_smask_gpart_floats", "mcaq_smask_train_backward")
+           "mcaq_smask_gpart_floats", "mcaq_smask_train_backward", "mcaq_ema_stats_ex", "mcaq_pack")
 
 _LIB = None
 
@@ -145,9 +153,13 @@ def _declare(lib):
     lib.mcaq_mapper_train_forward.restype = I
     lib.mcaq_mapper_train_forward.argtypes = [ctypes.POINTER(MapperParams), P, I, Fl, Fl, Fl, Fl, I, I, P, P, P]
     lib.mcaq_mapper_train_backward.restype = I
-    lib.mcaq_mapper_train_backward.argtypes = [ctypes.POINTER(MapperParams), P, I, P, Fl, Fl, Fl, P, P, P, P, P]
+    lib.mcaq_mapper_train_backward.argtypes = [ctypes.POINTER(MapperParams), P, I, P, Fl, Fl, Fl, P, P, P, P, I, P]
     lib.mcaq_head_train_backward.restype = I
-    lib.mcaq_head_train_backward.argtypes = [ctypes.POINTER(CmlpParams), P, P, P, I, I, I, P, P, P, P]
+    lib.mcaq_head_train_backward.argtypes = [ctypes.POINTER(CmlpParams), P, P, P, I, I, I, P, P, P, I, P]
+    lib.mcaq_ema_stats_ex.restype = I
+    lib.mcaq_ema_stats_ex.argtypes = [P, P, P, P, I, ctypes.c_double, I, P, P, P, P]
+    lib.mcaq_pack.restype = I
+    lib.mcaq_pack.argtypes = [ctypes.POINTER(PackSeg), I, P, I, P]
     lib.mcaq_smask_train_backward.restype = I
     lib.mcaq_smask_train_backward.argtypes = [ctypes.POINTER(SmaskParams), P, P, P, I, I, I, I, I, P, I, P, P, P]
     return lib

@@ -154,10 +154,39 @@ def _pad4(t):
     return torch.cat([t, t.new_zeros(n)]) if n else t
 
 
+def _device_pack(parts, mfma, total):
+    """The blob layout of _pack_* built by ONE kernel (mcaq_pack) from the live
+    parameter tensors: `parts` copied back to back, then the MFMA A operands
+    of the `mfma` weights, zero padded to `total` floats.  None when a tensor
+    is not a contiguous fp32 CUDA tensor (the torch packing then runs)."""
+    ts = list(parts) + list(mfma)
+    if not all(t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() for t in ts) or \
+            len(ts) > abi.MCAQ_PACK_MAXSEG:
+        return None
+    segs = (abi.PackSeg * len(ts))()
+    o = 0
+    for i, t in enumerate(parts):
+        segs[i].src, segs[i].n, segs[i].k, segs[i].mode, segs[i].dst = _p(t.detach()), t.numel(), 1, 0, o
+        o += t.numel()
+    for i, w in enumerate(mfma, len(parts)):
+        n, k = w.shape
+        segs[i].src, segs[i].n, segs[i].k, segs[i].mode, segs[i].dst = _p(w.detach()), n, k, 1, o
+        o += (n + 15) // 16 * ((k + 3) // 4) * 64
+    if o > total:
+        raise ValueError("blob overflow")
+    out = torch.empty(total, device=ts[0].device)
+    abi.check(abi.lib().mcaq_pack(segs, len(ts), _p(out), total, _stream()), "mcaq_pack")
+    return out
+
+
 def _pack_cmlp(seq):
     l0, ln1, l3, ln4, l6 = seq[0], seq[1], seq[3], seq[4], seq[6]
     parts = [l0.weight, l0.bias, ln1.weight, ln1.bias, l3.weight, l3.bias, ln4.weight, ln4.bias,
              l6.weight, l6.bias]
+    if sum(t.numel() for t in parts) == _CM_SIZE:
+        blob = _device_pack(parts, [l0.weight, l3.weight], (_CM_SIZE + 512 + 2048 + 3) // 4 * 4)
+        if blob is not None:
+            return blob
     flat = torch.cat([p.detach().float().reshape(-1) for p in parts])
     if flat.numel() != _CM_SIZE:
         raise ValueError("complexity MLP must be the reference Linear(8,64)-LN-ReLU-Linear(64,32)-LN-ReLU-"
@@ -172,6 +201,12 @@ def _pack_mapper(seq):
         lin, bn = seq[li], seq[bi]
         parts += [lin.weight, lin.bias, bn.weight, bn.bias, bn.running_mean, bn.running_var]
     parts += [seq[9].weight, seq[9].bias]
+    if sum(t.numel() for t in parts) == _MM_SIZE and len(parts) + 3 <= abi.MCAQ_PACK_MAXSEG:
+        total = _MM_SIZE + sum((w.shape[0] + 15) // 16 * ((w.shape[1] + 3) // 4) * 64
+                               for w in (seq[0].weight, seq[3].weight, seq[6].weight))
+        blob = _device_pack(parts, [seq[i].weight for i in (0, 3, 6)], (total + 3) // 4 * 4)
+        if blob is not None:
+            return blob
     flat = torch.cat([p.detach().float().reshape(-1) for p in parts])
     if flat.numel() != _MM_SIZE:
         raise ValueError("bit mapper must use hidden_dims [32, 64, 32]")
@@ -180,6 +215,10 @@ def _pack_mapper(seq):
 
 def _pack_softmask(seq):
     parts = [seq[0].weight, seq[0].bias, seq[2].weight, seq[2].bias]
+    if sum(t.numel() for t in parts) == _SM_SIZE:
+        blob = _device_pack(parts, [], (_SM_SIZE + 3) // 4 * 4)
+        if blob is not None:
+            return blob
     flat = torch.cat([p.detach().float().reshape(-1) for p in parts])
     if flat.numel() != _SM_SIZE:
         raise ValueError("soft mask must be the reference Conv2d(2,8,3)/Conv2d(8,2,1) net")
@@ -261,6 +300,7 @@ class MorphologicalComplexityAnalyzer(nn.Module):
         nn.init.zeros_(self.complexity_mlp[-2].bias)
         self.register_buffer("feature_weights", torch.ones(5) / 5)
         self._blob = _BlobCache()
+        self._gsink = _GradSink()
         if str(device).startswith("cuda") and torch.cuda.is_available():
             self.to(device)
 
@@ -535,6 +575,7 @@ class ComplexityToBitMappingNetwork(nn.Module):
         self.mapping_network = nn.Sequential(*layers)
         self.apply(self._init_weights)
         self._blob = _BlobCache()
+        self._gsink = _GradSink()
 
     _normalize_complexity_shape = staticmethod(_normalize_complexity_shape)
 
@@ -549,9 +590,14 @@ class ComplexityToBitMappingNetwork(nn.Module):
     def enforce_weight_constraints(self):
         """Eq.18: |W| for Linear layers and BatchNorm gammas (bit_allocation.py:186-197)."""
         if self.enforce_monotonicity:
-            for module in self.mapping_network.modules():
-                if isinstance(module, (nn.Linear, nn.BatchNorm1d)):
-                    module.weight.data.abs_()   # in place: parameter storage stays put (graph capture)
+            ws = [m.weight.data for m in self.mapping_network.modules() if isinstance(m, (nn.Linear, nn.BatchNorm1d))]
+            # in place (parameter storage stays put for graph capture); one
+            # multi-tensor launch on the GPU instead of one per layer
+            if ws and all(w.is_cuda for w in ws):
+                torch._foreach_abs_(ws)
+            else:
+                for w in ws:
+                    w.abs_()
 
     def create_augmented_features(self, complexity: torch.Tensor) -> torch.Tensor:
         """bit_allocation.py:199-216: z0 = [C, C^2, log1p C]."""
@@ -756,6 +802,48 @@ def _split_flat(flat, params):
     return out
 
 
+# The fused backwards of the modules shared by the three hook scales (the
+# complexity MLP and the bit mapper) accumulate their parameter gradients
+# directly into one persistent flat buffer whose views are the parameters'
+# .grad (as fused optimizers do), instead of returning them to autograd,
+# which would add the three scales' gradients with one ATen kernel per
+# parameter tensor (54 launches per QAT step).  Consequence: those gradients
+# reach .grad through backward() / loss.backward(), not through
+# torch.autograd.grad(..., inputs=params).  False: returned to autograd.
+DIRECT_GRAD_ACCUM = True
+
+
+class _GradSink:
+    """Flat gradient storage for a module's parameters; `target(params)`
+    returns (flat buffer, accumulate flag) for the next backward, or None when
+    some parameter's .grad is neither None nor this sink's view (gradients
+    from elsewhere: return them to autograd)."""
+
+    def __init__(self):
+        self.flat = None
+        self.views = None
+
+    def target(self, params):
+        if not DIRECT_GRAD_ACCUM or not all(p.requires_grad for p in params):
+            return None
+        n = sum(p.numel() for p in params)
+        dev = params[0].device
+        if self.flat is None or self.flat.numel() != n or self.flat.device != dev:
+            if torch.cuda.is_current_stream_capturing():
+                return None          # first use must happen outside capture (warm-up step)
+            self.flat = torch.zeros(n, device=dev)
+            self.views = _split_flat(self.flat, params)
+        mine = [p.grad is not None and p.grad.data_ptr() == v.data_ptr() and p.grad.shape == v.shape
+                for p, v in zip(params, self.views)]
+        if all(mine):
+            return self.flat, 1
+        if any(p.grad is not None for p in params):
+            return None
+        for p, v in zip(params, self.views):
+            p.grad = v
+        return self.flat, 0
+
+
 class _HeadTrainFn(torch.autograd.Function):
     """Analyzer in train mode: phi, C (= clamp(bilateral(MLP(phi)))) and the
     MLP output from the morph kernel (bit-exact forward); the backward is the
@@ -778,10 +866,14 @@ class _HeadTrainFn(torch.autograd.Function):
         L = abi.lib()
         q = abi.CmlpParams(*[_p(p.detach()) for p in params])
         gcraw = torch.empty(n, device=craw.device)
-        gflat = torch.empty(_CM_SIZE, device=craw.device)
+        mod_params = list(ctx.mod.complexity_mlp.parameters())
+        sink = ctx.mod._gsink.target(mod_params) if len(mod_params) == len(params) else None
+        gflat, acc = sink if sink is not None else (torch.empty(_CM_SIZE, device=craw.device), 0)
         gpart = torch.empty(L.mcaq_head_gpart_floats(n), device=craw.device)
         abi.check(L.mcaq_head_train_backward(ctypes.byref(q), _p(phi), _p(craw), _p(_f32c(gc)), B, ht, wt, _p(gcraw),
-                                             _p(gflat), _p(gpart), _stream()), "mcaq_head_train_backward")
+                                             _p(gflat), _p(gpart), acc, _stream()), "mcaq_head_train_backward")
+        if sink is not None:
+            return (None, None) + (None,) * len(params)
         return (None, None) + tuple(_split_flat(gflat, params))
 
 
@@ -824,11 +916,14 @@ class _MapperTrainFn(torch.autograd.Function):
         L = abi.lib()
         mod = ctx.mod
         gc = torch.empty(n, device=cf.device)
-        gflat = torch.empty(_MAPPER_G_SIZE, device=cf.device)
+        sink = mod._gsink.target(list(mod.mapping_network.parameters()))
+        gflat, acc = sink if sink is not None else (torch.empty(_MAPPER_G_SIZE, device=cf.device), 0)
         gpart = torch.empty(L.mcaq_mapper_gpart_floats(n), device=cf.device)
         abi.check(L.mcaq_mapper_train_backward(ctypes.byref(ctx.q), _p(cf), n, _p(_f32c(gbits)), mod.min_bits,
-                                               mod.max_bits, ctx.T, _p(work), _p(gc), _p(gflat), _p(gpart),
+                                               mod.max_bits, ctx.T, _p(work), _p(gc), _p(gflat), _p(gpart), acc,
                                                _stream()), "mcaq_mapper_train_backward")
+        if sink is not None:
+            return (None, gc.view(gbits.shape), None, None) + (None,) * len(params)
         return (None, gc.view(gbits.shape), None, None) + tuple(_split_flat(gflat, params))
 
 
@@ -1022,11 +1117,14 @@ class SpatialAdaptiveQuantization(nn.Module):
         self.num_batches_tracked += 1
 
     @torch.no_grad()
-    def update_running_stats(self, x: torch.Tensor, absmean: Optional[torch.Tensor] = None):
+    def update_running_stats(self, x: torch.Tensor, absmean: Optional[torch.Tensor] = None, want_copies=False):
         """quantization.py:319-353: EMA(momentum) of the batch min/max (pass 1 +
-        finalize + mcaq_ema_stats; absmean, if given, is filled by the same read)."""
+        finalize + mcaq_ema_stats; absmean, if given, is filled by the same read).
+        want_copies (per-channel, GPU): also return copies (xmin, xmax) of the
+        updated statistics, written by the EMA launch itself (the values this
+        step's quantizer reads; the running buffers change in place later)."""
         if self._frozen():
-            return
+            return None
         if not x.is_cuda:
             return self._update_running_stats_torch(x)
         _need_cuda(x, "x")
@@ -1062,10 +1160,21 @@ class SpatialAdaptiveQuantization(nn.Module):
             if not first:
                 rmin.copy_(self.running_min.reshape(nmin.shape))
                 rmax.copy_(self.running_max.reshape(nmax.shape))
-        abi.check(abi.lib().mcaq_ema_stats(_p(nmin), _p(nmax), _p(rmin), _p(rmax), nmin.numel(),
-                                           float(self.momentum), 1 if first else 0, _stream()), "mcaq_ema_stats")
+        nbt = self.num_batches_tracked
+        kernel_nbt = (nbt.device == nmin.device and nbt.dtype == torch.int64 and nbt.numel() == 1
+                      and nbt.is_contiguous())
+        cmin = cmax = None
+        if want_copies and self.per_channel:
+            cmin = torch.empty(nmin.numel(), device=nmin.device)
+            cmax = torch.empty(nmin.numel(), device=nmin.device)
+        # EMA, this step's copies and num_batches_tracked += 1 in one launch
+        abi.check(abi.lib().mcaq_ema_stats_ex(_p(nmin), _p(nmax), _p(rmin), _p(rmax), nmin.numel(),
+                                              float(self.momentum), 1 if first else 0, _p(cmin), _p(cmax),
+                                              _p(nbt) if kernel_nbt else None, _stream()), "mcaq_ema_stats_ex")
         self.running_min, self.running_max = rmin, rmax
-        self.num_batches_tracked += 1
+        if not kernel_nbt:
+            self.num_batches_tracked += 1
+        return (cmin, cmax) if cmin is not None else None
 
     def _stats_c(self, t, C):
         t = t.reshape(-1).float()
@@ -1083,15 +1192,18 @@ class SpatialAdaptiveQuantization(nn.Module):
         absmean = torch.empty(B, H, W, device=x.device) if want_m else None
         xf = _f32c(x)
         frozen = self._frozen()
+        copies = None
         if frozen:
             if want_m:
                 _run_stats(xf, absmean=absmean)
         else:
-            self.update_running_stats(xf, absmean)
+            copies = self.update_running_stats(xf, absmean, want_copies=self.training)
         # _calibrate_minmax (quantization.py:409-434): running stats in train
         # mode or when frozen, else this batch's min/max (copies: the running
         # buffers are updated in place by later steps)
-        if self.running_min is not None and (self.training or frozen):
+        if copies is not None:
+            xmin, xmax = copies
+        elif self.running_min is not None and (self.training or frozen):
             xmin = self._stats_c(self.running_min, C).clone()
             xmax = self._stats_c(self.running_max, C).clone()
         else:

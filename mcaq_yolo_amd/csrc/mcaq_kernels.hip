@@ -906,7 +906,12 @@ static int morph_plan(const MorphScale* s, int n, int* lds_mode, int* plane_stri
   for (int i = 0; i < n; ++i) pb = imax_(pb, (plane_bytes(s[i].Hc, s[i].Wc) + 15) & ~15);
   const int rest = fixed_bytes();   // pass A keeps no tile array in LDS
   const int limit = morph_lds_budget();
-  if (pb + rest <= limit) {
+#ifdef MCAQ_MORPH_GLOBAL_PLANES
+  const bool lds_fit = false;   // A/B: planes in global scratch (small LDS footprint beside streaming waves)
+#else
+  const bool lds_fit = pb + rest <= limit;
+#endif
+  if (lds_fit) {
     *lds_mode = 1; *plane_stride = pb; *dyn = (size_t)(pb + rest);
   } else if (rest <= limit) {
     *lds_mode = 0; *plane_stride = pb; *dyn = (size_t)rest;

@@ -321,16 +321,23 @@ __global__ __launch_bounds__(256) void mcaq_qat_fold_kernel(QatArgs a) {
 // running <- a * running + c * batch (first batch: running <- batch),
 // a = fp32(momentum), c = fp32(1 - momentum) as Python evaluates them.
 __global__ __launch_bounds__(256) void mcaq_ema_kernel(const float* bmin, const float* bmax, float* rmin,
-                                                       float* rmax, int C, float am, float cm, int first) {
+                                                       float* rmax, int C, float am, float cm, int first,
+                                                       float* cmin, float* cmax, long long* nbt) {
   const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c == 0 && nbt) nbt[0] += 1;     // num_batches_tracked (one thread of the launch)
   if (c >= C) return;
+  float lo, hi;
   if (first) {
-    rmin[c] = bmin[c];
-    rmax[c] = bmax[c];
+    lo = bmin[c];
+    hi = bmax[c];
   } else {
-    rmin[c] = am * rmin[c] + cm * bmin[c];
-    rmax[c] = am * rmax[c] + cm * bmax[c];
+    lo = am * rmin[c] + cm * bmin[c];
+    hi = am * rmax[c] + cm * bmax[c];
   }
+  rmin[c] = lo;
+  rmax[c] = hi;
+  if (cmin) cmin[c] = lo;             // copies for the quantizer of this step
+  if (cmax) cmax[c] = hi;
 }
 
 }  // namespace mcaq
@@ -415,7 +422,18 @@ int mcaq_ema_stats(const float* batch_min, const float* batch_max, float* runnin
   if (C < 1 || !batch_min || !batch_max || !running_min || !running_max) return (int)hipErrorInvalidValue;
   const float am = (float)momentum, cm = (float)(1.0 - momentum);
   hipLaunchKernelGGL(mcaq::mcaq_ema_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, batch_min, batch_max,
-                     running_min, running_max, C, am, cm, first ? 1 : 0);
+                     running_min, running_max, C, am, cm, first ? 1 : 0, (float*)nullptr, (float*)nullptr,
+                     (long long*)nullptr);
+  return (int)hipGetLastError();
+}
+
+int mcaq_ema_stats_ex(const float* batch_min, const float* batch_max, float* running_min, float* running_max,
+                      int C, double momentum, int first, float* copy_min, float* copy_max, long long* num_batches,
+                      hipStream_t stream) {
+  if (C < 1 || !batch_min || !batch_max || !running_min || !running_max) return (int)hipErrorInvalidValue;
+  const float am = (float)momentum, cm = (float)(1.0 - momentum);
+  hipLaunchKernelGGL(mcaq::mcaq_ema_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, batch_min, batch_max,
+                     running_min, running_max, C, am, cm, first ? 1 : 0, copy_min, copy_max, num_batches);
   return (int)hipGetLastError();
 }
 

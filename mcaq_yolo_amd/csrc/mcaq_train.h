@@ -28,10 +28,28 @@ constexpr int TR_TPB = 64;          // tiles per workgroup (one per lane of a wa
 
 __device__ __forceinline__ float tr_sigmoid(float a) { return 1.0f / (1.0f + expf(-a)); }
 
-// sum over the 64 lanes of a wave (every lane gets the total)
+// sum over the 64 lanes of a wave (every lane gets the total): DPP within
+// rows of 16 (quad xor 1, xor 2, half-row and row mirrors), then the gfx950
+// lane swaps across rows - no LDS round trips
+template <int CTRL>
+__device__ __forceinline__ float tr_dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+#if defined(__HIP_DEVICE_COMPILE__)
+  v += tr_dpp<0xB1>(v);     // quad_perm [1,0,3,2]
+  v += tr_dpp<0x4E>(v);     // quad_perm [2,3,0,1]
+  v += tr_dpp<0x141>(v);    // row_half_mirror
+  v += tr_dpp<0x140>(v);    // row_mirror
+  {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v += __uint_as_float((threadIdx.x & 16) ? r[0] : r[1]);
+  }
+  {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+    v += __uint_as_float((threadIdx.x & 32) ? r[0] : r[1]);
+  }
+#endif
   return v;
 }
 
@@ -131,8 +149,11 @@ __device__ __forceinline__ void map_bn(const mcaq_mapper_params& P, int L, const
   nbt = L == 1 ? P.nbt1 : (L == 2 ? P.nbt2 : P.nbt3);
 }
 
+constexpr int MW = 8;               // waves per mapper workgroup (lane = tile, waves split the features)
+constexpr int MTH = 64 * MW;
+
 // per-workgroup (mean, M2) of feature j over this workgroup's valid tiles;
-// 256 threads = 4 waves x 64 tiles, each wave one quarter of the features.
+// MW waves x 64 tiles, each wave 1/MW of the features.
 // v[f]: this lane's tile's value of feature f0 + f (f < NQ)
 template <int NQ>
 __device__ __forceinline__ void wg_moments(const float (&v)[NQ], bool valid, float nvalid, int f0, float* part, int nfeat) {
@@ -146,15 +167,42 @@ __device__ __forceinline__ void wg_moments(const float (&v)[NQ], bool valid, flo
   }
 }
 
-// batch statistics of layer L from the forward partials: mean, rstd for the
-// thread's quarter of features (and, once per launch, the running-stats update)
+// batch statistics of layer L from the forward partials: mean, rstd of every
+// feature in LDS (and, once per launch, the running-stats update).  The MW
+// waves combine interleaved subsets of the workgroups' partials in parallel
+// (Chan), then one thread per feature combines the MW results.
 template <int L>
-__device__ void map_stats(const MapperTrainArgs& A, const MapperWork& W, float* s_mean, float* s_rstd) {
+__device__ void map_stats(const MapperTrainArgs& A, const MapperWork& W, float* s_mean, float* s_rstd, float* s_tmp) {
   constexpr int N = MapL<L>::N;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, j = tid & 63, part = tid >> 6;
+  if (j < N) {
+    float n = 0.0f, m = 0.0f, M2 = 0.0f;
+    const float* fp = W.fpart(L);
+#pragma unroll 4
+    for (int w = part; w < A.nwg; w += MW) {
+      const float nb = W.cnt[w];
+      const float mb = fp[(size_t)w * 128 + j], M2b = fp[(size_t)w * 128 + N + j];
+      if (nb <= 0.0f) continue;
+      const float nn = n + nb, d = mb - m;
+      m = m + d * (nb / nn);
+      M2 = M2 + M2b + d * d * (n * nb / nn);
+      n = nn;
+    }
+    s_tmp[part * 192 + j] = n; s_tmp[part * 192 + 64 + j] = m; s_tmp[part * 192 + 128 + j] = M2;
+  }
+  __syncthreads();
   if (tid < N) {
-    float mean, var;
-    chan_combine(W.fpart(L), A.nwg, 128, tid, N, W.cnt, mean, var);
+    float n = 0.0f, m = 0.0f, M2 = 0.0f;
+#pragma unroll
+    for (int p = 0; p < MW; ++p) {
+      const float nb = s_tmp[p * 192 + tid], mb = s_tmp[p * 192 + 64 + tid], M2b = s_tmp[p * 192 + 128 + tid];
+      if (nb <= 0.0f) continue;
+      const float nn = n + nb, d = mb - m;
+      m = m + d * (nb / nn);
+      M2 = M2 + M2b + d * d * (n * nb / nn);
+      n = nn;
+    }
+    const float mean = m, var = n > 0.0f ? M2 / n : 0.0f;
     const float rstd = 1.0f / sqrtf(var + 1e-5f);
     s_mean[tid] = mean; s_rstd[tid] = rstd;
     if (blockIdx.x == 0) {
@@ -175,17 +223,18 @@ __device__ void map_stats(const MapperTrainArgs& A, const MapperWork& W, float* 
 
 // stage S (1..4) of the train-mode forward
 template <int S>
-__global__ __launch_bounds__(256) void mcaq_mapper_fwd_kernel(MapperTrainArgs A) {
+__global__ __launch_bounds__(MTH) void mcaq_mapper_fwd_kernel(MapperTrainArgs A) {
   __shared__ float s_in[TR_TPB][65];     // this workgroup's tiles' layer inputs
   __shared__ float s_mean[64], s_rstd[64];
+  __shared__ float s_tmp[MW * 192];
   const MapperWork W = mapper_work(A.work, A.n);
   const mcaq_mapper_params& P = A.P;
-  const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, q = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int t = blockIdx.x * TR_TPB + lane;
   const bool valid = t < A.n;
   const int tc = valid ? t : A.n - 1;
   const float nvalid = (float)imin_(TR_TPB, A.n - (int)blockIdx.x * TR_TPB);
-  if constexpr (S >= 2) map_stats<S - 1>(A, W, s_mean, s_rstd);
+  if constexpr (S >= 2) map_stats<S - 1>(A, W, s_mean, s_rstd, s_tmp);
   // ---- layer inputs of this workgroup's tiles -> s_in
   if constexpr (S == 1) {
     if (q == 0) {
@@ -200,7 +249,9 @@ __global__ __launch_bounds__(256) void mcaq_mapper_fwd_kernel(MapperTrainArgs A)
     const float* aprev = S == 2 ? W.a1 : (S == 3 ? W.a2 : W.a3);
     const float* g = S == 2 ? P.g1 : (S == 3 ? P.g2 : P.g3);
     const float* be = S == 2 ? P.be1 : (S == 3 ? P.be2 : P.be3);
-    for (int k = q; k < KP; k += 4) {
+#pragma unroll
+    for (int i = 0; i < KP / MW; ++i) {
+      const int k = q + i * MW;
       const float a = aprev[(size_t)tc * KP + k];
       const float y = g[k] * ((a - s_mean[k]) * s_rstd[k]) + be[k];
       s_in[lane][k] = y > 0.0f ? y : 0.0f;
@@ -208,7 +259,7 @@ __global__ __launch_bounds__(256) void mcaq_mapper_fwd_kernel(MapperTrainArgs A)
     __syncthreads();
   }
   if constexpr (S <= 3) {
-    constexpr int K = MapL<S>::K, N = MapL<S>::N, NQ = N / 4;
+    constexpr int K = MapL<S>::K, N = MapL<S>::N, NQ = N / MW;
     const float* w = S == 1 ? P.w1 : (S == 2 ? P.w2 : P.w3);
     const float* bb = S == 1 ? P.b1 : (S == 2 ? P.b2 : P.b3);
     float* aout = S == 1 ? W.a1 : (S == 2 ? W.a2 : W.a3);
@@ -252,13 +303,14 @@ __global__ __launch_bounds__(256) void mcaq_mapper_fwd_kernel(MapperTrainArgs A)
 //          partials, g_h(S-1) -> g_y(S-1), BN(S-1) partials
 //   S = 1: g_y1 + BN1 sums -> g_a1 -> W1 / b1 partials, g_z -> g_c
 template <int S>
-__global__ __launch_bounds__(256) void mcaq_mapper_bwd_kernel(MapperTrainArgs A) {
+__global__ __launch_bounds__(MTH) void mcaq_mapper_bwd_kernel(MapperTrainArgs A) {
   __shared__ float s_h[TR_TPB][65];     // this layer's input activations h(S-1)
   __shared__ float s_g[TR_TPB][65];     // gradient of this layer's pre-activation a(S)
   __shared__ float s_mean[64], s_rstd[64], s_sg[64], s_sgx[64];
+  __shared__ float s_tmp[MW * 128];
   const MapperWork W = mapper_work(A.work, A.n);
   const mcaq_mapper_params& P = A.P;
-  const int tid = threadIdx.x, lane = tid & 63, q = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, q = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int t = blockIdx.x * TR_TPB + lane;
   const bool valid = t < A.n;
   const int tc = valid ? t : A.n - 1;
@@ -273,14 +325,26 @@ __global__ __launch_bounds__(256) void mcaq_mapper_bwd_kernel(MapperTrainArgs A)
       s_g[lane][0] = valid ? (A.max_bits - A.min_bits) * g * (o * (1.0f - o)) : 0.0f;
     }
   } else {
-    // BN(S) backward: g_a = gamma rstd (g_y - S1/n - xhat S2/n)
+    // BN(S) backward: g_a = gamma rstd (g_y - S1/n - xhat S2/n); the BN sums
+    // over the workgroups' partials, MW interleaved subsets in parallel
     constexpr int N = MapL<S>::N;
     const float* g = S == 1 ? P.g1 : (S == 2 ? P.g2 : P.g3);
     const float* aS = S == 1 ? W.a1 : (S == 2 ? W.a2 : W.a3);
+    {
+      const int j = tid & 63, part = tid >> 6;
+      if (j < N) {
+        float s1 = 0.0f, s2 = 0.0f;
+        const float* bq = W.bpart_of(S + 1);   // written by the previous launch (stage S + 1)
+#pragma unroll 4
+        for (int w = part; w < A.nwg; w += MW) { s1 += bq[(size_t)w * 128 + j]; s2 += bq[(size_t)w * 128 + 64 + j]; }
+        s_tmp[part * 128 + j] = s1; s_tmp[part * 128 + 64 + j] = s2;
+      }
+    }
+    __syncthreads();
     if (tid < N) {
       float s1 = 0.0f, s2 = 0.0f;
-      const float* bq = W.bpart_of(S + 1);   // written by the previous launch (stage S + 1)
-      for (int w = 0; w < A.nwg; ++w) { s1 += bq[(size_t)w * 128 + tid]; s2 += bq[(size_t)w * 128 + 64 + tid]; }
+#pragma unroll
+      for (int p = 0; p < MW; ++p) { s1 += s_tmp[p * 128 + tid]; s2 += s_tmp[p * 128 + 64 + tid]; }
       s_sg[tid] = s1; s_sgx[tid] = s2;
       s_mean[tid] = W.stat[(S - 1) * 128 + tid]; s_rstd[tid] = W.stat[(S - 1) * 128 + 64 + tid];
       // gamma / beta gradients are the BN sums themselves: workgroup 0's
@@ -291,7 +355,9 @@ __global__ __launch_bounds__(256) void mcaq_mapper_bwd_kernel(MapperTrainArgs A)
     }
     __syncthreads();
     const float inv_n = 1.0f / (float)A.n;
-    for (int j = q; j < N; j += 4) {
+#pragma unroll
+    for (int i = 0; i < N / MW; ++i) {
+      const int j = q + i * MW;
       const float gy = W.gy[(size_t)tc * 64 + j];
       const float xh = (aS[(size_t)tc * N + j] - s_mean[j]) * s_rstd[j];
       s_g[lane][j] = valid ? g[j] * s_rstd[j] * (gy - s_sg[j] * inv_n - xh * (s_sgx[j] * inv_n)) : 0.0f;
@@ -309,7 +375,9 @@ __global__ __launch_bounds__(256) void mcaq_mapper_bwd_kernel(MapperTrainArgs A)
     const float* g = S == 4 ? P.g3 : (S == 3 ? P.g2 : P.g1);
     const float* be = S == 4 ? P.be3 : (S == 3 ? P.be2 : P.be1);
     const int L = S - 1;
-    for (int k = q; k < K; k += 4) {
+#pragma unroll
+    for (int i = 0; i < K / MW; ++i) {
+      const int k = q + i * MW;
       const float mean = W.stat[(L - 1) * 128 + k], rstd = W.stat[(L - 1) * 128 + 64 + k];
       const float y = g[k] * ((ap[(size_t)tc * K + k] - mean) * rstd) + be[k];
       s_h[lane][k] = valid && y > 0.0f ? y : 0.0f;
@@ -321,13 +389,26 @@ __global__ __launch_bounds__(256) void mcaq_mapper_bwd_kernel(MapperTrainArgs A)
     constexpr int NO = S == 4 ? 1 : MapL<S>::N;
     const int ow = S == 4 ? MG_W4 : (S == 3 ? MG_W3 : (S == 2 ? MG_W2 : MG_W1));
     const int ob = S == 4 ? MG_B4 : (S == 3 ? MG_B3 : (S == 2 ? MG_B2 : MG_B1));
-    for (int e = tid; e < NO * K; e += 256) {
-      const int j = e / K, k = e - (e / K) * K;
-      float s = 0.0f;
-      for (int u = 0; u < TR_TPB; ++u) s = fmaf(s_g[u][j], s_h[u][k], s);
-      gp[ow + e] = s;
+    if constexpr (NO * K == 4 * MTH) {
+      // one row x 4 columns per thread: 5 LDS reads per 4 FMAs
+      const int j0 = tid / (K / 4), k0 = (tid % (K / 4)) * 4;
+      float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      for (int u = 0; u < TR_TPB; ++u) {
+        const float g0 = s_g[u][j0];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] = fmaf(g0, s_h[u][k0 + c], acc[c]);
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c) gp[ow + j0 * K + k0 + c] = acc[c];
+    } else {
+      for (int e = tid; e < NO * K; e += MTH) {
+        const int j = e / K, k = e - (e / K) * K;
+        float s = 0.0f;
+        for (int u = 0; u < TR_TPB; ++u) s = fmaf(s_g[u][j], s_h[u][k], s);
+        gp[ow + e] = s;
+      }
     }
-    for (int j = tid; j < NO; j += 256) {
+    for (int j = tid; j < NO; j += MTH) {
       float s = 0.0f;
       for (int u = 0; u < TR_TPB; ++u) s += s_g[u][j];
       gp[ob + j] = s;
@@ -338,7 +419,7 @@ __global__ __launch_bounds__(256) void mcaq_mapper_bwd_kernel(MapperTrainArgs A)
     constexpr int NO = S == 4 ? 1 : MapL<S>::N;
     const float* w = S == 4 ? P.w4 : (S == 3 ? P.w3 : P.w2);
     const int L = S - 1;
-    constexpr int NQ = K / 4;
+    constexpr int NQ = K / MW;
     float gyv[NQ], xhv[NQ];
     const float* ap = S == 4 ? W.a3 : (S == 3 ? W.a2 : W.a1);
     const float* g = S == 4 ? P.g3 : (S == 3 ? P.g2 : P.g1);
@@ -347,6 +428,7 @@ __global__ __launch_bounds__(256) void mcaq_mapper_bwd_kernel(MapperTrainArgs A)
     for (int f = 0; f < NQ; ++f) {
       const int k = q * NQ + f;
       float acc = 0.0f;
+#pragma unroll 16
       for (int j = 0; j < NO; ++j) acc = fmaf(w[j * K + k], s_g[lane][j], acc);
       const float mean = W.stat[(L - 1) * 128 + k], rstd = W.stat[(L - 1) * 128 + 64 + k];
       const float xh = (ap[(size_t)tc * K + k] - mean) * rstd;
@@ -401,216 +483,250 @@ struct HeadTrainArgs {
 // bilateral (morphology.py:309-354, sigma_s 2, sigma_r 0.1, 5x5, replicate):
 // C_t = N_t / D_t, N = sum_k w_k p_k, D = sum_k w_k + 1e-8,
 // w_k = sp_k exp(-(p_k - c_t)^2 / 0.02), p_k = craw[clamp(t + o_k)].
-// One workgroup per image: forward quantities per tile, then the adjoint
-// gathered per tile u over every (t, k) with clamp(t + o_k) == u.
+// One workgroup per image.  Every (tile, tap) pair's weight is evaluated
+// once (LDS); the adjoint of tile u gathers, per tap k, the tiles t with
+// clamp(t + o_k) == u - one tile for an interior u, a short range at the
+// clamped border (tap_range) - in a fixed order (deterministic).
+__device__ __forceinline__ void tap_range(int u, int o, int n, int& lo, int& hi) {
+  // rows t in [0, n) with clamp(t + o, 0, n - 1) == u
+  lo = u == 0 ? 0 : u - o;
+  hi = u == n - 1 ? n - 1 : u - o;
+  lo = imax_(lo, 0);
+  hi = imin_(hi, n - 1);
+}
+
 __global__ __launch_bounds__(256) void mcaq_bilateral_bwd_kernel(HeadTrainArgs A) {
   extern __shared__ float smem_tr[];
   const int b = blockIdx.x, ht = A.ht, wt = A.wt, NT = ht * wt;
+  const int tid = threadIdx.x;
   float* cr = smem_tr;            // craw of the image
   float* gd = cr + NT;            // per tile: g_C / D  (0 outside the clamp)
-  float* gcen = gd + NT;          // per tile: sum_k gd (p_k - C) w_k (p_k - c)/0.01  (-> own craw)
-  float* cc = gcen + NT;          // C before the clamp
+  float* gcen = gd + NT;          // per tile: d/d c_t through its own range weights
+  float* wk = gcen + NT;          // [NT][25] range x spatial weights
+  float* cf = wk + 25 * NT;       // [NT][25] gd_t * dC_t / dp_k
   const float* crg = A.craw + (size_t)b * NT;
-  for (int t = threadIdx.x; t < NT; t += 256) cr[t] = crg[t];
+  for (int t = tid; t < NT; t += 256) cr[t] = crg[t];
   __syncthreads();
-  for (int t = threadIdx.x; t < NT; t += 256) {
+  for (int e = tid; e < NT * 25; e += 256) {
+    const int t = e / 25, k = e - t * 25;
+    const int th = t / wt, tw = t - th * wt;
+    const int hh = imin_(imax_(th + k / 5 - 2, 0), ht - 1), ww = imin_(imax_(tw + k % 5 - 2, 0), wt - 1);
+    const float d = cr[hh * wt + ww] - cr[t];
+    wk[e] = bits_as_float(k_bilat_sp_bits[k]) * expf(-(d * d) / 0.02f);
+  }
+  __syncthreads();
+  // per tile: forward C, g / D, the centre term
+  for (int t = tid; t < NT; t += 256) {
     const int th = t / wt, tw = t - th * wt;
     const float c = cr[t];
-    float num = 0.0f, den = 0.0f;
+    float num = 0.0f, den = 0.0f, sc = 0.0f;
+    float pv[25];
+#pragma unroll
     for (int k = 0; k < 25; ++k) {
       const int hh = imin_(imax_(th + k / 5 - 2, 0), ht - 1), ww = imin_(imax_(tw + k % 5 - 2, 0), wt - 1);
-      const float p = cr[hh * wt + ww];
-      const float d = p - c;
-      const float w = bits_as_float(k_bilat_sp_bits[k]) * expf(-(d * d) / 0.02f);
-      num = fmaf(w, p, num);
-      den += w;
+      pv[k] = cr[hh * wt + ww];
+      num = fmaf(wk[t * 25 + k], pv[k], num);
+      den += wk[t * 25 + k];
     }
     den += 1e-8f;
     const float Cv = num / den;
-    cc[t] = Cv;
     const float g = A.gC[(size_t)b * NT + t];
-    gd[t] = (Cv >= 0.0f && Cv <= 1.0f) ? g / den : 0.0f;
-  }
-  __syncthreads();
-  for (int t = threadIdx.x; t < NT; t += 256) {
-    const int th = t / wt, tw = t - th * wt;
-    const float c = cr[t], Cv = cc[t], g = gd[t];
-    float s = 0.0f;
+    const float gdt = (Cv >= 0.0f && Cv <= 1.0f) ? g / den : 0.0f;
+#pragma unroll
     for (int k = 0; k < 25; ++k) {
-      const int hh = imin_(imax_(th + k / 5 - 2, 0), ht - 1), ww = imin_(imax_(tw + k % 5 - 2, 0), wt - 1);
-      const float p = cr[hh * wt + ww];
-      const float d = p - c;
-      const float w = bits_as_float(k_bilat_sp_bits[k]) * expf(-(d * d) / 0.02f);
-      s = fmaf((p - Cv) * w, d / 0.01f, s);   // d C / d c_t through the range weights
+      const float w = wk[t * 25 + k], d = pv[k] - c;
+      sc = fmaf((pv[k] - Cv) * w, d / 0.01f, sc);                    // through the range weights, centre
+      cf[t * 25 + k] = gdt * (w - (pv[k] - Cv) * w * (d / 0.01f));    // d C_t / d p_k
     }
-    gcen[t] = g * s;
+    gd[t] = gdt;
+    gcen[t] = gdt * sc;
   }
   __syncthreads();
-  // adjoint gather: g_craw[u] = gcen[u] + sum over (t, k), clamp(t + o_k) = u, of
-  //   gd_t (w_k + (p_k - C_t) w_k (-(p_k - c_t) / 0.01))
-  for (int u = threadIdx.x; u < NT; u += 256) {
+  // adjoint gather: g_craw[u] = gcen[u] + sum over (k, t) with clamp(t + o_k) = u of cf[t][k]
+  for (int u = tid; u < NT; u += 256) {
     const int uh = u / wt, uw = u - uh * wt;
     float s = gcen[u];
-    for (int th = imax_(uh - 2, 0); th <= imin_(uh + 2, ht - 1); ++th) {
-      for (int i = 0; i < 5; ++i) {
-        if (imin_(imax_(th + i - 2, 0), ht - 1) != uh) continue;
-        for (int tw = imax_(uw - 2, 0); tw <= imin_(uw + 2, wt - 1); ++tw) {
-          const int t = th * wt + tw;
-          const float c = cr[t], Cv = cc[t], g = gd[t];
-          for (int j = 0; j < 5; ++j) {
-            if (imin_(imax_(tw + j - 2, 0), wt - 1) != uw) continue;
-            const float p = cr[u];
-            const float d = p - c;
-            const float w = bits_as_float(k_bilat_sp_bits[i * 5 + j]) * expf(-(d * d) / 0.02f);
-            s = fmaf(g, w - (p - Cv) * w * (d / 0.01f), s);
-          }
-        }
-      }
+    for (int k = 0; k < 25; ++k) {
+      int h0, h1, w0, w1;
+      tap_range(uh, k / 5 - 2, ht, h0, h1);
+      tap_range(uw, k % 5 - 2, wt, w0, w1);
+      for (int th = h0; th <= h1; ++th)
+        for (int tw = w0; tw <= w1; ++tw) s += cf[(th * wt + tw) * 25 + k];
     }
     A.gcraw[(size_t)b * NT + u] = s;
   }
 }
 
-// complexity MLP backward, one tile per lane, 64 tiles per workgroup (one
-// wave); the per-tile vectors meet in LDS and the weight partials are sums
-// over the workgroup's tiles in tile order
-__global__ __launch_bounds__(64) void mcaq_cmlp_bwd_kernel(HeadTrainArgs A) {
+// complexity MLP backward (Linear(8,64)-LN-ReLU-Linear(64,32)-LN-ReLU-
+// Linear(32,1)-sigmoid, recomputed): 64 tiles per workgroup, one per lane;
+// the CB_NW waves split each layer's features (wave q: 1 / CB_NW of them) and
+// meet in LDS for the LayerNorm sums.  Weight partials: sums over the
+// workgroup's tiles in tile order (W2 in 1 x 4 register blocks).
+constexpr int CB_NW = 8;                              // waves per workgroup
+constexpr int CB_ST = 8 + 64 * 4 + 32 * 4 + 1 + 4;   // per-tile LDS vector (floats, padded odd)
+enum : int { CB_PHI = 0, CB_R1 = 8, CB_GA1 = 72, CB_GY1 = 136, CB_GYX1 = 200, CB_R2 = 264, CB_GA2 = 296,
+             CB_GY2 = 328, CB_GYX2 = 360, CB_GA3 = 392 };
+
+__global__ __launch_bounds__(64 * CB_NW) void mcaq_cmlp_bwd_kernel(HeadTrainArgs A) {
+  constexpr int NW = CB_NW, F1 = 64 / NW, F2 = 32 / NW, NTH = 64 * NW;
   extern __shared__ float smem_tr[];
-  constexpr int ST = 8 + 64 + 64 + 32 + 32 + 64 + 64 + 32 + 32 + 1;   // per-tile vector floats
-  float* sv = smem_tr;                       // [TR_TPB][ST + 1]
+  float* sv = smem_tr;                       // [TR_TPB][CB_ST]
+  float* red = sv + TR_TPB * CB_ST;          // [NW][TR_TPB] cross-wave partial sums
   const mcaq_cmlp_params& P = A.P;
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, q = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int t = blockIdx.x * TR_TPB + lane;
   const bool valid = t < A.n;
   const int tc = valid ? t : A.n - 1;
-  float* v = sv + lane * (ST + 1);
-  float* phi = v;                 // 8
-  float* r1 = phi + 8;            // 64
-  float* ga1 = r1 + 64;           // 64
-  float* r2 = ga1 + 64;           // 32
-  float* ga2 = r2 + 32;           // 32
-  float* gyx1 = ga2 + 32;         // 64
-  float* gy1 = gyx1 + 64;         // 64
-  float* gyx2 = gy1 + 64;         // 32
-  float* gy2 = gyx2 + 32;         // 32
-  float* ga3 = gy2 + 32;          // 1
-  {
-    float ph[8];
+  float* v = sv + lane * CB_ST;
+  // cross-wave sum of one value per tile (every wave gets the total, in wave order)
+  auto xsum = [&](float x) {
+    red[q * TR_TPB + lane] = x;
+    __syncthreads();
+    float r = red[lane];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) { ph[k] = A.phi[(size_t)tc * 8 + k]; phi[k] = ph[k]; }
-    // ---- forward recompute
-    float a1[64];
-    float s = 0.0f;
+    for (int w = 1; w < NW; ++w) r += red[w * TR_TPB + lane];
+    __syncthreads();
+    return r;
+  };
+  float ph[8];
 #pragma unroll
-    for (int j = 0; j < 64; ++j) {
-      float acc = P.b1[j];
+  for (int k = 0; k < 8; ++k) ph[k] = A.phi[(size_t)tc * 8 + k];
+  if (q == 0) {
 #pragma unroll
-      for (int k = 0; k < 8; ++k) acc = fmaf(P.w1[j * 8 + k], ph[k], acc);
-      a1[j] = acc;
-      s += acc;
-    }
-    const float mu1 = s / 64.0f;
-    float vs = 0.0f;
+    for (int k = 0; k < 8; ++k) v[CB_PHI + k] = ph[k];
+  }
+  // ---- forward recompute: layer 1 (wave q: outputs F1 q .. F1 q + F1 - 1)
+  float x1[F1];
+  float s = 0.0f;
 #pragma unroll
-    for (int j = 0; j < 64; ++j) { const float d = a1[j] - mu1; vs = fmaf(d, d, vs); }
-    const float rs1 = 1.0f / sqrtf(vs / 64.0f + 1e-5f);
+  for (int f = 0; f < F1; ++f) {
+    const int j = q * F1 + f;
+    float acc = P.b1[j];
 #pragma unroll
-    for (int j = 0; j < 64; ++j) {
-      a1[j] = (a1[j] - mu1) * rs1;                      // xhat1
-      const float y = P.g1[j] * a1[j] + P.be1[j];
-      r1[j] = y > 0.0f ? y : 0.0f;
-    }
-    float a2[32];
-    s = 0.0f;
-    for (int j = 0; j < 32; ++j) {
-      float acc = P.b2[j];
-      for (int k = 0; k < 64; ++k) acc = fmaf(P.w2[j * 64 + k], r1[k], acc);
-      a2[j] = acc;
-      s += acc;
-    }
-    const float mu2 = s / 32.0f;
-    vs = 0.0f;
+    for (int k = 0; k < 8; ++k) acc = fmaf(P.w1[j * 8 + k], ph[k], acc);
+    x1[f] = acc;
+    s += acc;
+  }
+  const float mu1 = xsum(s) / 64.0f;
+  s = 0.0f;
 #pragma unroll
-    for (int j = 0; j < 32; ++j) { const float d = a2[j] - mu2; vs = fmaf(d, d, vs); }
-    const float rs2 = 1.0f / sqrtf(vs / 32.0f + 1e-5f);
-    float a3 = P.b3[0];
+  for (int f = 0; f < F1; ++f) { const float d = x1[f] - mu1; s = fmaf(d, d, s); }
+  const float rs1 = 1.0f / sqrtf(xsum(s) / 64.0f + 1e-5f);
 #pragma unroll
-    for (int j = 0; j < 32; ++j) {
-      a2[j] = (a2[j] - mu2) * rs2;                      // xhat2
-      const float y = P.g2[j] * a2[j] + P.be2[j];
-      r2[j] = y > 0.0f ? y : 0.0f;
-      a3 = fmaf(P.w3[j], r2[j], a3);
-    }
-    const float cv = tr_sigmoid(a3);
-    // ---- backward
-    const float g3 = valid ? A.gcraw[t] * (cv * (1.0f - cv)) : 0.0f;
-    ga3[0] = g3;
-    float gx2[32];
-    float m1 = 0.0f, m2 = 0.0f;
-#pragma unroll
-    for (int j = 0; j < 32; ++j) {
-      const float y = P.g2[j] * a2[j] + P.be2[j];
-      const float gy = y > 0.0f ? P.w3[j] * g3 : 0.0f;
-      gy2[j] = gy; gyx2[j] = gy * a2[j];
-      gx2[j] = gy * P.g2[j];
-      m1 += gx2[j]; m2 = fmaf(gx2[j], a2[j], m2);
-    }
-    m1 /= 32.0f; m2 /= 32.0f;
-#pragma unroll
-    for (int j = 0; j < 32; ++j) ga2[j] = rs2 * (gx2[j] - m1 - a2[j] * m2);
-    float gx1[64];
-    m1 = 0.0f; m2 = 0.0f;
-    for (int k = 0; k < 64; ++k) {
-      float acc = 0.0f;
-      for (int j = 0; j < 32; ++j) acc = fmaf(P.w2[j * 64 + k], ga2[j], acc);
-      const float y = P.g1[k] * a1[k] + P.be1[k];
-      const float gy = y > 0.0f ? acc : 0.0f;
-      gy1[k] = gy; gyx1[k] = gy * a1[k];
-      gx1[k] = gy * P.g1[k];
-      m1 += gx1[k]; m2 = fmaf(gx1[k], a1[k], m2);
-    }
-    m1 /= 64.0f; m2 /= 64.0f;
-    for (int k = 0; k < 64; ++k) ga1[k] = rs1 * (gx1[k] - m1 - a1[k] * m2);
+  for (int f = 0; f < F1; ++f) {
+    const int j = q * F1 + f;
+    x1[f] = (x1[f] - mu1) * rs1;                       // xhat1
+    const float y = P.g1[j] * x1[f] + P.be1[j];
+    v[CB_R1 + j] = y > 0.0f ? y : 0.0f;
   }
   __syncthreads();
-  // ---- weight partials: sums over the workgroup's tiles (invalid lanes hold zeros
-  // in ga*, gy*, gyx* because their upstream gradient is zero)
+  // layer 2 (wave q: outputs F2 q ..)
+  float x2[F2];
+  s = 0.0f;
+#pragma unroll
+  for (int f = 0; f < F2; ++f) {
+    const int j = q * F2 + f;
+    float acc = P.b2[j];
+#pragma unroll 16
+    for (int k = 0; k < 64; ++k) acc = fmaf(P.w2[j * 64 + k], v[CB_R1 + k], acc);
+    x2[f] = acc;
+    s += acc;
+  }
+  const float mu2 = xsum(s) / 32.0f;
+  s = 0.0f;
+#pragma unroll
+  for (int f = 0; f < F2; ++f) { const float d = x2[f] - mu2; s = fmaf(d, d, s); }
+  const float rs2 = 1.0f / sqrtf(xsum(s) / 32.0f + 1e-5f);
+  float a3p = 0.0f;
+#pragma unroll
+  for (int f = 0; f < F2; ++f) {
+    const int j = q * F2 + f;
+    x2[f] = (x2[f] - mu2) * rs2;                       // xhat2
+    const float y = P.g2[j] * x2[f] + P.be2[j];
+    const float r = y > 0.0f ? y : 0.0f;
+    v[CB_R2 + j] = r;
+    a3p = fmaf(P.w3[j], r, a3p);
+  }
+  const float a3 = xsum(a3p) + P.b3[0];
+  const float cv = tr_sigmoid(a3);
+  // ---- backward: sigmoid, layer 3, LN2
+  const float g3 = valid ? A.gcraw[t] * (cv * (1.0f - cv)) : 0.0f;
+  if (q == 0) v[CB_GA3] = g3;
+  float gx2[F2];
+  float m1 = 0.0f, m2 = 0.0f;
+#pragma unroll
+  for (int f = 0; f < F2; ++f) {
+    const int j = q * F2 + f;
+    const float y = P.g2[j] * x2[f] + P.be2[j];
+    const float gy = y > 0.0f ? P.w3[j] * g3 : 0.0f;
+    v[CB_GY2 + j] = gy; v[CB_GYX2 + j] = gy * x2[f];
+    gx2[f] = gy * P.g2[j];
+    m1 += gx2[f]; m2 = fmaf(gx2[f], x2[f], m2);
+  }
+  m1 = xsum(m1) / 32.0f; m2 = xsum(m2) / 32.0f;
+#pragma unroll
+  for (int f = 0; f < F2; ++f) v[CB_GA2 + q * F2 + f] = rs2 * (gx2[f] - m1 - x2[f] * m2);
+  __syncthreads();
+  // layer 2 transpose, LN1 (wave q: inputs F1 q ..)
+  float gx1[F1];
+  m1 = 0.0f; m2 = 0.0f;
+#pragma unroll
+  for (int f = 0; f < F1; ++f) {
+    const int k = q * F1 + f;
+    float acc = 0.0f;
+#pragma unroll 16
+    for (int j = 0; j < 32; ++j) acc = fmaf(P.w2[j * 64 + k], v[CB_GA2 + j], acc);
+    const float y = P.g1[k] * x1[f] + P.be1[k];
+    const float gy = y > 0.0f ? acc : 0.0f;
+    v[CB_GY1 + k] = gy; v[CB_GYX1 + k] = gy * x1[f];
+    gx1[f] = gy * P.g1[k];
+    m1 += gx1[f]; m2 = fmaf(gx1[f], x1[f], m2);
+  }
+  m1 = xsum(m1) / 64.0f; m2 = xsum(m2) / 64.0f;
+#pragma unroll
+  for (int f = 0; f < F1; ++f) v[CB_GA1 + q * F1 + f] = rs1 * (gx1[f] - m1 - x1[f] * m2);
+  __syncthreads();
+  // ---- weight partials over the workgroup's tiles (invalid lanes carry zero
+  // gradients).  W2 (32 x 64): thread = one row x 4 columns.
   float* gp = A.gpart + (size_t)blockIdx.x * CG_SIZE;
-  const int nt = TR_TPB;
-  auto tv = [&](int u) { return sv + u * (ST + 1); };
-  for (int e = lane; e < CG_SIZE; e += 64) {
-    float s = 0.0f;
-    if (e < CG_B1) {                       // W1 (64 x 8): ga1 (x) phi
-      const int j = e >> 3, k = e & 7;
-      for (int u = 0; u < nt; ++u) s = fmaf(tv(u)[72 + j], tv(u)[k], s);
-    } else if (e < CG_G1) {                // b1
-      const int j = e - CG_B1;
-      for (int u = 0; u < nt; ++u) s += tv(u)[72 + j];
-    } else if (e < CG_BE1) {               // LN1 gamma
-      const int j = e - CG_G1;
-      for (int u = 0; u < nt; ++u) s += tv(u)[200 + j];
-    } else if (e < CG_W2) {                // LN1 beta
-      const int j = e - CG_BE1;
-      for (int u = 0; u < nt; ++u) s += tv(u)[264 + j];
-    } else if (e < CG_B2) {                // W2 (32 x 64): ga2 (x) r1
-      const int jj = e - CG_W2, j = jj >> 6, k = jj & 63;
-      for (int u = 0; u < nt; ++u) s = fmaf(tv(u)[168 + j], tv(u)[8 + k], s);
-    } else if (e < CG_G2) {                // b2
-      const int j = e - CG_B2;
-      for (int u = 0; u < nt; ++u) s += tv(u)[168 + j];
-    } else if (e < CG_BE2) {               // LN2 gamma
-      const int j = e - CG_G2;
-      for (int u = 0; u < nt; ++u) s += tv(u)[328 + j];
-    } else if (e < CG_W3) {                // LN2 beta
-      const int j = e - CG_BE2;
-      for (int u = 0; u < nt; ++u) s += tv(u)[360 + j];
-    } else if (e < CG_B3) {                // W3 (1 x 32): ga3 * r2
-      const int k = e - CG_W3;
-      for (int u = 0; u < nt; ++u) s = fmaf(tv(u)[392], tv(u)[136 + k], s);
-    } else {                               // b3
-      for (int u = 0; u < nt; ++u) s += tv(u)[392];
+  auto tvec = [&](int u) { return sv + u * CB_ST; };
+  {
+    const int j0 = tid >> 4, k0 = (tid & 15) * 4;
+    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int u = 0; u < TR_TPB; ++u) {
+      const float* w = tvec(u);
+      const float g0 = w[CB_GA2 + j0];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[c] = fmaf(g0, w[CB_R1 + k0 + c], acc[c]);
     }
-    gp[e] = s;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) gp[CG_W2 + j0 * 64 + k0 + c] = acc[c];
+  }
+  // the rest: W1 (64 x 8) 512, b1 / LN1 64 + 64 + 64, b2 / LN2 32 + 32 + 32, W3 32, b3 1
+  for (int e = tid; e < CG_SIZE; e += NTH) {
+    if (e >= CG_W2 && e < CG_B2) continue;
+    float a = 0.0f;
+    if (e < CG_B1) {                       // W1: ga1 (x) phi
+      const int j = e >> 3, k = e & 7;
+      for (int u = 0; u < TR_TPB; ++u) a = fmaf(tvec(u)[CB_GA1 + j], tvec(u)[CB_PHI + k], a);
+    } else if (e < CG_G1) {                // b1
+      for (int u = 0; u < TR_TPB; ++u) a += tvec(u)[CB_GA1 + e - CG_B1];
+    } else if (e < CG_BE1) {               // LN1 gamma
+      for (int u = 0; u < TR_TPB; ++u) a += tvec(u)[CB_GYX1 + e - CG_G1];
+    } else if (e < CG_W2) {                // LN1 beta
+      for (int u = 0; u < TR_TPB; ++u) a += tvec(u)[CB_GY1 + e - CG_BE1];
+    } else if (e < CG_G2) {                // b2
+      for (int u = 0; u < TR_TPB; ++u) a += tvec(u)[CB_GA2 + e - CG_B2];
+    } else if (e < CG_BE2) {               // LN2 gamma
+      for (int u = 0; u < TR_TPB; ++u) a += tvec(u)[CB_GYX2 + e - CG_G2];
+    } else if (e < CG_W3) {                // LN2 beta
+      for (int u = 0; u < TR_TPB; ++u) a += tvec(u)[CB_GY2 + e - CG_BE2];
+    } else if (e < CG_B3) {                // W3: ga3 * r2
+      for (int u = 0; u < TR_TPB; ++u) a = fmaf(tvec(u)[CB_GA3], tvec(u)[CB_R2 + e - CG_W3], a);
+    } else {                               // b3
+      for (int u = 0; u < TR_TPB; ++u) a += tvec(u)[CB_GA3];
+    }
+    gp[e] = a;
   }
 }
 
@@ -630,7 +746,9 @@ struct MaskTrainArgs {
   int B, H, W, ht, wt, accumulate;
 };
 
-__global__ __launch_bounds__(256) void mcaq_smask_bwd_kernel(MaskTrainArgs A) {
+constexpr int SM_TH = 1024;   // threads per soft-mask backward workgroup (one image)
+
+__global__ __launch_bounds__(SM_TH) void mcaq_smask_bwd_kernel(MaskTrainArgs A) {
   extern __shared__ float smem_tr[];
   const int b = blockIdx.x, H = A.H, W = A.W, ht = A.ht, wt = A.wt, NT = ht * wt;
   const int tid = threadIdx.x;
@@ -640,12 +758,59 @@ __global__ __launch_bounds__(256) void mcaq_smask_bwd_kernel(MaskTrainArgs A) {
   float* gpre = gl + NT;             // per tile x 8: gradient of the hidden pre-activation
   float* rel = gpre + 8 * NT;        // per tile x 8: relu(hidden)
   float* red = rel + 8 * NT;         // 64 reduction slots
+  float* gmt = red + 64;             // per tile: gradient of m(tile)
+  int* hlo = (int*)(gmt + NT);       // rows / columns of every tile's nearest-upsample block
+  int* hhi = hlo + ht;
+  int* wlo = hhi + ht;
+  int* whi = wlo + wt;
+  float* part = (float*)(whi + wt);  // [H][wt] row partials of the upsample adjoint
+  float* tv = part + H * wt;         // [H][W] vertical pass of the smoothing adjoint
   const float* am = A.absmean + (size_t)b * H * W;
   const float* gm = A.gm + (size_t)b * H * W;
   const float sch = (float)ht / (float)H, scw = (float)wt / (float)W;
+  // the 5x5 smoothing kernel is the outer product of the 1-D Gaussian
+  // (quantization.py:207-209: g1 g1^T): g_d = sqrt(k_dd)
+  float g1[5];
+#pragma unroll
+  for (int d = 0; d < 5; ++d) g1[d] = sqrtf(bits_as_float(k_smooth5_bits[d * 6]));
+  for (int i = tid; i < ht; i += SM_TH) { hlo[i] = H; hhi[i] = -1; }
+  for (int j = tid; j < wt; j += SM_TH) { wlo[j] = W; whi[j] = -1; }
+  // adjoint of the smoothing (replicate pad), vertical pass:
+  // tv(q, w) = sum_d g_d sum_{p: clamp(p + d - 2) = q} g_m(p, w)
+  for (int e = tid; e < H * W; e += SM_TH) {
+    const int q = e / W, w = e - q * W;
+    float acc = 0.0f;
+    if (q >= 2 && q <= H - 3) {
+#pragma unroll
+      for (int d = 0; d < 5; ++d) acc = fmaf(g1[d], gm[(q - d + 2) * W + w], acc);
+    } else {
+#pragma unroll
+      for (int d = 0; d < 5; ++d) {
+        int p0, p1;
+        tap_range(q, d - 2, H, p0, p1);
+        float r = 0.0f;
+        for (int p = p0; p <= p1; ++p) r += gm[p * W + w];
+        acc = fmaf(g1[d], r, acc);
+      }
+    }
+    tv[e] = acc;
+  }
+  __syncthreads();
+  // nearest source row / column (floor(o * in / out), clamped) is monotone:
+  // every tile's block is a contiguous range
+  for (int h = tid; h < H; h += SM_TH) {
+    const int i = imin_((int)floorf((float)h * sch), ht - 1);
+    if (h == 0 || imin_((int)floorf((float)(h - 1) * sch), ht - 1) != i) hlo[i] = h;
+    if (h == H - 1 || imin_((int)floorf((float)(h + 1) * sch), ht - 1) != i) hhi[i] = h;
+  }
+  for (int w = tid; w < W; w += SM_TH) {
+    const int j = imin_((int)floorf((float)w * scw), wt - 1);
+    if (w == 0 || imin_((int)floorf((float)(w - 1) * scw), wt - 1) != j) wlo[j] = w;
+    if (w == W - 1 || imin_((int)floorf((float)(w + 1) * scw), wt - 1) != j) whi[j] = w;
+  }
   // ---- forward recompute: per-tile activation (adaptive_avg_pool2d), amax
   float lmx = -3.402823466e38f;
-  for (int t = tid; t < NT; t += 256) {
+  for (int t = tid; t < NT; t += SM_TH) {
     const int i = t / wt, j = t - i * wt;
     const int ha = (i * H) / ht, hb = ((i + 1) * H + ht - 1) / ht;
     const int wa = (j * W) / wt, wb = ((j + 1) * W + wt - 1) / wt;
@@ -662,14 +827,46 @@ __global__ __launch_bounds__(256) void mcaq_smask_bwd_kernel(MaskTrainArgs A) {
   for (int o = 32; o > 0; o >>= 1) lmx = fmax_(lmx, __shfl_xor(lmx, o, 64));
   if ((tid & 63) == 0) red[tid >> 6] = lmx;
   __syncthreads();
-  const float amax = fmax_(fmax_(red[0], red[1]), fmax_(red[2], red[3]));
+  float amax = red[0];
+#pragma unroll
+  for (int w = 1; w < SM_TH / 64; ++w) amax = fmax_(amax, red[w]);
   const float den = amax + 1e-8f;
-  for (int t = tid; t < NT; t += 256) f1[t] = f1[t] / den;
+  for (int t = tid; t < NT; t += SM_TH) f1[t] = f1[t] / den;
+  // horizontal pass + the nearest-upsample adjoint: one item = one row of one
+  // tile column's block, summed into part[h][j]
+  for (int it = tid; it < H * wt; it += SM_TH) {
+    const int h = it / wt, j = it - h * wt;
+    const float* row = tv + h * W;
+    float acc = 0.0f;
+    for (int q = wlo[j]; q <= whi[j]; ++q) {
+      float g = 0.0f;
+      if (q >= 2 && q <= W - 3) {
+#pragma unroll
+        for (int d = 0; d < 5; ++d) g = fmaf(g1[d], row[q - d + 2], g);
+      } else {
+#pragma unroll
+        for (int d = 0; d < 5; ++d) {
+          int p0, p1;
+          tap_range(q, d - 2, W, p0, p1);
+          float r = 0.0f;
+          for (int p = p0; p <= p1; ++p) r += row[p];
+          g = fmaf(g1[d], r, g);
+        }
+      }
+      acc += g;
+    }
+    part[it] = acc;
+  }
   __syncthreads();
-  // ---- per tile: hidden layer, logits, m(tile); gradient of m(tile) from
-  // the m(p) gradient through the 5x5 smoothing (replicate pad) and the
-  // nearest upsample: g_mt(t) = sum_p g_m(p) sum_{i,j: src(clamp(p + o_ij)) = t} k_ij
-  for (int t = tid; t < NT; t += 256) {
+  for (int t = tid; t < NT; t += SM_TH) {
+    const int i = t / wt, j = t - i * wt;
+    float g = 0.0f;
+    for (int h = hlo[i]; h <= hhi[i]; ++h) g += part[h * wt + j];
+    gmt[t] = g;
+  }
+  __syncthreads();
+  // ---- per tile: hidden layer, logits, m(tile), gradients of the logits
+  for (int t = tid; t < NT; t += SM_TH) {
     const int i = t / wt, j = t - i * wt;
     float hid[8];
 #pragma unroll
@@ -690,32 +887,8 @@ __global__ __launch_bounds__(256) void mcaq_smask_bwd_kernel(MaskTrainArgs A) {
 #pragma unroll
     for (int ic = 0; ic < 8; ++ic) { l0 = fmaf(A.P.w2[ic], rel[t * 8 + ic], l0); l1 = fmaf(A.P.w2[8 + ic], rel[t * 8 + ic], l1); }
     const float mt = 1.0f / (1.0f + expf(l1 - l0));
-    // pixels whose 5x5 window reaches this tile's nearest-upsample block
-    int h0 = H, h1 = -1, w0 = W, w1 = -1;
-    for (int h = 0; h < H; ++h) if (imin_((int)floorf((float)h * sch), ht - 1) == i) { h0 = imin_(h0, h); h1 = h; }
-    for (int w = 0; w < W; ++w) if (imin_((int)floorf((float)w * scw), wt - 1) == j) { w0 = imin_(w0, w); w1 = w; }
-    float gmt = 0.0f;
-    for (int h = imax_(h0 - 2, 0); h <= imin_(h1 + 2, H - 1); ++h) {
-      float rw[5];
-#pragma unroll
-      for (int ii = 0; ii < 5; ++ii) {
-        const int hs = imin_(imax_(h + ii - 2, 0), H - 1);
-        rw[ii] = (hs >= h0 && hs <= h1) ? 1.0f : 0.0f;
-      }
-      for (int w = imax_(w0 - 2, 0); w <= imin_(w1 + 2, W - 1); ++w) {
-        float kw = 0.0f;
-#pragma unroll
-        for (int jj = 0; jj < 5; ++jj) {
-          const int ws = imin_(imax_(w + jj - 2, 0), W - 1);
-          if (ws < w0 || ws > w1) continue;
-#pragma unroll
-          for (int ii = 0; ii < 5; ++ii) kw = fmaf(bits_as_float(k_smooth5_bits[ii * 5 + jj]), rw[ii], kw);
-        }
-        gmt = fmaf(gm[h * W + w], kw, gmt);
-      }
-    }
     // softmax (2 classes): d m / d l0 = m (1 - m) = -d m / d l1
-    const float g0 = gmt * (mt * (1.0f - mt));
+    const float g0 = gmt[t] * (mt * (1.0f - mt));
     gl[t] = g0;
 #pragma unroll
     for (int ic = 0; ic < 8; ++ic) {
@@ -726,7 +899,7 @@ __global__ __launch_bounds__(256) void mcaq_smask_bwd_kernel(MaskTrainArgs A) {
   __syncthreads();
   // ---- gradient of the bits feature: 3x3 transposed conv of gpre, then
   // through the clamp and the affine map
-  for (int u = tid; u < NT; u += 256) {
+  for (int u = tid; u < NT; u += SM_TH) {
     const int i = u / wt, j = u - i * wt;
     float s = 0.0f;
 #pragma unroll
@@ -745,7 +918,7 @@ __global__ __launch_bounds__(256) void mcaq_smask_bwd_kernel(MaskTrainArgs A) {
   }
   // ---- parameter partials of this image
   float* gp = A.gpart + (size_t)b * SG_SIZE;
-  for (int e = tid; e < SG_SIZE; e += 256) {
+  for (int e = tid; e < SG_SIZE; e += SM_TH) {
     float s = 0.0f;
     if (e < SG_B1) {                  // W1[oc][ic][qq]
       const int oc = e / 18, ic = (e / 9) & 1, qq = e % 9;
@@ -770,6 +943,39 @@ __global__ __launch_bounds__(256) void mcaq_smask_bwd_kernel(MaskTrainArgs A) {
   }
 }
 
+// ---- device packing of parameter blobs --------------------------------------
+// out[seg.dst + i] for every segment: mode 0 copies n floats from src; mode 1
+// writes the v_mfma_f32_16x16x4_f32 A operands of an (n, k) row-major weight
+// ([block][step][lane]: lane l of block b, step s holds W[16 b + (l & 15)]
+// [4 s + (l >> 4)], zero outside the weight); positions no segment covers
+// (tail padding) are zero.  One launch replaces the torch cat / zeros / index
+// sequence that re-packs a blob after every optimizer step.
+struct PackArgs {
+  mcaq_pack_seg seg[MCAQ_PACK_MAXSEG];
+  int nseg, total;
+};
+
+__global__ __launch_bounds__(256) void mcaq_pack_kernel(PackArgs a, float* __restrict__ out) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= a.total) return;
+  float v = 0.0f;
+  for (int i = 0; i < a.nseg; ++i) {
+    const mcaq_pack_seg& g = a.seg[i];
+    const int kp = (g.k + 3) & ~3, nb = (g.n + 15) >> 4;
+    const int len = g.mode == 0 ? g.n : nb * (kp >> 2) * 64;
+    const int u = e - g.dst;
+    if (u < 0 || u >= len) continue;
+    if (g.mode == 0) {
+      v = g.src[u];
+    } else {
+      const int lane = u & 63, st = (u >> 6) % (kp >> 2), b = (u >> 6) / (kp >> 2);
+      const int row = 16 * b + (lane & 15), col = 4 * st + (lane >> 4);
+      v = (row < g.n && col < g.k) ? g.src[(size_t)row * g.k + col] : 0.0f;
+    }
+  }
+  out[e] = v;
+}
+
 }  // namespace mcaq
 
 // ============================================================================
@@ -788,7 +994,7 @@ int mcaq_mapper_train_forward(const mcaq_mapper_params* P, const float* c, int n
   A.P = *P; A.c = c; A.bits = bits; A.work = work; A.n = n; A.nwg = (n + TR_TPB - 1) / TR_TPB;
   A.min_bits = min_bits; A.max_bits = max_bits; A.temperature = temperature; A.momentum = momentum;
   A.round_bits = round_bits; A.update_stats = update_stats;
-  const dim3 g(A.nwg), t(256);
+  const dim3 g(A.nwg), t(MTH);
   hipLaunchKernelGGL(mcaq_mapper_fwd_kernel<1>, g, t, 0, stream, A);
   hipLaunchKernelGGL(mcaq_mapper_fwd_kernel<2>, g, t, 0, stream, A);
   hipLaunchKernelGGL(mcaq_mapper_fwd_kernel<3>, g, t, 0, stream, A);
@@ -798,20 +1004,20 @@ int mcaq_mapper_train_forward(const mcaq_mapper_params* P, const float* c, int n
 
 int mcaq_mapper_train_backward(const mcaq_mapper_params* P, const float* c, int n, const float* gbits,
                                float min_bits, float max_bits, float temperature, float* work, float* gc,
-                               float* gparams, float* gpart, hipStream_t stream) {
+                               float* gparams, float* gpart, int accumulate, hipStream_t stream) {
   using namespace mcaq;
   if (!P || !c || !gbits || !gc || !gparams || !gpart || !work || n < 1) return (int)hipErrorInvalidValue;
   MapperTrainArgs A{};
   A.P = *P; A.c = c; A.gbits = gbits; A.gc = gc; A.work = work; A.gpart = gpart; A.n = n;
   A.nwg = (n + TR_TPB - 1) / TR_TPB;
   A.min_bits = min_bits; A.max_bits = max_bits; A.temperature = temperature;
-  const dim3 g(A.nwg), t(256);
+  const dim3 g(A.nwg), t(MTH);
   hipLaunchKernelGGL(mcaq_mapper_bwd_kernel<4>, g, t, 0, stream, A);
   hipLaunchKernelGGL(mcaq_mapper_bwd_kernel<3>, g, t, 0, stream, A);
   hipLaunchKernelGGL(mcaq_mapper_bwd_kernel<2>, g, t, 0, stream, A);
   hipLaunchKernelGGL(mcaq_mapper_bwd_kernel<1>, g, t, 0, stream, A);
   hipLaunchKernelGGL(mcaq_tr_reduce_kernel, dim3((MG_SIZE + 255) / 256), dim3(256), 0, stream, (const float*)gpart,
-                     A.nwg, (int)MG_SIZE, (int)MG_SIZE, gparams, 0);
+                     A.nwg, (int)MG_SIZE, (int)MG_SIZE, gparams, accumulate ? 1 : 0);
   return (int)hipGetLastError();
 }
 
@@ -820,32 +1026,51 @@ size_t mcaq_mapper_gpart_floats(int n) { return (size_t)((n + mcaq::TR_TPB - 1) 
 size_t mcaq_head_gpart_floats(int n) { return (size_t)((n + mcaq::TR_TPB - 1) / mcaq::TR_TPB) * mcaq::CG_SIZE; }
 
 int mcaq_head_train_backward(const mcaq_cmlp_params* P, const float* phi, const float* craw, const float* gC, int B,
-                             int ht, int wt, float* gcraw, float* gparams, float* gpart, hipStream_t stream) {
+                             int ht, int wt, float* gcraw, float* gparams, float* gpart, int accumulate,
+                             hipStream_t stream) {
   using namespace mcaq;
   if (!P || !phi || !craw || !gC || !gcraw || !gparams || !gpart || B < 1 || ht < 1 || wt < 1)
     return (int)hipErrorInvalidValue;
   HeadTrainArgs A{};
   A.P = *P; A.phi = phi; A.craw = craw; A.gC = gC; A.gcraw = gcraw; A.gpart = gpart;
   A.B = B; A.ht = ht; A.wt = wt; A.n = B * ht * wt; A.nwg = (A.n + TR_TPB - 1) / TR_TPB;
-  const size_t lb = (size_t)4 * ht * wt * sizeof(float);
-  if (lb > 64 * 1024) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(mcaq_bilateral_bwd_kernel, dim3(B), dim3(256), lb, stream, A);
-  constexpr int ST = 8 + 64 + 64 + 32 + 32 + 64 + 64 + 32 + 32 + 1;
-  const size_t lc = (size_t)TR_TPB * (ST + 1) * sizeof(float);
-  static bool set = false;
+  const size_t lb = (size_t)53 * ht * wt * sizeof(float);
+  if (lb > 160 * 1024 - 1024) return (int)hipErrorInvalidValue;
+  const size_t lc = (size_t)(TR_TPB * CB_ST + CB_NW * TR_TPB) * sizeof(float);
+  static int set = 0;
   if (!set) {
-    const hipError_t e = hipFuncSetAttribute((const void*)mcaq_cmlp_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             (int)lc);
+    hipError_t e = hipFuncSetAttribute((const void*)mcaq_cmlp_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)lc);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)mcaq_bilateral_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024 - 1024);
     if (e != hipSuccess) return (int)e;
-    set = true;
+    set = 1;
   }
-  hipLaunchKernelGGL(mcaq_cmlp_bwd_kernel, dim3(A.nwg), dim3(64), lc, stream, A);
+  hipLaunchKernelGGL(mcaq_bilateral_bwd_kernel, dim3(B), dim3(256), lb, stream, A);
+  hipLaunchKernelGGL(mcaq_cmlp_bwd_kernel, dim3(A.nwg), dim3(64 * CB_NW), lc, stream, A);
   hipLaunchKernelGGL(mcaq_tr_reduce_kernel, dim3((CG_SIZE + 255) / 256), dim3(256), 0, stream, (const float*)gpart,
-                     A.nwg, (int)CG_SIZE, (int)CG_SIZE, gparams, 0);
+                     A.nwg, (int)CG_SIZE, (int)CG_SIZE, gparams, accumulate ? 1 : 0);
   return (int)hipGetLastError();
 }
 
 size_t mcaq_smask_gpart_floats(int B) { return (size_t)B * mcaq::SG_SIZE; }
+
+int mcaq_pack(const mcaq_pack_seg* segs, int nseg, float* out, int total, hipStream_t stream) {
+  using namespace mcaq;
+  if (!segs || !out || nseg < 1 || nseg > MCAQ_PACK_MAXSEG || total < 1) return (int)hipErrorInvalidValue;
+  PackArgs a{};
+  for (int i = 0; i < nseg; ++i) {
+    const mcaq_pack_seg& g = segs[i];
+    if (!g.src || g.n < 1 || g.dst < 0 || (g.mode != 0 && (g.mode != 1 || g.k < 1))) return (int)hipErrorInvalidValue;
+    const int len = g.mode == 0 ? g.n : ((g.n + 15) >> 4) * (((g.k + 3) & ~3) >> 2) * 64;
+    if (g.dst + len > total) return (int)hipErrorInvalidValue;
+    a.seg[i] = g;
+  }
+  a.nseg = nseg; a.total = total;
+  hipLaunchKernelGGL(mcaq_pack_kernel, dim3((total + 255) / 256), dim3(256), 0, stream, a, out);
+  return (int)hipGetLastError();
+}
 
 int mcaq_smask_train_backward(const mcaq_smask_params* P, const float* bits, const float* absmean, const float* gm,
                               int B, int H, int W, int ht, int wt, float* gbits, int accumulate, float* gparams,
@@ -857,8 +1082,9 @@ int mcaq_smask_train_backward(const mcaq_smask_params* P, const float* bits, con
   A.P = *P; A.bits = bits; A.absmean = absmean; A.gm = gm; A.gbits = gbits; A.gpart = gpart;
   A.B = B; A.H = H; A.W = W; A.ht = ht; A.wt = wt; A.accumulate = accumulate;
   const int NT = ht * wt;
-  const size_t lb = ((size_t)19 * NT + 64) * sizeof(float);
-  if (lb > 160 * 1024 - 1024) return (int)hipErrorInvalidValue;
+  const size_t lb = ((size_t)20 * NT + 64 + (size_t)H * wt + (size_t)H * W) * sizeof(float) +   // + tv
+                    (size_t)2 * (ht + wt) * sizeof(int);
+  if (lb > 160 * 1024 - 1024) return (int)hipErrorInvalidValue;   // m(p) gradient of one image staged in LDS
   static int set = 0;
   if ((int)lb > set) {
     const hipError_t e = hipFuncSetAttribute((const void*)mcaq_smask_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -866,7 +1092,7 @@ int mcaq_smask_train_backward(const mcaq_smask_params* P, const float* bits, con
     if (e != hipSuccess) return (int)e;
     set = 160 * 1024 - 1024;
   }
-  hipLaunchKernelGGL(mcaq_smask_bwd_kernel, dim3(B), dim3(256), lb, stream, A);
+  hipLaunchKernelGGL(mcaq_smask_bwd_kernel, dim3(B), dim3(SM_TH), lb, stream, A);
   hipLaunchKernelGGL(mcaq_tr_reduce_kernel, dim3(1), dim3(256), 0, stream, (const float*)gpart, B, (int)SG_SIZE,
                      (int)SG_SIZE, gparams, 0);
   return (int)hipGetLastError();

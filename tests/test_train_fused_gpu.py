@@ -167,3 +167,43 @@ def test_fused_softmask_backward_vs_autograd():
         _rel(b1.grad, b0.grad, 1e-4)
         for a, p in zip(g_fused, sm.net.parameters()):
             _rel(a, p.grad, 1e-4)
+
+
+def test_device_pack_equals_torch_pack():
+    """mcaq_pack (one launch) builds the complexity-MLP and soft-mask blobs
+    bit-identically to the torch packing (cat / zeros / MFMA operand index)
+    that the CPU modules use."""
+    import copy
+    from mcaq_yolo_amd import core
+    torch.manual_seed(3)
+    an = core.MorphologicalComplexityAnalyzer(device="cpu")
+    sm = core.LearnedSoftMask()
+    for p in list(an.parameters()) + list(sm.parameters()):
+        with torch.no_grad():
+            p.add_(0.01 * torch.randn_like(p))
+    ref_c = core._pack_cmlp(an.complexity_mlp)
+    ref_s = core._pack_softmask(sm.net)
+    gpu_c = core._pack_cmlp(copy.deepcopy(an.complexity_mlp).to(DEV))
+    gpu_s = core._pack_softmask(copy.deepcopy(sm.net).to(DEV))
+    assert gpu_c.is_cuda and gpu_c.shape == ref_c.shape
+    assert torch.equal(gpu_c.cpu(), ref_c)
+    assert torch.equal(gpu_s.cpu(), ref_s)
+
+
+def test_direct_grad_accumulation_matches_autograd_return():
+    """core.DIRECT_GRAD_ACCUM: the shared modules' gradients of the three
+    scales accumulated by the fused kernels into .grad equal the ones
+    returned to autograd (and summed by it)."""
+    from mcaq_yolo_amd import core
+    res = {}
+    for direct in (True, False):
+        old = core.DIRECT_GRAD_ACCUM
+        core.DIRECT_GRAD_ACCUM = direct
+        try:
+            o, a, gx, g, b = _step(True, B=2, seed=11)
+            res[direct] = g
+        finally:
+            core.DIRECT_GRAD_ACCUM = old
+    assert set(res[True]) == set(res[False])
+    for k in res[False]:
+        _rel(res[True][k], res[False][k], 1e-5, floor=1e-12)
