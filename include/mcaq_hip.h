@@ -134,6 +134,10 @@ int mcaq_morph(const mcaq_morph_scale* scales, int nscales, hipStream_t stream);
 int mcaq_morph_finalize(const mcaq_morph_scale* scales, int nscales,
                         const mcaq_finalize_scale* fscales, int nfscales, hipStream_t stream);
 size_t mcaq_morph_scratch_bytes(int B, int Hc, int Wc, int ht, int wt);
+/* Global plane scratch of one scale when a launch runs with planes in global
+ * memory (the mode is common to a launch's scales: every scale needs this
+ * buffer as soon as one scale's mcaq_morph_scratch_bytes is non-zero). */
+size_t mcaq_morph_scratch_bytes_global(int B, int Hc, int Wc);
 
 /* ---- pass 2: y = dequant(quant_b(x)) * m ----------------------------------- */
 typedef struct {

@@ -78,7 +78,8 @@ F_CONT, F_HAS_T, F_NORM_C, F_MAP_LINEAR = 16, 32, 64, 128
 F_BIN_OTSU, F_NO_EULER, F_CANNY_LEGACY = 256, 512, 1024
 
 EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats", "mcaq_stats_units",
-           "mcaq_finalize", "mcaq_morph", "mcaq_morph_finalize", "mcaq_morph_scratch_bytes", "mcaq_quant",
+           "mcaq_finalize", "mcaq_morph", "mcaq_morph_finalize", "mcaq_morph_scratch_bytes", "mcaq_morph_scratch_bytes_global",
+           "mcaq_quant",
            "mcaq_qat_forward", "mcaq_qat_backward", "mcaq_qat_work_floats", "mcaq_ema_stats",
            "mcaq_nms", "mcaq_nms_work_floats", "mcaq_time_next_launch", "mcaq_time_launch",
            "mcaq_morph_pass", "mcaq_pipeline_create", "mcaq_pipeline_destroy", "mcaq_pipeline_stream",
@@ -133,6 +134,8 @@ def _declare(lib):
     lib.mcaq_stats_units.argtypes = [I, I, I, I]
     lib.mcaq_morph_scratch_bytes.restype = ctypes.c_size_t
     lib.mcaq_morph_scratch_bytes.argtypes = [I, I, I, I, I]
+    lib.mcaq_morph_scratch_bytes_global.restype = ctypes.c_size_t
+    lib.mcaq_morph_scratch_bytes_global.argtypes = [I, I, I]
     lib.mcaq_qat_work_floats.restype = ctypes.c_size_t
     lib.mcaq_qat_work_floats.argtypes = [I, I, I, I]
     lib.mcaq_ema_stats.restype = I

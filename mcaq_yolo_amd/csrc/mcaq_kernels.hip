@@ -30,6 +30,10 @@ namespace mcaq { __device__ unsigned long long g_mcaq_stamps[64]; }
 extern "C" int mcaq_read_stamps(unsigned long long* out) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(mcaq::g_mcaq_stamps), sizeof(mcaq::g_mcaq_stamps));
 }
+extern "C" int mcaq_reset_stamps(void) {
+  static const unsigned long long z[64] = {};
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(mcaq::g_mcaq_stamps), z, sizeof(z));
+}
 #endif
 
 // ---------------------------------------------------------------------------
@@ -935,6 +939,10 @@ static int morph_ipw(const MorphScale& S, int mode, int limit) {
   return ipw;
 }
 
+size_t mcaq_morph_scratch_bytes_global(int B, int Hc, int Wc) {
+  return (size_t)2 * B * ((plane_bytes(Hc, Wc) + 15) & ~15);   // edge + mask workgroup per image
+}
+
 size_t mcaq_morph_scratch_bytes(int B, int Hc, int Wc, int ht, int wt) {
   MorphScale s{};
   s.Hc = Hc; s.Wc = Wc; s.ht = ht; s.wt = wt; s.H = 2 * Hc; s.W = 2 * Wc;  // conservative: H < Hc + tile
@@ -1008,7 +1016,7 @@ static int morph_launch_config(const mcaq_morph_scale* scales, int nscales, cons
       if (!mode && !S.gscratch) return (int)hipErrorInvalidValue;
       const int pb = (plane_bytes(S.Hc, S.Wc) + 15) & ~15;
       a.ipw[i] = morph_ipw(S, mode, limit);
-      a.pstride[i] = mode ? pb : stride;
+      a.pstride[i] = pb;   // this scale's own plane bytes (global scratch: 2 B of them, mcaq_morph_scratch_bytes_global)
       a.gstride[i] = (mode ? pb : 0) + fixed_bytes();
       dyn = imax_((int)dyn, a.ipw[i] * a.gstride[i]);
       wg += 2 * ((S.B + a.ipw[i] - 1) / a.ipw[i]);

@@ -47,7 +47,7 @@ typedef const __attribute__((address_space(3))) float* lds_cf;
 typedef __attribute__((address_space(3))) float* lds_f;
 
 // diagnostic build only (-DMCAQ_STAMPS): wave-level cycle stamps (no barrier)
-#if defined(MCAQ_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
+#if defined(MCAQ_STAMPS) && !defined(MCAQ_STAMPS_ACC) && defined(__HIP_DEVICE_COMPILE__)
 #define WSTAMP(on, k) do { if ((on) && (threadIdx.x & 63) == 0) g_mcaq_stamps[(k)] = __builtin_amdgcn_s_memtime(); } while (0)
 #else
 #define WSTAMP(on, k) do {} while (0)

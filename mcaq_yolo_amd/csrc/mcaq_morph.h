@@ -123,7 +123,24 @@ struct Ctx { int tid, nthr; };
        _i += ctx.nthr, r_ += _dr, c_ += _dc, r_ += (c_ >= (cols)), c_ -= (c_ >= (cols)) ? (cols) : 0)
 
 // diagnostic build only (-DMCAQ_STAMPS): per-stage cycle stamps of workgroup 0
-#if defined(MCAQ_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
+#if defined(MCAQ_STAMPS) && defined(MCAQ_STAMPS_ACC) && defined(__HIP_DEVICE_COMPILE__)
+// accumulating variant (-DMCAQ_STAMPS_ACC): slot k sums, over every launch,
+// the cycles from the previous stamp to stamp k of scale 0's image 0
+// (tools/probe/stamps_contended.py: stage times inside the pipelined step)
+extern __device__ unsigned long long g_mcaq_stamps[64];
+#define MSTAMP_INIT(base)                                                           \
+  const int mstamp_base = (S.block_begin == 0) ? (base) : -1;                        \
+  unsigned long long mstamp_last = __builtin_amdgcn_s_memtime()
+#define MSTAMP(k)                                                                   \
+  do {                                                                              \
+    __syncthreads();                                                                \
+    if (ctx.tid == 0 && mstamp_base >= 0) {                                         \
+      const unsigned long long now_ = __builtin_amdgcn_s_memtime();                 \
+      atomicAdd(&g_mcaq_stamps[mstamp_base + (k)], now_ - mstamp_last);             \
+      mstamp_last = now_;                                                           \
+    }                                                                               \
+  } while (0)
+#elif defined(MCAQ_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
 extern __device__ unsigned long long g_mcaq_stamps[64];
 #define MSTAMP_INIT(base) const int mstamp_base = (base)
 #define MSTAMP(k)                                                                   \

@@ -79,6 +79,9 @@ class HookPlan:
         self.lib = abi.lib()
         d = self.device
         self.bufs = []
+        # planes in global memory for every scale when one scale's planes
+        # exceed the LDS budget (the mode is common to a launch's scales)
+        glob = any(self.lib.mcaq_morph_scratch_bytes(g.B, g.Hc, g.Wc, g.ht, g.wt) for g in self.geoms)
         for g in self.geoms:
             units = self.lib.mcaq_stats_units(g.B, g.C, g.H, g.W)
             nb = {}
@@ -102,7 +105,7 @@ class HookPlan:
                 nb["binmask"] = torch.empty(g.B, g.Hc, g.Wc, device=d, dtype=torch.uint8)
             else:
                 nb["edge"] = nb["binmask"] = None
-            sb = self.lib.mcaq_morph_scratch_bytes(g.B, g.Hc, g.Wc, g.ht, g.wt)
+            sb = self.lib.mcaq_morph_scratch_bytes_global(g.B, g.Hc, g.Wc) if glob else 0
             nb["gscratch"] = torch.empty(max(sb, 16), device=d, dtype=torch.uint8) if sb else None
             self.bufs.append(nb)
 

@@ -143,6 +143,19 @@ def test_mcaq_yolo_graph_capture_and_nms():
     """The whole e2e inference step (network + 3 hooks + NMS) captured as one
     HIP graph replays to the eager result."""
     from mcaq_yolo_amd.postprocess import nms_padded
+    # MIOpen may pick convolution algorithms with run-to-run rounding
+    # differences (seen once in a full-suite run: the network output, and with
+    # it the hooks' inputs, differed between the eager and the replayed step);
+    # the property under test is the capture of the hook path + NMS
+    det = torch.backends.cudnn.deterministic
+    torch.backends.cudnn.deterministic = True
+    try:
+        _graph_capture_and_nms(nms_padded)
+    finally:
+        torch.backends.cudnn.deterministic = det
+
+
+def _graph_capture_and_nms(nms_padded):
     m = _mcaq_yolo("mlp")
     x = torch.rand(2, 3, 256, 256, generator=torch.Generator().manual_seed(5)).to(DEV)
 

@@ -116,6 +116,19 @@ def test_random_shapes_vs_oracle(dev, blobs, shape, grid):
     check_against_oracle(out, x, blobs[0], grid, "linear")
 
 
+def test_three_scales_global_planes(dev, blobs):
+    """A launch whose largest scale does not fit the LDS (160x160 at grid 8)
+    runs every scale with planes in global scratch, each at its own stride."""
+    rng = np.random.default_rng(7)
+    xs = []
+    for (C, S) in ((8, 160), (16, 80), (32, 40)):
+        x = (rng.standard_normal((1, C, S, S)) * 1.5).astype(f32)
+        xs.append(np.where(x > 0, x, x * f32(0.1)).astype(f32))
+    outs = run_plan(dev, blobs, xs, 8, "mlp")
+    for o, x in zip(outs, xs):
+        check_against_oracle(o, x, blobs[0], 8, "mlp")
+
+
 def test_large_map_global_planes(dev, blobs):
     """t64_c1 (640x640, tile 64): planes do not fit LDS -> global workspace path."""
     d = load_case("t64_c1")
