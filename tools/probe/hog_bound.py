@@ -48,7 +48,10 @@ def graphs(fn):
 
 
 G = {"stream_only": graphs(lambda pl, s: (pl.launch_stats(s), pl.launch_quant(s))),
-     "full": graphs(lambda pl, s: pl.launch(s))}
+     "full": graphs(lambda pl, s: pl.launch(s)),
+     "morph_only": graphs(lambda pl, s: pl.launch_morph(s))}
+VARIANTS = sys.argv[1].split(",") if len(sys.argv) > 1 else ["stream_only", "full"]
+HOGS = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0, 32, 64, 104, 128, 160]
 
 
 def run(gs, K):
@@ -57,8 +60,8 @@ def run(gs, K):
             gs[i % 3].replay()
 
 
-for v in ("stream_only", "full"):
-    for nh in (0, 32, 64, 104, 128, 160):
+for v in VARIANTS:
+    for nh in HOGS:
         run(G[v], 30)
         torch.cuda.synchronize()
         if nh:
