@@ -14,10 +14,14 @@ roundf, so this op and SpatialAdaptiveQuantization._forward_pytorch agree
 bit-for-bit.
 
 To let the unmodified reference pick it up (`import mcaq_cuda_ops` at
-core/quantization.py:14-23) call `install()` before importing it.
+core/quantization.py:14-23) call `install()` before importing it.  The
+launch itself is the torch.library operator `torch.ops.mcaq.spatial_quantize`
+(with a fake implementation), so graphs that call it can be traced by
+torch.compile / torch.export.
 """
 import ctypes
 import sys
+from typing import Optional
 
 import torch
 
@@ -55,10 +59,24 @@ def spatial_quantize(input, bit_map, min_vals, max_vals, tile_h, tile_w, mask=No
         mptr = ctypes.c_void_p(mask.data_ptr())
     if bit_map.shape[0] != N:
         raise RuntimeError("bit_map batch %d != input batch %d" % (bit_map.shape[0], N))
+    return torch.ops.mcaq.spatial_quantize(input, bit_map, min_vals, max_vals, int(tile_h), int(tile_w), mask)
+
+
+# The launch as a torch.library operator (mcaq::spatial_quantize), so the
+# call is an opaque node that torch.compile / torch.export / FakeTensor
+# tracing can carry (its fake implementation gives the output's shape, dtype
+# and device); the checks above run in Python before it, on real or fake
+# tensors alike.
+@torch.library.custom_op("mcaq::spatial_quantize", mutates_args=())
+def _spatial_quantize_op(input: torch.Tensor, bit_map: torch.Tensor, min_vals: torch.Tensor,
+                         max_vals: torch.Tensor, tile_h: int, tile_w: int,
+                         mask: Optional[torch.Tensor]) -> torch.Tensor:
     out = torch.empty_like(input)
     if out.numel() == 0:
         return out
+    N, C, H, W = input.shape
     n_th, n_tw = int(bit_map.shape[1]), int(bit_map.shape[2])
+    mptr = ctypes.c_void_p(mask.data_ptr()) if mask is not None else None
     err = abi.lib().mcaq_launch_spatial_quantization(
         ctypes.c_void_p(input.data_ptr()), ctypes.c_void_p(bit_map.data_ptr()),
         ctypes.c_void_p(min_vals.data_ptr()), ctypes.c_void_p(max_vals.data_ptr()), mptr,
@@ -66,6 +84,11 @@ def spatial_quantize(input, bit_map, min_vals, max_vals, tile_h, tile_w, mask=No
         ctypes.c_void_p(torch.cuda.current_stream(input.device).cuda_stream))
     abi.check(err, "mcaq_launch_spatial_quantization")
     return out
+
+
+@_spatial_quantize_op.register_fake
+def _spatial_quantize_fake(input, bit_map, min_vals, max_vals, tile_h, tile_w, mask):
+    return torch.empty_like(input)
 
 
 def install():

@@ -159,6 +159,29 @@ def test_cuda_kernel_parity():
         assert torch.equal(y, y2)
 
 
+def test_spatial_quantize_traceable():
+    """mcaq_cuda_ops.spatial_quantize is the torch.library op
+    mcaq::spatial_quantize: torch.export and torch.compile (aot_eager, no code
+    generation) trace a module that calls it into one opaque node, and the
+    traced programs give the eager numbers."""
+    from mcaq_yolo_amd import mcaq_cuda_ops
+
+    class Q(torch.nn.Module):
+        def forward(self, x, bits, mn, mx):
+            return mcaq_cuda_ops.spatial_quantize(x, bits, mn, mx, 4, 4) * 2.0
+
+    g = torch.Generator().manual_seed(4)
+    x = torch.randn(2, 8, 16, 16, generator=g).to(DEV)
+    bits = (torch.rand(2, 4, 4, generator=g) * 6 + 2).round().to(DEV)
+    mn, mx = x.amin(dim=(0, 2, 3)).contiguous(), x.amax(dim=(0, 2, 3)).contiguous()
+    ref = Q()(x, bits, mn, mx)
+    ep = torch.export.export(Q(), (x, bits, mn, mx))
+    assert any("mcaq.spatial_quantize" in str(n.target) for n in ep.graph.nodes)
+    assert torch.equal(ep.module()(x, bits, mn, mx), ref)
+    comp = torch.compile(Q(), backend="aot_eager", fullgraph=True)
+    assert torch.equal(comp(x, bits, mn, mx), ref)
+
+
 def test_spatial_quantize_errors():
     """mcaq_ops.cpp:37-46 checks raise RuntimeError."""
     from mcaq_yolo_amd import mcaq_cuda_ops
