@@ -307,12 +307,17 @@ typedef struct {
 size_t mcaq_mapper_work_floats(int n);
 int mcaq_mapper_train_forward(const mcaq_mapper_params* P, const float* c, int n, float min_bits, float max_bits,
                               float temperature, float momentum, int round_bits, int update_stats, float* bits,
-                              float* work, hipStream_t stream);
+                              float* work, unsigned* grid_sync, hipStream_t stream);
 /* gc (n), gparams (4609: mapping_network parameters() order); 5 launches */
 size_t mcaq_mapper_gpart_floats(int n);
 int mcaq_mapper_train_backward(const mcaq_mapper_params* P, const float* c, int n, const float* gbits,
                                float min_bits, float max_bits, float temperature, float* work, float* gc,
-                               float* gparams, float* gpart, int accumulate, hipStream_t stream);
+                               float* gparams, float* gpart, int accumulate, unsigned* grid_sync,
+                               hipStream_t stream);
+/* grid_sync: NULL (one launch per batch-statistics barrier), or 2 zeroed
+ * uint32 that launches on one stream share (each launch leaves them zeroed):
+ * forward and backward then run as ONE launch each, with grid-wide barriers
+ * between the stages (n <= 256 * 64 tiles). */
 /* analyzer head: gC (B, ht, wt) -> gcraw (B, ht, wt) work, gparams (2881:
  * complexity_mlp parameters() order); phi (B*ht*wt, 8), craw = the MLP output
  * before the bilateral; 3 launches */

@@ -154,9 +154,9 @@ def _declare(lib):
         getattr(lib, n).restype = SZ
         getattr(lib, n).argtypes = [I]
     lib.mcaq_mapper_train_forward.restype = I
-    lib.mcaq_mapper_train_forward.argtypes = [ctypes.POINTER(MapperParams), P, I, Fl, Fl, Fl, Fl, I, I, P, P, P]
+    lib.mcaq_mapper_train_forward.argtypes = [ctypes.POINTER(MapperParams), P, I, Fl, Fl, Fl, Fl, I, I, P, P, P, P]
     lib.mcaq_mapper_train_backward.restype = I
-    lib.mcaq_mapper_train_backward.argtypes = [ctypes.POINTER(MapperParams), P, I, P, Fl, Fl, Fl, P, P, P, P, I, P]
+    lib.mcaq_mapper_train_backward.argtypes = [ctypes.POINTER(MapperParams), P, I, P, Fl, Fl, Fl, P, P, P, P, I, P, P]
     lib.mcaq_head_train_backward.restype = I
     lib.mcaq_head_train_backward.argtypes = [ctypes.POINTER(CmlpParams), P, P, P, I, I, I, P, P, P, I, P]
     lib.mcaq_ema_stats_ex.restype = I

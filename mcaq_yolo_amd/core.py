@@ -877,6 +877,32 @@ class _HeadTrainFn(torch.autograd.Function):
         return (None, None) + tuple(_split_flat(gflat, params))
 
 
+# one-launch train-mode mapper (grid barriers between its batch-statistics
+# stages) instead of one launch per stage: measured slower at config 5 (the
+# agent-scope release / acquire around each barrier costs more than a kernel
+# boundary: forward 46.7 vs 37.6 us, backward 68.7 vs ~55 us per scale,
+# profiles/r03_qat/one_launch_mapper_ab.txt), so off by default
+MAPPER_ONE_LAUNCH = False
+_GRID_SYNC = {}
+
+
+def _grid_sync_counter(device):
+    """Zeroed uint32 pair for the mapper's grid barriers: one persistent buffer
+    per (device, stream) - launches on one stream run one after another and
+    each leaves it zeroed; launches on different streams get different
+    buffers.  Created inside a graph capture, the buffer's zero fill is
+    captured too (every replay re-zeroes it).  None when MAPPER_ONE_LAUNCH is
+    off (multi-launch path)."""
+    if not MAPPER_ONE_LAUNCH:
+        return None
+    key = (torch.device(device), torch.cuda.current_stream(device).cuda_stream)
+    buf = _GRID_SYNC.get(key)
+    if buf is None:
+        buf = torch.zeros(2, dtype=torch.int32, device=device)
+        _GRID_SYNC[key] = buf
+    return buf
+
+
 class _MapperTrainFn(torch.autograd.Function):
     """ComplexityToBitMappingNetwork in train mode (batch-statistics
     BatchNorm, running stats updated, straight-through clamp / round) on the
@@ -903,7 +929,8 @@ class _MapperTrainFn(torch.autograd.Function):
         bits = torch.empty(n, device=c.device)
         abi.check(L.mcaq_mapper_train_forward(ctypes.byref(q), _p(cf), n, mod.min_bits, mod.max_bits, T,
                                               float(bns[0].momentum), 0 if return_continuous else 1, 1, _p(bits),
-                                              _p(work), _stream()), "mcaq_mapper_train_forward")
+                                              _p(work), _p(_grid_sync_counter(c.device)), _stream()),
+                  "mcaq_mapper_train_forward")
         ctx.q, ctx.T, ctx.mod = q, T, mod
         ctx.save_for_backward(cf, work, *params)
         return bits.view(c.shape)
@@ -921,7 +948,8 @@ class _MapperTrainFn(torch.autograd.Function):
         gpart = torch.empty(L.mcaq_mapper_gpart_floats(n), device=cf.device)
         abi.check(L.mcaq_mapper_train_backward(ctypes.byref(ctx.q), _p(cf), n, _p(_f32c(gbits)), mod.min_bits,
                                                mod.max_bits, ctx.T, _p(work), _p(gc), _p(gflat), _p(gpart), acc,
-                                               _stream()), "mcaq_mapper_train_backward")
+                                               _p(_grid_sync_counter(cf.device)), _stream()),
+                  "mcaq_mapper_train_backward")
         if sink is not None:
             return (None, gc.view(gbits.shape), None, None) + (None,) * len(params)
         return (None, gc.view(gbits.shape), None, None) + tuple(_split_flat(gflat, params))

@@ -150,6 +150,7 @@ __device__ __forceinline__ void map_bn(const mcaq_mapper_params& P, int L, const
 }
 
 constexpr int MW = 8;               // waves per mapper workgroup (lane = tile, waves split the features)
+constexpr int MAPPER_COOP_MAX_WG = 256;   // one-launch (grid-barrier) mapper up to this many workgroups
 constexpr int MTH = 64 * MW;
 
 // per-workgroup (mean, M2) of feature j over this workgroup's valid tiles;
@@ -222,11 +223,18 @@ __device__ void map_stats(const MapperTrainArgs& A, const MapperWork& W, float* 
 }
 
 // stage S (1..4) of the train-mode forward
+struct MapFwdLds {
+  float in[TR_TPB][65];     // this workgroup's tiles' layer inputs
+  float mean[64], rstd[64];
+  float tmp[MW * 192];
+};
+
 template <int S>
-__global__ __launch_bounds__(MTH) void mcaq_mapper_fwd_kernel(MapperTrainArgs A) {
-  __shared__ float s_in[TR_TPB][65];     // this workgroup's tiles' layer inputs
-  __shared__ float s_mean[64], s_rstd[64];
-  __shared__ float s_tmp[MW * 192];
+__device__ __forceinline__ void mapper_fwd_stage(const MapperTrainArgs& A, MapFwdLds& L) {
+  float (*s_in)[65] = L.in;
+  float* s_mean = L.mean;
+  float* s_rstd = L.rstd;
+  float* s_tmp = L.tmp;
   const MapperWork W = mapper_work(A.work, A.n);
   const mcaq_mapper_params& P = A.P;
   const int tid = threadIdx.x, lane = tid & 63, q = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -295,6 +303,57 @@ __global__ __launch_bounds__(MTH) void mcaq_mapper_fwd_kernel(MapperTrainArgs A)
   }
 }
 
+template <int S>
+__global__ __launch_bounds__(MTH) void mcaq_mapper_fwd_kernel(MapperTrainArgs A) {
+  __shared__ MapFwdLds L;
+  mapper_fwd_stage<S>(A, L);
+}
+
+// grid-wide barrier of a launch whose workgroups are all resident (the mapper
+// grids are n / 64 <= a few hundred 512-thread workgroups): every wave
+// releases its writes at agent scope, one thread counts in and waits, every
+// wave acquires.  `bar` is a persistent zeroed counter the launch leaves
+// zeroed (mapper_grid_exit); a bounded spin never hangs the GPU.
+__device__ __forceinline__ void mapper_grid_sync(unsigned* bar, unsigned target) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned spins = 0;
+    while (__hip_atomic_load(bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target && spins < (1u << 24)) {
+      __builtin_amdgcn_s_sleep(1);
+      ++spins;
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+}
+
+// the last workgroup out resets the counters for the next launch on the stream
+__device__ __forceinline__ void mapper_grid_exit(unsigned* bar, int nwg) {
+  if (threadIdx.x == 0) {
+    const unsigned out = __hip_atomic_fetch_add(bar + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (out == (unsigned)nwg - 1) {
+      __hip_atomic_store(bar, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(bar + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// the four forward stages in one launch, grid barriers between them
+__global__ __launch_bounds__(MTH) void mcaq_mapper_fwd_coop_kernel(MapperTrainArgs A, unsigned* bar) {
+  __shared__ MapFwdLds L;
+  const unsigned n = (unsigned)A.nwg;
+  mapper_fwd_stage<1>(A, L);
+  mapper_grid_sync(bar, n);
+  mapper_fwd_stage<2>(A, L);
+  mapper_grid_sync(bar, 2 * n);
+  mapper_fwd_stage<3>(A, L);
+  mapper_grid_sync(bar, 3 * n);
+  mapper_fwd_stage<4>(A, L);
+  mapper_grid_exit(bar, A.nwg);
+}
+
 // backward stage S (4, 3, 2, 1): gradient of layer S's output activation ->
 // (BN S-1 backward inputs, weight partials of layer S)
 //   S = 4: g_bits -> g_a4 -> g_h3 -> g_y3 (through ReLU), partials of W4 / b4
@@ -302,12 +361,22 @@ __global__ __launch_bounds__(MTH) void mcaq_mapper_fwd_kernel(MapperTrainArgs A)
 //   S = 3, 2: g_y(S) + BN(S) sums -> g_a(S) -> W(S) / b(S) / BN(S) gamma-beta
 //          partials, g_h(S-1) -> g_y(S-1), BN(S-1) partials
 //   S = 1: g_y1 + BN1 sums -> g_a1 -> W1 / b1 partials, g_z -> g_c
+struct MapBwdLds {
+  float h[TR_TPB][65];     // this layer's input activations h(S-1)
+  float g[TR_TPB][65];     // gradient of this layer's pre-activation a(S)
+  float mean[64], rstd[64], sg[64], sgx[64];
+  float tmp[MW * 128];
+};
+
 template <int S>
-__global__ __launch_bounds__(MTH) void mcaq_mapper_bwd_kernel(MapperTrainArgs A) {
-  __shared__ float s_h[TR_TPB][65];     // this layer's input activations h(S-1)
-  __shared__ float s_g[TR_TPB][65];     // gradient of this layer's pre-activation a(S)
-  __shared__ float s_mean[64], s_rstd[64], s_sg[64], s_sgx[64];
-  __shared__ float s_tmp[MW * 128];
+__device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBwdLds& L) {
+  float (*s_h)[65] = L.h;
+  float (*s_g)[65] = L.g;
+  float* s_mean = L.mean;
+  float* s_rstd = L.rstd;
+  float* s_sg = L.sg;
+  float* s_sgx = L.sgx;
+  float* s_tmp = L.tmp;
   const MapperWork W = mapper_work(A.work, A.n);
   const mcaq_mapper_params& P = A.P;
   const int tid = threadIdx.x, lane = tid & 63, q = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -458,6 +527,35 @@ __global__ __launch_bounds__(MTH) void mcaq_mapper_bwd_kernel(MapperTrainArgs A)
       A.gc[t] = (craw >= 0.0f && craw <= 1.0f) ? gcv : 0.0f;
     }
   }
+}
+
+template <int S>
+__global__ __launch_bounds__(MTH) void mcaq_mapper_bwd_kernel(MapperTrainArgs A) {
+  __shared__ MapBwdLds L;
+  mapper_bwd_stage<S>(A, L);
+}
+
+// the four backward stages and the parameter reduction in one launch
+__global__ __launch_bounds__(MTH) void mcaq_mapper_bwd_coop_kernel(MapperTrainArgs A, unsigned* bar, float* gparams,
+                                                                   int accumulate) {
+  __shared__ MapBwdLds L;
+  const unsigned n = (unsigned)A.nwg;
+  mapper_bwd_stage<4>(A, L);
+  mapper_grid_sync(bar, n);
+  mapper_bwd_stage<3>(A, L);
+  mapper_grid_sync(bar, 2 * n);
+  mapper_bwd_stage<2>(A, L);
+  mapper_grid_sync(bar, 3 * n);
+  mapper_bwd_stage<1>(A, L);
+  mapper_grid_sync(bar, 4 * n);
+  // parameter gradients: sum of the workgroups' partials in workgroup order,
+  // each workgroup a slice of the flat vector
+  for (int e = (int)blockIdx.x * MTH + (int)threadIdx.x; e < MG_SIZE; e += (int)n * MTH) {
+    float sum = 0.0f;
+    for (int w = 0; w < A.nwg; ++w) sum += A.gpart[(size_t)w * MG_SIZE + e];
+    gparams[e] = accumulate ? gparams[e] + sum : sum;
+  }
+  mapper_grid_exit(bar, A.nwg);
 }
 
 // ============================================================================
@@ -987,7 +1085,7 @@ size_t mcaq_mapper_work_floats(int n) { return mcaq::mapper_work_floats(n); }
 
 int mcaq_mapper_train_forward(const mcaq_mapper_params* P, const float* c, int n, float min_bits, float max_bits,
                               float temperature, float momentum, int round_bits, int update_stats, float* bits,
-                              float* work, hipStream_t stream) {
+                              float* work, unsigned* grid_sync, hipStream_t stream) {
   using namespace mcaq;
   if (!P || !c || !bits || !work || n < 1) return (int)hipErrorInvalidValue;
   MapperTrainArgs A{};
@@ -995,6 +1093,10 @@ int mcaq_mapper_train_forward(const mcaq_mapper_params* P, const float* c, int n
   A.min_bits = min_bits; A.max_bits = max_bits; A.temperature = temperature; A.momentum = momentum;
   A.round_bits = round_bits; A.update_stats = update_stats;
   const dim3 g(A.nwg), t(MTH);
+  if (grid_sync && A.nwg <= MAPPER_COOP_MAX_WG) {
+    hipLaunchKernelGGL(mcaq_mapper_fwd_coop_kernel, g, t, 0, stream, A, grid_sync);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(mcaq_mapper_fwd_kernel<1>, g, t, 0, stream, A);
   hipLaunchKernelGGL(mcaq_mapper_fwd_kernel<2>, g, t, 0, stream, A);
   hipLaunchKernelGGL(mcaq_mapper_fwd_kernel<3>, g, t, 0, stream, A);
@@ -1004,7 +1106,8 @@ int mcaq_mapper_train_forward(const mcaq_mapper_params* P, const float* c, int n
 
 int mcaq_mapper_train_backward(const mcaq_mapper_params* P, const float* c, int n, const float* gbits,
                                float min_bits, float max_bits, float temperature, float* work, float* gc,
-                               float* gparams, float* gpart, int accumulate, hipStream_t stream) {
+                               float* gparams, float* gpart, int accumulate, unsigned* grid_sync,
+                               hipStream_t stream) {
   using namespace mcaq;
   if (!P || !c || !gbits || !gc || !gparams || !gpart || !work || n < 1) return (int)hipErrorInvalidValue;
   MapperTrainArgs A{};
@@ -1012,6 +1115,10 @@ int mcaq_mapper_train_backward(const mcaq_mapper_params* P, const float* c, int 
   A.nwg = (n + TR_TPB - 1) / TR_TPB;
   A.min_bits = min_bits; A.max_bits = max_bits; A.temperature = temperature;
   const dim3 g(A.nwg), t(MTH);
+  if (grid_sync && A.nwg <= MAPPER_COOP_MAX_WG) {
+    hipLaunchKernelGGL(mcaq_mapper_bwd_coop_kernel, g, t, 0, stream, A, grid_sync, gparams, accumulate ? 1 : 0);
+    return (int)hipGetLastError();
+  }
   hipLaunchKernelGGL(mcaq_mapper_bwd_kernel<4>, g, t, 0, stream, A);
   hipLaunchKernelGGL(mcaq_mapper_bwd_kernel<3>, g, t, 0, stream, A);
   hipLaunchKernelGGL(mcaq_mapper_bwd_kernel<2>, g, t, 0, stream, A);

@@ -207,3 +207,32 @@ def test_direct_grad_accumulation_matches_autograd_return():
     assert set(res[True]) == set(res[False])
     for k in res[False]:
         _rel(res[True][k], res[False][k], 1e-5, floor=1e-12)
+
+
+def test_mapper_one_launch_equals_staged_launches():
+    """The train-mode mapper as ONE launch per direction (grid barriers
+    between the batch-statistics stages) gives the values of the per-stage
+    launches: bits, c gradient, parameter gradients and running stats."""
+    from mcaq_yolo_amd import core
+    W = load_weights()
+    g = torch.Generator().manual_seed(21)
+    res = {}
+    for one in (True, False):
+        old = core.MAPPER_ONE_LAUNCH
+        core.MAPPER_ONE_LAUNCH = one
+        try:
+            m = core.ComplexityToBitMappingNetwork().to(DEV)
+            m.load_state_dict({k[len("bit_mapper."):]: torch.from_numpy(np.asarray(v))
+                               for k, v in W.items() if k.startswith("bit_mapper.")})
+            m.train()
+            torch.manual_seed(21)
+            c = torch.rand(5, 37, 41).to(DEV).requires_grad_(True)     # 7585 tiles: 119 workgroups
+            bits = m(c, 2.0, return_continuous=True)
+            bits.backward(torch.randn(bits.shape, generator=g.manual_seed(22)).to(DEV))
+            torch.cuda.synchronize()
+            res[one] = ([bits.detach().clone(), c.grad.clone()] + [p.grad.clone() for p in m.parameters()] +
+                        [b.clone() for b in m.buffers()])
+        finally:
+            core.MAPPER_ONE_LAUNCH = old
+    for a, b in zip(res[True], res[False]):
+        assert torch.equal(a, b)
