@@ -248,15 +248,52 @@ def _run_stats(x, gray=None, absmean=None, pmin=None, pmax=None, Hc=None, Wc=Non
     abi.check(abi.lib().mcaq_stats(ctypes.byref(s), 1, _stream()), "mcaq_stats")
 
 
+# Pass-1 sharing inside one hook call (train mode): the analyzer's pass 1
+# (gray) also writes |x| channel means and the channel min/max partials of the
+# same read, and the quantizer that follows on the same feature tensor
+# (unchanged: data pointer, version, shape) takes them instead of reading x
+# again.  One slot; False: every module runs its own pass 1.
+PASS1_SHARE = True
+_PASS1 = {"armed": False, "slot": None}
+
+
+class pass1_sharing:
+    """Scope of one hook call (MCAQHooks._run_scale_modules): inside it the
+    analyzer leaves its pass-1 by-products for the quantizer; outside it
+    nothing is cached (a recycled tensor address can never hit)."""
+
+    def __enter__(self):
+        _PASS1["armed"], _PASS1["slot"] = PASS1_SHARE, None
+        return self
+
+    def __exit__(self, *exc):
+        _PASS1["armed"], _PASS1["slot"] = False, None
+        return False
+
+
+def _pass1_key(x):
+    return (x.data_ptr(), x._version, tuple(x.shape), x.device, torch.cuda.current_stream(x.device).cuda_stream)
+
+
+def _pass1_lookup(x):
+    e = _PASS1["slot"]
+    return e if (_PASS1["armed"] and e is not None and e["key"] == _pass1_key(x)) else None
+
+
 def _channel_minmax(x, absmean=None):
     """Per-channel min/max over (batch, H, W) (quantization.py:650-654) by pass 1
-    + the finalize reduction; optionally the |x| channel mean in the same read."""
+    + the finalize reduction; optionally the |x| channel mean in the same read
+    (or both from the analyzer's pass 1 over the same tensor, _pass1_lookup)."""
     B, C, H, W = x.shape
     L = abi.lib()
     units = L.mcaq_stats_units(B, C, H, W)
-    pmin = torch.empty(units, C, device=x.device)
-    pmax = torch.empty(units, C, device=x.device)
-    _run_stats(x, absmean=absmean, pmin=pmin, pmax=pmax)
+    hit = _pass1_lookup(x)
+    if hit is not None and (absmean is None or absmean is hit["absmean"]):
+        pmin, pmax = hit["pmin"], hit["pmax"]
+    else:
+        pmin = torch.empty(units, C, device=x.device)
+        pmax = torch.empty(units, C, device=x.device)
+        _run_stats(x, absmean=absmean, pmin=pmin, pmax=pmax)
     xmin = torch.empty(C, device=x.device)
     xmax = torch.empty(C, device=x.device)
     f = abi.FinalizeScale()
@@ -334,7 +371,16 @@ class MorphologicalComplexityAnalyzer(nn.Module):
             raise ValueError("feature map %dx%d: tile %d unsupported" % (H, W, T))
         dev = x.device
         gray = torch.empty(B, ht * T, wt * T, device=dev)
-        _run_stats(x, gray=gray, Hc=ht * T, Wc=wt * T)
+        if _PASS1["armed"] and self.training:
+            # the quantizer of this hook reads the same x next: |x| means and
+            # min/max partials in the same pass (_pass1_lookup)
+            units = abi.lib().mcaq_stats_units(B, C, H, W)
+            e = {"key": _pass1_key(x), "absmean": torch.empty(B, H, W, device=dev),
+                 "pmin": torch.empty(units, C, device=dev), "pmax": torch.empty(units, C, device=dev)}
+            _run_stats(x, gray=gray, absmean=e["absmean"], pmin=e["pmin"], pmax=e["pmax"], Hc=ht * T, Wc=wt * T)
+            _PASS1["slot"] = e
+        else:
+            _run_stats(x, gray=gray, Hc=ht * T, Wc=wt * T)
         phi = torch.empty(B, ht, wt, 8, device=dev)
         flags = abi.F_PHI | self._flags()
         ptrs = dict(gray=gray, phi_out=phi, tile_tmp=torch.empty(B, ht * wt, 32, device=dev))
@@ -1217,12 +1263,13 @@ class SpatialAdaptiveQuantization(nn.Module):
         if bit_map.dim() != 3 or bit_map.shape[0] != B:
             raise AssertionError(f"Batch size mismatch: {B} vs {bit_map.shape[0]}")
         want_m = self.smooth_transitions and self.soft_mask is not None
-        absmean = torch.empty(B, H, W, device=x.device) if want_m else None
         xf = _f32c(x)
+        hit = _pass1_lookup(xf)
+        absmean = (hit["absmean"] if hit is not None else torch.empty(B, H, W, device=x.device)) if want_m else None
         frozen = self._frozen()
         copies = None
         if frozen:
-            if want_m:
+            if want_m and hit is None:
                 _run_stats(xf, absmean=absmean)
         else:
             copies = self.update_running_stats(xf, absmean, want_copies=self.training)

@@ -21,6 +21,7 @@ import torch.nn as nn
 
 from .core import (ComplexityToBitMappingNetwork, LinearBitMapper, MorphologicalComplexityAnalyzer,
                    SpatialAdaptiveQuantization)
+from . import core
 from .engine import HookPlan, ScaleGeom
 
 DEFAULT_INDICES = (4, 6, 9)   # models/mcaq_yolo.py:361 fallback (C3/C4/C5 of YOLOv8)
@@ -126,6 +127,12 @@ class MCAQHooks(nn.Module):
         bt = self.batch_total
         if not self.training and not feat.is_cuda and bt is not None and bt > B:
             return self._run_scale_shard_cpu(layer_idx, feat, state)
+        if feat.is_cuda:
+            with core.pass1_sharing():
+                return self._run_scale_modules_body(layer_idx, feat, state)
+        return self._run_scale_modules_body(layer_idx, feat, state)
+
+    def _run_scale_modules_body(self, layer_idx, feat, state):
         complexity = self.complexity_analyzer(feat)
         if self.normalize_complexity:
             B = complexity.shape[0]

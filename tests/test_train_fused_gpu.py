@@ -236,3 +236,26 @@ def test_mapper_one_launch_equals_staged_launches():
             core.MAPPER_ONE_LAUNCH = old
     for a, b in zip(res[True], res[False]):
         assert torch.equal(a, b)
+
+
+def test_pass1_sharing_equals_separate_passes():
+    """core.PASS1_SHARE: the quantizer taking the analyzer's |x| means and
+    min/max partials of the same read gives exactly the step of separate
+    pass-1 launches (outputs, feature gradients, parameter gradients, EMA
+    statistics)."""
+    from mcaq_yolo_amd import core
+    res = {}
+    for share in (True, False):
+        old = core.PASS1_SHARE
+        core.PASS1_SHARE = share
+        try:
+            res[share] = _step(True, B=2, seed=13)
+        finally:
+            core.PASS1_SHARE = old
+    (o1, a1, gx1, g1, b1), (o0, a0, gx0, g0, b0) = res[True], res[False]
+    for x, y in zip(o1 + gx1, o0 + gx0):
+        assert torch.equal(x, y)
+    for k in g0:
+        assert torch.equal(g1[k], g0[k]), k
+    for k in b0:
+        assert torch.equal(b1[k], b0[k]), k
