@@ -208,6 +208,41 @@ __device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, fl
   const int nblk = (C + ST_CG - 1) / ST_CG;
   const int rounds = (nblk + ST_WAVES - 1) / ST_WAVES;
 
+  // ---- tail columns (row_sum order), all in the image's last unit
+  const int tstart = imax_(aten_tail_start(HW), base);
+  const int tend = imin_(HW, base + UPIX);
+  const int ntail = tend - tstart;
+  const int nilp = C >> 2;                        // rows per interleaved cascade
+  const int nbt = (nilp + 15) >> 4;               // 16-row blocks per cascade
+#ifdef MCAQ_PROBE_STATS_NO_TAIL   // timing probe only (wrong tail sums): tools/probe/stats_probe.sh
+  const bool need_tail = false;
+#else
+  const bool need_tail = ntail > 0 && (want_a || (want_g && !cropped));
+#endif
+  const bool coop = nbt <= 16;                    // 31 px x 4 x 16 x 2 floats fit the LDS
+  const int titems = need_tail && coop ? ntail * 4 * nbt : 0;
+#ifdef MCAQ_STATS_TAIL_EARLY
+  // the tail's strided loads are issued before the channel rounds, so their
+  // latency overlaps the rounds' instead of following them (C <= 512)
+  constexpr int TE = 1;
+  const bool early = PPL == 1 && titems > 0 && titems <= TE * 256;   // the many-channel scales
+  float tv[TE][16];
+  if (early) {
+#pragma unroll
+    for (int e2 = 0; e2 < TE; ++e2) {
+      const int it = imin_(tid + e2 * 256, titems - 1);
+      const int i = it / (4 * nbt), rem = it - i * (4 * nbt);
+      const int k = rem / nbt, j = rem - k * nbt;
+      const int p = tstart + i;
+      const int r0 = 16 * j, n = imin_(16, nilp - r0);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) tv[e2][e] = xb[(size_t)(4 * (r0 + (e < n ? e : 0)) + k) * HW + p];
+    }
+  }
+#else
+  constexpr bool early = false;
+#endif
+
   Fold fg, fa;   // pixel `tid` (tid < UPIX)
   fg.init(); fa.init();
   // MR rounds of 16-row blocks are loaded before the first is reduced (MR * 16
@@ -304,24 +339,27 @@ __device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, fl
     }
   }
 
-  // ---- tail columns (row_sum order), all in the image's last unit
-  const int tstart = imax_(aten_tail_start(HW), base);
-  const int tend = imin_(HW, base + UPIX);
-  const int ntail = tend - tstart;
-  const int nilp = C >> 2;                        // rows per interleaved cascade
-  const int nbt = (nilp + 15) >> 4;               // 16-row blocks per cascade
-#ifdef MCAQ_PROBE_STATS_NO_TAIL   // timing probe only (wrong tail sums): tools/probe/stats_probe.sh
-  const bool need_tail = false;
-#else
-  const bool need_tail = ntail > 0 && (want_a || (want_g && !cropped));
-#endif
-  const bool coop = nbt <= 16;                    // 31 px x 4 x 16 x 2 floats fit the LDS
   float tg = 0.0f, ta = 0.0f;
   if (need_tail && coop) {
     float* tsg = lds;                             // [px][k][j]
     float* tsa = lds + ST_LDS / 2;
-    const int items = ntail * 4 * nbt;
-    for (int it = tid; it < items; it += 256) {
+    const int items = titems;
+#ifdef MCAQ_STATS_TAIL_EARLY
+    if (early) {
+#pragma unroll
+      for (int e2 = 0; e2 < TE; ++e2) {
+        const int it = tid + e2 * 256;
+        if (it < items) {
+          const int r0 = 16 * ((it % (4 * nbt)) % nbt), n = imin_(16, nilp - r0);
+          float sg = 0.0f, sa = 0.0f;
+#pragma unroll
+          for (int e = 0; e < 16; ++e) if (e < n) { sg = sg + tv[e2][e]; sa = sa + fabsf(tv[e2][e]); }
+          tsg[it] = sg; tsa[it] = sa;
+        }
+      }
+    }
+#endif
+    for (int it = early ? items : tid; it < items; it += 256) {
       const int i = it / (4 * nbt), rem = it - i * (4 * nbt);
       const int k = rem / nbt, j = rem - k * nbt;
       const int p = tstart + i;

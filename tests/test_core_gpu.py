@@ -263,6 +263,34 @@ def test_hooks_forward_features_vs_oracle():
     assert 2.0 <= float(avg) <= 8.0
 
 
+def test_hook_descriptor_reuse_equals_fresh_plan():
+    """Repeated eager hook calls reuse the plan's launch descriptors and only
+    rebind x and the fresh outputs: every call's outputs (kept, not copied)
+    equal those of a plan built from scratch for that call, and an option
+    change (temperature) rebuilds the descriptors."""
+    from mcaq_yolo_amd.hooks import MCAQHooks
+    torch.manual_seed(1)
+    h = MCAQHooks(device=DEV, indices=(4,)).eval()
+    xs = [torch.nn.functional.silu(2 * torch.randn(2, 16, 40, 40, device=DEV)) for _ in range(3)]
+    calls = [(xs[0], 1.0), (xs[1], 1.0), (xs[2], 1.0), (xs[0], 0.5), (xs[1], 0.5)]
+    got, sts = [], []
+    for x, T in calls:
+        aux = h.begin(temperature=T)
+        y = h.run_scale(4, x, h._mcaq_state)
+        h.end()
+        got.append((y, aux[0]["bit_map"], aux[0]["complexity"]))
+        plan, = h._plans.values()
+        sts.append(id(plan._st))
+    assert sts[0] == sts[1] == sts[2] and sts[3] != sts[2] and sts[3] == sts[4]
+    for (x, T), (y, bits, c) in zip(calls, got):
+        h._plans = {}
+        aux = h.begin(temperature=T)
+        ry = h.run_scale(4, x, h._mcaq_state)
+        h.end()
+        assert torch.equal(bits, aux[0]["bit_map"]) and torch.equal(c, aux[0]["complexity"])
+        assert torch.equal(y, ry)
+
+
 def test_hooks_on_a_module_chain():
     """register_forward_hook wiring: the hooked layer's output is replaced by the
     quantized map only while a forward is open (models/mcaq_yolo.py:409-455)."""

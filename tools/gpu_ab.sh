@@ -10,7 +10,7 @@ cp /tmp/base.so tools/probe/ab/base.so
 ok="base"
 for v in "$@"; do
   cp tools/probe/ab/$v.so $L
-  timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "golden_case or packed or three_scales or bench_config" > gpurun_out/ab/$v.pytest.log 2>&1
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "golden_case or packed or three_scales or bench_config or stats_pass" > gpurun_out/ab/$v.pytest.log 2>&1
   rc=$?; echo "$v pytest rc=$rc $(tail -1 gpurun_out/ab/$v.pytest.log)"
   if [ $rc -ne 0 ]; then grep -E "FAIL|assert" gpurun_out/ab/$v.pytest.log | head -5; continue; fi
   ok="$ok $v"
