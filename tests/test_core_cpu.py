@@ -104,3 +104,29 @@ def test_mfma_operand_packing_matches_host_packer():
     assert np.array_equal(a.cmlp_blob().numpy(), params.pack_complexity_mlp(params.sub(W, "complexity_analyzer.")))
     assert np.array_equal(m.mapper_blob().numpy(), params.pack_mapper_mlp(params.sub(W, "bit_mapper.")))
     assert np.array_equal(sm.blob().numpy(), params.pack_soft_mask(params.sub(W, "soft_mask.")))
+
+
+def test_plan_descriptor_signature():
+    """HookPlan._signature (descriptor reuse of eager hook calls): the
+    rebound outputs y / complexity / bits and x do not enter it; any other
+    buffer, blob, frozen min/max or option does, and a frozen min/max that
+    prepare() would copy disables reuse."""
+    from mcaq_yolo_amd.engine import HookPlan
+    p = HookPlan.__new__(HookPlan)
+    p.bufs = [{"y": torch.empty(8), "bits": torch.empty(2), "complexity": torch.empty(2),
+               "gray": torch.empty(4), "units": 3, "m": None}]
+    cm, mm, sm = torch.empty(5), torch.empty(6), torch.empty(7)
+    lo, hi = torch.empty(4), torch.empty(4)
+    opts = (1.0, "mlp", False)
+    s0 = p._signature(cm, mm, [sm], None, opts)
+    keep = [p.bufs[0]["y"], p.bufs[0]["bits"]]
+    p.bufs[0]["y"], p.bufs[0]["bits"] = torch.empty(8), torch.empty(2)
+    assert p._signature(cm, mm, [sm], None, opts) == s0
+    assert p._signature(cm, mm, [sm], None, (0.5, "mlp", False)) != s0
+    assert p._signature(cm, mm, [None], None, opts) != s0
+    assert p._signature(cm, mm, [sm], [(lo, hi)], opts) != s0
+    assert p._signature(cm, mm, [sm], [(lo, hi)], opts) == p._signature(cm, mm, [sm], [(lo, hi)], opts)
+    assert p._signature(cm, mm, [sm], [(lo.double(), hi)], opts) is None
+    keep.append(p.bufs[0]["gray"])
+    p.bufs[0]["gray"] = torch.empty(4)
+    assert p._signature(cm, mm, [sm], None, opts) != s0
