@@ -130,3 +130,60 @@ def test_plan_descriptor_signature():
     keep.append(p.bufs[0]["gray"])
     p.bufs[0]["gray"] = torch.empty(4)
     assert p._signature(cm, mm, [sm], None, opts) != s0
+
+
+def test_plan_descriptor_reuse_equals_rebuild(monkeypatch):
+    """HookPlan.prepare's reuse path (same blobs / buffers / options, new x
+    and new y / complexity / bits) leaves every descriptor field equal to a
+    full rebuild's.  Host-side only: plan buffers are CPU tensors, nothing
+    is launched."""
+    from mcaq_yolo_amd import engine
+    from mcaq_yolo_amd.engine import HookPlan, ScaleGeom
+    monkeypatch.setattr(engine, "_require_cuda", lambda *ts: None)
+    shapes = ((2, 16, 80, 80), (2, 32, 40, 40), (2, 64, 20, 20))
+    p = HookPlan.__new__(HookPlan)
+    p.geoms = [ScaleGeom(*s, 8) for s in shapes]
+    p.device = torch.device("cpu")
+    p.lib = None
+    p.bufs = []
+    for g in p.geoms:
+        b = {"units": 7}
+        for k in ("gray", "absmean", "pmin", "pmax", "xmin", "xmax", "complexity", "bits", "mt", "y", "phi",
+                  "tile_tmp", "cmlp"):
+            b[k] = torch.empty(4)
+        b["m"] = b["edge"] = b["binmask"] = b["gscratch"] = None
+        p.bufs.append(b)
+    cm, mm, sms = torch.empty(8), torch.empty(8), [torch.empty(8) for _ in shapes]
+
+    def snap():
+        out = {}
+        for name in ("_st", "_fz", "_mo", "_qs"):
+            arr = getattr(p, name)
+            for i in range(len(arr)):
+                for f, _ in arr[i]._fields_:
+                    v = getattr(arr[i], f)
+                    out[(name, i, f)] = list(v) if hasattr(v, "__len__") else v
+        return out
+
+    def fresh_io():
+        feats = [torch.empty(s) for s in shapes]
+        for b in p.bufs:
+            for k in HookPlan._REBOUND:
+                b[k] = torch.empty(4)
+        return feats
+
+    keep = []
+    for kw in ({}, {"temperature": 0.5, "per_tensor": True}, {"minmax": [(torch.empty(16), torch.empty(16)), None, None]}):
+        feats = fresh_io()
+        keep.append((feats, [dict(b) for b in p.bufs]))
+        p.prepare(feats, cm, mm, sms, **kw)
+        st0 = id(p._st)
+        feats = fresh_io()
+        keep.append((feats, [dict(b) for b in p.bufs]))
+        p.prepare(feats, cm, mm, sms, **kw)
+        assert id(p._st) == st0                      # reused
+        reused = snap()
+        p._sig = None
+        p.prepare(feats, cm, mm, sms, **kw)          # rebuilt from scratch
+        assert id(p._st) != st0
+        assert snap() == reused
