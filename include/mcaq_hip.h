@@ -339,7 +339,7 @@ int mcaq_smask_train_backward(const mcaq_smask_params* P, const float* bits, con
  * mode 1 writes the v_mfma_f32_16x16x4_f32 A operands of an (n, k) row-major
  * weight (ceil(n/16) blocks x ceil(k/4) steps x 64 lanes, zero padded);
  * out[0 .. total) not covered by a segment is zeroed.  One launch. */
-#define MCAQ_PACK_MAXSEG 16
+#define MCAQ_PACK_MAXSEG 24
 typedef struct {
   const float* src;
   int n, k, mode, dst;

@@ -60,7 +60,7 @@ class CmlpParams(ctypes.Structure):
     _fields_ = [(n, P) for n in ("w1", "b1", "g1", "be1", "w2", "b2", "g2", "be2", "w3", "b3")]
 
 
-MCAQ_PACK_MAXSEG = 16
+MCAQ_PACK_MAXSEG = 24
 
 
 class PackSeg(ctypes.Structure):

@@ -494,7 +494,8 @@ class MorphologicalComplexityAnalyzer(nn.Module):
             # value and its gradient reaches complexity_mlp through the fused
             # head backward (mcaq_head_train_backward) or, FUSED_TRAIN off, the
             # torch restatement of the MLP + bilateral
-            if FUSED_TRAIN:
+            ht, wt = _tile_grid(features.shape[-2], features.shape[-1], self.grid_size)
+            if FUSED_TRAIN and _head_bwd_fits(ht, wt):
                 out = _HeadTrainFn.apply(self, features, *self.complexity_mlp.parameters())
                 phi, c = self._last_phi, out
                 self._last_phi = None
@@ -818,7 +819,7 @@ class _SoftMaskFn(torch.autograd.Function):
         bit_map, absmean = ctx.saved_tensors
         mod = ctx.mod
         params = list(mod.net.parameters())
-        if FUSED_TRAIN:
+        if FUSED_TRAIN and _smask_bwd_fits(absmean.shape[-2], absmean.shape[-1], bit_map.shape[-2], bit_map.shape[-1]):
             return _smask_backward_fused(ctx, mod, bit_map, absmean, gm, params)
         with torch.enable_grad():
             b = bit_map.detach().requires_grad_(ctx.needs_input_grad[0])
@@ -837,6 +838,28 @@ class _SoftMaskFn(torch.autograd.Function):
 # False: the torch autograd restatement of the analyzer head, the train-mode
 # mapper and the soft-mask backward (the r02 path; A/B and cross-check)
 FUSED_TRAIN = True
+
+
+# LDS the fused train-mode backwards stage per workgroup (csrc/mcaq_train.h
+# launchers; the kernels take at most 159 KiB): when an image does not fit,
+# the call takes the torch restatement (the FUSED_TRAIN = False branch)
+_TRAIN_LDS_LIMIT = 160 * 1024 - 1024
+
+
+def _head_bwd_fits(ht, wt):
+    """mcaq_head_train_backward: 53 floats per tile of one image."""
+    return 53 * ht * wt * 4 <= _TRAIN_LDS_LIMIT
+
+
+def _smask_bwd_fits(H, W, ht, wt):
+    """mcaq_smask_train_backward: one image's m(p) gradient plus tile and
+    row tables."""
+    return (20 * ht * wt + 64 + H * wt + H * W) * 4 + 2 * (ht + wt) * 4 <= _TRAIN_LDS_LIMIT
+
+
+def _tile_grid(H, W, grid_size):
+    tile = tile_size(H, grid_size)
+    return H // tile, W // tile
 
 
 def _split_flat(flat, params):
@@ -859,6 +882,21 @@ def _split_flat(flat, params):
 DIRECT_GRAD_ACCUM = True
 
 
+def _grads_observed(params):
+    """True when something outside backward() must see these parameters'
+    gradients as autograd results: torch DDP's reducer (BASELINE config 5 is
+    DDP; it hooks every parameter's AccumulateGrad and would never see a
+    gradient written straight into .grad) or any parameter hook.  Direct
+    accumulation is then off and the gradients go back to autograd."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        return True
+    for p in params:
+        if getattr(p, "_backward_hooks", None) or getattr(p, "_post_accumulate_grad_hooks", None):
+            return True
+    return False
+
+
 class _GradSink:
     """Flat gradient storage for a module's parameters; `target(params)`
     returns (flat buffer, accumulate flag) for the next backward, or None when
@@ -871,6 +909,8 @@ class _GradSink:
 
     def target(self, params):
         if not DIRECT_GRAD_ACCUM or not all(p.requires_grad for p in params):
+            return None
+        if _grads_observed(params):
             return None
         n = sum(p.numel() for p in params)
         dev = params[0].device

@@ -81,23 +81,30 @@ def sync_mapper_batchnorm(mapper, process_group):
 def allreduce_gradients(params, process_group, average=True):
     """Average the gradients of `params` over the group with ONE collective:
     every parameter that requires grad goes into a single flat bucket in the
-    order given (a None grad contributes zeros), so every rank reduces
-    buffers of the same length and layout even when ranks disagree on which
-    grads are None; afterwards every such parameter holds the averaged
-    gradient (as DDP leaves it)."""
+    order given (a None grad contributes zeros), followed by one "has a
+    gradient" flag per parameter, so every rank reduces buffers of the same
+    length and layout even when ranks disagree on which grads are None.
+    Afterwards every parameter that had a gradient on some rank holds the
+    averaged gradient, and one whose grad was None on every rank keeps None
+    (as DDP leaves globally unused parameters: optimizers then skip them)."""
     import torch.distributed as dist
     ps = [p for p in params if p.requires_grad]
     if not ps:
         return
-    flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in ps])
+    has = [p.grad is not None for p in ps]
+    flags = torch.tensor(has, dtype=ps[0].dtype, device=ps[0].device)
+    flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in ps] + [flags])
     dist.all_reduce(flat, group=process_group)
     if average:
-        flat /= dist.get_world_size(process_group)
+        flat[:-len(ps)] /= dist.get_world_size(process_group)
+    any_grad = (flat[-len(ps):] > 0).tolist()
     o = 0
-    for p in ps:
+    for p, h_any in zip(ps, any_grad):
         n = p.numel()
         g = flat[o:o + n].view_as(p)
-        if p.grad is None:
+        if not h_any:
+            p.grad = None
+        elif p.grad is None:
             p.grad = g.clone()
         else:
             p.grad.copy_(g)

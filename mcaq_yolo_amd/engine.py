@@ -459,6 +459,12 @@ class HookPipeline:
         i0 = i_now if at is None else at
         if i0 < 3 or self.last is not None or nsteps < 1:
             raise ValueError("capture: steps from index >= 3 of an undrained pipeline")
+        if nsteps > len(self.plans) - 4:
+            # a longer capture would put a buffer-reuse edge (pass 1 of batch
+            # j after pass 2 of batch j - NP) inside the graph: two side
+            # streams waiting on each other's events, the topology whose
+            # hipStreamEndCapture segfaulted (capture_probe C2)
+            raise ValueError("capture: nsteps %d > len(plans) - 4 = %d" % (nsteps, len(self.plans) - 4))
         g = torch.cuda.CUDAGraph()
         self.i = i0
         abi.check(self.lib.mcaq_pipeline_set_step(self.handle, i0), "mcaq_pipeline_set_step")

@@ -51,12 +51,10 @@ def spatial_quantize(input, bit_map, min_vals, max_vals, tile_h, tile_w, mask=No
         raise RuntimeError("min_vals/max_vals must have one entry per channel (C=%d), got %d - expand "
                            "per-tensor stats before calling (see SpatialAdaptiveQuantization._forward_cuda)"
                            % (C, min_vals.numel()))
-    mptr = None
     if mask is not None:
         _check(mask, "mask")
         if mask.numel() != N * H * W:
             raise RuntimeError("mask must be (N, 1, H, W)")
-        mptr = ctypes.c_void_p(mask.data_ptr())
     if bit_map.shape[0] != N:
         raise RuntimeError("bit_map batch %d != input batch %d" % (bit_map.shape[0], N))
     return torch.ops.mcaq.spatial_quantize(input, bit_map, min_vals, max_vals, int(tile_h), int(tile_w), mask)

@@ -181,6 +181,19 @@ def test_spatial_quantize_traceable():
     comp = torch.compile(Q(), backend="aot_eager", fullgraph=True)
     assert torch.equal(comp(x, bits, mn, mx), ref)
 
+    # with a soft mask (the wrapper must not touch the mask's data
+    # pointer, which a FakeTensor does not have)
+    class QM(torch.nn.Module):
+        def forward(self, x, bits, mn, mx, m):
+            return mcaq_cuda_ops.spatial_quantize(x, bits, mn, mx, 4, 4, m) + 1.0
+
+    m = (torch.rand(2, 1, 16, 16, generator=g) * 0.5 + 0.5).to(DEV)
+    refm = QM()(x, bits, mn, mx, m)
+    epm = torch.export.export(QM(), (x, bits, mn, mx, m))
+    assert torch.equal(epm.module()(x, bits, mn, mx, m), refm)
+    compm = torch.compile(QM(), backend="aot_eager", fullgraph=True)
+    assert torch.equal(compm(x, bits, mn, mx, m), refm)
+
 
 def test_spatial_quantize_errors():
     """mcaq_ops.cpp:37-46 checks raise RuntimeError."""

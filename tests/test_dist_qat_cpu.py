@@ -185,14 +185,16 @@ def _none_grad_worker(rank, world):
         a.grad, c.grad = torch.full((3,), 1.0), torch.full((2,), 10.0)
     else:
         b.grad, c.grad = torch.full((5,), 2.0), torch.full((2,), 20.0)
-    mdist.allreduce_gradients([a, b, c], dist.group.WORLD)
-    return a.grad.numpy(), b.grad.numpy(), c.grad.numpy()
+    d = torch.nn.Parameter(torch.zeros(4))          # None on every rank
+    mdist.allreduce_gradients([a, b, d, c], dist.group.WORLD)
+    return a.grad.numpy(), b.grad.numpy(), c.grad.numpy(), d.grad
 
 
 def test_allreduce_gradients_ranks_disagree_on_none():
     res = _run("_none_grad_worker")
     for r in range(2):
-        a, b, c = res[r]
+        a, b, c, d = res[r]
+        assert d is None        # globally unused: stays None (optimizers skip it), as DDP leaves it
         assert np.array_equal(a, np.full(3, 0.5, np.float32))
         assert np.array_equal(b, np.full(5, 1.0, np.float32))
         assert np.array_equal(c, np.full(2, 15.0, np.float32))
@@ -222,3 +224,25 @@ def test_group_batchnorm_large_mean_two_ranks():
     for r in range(2):
         np.testing.assert_allclose(res[r][0], y[r * 32:(r + 1) * 32], rtol=1e-3, atol=2e-3)
         np.testing.assert_allclose(res[r][1], bn.running_var.numpy(), rtol=1e-3)
+
+
+def _sink_worker(rank, world):
+    from mcaq_yolo_amd import core
+    p = torch.nn.Parameter(torch.zeros(3))
+    return core._grads_observed([p]), core._GradSink().target([p]) is None
+
+
+def test_direct_grad_accumulation_off_under_torch_distributed():
+    """with torch.distributed initialised (DDP's reducer hooks every
+    parameter's AccumulateGrad) or a parameter hook registered, the fused
+    backwards return their gradients to autograd instead of writing .grad."""
+    from mcaq_yolo_amd import core
+    p = torch.nn.Parameter(torch.zeros(3))
+    assert not core._grads_observed([p])
+    p.register_hook(lambda g: g)
+    assert core._grads_observed([p])
+    q = torch.nn.Parameter(torch.zeros(3))
+    q.register_post_accumulate_grad_hook(lambda t: None)
+    assert core._grads_observed([q])
+    res = _run("_sink_worker")
+    assert [tuple(res[r]) for r in range(2)] == [(True, True), (True, True)]

@@ -45,7 +45,7 @@ def _hooks(mapper="mlp"):
     return h.train()
 
 
-def _step(fused, B=4, seed=5, mapper="mlp", temperature=1.0):
+def _step(fused, B=4, seed=5, mapper="mlp", temperature=1.0, shapes=((64, 80), (128, 40), (256, 20))):
     """One train-mode forward + backward of the three hooks; returns outputs,
     aux, feature grads, parameter grads and buffers."""
     from mcaq_yolo_amd import core
@@ -55,7 +55,7 @@ def _step(fused, B=4, seed=5, mapper="mlp", temperature=1.0):
         h = _hooks(mapper)
         gen = torch.Generator(device="cpu").manual_seed(seed)
         feats = []
-        for c, s in ((64, 80), (128, 40), (256, 20)):
+        for c, s in shapes:
             lo = torch.randn(B, c, s // 8, s // 8, generator=gen)
             hi = torch.randn(B, c, s, s, generator=gen)
             up = torch.nn.functional.interpolate(lo, size=(s, s), mode="bilinear", align_corners=False)
@@ -188,6 +188,27 @@ def test_device_pack_equals_torch_pack():
     assert gpu_c.is_cuda and gpu_c.shape == ref_c.shape
     assert torch.equal(gpu_c.cpu(), ref_c)
     assert torch.equal(gpu_s.cpu(), ref_s)
+    # the mapper (20 tensors + 3 MFMA operand segments) also takes the one-launch
+    # device path (MCAQ_PACK_MAXSEG was 16 < 23, so it never did)
+    mp = core.ComplexityToBitMappingNetwork()
+    for p in mp.parameters():
+        with torch.no_grad():
+            p.add_(0.01 * torch.randn_like(p))
+    ref_m = core._pack_mapper(mp.mapping_network)
+    calls = []
+    orig = core._device_pack
+
+    def spy(*a, **k):
+        r = orig(*a, **k)
+        calls.append(r is not None)
+        return r
+    core._device_pack = spy
+    try:
+        gpu_m = core._pack_mapper(copy.deepcopy(mp.mapping_network).to(DEV))
+    finally:
+        core._device_pack = orig
+    assert calls == [True], "mapper blob did not take the device pack"
+    assert torch.equal(gpu_m.cpu(), ref_m)
 
 
 def test_direct_grad_accumulation_matches_autograd_return():
@@ -259,3 +280,22 @@ def test_pass1_sharing_equals_separate_passes():
         assert torch.equal(g1[k], g0[k]), k
     for k in b0:
         assert torch.equal(b1[k], b0[k]), k
+
+
+def test_fused_train_large_map_takes_torch_backward():
+    """the fused soft-mask backward stages one image's m(p)
+    gradient in LDS and cannot take a 208x208 map (173 KiB); the call takes
+    the torch recompute instead of raising, and the step still equals the
+    all-torch path.  Host checks of both LDS bounds."""
+    from mcaq_yolo_amd import core
+    assert not core._smask_bwd_fits(208, 208, 13, 13) and core._smask_bwd_fits(80, 80, 10, 10)
+    assert core._head_bwd_fits(10, 10) and not core._head_bwd_fits(32, 32)
+    shapes = ((8, 208), (8, 104), (8, 52))
+    o1, a1, gx1, g1, b1 = _step(True, B=1, shapes=shapes)
+    o0, a0, gx0, g0, b0 = _step(False, B=1, shapes=shapes)
+    for x, y in zip(o1, o0):
+        _rel(x, y, 1e-5)
+    for x, y in zip(gx1, gx0):
+        _rel(x, y, 1e-3, floor=1e-12)
+    for k in g0:
+        _rel(g1[k], g0[k], 1e-3, floor=1e-12)
