@@ -41,7 +41,7 @@ typedef void* hipEvent_t;
 extern "C" {
 #endif
 
-#define MCAQ_ABI_VERSION 11
+#define MCAQ_ABI_VERSION 12
 /* largest dynamic LDS request of the morph kernel (gfx950: 160 KiB per CU) */
 #define MCAQ_MORPH_LDS_LIMIT 163840
 
@@ -127,6 +127,13 @@ typedef struct {
   int softmax_threads; /* torch.get_num_threads() of the reference CPU run the
                           soft mask's channel softmax reproduces (its exp per
                           tile depends on ATen's thread partition); <1 = 1 */
+  float* pwork;      /* mcaq_morph_work_bytes() bytes, or NULL: pixel-pass
+                        workspace of the band / edge kernels (NMS value plane
+                        + per-band Otsu histograms).  When every scale of a
+                        launch has one and is eligible (default Canny,
+                        adaptive binarize, tile 4/8/16, map <= 128 x 128), pass
+                        A runs as one workgroup per 16-row band + one per
+                        image instead of one whole-CU workgroup per image. */
 } mcaq_morph_scale;
 int mcaq_morph(const mcaq_morph_scale* scales, int nscales, hipStream_t stream);
 /* mcaq_morph + mcaq_finalize in one launch: the channel min/max reduction
@@ -138,6 +145,8 @@ size_t mcaq_morph_scratch_bytes(int B, int Hc, int Wc, int ht, int wt);
  * memory (the mode is common to a launch's scales: every scale needs this
  * buffer as soon as one scale's mcaq_morph_scratch_bytes is non-zero). */
 size_t mcaq_morph_scratch_bytes_global(int B, int Hc, int Wc);
+/* pwork bytes of one scale (0: the scale cannot take the band path) */
+size_t mcaq_morph_work_bytes(int B, int Hc, int Wc, int tile);
 
 /* ---- pass 2: y = dequant(quant_b(x)) * m ----------------------------------- */
 typedef struct {

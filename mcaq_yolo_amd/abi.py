@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libmcaq_hip.so")
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -33,7 +33,7 @@ class MorphScale(ctypes.Structure):
                 ("B", I), ("H", I), ("W", I), ("Hc", I), ("Wc", I), ("tile", I), ("ht", I), ("wt", I),
                 ("batch_offset", I), ("batch_total", I), ("flags", I), ("hyst_iters", I),
                 ("temperature", Fl), ("min_bits", Fl), ("max_bits", Fl), ("block_begin", I),
-                ("softmax_threads", I)]
+                ("softmax_threads", I), ("pwork", P)]
 
 
 class QuantScale(ctypes.Structure):
@@ -78,7 +78,7 @@ F_CONT, F_HAS_T, F_NORM_C, F_MAP_LINEAR = 16, 32, 64, 128
 F_BIN_OTSU, F_NO_EULER, F_CANNY_LEGACY = 256, 512, 1024
 
 EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats", "mcaq_stats_units",
-           "mcaq_finalize", "mcaq_morph", "mcaq_morph_finalize", "mcaq_morph_scratch_bytes", "mcaq_morph_scratch_bytes_global",
+           "mcaq_finalize", "mcaq_morph", "mcaq_morph_finalize", "mcaq_morph_scratch_bytes", "mcaq_morph_scratch_bytes_global", "mcaq_morph_work_bytes",
            "mcaq_quant",
            "mcaq_qat_forward", "mcaq_qat_backward", "mcaq_qat_work_floats", "mcaq_ema_stats",
            "mcaq_nms", "mcaq_nms_work_floats", "mcaq_time_next_launch", "mcaq_time_launch",
@@ -136,6 +136,8 @@ def _declare(lib):
     lib.mcaq_morph_scratch_bytes.argtypes = [I, I, I, I, I]
     lib.mcaq_morph_scratch_bytes_global.restype = ctypes.c_size_t
     lib.mcaq_morph_scratch_bytes_global.argtypes = [I, I, I]
+    lib.mcaq_morph_work_bytes.restype = ctypes.c_size_t
+    lib.mcaq_morph_work_bytes.argtypes = [I, I, I, I]
     lib.mcaq_qat_work_floats.restype = ctypes.c_size_t
     lib.mcaq_qat_work_floats.argtypes = [I, I, I, I]
     lib.mcaq_ema_stats.restype = I

@@ -41,6 +41,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from . import abi, fallback
+from . import engine as _engine
 from .engine import tile_size
 
 _CM_SIZE, _MM_SIZE, _SM_SIZE = 2881, 4865, 170
@@ -394,6 +395,9 @@ class MorphologicalComplexityAnalyzer(nn.Module):
         scratch = L.mcaq_morph_scratch_bytes(B, ht * T, wt * T, ht, wt)
         if scratch:
             ptrs["gscratch"] = torch.empty(scratch, device=dev, dtype=torch.uint8)
+        wb = L.mcaq_morph_work_bytes(B, ht * T, wt * T, T) if _engine.BAND_PASS else 0
+        if wb:
+            ptrs["pwork"] = torch.empty(wb // 4, device=dev)   # pass A as band + edge workgroups
         s = _morph_struct(B, H, W, T, ht, wt, flags, **ptrs)
         abi.check(L.mcaq_morph(ctypes.byref(s), 1, _stream()), "mcaq_morph")
         if want_craw:

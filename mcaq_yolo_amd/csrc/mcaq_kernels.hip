@@ -588,6 +588,55 @@ __global__ __launch_bounds__(MORPH_THREADS, MCAQ_MORPH_MINW) void mcaq_morph_ker
   morph_edges<kLegacy>(ctx, S, b, role, pl, sh);
 }
 
+// pass A in band mode (mcaq_band.h): one 256-thread workgroup per (scale,
+// image, 16-row band) with its halo rows in ~40 KB of LDS, then one per
+// (scale, image) for the Otsu threshold, hysteresis and box counts.  The
+// channel min/max workgroups ride along with the band launch.
+#ifndef MCAQ_BAND_MINW      // min waves per SIMD of the band kernel (register budget 512 / MINW)
+#define MCAQ_BAND_MINW 4
+#endif
+#ifndef MCAQ_EDGE_MINW
+#define MCAQ_EDGE_MINW 4
+#endif
+#ifndef MCAQ_BAND_PRIO      // wave priority of the band / edge kernels
+#define MCAQ_BAND_PRIO MCAQ_MORPH_PRIO
+#endif
+__global__ __launch_bounds__(256, MCAQ_BAND_MINW) void mcaq_band_kernel(MorphArgs a, FinalizeArgs f) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int nwg = a.bwg_begin[a.nscales];
+  if ((int)blockIdx.x >= nwg) {
+    finalize_body(f, (int)blockIdx.x - nwg, reinterpret_cast<float*>(smem));
+    return;
+  }
+  __builtin_amdgcn_s_setprio(MCAQ_BAND_PRIO);
+  int si = 0;
+  while (si + 1 < a.nscales && (int)blockIdx.x >= a.bwg_begin[si + 1]) ++si;
+  const MorphScale& S = a.s[si];
+  const int wg = (int)blockIdx.x - a.bwg_begin[si];
+  const int nb = band_count(S.Hc, S.tile);
+  const int b = wg / nb;
+  Ctx ctx{(int)threadIdx.x, 256};
+#ifdef MCAQ_TWICE   // diagnostic: a second, identical run finds the code in the instruction cache
+  band_pass(ctx, S, b, wg - b * nb, smem);
+  __syncthreads();
+#endif
+  band_pass(ctx, S, b, wg - b * nb, smem);
+}
+
+__global__ __launch_bounds__(256, MCAQ_EDGE_MINW) void mcaq_edge_kernel(MorphArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __builtin_amdgcn_s_setprio(MCAQ_BAND_PRIO);
+  int si = 0;
+  while (si + 1 < a.nscales && (int)blockIdx.x >= a.ewg_begin[si + 1]) ++si;
+  const MorphScale& S = a.s[si];
+  Ctx ctx{(int)threadIdx.x, 256};
+#ifdef MCAQ_TWICE
+  edge_image(ctx, S, (int)blockIdx.x - a.ewg_begin[si], smem);
+  __syncthreads();
+#endif
+  edge_image(ctx, S, (int)blockIdx.x - a.ewg_begin[si], smem);
+}
+
 // pass B: image group g of a workgroup owns threads [g*G, (g+1)*G) and its own
 // LDS tile arrays; the staged weights are shared by the workgroup.  A group
 // past the batch end recomputes the last image (identical values written twice).
@@ -616,6 +665,10 @@ struct QuantArgs {
   mcaq_quant_scale s[3];
   int nscales;
   int units_total;
+  // tile-aligned path (mcaq_quant_tile_kernel): H = ht << sh, W = wt << sw;
+  // reciprocals of the slice count, units per image and W for div_small
+  int sh[3], sw[3];
+  float rnsl[3], rupi[3], rw[3];
 };
 
 #ifndef MCAQ_QSLICE
@@ -824,6 +877,150 @@ __global__ MCAQ_QUANT_LB void mcaq_quant_kernel(QuantArgs a) {
   }
 }
 
+// Pass 2, tile-aligned path.  When every scale's map is a power-of-two
+// multiple of its tile grid (H = ht << sh, W = wt << sw, sw >= 2 - every hook
+// scale), a lane's 4 consecutive pixels lie in ONE tile: one bit width, so one
+// (scale, zp, 1/scale) table entry per channel serves all 4, read from a
+// [bits][channel] LDS table at an immediate offset, and the quantizer runs on
+// pixel pairs with packed fp32 instructions (v_pk_mul / v_pk_fma / v_pk_add,
+// each an IEEE fp32 operation per component: the values are those of
+// quant_dequant).  Pixel -> tile and m(p)'s source rows / columns are shifts;
+// no integer division anywhere (the general kernel spent ~2/3 of its ~1,070
+// VALU instructions per wave on index arithmetic and its integer divisions:
+// rocprofv3 SQ_INSTS_VALU, profiles/r04_sq/).  Soft mask: none or m(tile)
+// values (QM_NONE / QM_MT_LDS); at most 8 bit widths.
+template <bool kNTL, bool kNTS, int kM>
+__global__ MCAQ_QUANT_LB void mcaq_quant_tile_kernel(QuantArgs a) {
+  __shared__ float4 qt[8 * QSLICE];           // [kb][c]: scale, zp, 1/scale
+  __shared__ float mts[kM == QM_MT_LDS ? QMAXNT : 1];
+  __shared__ float4 mq4[64];                  // m(p) of each lane's 4 pixels
+  __shared__ int qany[QSLICE];
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const int unit = blockIdx.x;
+  int si = 0;
+  while (si + 1 < a.nscales && unit >= a.s[si + 1].unit_begin) ++si;
+  const mcaq_quant_scale& S = a.s[si];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int H = S.H, W = S.W, HW = H * W;
+  const int sh = si == 0 ? a.sh[0] : si == 1 ? a.sh[1] : a.sh[2];
+  const int sw = si == 0 ? a.sw[0] : si == 1 ? a.sw[1] : a.sw[2];
+  const float rnsl = si == 0 ? a.rnsl[0] : si == 1 ? a.rnsl[1] : a.rnsl[2];
+  const float rupi = si == 0 ? a.rupi[0] : si == 1 ? a.rupi[1] : a.rupi[2];
+  const float rw = si == 0 ? a.rw[0] : si == 1 ? a.rw[1] : a.rw[2];
+  const int nsl = (S.C + QSLICE - 1) / QSLICE, upi = (HW + 255) >> 8;
+  const int lu = unit - S.unit_begin;
+  const int q1 = div_small(lu, nsl, rnsl);
+  const int slice = lu - q1 * nsl;
+  const int b = div_small(q1, upi, rupi);
+  const int chunk = q1 - b * upi;
+  const int c0 = slice * QSLICE;
+  const int nc = imin_(QSLICE, S.C - c0);
+  const int NB = S.nbits;
+  const int NTq = S.ht * S.wt;
+  // ---- 1. small operands: this thread's table entry (bit width tid / 32,
+  // channel tid % 32), its m(tile) value, the lane's tile bits (one load: its
+  // 4 pixels share the tile)
+  const int tc = imin_(tid & (QSLICE - 1), nc - 1);
+  const float tmn = S.xmin[c0 + tc], tmx = S.xmax[c0 + tc];
+  float mtv = 0.0f;
+  if (kM == QM_MT_LDS) mtv = S.mt[(size_t)b * NTq + imin_(tid, NTq - 1)];
+  const int q0 = chunk * 256 + lane * 4;
+  const bool pv = q0 < HW;                     // HW % 4 == 0: all 4 pixels in or out
+  const int qa = pv ? q0 : 0;
+  const int h0 = div_small(qa, W, rw), w0 = qa - h0 * W;
+  const float bv = S.bits[((size_t)b * S.ht + (h0 >> sh)) * S.wt + (w0 >> sw)];
+  // ---- 2. the x rows (8 x 16 B per lane), in flight through the prologue
+  const int cw = wv * QCW;
+  const int ncw = imin_(QCW, nc - cw);
+  const size_t rowbase = ((size_t)b * S.C + c0 + imax_(imin_(cw, nc - 1), 0)) * HW;
+  const float* xb = S.x + rowbase;
+  float* yb = S.y + rowbase;
+  typedef float f4v __attribute__((ext_vector_type(4)));
+  f4v v[QCW];
+#pragma unroll
+  for (int c = 0; c < QCW; ++c) {
+    const f4v* row = reinterpret_cast<const f4v*>(xb + (size_t)imin_(c, imax_(ncw - 1, 0)) * HW + qa);
+    v[c] = kNTL ? __builtin_nontemporal_load(row) : *row;
+  }
+  // ---- 3. the table (IEEE divisions of QuantizationParameters), staged m(tile)
+  {
+    const int kq = imin_(tid >> 5, NB - 1);     // every thread stores an entry (unused rows harmless)
+    const QParam q = qparam(tmn, tmx, S.bits_lo + kq);
+    qt[tid] = make_float4(q.scale, q.zp, q.rs, 0.0f);
+    if (tid < QSLICE) qany[tid] = (!S.stats_cover_x || stats_need_any(tmn, tmx)) ? 1 : 0;
+  }
+  if (kM == QM_MT_LDS) {
+    if (tid < NTq) mts[tid] = mtv;
+    for (int i = tid + 256; i < NTq; i += 256) mts[i] = S.mt[(size_t)b * NTq + i];
+  }
+  const int kb = imin_(imax_((int)rintf(bv), S.bits_lo), S.bits_lo + NB - 1) - S.bits_lo;
+  const int hb = 1 << (S.bits_lo + kb - 1);
+  const float qlo = (float)(-hb), qhi = (float)(hb - 1);
+  __syncthreads();   // qt, mts ready
+  // ---- 4. m(p) = 5x5 Gaussian (replicate pad) of the nearest-upsampled tile
+  // values, taps row-major from 0 (quantization.py:235-238); wave w computes
+  // pixel w of every lane's quad
+  f2 m01 = {1.0f, 1.0f}, m23 = {1.0f, 1.0f};
+  if (kM == QM_MT_LDS) {
+    const int w = w0 + wv;
+    int cs[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) cs[j] = imin_(imax_(w + j - 2, 0), W - 1) >> sw;
+    float acc = 0.0f;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      const int rb = (imin_(imax_(h0 + i - 2, 0), H - 1) >> sh) * S.wt;
+#pragma unroll
+      for (int j = 0; j < 5; ++j) acc = fmaf(bits_as_float(k_smooth5_bits[i * 5 + j]), mts[rb + cs[j]], acc);
+    }
+    reinterpret_cast<float*>(mq4)[lane * 4 + wv] = acc;
+    __syncthreads();
+    const float4 mm = mq4[lane];
+    m01 = f2{mm.x, mm.y};
+    m23 = f2{mm.z, mm.w};
+  }
+  if (ncw <= 0) return;
+  int anyc = 0;
+#pragma unroll
+  for (int c = 0; c < QCW; ++c) anyc |= c < ncw ? qany[cw + c] : 0;
+  const bool any_x = __builtin_amdgcn_readfirstlane(anyc) != 0;
+  const float4* qrow = qt + kb * QSLICE + cw;   // the lane's entries: immediate offsets c * 16
+#pragma unroll
+  for (int c = 0; c < QCW; ++c) {
+    if (c >= ncw) break;
+    const float4 e = qrow[c];
+    f4v o;
+    if (!any_x) {
+      // quant_dequant (mcaq_math.h) on pixel pairs: x / s by the reciprocal
+      // and one FMA correction, + zp, round half to even, clamp, - zp, * s, * m
+      const f2 x01 = f2{v[c].x, v[c].y}, x23 = f2{v[c].z, v[c].w};
+      const f2 s2 = f2{e.x, e.x}, r2 = f2{e.z, e.z};
+      const f2 p01 = x01 * e.z, p23 = x23 * e.z;
+      const f2 d01 = __builtin_elementwise_fma(__builtin_elementwise_fma(-p01, s2, x01), r2, p01);
+      const f2 d23 = __builtin_elementwise_fma(__builtin_elementwise_fma(-p23, s2, x23), r2, p23);
+      f2 t01 = d01 + e.y, t23 = d23 + e.y;
+      t01.x = __builtin_amdgcn_fmed3f(rintf(t01.x), qlo, qhi);
+      t01.y = __builtin_amdgcn_fmed3f(rintf(t01.y), qlo, qhi);
+      t23.x = __builtin_amdgcn_fmed3f(rintf(t23.x), qlo, qhi);
+      t23.y = __builtin_amdgcn_fmed3f(rintf(t23.y), qlo, qhi);
+      f2 y01 = (t01 - e.y) * e.x, y23 = (t23 - e.y) * e.x;
+      if (kM != QM_NONE) { y01 = y01 * m01; y23 = y23 * m23; }
+      o = f4v{y01.x, y01.y, y23.x, y23.y};
+    } else {
+      QParam q;
+      q.scale = e.x; q.zp = e.y; q.rs = e.z; q.qmin = qlo; q.qmax = qhi;
+      o = f4v{quant_dequant_any(v[c].x, q), quant_dequant_any(v[c].y, q), quant_dequant_any(v[c].z, q),
+              quant_dequant_any(v[c].w, q)};
+      if (kM != QM_NONE) o = o * f4v{m01.x, m01.y, m23.x, m23.y};
+    }
+    if (pv) {
+      f4v* orow = reinterpret_cast<f4v*>(yb + (size_t)c * HW + q0);
+      if (kNTS) __builtin_nontemporal_store(o, orow);
+      else *orow = o;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // extern "C" launchers
 // ---------------------------------------------------------------------------
@@ -981,6 +1178,11 @@ size_t mcaq_morph_scratch_bytes_global(int B, int Hc, int Wc) {
   return (size_t)2 * B * ((plane_bytes(Hc, Wc) + 15) & ~15);   // edge + mask workgroup per image
 }
 
+size_t mcaq_morph_work_bytes(int B, int Hc, int Wc, int tile) {
+  if (B < 1 || Hc < 1 || Wc < 1 || Hc > 128 || Wc > 128 || !(tile == 4 || tile == 8 || tile == 16)) return 0;
+  return band_work_bytes(B, Hc, Wc, tile);
+}
+
 size_t mcaq_morph_scratch_bytes(int B, int Hc, int Wc, int ht, int wt) {
   MorphScale s{};
   s.Hc = Hc; s.Wc = Wc; s.ht = ht; s.wt = wt; s.H = 2 * Hc; s.W = 2 * Wc;  // conservative: H < Hc + tile
@@ -1005,6 +1207,8 @@ struct MorphLaunch {
   size_t dyn_a;
   int grid_b, wlds;        // pass B grid (0: no pass B), weights staged in LDS
   size_t dyn_b;
+  int band, grid_e;        // pass A in band mode: band grid = grid_a, edge grid
+  size_t dyn_e;
 };
 
 static int morph_launch_config(const mcaq_morph_scale* scales, int nscales, const mcaq_finalize_scale* fscales,
@@ -1039,7 +1243,34 @@ static int morph_launch_config(const mcaq_morph_scale* scales, int nscales, cons
   L.any_phi = any_phi;
   L.any_tiles = any_tiles;
   L.grid_a = 0; L.grid_b = 0; L.dyn_a = 0; L.dyn_b = 0; L.var_a = 0; L.wlds = 0;
-  if (any_phi) {
+  L.band = 0; L.grid_e = 0; L.dyn_e = 0;
+  bool band = any_phi != 0;
+  for (int i = 0; i < nscales; ++i)
+    if ((a.s[i].flags & F_PHI) && !band_eligible(a.s[i])) band = false;
+#ifdef MCAQ_NO_BAND
+  band = false;   // A/B: the per-image pass A
+#endif
+  if (band) {
+    int wg = 0, ewg = 0, dynb = 0, dyne = 0;
+    for (int i = 0; i < nscales; ++i) {
+      const MorphScale& S = a.s[i];
+      a.bwg_begin[i] = wg;
+      a.ewg_begin[i] = ewg;
+      if (!(S.flags & F_PHI)) continue;
+      wg += S.B * band_count(S.Hc, S.tile);
+      ewg += S.B;
+      dynb = imax_(dynb, (band_lds_bytes(S.Wc, S.tile) + 15) & ~15);
+      dyne = imax_(dyne, (edge_lds_bytes(S.Hc, S.Wc) + 15) & ~15);
+    }
+    a.bwg_begin[nscales] = wg;
+    a.ewg_begin[nscales] = ewg;
+    if (fa.nblocks > 0) dynb = imax_(dynb, 8 * 256);   // finalize_body's LDS
+    L.band = 1;
+    L.grid_a = wg + fa.nblocks;
+    L.dyn_a = (size_t)dynb;
+    L.grid_e = ewg;
+    L.dyn_e = (size_t)dyne;
+  } else if (any_phi) {
     int mode, stride; size_t dyn;
     int e = morph_plan(a.s, nscales, &mode, &stride, &dyn);
     if (e) return e;
@@ -1112,7 +1343,24 @@ static int morph_launch(const MorphLaunch& L, int passes, hipStream_t stream) {
     const hipError_t fe = hipGetLastError();
     if (fe != hipSuccess) return (int)fe;
   }
-  if ((passes & 1) && L.grid_a > 0) {
+  if ((passes & 1) && L.band) {
+    static int set_band = 0;   // raise the dynamic LDS limit once (not during graph capture)
+    if (!set_band) {
+      hipError_t ae = hipFuncSetAttribute((const void*)mcaq_band_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                          MCAQ_MORPH_LDS_LIMIT - 1024);
+      if (ae == hipSuccess)
+        ae = hipFuncSetAttribute((const void*)mcaq_edge_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 MCAQ_MORPH_LDS_LIMIT - 1024);
+      if (ae != hipSuccess) return (int)ae;
+      set_band = 1;
+    }
+    hipLaunchKernelGGL(mcaq_band_kernel, dim3(L.grid_a), dim3(256), L.dyn_a, stream, a, fa);
+    hipError_t le = hipGetLastError();
+    if (le != hipSuccess) return (int)le;
+    hipLaunchKernelGGL(mcaq_edge_kernel, dim3(L.grid_e), dim3(256), L.dyn_e, stream, a);
+    le = hipGetLastError();
+    if (le != hipSuccess) return (int)le;
+  } else if ((passes & 1) && L.grid_a > 0) {
     const int limit = morph_lds_budget();
     static int set[4] = {0, 0, 0, 0};  // raise the dynamic LDS limit once (not during graph capture)
     const int var = L.var_a;
@@ -1216,6 +1464,39 @@ int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream) 
     big = big || imin_(QSLICE, q.C) * q.nbits > 256 || (k == QM_MT_LDS && NT > 256);
   }
   const dim3 g(units), t(256);
+#ifndef MCAQ_TRUE_DIV
+  // tile-aligned path: every scale's map a power-of-two multiple of its tile
+  // grid (tiles >= 4 pixels wide), <= 8 bit widths, no plane / compat indexing
+  bool tile_ok = vec && (kind == QM_NONE || kind == QM_MT_LDS);
+  for (int i = 0; i < nscales && tile_ok; ++i) {
+    const mcaq_quant_scale& q = scales[i];
+    int sh = 0, sw = 0;
+    while ((q.ht << sh) < q.H) ++sh;
+    while ((q.wt << sw) < q.W) ++sw;
+    tile_ok = (q.ht << sh) == q.H && (q.wt << sw) == q.W && sw >= 2 && q.nbits <= 8 && q.compat_tile_h <= 0 &&
+              q.compat_tile_w <= 0 && q.ht * q.wt <= QMAXNT;
+    a.sh[i] = sh; a.sw[i] = sw;
+    a.rnsl[i] = 1.0f / (float)((q.C + QSLICE - 1) / QSLICE);
+    a.rupi[i] = 1.0f / (float)((q.H * q.W + 255) / 256);
+    a.rw[i] = 1.0f / (float)q.W;
+  }
+#ifdef MCAQ_NO_QUANT_TILE
+  tile_ok = false;   // A/B: the general kernel
+#endif
+  if (tile_ok) {
+    switch ((kind == QM_NONE ? 0 : 4) + (nt & 3)) {
+      case 0: launch_k(mcaq_quant_tile_kernel<false, false, QM_NONE>, g, t, 0, stream, a); break;
+      case 1: launch_k(mcaq_quant_tile_kernel<false, true, QM_NONE>, g, t, 0, stream, a); break;
+      case 2: launch_k(mcaq_quant_tile_kernel<true, false, QM_NONE>, g, t, 0, stream, a); break;
+      case 3: launch_k(mcaq_quant_tile_kernel<true, true, QM_NONE>, g, t, 0, stream, a); break;
+      case 4: launch_k(mcaq_quant_tile_kernel<false, false, QM_MT_LDS>, g, t, 0, stream, a); break;
+      case 5: launch_k(mcaq_quant_tile_kernel<false, true, QM_MT_LDS>, g, t, 0, stream, a); break;
+      case 6: launch_k(mcaq_quant_tile_kernel<true, false, QM_MT_LDS>, g, t, 0, stream, a); break;
+      default: launch_k(mcaq_quant_tile_kernel<true, true, QM_MT_LDS>, g, t, 0, stream, a); break;
+    }
+    return (int)hipGetLastError();
+  }
+#endif
 #define MCAQ_Q_LAUNCH(V, L, S_)                                                                              \
   do {                                                                                                       \
     switch (kind * 2 + (big ? 1 : 0)) {                                                                      \

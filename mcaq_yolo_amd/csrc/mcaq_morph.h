@@ -71,6 +71,8 @@ struct MorphArgs {
   int ipw[3], gstride[3], pstride[3], wg_begin[4];
   // pass B packing: images per workgroup, LDS bytes per image, first workgroup
   int tipw[3], tgstride[3], twg_begin[4];
+  // band mode of pass A (mcaq_band.h): first band / edge workgroup of each scale
+  int bwg_begin[4], ewg_begin[4];
 };
 
 // bit planes
@@ -724,6 +726,95 @@ MCAQ_HD void sobel_stage(const Ctx& ctx, Planes& pl, int Hc, int Wc) {
   }
 }
 
+// Canny hysteresis on bit planes (morphology.py:504-509): `iters` Jacobi
+// sweeps e' = e | (weak & dilate3x3(e)), stopping early once a sweep changes
+// nothing (every later sweep would be the identity).  E0 holds the strong
+// pixels, E1 is scratch; returns the plane holding the result.  Ends synced.
+MCAQ_HD const uint32_t* hysteresis_run(const Ctx& ctx, uint32_t* E0, uint32_t* E1, const uint32_t* WK, int Hc, int WPR,
+                                       int iters) {
+  uint32_t* src = E0;
+  uint32_t* dst = E1;
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (Hc <= 128 && WPR <= 4) {
+    // one wave, planes in registers (lane l: rows 2l, 2l+1), neighbour rows by
+    // lane shuffles: no barrier per iteration.  Same Jacobi sweeps and the
+    // same stop rule as the workgroup loop below.
+    if (ctx.tid < 64) {
+      const int lane = ctx.tid;
+      uint32_t e[2][4], wk[2][4];
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int row = 2 * lane + rr;
+          const bool ok = row < Hc && k < WPR;
+          e[rr][k] = ok ? src[row * WPR + k] : 0u;
+          wk[rr][k] = ok ? WK[row * WPR + k] : 0u;
+        }
+      }
+      for (int it = 0; it < iters; ++it) {
+        uint32_t up[4], dn[4], d[4][4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          // DPP wave_shr:1 / wave_shl:1 (lane l <- l-1 / l+1; 0 past the ends)
+          up[k] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)e[1][k], 0x138, 0xF, 0xF, false);
+          dn[k] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)e[0][k], 0x130, 0xF, 0xF, false);
+        }
+        // horizontal 3-dilation of the 4 rows up, e0, e1, dn
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          d[0][k] = dil3(up, k);
+          d[1][k] = dil3(e[0], k);
+          d[2][k] = dil3(e[1], k);
+          d[3][k] = dil3(dn, k);
+        }
+        bool ch = false;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t n0 = e[0][k] | (wk[0][k] & (d[0][k] | d[1][k] | d[2][k]));
+          const uint32_t n1 = e[1][k] | (wk[1][k] & (d[1][k] | d[2][k] | d[3][k]));
+          ch = ch || (n0 != e[0][k]) || (n1 != e[1][k]);
+          e[0][k] = n0; e[1][k] = n1;
+        }
+        if (!__any(ch)) break;
+      }
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int row = 2 * lane + rr;
+          if (row < Hc && k < WPR) src[row * WPR + k] = e[rr][k];
+        }
+      }
+    }
+    MSYNC();
+  } else
+#endif
+  {
+    for (int it = 0; it < iters; ++it) {
+      int changed = 0;
+      MFOR2(h, k, Hc, WPR) {
+        const uint32_t cur = src[h * WPR + k];
+        uint32_t g = 0u;
+        for (int hh = imax_(h - 1, 0); hh <= imin_(h + 1, Hc - 1); ++hh) {
+          const uint32_t* row = src + hh * WPR;
+          const uint32_t c = row[k];
+          const uint32_t l = (c << 1) | (k > 0 ? row[k - 1] >> 31 : 0u);
+          const uint32_t r = (c >> 1) | (k + 1 < WPR ? row[k + 1] << 31 : 0u);
+          g |= c | l | r;
+        }
+        const uint32_t nv = cur | (WK[h * WPR + k] & g);
+        changed |= (nv != cur);
+        dst[h * WPR + k] = nv;
+      }
+      const int any = block_or(ctx, changed);
+      uint32_t* t = src; src = dst; dst = t;
+      if (!any) break;
+    }
+  }
+  return src;
+}
+
 // ---- pass A: per-image pixel work -> phi (one 1024-thread workgroup per image)
 // kLegacy: the canny_impl='legacy' instantiation (a separate kernel on the
 // device, so the default edge path keeps its register allocation)
@@ -909,88 +1000,7 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, P
     }
     MSTAMP(5);
     // -- hysteresis on words: e' = e | (weak & dilate3x3(e)), Jacobi, early exit
-    uint32_t* src = E0;
-    uint32_t* dst = E1;
-    const int iters = legacy ? 2 : (S.hyst_iters < 1 ? 1 : S.hyst_iters);
-#if defined(__HIP_DEVICE_COMPILE__)
-    if (Hc <= 128 && WPR <= 4) {
-      // one wave, planes in registers (lane l: rows 2l, 2l+1), neighbour rows by
-      // lane shuffles: no barrier per iteration.  Same Jacobi sweeps and the
-      // same stop rule as the workgroup loop below.
-      if (ctx.tid < 64) {
-        const int lane = ctx.tid;
-        uint32_t e[2][4], wk[2][4];
-#pragma unroll
-        for (int rr = 0; rr < 2; ++rr) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int row = 2 * lane + rr;
-            const bool ok = row < Hc && k < WPR;
-            e[rr][k] = ok ? src[row * WPR + k] : 0u;
-            wk[rr][k] = ok ? WK[row * WPR + k] : 0u;
-          }
-        }
-        for (int it = 0; it < iters; ++it) {
-          uint32_t up[4], dn[4], d[4][4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            // DPP wave_shr:1 / wave_shl:1 (lane l <- l-1 / l+1; 0 past the ends)
-            up[k] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)e[1][k], 0x138, 0xF, 0xF, false);
-            dn[k] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)e[0][k], 0x130, 0xF, 0xF, false);
-          }
-          // horizontal 3-dilation of the 4 rows up, e0, e1, dn
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            d[0][k] = dil3(up, k);
-            d[1][k] = dil3(e[0], k);
-            d[2][k] = dil3(e[1], k);
-            d[3][k] = dil3(dn, k);
-          }
-          bool ch = false;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const uint32_t n0 = e[0][k] | (wk[0][k] & (d[0][k] | d[1][k] | d[2][k]));
-            const uint32_t n1 = e[1][k] | (wk[1][k] & (d[1][k] | d[2][k] | d[3][k]));
-            ch = ch || (n0 != e[0][k]) || (n1 != e[1][k]);
-            e[0][k] = n0; e[1][k] = n1;
-          }
-          if (!__any(ch)) break;
-        }
-#pragma unroll
-        for (int rr = 0; rr < 2; ++rr) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int row = 2 * lane + rr;
-            if (row < Hc && k < WPR) src[row * WPR + k] = e[rr][k];
-          }
-        }
-      }
-      MSYNC();
-    } else
-#endif
-    {
-      for (int it = 0; it < iters; ++it) {
-        int changed = 0;
-        MFOR2(h, k, Hc, WPR) {
-          const uint32_t cur = src[h * WPR + k];
-          uint32_t g = 0u;
-          for (int hh = imax_(h - 1, 0); hh <= imin_(h + 1, Hc - 1); ++hh) {
-            const uint32_t* row = src + hh * WPR;
-            const uint32_t c = row[k];
-            const uint32_t l = (c << 1) | (k > 0 ? row[k - 1] >> 31 : 0u);
-            const uint32_t r = (c >> 1) | (k + 1 < WPR ? row[k + 1] << 31 : 0u);
-            g |= c | l | r;
-          }
-          const uint32_t nv = cur | (WK[h * WPR + k] & g);
-          changed |= (nv != cur);
-          dst[h * WPR + k] = nv;
-        }
-        const int any = block_or(ctx, changed);
-        uint32_t* t = src; src = dst; dst = t;
-        if (!any) break;
-      }
-    }
-    edge = src;
+    edge = hysteresis_run(ctx, E0, E1, WK, Hc, WPR, legacy ? 2 : (S.hyst_iters < 1 ? 1 : S.hyst_iters));
     MSTAMP(6);
 
     } else {
@@ -1761,3 +1771,5 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
 }
 
 }  // namespace mcaq
+
+#include "mcaq_band.h"   // pass A as band + edge workgroups

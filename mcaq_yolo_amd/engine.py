@@ -46,6 +46,14 @@ def _stream_handle(stream):
     return ctypes.c_void_p(s.cuda_stream)
 
 
+# Pass A of the morphology as band + edge workgroups (csrc/mcaq_band.h) for
+# every scale that supports it.  Bit-identical to the per-image pass A, but
+# measured slower in the pipelined step (r04: 66.4-67.2 vs 62.2-62.8 us per
+# step at config 2, profiles/r04_morph/): its 16-row bands run ~30 us each
+# on 1-4 waves per SIMD, so its CU-time is no lower.  Off by default.
+BAND_PASS = False
+
+
 class ScaleGeom:
     """Shape bookkeeping for one hook scale."""
 
@@ -107,6 +115,10 @@ class HookPlan:
                 nb["edge"] = nb["binmask"] = None
             sb = self.lib.mcaq_morph_scratch_bytes_global(g.B, g.Hc, g.Wc) if glob else 0
             nb["gscratch"] = torch.empty(max(sb, 16), device=d, dtype=torch.uint8) if sb else None
+            # pass A in band mode (NMS plane + per-band Otsu histograms); 0 bytes:
+            # the scale keeps the per-image pass A
+            wb = 0 if not BAND_PASS else self.lib.mcaq_morph_work_bytes(g.B, g.Hc, g.Wc, g.tile)
+            nb["pwork"] = torch.empty(wb // 4, device=d) if wb else None
             self.bufs.append(nb)
 
     # ------------------------------------------------------------------
@@ -225,6 +237,7 @@ class HookPlan:
             s.mt_out = _p(b["mt"]) if (with_mask[i] and quantize) else None
             s.edge_out, s.bin_out = _p(b["edge"]), _p(b["binmask"])
             s.gscratch = _p(b["gscratch"])
+            s.pwork = _p(b["pwork"])
             s.tile_tmp = _p(b["tile_tmp"])
             s.B, s.H, s.W, s.Hc, s.Wc = g.B, g.H, g.W, g.Hc, g.Wc
             s.tile, s.ht, s.wt = g.tile, g.ht, g.wt

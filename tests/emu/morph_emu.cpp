@@ -30,3 +30,25 @@ extern "C" int emu_morph(const mcaq_morph_scale* s) {
   }
   return 0;
 }
+
+// pass A in band mode (mcaq_band.h): every band of an image, then its edge
+// workgroup, then pass B as above.  s->pwork must hold
+// band_work_bytes(B, Hc, Wc, tile) bytes.
+extern "C" int emu_morph_band(const mcaq_morph_scale* s) {
+  using namespace mcaq;
+  if (!band_eligible(*s)) return 1;
+  const int NT = s->ht * s->wt;
+  std::vector<char> blds(band_lds_bytes(s->Wc, s->tile) + 64), elds(edge_lds_bytes(s->Hc, s->Wc) + 64);
+  std::vector<char> tshm(tiles_lds_bytes(s->H, s->W, NT) + 64);
+  const int nb = band_count(s->Hc, s->tile);
+  Ctx ctx{0, 1};
+  for (int b = 0; b < s->B; ++b)
+    for (int k = 0; k < nb; ++k) band_pass(ctx, *s, b, k, blds.data());
+  for (int b = 0; b < s->B; ++b) edge_image(ctx, *s, b, elds.data());
+  for (int b = 0; b < s->B; ++b) {
+    Shared sh2;
+    carve_shared(tshm.data(), sh2);
+    morph_tiles(ctx, *s, b, sh2, nullptr, 0, 1, nullptr);
+  }
+  return 0;
+}

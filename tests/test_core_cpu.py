@@ -151,7 +151,7 @@ def test_plan_descriptor_reuse_equals_rebuild(monkeypatch):
         for k in ("gray", "absmean", "pmin", "pmax", "xmin", "xmax", "complexity", "bits", "mt", "y", "phi",
                   "tile_tmp", "cmlp"):
             b[k] = torch.empty(4)
-        b["m"] = b["edge"] = b["binmask"] = b["gscratch"] = None
+        b["m"] = b["edge"] = b["binmask"] = b["gscratch"] = b["pwork"] = None
         p.bufs.append(b)
     cm, mm, sms = torch.empty(8), torch.empty(8), [torch.empty(8) for _ in shapes]
 

@@ -24,6 +24,7 @@ f32 = np.float32
 def emu():
     lib = ctypes.CDLL(build_emu.build())
     lib.emu_morph.argtypes = [ctypes.POINTER(abi.MorphScale)]
+    lib.emu_morph_band.argtypes = [ctypes.POINTER(abi.MorphScale)]
     W = load_weights()
     blobs = (params.pack_complexity_mlp(params.sub(W, "complexity_analyzer.")),
              params.pack_mapper_mlp(params.sub(W, "bit_mapper.")),
@@ -35,7 +36,7 @@ def _ptr(a):
     return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
 
 
-def run_emu(emu, x, grid, flags, T=1.0, c_in=None, bits_in=None):
+def run_emu(emu, x, grid, flags, T=1.0, c_in=None, bits_in=None, band=False):
     lib, W, (cm, mm, sm) = emu
     B, C, H, Wd = x.shape
     tile = O.tile_size(H, grid)
@@ -60,7 +61,14 @@ def run_emu(emu, x, grid, flags, T=1.0, c_in=None, bits_in=None):
     s.hyst_iters = 8
     s.softmax_threads = O.REF_THREADS
     s.temperature, s.min_bits, s.max_bits = max(T, 0.1), 2.0, 8.0
-    lib.emu_morph(ctypes.byref(s))
+    if band:
+        # pass A as band + edge workgroups (mcaq_band.h): pwork = NMS plane + band histograms
+        nb = -(-Hc // max(tile, 16))
+        out["pwork"] = np.zeros(B * Hc * Wc + B * nb * 256, f32)
+        s.pwork = _ptr(out["pwork"])
+        assert lib.emu_morph_band(ctypes.byref(s)) == 0, "scale not eligible for the band path"
+    else:
+        lib.emu_morph(ctypes.byref(s))
     return out
 
 
@@ -192,3 +200,51 @@ def test_emu_analyzer_switches_vs_reference(emu, name):
     assert np.array_equal(out["phi"], ref["phi"])
     assert np.array_equal(out["c"], ref["complexity"])
     assert np.array_equal(out["m"], ref["m"])
+
+
+def _band_ok(x, grid, flags):
+    tile = O.tile_size(x.shape[2], grid)
+    Hc, Wc = (x.shape[2] // tile) * tile, (x.shape[3] // tile) * tile
+    return tile in (4, 8, 16) and Hc <= 128 and Wc <= 128 and not flags & (abi.F_CANNY_LEGACY | abi.F_BIN_OTSU)
+
+
+BAND_KEYS = ("tile_tmp", "edge", "bin", "phi", "cmlp", "c", "bits", "m")
+
+
+@pytest.mark.parametrize("name", ["case_" + c for c in case_names()] + OPT_CASES)
+def test_emu_band_pass_equals_image_pass(emu, name):
+    """Pass A as band + edge workgroups (round 4, mcaq_band.h) against the
+    per-image pass A of the same source: every per-tile partial, the edge and
+    mask planes and everything downstream bit for bit, on every golden case
+    whose scale the band path takes (and the option switches it supports)."""
+    d = np.load(os.path.join(GOLDEN, name + ".npz"))
+    x = d["x"].astype(f32)
+    grid = int(d["grid"])
+    opts = {k[4:]: (str(d[k]) if d[k].dtype.kind == "U" else d[k].item()) for k in d.files if k.startswith("opt_")}
+    flags = ALL | (abi.F_BIN_OTSU if opts.get("binarize_impl") == "otsu" else 0) | \
+        (0 if opts.get("contour_components", True) else abi.F_NO_EULER) | \
+        (abi.F_CANNY_LEGACY if opts.get("canny_impl") == "legacy" else 0)
+    if not _band_ok(x, grid, flags):
+        pytest.skip("scale not eligible for the band path (kept on the per-image pass A)")
+    ref = run_emu(emu, x, grid, flags)
+    out = run_emu(emu, x, grid, flags, band=True)
+    for k in BAND_KEYS:
+        assert np.array_equal(out[k], ref[k]), k
+    if "bits_mlp" in d.files:
+        assert np.array_equal(out["bits"], d["bits_mlp"])
+
+
+def test_emu_band_pass_near_ties_and_batch(emu):
+    """The adaptive threshold's exact fallback inside band halos, several
+    images per launch, and an image whose rows are not a multiple of 16."""
+    rng = np.random.default_rng(11)
+    for shape, grid in (((3, 4, 48, 40), 8), ((2, 8, 36, 52), 8), ((2, 3, 128, 128), 8), ((1, 2, 64, 64), 4)):
+        x = rng.uniform(0.0, 1.0, size=shape).astype(f32)
+        x[:, :, ::7, ::5] = 0.5          # plateaus: ties in LBP, NMS and the threshold
+        flags = ALL
+        if not _band_ok(x, grid, flags):
+            continue
+        ref = run_emu(emu, x, grid, flags)
+        out = run_emu(emu, x, grid, flags, band=True)
+        for k in BAND_KEYS:
+            assert np.array_equal(out[k], ref[k]), (shape, k)

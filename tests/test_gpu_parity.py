@@ -362,3 +362,37 @@ def test_m_plane_option_same_y(dev, blobs):
     for oa, ob, x in zip(a, b, xs):
         assert np.array_equal(oa["y"], ob["y"])
         check_against_oracle(ob, x, blobs[0], 8, "mlp")
+
+
+@pytest.mark.parametrize("cfg", [("c2", [(32, 64, 80, 80), (32, 128, 40, 40), (32, 256, 20, 20)], 8),
+                                 ("c3", [(64, 128, 80, 80), (64, 256, 40, 40), (64, 512, 20, 20)], 16)])
+def test_band_pass_equals_image_pass_full_size(dev, blobs, cfg):
+    """Pass A as band + edge workgroups (round 4, csrc/mcaq_band.h) against the
+    per-image pass A on the GPU at BASELINE config 2 / 3 full shapes: every
+    debug plane and output bit for bit (tile partials through phi, edge and
+    mask planes, complexity, bits, y)."""
+    import torch
+    from mcaq_yolo_amd import engine
+    from mcaq_yolo_amd.engine import HookPlan, ScaleGeom
+    name, shapes, grid = cfg
+    W, cm, mm, sm = blobs
+    g = torch.Generator(device="cpu").manual_seed(41)
+    feats = [torch.nn.functional.silu(1.5 * torch.randn(s, generator=g)).to(dev) for s in shapes]
+    outs = {}
+    for band in (True, False):
+        old = engine.BAND_PASS
+        engine.BAND_PASS = band
+        try:
+            plan = HookPlan([ScaleGeom(*s, grid) for s in shapes], dev, want=("phi", "cmlp", "debug"))
+            assert all((b["pwork"] is not None) == band for b in plan.bufs)
+            bufs = plan.run(feats, cm, mm, [sm] * len(shapes))
+            torch.cuda.synchronize()
+            outs[band] = [{k: v.clone() for k, v in b.items() if torch.is_tensor(v) and k != "pwork"} for b in bufs]
+        finally:
+            engine.BAND_PASS = old
+    for a, b, s in zip(outs[True], outs[False], shapes):
+        T = ScaleGeom(*s, grid).tile
+        nit = 20 + (T.bit_length() - 2)      # 20 + number of box-counting scales 2..T
+        assert torch.equal(a["tile_tmp"][..., :nit], b["tile_tmp"][..., :nit]), (name, "tile_tmp")
+        for k in ("edge", "binmask", "phi", "cmlp", "complexity", "bits", "mt", "m", "y"):
+            assert torch.equal(a[k], b[k]), (name, k)
