@@ -76,6 +76,7 @@ class SmaskParams(ctypes.Structure):
 F_PHI, F_CMLP, F_MAPPER, F_SOFTMASK = 1, 2, 4, 8
 F_CONT, F_HAS_T, F_NORM_C, F_MAP_LINEAR = 16, 32, 64, 128
 F_BIN_OTSU, F_NO_EULER, F_CANNY_LEGACY = 256, 512, 1024
+F_TILES_IMAGE = 2048   # force the per-image pass B
 
 EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats", "mcaq_stats_units",
            "mcaq_finalize", "mcaq_morph", "mcaq_morph_finalize", "mcaq_morph_scratch_bytes", "mcaq_morph_scratch_bytes_global", "mcaq_morph_work_bytes",

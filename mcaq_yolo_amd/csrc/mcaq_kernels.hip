@@ -637,6 +637,146 @@ __global__ __launch_bounds__(256, MCAQ_EDGE_MINW) void mcaq_edge_kernel(MorphArg
   edge_image(ctx, S, (int)blockIdx.x - a.ewg_begin[si], smem);
 }
 
+// pass B, batch-wide (mcaq_tiles_batch.h): one 64-thread workgroup (one wave,
+// lane = tile) per 64 consecutive tiles of a scale's batch, ~14 KB of LDS
+__device__ __forceinline__ int tb_scale_of(const MorphArgs& a) {
+  int si = 0;
+  while (si + 1 < a.nscales && (int)blockIdx.x >= a.tb_begin[si + 1]) ++si;
+  return si;
+}
+
+__global__ __launch_bounds__(64) void mcaq_tb_head_kernel(MorphArgs a) {
+  __shared__ float tiles[TB_TILES * TB_TS];
+  __shared__ float xs[MLP_SCRATCH_FLOATS];
+  __builtin_amdgcn_s_setprio(MCAQ_MORPH_PRIO);
+  const int si = tb_scale_of(a);
+  const MorphScale& S = a.s[si];
+  const int NT = S.ht * S.wt;
+  const int u0 = ((int)blockIdx.x - a.tb_begin[si]) * TB_TILES;
+  const int n = imin_(TB_TILES, S.B * NT - u0);
+  const int lane = (int)threadIdx.x, u = u0 + imin_(lane, n - 1);
+  const int b = div_small(u, NT, 1.0f / (float)NT), t = u - b * NT;
+  float* tt = S.tile_tmp + (size_t)u * TT_STRIDE;
+  {
+    float tv[28];   // the pass-A partials [0, 20 + S) of this tile (S <= 7)
+#pragma unroll
+    for (int i = 0; i < 7; ++i) {
+      const float4 q = reinterpret_cast<const float4*>(tt)[i];
+      tv[4 * i] = q.x; tv[4 * i + 1] = q.y; tv[4 * i + 2] = q.z; tv[4 * i + 3] = q.w;
+    }
+    float p[8];
+    phi_of_tile(S, b, t, tv, p);
+    if (lane < n) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) tiles[lane * TB_TS + T_PHI + k] = p[k];
+      if (S.phi_out) {
+        float4* o = reinterpret_cast<float4*>(S.phi_out + (size_t)u * 8);
+        o[0] = make_float4(p[0], p[1], p[2], p[3]);
+        o[1] = make_float4(p[4], p[5], p[6], p[7]);
+      }
+    }
+  }
+  __syncthreads();
+#if defined(__HIP_DEVICE_COMPILE__)
+  cmlp_block_mfma<2, const float*, TB_TS>(S.cmlp, tiles, n, 0, lane, (lds_f)xs);
+  if (n > 32) cmlp_block_mfma<2, const float*, TB_TS>(S.cmlp, tiles, n, 32, lane, (lds_f)xs);
+#else
+  (void)xs;
+#endif
+  __syncthreads();
+  if (lane < n) {
+    const float c = tiles[lane * TB_TS + T_CMLP];
+    tt[TT_CRAW] = c;
+    if (S.cmlp_out) S.cmlp_out[u] = c;
+  }
+}
+
+__global__ __launch_bounds__(64) void mcaq_tb_map_kernel(MorphArgs a) {
+  __shared__ float tiles[TB_TILES * TB_TS];
+  __shared__ float xs[MLP_SCRATCH_FLOATS];
+  __shared__ float ab[256];
+  __builtin_amdgcn_s_setprio(MCAQ_MORPH_PRIO);
+  const int si = tb_scale_of(a);
+  const MorphScale& S = a.s[si];
+  const int NT = S.ht * S.wt;
+  const int u0 = ((int)blockIdx.x - a.tb_begin[si]) * TB_TILES;
+  const int n = imin_(TB_TILES, S.B * NT - u0);
+  const int lane = (int)threadIdx.x, u = u0 + imin_(lane, n - 1);
+  const int b = div_small(u, NT, 1.0f / (float)NT), t = u - b * NT;
+  const int th = div_small(t, S.wt, 1.0f / (float)S.wt), tw = t - th * S.wt;
+  float* tt = S.tile_tmp + (size_t)u * TT_STRIDE;
+  for (int j = lane; j < 128; j += 64) fold_mapper_bn(S.mapper, ab, j);
+  const float* crow = S.tile_tmp + (size_t)b * NT * TT_STRIDE + TT_CRAW;
+  const float c = bilateral_tile(t, th, tw, S.ht, S.wt, NT, [&](int k) { return crow[(size_t)k * TT_STRIDE]; });
+  float act = 0.0f;
+  if (S.flags & F_SOFTMASK) act = act_tile(S.absmean + (size_t)b * S.H * S.W, S.H, S.W, S.ht, S.wt, th, tw);
+  if (lane < n) {
+    tiles[lane * TB_TS + T_C] = c;
+    if (S.c_out) S.c_out[u] = c;
+    if (S.flags & F_SOFTMASK) tt[TT_ACT] = act;
+  }
+  __syncthreads();
+#if defined(__HIP_DEVICE_COMPILE__)
+  mapper_block_mfma<2, const float*, TB_TS>(S.mapper, (const float*)ab, tiles, n, 0, lane, T_C, S.min_bits, S.max_bits,
+                                           (lds_f)xs);
+  if (n > 32)
+    mapper_block_mfma<2, const float*, TB_TS>(S.mapper, (const float*)ab, tiles, n, 32, lane, T_C, S.min_bits,
+                                             S.max_bits, (lds_f)xs);
+#else
+  (void)xs;
+#endif
+  __syncthreads();
+  if (lane < n) {
+    const float bv = finish_bits(tiles[lane * TB_TS + T_AUX], S);
+    tt[TT_BITS] = bv;
+    if (S.bits_out) S.bits_out[u] = bv;
+  }
+}
+
+__global__ __launch_bounds__(64) void mcaq_tb_mask_kernel(MorphArgs a) {
+  __builtin_amdgcn_s_setprio(MCAQ_MORPH_PRIO);
+  const int si = tb_scale_of(a);
+  const MorphScale& S = a.s[si];
+  if (!(S.flags & F_SOFTMASK)) return;
+  const int NT = S.ht * S.wt;
+  const float rnt = 1.0f / (float)NT;
+  const int u0 = ((int)blockIdx.x - a.tb_begin[si]) * TB_TILES;
+  const int n = imin_(TB_TILES, S.B * NT - u0);
+  const int lane = (int)threadIdx.x, u = u0 + imin_(lane, n - 1);
+  const int b = div_small(u, NT, rnt), t = u - b * NT;
+  const int th = div_small(t, S.wt, 1.0f / (float)S.wt), tw = t - th * S.wt;
+  // max of the tile activations of every image this block touches (NaN-propagating, as torch.amax)
+  float amax = 0.0f;
+  const int bf = div_small(u0, NT, rnt), bl = div_small(u0 + n - 1, NT, rnt);
+  for (int bb = bf; bb <= bl; ++bb) {
+    float lm = -3.402823466e38f;
+    for (int j = lane; j < NT; j += 64) lm = fmaxp(lm, S.tile_tmp[((size_t)bb * NT + j) * TT_STRIDE + TT_ACT]);
+    for (int o = 32; o > 0; o >>= 1) lm = fmaxp(lm, __shfl_xor(lm, o, 64));
+    if (bb == b) amax = lm;
+  }
+  const float den = amax + 1e-8f;
+  const float* row = S.tile_tmp + (size_t)b * NT * TT_STRIDE;
+  const bool vl = aten_softmax_vec_lane((long long)(S.batch_offset + b) * NT + t, (long long)S.batch_total * NT, NT,
+                                        S.softmax_threads);
+  const float mtv = smask_tile(
+      S.smask, th, tw, S.ht, S.wt,
+      [&](int s) { return clampf_((row[(size_t)s * TT_STRIDE + TT_BITS] - 2.0f) / 6.0f, 0.0f, 1.0f); },
+      [&](int s) { return row[(size_t)s * TT_STRIDE + TT_ACT] / den; }, vl);
+  if (lane < n && S.mt_out) S.mt_out[u] = mtv;
+}
+
+// the m(p) plane of the batch-wide pass B (debug / m_plane): one thread per pixel
+__global__ __launch_bounds__(256) void mcaq_tb_mplane_kernel(MorphArgs a, int total) {
+  const int g = (int)(blockIdx.x * 256 + threadIdx.x);
+  if (g >= total) return;
+  int si = 0, o = g;
+  while (si + 1 < a.nscales && o >= a.s[si].B * a.s[si].H * a.s[si].W) { o -= a.s[si].B * a.s[si].H * a.s[si].W; ++si; }
+  const MorphScale& S = a.s[si];
+  if (!S.m_out || !(S.flags & F_SOFTMASK)) return;
+  const int HW = S.H * S.W, b = o / HW, p = o - b * HW, h = p / S.W, w = p - h * S.W;
+  S.m_out[o] = mplane_pixel(S.mt_out + (size_t)b * S.ht * S.wt, S.H, S.W, S.ht, S.wt, h, w);
+}
+
 // pass B: image group g of a workgroup owns threads [g*G, (g+1)*G) and its own
 // LDS tile arrays; the staged weights are shared by the workgroup.  A group
 // past the batch end recomputes the last image (identical values written twice).
@@ -1209,6 +1349,7 @@ struct MorphLaunch {
   size_t dyn_b;
   int band, grid_e;        // pass A in band mode: band grid = grid_a, edge grid
   size_t dyn_e;
+  int tb, any_mask;        // pass B as batch-wide tile kernels (grid_b = 64-tile workgroups)
 };
 
 static int morph_launch_config(const mcaq_morph_scale* scales, int nscales, const mcaq_finalize_scale* fscales,
@@ -1303,7 +1444,28 @@ static int morph_launch_config(const mcaq_morph_scale* scales, int nscales, cons
     L.var_a = 2 * leg + mode;
     L.dyn_a = dyn;
   }
-  if (any_tiles) {
+  L.tb = 0; L.any_mask = 0;
+  bool tb = any_tiles != 0;
+  for (int i = 0; i < nscales; ++i) {
+    const int tf = a.s[i].flags & (F_PHI | F_CMLP | F_MAPPER | F_SOFTMASK);
+    if (tf && !tiles_batch_eligible(a.s[i])) tb = false;
+  }
+#ifdef MCAQ_NO_TILES_BATCH
+  tb = false;   // A/B: the per-image pass B
+#endif
+  if (tb) {
+    int blk = 0;
+    for (int i = 0; i < nscales; ++i) {
+      const MorphScale& S = a.s[i];
+      a.tb_begin[i] = blk;
+      if (!(S.flags & (F_PHI | F_CMLP | F_MAPPER | F_SOFTMASK))) continue;
+      blk += (S.B * S.ht * S.wt + TB_TILES - 1) / TB_TILES;
+      L.any_mask |= (S.flags & F_SOFTMASK) != 0;
+    }
+    a.tb_begin[nscales] = blk;
+    L.tb = 1;
+    L.grid_b = blk;
+  } else if (any_tiles) {
     // pass B packing: the waves an image needs for one MLP block of MLP_TPW
     // tiles each (at most the whole workgroup); small images share a workgroup
     int twg = 0, per = 0;
@@ -1381,7 +1543,18 @@ static int morph_launch(const MorphLaunch& L, int passes, hipStream_t stream) {
     hipError_t le = hipGetLastError();
     if (le != hipSuccess) return (int)le;
   }
-  if ((passes & 2) && L.grid_b > 0) {
+  if ((passes & 2) && L.tb && L.grid_b > 0) {
+    hipLaunchKernelGGL(mcaq_tb_head_kernel, dim3(L.grid_b), dim3(64), 0, stream, a);
+    hipLaunchKernelGGL(mcaq_tb_map_kernel, dim3(L.grid_b), dim3(64), 0, stream, a);
+    if (L.any_mask) hipLaunchKernelGGL(mcaq_tb_mask_kernel, dim3(L.grid_b), dim3(64), 0, stream, a);
+    int px = 0;
+    bool mp = false;
+    for (int i = 0; i < a.nscales; ++i) {
+      px += a.s[i].B * a.s[i].H * a.s[i].W;
+      mp = mp || (a.s[i].m_out && (a.s[i].flags & F_SOFTMASK));
+    }
+    if (mp) hipLaunchKernelGGL(mcaq_tb_mplane_kernel, dim3((px + 255) / 256), dim3(256), 0, stream, a, px);
+  } else if ((passes & 2) && L.grid_b > 0) {
     const int lim = MCAQ_MORPH_LDS_LIMIT - 1024;
     static int set_tiles = 0;
     if ((int)L.dyn_b > set_tiles) {

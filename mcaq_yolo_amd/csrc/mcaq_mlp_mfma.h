@@ -178,7 +178,7 @@ __device__ __forceinline__ void bn_relu16(f32x4 (&D)[NH][NB], PT alpha, PT beta,
 }
 
 // complexity MLP for the 16*NH tiles [t0, t0+16*NH) of one image; writes T_CMLP
-template <int NH, typename PT>
+template <int NH, typename PT, int TS = TILE_FLOATS>   // TS: floats per tile of `tiles`
 __device__ void cmlp_block_mfma(PT P, float* tiles, int NT, int t0, int lane, lds_f xs, bool stamp = false) {
   const int j = lane & 15, q = lane >> 4;
   WSTAMP(stamp, 40);
@@ -189,7 +189,7 @@ __device__ void cmlp_block_mfma(PT P, float* tiles, int NT, int t0, int lane, ld
 #pragma unroll
     for (int h = 0; h < NH; ++h) {
       const int t = t0 + 16 * h + j;
-      const float* tp = tiles + (t < NT ? t : 0) * TILE_FLOATS + T_PHI;
+      const float* tp = tiles + (t < NT ? t : 0) * TS + T_PHI;
 #pragma unroll
       for (int s = 0; s < 2; ++s) bb[h][s] = t < NT ? tp[4 * s + q] : 0.0f;
     }
@@ -236,7 +236,7 @@ __device__ void cmlp_block_mfma(PT P, float* tiles, int NT, int t0, int lane, ld
 #pragma unroll
     for (int n = 0; n < 32; ++n) acc = fmaf(fmax_(xs[lane * MLP_XS + n], 0.0f), P[CM_W3 + n], acc);
     const float z = acc + P[CM_B3];
-    if (t < NT) tiles[t * TILE_FLOATS + T_CMLP] = 1.0f / (1.0f + cr_exp(-z));
+    if (t < NT) tiles[t * TS + T_CMLP] = 1.0f / (1.0f + cr_exp(-z));
   }
   WSTAMP(stamp, 45);
 }
@@ -244,7 +244,7 @@ __device__ void cmlp_block_mfma(PT P, float* tiles, int NT, int t0, int lane, ld
 // MLP bit mapper for the tiles [t0, t0+16*NH): pre-temperature bits into T_AUX
 // ab: folded BN terms in LDS, alpha at [0,128) and beta at [128,256) for the
 // 32 + 64 + 32 neurons of BN1/BN2/BN3 (mcaq_morph.h, bn fold)
-template <int NH, typename PT>
+template <int NH, typename PT, int TS = TILE_FLOATS>
 __device__ void mapper_block_mfma(PT P, PT ab, float* tiles, int NT, int t0, int lane, int csrc, float min_bits,
                                   float max_bits, lds_f xs, bool stamp = false) {
   const int j = lane & 15, q = lane >> 4;
@@ -255,13 +255,13 @@ __device__ void mapper_block_mfma(PT P, PT ab, float* tiles, int NT, int t0, int
     // lane l < 16*NH evaluates log1p for tile l once; lanes (q = 2, j) of
     // half h take it from lane 16h + j
     const int tl = t0 + (lane & (16 * NH - 1));
-    const float cl = clampf_(tl < NT ? tiles[tl * TILE_FLOATS + csrc] : 0.0f, 0.0f, 1.0f);
+    const float cl = clampf_(tl < NT ? tiles[tl * TS + csrc] : 0.0f, 0.0f, 1.0f);
     const float lg = lane < 16 * NH ? cr_log1p(cl) : 0.0f;
     float bb[NH];
 #pragma unroll
     for (int h = 0; h < NH; ++h) {
       const int t = t0 + 16 * h + j;
-      float c = t < NT ? tiles[t * TILE_FLOATS + csrc] : 0.0f;
+      float c = t < NT ? tiles[t * TS + csrc] : 0.0f;
       c = clampf_(c, 0.0f, 1.0f);
       const float lh = __shfl(lg, 16 * h + j, 64);
       bb[h] = q == 0 ? c : (q == 1 ? c * c : (q == 2 ? lh : 0.0f));
@@ -299,7 +299,7 @@ __device__ void mapper_block_mfma(PT P, PT ab, float* tiles, int NT, int t0, int
     const float z = acc + P[MM_B4];
     WSTAMP(stamp, 53);
     const float hs = 1.0f / (1.0f + cr_exp(-z));
-    if (t < NT) tiles[t * TILE_FLOATS + T_AUX] = min_bits + (max_bits - min_bits) * hs;
+    if (t < NT) tiles[t * TS + T_AUX] = min_bits + (max_bits - min_bits) * hs;
   }
   WSTAMP(stamp, 54);
 }

@@ -58,6 +58,7 @@ enum : int {
   F_BIN_OTSU = 256,   // binarize_impl='otsu'
   F_NO_EULER = 512,   // contour_components=False
   F_CANNY_LEGACY = 1024,  // canny_impl='legacy'
+  F_TILES_IMAGE = 2048,   // pass B per image (morph_tiles) even where the batch-wide tile kernels apply
 };
 
 using MorphScale = mcaq_morph_scale;  // include/mcaq_hip.h
@@ -73,6 +74,8 @@ struct MorphArgs {
   int tipw[3], tgstride[3], twg_begin[4];
   // band mode of pass A (mcaq_band.h): first band / edge workgroup of each scale
   int bwg_begin[4], ewg_begin[4];
+  // batch-wide pass B (mcaq_tiles_batch.h): first 64-tile workgroup of each scale
+  int tb_begin[4];
 };
 
 // bit planes
@@ -1261,14 +1264,16 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, P
   MSTAMP(9);
 }
 
-// phi1..phi5 + interactions from the per-tile partial quantities in
-// tiles[T_TMP..] (pass B; morphology.py:576-739, :860-864)
-MCAQ_HD void assemble_phi(const Ctx& ctx, const MorphScale& S, int b, float* tiles) {
+// phi1..phi5 + interactions of tile t of image b from its per-tile partial
+// quantities tv[0..20+S) (morphology.py:576-739, :860-864) into tp[0..8)
+MCAQ_HD void phi_of_tile(const MorphScale& S, int b, int t, const float* tv, float* tp) {
   const int T = S.tile, NT = S.ht * S.wt;
   const float fT2 = (float)(T * T);
   int S_ = 0;
   for (int s = 2; s <= T; s *= 2) ++S_;
-  {
+  // phi1: weighted log-log regression slope (morphology.py:596-621)
+  float p1;
+  if (S_ >= 2) {
     const int ycut = aten_tail_start(S.batch_total * NT);
     float xs[8], ws[8];
 #pragma unroll
@@ -1279,60 +1284,60 @@ MCAQ_HD void assemble_phi(const Ctx& ctx, const MorphScale& S, int b, float* til
     const float w_sum = bits_as_float(k_frac_st_bits[4 * S_ + 0]);
     const float x_mean = bits_as_float(k_frac_st_bits[4 * S_ + 1]);
     const float var = bits_as_float(k_frac_st_bits[4 * S_ + 2]);
-
-    MFOR(t, NT) {
-      const float* tv = tiles + t * TILE_FLOATS + T_TMP;
-      // phi1: weighted log-log regression slope (morphology.py:596-621)
-      float p1;
-      if (S_ >= 2) {
-        const bool tail = ((S.batch_offset + b) * NT + t) >= ycut;
-        float ys[8], wy[8], cv[8];
+    const bool tail = ((S.batch_offset + b) * NT + t) >= ycut;
+    float ys[8], wy[8], cv[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) ys[i] = i < S_ ? tv[4 + i] : 0.0f;
+    for (int i = 0; i < 8; ++i) ys[i] = i < S_ ? tv[4 + i] : 0.0f;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) wy[i] = ws[i] * ys[i];
-        const float y_mean = small_sum(wy, S_, tail) / w_sum;
+    for (int i = 0; i < 8; ++i) wy[i] = ws[i] * ys[i];
+    const float y_mean = small_sum(wy, S_, tail) / w_sum;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) cv[i] = (ws[i] * (xs[i] - x_mean)) * (ys[i] - y_mean);
-        const float cov = small_sum(cv, S_, tail);
-        p1 = clampf_(-(cov / (var + 1e-12f)), 1.0f, 2.0f) / 2.0f;
-      } else {
-        p1 = 1.0f / 2.0f;
-      }
-      // phi2: LBP entropy, bins summed 8, 9, 0..7 (channels-last inner sum)
-      const float* terms = tv + 4 + S_;
-      float ent = 0.0f;
-      ent = ent + terms[8];
-      ent = ent + terms[9];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) ent = ent + terms[k];
-      const float p2 = (-ent) / (float)3.321928094887362;
-      // phi3: gradient variance
-      const float mgx = tv[0] / fT2, mgx2 = tv[1] / fT2, mgy = tv[2] / fT2, mgy2 = tv[3] / fT2;
-      const float v = fmax_(mgx2 - mgx * mgx, 0.0f) + fmax_(mgy2 - mgy * mgy, 0.0f);
-      const float p3 = v / (v + 1.0f);
-      // phi4 edge density, phi5 contour complexity
-      const float* cn = tv + 14 + S_;
-      const float p4 = cn[0] / fT2;
-      const float fa = cn[1], fp = cn[2];
-      float ic = (fp * fp) / ((float)(4.0 * 3.14159265358979323846) * fa + 1e-6f);
-      if (!(S.flags & F_NO_EULER)) {
-        // Euler sum = (q1 - q3 - 2 qd) / 4: a multiple of 0.25, exact in fp32
-        const float esum = (cn[3] - cn[4] - 2.0f * cn[5]) * 0.25f;
-        ic = ic / fmax_(rintf((esum / fT2) * fT2), 1.0f);
-      }
-      const float p5 = fa > 0.0f ? 1.0f - 1.0f / fmax_(ic, 1.0f) : 0.0f;
-      const float p8 = cr_sqrt(p4 * p5 + 1e-12f);
-      float* tp = tiles + t * TILE_FLOATS + T_PHI;
-      tp[0] = p1; tp[1] = p2; tp[2] = p3; tp[3] = p4; tp[4] = p5;
-      tp[5] = p1 * p2; tp[6] = p3 * p3; tp[7] = p8;
-      if (S.phi_out) {
-        float* o = S.phi_out + ((size_t)b * NT + t) * 8;
-        for (int k = 0; k < 8; ++k) o[k] = tp[k];
-      }
-    }
-    MSYNC();
+    for (int i = 0; i < 8; ++i) cv[i] = (ws[i] * (xs[i] - x_mean)) * (ys[i] - y_mean);
+    const float cov = small_sum(cv, S_, tail);
+    p1 = clampf_(-(cov / (var + 1e-12f)), 1.0f, 2.0f) / 2.0f;
+  } else {
+    p1 = 1.0f / 2.0f;
   }
+  // phi2: LBP entropy, bins summed 8, 9, 0..7 (channels-last inner sum)
+  const float* terms = tv + 4 + S_;
+  float ent = 0.0f;
+  ent = ent + terms[8];
+  ent = ent + terms[9];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) ent = ent + terms[k];
+  const float p2 = (-ent) / (float)3.321928094887362;
+  // phi3: gradient variance
+  const float mgx = tv[0] / fT2, mgx2 = tv[1] / fT2, mgy = tv[2] / fT2, mgy2 = tv[3] / fT2;
+  const float v = fmax_(mgx2 - mgx * mgx, 0.0f) + fmax_(mgy2 - mgy * mgy, 0.0f);
+  const float p3 = v / (v + 1.0f);
+  // phi4 edge density, phi5 contour complexity
+  const float* cn = tv + 14 + S_;
+  const float p4 = cn[0] / fT2;
+  const float fa = cn[1], fp = cn[2];
+  float ic = (fp * fp) / ((float)(4.0 * 3.14159265358979323846) * fa + 1e-6f);
+  if (!(S.flags & F_NO_EULER)) {
+    // Euler sum = (q1 - q3 - 2 qd) / 4: a multiple of 0.25, exact in fp32
+    const float esum = (cn[3] - cn[4] - 2.0f * cn[5]) * 0.25f;
+    ic = ic / fmax_(rintf((esum / fT2) * fT2), 1.0f);
+  }
+  const float p5 = fa > 0.0f ? 1.0f - 1.0f / fmax_(ic, 1.0f) : 0.0f;
+  const float p8 = cr_sqrt(p4 * p5 + 1e-12f);
+  tp[0] = p1; tp[1] = p2; tp[2] = p3; tp[3] = p4; tp[4] = p5;
+  tp[5] = p1 * p2; tp[6] = p3 * p3; tp[7] = p8;
+}
+
+// phi of every tile of image b from the partials staged in tiles[t][T_TMP..] (pass B)
+MCAQ_HD void assemble_phi(const Ctx& ctx, const MorphScale& S, int b, float* tiles) {
+  const int NT = S.ht * S.wt;
+  MFOR(t, NT) {
+    float* tp = tiles + t * TILE_FLOATS + T_PHI;
+    phi_of_tile(S, b, t, tiles + t * TILE_FLOATS + T_TMP, tp);
+    if (S.phi_out) {
+      float* o = S.phi_out + ((size_t)b * NT + t) * 8;
+      for (int k = 0; k < 8; ++k) o[k] = tp[k];
+    }
+  }
+  MSYNC();
 }
 
 // batched copy of n values: every thread issues up to K loads before its
@@ -1773,3 +1778,4 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
 }  // namespace mcaq
 
 #include "mcaq_band.h"   // pass A as band + edge workgroups
+#include "mcaq_tiles_batch.h"   // pass B as batch-wide tile kernels

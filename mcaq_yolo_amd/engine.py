@@ -53,6 +53,10 @@ def _stream_handle(stream):
 # on 1-4 waves per SIMD, so its CU-time is no lower.  Off by default.
 BAND_PASS = False
 
+# Pass B of the morphology as batch-wide tile kernels (csrc/mcaq_tiles_batch.h)
+# wherever the flags allow it; False: the per-image pass B (A/B, cross-check)
+TILES_BATCH = True
+
 
 class ScaleGeom:
     """Shape bookkeeping for one hook scale."""
@@ -243,7 +247,8 @@ class HookPlan:
             s.tile, s.ht, s.wt = g.tile, g.ht, g.wt
             s.batch_offset = batch_offset
             s.batch_total = batch_total if batch_total is not None else g.B
-            s.flags = flags | (abi.F_SOFTMASK if (with_mask[i] and quantize) else 0)
+            s.flags = flags | (abi.F_SOFTMASK if (with_mask[i] and quantize) else 0) | \
+                (0 if TILES_BATCH else abi.F_TILES_IMAGE)
             s.hyst_iters = hysteresis_iters
             s.softmax_threads = int(softmax_threads) if softmax_threads else torch.get_num_threads()
             s.temperature, s.min_bits, s.max_bits = T, float(min_bits), float(max_bits)

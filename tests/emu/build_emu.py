@@ -6,7 +6,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "libmcaq_emu.so")
 SRC = os.path.join(HERE, "morph_emu.cpp")
 DEPS = [SRC] + [os.path.join(HERE, "..", "..", "mcaq_yolo_amd", "csrc", f)
-                for f in ("mcaq_morph.h", "mcaq_band.h", "mcaq_math.h", "mcaq_tables.h")] + \
+                for f in ("mcaq_morph.h", "mcaq_band.h", "mcaq_tiles_batch.h", "mcaq_math.h", "mcaq_tables.h")] + \
        [os.path.join(HERE, "..", "..", "include", "mcaq_hip.h")]
 
 

@@ -25,6 +25,7 @@ def emu():
     lib = ctypes.CDLL(build_emu.build())
     lib.emu_morph.argtypes = [ctypes.POINTER(abi.MorphScale)]
     lib.emu_morph_band.argtypes = [ctypes.POINTER(abi.MorphScale)]
+    lib.emu_morph_tb.argtypes = [ctypes.POINTER(abi.MorphScale)]
     W = load_weights()
     blobs = (params.pack_complexity_mlp(params.sub(W, "complexity_analyzer.")),
              params.pack_mapper_mlp(params.sub(W, "bit_mapper.")),
@@ -36,7 +37,7 @@ def _ptr(a):
     return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
 
 
-def run_emu(emu, x, grid, flags, T=1.0, c_in=None, bits_in=None, band=False):
+def run_emu(emu, x, grid, flags, T=1.0, c_in=None, bits_in=None, band=False, tb=False):
     lib, W, (cm, mm, sm) = emu
     B, C, H, Wd = x.shape
     tile = O.tile_size(H, grid)
@@ -54,6 +55,8 @@ def run_emu(emu, x, grid, flags, T=1.0, c_in=None, bits_in=None, band=False):
     s.phi_out, s.cmlp_out, s.c_out = _ptr(out["phi"]), _ptr(out["cmlp"]), _ptr(out["c"])
     s.bits_out, s.m_out, s.edge_out, s.bin_out = _ptr(out["bits"]), _ptr(out["m"]), _ptr(out["edge"]), _ptr(out["bin"])
     out["tile_tmp"] = np.zeros((B, ht * wt, 32), f32)
+    out["mt"] = np.zeros((B, ht, wt), f32)
+    s.mt_out = _ptr(out["mt"])
     s.tile_tmp = _ptr(out["tile_tmp"])
     s.B, s.H, s.W, s.Hc, s.Wc, s.tile, s.ht, s.wt = B, H, Wd, Hc, Wc, tile, ht, wt
     s.batch_offset, s.batch_total = 0, B
@@ -61,7 +64,10 @@ def run_emu(emu, x, grid, flags, T=1.0, c_in=None, bits_in=None, band=False):
     s.hyst_iters = 8
     s.softmax_threads = O.REF_THREADS
     s.temperature, s.min_bits, s.max_bits = max(T, 0.1), 2.0, 8.0
-    if band:
+    if tb:
+        # pass B as the batch-wide tile kernels (mcaq_tiles_batch.h)
+        assert lib.emu_morph_tb(ctypes.byref(s)) == 0, "flags not eligible for the batch-wide tile pass"
+    elif band:
         # pass A as band + edge workgroups (mcaq_band.h): pwork = NMS plane + band histograms
         nb = -(-Hc // max(tile, 16))
         out["pwork"] = np.zeros(B * Hc * Wc + B * nb * 256, f32)
@@ -248,3 +254,29 @@ def test_emu_band_pass_near_ties_and_batch(emu):
         out = run_emu(emu, x, grid, flags, band=True)
         for k in BAND_KEYS:
             assert np.array_equal(out[k], ref[k]), (shape, k)
+
+
+TB_KEYS = ("phi", "cmlp", "c", "bits", "mt", "m")
+
+
+@pytest.mark.parametrize("name", ["case_" + c for c in case_names()] + OPT_CASES)
+def test_emu_batch_tile_pass_equals_image_pass(emu, name):
+    """Pass B as batch-wide tile kernels (round 4, mcaq_tiles_batch.h) against
+    the per-image pass B of the same source: phi, raw and filtered complexity,
+    bits and the soft-mask tile values bit for bit on every golden case, with
+    the option switches and a temperature / continuous bits variant."""
+    d = np.load(os.path.join(GOLDEN, name + ".npz"))
+    x = d["x"].astype(f32)
+    grid = int(d["grid"])
+    opts = {k[4:]: (str(d[k]) if d[k].dtype.kind == "U" else d[k].item()) for k in d.files if k.startswith("opt_")}
+    if opts.get("canny_impl") == "legacy":
+        pytest.skip("legacy Canny: the host emulation of the batch path runs the default pass A")
+    flags = ALL | (abi.F_BIN_OTSU if opts.get("binarize_impl") == "otsu" else 0) | \
+        (0 if opts.get("contour_components", True) else abi.F_NO_EULER)
+    for fl, T in ((flags, 1.0), (flags | abi.F_CONT, 0.7)):
+        ref = run_emu(emu, x, grid, fl, T=T)
+        out = run_emu(emu, x, grid, fl, T=T, tb=True)
+        for k in TB_KEYS:
+            assert np.array_equal(out[k], ref[k]), (k, fl)
+    if "bits_mlp" in d.files:
+        assert np.array_equal(out["bits"], ref["bits"])

@@ -396,3 +396,35 @@ def test_band_pass_equals_image_pass_full_size(dev, blobs, cfg):
         assert torch.equal(a["tile_tmp"][..., :nit], b["tile_tmp"][..., :nit]), (name, "tile_tmp")
         for k in ("edge", "binmask", "phi", "cmlp", "complexity", "bits", "mt", "m", "y"):
             assert torch.equal(a[k], b[k]), (name, k)
+
+
+@pytest.mark.parametrize("cfg", [("c2", [(32, 64, 80, 80), (32, 128, 40, 40), (32, 256, 20, 20)], 8, {}),
+                                 ("c3", [(64, 128, 80, 80), (64, 256, 40, 40), (64, 512, 20, 20)], 16, {}),
+                                 ("c2_T", [(8, 64, 80, 80), (8, 128, 40, 40), (8, 256, 20, 20)], 8,
+                                  {"temperature": 0.6, "continuous": True})])
+def test_batch_tile_pass_equals_image_pass_full_size(dev, blobs, cfg):
+    """Pass B as batch-wide tile kernels (round 4, csrc/mcaq_tiles_batch.h)
+    against the per-image pass B on the GPU at BASELINE config 2 / 3 full
+    shapes (and a temperature / continuous-bits variant): phi, raw and
+    filtered complexity, bits, m(tile), the m(p) plane and y bit for bit."""
+    import torch
+    from mcaq_yolo_amd import engine
+    from mcaq_yolo_amd.engine import HookPlan, ScaleGeom
+    name, shapes, grid, kw = cfg
+    W, cm, mm, sm = blobs
+    g = torch.Generator(device="cpu").manual_seed(43)
+    feats = [torch.nn.functional.silu(1.5 * torch.randn(s, generator=g)).to(dev) for s in shapes]
+    outs = {}
+    for batch in (True, False):
+        old = engine.TILES_BATCH
+        engine.TILES_BATCH = batch
+        try:
+            plan = HookPlan([ScaleGeom(*s, grid) for s in shapes], dev, want=("phi", "cmlp", "debug"))
+            bufs = plan.run(feats, cm, mm, [sm] * len(shapes), **kw)
+            torch.cuda.synchronize()
+            outs[batch] = [{k: v.clone() for k, v in b.items() if torch.is_tensor(v)} for b in bufs]
+        finally:
+            engine.TILES_BATCH = old
+    for a, b in zip(outs[True], outs[False]):
+        for k in ("phi", "cmlp", "complexity", "bits", "mt", "m", "y"):
+            assert torch.equal(a[k], b[k]), (name, k)
