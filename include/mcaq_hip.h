@@ -323,6 +323,30 @@ int mcaq_mapper_train_backward(const mcaq_mapper_params* P, const float* c, int 
                                float min_bits, float max_bits, float temperature, float* work, float* gc,
                                float* gparams, float* gpart, int accumulate, unsigned* grid_sync,
                                hipStream_t stream);
+/* Batch sharded over `world` ranks with process-group BatchNorm (the train-
+ * mode mapper of a DDP QAT step, dist.GroupBatchNorm1d semantics): the same
+ * kernels one stage per call, the caller's collectives between them.
+ *   forward  stage 1..4; before stage s >= 2: every rank's
+ *            mcaq_mapper_train_reduce(kind 0, layer s - 1) output (129 floats)
+ *            all-gathered in rank order -> `gathered` (world x 129)
+ *   backward stage 4..1; before stage s <= 3: mcaq_mapper_train_reduce
+ *            (kind 1, layer s) summed over the ranks -> `gsums` (128 floats);
+ *            gathered1 = the forward's gathered layer-1 entries (tile counts);
+ *            then mcaq_mapper_train_grad_reduce: this rank's parameter
+ *            gradients (the caller all-reduces them as DDP does).
+ * Replaces the autograd through GroupBatchNorm1d's all-reduces (dist.py). */
+int mcaq_mapper_train_forward_stage(const mcaq_mapper_params* P, const float* c, int n, float min_bits,
+                                    float max_bits, float temperature, float momentum, int round_bits,
+                                    int update_stats, float* bits, float* work, int stage, const float* gathered,
+                                    int world, hipStream_t stream);
+int mcaq_mapper_train_backward_stage(const mcaq_mapper_params* P, const float* c, int n, const float* gbits,
+                                     float min_bits, float max_bits, float temperature, float* work, float* gc,
+                                     float* gpart, int stage, const float* gsums, const float* gathered1, int world,
+                                     hipStream_t stream);
+/* kind 0: this rank's (mean[64], M2[64], n) of layer 1..3 (forward);
+ * kind 1: this rank's BN sums (S1[64], S2[64]) of layer 1..3 (backward) */
+int mcaq_mapper_train_reduce(const float* work, int n, int kind, int layer, float* out, hipStream_t stream);
+int mcaq_mapper_train_grad_reduce(int n, const float* gpart, float* gparams, int accumulate, hipStream_t stream);
 /* grid_sync: NULL (one launch per batch-statistics barrier), or 2 zeroed
  * uint32 that launches on one stream share (each launch leaves them zeroed):
  * forward and backward then run as ONE launch each, with grid-wide barriers

@@ -88,7 +88,9 @@ EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats",
            "mcaq_pipeline_get_step", "mcaq_pipeline_set_step",
            "mcaq_mapper_work_floats", "mcaq_mapper_train_forward", "mcaq_mapper_gpart_floats",
            "mcaq_mapper_train_backward", "mcaq_head_gpart_floats", "mcaq_head_train_backward",
-           "mcaq_smask_gpart_floats", "mcaq_smask_train_backward", "mcaq_ema_stats_ex", "mcaq_pack")
+           "mcaq_smask_gpart_floats", "mcaq_smask_train_backward", "mcaq_ema_stats_ex", "mcaq_pack",
+           "mcaq_mapper_train_forward_stage", "mcaq_mapper_train_backward_stage", "mcaq_mapper_train_reduce",
+           "mcaq_mapper_train_grad_reduce")
 
 _LIB = None
 
@@ -160,6 +162,16 @@ def _declare(lib):
     lib.mcaq_mapper_train_forward.argtypes = [ctypes.POINTER(MapperParams), P, I, Fl, Fl, Fl, Fl, I, I, P, P, P, P]
     lib.mcaq_mapper_train_backward.restype = I
     lib.mcaq_mapper_train_backward.argtypes = [ctypes.POINTER(MapperParams), P, I, P, Fl, Fl, Fl, P, P, P, P, I, P, P]
+    lib.mcaq_mapper_train_forward_stage.restype = I
+    lib.mcaq_mapper_train_forward_stage.argtypes = [ctypes.POINTER(MapperParams), P, I, Fl, Fl, Fl, Fl, I, I, P, P, I, P,
+                                                    I, P]
+    lib.mcaq_mapper_train_backward_stage.restype = I
+    lib.mcaq_mapper_train_backward_stage.argtypes = [ctypes.POINTER(MapperParams), P, I, P, Fl, Fl, Fl, P, P, P, I, P,
+                                                     P, I, P]
+    lib.mcaq_mapper_train_reduce.restype = I
+    lib.mcaq_mapper_train_reduce.argtypes = [P, I, I, I, P, P]
+    lib.mcaq_mapper_train_grad_reduce.restype = I
+    lib.mcaq_mapper_train_grad_reduce.argtypes = [I, P, P, I, P]
     lib.mcaq_head_train_backward.restype = I
     lib.mcaq_head_train_backward.argtypes = [ctypes.POINTER(CmlpParams), P, P, P, I, I, I, P, P, P, I, P]
     lib.mcaq_ema_stats_ex.restype = I

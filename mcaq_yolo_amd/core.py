@@ -666,11 +666,16 @@ class ComplexityToBitMappingNetwork(nn.Module):
 
     def _fusable(self):
         """The fused train-mode kernels take the reference stack with plain
-        BatchNorm1d layers (a process-group BatchNorm, dist.GroupBatchNorm1d,
-        keeps the torch path: its statistics span the ranks)."""
+        BatchNorm1d layers, or with dist.GroupBatchNorm1d layers of one
+        process group (statistics over every rank's tiles: the kernels run one
+        stage per launch with the collectives between them)."""
+        from .dist import GroupBatchNorm1d
         net = self.mapping_network
-        return all(type(net[i]) is nn.BatchNorm1d and net[i].track_running_stats and net[i].momentum is not None
-                   and net[i].affine for i in (1, 4, 7))
+        bns = [net[i] for i in (1, 4, 7)]
+        if not all(type(b) in (nn.BatchNorm1d, GroupBatchNorm1d) and b.track_running_stats and
+                   b.momentum is not None and b.affine for b in bns):
+            return False
+        return len({getattr(b, "process_group", None) for b in bns}) == 1
 
     def mapper_blob(self):
         net = self.mapping_network
@@ -1017,10 +1022,31 @@ class _MapperTrainFn(torch.autograd.Function):
         T = max(float(temperature), 0.1) if temperature is not None else 0.0
         work = torch.empty(L.mcaq_mapper_work_floats(n), device=c.device)
         bits = torch.empty(n, device=c.device)
-        abi.check(L.mcaq_mapper_train_forward(ctypes.byref(q), _p(cf), n, mod.min_bits, mod.max_bits, T,
-                                              float(bns[0].momentum), 0 if return_continuous else 1, 1, _p(bits),
-                                              _p(work), _p(_grid_sync_counter(c.device)), _stream()),
-                  "mcaq_mapper_train_forward")
+        pg = _mapper_group(net)
+        ctx.pg, ctx.gath1 = pg, None
+        if pg is None:
+            abi.check(L.mcaq_mapper_train_forward(ctypes.byref(q), _p(cf), n, mod.min_bits, mod.max_bits, T,
+                                                  float(bns[0].momentum), 0 if return_continuous else 1, 1, _p(bits),
+                                                  _p(work), _p(_grid_sync_counter(c.device)), _stream()),
+                      "mcaq_mapper_train_forward")
+        else:
+            # batch sharded over the group (GroupBatchNorm1d): the BatchNorm
+            # statistics of every layer span the ranks' tiles - each rank's
+            # (mean, M2, n) all-gathered between the stage launches
+            import torch.distributed as dist
+            world = dist.get_world_size(pg)
+            gath = [None] * 4
+            for st in (1, 2, 3, 4):
+                abi.check(L.mcaq_mapper_train_forward_stage(
+                    ctypes.byref(q), _p(cf), n, mod.min_bits, mod.max_bits, T, float(bns[0].momentum),
+                    0 if return_continuous else 1, 1, _p(bits), _p(work), st, _p(gath[st - 1]), world, _stream()),
+                    "mcaq_mapper_train_forward_stage")
+                if st <= 3:
+                    rk = torch.empty(_RANK_ENT, device=c.device)
+                    abi.check(L.mcaq_mapper_train_reduce(_p(work), n, 0, st, _p(rk), _stream()),
+                              "mcaq_mapper_train_reduce")
+                    gath[st] = _all_gather_flat(rk, pg, world)
+            ctx.gath1, ctx.world = gath[1], world
         ctx.q, ctx.T, ctx.mod = q, T, mod
         ctx.save_for_backward(cf, work, *params)
         return bits.view(c.shape)
@@ -1036,16 +1062,61 @@ class _MapperTrainFn(torch.autograd.Function):
         sink = mod._gsink.target(list(mod.mapping_network.parameters()))
         gflat, acc = sink if sink is not None else (torch.empty(_MAPPER_G_SIZE, device=cf.device), 0)
         gpart = torch.empty(L.mcaq_mapper_gpart_floats(n), device=cf.device)
-        abi.check(L.mcaq_mapper_train_backward(ctypes.byref(ctx.q), _p(cf), n, _p(_f32c(gbits)), mod.min_bits,
-                                               mod.max_bits, ctx.T, _p(work), _p(gc), _p(gflat), _p(gpart), acc,
-                                               _p(_grid_sync_counter(cf.device)), _stream()),
-                  "mcaq_mapper_train_backward")
+        gb = _f32c(gbits)
+        if ctx.pg is None:
+            abi.check(L.mcaq_mapper_train_backward(ctypes.byref(ctx.q), _p(cf), n, _p(gb), mod.min_bits,
+                                                   mod.max_bits, ctx.T, _p(work), _p(gc), _p(gflat), _p(gpart), acc,
+                                                   _p(_grid_sync_counter(cf.device)), _stream()),
+                      "mcaq_mapper_train_backward")
+        else:
+            # BN backward sums (S1, S2) of each layer all-reduced over the
+            # ranks before the stage that consumes them (the autograd of
+            # GroupBatchNorm1d's all-reduce); parameter gradients stay this
+            # rank's own, for the gradient all-reduce
+            import torch.distributed as dist
+            gs = [None] * 5
+            for st in (4, 3, 2, 1):
+                abi.check(L.mcaq_mapper_train_backward_stage(
+                    ctypes.byref(ctx.q), _p(cf), n, _p(gb), mod.min_bits, mod.max_bits, ctx.T, _p(work), _p(gc),
+                    _p(gpart), st, _p(gs[st]), _p(ctx.gath1), ctx.world, _stream()),
+                    "mcaq_mapper_train_backward_stage")
+                if st >= 2:
+                    bs = torch.empty(128, device=cf.device)
+                    abi.check(L.mcaq_mapper_train_reduce(_p(work), n, 1, st - 1, _p(bs), _stream()),
+                              "mcaq_mapper_train_reduce")
+                    dist.all_reduce(bs, group=ctx.pg)
+                    gs[st - 1] = bs
+            abi.check(L.mcaq_mapper_train_grad_reduce(n, _p(gpart), _p(gflat), acc, _stream()),
+                      "mcaq_mapper_train_grad_reduce")
         if sink is not None:
             return (None, gc.view(gbits.shape), None, None) + (None,) * len(params)
         return (None, gc.view(gbits.shape), None, None) + tuple(_split_flat(gflat, params))
 
 
 _MAPPER_G_SIZE = 4609
+_RANK_ENT = 129          # (mean[64], M2[64], n) of one rank's tiles (csrc/mcaq_train.h RANK_ENT)
+
+
+def _mapper_group(net):
+    """The process group of a mapping network whose BatchNorm layers are
+    dist.GroupBatchNorm1d over one group, else None."""
+    pg = getattr(net[1], "process_group", None)
+    if pg is None:
+        return None
+    import torch.distributed as dist
+    return pg if dist.is_available() and dist.is_initialized() else None
+
+
+def _all_gather_flat(t, pg, world):
+    """All ranks' copies of the flat tensor t, concatenated in rank order."""
+    import torch.distributed as dist
+    if dist.get_backend(pg) == "nccl":
+        out = torch.empty(world * t.numel(), device=t.device, dtype=t.dtype)
+        dist.all_gather_into_tensor(out, t, group=pg)
+        return out
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t, group=pg)
+    return torch.cat(parts)
 
 
 def _smask_backward_fused(ctx, mod, bit_map, absmean, gm, params):

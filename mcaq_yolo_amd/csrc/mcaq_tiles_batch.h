@@ -33,7 +33,10 @@
 
 namespace mcaq {
 
-constexpr int TB_TILES = 64;   // tiles per workgroup (one wave, lane = tile)
+#ifndef MCAQ_TB_TILES
+#define MCAQ_TB_TILES 64
+#endif
+constexpr int TB_TILES = MCAQ_TB_TILES;   // tiles per workgroup (one wave, lane = tile; 32 or 64)
 constexpr int TB_TS = 16;      // floats per tile of the wave's LDS tile array
 enum : int { TT_ACT = 29, TT_BITS = 30, TT_CRAW = 31 };   // tile_tmp slots of the tile kernels
 

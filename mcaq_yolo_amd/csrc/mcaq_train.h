@@ -103,7 +103,18 @@ struct MapperTrainArgs {
   int n, nwg;
   float min_bits, max_bits, temperature, momentum;   // temperature <= 0: none
   int round_bits, update_stats;
+  // batch sharded over `gworld` ranks (process-group BatchNorm, one stage per
+  // launch): gstat = every rank's (mean[64], M2[64], n) of the previous layer
+  // (all-gathered, RANK_ENT floats each), read instead of this launch's
+  // workgroup partials; gbsum = the BN sums (S1[64], S2[64]) of this stage's
+  // layer all-reduced over the ranks; gstat1 = the gathered layer-1 entries
+  // (their counts give the global tile count).  gworld = 0: one process.
+  const float* gstat;
+  const float* gbsum;
+  const float* gstat1;
+  int gworld;
 };
+constexpr int RANK_ENT = 129;   // (mean[64], M2[64], n) of one rank
 
 // work layout (floats)
 struct MapperWork {
@@ -179,10 +190,13 @@ __device__ void map_stats(const MapperTrainArgs& A, const MapperWork& W, float* 
   if (j < N) {
     float n = 0.0f, m = 0.0f, M2 = 0.0f;
     const float* fp = W.fpart(L);
+    // one process: this launch's workgroup partials; sharded: every rank's
+    const int nsrc = A.gworld > 0 ? A.gworld : A.nwg;
 #pragma unroll 4
-    for (int w = part; w < A.nwg; w += MW) {
-      const float nb = W.cnt[w];
-      const float mb = fp[(size_t)w * 128 + j], M2b = fp[(size_t)w * 128 + N + j];
+    for (int w = part; w < nsrc; w += MW) {
+      const float nb = A.gworld > 0 ? A.gstat[(size_t)w * RANK_ENT + 128] : W.cnt[w];
+      const float mb = A.gworld > 0 ? A.gstat[(size_t)w * RANK_ENT + j] : fp[(size_t)w * 128 + j];
+      const float M2b = A.gworld > 0 ? A.gstat[(size_t)w * RANK_ENT + 64 + j] : fp[(size_t)w * 128 + N + j];
       if (nb <= 0.0f) continue;
       const float nn = n + nb, d = mb - m;
       m = m + d * (nb / nn);
@@ -212,8 +226,8 @@ __device__ void map_stats(const MapperTrainArgs& A, const MapperWork& W, float* 
       if (A.update_stats) {
         const float* g; const float* be; float* rm; float* rv; long long* nbt;
         map_bn(A.P, L, g, be, rm, rv, nbt);
-        const float nf = (float)A.n;
-        const float unb = A.n > 1 ? var * (nf / (nf - 1.0f)) : var;
+        const float nf = n;   // the batch's tile count (all ranks' when sharded)
+        const float unb = nf > 1.0f ? var * (nf / (nf - 1.0f)) : var;
         rm[tid] = (1.0f - A.momentum) * rm[tid] + A.momentum * mean;
         rv[tid] = (1.0f - A.momentum) * rv[tid] + A.momentum * unb;
         if (tid == 0 && nbt) nbt[0] += 1;
@@ -414,7 +428,11 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
       float s1 = 0.0f, s2 = 0.0f;
 #pragma unroll
       for (int p = 0; p < MW; ++p) { s1 += s_tmp[p * 128 + tid]; s2 += s_tmp[p * 128 + 64 + tid]; }
-      s_sg[tid] = s1; s_sgx[tid] = s2;
+      // sharded: the BN backward takes the sums over every rank's tiles; the
+      // gamma / beta gradients below stay this rank's own (summed by the
+      // gradient all-reduce)
+      s_sg[tid] = A.gworld > 0 ? A.gbsum[tid] : s1;
+      s_sgx[tid] = A.gworld > 0 ? A.gbsum[64 + tid] : s2;
       s_mean[tid] = W.stat[(S - 1) * 128 + tid]; s_rstd[tid] = W.stat[(S - 1) * 128 + 64 + tid];
       // gamma / beta gradients are the BN sums themselves: workgroup 0's
       // partial slot holds them, the others zero
@@ -423,7 +441,12 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
       gp[ob + tid] = blockIdx.x == 0 ? s1 : 0.0f;
     }
     __syncthreads();
-    const float inv_n = 1.0f / (float)A.n;
+    float ntot = (float)A.n;
+    if (A.gworld > 0) {
+      ntot = 0.0f;
+      for (int r = 0; r < A.gworld; ++r) ntot += A.gstat1[(size_t)r * RANK_ENT + 128];
+    }
+    const float inv_n = 1.0f / ntot;
 #pragma unroll
     for (int i = 0; i < N / MW; ++i) {
       const int j = q + i * MW;
@@ -526,6 +549,42 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
       const float gcv = g0 + 2.0f * c * g1 + g2 / (1.0f + c);
       A.gc[t] = (craw >= 0.0f && craw <= 1.0f) ? gcv : 0.0f;
     }
+  }
+}
+
+// sharded mapper: this rank's share of a batch statistic, in workgroup order.
+// kind 0: (mean[64], M2[64], n) of layer `layer` from the forward partials
+// (Chan's combination, as map_stats); kind 1: the BN sums (S1[64], S2[64])
+// of layer `layer` from the backward partials of stage layer + 1
+__global__ __launch_bounds__(64) void mcaq_mapper_reduce_kernel(const float* work, int n, int kind, int layer,
+                                                                float* out) {
+  const MapperWork W = mapper_work(const_cast<float*>(work), n);
+  const int j = threadIdx.x;
+  const int N = layer == 2 ? 64 : 32;
+  if (kind == 0) {
+    float c = 0.0f, m = 0.0f, M2 = 0.0f;
+    const float* fp = W.fpart(layer);
+    for (int w = 0; w < W.nwg; ++w) {
+      const float nb = W.cnt[w];
+      if (nb <= 0.0f || j >= N) continue;
+      const float mb = fp[(size_t)w * 128 + j], M2b = fp[(size_t)w * 128 + N + j];
+      const float nn = c + nb, d = mb - m;
+      m = m + d * (nb / nn);
+      M2 = M2 + M2b + d * d * (c * nb / nn);
+      c = nn;
+    }
+    float cnt = 0.0f;
+    for (int w = 0; w < W.nwg; ++w) cnt += W.cnt[w];
+    out[j] = j < N ? m : 0.0f;
+    out[64 + j] = j < N ? M2 : 0.0f;
+    if (j == 0) out[128] = cnt;
+  } else {
+    const float* bq = W.bpart_of(layer + 1);
+    float s1 = 0.0f, s2 = 0.0f;
+    if (j < N)
+      for (int w = 0; w < W.nwg; ++w) { s1 += bq[(size_t)w * 128 + j]; s2 += bq[(size_t)w * 128 + 64 + j]; }
+    out[j] = s1;
+    out[64 + j] = s2;
   }
 }
 
@@ -1125,6 +1184,67 @@ int mcaq_mapper_train_backward(const mcaq_mapper_params* P, const float* c, int 
   hipLaunchKernelGGL(mcaq_mapper_bwd_kernel<1>, g, t, 0, stream, A);
   hipLaunchKernelGGL(mcaq_tr_reduce_kernel, dim3((MG_SIZE + 255) / 256), dim3(256), 0, stream, (const float*)gpart,
                      A.nwg, (int)MG_SIZE, (int)MG_SIZE, gparams, accumulate ? 1 : 0);
+  return (int)hipGetLastError();
+}
+
+int mcaq_mapper_train_forward_stage(const mcaq_mapper_params* P, const float* c, int n, float min_bits,
+                                    float max_bits, float temperature, float momentum, int round_bits,
+                                    int update_stats, float* bits, float* work, int stage, const float* gathered,
+                                    int world, hipStream_t stream) {
+  using namespace mcaq;
+  if (!P || !c || !bits || !work || n < 1 || stage < 1 || stage > 4 || world < 1 || (stage >= 2 && !gathered))
+    return (int)hipErrorInvalidValue;
+  MapperTrainArgs A{};
+  A.P = *P; A.c = c; A.bits = bits; A.work = work; A.n = n; A.nwg = (n + TR_TPB - 1) / TR_TPB;
+  A.min_bits = min_bits; A.max_bits = max_bits; A.temperature = temperature; A.momentum = momentum;
+  A.round_bits = round_bits; A.update_stats = update_stats;
+  A.gstat = gathered; A.gworld = stage >= 2 ? world : 0;
+  const dim3 g(A.nwg), t(MTH);
+  switch (stage) {
+    case 1: hipLaunchKernelGGL(mcaq_mapper_fwd_kernel<1>, g, t, 0, stream, A); break;
+    case 2: hipLaunchKernelGGL(mcaq_mapper_fwd_kernel<2>, g, t, 0, stream, A); break;
+    case 3: hipLaunchKernelGGL(mcaq_mapper_fwd_kernel<3>, g, t, 0, stream, A); break;
+    default: hipLaunchKernelGGL(mcaq_mapper_fwd_kernel<4>, g, t, 0, stream, A); break;
+  }
+  return (int)hipGetLastError();
+}
+
+int mcaq_mapper_train_backward_stage(const mcaq_mapper_params* P, const float* c, int n, const float* gbits,
+                                     float min_bits, float max_bits, float temperature, float* work, float* gc,
+                                     float* gpart, int stage, const float* gsums, const float* gathered1, int world,
+                                     hipStream_t stream) {
+  using namespace mcaq;
+  if (!P || !c || !gbits || !gc || !gpart || !work || n < 1 || stage < 1 || stage > 4 || world < 1 ||
+      (stage <= 3 && (!gsums || !gathered1)))
+    return (int)hipErrorInvalidValue;
+  MapperTrainArgs A{};
+  A.P = *P; A.c = c; A.gbits = gbits; A.gc = gc; A.work = work; A.gpart = gpart; A.n = n;
+  A.nwg = (n + TR_TPB - 1) / TR_TPB;
+  A.min_bits = min_bits; A.max_bits = max_bits; A.temperature = temperature;
+  A.gbsum = gsums; A.gstat1 = gathered1; A.gworld = stage <= 3 ? world : 0;
+  const dim3 g(A.nwg), t(MTH);
+  switch (stage) {
+    case 4: hipLaunchKernelGGL(mcaq_mapper_bwd_kernel<4>, g, t, 0, stream, A); break;
+    case 3: hipLaunchKernelGGL(mcaq_mapper_bwd_kernel<3>, g, t, 0, stream, A); break;
+    case 2: hipLaunchKernelGGL(mcaq_mapper_bwd_kernel<2>, g, t, 0, stream, A); break;
+    default: hipLaunchKernelGGL(mcaq_mapper_bwd_kernel<1>, g, t, 0, stream, A); break;
+  }
+  return (int)hipGetLastError();
+}
+
+int mcaq_mapper_train_reduce(const float* work, int n, int kind, int layer, float* out, hipStream_t stream) {
+  using namespace mcaq;
+  if (!work || !out || n < 1 || kind < 0 || kind > 1 || layer < 1 || layer > 3) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(mcaq_mapper_reduce_kernel, dim3(1), dim3(64), 0, stream, work, n, kind, layer, out);
+  return (int)hipGetLastError();
+}
+
+int mcaq_mapper_train_grad_reduce(int n, const float* gpart, float* gparams, int accumulate, hipStream_t stream) {
+  using namespace mcaq;
+  if (!gpart || !gparams || n < 1) return (int)hipErrorInvalidValue;
+  const int nwg = (n + TR_TPB - 1) / TR_TPB;
+  hipLaunchKernelGGL(mcaq_tr_reduce_kernel, dim3((MG_SIZE + 255) / 256), dim3(256), 0, stream, gpart, nwg,
+                     (int)MG_SIZE, (int)MG_SIZE, gparams, accumulate ? 1 : 0);
   return (int)hipGetLastError();
 }
 
