@@ -550,6 +550,58 @@ class Runner(_RunMixin):
             torch.cuda.current_stream().wait_stream(st)
 
 
+class PrefetchRunner(_RunMixin):
+    """--schedule prefetch (N = 1): `depth` streams; step i replays, on stream
+    i % depth, one HIP graph of two branches - pass 1 of batch i + depth on a
+    side stream (the HBM read of a batch `depth` steps ahead) beside the
+    morphology and pass 2 of batch i (whose pass 1 the same stream ran
+    `depth` steps before) - so a stream's critical path per step is max(pass
+    1, morphology + pass 2) instead of their sum.  2 * depth plans: batch j
+    uses plan j % (2 depth); a plan's next pass 1 is in the graph after the
+    one that consumed it on the same stream (stream order protects it)."""
+
+    def __init__(self, plans, depth):
+        if len(plans) < 2 * depth:
+            raise ValueError("prefetch schedule needs >= 2 * depth input batches")
+        self.plans, self.depth = plans, depth
+        self.streams = [torch.cuda.Stream() for _ in range(depth)]
+        self.sides = [torch.cuda.Stream() for _ in range(depth)]
+        self.i = 0
+        P = len(plans)
+        torch.cuda.synchronize()
+        for plan in plans:                       # warm the launchers outside capture
+            plan.launch()
+        torch.cuda.synchronize()
+        self.graphs = {}
+        for i in range(P):
+            st, side = self.streams[i % depth], self.sides[i % depth]
+            cur, nxt = plans[i % P], plans[(i + depth) % P]
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=st):
+                side.wait_stream(st)
+                with torch.cuda.stream(side):
+                    nxt.launch_stats(side)
+                cur.launch_morph(st)
+                cur.launch_quant(st)
+                st.wait_stream(side)
+            self.graphs[i % P] = g
+        torch.cuda.synchronize()
+        for k in range(depth):                   # prologue: pass 1 of the first `depth` batches
+            with torch.cuda.stream(self.streams[k]):
+                plans[k].launch_stats(self.streams[k])
+
+    def step(self):
+        i = self.i
+        self.i += 1
+        st = self.streams[i % self.depth]
+        with torch.cuda.stream(st):
+            self.graphs[i % len(self.plans)].replay()
+
+    def sync(self):
+        for st in self.streams:
+            torch.cuda.current_stream().wait_stream(st)
+
+
 class SplitRunner(_RunMixin):
     """--schedule split (N = 1, eager): the HBM passes of every batch on ONE
     streaming stream, back to back (stats(j + L), then quant(j)), the
@@ -735,7 +787,7 @@ def main():
     ap.add_argument("--channels-last", action="store_true", help="--e2e: NHWC network (experiment)")
     ap.add_argument("--find", action="store_true", help="--e2e: MIOpen Find (torch.backends.cudnn.benchmark)")
     ap.add_argument("--eager", action="store_true", help="no HIP graphs")
-    ap.add_argument("--schedule", choices=("staged", "streams", "split"), default="streams",
+    ap.add_argument("--schedule", choices=("staged", "streams", "split", "prefetch"), default="streams",
                     help="streams (default): --pipeline batches in flight, one HIP graph each; staged: software "
                          "pipeline, pass 1 (i) + pass 2 (i-3) | pass A (i-1) | pass B (i-2) on three streams "
                          "(eager, host-enqueue bound: 77 vs 64 us per step, profiles/r03_base); split: HBM "
@@ -787,6 +839,8 @@ def main():
         nin = max(nin, args.staged_plans)
     if args.schedule == "split":
         nin = max(nin, args.lookahead + 1)
+    if args.schedule == "prefetch":
+        nin = max(nin, 2 * depth)
     for p in range(nin):
         # each batch in flight has its own synthetic input (seeded per rank and slot)
         feats = [synth_features(B, c, h, w, 1000 * args.config + i + 7919 * rank + 104729 * p, dev)
@@ -798,13 +852,17 @@ def main():
         plans.append(plan)
     torch.cuda.synchronize()
 
-    use_graph = not args.eager and args.schedule == "streams"
+    use_graph = not args.eager and args.schedule in ("streams", "prefetch")
     if args.schedule == "staged":
         runner = StagedRunner(plans, pg, cu_masks_for(args.morph_cus), group=args.graph_steps)
     elif args.schedule == "split":
         if pg is not None:
             raise SystemExit("--schedule split is a single-GPU experiment")
         runner = SplitRunner(plans, args.lookahead)
+    elif args.schedule == "prefetch":
+        if pg is not None:
+            raise SystemExit("--schedule prefetch is single-process (N = 1)")
+        runner = PrefetchRunner(plans, depth)
     else:
         runner = Runner(plans, pg, use_graph, depth)
     runner.run(max(args.warmup, 1))
@@ -919,7 +977,9 @@ def main():
                                                   ", morph on %d CUs" % args.morph_cus if args.morph_cus else ""),
                                     "streams": "streams: %d batch chains on %d streams, one HIP graph each"
                                                % (depth, depth),
-                                    "split": "split (look-ahead %d)" % args.lookahead}[args.schedule],
+                                    "split": "split (look-ahead %d)" % args.lookahead,
+                                    "prefetch": "prefetch: %d streams, per step one HIP graph = pass 1 of batch i+%d "
+                                                "beside morphology + pass 2 of batch i" % (depth, depth)}[args.schedule],
                        "input_batches": len(plans),
                        "latency_ms_single_batch": round(latency_ms, 4),
                        "host_enqueue_us_per_step": round(t_enq / args.steps * 1e6, 1),
