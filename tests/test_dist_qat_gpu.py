@@ -64,7 +64,8 @@ def _inputs():
         up = torch.nn.functional.interpolate(lo, size=(s, s), mode="bilinear", align_corners=False)
         feats.append(torch.nn.functional.silu(1.5 * hi + 2 * up))
         G.append(torch.randn(B, c, s, s, generator=gen) * 1e-3)
-    GB = [torch.randn(B, s // 8, s // 8, generator=gen) for _, s in SHAPES]
+    from mcaq_yolo_amd.engine import tile_size
+    GB = [torch.randn(B, s // tile_size(s, 8), s // tile_size(s, 8), generator=gen) for _, s in SHAPES]
     return feats, G, GB
 
 
