@@ -147,6 +147,15 @@ def main_qat(args, world, rank, dev, pg):
     opt = torch.optim.SGD(params_, lr=1e-3, momentum=0.9)
     target_bits = 4.0
 
+    # how the train-mode mapper ran (fused kernels, or the torch autograd path)
+    fused = {"calls": 0}
+    orig_apply = core._MapperTrainFn.apply
+
+    def counted(*a, **k):
+        fused["calls"] += 1
+        return orig_apply(*a, **k)
+    core._MapperTrainFn.apply = counted
+
     def step():
         opt.zero_grad(set_to_none=True)
         for f in feats:
@@ -238,6 +247,8 @@ def main_qat(args, world, rank, dev, pg):
         run()
     torch.cuda.synchronize()
     step_s = (time.perf_counter() - t0) / args.steps
+    core._MapperTrainFn.apply = orig_apply
+    fused_per_step = fused["calls"] / max(1, args.steps + max(args.warmup, 3)) if not use_graph else None
     if pg is not None:
         import torch.distributed as dist
         t = torch.tensor([step_s], device=dev, dtype=torch.float64)
@@ -279,6 +290,9 @@ def main_qat(args, world, rank, dev, pg):
                               "alg_bytes_per_step": 24 * elems},
             "kernels": kern,
             "cpu_baseline": None,
+            "mapper": {"fused_kernels": fused["calls"] > 0,
+                       "batchnorm": type(h.bit_mapper.mapping_network[1]).__name__,
+                       "fused_calls_per_eager_step": fused_per_step},
         }
         if not args.no_cpu and world == 1:
             out["cpu_baseline"] = cpu_baseline_qat()
