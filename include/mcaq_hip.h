@@ -41,7 +41,7 @@ typedef void* hipEvent_t;
 extern "C" {
 #endif
 
-#define MCAQ_ABI_VERSION 12
+#define MCAQ_ABI_VERSION 13
 /* largest dynamic LDS request of the morph kernel (gfx950: 160 KiB per CU) */
 #define MCAQ_MORPH_LDS_LIMIT 163840
 
@@ -311,8 +311,10 @@ typedef struct {
 
 /* bits (n) = train-mode mapper of c (n): 4 launches; work keeps the
  * activations and batch statistics for the backward (temperature <= 0:
- * none; round_bits: straight-through round; update_stats: BN running stats
- * with `momentum`, num_batches_tracked += 1) */
+ * none; round_bits: straight-through round; update_stats 1: BN running stats
+ * with `momentum`, num_batches_tracked += 1; update_stats 2: the update is
+ * deferred - its batch mean / unbiased variance stay in `work` for
+ * mcaq_mapper_running_update) */
 size_t mcaq_mapper_work_floats(int n);
 int mcaq_mapper_train_forward(const mcaq_mapper_params* P, const float* c, int n, float min_bits, float max_bits,
                               float temperature, float momentum, int round_bits, int update_stats, float* bits,
@@ -347,17 +349,26 @@ int mcaq_mapper_train_backward_stage(const mcaq_mapper_params* P, const float* c
  * kind 1: this rank's BN sums (S1[64], S2[64]) of layer 1..3 (backward) */
 int mcaq_mapper_train_reduce(const float* work, int n, int kind, int layer, float* out, hipStream_t stream);
 int mcaq_mapper_train_grad_reduce(int n, const float* gpart, float* gparams, int accumulate, hipStream_t stream);
+/* The deferred running-stats updates of `count` (<= 8) forwards run with
+ * update_stats 2 (works[k] of ns[k] tiles), applied in list order - the
+ * values those forwards would have left with update_stats 1 one after
+ * another.  For hook scales whose train-mode mappers run concurrently on
+ * several streams (the running buffers are shared).  1 launch. */
+int mcaq_mapper_running_update(const mcaq_mapper_params* P, const float* const* works, const int* ns, int count,
+                               float momentum, hipStream_t stream);
 /* grid_sync: NULL (one launch per batch-statistics barrier), or 2 zeroed
  * uint32 that launches on one stream share (each launch leaves them zeroed):
  * forward and backward then run as ONE launch each, with grid-wide barriers
  * between the stages (n <= 256 * 64 tiles). */
 /* analyzer head: gC (B, ht, wt) -> gcraw (B, ht, wt) work, gparams (2881:
  * complexity_mlp parameters() order); phi (B*ht*wt, 8), craw = the MLP output
- * before the bilateral; 3 launches */
+ * before the bilateral; 3 launches (2 with gparams NULL: the caller then
+ * reduces gpart with mcaq_head_train_grad_reduce) */
 size_t mcaq_head_gpart_floats(int n);
 int mcaq_head_train_backward(const mcaq_cmlp_params* P, const float* phi, const float* craw, const float* gC, int B,
                              int ht, int wt, float* gcraw, float* gparams, float* gpart, int accumulate,
                              hipStream_t stream);
+int mcaq_head_train_grad_reduce(int n, const float* gpart, float* gparams, int accumulate, hipStream_t stream);
 /* soft mask: gm (B, H, W) -> gbits (B, ht, wt) (accumulate != 0: added),
  * gparams (170: net parameters() order); 2 launches */
 size_t mcaq_smask_gpart_floats(int B);
@@ -365,7 +376,10 @@ int mcaq_smask_train_backward(const mcaq_smask_params* P, const float* bits, con
                               int B, int H, int W, int ht, int wt, float* gbits, int accumulate, float* gparams,
                               float* gpart, hipStream_t stream);
 /* gparams of the mapper / head backward: accumulate != 0 adds to gparams
- * (the parameters' persistent gradient storage), 0 overwrites it. */
+ * (the parameters' persistent gradient storage), 0 overwrites it; NULL
+ * (without grid_sync): no reduction launch - the partials stay in gpart for
+ * the matching *_grad_reduce call, which a caller with several streams
+ * orders itself. */
 
 /* ---- device packing of parameter blobs (the kernels' weight layouts) -------
  * Segment i fills out[dst .. dst + len): mode 0 copies n floats from src;

@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libmcaq_hip.so")
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -90,7 +90,7 @@ EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats",
            "mcaq_mapper_train_backward", "mcaq_head_gpart_floats", "mcaq_head_train_backward",
            "mcaq_smask_gpart_floats", "mcaq_smask_train_backward", "mcaq_ema_stats_ex", "mcaq_pack",
            "mcaq_mapper_train_forward_stage", "mcaq_mapper_train_backward_stage", "mcaq_mapper_train_reduce",
-           "mcaq_mapper_train_grad_reduce")
+           "mcaq_mapper_train_grad_reduce", "mcaq_mapper_running_update", "mcaq_head_train_grad_reduce")
 
 _LIB = None
 
@@ -172,6 +172,11 @@ def _declare(lib):
     lib.mcaq_mapper_train_reduce.argtypes = [P, I, I, I, P, P]
     lib.mcaq_mapper_train_grad_reduce.restype = I
     lib.mcaq_mapper_train_grad_reduce.argtypes = [I, P, P, I, P]
+    lib.mcaq_mapper_running_update.restype = I
+    lib.mcaq_mapper_running_update.argtypes = [ctypes.POINTER(MapperParams), ctypes.POINTER(P), ctypes.POINTER(I), I,
+                                               Fl, P]
+    lib.mcaq_head_train_grad_reduce.restype = I
+    lib.mcaq_head_train_grad_reduce.argtypes = [I, P, P, I, P]
     lib.mcaq_head_train_backward.restype = I
     lib.mcaq_head_train_backward.argtypes = [ctypes.POINTER(CmlpParams), P, P, P, I, I, I, P, P, P, I, P]
     lib.mcaq_ema_stats_ex.restype = I

@@ -134,8 +134,11 @@ class _BlobCache:
     def __init__(self):
         self.key = None
         self.blob = None
+        self.pinned = None
 
     def get(self, tensors, pack):
+        if self.pinned is not None:
+            return self.pinned
         key = tuple((t.data_ptr(), t._version, t.device) for t in tensors)
         # under HIP-graph capture the pack is always recorded, so every replay
         # rebuilds the blob from the live parameters (an optimizer step inside
@@ -949,6 +952,7 @@ class _HeadTrainFn(torch.autograd.Function):
         phi, c, craw = mod._run(features, want_c=True, want_craw=True)
         mod._last_phi = phi
         ctx.mod = mod
+        ctx.conc = concurrent_scales.active
         ctx.save_for_backward(phi, craw, *params)
         return c
 
@@ -965,11 +969,107 @@ class _HeadTrainFn(torch.autograd.Function):
         sink = ctx.mod._gsink.target(mod_params) if len(mod_params) == len(params) else None
         gflat, acc = sink if sink is not None else (torch.empty(_CM_SIZE, device=craw.device), 0)
         gpart = torch.empty(L.mcaq_head_gpart_floats(n), device=craw.device)
+        if ctx.conc is not None:
+            ctx.conc.join_after_backward()
+        conc = ctx.conc if sink is not None else None    # shared flat buffer, scales on several streams
         abi.check(L.mcaq_head_train_backward(ctypes.byref(q), _p(phi), _p(craw), _p(_f32c(gc)), B, ht, wt, _p(gcraw),
-                                             _p(gflat), _p(gpart), acc, _stream()), "mcaq_head_train_backward")
+                                             None if conc else _p(gflat), _p(gpart), acc, _stream()),
+                  "mcaq_head_train_backward")
+        if conc is not None:
+            conc.ordered(ctx.mod._gsink, lambda: abi.check(
+                L.mcaq_head_train_grad_reduce(n, _p(gpart), _p(gflat), acc, _stream()), "mcaq_head_train_grad_reduce"))
         if sink is not None:
             return (None, None) + (None,) * len(params)
         return (None, None) + tuple(_split_flat(gflat, params))
+
+
+# ---------------------------------------------------------------------------
+# hook scales on concurrent streams (train mode, MCAQHooks.forward_features)
+# ---------------------------------------------------------------------------
+class concurrent_scales:
+    """Scope of one train-mode hook step whose scales run on their own HIP
+    streams (each scale's forward, and so its backward, on its stream).  The
+    modules the scales share get ordered here instead of by one stream:
+      * the complexity-MLP blob is packed once, before the fork (pinned);
+      * the train-mode mapper's BatchNorm running statistics: each scale's
+        forward leaves its batch mean / unbiased variance in its work buffer
+        (update_stats 2) and `finish` applies the updates in scale order on
+        the joining stream (mcaq_mapper_running_update: the values the scales
+        would have left one after another);
+      * gradients accumulated in-kernel into the shared flat buffers
+        (_GradSink): each backward's reduction launch waits for the previous
+        one (events, in autograd's launch order) - a fixed order of fp32 sums.
+    Entered by the caller on its own stream; `finish(stream)` after the join."""
+
+    active = None
+
+    def __init__(self, analyzer=None, main=None, streams=()):
+        self.analyzer = analyzer
+        self.mapper = {}          # id(module) -> [q, works, ns, momentum, keepalive]
+        self.events = {}          # grad sink -> event of its last reduction launch
+        self.main, self.streams = main, list(streams)
+        self._join_queued = False
+
+    def __enter__(self):
+        if concurrent_scales.active is not None:
+            raise RuntimeError("concurrent_scales scopes do not nest")
+        if self.analyzer is not None:
+            an = self.analyzer
+            an._blob.pinned = an.cmlp_blob()
+        concurrent_scales.active = self
+        return self
+
+    def __exit__(self, *exc):
+        concurrent_scales.active = None
+        if self.analyzer is not None:
+            self.analyzer._blob.pinned = None
+        return False
+
+    def defer_mapper(self, mod, q, work, n, momentum):
+        e = self.mapper.setdefault(id(mod), [q, [], [], momentum, mod])
+        e[1].append(work)
+        e[2].append(n)
+
+    def finish(self):
+        """On the joining stream, after every scale's stream: the deferred
+        mapper running-statistics updates, in scale order."""
+        L = abi.lib()
+        for q, works, ns, momentum, _mod in self.mapper.values():
+            for k in range(0, len(works), 8):
+                w, n = works[k:k + 8], ns[k:k + 8]
+                wa = (abi.P * len(w))(*[_p(t) for t in w])
+                na = (abi.I * len(n))(*n)
+                abi.check(L.mcaq_mapper_running_update(ctypes.byref(q), wa, na, len(w), float(momentum), _stream()),
+                          "mcaq_mapper_running_update")
+        self.mapper = {}
+
+    def join_after_backward(self):
+        """Called from the backward of a scale's node: once per backward pass,
+        queue an engine callback that makes the stream the forward joined on
+        wait for every scale stream (the in-kernel gradient accumulations on
+        those streams are not autograd results, so the engine's own leaf-stream
+        sync need not cover them)."""
+        if self._join_queued or self.main is None:
+            return
+        self._join_queued = True
+
+        def join():
+            self._join_queued = False
+            for st in self.streams:
+                self.main.wait_stream(st)
+        torch.autograd.Variable._execution_engine.queue_callback(join)
+
+    def ordered(self, key, launch):
+        """Run `launch()` (a reduction into a buffer the scales share) on the
+        current stream after the previous one of the same key."""
+        st = torch.cuda.current_stream()
+        ev = self.events.get(key)
+        if ev is not None:
+            st.wait_event(ev)
+        launch()
+        ev = torch.cuda.Event()
+        ev.record(st)
+        self.events[key] = ev
 
 
 # one-launch train-mode mapper (grid barriers between its batch-statistics
@@ -1024,11 +1124,18 @@ class _MapperTrainFn(torch.autograd.Function):
         bits = torch.empty(n, device=c.device)
         pg = _mapper_group(net)
         ctx.pg, ctx.gath1 = pg, None
+        conc = concurrent_scales.active if pg is None else None
+        ctx.conc = conc
         if pg is None:
+            # scales on concurrent streams: the shared running statistics are
+            # updated later, in scale order (concurrent_scales.finish)
             abi.check(L.mcaq_mapper_train_forward(ctypes.byref(q), _p(cf), n, mod.min_bits, mod.max_bits, T,
-                                                  float(bns[0].momentum), 0 if return_continuous else 1, 1, _p(bits),
+                                                  float(bns[0].momentum), 0 if return_continuous else 1,
+                                                  2 if conc is not None else 1, _p(bits),
                                                   _p(work), _p(_grid_sync_counter(c.device)), _stream()),
                       "mcaq_mapper_train_forward")
+            if conc is not None:
+                conc.defer_mapper(mod, q, work, n, float(bns[0].momentum))
         else:
             # batch sharded over the group (GroupBatchNorm1d): the BatchNorm
             # statistics of every layer span the ranks' tiles - each rank's
@@ -1063,7 +1170,18 @@ class _MapperTrainFn(torch.autograd.Function):
         gflat, acc = sink if sink is not None else (torch.empty(_MAPPER_G_SIZE, device=cf.device), 0)
         gpart = torch.empty(L.mcaq_mapper_gpart_floats(n), device=cf.device)
         gb = _f32c(gbits)
-        if ctx.pg is None:
+        if ctx.conc is not None:
+            ctx.conc.join_after_backward()
+        conc = ctx.conc if sink is not None else None
+        if ctx.pg is None and conc is not None:
+            # the scales' reductions into the shared flat buffer, one after another
+            abi.check(L.mcaq_mapper_train_backward(ctypes.byref(ctx.q), _p(cf), n, _p(gb), mod.min_bits,
+                                                   mod.max_bits, ctx.T, _p(work), _p(gc), None, _p(gpart), acc,
+                                                   None, _stream()), "mcaq_mapper_train_backward")
+            conc.ordered(mod._gsink, lambda: abi.check(
+                L.mcaq_mapper_train_grad_reduce(n, _p(gpart), _p(gflat), acc, _stream()),
+                "mcaq_mapper_train_grad_reduce"))
+        elif ctx.pg is None:
             abi.check(L.mcaq_mapper_train_backward(ctypes.byref(ctx.q), _p(cf), n, _p(gb), mod.min_bits,
                                                    mod.max_bits, ctx.T, _p(work), _p(gc), _p(gflat), _p(gpart), acc,
                                                    _p(_grid_sync_counter(cf.device)), _stream()),

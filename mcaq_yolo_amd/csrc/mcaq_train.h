@@ -122,6 +122,7 @@ struct MapperWork {
   float *part, *cnt;              // per-workgroup (mean[64], M2[64]) and counts
   float *stat;                    // 3 layers x (mean[64], rstd[64])
   float *bpart;                   // backward BN partials [2][nwg][2 x 64]
+  float *rstat;                   // update_stats == 2: 3 layers x (mean[64], unbiased var[64]), deferred update
   int nwg;
   __host__ __device__ float* fpart(int layer) const { return part + (size_t)(layer & 1) * nwg * 128; }
   __host__ __device__ float* bpart_of(int stage) const { return bpart + (size_t)(stage & 1) * nwg * 128; }
@@ -130,7 +131,8 @@ struct MapperWork {
 // partials the previous launch wrote while writing its own
 __host__ __device__ inline size_t mapper_work_floats(int n) {
   const int nwg = (n + TR_TPB - 1) / TR_TPB;
-  return (size_t)n * (32 + 64 + 32 + 1 + 64) + (size_t)2 * nwg * 128 + nwg + 3 * 128 + (size_t)2 * nwg * 128 + 64;
+  return (size_t)n * (32 + 64 + 32 + 1 + 64) + (size_t)2 * nwg * 128 + nwg + 3 * 128 + (size_t)2 * nwg * 128 + 64 +
+         3 * 128;
 }
 __host__ __device__ inline MapperWork mapper_work(float* w, int n) {
   const int nwg = (n + TR_TPB - 1) / TR_TPB;
@@ -138,6 +140,7 @@ __host__ __device__ inline MapperWork mapper_work(float* w, int n) {
   m.a1 = w; m.a2 = m.a1 + (size_t)n * 32; m.a3 = m.a2 + (size_t)n * 64; m.o = m.a3 + (size_t)n * 32;
   m.gy = m.o + n; m.part = m.gy + (size_t)n * 64; m.cnt = m.part + (size_t)2 * nwg * 128; m.stat = m.cnt + nwg;
   m.bpart = m.stat + 3 * 128;
+  m.rstat = m.bpart + (size_t)2 * nwg * 128 + 64;
   m.nwg = nwg;
   return m;
 }
@@ -176,6 +179,40 @@ __device__ __forceinline__ void wg_moments(const float (&v)[NQ], bool valid, flo
     const float d = valid ? v[f] - mean : 0.0f;
     const float M2 = wave_sum(d * d);
     if ((threadIdx.x & 63) == 0) { part[f0 + f] = mean; part[nfeat + f0 + f] = M2; }
+  }
+}
+
+// BatchNorm1d running-stats update (momentum form of torch's batch_norm)
+__device__ __forceinline__ void map_running_update(float* rm, float* rv, long long* nbt, int j, float momentum,
+                                                   float mean, float unb) {
+  rm[j] = (1.0f - momentum) * rm[j] + momentum * mean;
+  rv[j] = (1.0f - momentum) * rv[j] + momentum * unb;
+  if (j == 0 && nbt) nbt[0] += 1;
+}
+
+// deferred running-stats updates (update_stats == 2) of up to MAPPER_RU_MAX
+// forwards, applied in list order: the same arithmetic, in the same order, as
+// those forwards updating the buffers themselves one after another
+constexpr int MAPPER_RU_MAX = 8;
+struct MapperRunningArgs {
+  mcaq_mapper_params P;
+  const float* rstat[MAPPER_RU_MAX];
+  int count;
+  float momentum;
+};
+__global__ __launch_bounds__(64) void mcaq_mapper_running_kernel(MapperRunningArgs A) {
+  const int j = threadIdx.x;
+  for (int k = 0; k < A.count; ++k) {
+#pragma unroll
+    for (int L = 1; L <= 3; ++L) {
+      const int N = L == 2 ? 64 : 32;
+      if (j < N) {
+        const float* g; const float* be; float* rm; float* rv; long long* nbt;
+        map_bn(A.P, L, g, be, rm, rv, nbt);
+        map_running_update(rm, rv, nbt, j, A.momentum, A.rstat[k][(L - 1) * 128 + j],
+                           A.rstat[k][(L - 1) * 128 + 64 + j]);
+      }
+    }
   }
 }
 
@@ -224,13 +261,18 @@ __device__ void map_stats(const MapperTrainArgs& A, const MapperWork& W, float* 
       W.stat[(L - 1) * 128 + tid] = mean;
       W.stat[(L - 1) * 128 + 64 + tid] = rstd;
       if (A.update_stats) {
-        const float* g; const float* be; float* rm; float* rv; long long* nbt;
-        map_bn(A.P, L, g, be, rm, rv, nbt);
         const float nf = n;   // the batch's tile count (all ranks' when sharded)
         const float unb = nf > 1.0f ? var * (nf / (nf - 1.0f)) : var;
-        rm[tid] = (1.0f - A.momentum) * rm[tid] + A.momentum * mean;
-        rv[tid] = (1.0f - A.momentum) * rv[tid] + A.momentum * unb;
-        if (tid == 0 && nbt) nbt[0] += 1;
+        if (A.update_stats == 2) {
+          // deferred: the caller applies the update later, in its own order
+          // (several hook scales on concurrent streams share these buffers)
+          W.rstat[(L - 1) * 128 + tid] = mean;
+          W.rstat[(L - 1) * 128 + 64 + tid] = unb;
+        } else {
+          const float* g; const float* be; float* rm; float* rv; long long* nbt;
+          map_bn(A.P, L, g, be, rm, rv, nbt);
+          map_running_update(rm, rv, nbt, tid, A.momentum, mean, unb);
+        }
       }
     }
   }
@@ -1168,7 +1210,7 @@ int mcaq_mapper_train_backward(const mcaq_mapper_params* P, const float* c, int 
                                float* gparams, float* gpart, int accumulate, unsigned* grid_sync,
                                hipStream_t stream) {
   using namespace mcaq;
-  if (!P || !c || !gbits || !gc || !gparams || !gpart || !work || n < 1) return (int)hipErrorInvalidValue;
+  if (!P || !c || !gbits || !gc || !gpart || !work || n < 1 || (!gparams && grid_sync)) return (int)hipErrorInvalidValue;
   MapperTrainArgs A{};
   A.P = *P; A.c = c; A.gbits = gbits; A.gc = gc; A.work = work; A.gpart = gpart; A.n = n;
   A.nwg = (n + TR_TPB - 1) / TR_TPB;
@@ -1182,8 +1224,23 @@ int mcaq_mapper_train_backward(const mcaq_mapper_params* P, const float* c, int 
   hipLaunchKernelGGL(mcaq_mapper_bwd_kernel<3>, g, t, 0, stream, A);
   hipLaunchKernelGGL(mcaq_mapper_bwd_kernel<2>, g, t, 0, stream, A);
   hipLaunchKernelGGL(mcaq_mapper_bwd_kernel<1>, g, t, 0, stream, A);
-  hipLaunchKernelGGL(mcaq_tr_reduce_kernel, dim3((MG_SIZE + 255) / 256), dim3(256), 0, stream, (const float*)gpart,
-                     A.nwg, (int)MG_SIZE, (int)MG_SIZE, gparams, accumulate ? 1 : 0);
+  if (gparams)   // NULL: the caller reduces gpart (mcaq_mapper_train_grad_reduce)
+    hipLaunchKernelGGL(mcaq_tr_reduce_kernel, dim3((MG_SIZE + 255) / 256), dim3(256), 0, stream, (const float*)gpart,
+                       A.nwg, (int)MG_SIZE, (int)MG_SIZE, gparams, accumulate ? 1 : 0);
+  return (int)hipGetLastError();
+}
+
+int mcaq_mapper_running_update(const mcaq_mapper_params* P, const float* const* works, const int* ns, int count,
+                               float momentum, hipStream_t stream) {
+  using namespace mcaq;
+  if (!P || !works || !ns || count < 1 || count > MAPPER_RU_MAX) return (int)hipErrorInvalidValue;
+  MapperRunningArgs A{};
+  A.P = *P; A.count = count; A.momentum = momentum;
+  for (int k = 0; k < count; ++k) {
+    if (!works[k] || ns[k] < 1) return (int)hipErrorInvalidValue;
+    A.rstat[k] = mapper_work(const_cast<float*>(works[k]), ns[k]).rstat;
+  }
+  hipLaunchKernelGGL(mcaq_mapper_running_kernel, dim3(1), dim3(64), 0, stream, A);
   return (int)hipGetLastError();
 }
 
@@ -1256,7 +1313,7 @@ int mcaq_head_train_backward(const mcaq_cmlp_params* P, const float* phi, const 
                              int ht, int wt, float* gcraw, float* gparams, float* gpart, int accumulate,
                              hipStream_t stream) {
   using namespace mcaq;
-  if (!P || !phi || !craw || !gC || !gcraw || !gparams || !gpart || B < 1 || ht < 1 || wt < 1)
+  if (!P || !phi || !craw || !gC || !gcraw || !gpart || B < 1 || ht < 1 || wt < 1)
     return (int)hipErrorInvalidValue;
   HeadTrainArgs A{};
   A.P = *P; A.phi = phi; A.craw = craw; A.gC = gC; A.gcraw = gcraw; A.gpart = gpart;
@@ -1276,8 +1333,18 @@ int mcaq_head_train_backward(const mcaq_cmlp_params* P, const float* phi, const 
   }
   hipLaunchKernelGGL(mcaq_bilateral_bwd_kernel, dim3(B), dim3(256), lb, stream, A);
   hipLaunchKernelGGL(mcaq_cmlp_bwd_kernel, dim3(A.nwg), dim3(64 * CB_NW), lc, stream, A);
-  hipLaunchKernelGGL(mcaq_tr_reduce_kernel, dim3((CG_SIZE + 255) / 256), dim3(256), 0, stream, (const float*)gpart,
-                     A.nwg, (int)CG_SIZE, (int)CG_SIZE, gparams, accumulate ? 1 : 0);
+  if (gparams)   // NULL: the caller reduces gpart (mcaq_head_train_grad_reduce)
+    hipLaunchKernelGGL(mcaq_tr_reduce_kernel, dim3((CG_SIZE + 255) / 256), dim3(256), 0, stream, (const float*)gpart,
+                       A.nwg, (int)CG_SIZE, (int)CG_SIZE, gparams, accumulate ? 1 : 0);
+  return (int)hipGetLastError();
+}
+
+int mcaq_head_train_grad_reduce(int n, const float* gpart, float* gparams, int accumulate, hipStream_t stream) {
+  using namespace mcaq;
+  if (!gpart || !gparams || n < 1) return (int)hipErrorInvalidValue;
+  const int nwg = (n + TR_TPB - 1) / TR_TPB;
+  hipLaunchKernelGGL(mcaq_tr_reduce_kernel, dim3((CG_SIZE + 255) / 256), dim3(256), 0, stream, gpart, nwg,
+                     (int)CG_SIZE, (int)CG_SIZE, gparams, accumulate ? 1 : 0);
   return (int)hipGetLastError();
 }
 

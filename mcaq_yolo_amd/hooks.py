@@ -26,6 +26,15 @@ from .engine import HookPlan, ScaleGeom
 
 DEFAULT_INDICES = (4, 6, 9)   # models/mcaq_yolo.py:361 fallback (C3/C4/C5 of YOLOv8)
 
+# Train mode (QAT) through forward_features: every hook scale's chain of small
+# latency-bound launches (pass 1, morph, mapper stages, soft mask, quantizer;
+# and, through autograd's stream semantics, their backwards) on its own HIP
+# stream, so the three chains overlap instead of running back to back.  The
+# state the scales share is ordered by core.concurrent_scales (values equal
+# the sequential step's; tests/test_concurrent_scales_gpu.py).  False: one
+# stream, scale after scale.
+CONCURRENT_TRAIN_SCALES = True
+
 
 class MCAQHooks(nn.Module):
     def __init__(self, grid_size=8, min_bits=2, max_bits=8, bit_mapping="mlp", normalize_complexity=False,
@@ -216,11 +225,55 @@ class MCAQHooks(nn.Module):
 
     def forward_features(self, feats, temperature=1.0, quantize=True):
         """Run the hook body directly on a list of (C3, C4, C5) feature maps
-        (one per backbone index); returns (quantized maps, aux)."""
+        (one per backbone index); returns (quantized maps, aux).  In train mode
+        on the GPU the scales run on concurrent streams (CONCURRENT_TRAIN_SCALES)."""
         aux = self.begin(temperature=temperature, quantize=quantize)
-        outs = []
-        for idx, f in zip(self.backbone_out_indices, feats):
-            y = self.run_scale(idx, f, self._mcaq_state)
-            outs.append(f if y is None else y)
+        if self._concurrent_ok(feats):
+            outs = self._forward_features_concurrent(feats)
+        else:
+            outs = []
+            for idx, f in zip(self.backbone_out_indices, feats):
+                y = self.run_scale(idx, f, self._mcaq_state)
+                outs.append(f if y is None else y)
         self.end()
         return outs, aux
+
+    def _concurrent_ok(self, feats):
+        if not (CONCURRENT_TRAIN_SCALES and self.training and core.FUSED_TRAIN and len(feats) > 1):
+            return False
+        if not all(torch.is_tensor(f) and f.is_cuda and f.dim() == 4 for f in feats):
+            return False
+        if len({f.device for f in feats}) != 1:
+            return False
+        # batch-sharded steps keep one stream: their collectives sit between
+        # the stage launches (dist.shard_hooks)
+        if self.process_group is not None or any(q.process_group is not None for q in self.quantizers.values()):
+            return False
+        if isinstance(self.bit_mapper, ComplexityToBitMappingNetwork) and \
+                core._mapper_group(self.bit_mapper.mapping_network) is not None:
+            return False
+        return True
+
+    def _scale_streams(self, device, n):
+        key = (torch.device(device), n)
+        cache = self.__dict__.setdefault("_streams", {})
+        if key not in cache:
+            cache[key] = [torch.cuda.Stream(device=device) for _ in range(n)]
+        return cache[key]
+
+    def _forward_features_concurrent(self, feats):
+        dev = feats[0].device
+        main = torch.cuda.current_stream(dev)
+        streams = self._scale_streams(dev, len(feats))
+        outs = []
+        with core.concurrent_scales(self.complexity_analyzer, main, streams) as scope:
+            for st in streams:
+                st.wait_stream(main)
+            for idx, f, st in zip(self.backbone_out_indices, feats, streams):
+                with torch.cuda.stream(st):
+                    y = self.run_scale(idx, f, self._mcaq_state)
+                outs.append(f if y is None else y)
+            for st in streams:
+                main.wait_stream(st)
+            scope.finish()
+        return outs
