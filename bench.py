@@ -277,7 +277,9 @@ def main_qat(args, world, rank, dev, pg):
             "config": {"workload": "%s QAT bs%d/GPU 640x640 MCAQ hooks C3/C4/C5 train step (grid %d, %s mapper, "
                                    "continuous bits, STE, stage-3 temperature 1); YOLOv8 network excluded"
                                    % (name, B, grid, mapper),
-                       "global_batch": world * B, "parallelism": "dp%d" % world, "hip_graph": use_graph},
+                       "global_batch": world * B, "parallelism": "dp%d" % world, "hip_graph": use_graph,
+                       "scales": "concurrent streams" if (_hooks_mod().CONCURRENT_TRAIN_SCALES and pg is None)
+                       else "one stream"},
             "roofline": {"bound": "hbm", "achieved": kern["qat_backward_kernel"]["GB/s"], "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": kern["qat_backward_kernel"]["frac"], "traffic": None,
                          "kernel": "mcaq_qat_kernel<bwd> (read g, x + write grad_x: 12 B per element, + 4 B per "
@@ -501,6 +503,16 @@ def cpu_baseline(cfg_id, budget_s=10.0):
             "sample": "%d batches x %d images x 3 hook scales (%s %s, grid %d, %s mapper) through the package's "
                       "pure-PyTorch path (mcaq_yolo_amd/fallback.py), fp32, %d threads, %.1f s"
                       % (n, B, name, "x".join(map(str, chans)), grid, mapper, torch.get_num_threads(), dt)}
+
+
+def _hooks_mod():
+    from mcaq_yolo_amd import hooks
+    return hooks
+
+
+def _engine_mod():
+    from mcaq_yolo_amd import engine
+    return engine
 
 
 class _RunMixin:
@@ -816,7 +828,17 @@ def main():
                          "buffer-reuse edges between graphs)")
     ap.add_argument("--m-plane", action="store_true",
                     help="pass B writes the m(p) plane and pass 2 reads it (instead of regenerating m per slice)")
+    ap.add_argument("--qat-scales", choices=("concurrent", "sequential"), default=None,
+                    help="--config 5: hook scales on concurrent streams or one after another (default: hooks')")
+    ap.add_argument("--pass-b", choices=("image", "batch"), default=None,
+                    help="morphology pass B: per-image workgroups or batch-wide tile kernels (default: engine's)")
     args = ap.parse_args()
+    if args.qat_scales is not None:
+        from mcaq_yolo_amd import hooks as _hooks
+        _hooks.CONCURRENT_TRAIN_SCALES = args.qat_scales == "concurrent"
+    if args.pass_b is not None:
+        from mcaq_yolo_amd import engine as _engine
+        _engine.TILES_BATCH = args.pass_b == "batch"
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -982,6 +1004,7 @@ def main():
                                    "quant/dequant; YOLOv8 network excluded (see e2e)" % (name, B, grid, mapper),
                        "global_batch": world * B, "grid_size": grid, "mapper": mapper,
                        "parallelism": "dp%d" % world,
+                       "pass_b": "batch-wide tile kernels" if _engine_mod().TILES_BATCH else "per-image workgroups",
                        "hip_graph": use_graph or getattr(runner, "use_graph", False),
                        "batches_in_flight": 4 if args.schedule == "staged" else depth,
                        "schedule": {"staged": "staged: pass 1 (i) | pass A (i-1) | pass B (i-2) | pass 2 (i-3) on 4 "

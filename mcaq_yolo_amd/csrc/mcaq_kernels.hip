@@ -420,6 +420,18 @@ __device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, fl
   }
 }
 
+// XCD-aware unit order: workgroups are placed on the 8 XCDs round-robin by
+// blockIdx, so consecutive units of one image land on different XCDs, and a
+// 128-byte line that two of them share (a channel row not 128-byte aligned,
+// as C5's 1,600-byte rows on every other channel) is fetched once per XCD.
+// Permuted so that every unit of image b runs on XCD b % 8, the shared line
+// is fetched once and the neighbour reads it from that XCD's L2 (needs the
+// scale's block range to start at a multiple of 8 and B % 8 == 0; else the
+// plain order).  0: plain order (A/B).
+#ifndef MCAQ_STATS_XCD
+#define MCAQ_STATS_XCD 1
+#endif
+
 template <bool kVec>   // kVec: 8/16-byte row accesses for ppl 2/4 (host checks alignment)
 __global__ __launch_bounds__(256, MCAQ_STATS_MINW) void mcaq_stats_kernel(StatsArgs a) {
   __shared__ float lds[ST_LDS];
@@ -427,9 +439,20 @@ __global__ __launch_bounds__(256, MCAQ_STATS_MINW) void mcaq_stats_kernel(StatsA
   const int unit = a.units_total - 1 - (int)blockIdx.x;
   int si = 0;
   while (si + 1 < a.nscales && unit >= a.s[si + 1].unit_begin) ++si;
-  const int lu = unit - a.s[si].unit_begin;
+  int lu = unit - a.s[si].unit_begin;
   const mcaq_stats_scale S = si == 0 ? a.s[0] : si == 1 ? a.s[1] : a.s[2];   // by value: no indexed kernarg copy
   const int ppl = si == 0 ? a.ppl[0] : si == 1 ? a.ppl[1] : a.ppl[2];
+#if MCAQ_STATS_XCD
+  {
+    const int n = (si + 1 < a.nscales ? a.s[si + 1].unit_begin : a.units_total) - a.s[si].unit_begin;
+    const int x0 = a.units_total - a.s[si].unit_begin - n;     // first blockIdx of this scale
+    const int upi = (S.H * S.W + 64 * ppl - 1) / (64 * ppl);   // units per image
+    if ((x0 & 7) == 0 && (S.B & 7) == 0) {
+      const int j = (int)blockIdx.x - x0, slot = j >> 3, q = slot / upi;
+      lu = ((j & 7) + 8 * q) * upi + (slot - q * upi);
+    }
+  }
+#endif
   if constexpr (MCAQ_STATS_MAXPPL >= 4) {
     if (ppl == 4) { stats_unit<4, kVec>(S, lu, lds); return; }
   }

@@ -54,8 +54,11 @@ def _stream_handle(stream):
 BAND_PASS = False
 
 # Pass B of the morphology as batch-wide tile kernels (csrc/mcaq_tiles_batch.h)
-# wherever the flags allow it; False: the per-image pass B (A/B, cross-check)
-TILES_BATCH = True
+# wherever the flags allow it.  Bit-identical to the per-image pass B but
+# measured slower in the pipelined step (r04, bench --pass-b, 3 interleaved
+# rounds: 502-507 k vs 518-530 k img/s at config 2, profiles/r04_passb/):
+# off by default; True for A/B and the cross-check tests.
+TILES_BATCH = False
 
 
 class ScaleGeom:

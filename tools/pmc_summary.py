@@ -22,7 +22,8 @@ def load(root, counter):
 
 
 def short(name):
-    for k in ("mcaq_stats_kernel", "mcaq_morph_kernel", "mcaq_tiles_kernel", "mcaq_quant_kernel", "mcaq_finalize"):
+    for k in ("mcaq_stats_kernel", "mcaq_morph_kernel", "mcaq_tiles_kernel", "mcaq_quant_tile_kernel",
+              "mcaq_quant_kernel", "mcaq_finalize", "mcaq_tb_head_kernel", "mcaq_tb_map_kernel", "mcaq_tb_mask_kernel"):
         if k in name:
             return k
     return name[:40]
@@ -37,6 +38,8 @@ def main():
         k = short(name)
         f = 2 * 1024 * sum(fetch.get(name, [0])) / max(len(fetch.get(name, [])), 1)
         w = 1024 * sum(write.get(name, [0])) / max(len(write.get(name, [])), 1)
+        if k in out["kernels"]:          # several template instances of one kernel
+            k = name[:60]
         out["kernels"][k] = {"read": round(f), "write": round(w), "total": round(f + w),
                              "launches": max(len(fetch.get(name, [])), len(write.get(name, [])))}
         if k.startswith("mcaq_"):
