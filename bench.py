@@ -245,9 +245,18 @@ def main_qat(args, world, rank, dev, pg):
     t0 = time.perf_counter()
     for _ in range(args.steps):
         run()
+    t_enq = time.perf_counter() - t0
     torch.cuda.synchronize()
     step_s = (time.perf_counter() - t0) / args.steps
     core._MapperTrainFn.apply = orig_apply
+    # one step alone (device idle before it): its latency, and how long the
+    # host takes to issue it
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    run()
+    t_one_enq = time.perf_counter() - t1
+    torch.cuda.synchronize()
+    t_one = time.perf_counter() - t1
     fused_per_step = fused["calls"] / max(1, args.steps + max(args.warmup, 3)) if not use_graph else None
     if pg is not None:
         import torch.distributed as dist
@@ -279,7 +288,10 @@ def main_qat(args, world, rank, dev, pg):
                                    % (name, B, grid, mapper),
                        "global_batch": world * B, "parallelism": "dp%d" % world, "hip_graph": use_graph,
                        "scales": "concurrent streams" if (_hooks_mod().CONCURRENT_TRAIN_SCALES and pg is None)
-                       else "one stream"},
+                       else "one stream",
+                       "host_enqueue_us_per_step": round(t_enq / args.steps * 1e6, 1),
+                       "single_step_latency_us": round(t_one * 1e6, 1),
+                       "single_step_enqueue_us": round(t_one_enq * 1e6, 1)},
             "roofline": {"bound": "hbm", "achieved": kern["qat_backward_kernel"]["GB/s"], "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": kern["qat_backward_kernel"]["frac"], "traffic": None,
                          "kernel": "mcaq_qat_kernel<bwd> (read g, x + write grad_x: 12 B per element, + 4 B per "
