@@ -287,8 +287,7 @@ def main_qat(args, world, rank, dev, pg):
                                    "continuous bits, STE, stage-3 temperature 1); YOLOv8 network excluded"
                                    % (name, B, grid, mapper),
                        "global_batch": world * B, "parallelism": "dp%d" % world, "hip_graph": use_graph,
-                       "scales": "concurrent streams" if (_hooks_mod().CONCURRENT_TRAIN_SCALES and pg is None)
-                       else "one stream",
+                       "scales": _qat_scales_mode(pg),
                        "host_enqueue_us_per_step": round(t_enq / args.steps * 1e6, 1),
                        "single_step_latency_us": round(t_one * 1e6, 1),
                        "single_step_enqueue_us": round(t_one_enq * 1e6, 1)},
@@ -515,6 +514,15 @@ def cpu_baseline(cfg_id, budget_s=10.0):
             "sample": "%d batches x %d images x 3 hook scales (%s %s, grid %d, %s mapper) through the package's "
                       "pure-PyTorch path (mcaq_yolo_amd/fallback.py), fp32, %d threads, %.1f s"
                       % (n, B, name, "x".join(map(str, chans)), grid, mapper, torch.get_num_threads(), dt)}
+
+
+def _qat_scales_mode(pg):
+    hk = _hooks_mod()
+    if pg is None and hk.MULTI_SCALE_TRAIN:
+        return "multi-segment launches (one per stage for all scales, one stream)"
+    if pg is None and hk.CONCURRENT_TRAIN_SCALES:
+        return "per-scale modules on concurrent streams"
+    return "per-scale modules, one stream"
 
 
 def _hooks_mod():
@@ -840,13 +848,15 @@ def main():
                          "buffer-reuse edges between graphs)")
     ap.add_argument("--m-plane", action="store_true",
                     help="pass B writes the m(p) plane and pass 2 reads it (instead of regenerating m per slice)")
-    ap.add_argument("--qat-scales", choices=("concurrent", "sequential"), default=None,
-                    help="--config 5: hook scales on concurrent streams or one after another (default: hooks')")
+    ap.add_argument("--qat-scales", choices=("multi", "concurrent", "sequential"), default=None,
+                    help="--config 5: every stage once for all hook scales (multi-segment launches), the per-scale "
+                         "modules on concurrent streams, or one after another (default: hooks')")
     ap.add_argument("--pass-b", choices=("image", "batch"), default=None,
                     help="morphology pass B: per-image workgroups or batch-wide tile kernels (default: engine's)")
     args = ap.parse_args()
     if args.qat_scales is not None:
         from mcaq_yolo_amd import hooks as _hooks
+        _hooks.MULTI_SCALE_TRAIN = args.qat_scales == "multi"
         _hooks.CONCURRENT_TRAIN_SCALES = args.qat_scales == "concurrent"
     if args.pass_b is not None:
         from mcaq_yolo_amd import engine as _engine

@@ -41,7 +41,7 @@ typedef void* hipEvent_t;
 extern "C" {
 #endif
 
-#define MCAQ_ABI_VERSION 13
+#define MCAQ_ABI_VERSION 14
 /* largest dynamic LDS request of the morph kernel (gfx950: 160 KiB per CU) */
 #define MCAQ_MORPH_LDS_LIMIT 163840
 
@@ -375,6 +375,57 @@ size_t mcaq_smask_gpart_floats(int B);
 int mcaq_smask_train_backward(const mcaq_smask_params* P, const float* bits, const float* absmean, const float* gm,
                               int B, int H, int W, int ht, int wt, float* gbits, int accumulate, float* gparams,
                               float* gpart, hipStream_t stream);
+/* ---- multi-segment train launches: the hook scales of one QAT step (each
+ * scale its own tensors, the same module parameters) in ONE launch per stage
+ * instead of one per scale and stage - the values of the per-scale launches.
+ * At most MCAQ_TRAIN_MAXSEG segments.  Parameter gradients stay per-segment
+ * partials (gpart, as the single-scale launchers' sizes) for
+ * mcaq_train_reduce_multi. */
+#define MCAQ_TRAIN_MAXSEG 3
+typedef struct {
+  const float* c;        /* (n) complexity */
+  float* bits;           /* (n) forward output */
+  float* work;           /* mcaq_mapper_work_floats(n) */
+  const float* gbits;    /* (n) backward: upstream gradient */
+  float* gc;             /* (n) backward: gradient of c */
+  float* gpart;          /* backward: mcaq_mapper_gpart_floats(n) */
+  int n;
+} mcaq_mapper_seg;
+/* 4 launches; update_stats 0 or 2 (deferred, then mcaq_mapper_running_update
+ * in segment order) when nseg > 1 */
+int mcaq_mapper_train_forward_multi(const mcaq_mapper_params* P, const mcaq_mapper_seg* segs, int nseg,
+                                    float min_bits, float max_bits, float temperature, float momentum,
+                                    int round_bits, int update_stats, hipStream_t stream);
+/* 4 launches (no parameter reduction) */
+int mcaq_mapper_train_backward_multi(const mcaq_mapper_params* P, const mcaq_mapper_seg* segs, int nseg,
+                                     float min_bits, float max_bits, float temperature, hipStream_t stream);
+typedef struct {
+  const float* phi; const float* craw; const float* gC;
+  float* gcraw;          /* (B*ht*wt) work */
+  float* gpart;          /* mcaq_head_gpart_floats(B*ht*wt) */
+  int B, ht, wt;
+} mcaq_head_seg;
+/* 2 launches (bilateral adjoint, complexity MLP backward; no reduction) */
+int mcaq_head_train_backward_multi(const mcaq_cmlp_params* P, const mcaq_head_seg* segs, int nseg, hipStream_t stream);
+typedef struct {
+  mcaq_smask_params P;   /* each segment its own soft-mask net (one per quantizer) */
+  const float* bits; const float* absmean; const float* gm;
+  float* gbits;          /* (B, ht, wt), added to when accumulate */
+  float* gpart;          /* mcaq_smask_gpart_floats(B) */
+  int B, H, W, ht, wt, accumulate;
+} mcaq_smask_seg;
+/* 1 launch (no reduction) */
+int mcaq_smask_train_backward_multi(const mcaq_smask_seg* segs, int nseg, hipStream_t stream);
+typedef struct {
+  const float* part;     /* [nparts][stride] partial sums */
+  float* out;            /* count floats (chain: segment 0's only) */
+  int nparts, stride, count, accumulate;
+} mcaq_reduce_seg;
+/* chain 0: out_k (+)= sum of segment k's partials; chain 1: segment 0's out
+ * = s_0 (+ out if accumulate) + s_1 + s_2 in segment order (the values of
+ * one reduction per segment, the later ones accumulating).  1 launch. */
+int mcaq_train_reduce_multi(const mcaq_reduce_seg* segs, int nseg, int chain, hipStream_t stream);
+
 /* gparams of the mapper / head backward: accumulate != 0 adds to gparams
  * (the parameters' persistent gradient storage), 0 overwrites it; NULL
  * (without grid_sync): no reduction launch - the partials stay in gpart for

@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libmcaq_hip.so")
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -72,6 +72,30 @@ class SmaskParams(ctypes.Structure):
     _fields_ = [(n, P) for n in ("w1", "b1", "w2", "b2")]
 
 
+MCAQ_TRAIN_MAXSEG = 3
+
+
+class MapperSeg(ctypes.Structure):
+    """mcaq_mapper_seg."""
+    _fields_ = [("c", P), ("bits", P), ("work", P), ("gbits", P), ("gc", P), ("gpart", P), ("n", I)]
+
+
+class HeadSeg(ctypes.Structure):
+    """mcaq_head_seg."""
+    _fields_ = [("phi", P), ("craw", P), ("gC", P), ("gcraw", P), ("gpart", P), ("B", I), ("ht", I), ("wt", I)]
+
+
+class SmaskSeg(ctypes.Structure):
+    """mcaq_smask_seg."""
+    _fields_ = [("P", SmaskParams), ("bits", P), ("absmean", P), ("gm", P), ("gbits", P), ("gpart", P),
+                ("B", I), ("H", I), ("W", I), ("ht", I), ("wt", I), ("accumulate", I)]
+
+
+class ReduceSeg(ctypes.Structure):
+    """mcaq_reduce_seg."""
+    _fields_ = [("part", P), ("out", P), ("nparts", I), ("stride", I), ("count", I), ("accumulate", I)]
+
+
 # morph stage flags (mcaq_morph.h)
 F_PHI, F_CMLP, F_MAPPER, F_SOFTMASK = 1, 2, 4, 8
 F_CONT, F_HAS_T, F_NORM_C, F_MAP_LINEAR = 16, 32, 64, 128
@@ -90,7 +114,9 @@ EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats",
            "mcaq_mapper_train_backward", "mcaq_head_gpart_floats", "mcaq_head_train_backward",
            "mcaq_smask_gpart_floats", "mcaq_smask_train_backward", "mcaq_ema_stats_ex", "mcaq_pack",
            "mcaq_mapper_train_forward_stage", "mcaq_mapper_train_backward_stage", "mcaq_mapper_train_reduce",
-           "mcaq_mapper_train_grad_reduce", "mcaq_mapper_running_update", "mcaq_head_train_grad_reduce")
+           "mcaq_mapper_train_grad_reduce", "mcaq_mapper_running_update", "mcaq_head_train_grad_reduce",
+           "mcaq_mapper_train_forward_multi", "mcaq_mapper_train_backward_multi", "mcaq_head_train_backward_multi",
+           "mcaq_smask_train_backward_multi", "mcaq_train_reduce_multi")
 
 _LIB = None
 
@@ -177,6 +203,18 @@ def _declare(lib):
                                                Fl, P]
     lib.mcaq_head_train_grad_reduce.restype = I
     lib.mcaq_head_train_grad_reduce.argtypes = [I, P, P, I, P]
+    lib.mcaq_mapper_train_forward_multi.restype = I
+    lib.mcaq_mapper_train_forward_multi.argtypes = [ctypes.POINTER(MapperParams), ctypes.POINTER(MapperSeg), I, Fl, Fl,
+                                                    Fl, Fl, I, I, P]
+    lib.mcaq_mapper_train_backward_multi.restype = I
+    lib.mcaq_mapper_train_backward_multi.argtypes = [ctypes.POINTER(MapperParams), ctypes.POINTER(MapperSeg), I, Fl,
+                                                     Fl, Fl, P]
+    lib.mcaq_head_train_backward_multi.restype = I
+    lib.mcaq_head_train_backward_multi.argtypes = [ctypes.POINTER(CmlpParams), ctypes.POINTER(HeadSeg), I, P]
+    lib.mcaq_smask_train_backward_multi.restype = I
+    lib.mcaq_smask_train_backward_multi.argtypes = [ctypes.POINTER(SmaskSeg), I, P]
+    lib.mcaq_train_reduce_multi.restype = I
+    lib.mcaq_train_reduce_multi.argtypes = [ctypes.POINTER(ReduceSeg), I, I, P]
     lib.mcaq_head_train_backward.restype = I
     lib.mcaq_head_train_backward.argtypes = [ctypes.POINTER(CmlpParams), P, P, P, I, I, I, P, P, P, I, P]
     lib.mcaq_ema_stats_ex.restype = I

@@ -284,14 +284,15 @@ def _pass1_lookup(x):
     return e if (_PASS1["armed"] and e is not None and e["key"] == _pass1_key(x)) else None
 
 
-def _channel_minmax(x, absmean=None):
+def _channel_minmax(x, absmean=None, partials=None):
     """Per-channel min/max over (batch, H, W) (quantization.py:650-654) by pass 1
     + the finalize reduction; optionally the |x| channel mean in the same read
-    (or both from the analyzer's pass 1 over the same tensor, _pass1_lookup)."""
+    (or both from the analyzer's pass 1 over the same tensor, _pass1_lookup,
+    or `partials` = that pass's (pmin, pmax))."""
     B, C, H, W = x.shape
     L = abi.lib()
     units = L.mcaq_stats_units(B, C, H, W)
-    hit = _pass1_lookup(x)
+    hit = _pass1_lookup(x) if partials is None else {"pmin": partials[0], "pmax": partials[1], "absmean": absmean}
     if hit is not None and (absmean is None or absmean is hit["absmean"]):
         pmin, pmax = hit["pmin"], hit["pmax"]
     else:
@@ -1424,7 +1425,8 @@ class SpatialAdaptiveQuantization(nn.Module):
         self.num_batches_tracked += 1
 
     @torch.no_grad()
-    def update_running_stats(self, x: torch.Tensor, absmean: Optional[torch.Tensor] = None, want_copies=False):
+    def update_running_stats(self, x: torch.Tensor, absmean: Optional[torch.Tensor] = None, want_copies=False,
+                             partials=None):
         """quantization.py:319-353: EMA(momentum) of the batch min/max (pass 1 +
         finalize + mcaq_ema_stats; absmean, if given, is filled by the same read).
         want_copies (per-channel, GPU): also return copies (xmin, xmax) of the
@@ -1436,7 +1438,7 @@ class SpatialAdaptiveQuantization(nn.Module):
             return self._update_running_stats_torch(x)
         _need_cuda(x, "x")
         xf = _f32c(x)
-        xmin, xmax = _channel_minmax(xf, absmean)
+        xmin, xmax = _channel_minmax(xf, absmean, partials)
         if self.process_group is not None:
             # data-parallel QAT: the EMA sees the global batch's min/max (one
             # all-reduce, MAX over [-min, max]), as a single process would

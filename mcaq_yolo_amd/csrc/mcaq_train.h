@@ -113,6 +113,7 @@ struct MapperTrainArgs {
   const float* gbsum;
   const float* gstat1;
   int gworld;
+  int wg0;              // first workgroup of this segment in a multi-segment launch (else 0)
 };
 constexpr int RANK_ENT = 129;   // (mean[64], M2[64], n) of one rank
 
@@ -257,7 +258,7 @@ __device__ void map_stats(const MapperTrainArgs& A, const MapperWork& W, float* 
     const float mean = m, var = n > 0.0f ? M2 / n : 0.0f;
     const float rstd = 1.0f / sqrtf(var + 1e-5f);
     s_mean[tid] = mean; s_rstd[tid] = rstd;
-    if (blockIdx.x == 0) {
+    if ((int)blockIdx.x == A.wg0) {
       W.stat[(L - 1) * 128 + tid] = mean;
       W.stat[(L - 1) * 128 + 64 + tid] = rstd;
       if (A.update_stats) {
@@ -294,10 +295,11 @@ __device__ __forceinline__ void mapper_fwd_stage(const MapperTrainArgs& A, MapFw
   const MapperWork W = mapper_work(A.work, A.n);
   const mcaq_mapper_params& P = A.P;
   const int tid = threadIdx.x, lane = tid & 63, q = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int t = blockIdx.x * TR_TPB + lane;
+  const int wgi = (int)blockIdx.x - A.wg0;   // workgroup within this segment
+  const int t = wgi * TR_TPB + lane;
   const bool valid = t < A.n;
   const int tc = valid ? t : A.n - 1;
-  const float nvalid = (float)imin_(TR_TPB, A.n - (int)blockIdx.x * TR_TPB);
+  const float nvalid = (float)imin_(TR_TPB, A.n - wgi * TR_TPB);
   if constexpr (S >= 2) map_stats<S - 1>(A, W, s_mean, s_rstd, s_tmp);
   // ---- layer inputs of this workgroup's tiles -> s_in
   if constexpr (S == 1) {
@@ -340,8 +342,8 @@ __device__ __forceinline__ void mapper_fwd_stage(const MapperTrainArgs& A, MapFw
       o[f] = acc;
       if (valid) aout[(size_t)t * N + j] = acc;
     }
-    wg_moments<NQ>(o, valid, nvalid, q * NQ, W.fpart(S) + (size_t)blockIdx.x * 128, N);
-    if (tid == 0) W.cnt[blockIdx.x] = nvalid;
+    wg_moments<NQ>(o, valid, nvalid, q * NQ, W.fpart(S) + (size_t)wgi * 128, N);
+    if (tid == 0) W.cnt[wgi] = nvalid;
   } else {
     // last layer + sigmoid + bit range, temperature, clamp (+ round)
     if (q == 0 && valid) {
@@ -436,11 +438,12 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
   const MapperWork W = mapper_work(A.work, A.n);
   const mcaq_mapper_params& P = A.P;
   const int tid = threadIdx.x, lane = tid & 63, q = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int t = blockIdx.x * TR_TPB + lane;
+  const int wgi = (int)blockIdx.x - A.wg0;   // workgroup within this segment
+  const int t = wgi * TR_TPB + lane;
   const bool valid = t < A.n;
   const int tc = valid ? t : A.n - 1;
-  float* gp = A.gpart + (size_t)blockIdx.x * MG_SIZE;
-  float* bp = W.bpart_of(S) + (size_t)blockIdx.x * 128;   // BN(S-1) partials written here
+  float* gp = A.gpart + (size_t)wgi * MG_SIZE;
+  float* bp = W.bpart_of(S) + (size_t)wgi * 128;   // BN(S-1) partials written here
   // ---- 1. gradient of a(S) for this workgroup's tiles -> s_g
   if constexpr (S == 4) {
     if (q == 0) {
@@ -479,8 +482,8 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
       // gamma / beta gradients are the BN sums themselves: workgroup 0's
       // partial slot holds them, the others zero
       const int og = S == 1 ? MG_G1 : (S == 2 ? MG_G2 : MG_G3), ob = S == 1 ? MG_BE1 : (S == 2 ? MG_BE2 : MG_BE3);
-      gp[og + tid] = blockIdx.x == 0 ? s2 : 0.0f;
-      gp[ob + tid] = blockIdx.x == 0 ? s1 : 0.0f;
+      gp[og + tid] = wgi == 0 ? s2 : 0.0f;
+      gp[ob + tid] = wgi == 0 ? s1 : 0.0f;
     }
     __syncthreads();
     float ntot = (float)A.n;
@@ -677,6 +680,7 @@ struct HeadTrainArgs {
   float* gcraw;         // (n) work: gradient of craw
   float* gpart;         // [nwg][CG_SIZE]
   int B, ht, wt, n, nwg;
+  int wg0;              // first workgroup of this segment in a multi-segment launch (else 0)
 };
 
 // bilateral (morphology.py:309-354, sigma_s 2, sigma_r 0.1, 5x5, replicate):
@@ -694,9 +698,9 @@ __device__ __forceinline__ void tap_range(int u, int o, int n, int& lo, int& hi)
   hi = imin_(hi, n - 1);
 }
 
-__global__ __launch_bounds__(256) void mcaq_bilateral_bwd_kernel(HeadTrainArgs A) {
+__device__ __forceinline__ void mcaq_bilateral_bwd_body(const HeadTrainArgs& A) {
   extern __shared__ float smem_tr[];
-  const int b = blockIdx.x, ht = A.ht, wt = A.wt, NT = ht * wt;
+  const int b = (int)blockIdx.x - A.wg0, ht = A.ht, wt = A.wt, NT = ht * wt;
   const int tid = threadIdx.x;
   float* cr = smem_tr;            // craw of the image
   float* gd = cr + NT;            // per tile: g_C / D  (0 outside the clamp)
@@ -755,6 +759,7 @@ __global__ __launch_bounds__(256) void mcaq_bilateral_bwd_kernel(HeadTrainArgs A
     A.gcraw[(size_t)b * NT + u] = s;
   }
 }
+__global__ __launch_bounds__(256) void mcaq_bilateral_bwd_kernel(HeadTrainArgs A) { mcaq_bilateral_bwd_body(A); }
 
 // complexity MLP backward (Linear(8,64)-LN-ReLU-Linear(64,32)-LN-ReLU-
 // Linear(32,1)-sigmoid, recomputed): 64 tiles per workgroup, one per lane;
@@ -766,14 +771,15 @@ constexpr int CB_ST = 8 + 64 * 4 + 32 * 4 + 1 + 4;   // per-tile LDS vector (flo
 enum : int { CB_PHI = 0, CB_R1 = 8, CB_GA1 = 72, CB_GY1 = 136, CB_GYX1 = 200, CB_R2 = 264, CB_GA2 = 296,
              CB_GY2 = 328, CB_GYX2 = 360, CB_GA3 = 392 };
 
-__global__ __launch_bounds__(64 * CB_NW) void mcaq_cmlp_bwd_kernel(HeadTrainArgs A) {
+__device__ __forceinline__ void mcaq_cmlp_bwd_body(const HeadTrainArgs& A) {
   constexpr int NW = CB_NW, F1 = 64 / NW, F2 = 32 / NW, NTH = 64 * NW;
   extern __shared__ float smem_tr[];
   float* sv = smem_tr;                       // [TR_TPB][CB_ST]
   float* red = sv + TR_TPB * CB_ST;          // [NW][TR_TPB] cross-wave partial sums
   const mcaq_cmlp_params& P = A.P;
   const int tid = threadIdx.x, lane = tid & 63, q = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int t = blockIdx.x * TR_TPB + lane;
+  const int wgi = (int)blockIdx.x - A.wg0;   // workgroup within this segment
+  const int t = wgi * TR_TPB + lane;
   const bool valid = t < A.n;
   const int tc = valid ? t : A.n - 1;
   float* v = sv + lane * CB_ST;
@@ -887,7 +893,7 @@ __global__ __launch_bounds__(64 * CB_NW) void mcaq_cmlp_bwd_kernel(HeadTrainArgs
   __syncthreads();
   // ---- weight partials over the workgroup's tiles (invalid lanes carry zero
   // gradients).  W2 (32 x 64): thread = one row x 4 columns.
-  float* gp = A.gpart + (size_t)blockIdx.x * CG_SIZE;
+  float* gp = A.gpart + (size_t)wgi * CG_SIZE;
   auto tvec = [&](int u) { return sv + u * CB_ST; };
   {
     const int j0 = tid >> 4, k0 = (tid & 15) * 4;
@@ -928,6 +934,7 @@ __global__ __launch_bounds__(64 * CB_NW) void mcaq_cmlp_bwd_kernel(HeadTrainArgs
     gp[e] = a;
   }
 }
+__global__ __launch_bounds__(64 * CB_NW) void mcaq_cmlp_bwd_kernel(HeadTrainArgs A) { mcaq_cmlp_bwd_body(A); }
 
 // ============================================================================
 // soft mask backward (one workgroup per image)
@@ -943,13 +950,14 @@ struct MaskTrainArgs {
   float* gbits;          // (B, ht, wt) gradient of the bit map (accumulated if accumulate)
   float* gpart;          // [B][SG_SIZE]
   int B, H, W, ht, wt, accumulate;
+  int wg0;               // first workgroup of this segment in a multi-segment launch (else 0)
 };
 
 constexpr int SM_TH = 1024;   // threads per soft-mask backward workgroup (one image)
 
-__global__ __launch_bounds__(SM_TH) void mcaq_smask_bwd_kernel(MaskTrainArgs A) {
+__device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
   extern __shared__ float smem_tr[];
-  const int b = blockIdx.x, H = A.H, W = A.W, ht = A.ht, wt = A.wt, NT = ht * wt;
+  const int b = (int)blockIdx.x - A.wg0, H = A.H, W = A.W, ht = A.ht, wt = A.wt, NT = ht * wt;
   const int tid = threadIdx.x;
   float* f0 = smem_tr;               // bits feature, clamp((b - 2) / 6, 0, 1)
   float* f1 = f0 + NT;               // activation feature
@@ -1141,6 +1149,7 @@ __global__ __launch_bounds__(SM_TH) void mcaq_smask_bwd_kernel(MaskTrainArgs A) 
     gp[e] = s;
   }
 }
+__global__ __launch_bounds__(SM_TH) void mcaq_smask_bwd_kernel(MaskTrainArgs A) { mcaq_smask_bwd_body(A); }
 
 // ---- device packing of parameter blobs --------------------------------------
 // out[seg.dst + i] for every segment: mode 0 copies n floats from src; mode 1
@@ -1180,6 +1189,73 @@ __global__ __launch_bounds__(256) void mcaq_pack_kernel(PackArgs a, float* __res
 // ============================================================================
 // C ABI
 // ============================================================================
+// ============================================================================
+// multi-segment launches: the hook scales of one train step (each its own
+// tensors, the same parameters) in ONE launch per stage.  A segment is the
+// single-scale launch's argument block with wg0 = its first workgroup; every
+// workgroup runs the single-scale body of its segment, so the values are those
+// of the per-scale launches.  Single-stream HIP graphs of the QAT step then
+// carry a third of the kernel nodes (graph replay issues a multi-stream graph
+// node by node: tools/probe/graph_replay_probe.py).
+// ============================================================================
+constexpr int TR_MAXSEG = 3;
+template <typename T> struct TrMulti { T s[TR_MAXSEG]; int nseg; };
+template <typename T>
+__device__ __forceinline__ const T& tr_seg(const TrMulti<T>& M) {
+  const int x = (int)blockIdx.x;
+  return (M.nseg > 2 && x >= M.s[2].wg0) ? M.s[2] : ((M.nseg > 1 && x >= M.s[1].wg0) ? M.s[1] : M.s[0]);
+}
+
+template <int S>
+__global__ __launch_bounds__(MTH) void mcaq_mapper_fwd_multi_kernel(TrMulti<MapperTrainArgs> M) {
+  __shared__ MapFwdLds L;
+  mapper_fwd_stage<S>(tr_seg(M), L);
+}
+template <int S>
+__global__ __launch_bounds__(MTH) void mcaq_mapper_bwd_multi_kernel(TrMulti<MapperTrainArgs> M) {
+  __shared__ MapBwdLds L;
+  mapper_bwd_stage<S>(tr_seg(M), L);
+}
+__global__ __launch_bounds__(256) void mcaq_bilateral_bwd_multi_kernel(TrMulti<HeadTrainArgs> M) {
+  mcaq_bilateral_bwd_body(tr_seg(M));
+}
+__global__ __launch_bounds__(64 * CB_NW) void mcaq_cmlp_bwd_multi_kernel(TrMulti<HeadTrainArgs> M) {
+  mcaq_cmlp_bwd_body(tr_seg(M));
+}
+__global__ __launch_bounds__(SM_TH) void mcaq_smask_bwd_multi_kernel(TrMulti<MaskTrainArgs> M) {
+  mcaq_smask_bwd_body(tr_seg(M));
+}
+
+// parameter-gradient reductions of several segments.  chain = 0: segment k
+// (blockIdx.y) reduces its partials into its own output, as
+// mcaq_tr_reduce_kernel; chain = 1: every segment into segment 0's output, in
+// segment order - v = s0 (+ out if accumulate), v += s1, v += s2 - the values
+// one reduction launch per segment leaves (the first with `accumulate`, the
+// others accumulating)
+struct TrReduceSeg { const float* part; float* out; int nwg, stride, count, accumulate; };
+__global__ __launch_bounds__(256) void mcaq_tr_reduce_multi_kernel(TrMulti<TrReduceSeg> M, int chain) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (chain) {
+    const TrReduceSeg& s0 = M.s[0];
+    if (e >= s0.count) return;
+    float v = 0.0f;
+    for (int k = 0; k < M.nseg; ++k) {
+      const TrReduceSeg& g = k == 0 ? M.s[0] : (k == 1 ? M.s[1] : M.s[2]);
+      float sum = 0.0f;
+      for (int w = 0; w < g.nwg; ++w) sum += g.part[(size_t)w * g.stride + e];
+      v = k == 0 ? (s0.accumulate ? s0.out[e] + sum : sum) : v + sum;
+    }
+    s0.out[e] = v;
+  } else {
+    const int k = blockIdx.y;
+    const TrReduceSeg& g = k == 0 ? M.s[0] : (k == 1 ? M.s[1] : M.s[2]);
+    if (k >= M.nseg || e >= g.count) return;
+    float sum = 0.0f;
+    for (int w = 0; w < g.nwg; ++w) sum += g.part[(size_t)w * g.stride + e];
+    g.out[e] = g.accumulate ? g.out[e] + sum : sum;
+  }
+}
+
 extern "C" {
 
 size_t mcaq_mapper_work_floats(int n) { return mcaq::mapper_work_floats(n); }
@@ -1336,6 +1412,145 @@ int mcaq_head_train_backward(const mcaq_cmlp_params* P, const float* phi, const 
   if (gparams)   // NULL: the caller reduces gpart (mcaq_head_train_grad_reduce)
     hipLaunchKernelGGL(mcaq_tr_reduce_kernel, dim3((CG_SIZE + 255) / 256), dim3(256), 0, stream, (const float*)gpart,
                        A.nwg, (int)CG_SIZE, (int)CG_SIZE, gparams, accumulate ? 1 : 0);
+  return (int)hipGetLastError();
+}
+
+int mcaq_mapper_train_forward_multi(const mcaq_mapper_params* P, const mcaq_mapper_seg* segs, int nseg,
+                                    float min_bits, float max_bits, float temperature, float momentum,
+                                    int round_bits, int update_stats, hipStream_t stream) {
+  using namespace mcaq;
+  // one launch per stage for every segment: several segments updating the
+  // shared running statistics in-kernel would race (update_stats 1)
+  if (!P || !segs || nseg < 1 || nseg > TR_MAXSEG || (nseg > 1 && update_stats == 1)) return (int)hipErrorInvalidValue;
+  TrMulti<MapperTrainArgs> M{};
+  int wg = 0;
+  for (int k = 0; k < nseg; ++k) {
+    const mcaq_mapper_seg& g = segs[k];
+    if (!g.c || !g.bits || !g.work || g.n < 1) return (int)hipErrorInvalidValue;
+    MapperTrainArgs& A = M.s[k];
+    A.P = *P; A.c = g.c; A.bits = g.bits; A.work = g.work; A.n = g.n; A.nwg = (g.n + TR_TPB - 1) / TR_TPB;
+    A.min_bits = min_bits; A.max_bits = max_bits; A.temperature = temperature; A.momentum = momentum;
+    A.round_bits = round_bits; A.update_stats = update_stats; A.wg0 = wg;
+    wg += A.nwg;
+  }
+  M.nseg = nseg;
+  const dim3 g(wg), t(MTH);
+  hipLaunchKernelGGL(mcaq_mapper_fwd_multi_kernel<1>, g, t, 0, stream, M);
+  hipLaunchKernelGGL(mcaq_mapper_fwd_multi_kernel<2>, g, t, 0, stream, M);
+  hipLaunchKernelGGL(mcaq_mapper_fwd_multi_kernel<3>, g, t, 0, stream, M);
+  hipLaunchKernelGGL(mcaq_mapper_fwd_multi_kernel<4>, g, t, 0, stream, M);
+  return (int)hipGetLastError();
+}
+
+int mcaq_mapper_train_backward_multi(const mcaq_mapper_params* P, const mcaq_mapper_seg* segs, int nseg,
+                                     float min_bits, float max_bits, float temperature, hipStream_t stream) {
+  using namespace mcaq;
+  if (!P || !segs || nseg < 1 || nseg > TR_MAXSEG) return (int)hipErrorInvalidValue;
+  TrMulti<MapperTrainArgs> M{};
+  int wg = 0;
+  for (int k = 0; k < nseg; ++k) {
+    const mcaq_mapper_seg& g = segs[k];
+    if (!g.c || !g.gbits || !g.gc || !g.gpart || !g.work || g.n < 1) return (int)hipErrorInvalidValue;
+    MapperTrainArgs& A = M.s[k];
+    A.P = *P; A.c = g.c; A.gbits = g.gbits; A.gc = g.gc; A.work = g.work; A.gpart = g.gpart; A.n = g.n;
+    A.nwg = (g.n + TR_TPB - 1) / TR_TPB;
+    A.min_bits = min_bits; A.max_bits = max_bits; A.temperature = temperature; A.wg0 = wg;
+    wg += A.nwg;
+  }
+  M.nseg = nseg;
+  const dim3 g(wg), t(MTH);
+  hipLaunchKernelGGL(mcaq_mapper_bwd_multi_kernel<4>, g, t, 0, stream, M);
+  hipLaunchKernelGGL(mcaq_mapper_bwd_multi_kernel<3>, g, t, 0, stream, M);
+  hipLaunchKernelGGL(mcaq_mapper_bwd_multi_kernel<2>, g, t, 0, stream, M);
+  hipLaunchKernelGGL(mcaq_mapper_bwd_multi_kernel<1>, g, t, 0, stream, M);
+  return (int)hipGetLastError();
+}
+
+int mcaq_head_train_backward_multi(const mcaq_cmlp_params* P, const mcaq_head_seg* segs, int nseg, hipStream_t stream) {
+  using namespace mcaq;
+  if (!P || !segs || nseg < 1 || nseg > TR_MAXSEG) return (int)hipErrorInvalidValue;
+  TrMulti<HeadTrainArgs> Mb{}, Mc{};
+  int wb = 0, wc = 0;
+  size_t lb = 0;
+  for (int k = 0; k < nseg; ++k) {
+    const mcaq_head_seg& g = segs[k];
+    if (!g.phi || !g.craw || !g.gC || !g.gcraw || !g.gpart || g.B < 1 || g.ht < 1 || g.wt < 1)
+      return (int)hipErrorInvalidValue;
+    HeadTrainArgs A{};
+    A.P = *P; A.phi = g.phi; A.craw = g.craw; A.gC = g.gC; A.gcraw = g.gcraw; A.gpart = g.gpart;
+    A.B = g.B; A.ht = g.ht; A.wt = g.wt; A.n = g.B * g.ht * g.wt; A.nwg = (A.n + TR_TPB - 1) / TR_TPB;
+    const size_t l = (size_t)53 * g.ht * g.wt * sizeof(float);
+    if (l > 160 * 1024 - 1024) return (int)hipErrorInvalidValue;
+    lb = l > lb ? l : lb;
+    Mb.s[k] = A; Mb.s[k].wg0 = wb; wb += A.B;      // bilateral: one workgroup per image
+    Mc.s[k] = A; Mc.s[k].wg0 = wc; wc += A.nwg;    // MLP: 64 tiles per workgroup
+  }
+  Mb.nseg = Mc.nseg = nseg;
+  const size_t lc = (size_t)(TR_TPB * CB_ST + CB_NW * TR_TPB) * sizeof(float);
+  static int set = 0;
+  if (!set) {
+    hipError_t e = hipFuncSetAttribute((const void*)mcaq_cmlp_bwd_multi_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lc);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)mcaq_bilateral_bwd_multi_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024 - 1024);
+    if (e != hipSuccess) return (int)e;
+    set = 1;
+  }
+  hipLaunchKernelGGL(mcaq_bilateral_bwd_multi_kernel, dim3(wb), dim3(256), lb, stream, Mb);
+  hipLaunchKernelGGL(mcaq_cmlp_bwd_multi_kernel, dim3(wc), dim3(64 * CB_NW), lc, stream, Mc);
+  return (int)hipGetLastError();
+}
+
+int mcaq_smask_train_backward_multi(const mcaq_smask_seg* segs, int nseg, hipStream_t stream) {
+  using namespace mcaq;
+  if (!segs || nseg < 1 || nseg > TR_MAXSEG) return (int)hipErrorInvalidValue;
+  TrMulti<MaskTrainArgs> M{};
+  int wg = 0;
+  size_t lb = 0;
+  for (int k = 0; k < nseg; ++k) {
+    const mcaq_smask_seg& g = segs[k];
+    if (!g.bits || !g.absmean || !g.gm || !g.gbits || !g.gpart || g.B < 1 || g.ht < 1 || g.wt < 1 || g.H < g.ht ||
+        g.W < g.wt)
+      return (int)hipErrorInvalidValue;
+    MaskTrainArgs& A = M.s[k];
+    A.P = g.P; A.bits = g.bits; A.absmean = g.absmean; A.gm = g.gm; A.gbits = g.gbits; A.gpart = g.gpart;
+    A.B = g.B; A.H = g.H; A.W = g.W; A.ht = g.ht; A.wt = g.wt; A.accumulate = g.accumulate; A.wg0 = wg;
+    wg += g.B;
+    const int NT = g.ht * g.wt;
+    const size_t l = ((size_t)20 * NT + 64 + (size_t)g.H * g.wt + (size_t)g.H * g.W) * sizeof(float) +
+                     (size_t)2 * (g.ht + g.wt) * sizeof(int);
+    if (l > 160 * 1024 - 1024) return (int)hipErrorInvalidValue;
+    lb = l > lb ? l : lb;
+  }
+  M.nseg = nseg;
+  static int set = 0;
+  if (!set) {
+    const hipError_t e = hipFuncSetAttribute((const void*)mcaq_smask_bwd_multi_kernel,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024);
+    if (e != hipSuccess) return (int)e;
+    set = 1;
+  }
+  hipLaunchKernelGGL(mcaq_smask_bwd_multi_kernel, dim3(wg), dim3(SM_TH), lb, stream, M);
+  return (int)hipGetLastError();
+}
+
+int mcaq_train_reduce_multi(const mcaq_reduce_seg* segs, int nseg, int chain, hipStream_t stream) {
+  using namespace mcaq;
+  if (!segs || nseg < 1 || nseg > TR_MAXSEG) return (int)hipErrorInvalidValue;
+  TrMulti<TrReduceSeg> M{};
+  int cmax = 0;
+  for (int k = 0; k < nseg; ++k) {
+    const mcaq_reduce_seg& g = segs[k];
+    if (!g.part || (!g.out && !(chain && k > 0)) || g.nparts < 1 || g.stride < g.count || g.count < 1)
+      return (int)hipErrorInvalidValue;
+    if (chain && g.count != segs[0].count) return (int)hipErrorInvalidValue;
+    M.s[k] = TrReduceSeg{g.part, g.out, g.nparts, g.stride, g.count, g.accumulate};
+    cmax = g.count > cmax ? g.count : cmax;
+  }
+  M.nseg = nseg;
+  hipLaunchKernelGGL(mcaq_tr_reduce_multi_kernel, dim3((cmax + 255) / 256, chain ? 1 : nseg), dim3(256), 0, stream, M,
+                     chain ? 1 : 0);
   return (int)hipGetLastError();
 }
 

@@ -21,18 +21,23 @@ import torch.nn as nn
 
 from .core import (ComplexityToBitMappingNetwork, LinearBitMapper, MorphologicalComplexityAnalyzer,
                    SpatialAdaptiveQuantization)
-from . import core
+from . import core, train_step
 from .engine import HookPlan, ScaleGeom
 
 DEFAULT_INDICES = (4, 6, 9)   # models/mcaq_yolo.py:361 fallback (C3/C4/C5 of YOLOv8)
 
-# Train mode (QAT) through forward_features: every hook scale's chain of small
-# latency-bound launches (pass 1, morph, mapper stages, soft mask, quantizer;
-# and, through autograd's stream semantics, their backwards) on its own HIP
-# stream, so the three chains overlap instead of running back to back.  The
-# state the scales share is ordered by core.concurrent_scales (values equal
-# the sequential step's; tests/test_concurrent_scales_gpu.py).  False: one
-# stream, scale after scale.
+# Train mode (QAT) through forward_features, fastest first:
+#  * MULTI_SCALE_TRAIN: every stage once for all scales (train_step.py: one
+#    launch per stage with per-scale segments, one stream) - values equal the
+#    per-scale path's (tests/test_train_multi_gpu.py);
+#  * CONCURRENT_TRAIN_SCALES: the per-scale modules, each scale's chain of
+#    launches (and, through autograd's stream semantics, its backward) on its
+#    own HIP stream; the state the scales share is ordered by
+#    core.concurrent_scales (tests/test_concurrent_scales_gpu.py).  Captured
+#    in a HIP graph this is a multi-stream graph, which ROCm issues node by
+#    node (tools/probe/graph_replay_probe.py), so it is the second choice;
+#  * else one stream, scale after scale.
+MULTI_SCALE_TRAIN = True
 CONCURRENT_TRAIN_SCALES = True
 
 
@@ -228,7 +233,9 @@ class MCAQHooks(nn.Module):
         (one per backbone index); returns (quantized maps, aux).  In train mode
         on the GPU the scales run on concurrent streams (CONCURRENT_TRAIN_SCALES)."""
         aux = self.begin(temperature=temperature, quantize=quantize)
-        if self._concurrent_ok(feats):
+        if MULTI_SCALE_TRAIN and train_step.multi_ok(self, feats):
+            outs = train_step.forward_features(self, feats, self._mcaq_state)
+        elif self._concurrent_ok(feats):
             outs = self._forward_features_concurrent(feats)
         else:
             outs = []

@@ -1,0 +1,404 @@
+"""The three hook scales of one QAT training step as multi-scale launches.
+
+The per-scale train path (hooks.MCAQHooks._run_scale_modules: analyzer,
+mapper, quantizer module by module, models/mcaq_yolo.py:409-455 in train
+mode) issues every kernel once per scale: ~85 launches per step at config 5,
+each a few microseconds of kernel and a kernel boundary.  Here every stage
+runs once for all scales (the kernels take per-scale segments: mcaq_stats /
+mcaq_morph / mcaq_qat_* with nscales = 3, the mcaq_*_multi train launchers of
+csrc/mcaq_train.h), so a single-stream HIP graph of the step carries about a
+third of the nodes and each node costs about its slowest scale instead of the
+sum.  The values are those of the per-scale path, bit for bit
+(tests/test_train_multi_gpu.py): the same per-scale kernels' bodies run on
+the same data; the mapper's BatchNorm running statistics are updated in scale
+order after the forward (as the per-scale calls leave them); the shared
+modules' parameter gradients are reduced in the order autograd runs the
+per-scale backwards (the last scale first).
+
+Autograd: one Function per stage spans the scales (_HeadMulti, _MapperMulti,
+_SoftMaskMulti, _QATMulti); LinearBitMapper, normalize_complexity and frozen /
+per-tensor quantizers keep their per-scale pieces in between.
+"""
+import ctypes
+
+import torch
+
+from . import abi, core
+from .core import _f32c, _p, _stream
+
+
+def _cmlp_params(an):
+    return list(an.complexity_mlp.parameters())
+
+
+def _run_analyzer_multi(an, xs):
+    """Pass 1 (gray, |x| means, channel min/max partials) and the morphology
+    (phi, complexity MLP, bilateral -> C) of every scale: 2 launches of
+    mcaq_stats / mcaq_morph instead of 2 per scale."""
+    L = abi.lib()
+    n = len(xs)
+    stats = (abi.StatsScale * n)()
+    morphs = (abi.MorphScale * n)()
+    outs, keep = [], []
+    blob = an.cmlp_blob()
+    flags = abi.F_PHI | abi.F_CMLP | an._flags()
+    for i, x in enumerate(xs):
+        B, C, H, W = x.shape
+        T = core.tile_size(H, an.grid_size)
+        ht, wt = H // T, W // T
+        if ht < 1 or wt < 1 or T > 128:
+            raise ValueError("feature map %dx%d: tile %d unsupported" % (H, W, T))
+        dev = x.device
+        units = L.mcaq_stats_units(B, C, H, W)
+        o = {"gray": torch.empty(B, ht * T, wt * T, device=dev), "absmean": torch.empty(B, H, W, device=dev),
+             "pmin": torch.empty(units, C, device=dev), "pmax": torch.empty(units, C, device=dev),
+             "phi": torch.empty(B, ht, wt, 8, device=dev), "c": torch.empty(B, ht, wt, device=dev),
+             "craw": torch.empty(B, ht, wt, device=dev), "tile_tmp": torch.empty(B, ht * wt, 32, device=dev)}
+        s = stats[i]
+        s.x, s.gray, s.absmean, s.pmin, s.pmax = _p(x), _p(o["gray"]), _p(o["absmean"]), _p(o["pmin"]), _p(o["pmax"])
+        s.B, s.C, s.H, s.W, s.Hc, s.Wc = B, C, H, W, ht * T, wt * T
+        ptrs = dict(gray=o["gray"], phi_out=o["phi"], tile_tmp=o["tile_tmp"], cmlp=blob, c_out=o["c"],
+                    cmlp_out=o["craw"])
+        scratch = L.mcaq_morph_scratch_bytes(B, ht * T, wt * T, ht, wt)
+        if scratch:
+            ptrs["gscratch"] = torch.empty(scratch, device=dev, dtype=torch.uint8)
+            keep.append(ptrs["gscratch"])
+        morphs[i] = core._morph_struct(B, H, W, T, ht, wt, flags, **ptrs)
+        outs.append(o)
+    abi.check(L.mcaq_stats(stats, n, _stream()), "mcaq_stats")
+    abi.check(L.mcaq_morph(morphs, n, _stream()), "mcaq_morph")
+    return outs
+
+
+class _HeadMulti(torch.autograd.Function):
+    """Analyzer of every scale in train mode: C per scale (values of the morph
+    kernel); backward = bilateral adjoint + complexity MLP backward of every
+    scale in 2 launches, parameter gradients reduced in one."""
+
+    @staticmethod
+    def forward(ctx, an, n, box, *args):
+        xs, params = args[:n], args[n:]
+        outs = _run_analyzer_multi(an, [x.detach() for x in xs])
+        box.extend(outs)                    # pass-1 by-products for the quantizers
+        an._last_phi = outs[-1]["phi"]
+        ctx.an, ctx.n = an, n
+        ctx.save_for_backward(*[o["phi"] for o in outs], *[o["craw"] for o in outs], *params)
+        return tuple(o["c"] for o in outs)
+
+    @staticmethod
+    def backward(ctx, *gcs):
+        n = ctx.n
+        phis, craws = ctx.saved_tensors[:n], ctx.saved_tensors[n:2 * n]
+        params = ctx.saved_tensors[2 * n:]
+        L = abi.lib()
+        dev = craws[0].device
+        q = abi.CmlpParams(*[_p(p.detach()) for p in params])
+        segs = (abi.HeadSeg * n)()
+        gparts, keep = [], []
+        for i in range(n):
+            B, ht, wt = craws[i].shape
+            m = B * ht * wt
+            g = _f32c(gcs[i]) if gcs[i] is not None else torch.zeros(B, ht, wt, device=dev)
+            gcraw = torch.empty(m, device=dev)
+            gp = torch.empty(L.mcaq_head_gpart_floats(m), device=dev)
+            keep += [g, gcraw]
+            gparts.append((gp, (m + 63) // 64))
+            sg = segs[i]
+            sg.phi, sg.craw, sg.gC, sg.gcraw, sg.gpart = _p(phis[i]), _p(craws[i]), _p(g), _p(gcraw), _p(gp)
+            sg.B, sg.ht, sg.wt = B, ht, wt
+        abi.check(L.mcaq_head_train_backward_multi(ctypes.byref(q), segs, n, _stream()),
+                  "mcaq_head_train_backward_multi")
+        mod_params = _cmlp_params(ctx.an)
+        sink = ctx.an._gsink.target(mod_params) if len(mod_params) == len(params) else None
+        gflat, acc = sink if sink is not None else (torch.empty(core._CM_SIZE, device=dev), 0)
+        _reduce_chain(gparts, gflat, acc, core._CM_SIZE)
+        grads = (None,) * len(params) if sink is not None else tuple(core._split_flat(gflat, params))
+        return (None, None, None) + (None,) * n + grads
+
+
+def _reduce_chain(gparts, out, acc, count):
+    """Sum every scale's per-workgroup partials into `out` in the order the
+    per-scale backwards accumulate them (autograd runs the last scale's first)."""
+    n = len(gparts)
+    segs = (abi.ReduceSeg * n)()
+    for k, (gp, nparts) in enumerate(reversed(gparts)):
+        s = segs[k]
+        s.part, s.out, s.nparts, s.stride, s.count, s.accumulate = _p(gp), _p(out), nparts, count, count, acc
+    abi.check(abi.lib().mcaq_train_reduce_multi(segs, n, 1, _stream()), "mcaq_train_reduce_multi")
+
+
+class _MapperMulti(torch.autograd.Function):
+    """Train-mode bit mapper of every scale: 4 forward launches (one per
+    batch-statistics barrier) + the running-statistics update in scale order;
+    4 backward launches + one parameter reduction."""
+
+    @staticmethod
+    def forward(ctx, mod, temperature, return_continuous, n, *args):
+        cs, params = args[:n], args[n:]
+        net = mod.mapping_network
+        L = abi.lib()
+        dev = cs[0].device
+        bns = [net[i] for i in (1, 4, 7)]
+        q = abi.MapperParams()
+        for k, t in zip(("w1", "b1", "w2", "b2", "w3", "b3", "w4", "b4"),
+                        (net[0].weight, net[0].bias, net[3].weight, net[3].bias, net[6].weight, net[6].bias,
+                         net[9].weight, net[9].bias)):
+            setattr(q, k, _p(t.detach()))
+        for i, bn in enumerate(bns, 1):
+            for k, t in (("g", bn.weight), ("be", bn.bias), ("rm", bn.running_mean), ("rv", bn.running_var),
+                         ("nbt", bn.num_batches_tracked)):
+                setattr(q, "%s%d" % (k, i), _p(t.detach()) if t is not None else None)
+        T = max(float(temperature), 0.1) if temperature is not None else 0.0
+        segs = (abi.MapperSeg * n)()
+        cfs, works, bits = [], [], []
+        for i, c in enumerate(cs):
+            cf = _f32c(c).reshape(-1)
+            m = cf.numel()
+            w = torch.empty(L.mcaq_mapper_work_floats(m), device=dev)
+            b = torch.empty(m, device=dev)
+            cfs.append(cf); works.append(w); bits.append(b)
+            segs[i].c, segs[i].bits, segs[i].work, segs[i].n = _p(cf), _p(b), _p(w), m
+        mom = float(bns[0].momentum)
+        abi.check(L.mcaq_mapper_train_forward_multi(ctypes.byref(q), segs, n, mod.min_bits, mod.max_bits, T, mom,
+                                                    0 if return_continuous else 1, 2, _stream()),
+                  "mcaq_mapper_train_forward_multi")
+        wa = (abi.P * n)(*[_p(w) for w in works])
+        na = (abi.I * n)(*[c.numel() for c in cfs])
+        abi.check(L.mcaq_mapper_running_update(ctypes.byref(q), wa, na, n, mom, _stream()),
+                  "mcaq_mapper_running_update")
+        ctx.q, ctx.T, ctx.mod, ctx.n = q, T, mod, n
+        ctx.shapes = [c.shape for c in cs]
+        ctx.save_for_backward(*cfs, *works, *params)
+        return tuple(b.view(c.shape) for b, c in zip(bits, cs))
+
+    @staticmethod
+    def backward(ctx, *gbits):
+        n, mod = ctx.n, ctx.mod
+        cfs, works = ctx.saved_tensors[:n], ctx.saved_tensors[n:2 * n]
+        params = ctx.saved_tensors[2 * n:]
+        L = abi.lib()
+        dev = cfs[0].device
+        segs = (abi.MapperSeg * n)()
+        gcs, gparts, keep = [], [], []
+        for i in range(n):
+            m = cfs[i].numel()
+            g = _f32c(gbits[i]).reshape(-1) if gbits[i] is not None else torch.zeros(m, device=dev)
+            gc = torch.empty(m, device=dev)
+            gp = torch.empty(L.mcaq_mapper_gpart_floats(m), device=dev)
+            keep.append(g)
+            gcs.append(gc)
+            gparts.append((gp, (m + 63) // 64))
+            s = segs[i]
+            s.c, s.work, s.gbits, s.gc, s.gpart, s.n = _p(cfs[i]), _p(works[i]), _p(g), _p(gc), _p(gp), m
+        abi.check(L.mcaq_mapper_train_backward_multi(ctypes.byref(ctx.q), segs, n, mod.min_bits, mod.max_bits, ctx.T,
+                                                     _stream()), "mcaq_mapper_train_backward_multi")
+        sink = mod._gsink.target(list(mod.mapping_network.parameters()))
+        gflat, acc = sink if sink is not None else (torch.empty(core._MAPPER_G_SIZE, device=dev), 0)
+        _reduce_chain(gparts, gflat, acc, core._MAPPER_G_SIZE)
+        grads = (None,) * len(params) if sink is not None else tuple(core._split_flat(gflat, params))
+        return (None, None, None, None) + tuple(g.view(s) for g, s in zip(gcs, ctx.shapes)) + grads
+
+
+class _SoftMaskMulti(torch.autograd.Function):
+    """LearnedSoftMask of every scale (each quantizer its own net): m(p)
+    planes by one morph launch; backward by one launch + one reduction."""
+
+    @staticmethod
+    def forward(ctx, mods, n, *args):
+        bits, absmeans = args[:n], args[n:2 * n]
+        L = abi.lib()
+        morphs = (abi.MorphScale * n)()
+        ms = []
+        for i in range(n):
+            b = _f32c(bits[i]).detach()
+            B, H, W = absmeans[i].shape
+            _, ht, wt = b.shape
+            if 4 * ht > H or 4 * wt > W:
+                raise NotImplementedError("soft mask on a tile grid finer than 4 pixels per tile")
+            m = torch.empty(B, 1, H, W, device=b.device)
+            ms.append(m)
+            morphs[i] = core._morph_struct(B, H, W, 4, ht, wt, abi.F_SOFTMASK, absmean=absmeans[i], bits_in=b,
+                                           smask=mods[i].blob(), m_out=m)
+        abi.check(L.mcaq_morph(morphs, n, _stream()), "mcaq_morph(soft mask)")
+        ctx.mods, ctx.n = mods, n
+        ctx.save_for_backward(*bits, *absmeans)
+        return tuple(ms)
+
+    @staticmethod
+    def backward(ctx, *gms):
+        n = ctx.n
+        bits, absmeans = ctx.saved_tensors[:n], ctx.saved_tensors[n:2 * n]
+        L = abi.lib()
+        segs = (abi.SmaskSeg * n)()
+        rsegs = (abi.ReduceSeg * n)()
+        gbs, gflats, keep = [], [], []
+        for i in range(n):
+            b = _f32c(bits[i])
+            B, H, W = absmeans[i].shape
+            _, ht, wt = b.shape
+            gm = _f32c(gms[i]) if gms[i] is not None else torch.zeros(B, H, W, device=b.device)
+            gb = torch.empty(B, ht, wt, device=b.device)
+            gp = torch.empty(L.mcaq_smask_gpart_floats(B), device=b.device)
+            gf = torch.empty(core._SM_SIZE, device=b.device)
+            keep += [b, gm, gp]
+            gbs.append(gb); gflats.append(gf)
+            s = segs[i]
+            s.P = abi.SmaskParams(*[_p(p.detach()) for p in ctx.mods[i].net.parameters()])
+            s.bits, s.absmean, s.gm, s.gbits, s.gpart = _p(b), _p(absmeans[i]), _p(gm), _p(gb), _p(gp)
+            s.B, s.H, s.W, s.ht, s.wt, s.accumulate = B, H, W, ht, wt, 0
+            r = rsegs[i]
+            r.part, r.out, r.nparts, r.stride, r.count, r.accumulate = _p(gp), _p(gf), B, core._SM_SIZE, \
+                core._SM_SIZE, 0
+        abi.check(L.mcaq_smask_train_backward_multi(segs, n, _stream()), "mcaq_smask_train_backward_multi")
+        abi.check(L.mcaq_train_reduce_multi(rsegs, n, 0, _stream()), "mcaq_train_reduce_multi")
+        pgrads = []
+        for i in range(n):
+            params = list(ctx.mods[i].net.parameters())
+            pgrads += [g if p.requires_grad else None for g, p in zip(core._split_flat(gflats[i], params), params)]
+        return (None, None) + tuple(gbs[i] if ctx.needs_input_grad[2 + i] else None for i in range(n)) + \
+            (None,) * n + tuple(pgrads)
+
+
+class _QATMulti(torch.autograd.Function):
+    """Fractional-bit straight-through quantizer x m(p) of every scale: one
+    forward launch, one backward launch (+ its fold)."""
+
+    @staticmethod
+    def forward(ctx, n, *args):
+        xs, bits, ms, mins, maxs = (args[k * n:(k + 1) * n] for k in range(5))
+        xs = [_f32c(x) for x in xs]
+        bits = [_f32c(b) for b in bits]
+        ms = [None if m is None else _f32c(m) for m in ms]
+        arr = (abi.QatScale * n)()
+        ys = []
+        for i in range(n):
+            y = torch.empty_like(xs[i])
+            ys.append(y)
+            q = core._qat_struct(xs[i], bits[i], ms[i], mins[i], maxs[i])
+            q.y = _p(y)
+            arr[i] = q
+        abi.check(abi.lib().mcaq_qat_forward(arr, n, _stream()), "mcaq_qat_forward")
+        ctx.n = n
+        ctx.has_m = [m is not None for m in ms]
+        ctx.save_for_backward(*xs, *bits, *[m for m in ms if m is not None], *mins, *maxs)
+        return tuple(ys)
+
+    @staticmethod
+    def backward(ctx, *gys):
+        n = ctx.n
+        sv = ctx.saved_tensors
+        xs, bits = sv[:n], sv[n:2 * n]
+        nm = sum(ctx.has_m)
+        mit = iter(sv[2 * n:2 * n + nm])
+        ms = [next(mit) if h else None for h in ctx.has_m]
+        mins, maxs = sv[2 * n + nm:3 * n + nm], sv[3 * n + nm:]
+        L = abi.lib()
+        arr = (abi.QatScale * n)()
+        gxs, gbs, gmsl, keep = [], [], [], []
+        for i in range(n):
+            x = xs[i]
+            B, C, H, W = x.shape
+            g = _f32c(gys[i]) if gys[i] is not None else torch.zeros_like(x)
+            gx = torch.empty_like(x)
+            gm = torch.empty(B, H, W, device=x.device) if (ms[i] is not None and ctx.needs_input_grad[1 + 2 * n + i]) \
+                else None
+            gb = torch.empty(bits[i].shape, device=x.device) if ctx.needs_input_grad[1 + n + i] else None
+            work = torch.empty(L.mcaq_qat_work_floats(B, C, H, W), device=x.device)
+            keep += [g, work]
+            q = core._qat_struct(x, bits[i], ms[i], mins[i], maxs[i])
+            q.g, q.gx, q.gm, q.gb, q.work = _p(g), _p(gx), _p(gm), _p(gb), _p(work)
+            arr[i] = q
+            gxs.append(gx); gbs.append(gb); gmsl.append(None if gm is None else gm.view(ms[i].shape))
+        abi.check(L.mcaq_qat_backward(arr, n, _stream()), "mcaq_qat_backward")
+        return (None,) + tuple(gxs) + tuple(gbs) + tuple(gmsl) + (None,) * (2 * n)
+
+
+def multi_ok(hooks, feats):
+    """The multi-scale step covers train mode with the fused kernels on one
+    device, an unsharded batch and the reference modules (mlp or linear mapper,
+    per-channel or per-tensor quantizers)."""
+    if not (hooks.training and core.FUSED_TRAIN and len(feats) > 1):
+        return False
+    if not all(torch.is_tensor(f) and f.is_cuda and f.dim() == 4 for f in feats):
+        return False
+    if len({f.device for f in feats}) != 1 or len(feats) > abi.MCAQ_TRAIN_MAXSEG:
+        return False
+    if hooks.process_group is not None or any(q.process_group is not None for q in hooks.quantizers.values()):
+        return False
+    an = hooks.complexity_analyzer
+    if any(not core._head_bwd_fits(*core._tile_grid(f.shape[2], f.shape[3], an.grid_size)) for f in feats):
+        return False
+    if isinstance(hooks.bit_mapper, core.ComplexityToBitMappingNetwork):
+        if not hooks.bit_mapper._fusable() or core._mapper_group(hooks.bit_mapper.mapping_network) is not None:
+            return False
+    for idx, f in zip(hooks.backbone_out_indices, feats):
+        q = hooks.quantizers[str(idx)]
+        if q.smooth_transitions and q.soft_mask is not None:
+            ht, wt = core._tile_grid(f.shape[2], f.shape[3], an.grid_size)
+            if not core._smask_bwd_fits(f.shape[2], f.shape[3], ht, wt):
+                return False
+    return True
+
+
+def forward_features(hooks, feats, state):
+    """models/mcaq_yolo.py:409-455 in train mode for all scales at once;
+    appends one aux entry per scale to state['aux'] and returns the quantized
+    maps (or the inputs when state['quantize'] is False)."""
+    n = len(feats)
+    an, mapper = hooks.complexity_analyzer, hooks.bit_mapper
+    idxs = list(hooks.backbone_out_indices)[:n]
+    xs = [f.float().contiguous() for f in feats]
+    box = []
+    cs = list(_HeadMulti.apply(an, n, box, *xs, *_cmlp_params(an)))
+    if hooks.normalize_complexity:
+        for i, c in enumerate(cs):
+            B = c.shape[0]
+            flat = c.reshape(B, -1)
+            lo = torch.quantile(flat, 0.02, dim=1, keepdim=True).unsqueeze(-1)
+            hi = torch.quantile(flat, 0.98, dim=1, keepdim=True).unsqueeze(-1)
+            cs[i] = ((c - lo) / (hi - lo + 1e-8)).clamp(0.0, 1.0)
+    T = state.get("temperature", 1.0)
+    if isinstance(mapper, core.ComplexityToBitMappingNetwork):
+        ncs = [core._normalize_complexity_shape(c) for c in cs]
+        bits = list(_MapperMulti.apply(mapper, T, True, n, *ncs, *mapper.mapping_network.parameters()))
+    else:
+        bits = [mapper(c, T, return_continuous=True) for c in cs]
+    quantize = state.get("quantize", True)
+    if not quantize:
+        for i in range(n):
+            state.setdefault("aux", []).append({"layer": idxs[i], "complexity": cs[i], "bit_map": bits[i],
+                                                "features_q": feats[i]})
+        return list(feats)
+    qs = [hooks.quantizers[str(i)] for i in idxs]
+    mins, maxs = [], []
+    for i, (q, x) in enumerate(zip(qs, xs)):
+        B, C, H, W = x.shape
+        if bits[i].dim() != 3 or bits[i].shape[0] != B:
+            raise AssertionError(f"Batch size mismatch: {B} vs {bits[i].shape[0]}")
+        p1 = box[i]
+        copies = None
+        frozen = q._frozen()
+        if not frozen:
+            copies = q.update_running_stats(x, p1["absmean"], want_copies=q.training,
+                                            partials=(p1["pmin"], p1["pmax"]))
+        if copies is not None:
+            xmin, xmax = copies
+        elif q.running_min is not None and (q.training or frozen):
+            xmin = q._stats_c(q.running_min, C).clone()
+            xmax = q._stats_c(q.running_max, C).clone()
+        else:
+            xmin, xmax = q.batch_minmax(x, None)
+        mins.append(xmin); maxs.append(xmax)
+    want = [q.smooth_transitions and q.soft_mask is not None for q in qs]
+    ms = [None] * n
+    if all(want):
+        ms = list(_SoftMaskMulti.apply([q.soft_mask for q in qs], n, *bits, *[b["absmean"] for b in box],
+                                       *[p for q in qs for p in q.soft_mask.net.parameters()]))
+    elif any(want):
+        ms = [q.soft_mask(b, x, absmean=p1["absmean"]) if w else None
+              for q, b, x, p1, w in zip(qs, bits, xs, box, want)]
+    ys = list(_QATMulti.apply(n, *feats, *bits, *ms, *mins, *maxs))
+    for i in range(n):
+        state.setdefault("aux", []).append({"layer": idxs[i], "complexity": cs[i], "bit_map": bits[i],
+                                            "features_q": ys[i]})
+    return ys

@@ -27,10 +27,12 @@ def _feats(B=4, seed=5, shapes=((64, 80), (128, 40), (256, 20))):
     return feats, gens
 
 
-def _run(concurrent, steps=3, graph=False, mapper="mlp"):
+def _run(concurrent, steps=3, graph=False, mapper="mlp", multi=False):
+    """concurrent / multi select the train path (hooks.CONCURRENT_TRAIN_SCALES,
+    hooks.MULTI_SCALE_TRAIN); both False: per-scale modules on one stream."""
     from mcaq_yolo_amd import hooks
-    old = hooks.CONCURRENT_TRAIN_SCALES
-    hooks.CONCURRENT_TRAIN_SCALES = concurrent
+    old = hooks.CONCURRENT_TRAIN_SCALES, hooks.MULTI_SCALE_TRAIN
+    hooks.CONCURRENT_TRAIN_SCALES, hooks.MULTI_SCALE_TRAIN = concurrent, multi
     try:
         h = _hooks(mapper)
         feats, gens = _feats()
@@ -77,7 +79,7 @@ def _run(concurrent, steps=3, graph=False, mapper="mlp"):
         snap["bufs"] = {k: b.detach().clone() for k, b in h.named_buffers() if b is not None}
         return snap
     finally:
-        hooks.CONCURRENT_TRAIN_SCALES = old
+        hooks.CONCURRENT_TRAIN_SCALES, hooks.MULTI_SCALE_TRAIN = old
 
 
 def _same(a, b):
@@ -117,9 +119,12 @@ def test_concurrent_scales_runs_on_side_streams():
         seen.append(torch.cuda.current_stream().cuda_stream)
         return orig(ctx, *a)
     core._MapperTrainFn.forward = staticmethod(spy)
+    old = hooks.MULTI_SCALE_TRAIN
+    hooks.MULTI_SCALE_TRAIN = False
     try:
         h.forward_features(feats)
     finally:
         core._MapperTrainFn.forward = staticmethod(orig)
+        hooks.MULTI_SCALE_TRAIN = old
     main = torch.cuda.current_stream().cuda_stream
     assert len(seen) == 3 and len(set(seen)) == 3 and main not in seen

@@ -74,15 +74,20 @@ def _step(h, feats, G, GB, dev, pg=None):
     returns numpy copies of outputs, bits, feature / parameter gradients and
     buffers.  The loss sum_i (y_i g_i) + sum_t (bits_t gb_t) is a sum over
     samples."""
-    from mcaq_yolo_amd import core
+    from mcaq_yolo_amd import core, train_step
     xs = [f.to(dev).requires_grad_(True) for f in feats]
     calls = {"fused": 0}
-    orig = core._MapperTrainFn.apply
+    orig, orig_m = core._MapperTrainFn.apply, train_step._MapperMulti.apply
 
     def spy(*a, **k):
         calls["fused"] += 1
         return orig(*a, **k)
+
+    def spy_m(*a, **k):        # one call for every scale (multi-segment launches)
+        calls["fused"] += a[3]
+        return orig_m(*a, **k)
     core._MapperTrainFn.apply = spy
+    train_step._MapperMulti.apply = spy_m
     try:
         outs, aux = h.forward_features(xs, temperature=1.0)
         loss = sum((o * g.to(dev)).sum() for o, g in zip(outs, G)) + \
@@ -90,6 +95,7 @@ def _step(h, feats, G, GB, dev, pg=None):
         loss.backward()
     finally:
         core._MapperTrainFn.apply = orig
+        train_step._MapperMulti.apply = orig_m
     params = [p for p in h.parameters() if p.requires_grad]
     if pg is not None:
         from mcaq_yolo_amd.dist import allreduce_gradients

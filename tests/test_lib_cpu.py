@@ -33,7 +33,9 @@ def test_struct_layouts_match_header():
     src = open(HDR).read()
     for cname, py in (("mcaq_stats_scale", abi.StatsScale), ("mcaq_finalize_scale", abi.FinalizeScale),
                       ("mcaq_morph_scale", abi.MorphScale), ("mcaq_quant_scale", abi.QuantScale),
-                      ("mcaq_qat_scale", abi.QatScale)):
+                      ("mcaq_qat_scale", abi.QatScale), ("mcaq_mapper_seg", abi.MapperSeg),
+                      ("mcaq_head_seg", abi.HeadSeg), ("mcaq_smask_seg", abi.SmaskSeg),
+                      ("mcaq_reduce_seg", abi.ReduceSeg)):
         body = re.search(r"typedef struct \{([^{}]*)\} %s;" % cname, src).group(1)
         body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
         fields = []

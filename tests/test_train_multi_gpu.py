@@ -1,0 +1,79 @@
+"""The multi-scale QAT step (train_step.py: every stage once for all hook
+scales, per-scale segments in one launch) against the per-scale modules on one
+stream (hooks.MULTI_SCALE_TRAIN / CONCURRENT_TRAIN_SCALES off).  The segments
+run the per-scale kernels' bodies on the same data, the mapper's running
+statistics are updated in scale order and the shared parameter gradients are
+summed in autograd's per-scale order, so every value is bit-identical:
+outputs, complexity / bit maps, feature and parameter gradients, parameters
+after SGD steps, every buffer - eager and captured in a HIP graph."""
+import pytest
+import torch
+
+from test_concurrent_scales_gpu import _feats, _run, _same
+from test_train_fused_gpu import _hooks
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("mapper", ["mlp", "linear"])
+def test_multi_scale_step_equals_per_scale_eager(mapper):
+    _same(_run(False, mapper=mapper, multi=True), _run(False, mapper=mapper))
+
+
+def test_multi_scale_step_equals_per_scale_graph():
+    _same(_run(False, steps=3, graph=True, multi=True), _run(False, steps=4))
+
+
+def test_multi_scale_step_launches_once_per_stage():
+    """One train-mode mapper forward / backward call for all three scales,
+    and none of the per-scale Functions."""
+    from mcaq_yolo_amd import core, hooks, train_step
+    assert hooks.MULTI_SCALE_TRAIN
+    h = _hooks()
+    feats, gens = _feats()
+    calls = {"multi": 0, "per_scale": 0}
+    om, op = train_step._MapperMulti.forward, core._MapperTrainFn.forward
+
+    def spy_m(ctx, *a):
+        calls["multi"] += 1
+        return om(ctx, *a)
+
+    def spy_p(ctx, *a):
+        calls["per_scale"] += 1
+        return op(ctx, *a)
+    train_step._MapperMulti.forward = staticmethod(spy_m)
+    core._MapperTrainFn.forward = staticmethod(spy_p)
+    try:
+        outs, aux = h.forward_features(feats)
+        sum((o * g).sum() for o, g in zip(outs, gens)).backward()
+        torch.cuda.synchronize()
+    finally:
+        train_step._MapperMulti.forward = staticmethod(om)
+        core._MapperTrainFn.forward = staticmethod(op)
+    assert calls == {"multi": 1, "per_scale": 0}
+    assert len(aux) == 3 and all(f.grad is not None for f in feats)
+
+
+def test_multi_scale_step_quantize_off_and_frozen():
+    """quantize=False (aux only, inputs returned) and frozen quantizer
+    statistics take the same values on both paths."""
+    from mcaq_yolo_amd import hooks
+    feats, _ = _feats()
+    res = []
+    for multi in (True, False):
+        old = hooks.MULTI_SCALE_TRAIN, hooks.CONCURRENT_TRAIN_SCALES
+        hooks.MULTI_SCALE_TRAIN, hooks.CONCURRENT_TRAIN_SCALES = multi, False
+        try:
+            h = _hooks()
+            outs, aux = h.forward_features(feats, quantize=False)
+            assert all(o is f for o, f in zip(outs, feats))
+            h.forward_features(feats)                  # running stats exist
+            for q in h.quantizers.values():
+                q.freeze_calibration()
+            outs2, aux2 = h.forward_features(feats)
+            torch.cuda.synchronize()
+            res.append([a["bit_map"].detach().clone() for a in aux] + [o.detach().clone() for o in outs2])
+        finally:
+            hooks.MULTI_SCALE_TRAIN, hooks.CONCURRENT_TRAIN_SCALES = old
+    for a, b in zip(*res):
+        assert torch.equal(a, b)

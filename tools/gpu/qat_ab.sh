@@ -8,8 +8,8 @@ T=${1:-r04_qat_ab}
 mkdir -p $R/gpurun_out/$T
 cd $R
 for r in 1 2; do
-  for sc in concurrent sequential; do
-    for pc in default 0; do
+  for sc in ${SCALES:-multi concurrent sequential}; do
+    for pc in ${PCS:-default}; do
       if [ $pc = default ]; then unset DEBUG_CLR_GRAPH_PACKET_CAPTURE; else export DEBUG_CLR_GRAPH_PACKET_CAPTURE=$pc; fi
       for mode in graph eager; do
         ex=""; [ $mode = eager ] && ex="--eager"
