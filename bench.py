@@ -192,6 +192,12 @@ def main_qat(args, world, rank, dev, pg):
             run()
     torch.cuda.synchronize()
 
+    # HBM-side bytes per launch of the QAT kernels (rocprofv3 PMC passes,
+    # tools/gpu/pmc_r04.sh -> profiles/pmc_traffic_config5.json)
+    qat_traffic = {}
+    tpath = os.path.join(ROOT, "profiles", "pmc_traffic_config5.json")
+    if os.path.exists(tpath):
+        qat_traffic = {k: v["total"] for k, v in json.load(open(tpath)).get("kernels", {}).items()}
     # per-kernel device time of the QAT quantizer over the three scales in one launch
     L = abi.lib()
     stream = torch.cuda.current_stream()
@@ -292,7 +298,8 @@ def main_qat(args, world, rank, dev, pg):
                        "single_step_latency_us": round(t_one * 1e6, 1),
                        "single_step_enqueue_us": round(t_one_enq * 1e6, 1)},
             "roofline": {"bound": "hbm", "achieved": kern["qat_backward_kernel"]["GB/s"], "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s", "frac": kern["qat_backward_kernel"]["frac"], "traffic": None,
+                         "unit": "GB/s", "frac": kern["qat_backward_kernel"]["frac"],
+                         "traffic": qat_traffic.get("mcaq_qat_kernel<bwd>"),
                          "kernel": "mcaq_qat_kernel<bwd> (read g, x + write grad_x: 12 B per element, + 4 B per "
                                    "pixel of mask); its fold kernel is kernels.qat_fold",
                          "alg_bytes_per_launch": kern["qat_backward_kernel"]["alg_bytes"],
@@ -1056,8 +1063,11 @@ def main():
             # the dominant kernel (pass 2): algorithmic bytes per launch over its
             # launch time (HIP events on its stream, single-batch steps in sequence)
             "roofline": {"bound": "hbm", "achieved": kern["quant"]["GB/s"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": kern["quant"]["frac"], "traffic": traffic_k.get("mcaq_quant_kernel"),
-                         "kernel": "mcaq_quant_kernel (pass 2: read x + write y, 8 B per feature element)",
+                         "frac": kern["quant"]["frac"],
+                         "traffic": traffic_k.get("mcaq_quant_tile_kernel", traffic_k.get("mcaq_quant_kernel")),
+                         "kernel": "%s (pass 2: read x + write y, 8 B per feature element)"
+                                   % ("mcaq_quant_tile_kernel" if "mcaq_quant_tile_kernel" in traffic_k
+                                      else "mcaq_quant_kernel"),
                          "alg_bytes_per_launch": 8 * elems, "us_per_launch": kern["quant"]["us"]},
             "kernels": kern,
             "cpu_baseline": None,

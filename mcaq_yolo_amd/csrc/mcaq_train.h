@@ -73,13 +73,29 @@ __device__ __forceinline__ void chan_combine(const float* part, int nwg, int str
 }
 
 // ---- parameter-gradient reduction ------------------------------------------
+// sum_w part[w * stride + e] in workgroup order; the loads of 8 partials are
+// issued before their adds (the sum is a chain of dependent adds, the loads
+// are not: one memory latency per 8 partials instead of per partial)
+__device__ __forceinline__ float tr_ordered_sum(const float* __restrict__ part, int nwg, int stride, int e) {
+  float s = 0.0f;
+  int w = 0;
+  for (; w + 8 <= nwg; w += 8) {
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = part[(size_t)(w + k) * stride + e];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += v[k];
+  }
+  for (; w < nwg; ++w) s += part[(size_t)w * stride + e];
+  return s;
+}
+
 // out[e] (+)= sum_w part[w * stride + e], e < count, w in order
 __global__ __launch_bounds__(256) void mcaq_tr_reduce_kernel(const float* __restrict__ part, int nwg, int stride,
                                                              int count, float* __restrict__ out, int accumulate) {
   const int e = blockIdx.x * 256 + threadIdx.x;
   if (e >= count) return;
-  float s = 0.0f;
-  for (int w = 0; w < nwg; ++w) s += part[(size_t)w * stride + e];
+  const float s = tr_ordered_sum(part, nwg, stride, e);
   out[e] = accumulate ? out[e] + s : s;
 }
 
@@ -1241,8 +1257,7 @@ __global__ __launch_bounds__(256) void mcaq_tr_reduce_multi_kernel(TrMulti<TrRed
     float v = 0.0f;
     for (int k = 0; k < M.nseg; ++k) {
       const TrReduceSeg& g = k == 0 ? M.s[0] : (k == 1 ? M.s[1] : M.s[2]);
-      float sum = 0.0f;
-      for (int w = 0; w < g.nwg; ++w) sum += g.part[(size_t)w * g.stride + e];
+      const float sum = tr_ordered_sum(g.part, g.nwg, g.stride, e);
       v = k == 0 ? (s0.accumulate ? s0.out[e] + sum : sum) : v + sum;
     }
     s0.out[e] = v;
@@ -1250,8 +1265,7 @@ __global__ __launch_bounds__(256) void mcaq_tr_reduce_multi_kernel(TrMulti<TrRed
     const int k = blockIdx.y;
     const TrReduceSeg& g = k == 0 ? M.s[0] : (k == 1 ? M.s[1] : M.s[2]);
     if (k >= M.nseg || e >= g.count) return;
-    float sum = 0.0f;
-    for (int w = 0; w < g.nwg; ++w) sum += g.part[(size_t)w * g.stride + e];
+    const float sum = tr_ordered_sum(g.part, g.nwg, g.stride, e);
     g.out[e] = g.accumulate ? g.out[e] + sum : sum;
   }
 }

@@ -22,6 +22,10 @@ def load(root, counter):
 
 
 def short(name):
+    if "mcaq_qat_kernel<true" in name:
+        return "mcaq_qat_kernel<bwd>"
+    if "mcaq_qat_kernel<false" in name:
+        return "mcaq_qat_kernel<fwd>"
     for k in ("mcaq_stats_kernel", "mcaq_morph_kernel", "mcaq_tiles_kernel", "mcaq_quant_tile_kernel",
               "mcaq_quant_kernel", "mcaq_finalize", "mcaq_tb_head_kernel", "mcaq_tb_map_kernel", "mcaq_tb_mask_kernel"):
         if k in name:
