@@ -603,182 +603,6 @@ class Runner(_RunMixin):
             torch.cuda.current_stream().wait_stream(st)
 
 
-class PrefetchRunner(_RunMixin):
-    """--schedule prefetch (N = 1): `depth` streams; step i replays, on stream
-    i % depth, one HIP graph of two branches - pass 1 of batch i + depth on a
-    side stream (the HBM read of a batch `depth` steps ahead) beside the
-    morphology and pass 2 of batch i (whose pass 1 the same stream ran
-    `depth` steps before) - so a stream's critical path per step is max(pass
-    1, morphology + pass 2) instead of their sum.  2 * depth plans: batch j
-    uses plan j % (2 depth); a plan's next pass 1 is in the graph after the
-    one that consumed it on the same stream (stream order protects it)."""
-
-    def __init__(self, plans, depth):
-        if len(plans) < 2 * depth:
-            raise ValueError("prefetch schedule needs >= 2 * depth input batches")
-        self.plans, self.depth = plans, depth
-        self.streams = [torch.cuda.Stream() for _ in range(depth)]
-        self.sides = [torch.cuda.Stream() for _ in range(depth)]
-        self.i = 0
-        P = len(plans)
-        torch.cuda.synchronize()
-        for plan in plans:                       # warm the launchers outside capture
-            plan.launch()
-        torch.cuda.synchronize()
-        self.graphs = {}
-        for i in range(P):
-            st, side = self.streams[i % depth], self.sides[i % depth]
-            cur, nxt = plans[i % P], plans[(i + depth) % P]
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=st):
-                side.wait_stream(st)
-                with torch.cuda.stream(side):
-                    nxt.launch_stats(side)
-                cur.launch_morph(st)
-                cur.launch_quant(st)
-                st.wait_stream(side)
-            self.graphs[i % P] = g
-        torch.cuda.synchronize()
-        for k in range(depth):                   # prologue: pass 1 of the first `depth` batches
-            with torch.cuda.stream(self.streams[k]):
-                plans[k].launch_stats(self.streams[k])
-
-    def step(self):
-        i = self.i
-        self.i += 1
-        st = self.streams[i % self.depth]
-        with torch.cuda.stream(st):
-            self.graphs[i % len(self.plans)].replay()
-
-    def sync(self):
-        for st in self.streams:
-            torch.cuda.current_stream().wait_stream(st)
-
-
-class SplitRunner(_RunMixin):
-    """--schedule split (N = 1, eager): the HBM passes of every batch on ONE
-    streaming stream, back to back (stats(j + L), then quant(j)), the
-    per-image morphology of each batch on one of two high-priority streams
-    between them (after stats(j) via an event; quant(j) waits for its tiles
-    pass).  L batches of look-ahead cover the morphology chain; plan buffers
-    are reused every len(plans) >= L + 1 batches, and every reuse hazard is
-    ordered by the streaming stream's program order."""
-
-    def __init__(self, plans, lookahead):
-        if len(plans) < lookahead + 1:
-            raise ValueError("split schedule needs >= lookahead + 1 input batches")
-        self.plans, self.L = plans, lookahead
-        self.S = torch.cuda.Stream(priority=0)
-        lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") else (0, -1)
-        self.M = [torch.cuda.Stream(priority=hi) for _ in range(2)]
-        self.ev_s, self.ev_t = {}, {}
-        self.i = 0
-        for j in range(lookahead):
-            self._front(j)
-
-    def _front(self, j):
-        plan = self.plans[j % len(self.plans)]
-        with torch.cuda.stream(self.S):
-            plan.launch_stats(self.S)
-            e = torch.cuda.Event()
-            e.record(self.S)
-        M = self.M[j % 2]
-        M.wait_event(e)
-        with torch.cuda.stream(M):
-            plan.launch_morph(M)
-            t = torch.cuda.Event()
-            t.record(M)
-        self.ev_t[j] = t
-
-    def step(self):
-        j = self.i
-        self.i += 1
-        self._front(j + self.L)
-        self.S.wait_event(self.ev_t.pop(j))
-        with torch.cuda.stream(self.S):
-            self.plans[j % len(self.plans)].launch_quant(self.S)
-
-    def sync(self):
-        for st in [self.S] + self.M:
-            torch.cuda.current_stream().wait_stream(st)
-
-
-class StagedRunner:
-    """--schedule staged: the software-pipelined step of
-    engine.HookPipeline - pass 1 of batch i, morph pass A of batch i-1, pass
-    B of batch i-2 and pass 2 of batch i-3, each on its own stream, every
-    piece waiting only for the earlier steps' pieces it depends on.  N = 1:
-    runs of `group` steps are captured as HIP graphs (the four streams as
-    parallel branches, event edges between them; one graph per buffer-set
-    phase) and replayed, so no host work or cross-stream event round trip is
-    paid per launch.  N > 1 (the RCCL min/max all-reduce of each batch on the
-    pass-A stream): eager steps.  After the first 3 (filling) steps every step
-    carries one batch's worth of every stage, and a step's pieces depend only
-    on earlier steps', so synchronising before the timed window does not
-    drain the pipeline: the first timed step already runs all four."""
-
-    def __init__(self, plans, pg, cu_masks=None, group=4):
-        from mcaq_yolo_amd.engine import HookPipeline
-        self.pipe = HookPipeline(plans, cu_masks=cu_masks, process_group=pg)
-        self.graphs = {}
-        self.group = group
-        self.use_graph = pg is None
-        self.stream = torch.cuda.Stream()
-        if self.use_graph:
-            for _ in range(3):                    # fill eagerly
-                self.pipe.submit()
-            self.pipe.join(self.stream)
-
-    def _plan_runs(self, steps):
-        n, i, out = len(self.pipe.plans), self.pipe.i, []
-        while steps > 0:
-            k = min(self.group, steps)
-            out.append((i % n, k))
-            i += k
-            steps -= k
-        return out
-
-    def prepare(self, steps):
-        """Capture every graph a `steps` window needs (before timing)."""
-        if not self.use_graph:
-            return
-        i = self.pipe.i
-        for ph, k in self._plan_runs(steps):
-            if (ph, k) not in self.graphs:
-                self.graphs[(ph, k)] = self.pipe.capture(k, self.stream, at=i)
-            i += k
-
-    def run(self, steps):
-        """Issue exactly `steps` steps."""
-        if not self.use_graph:
-            for _ in range(steps):
-                self.pipe.submit()
-            return
-        self.prepare(steps)
-        for key in self._plan_runs(steps):
-            self.pipe.replay(self.graphs[key], self.stream)
-
-    def step(self):
-        self.run(1)
-
-    def sync(self):
-        if self.use_graph:
-            torch.cuda.current_stream().wait_stream(self.stream)
-        else:
-            self.pipe.join(torch.cuda.current_stream())
-
-
-def cu_masks_for(n_morph, ncus=256):
-    """CU masks: n_morph CUs (spread evenly over the chip) for the two morph
-    streams, the rest for the two streaming streams; 0 = no masks."""
-    if n_morph <= 0:
-        return None
-    step = ncus / float(n_morph)
-    morph = sorted({int(k * step) for k in range(n_morph)})
-    stream = [c for c in range(ncus) if c not in set(morph)]
-    return [stream, morph, morph, stream]
-
-
 def kernel_timing(plans, reps=40, evict=None):
     """Per-launch device time of each kernel of a step, in sequence: `reps`
     single-batch steps on one stream, cycling the plans (>= 4 input batches:
@@ -840,19 +664,9 @@ def main():
     ap.add_argument("--channels-last", action="store_true", help="--e2e: NHWC network (experiment)")
     ap.add_argument("--find", action="store_true", help="--e2e: MIOpen Find (torch.backends.cudnn.benchmark)")
     ap.add_argument("--eager", action="store_true", help="no HIP graphs")
-    ap.add_argument("--schedule", choices=("staged", "streams", "split", "prefetch"), default="streams",
-                    help="streams (default): --pipeline batches in flight, one HIP graph each; staged: software "
-                         "pipeline, pass 1 (i) + pass 2 (i-3) | pass A (i-1) | pass B (i-2) on three streams "
-                         "(eager, host-enqueue bound: 77 vs 64 us per step, profiles/r03_base); split: HBM "
-                         "passes on one stream, morphology on two (SplitRunner, eager, N = 1)")
-    ap.add_argument("--morph-cus", type=int, default=0,
-                    help="--schedule staged: pin the morph streams to this many CUs (0: no CU masks)")
-    ap.add_argument("--lookahead", type=int, default=3, help="--schedule split: batches of look-ahead")
-    ap.add_argument("--staged-plans", type=int, default=8,
-                    help="--schedule staged: buffer sets / input batches cycled (>= 4)")
-    ap.add_argument("--graph-steps", type=int, default=4,
-                    help="--schedule staged, N = 1: steps per captured HIP graph (<= --staged-plans - 4 keeps the "
-                         "buffer-reuse edges between graphs)")
+    ap.add_argument("--schedule", choices=("streams",), default="streams",
+                    help="streams: --pipeline batches in flight on as many HIP streams, one graph each (the staged, "
+                         "split and prefetch schedules of rounds 2-4 measured slower and were removed, DESIGN.md)")
     ap.add_argument("--m-plane", action="store_true",
                     help="pass B writes the m(p) plane and pass 2 reads it (instead of regenerating m per slice)")
     ap.add_argument("--qat-scales", choices=("multi", "concurrent", "sequential"), default=None,
@@ -900,12 +714,6 @@ def main():
     geoms = [ScaleGeom(B, c, h, w, grid) for c, (h, w) in zip(chans, SIZES)]
     plans = []
     nin = max(args.inputs or max(3, depth), depth)
-    if args.schedule == "staged":
-        nin = max(nin, args.staged_plans)
-    if args.schedule == "split":
-        nin = max(nin, args.lookahead + 1)
-    if args.schedule == "prefetch":
-        nin = max(nin, 2 * depth)
     for p in range(nin):
         # each batch in flight has its own synthetic input (seeded per rank and slot)
         feats = [synth_features(B, c, h, w, 1000 * args.config + i + 7919 * rank + 104729 * p, dev)
@@ -917,19 +725,8 @@ def main():
         plans.append(plan)
     torch.cuda.synchronize()
 
-    use_graph = not args.eager and args.schedule in ("streams", "prefetch")
-    if args.schedule == "staged":
-        runner = StagedRunner(plans, pg, cu_masks_for(args.morph_cus), group=args.graph_steps)
-    elif args.schedule == "split":
-        if pg is not None:
-            raise SystemExit("--schedule split is a single-GPU experiment")
-        runner = SplitRunner(plans, args.lookahead)
-    elif args.schedule == "prefetch":
-        if pg is not None:
-            raise SystemExit("--schedule prefetch is single-process (N = 1)")
-        runner = PrefetchRunner(plans, depth)
-    else:
-        runner = Runner(plans, pg, use_graph, depth)
+    use_graph = not args.eager
+    runner = Runner(plans, pg, use_graph, depth)
     runner.run(max(args.warmup, 1))
     runner.sync()
     torch.cuda.synchronize()
@@ -960,7 +757,6 @@ def main():
     # difference is K steady-state steps (the fill and drain cancel), which
     # is what ms_per_step reports; the raw K-step window is kept beside it.
     def window(k):
-        runner.prepare(k)        # staged schedule: capture this window's graphs first (untimed)
         runner.sync()
         if pg is not None:
             import torch.distributed as dist
@@ -1034,18 +830,9 @@ def main():
                        "global_batch": world * B, "grid_size": grid, "mapper": mapper,
                        "parallelism": "dp%d" % world,
                        "pass_b": "batch-wide tile kernels" if _engine_mod().TILES_BATCH else "per-image workgroups",
-                       "hip_graph": use_graph or getattr(runner, "use_graph", False),
-                       "batches_in_flight": 4 if args.schedule == "staged" else depth,
-                       "schedule": {"staged": "staged: pass 1 (i) | pass A (i-1) | pass B (i-2) | pass 2 (i-3) on 4 "
-                                              "streams, event edges%s%s" % (
-                                                  ", %d steps per HIP graph" % args.graph_steps
-                                                  if getattr(runner, "use_graph", False) else ", eager",
-                                                  ", morph on %d CUs" % args.morph_cus if args.morph_cus else ""),
-                                    "streams": "streams: %d batch chains on %d streams, one HIP graph each"
-                                               % (depth, depth),
-                                    "split": "split (look-ahead %d)" % args.lookahead,
-                                    "prefetch": "prefetch: %d streams, per step one HIP graph = pass 1 of batch i+%d "
-                                                "beside morphology + pass 2 of batch i" % (depth, depth)}[args.schedule],
+                       "hip_graph": use_graph,
+                       "batches_in_flight": depth,
+                       "schedule": "streams: %d batch chains on %d streams, one HIP graph each" % (depth, depth),
                        "input_batches": len(plans),
                        "latency_ms_single_batch": round(latency_ms, 4),
                        "host_enqueue_us_per_step": round(t_enq / args.steps * 1e6, 1),

@@ -41,7 +41,7 @@ typedef void* hipEvent_t;
 extern "C" {
 #endif
 
-#define MCAQ_ABI_VERSION 14
+#define MCAQ_ABI_VERSION 15
 /* largest dynamic LDS request of the morph kernel (gfx950: 160 KiB per CU) */
 #define MCAQ_MORPH_LDS_LIMIT 163840
 
@@ -178,38 +178,6 @@ int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream);
  * Pass B reads what pass A wrote (tile_tmp). */
 int mcaq_morph_pass(const mcaq_morph_scale* scales, int nscales,
                     const mcaq_finalize_scale* fscales, int nfscales, int passes, hipStream_t stream);
-
-/* ---- software-pipelined hook path (batched throughput) --------------------
- * Step i issues pass 1 of batch i on stream 0, morph pass A (+ channel
- * min/max) of batch i-1 on stream 1, pass B of batch i-2 on stream 2 and
- * pass 2 of batch i-3 on stream 3; each piece waits only for the earlier
- * steps' pieces it reads or whose buffers it rewrites (events), so the
- * morphology and both HBM passes of four batches run side by side.  Batch j
- * uses buffer set j % nplans (nplans >= 4).  cu_masks: NULL, or 4 x
- * mask_words CU bit masks (streams 0..3; an all-zero mask = no mask).
- * hold_a: leave stream 1's end-of-step event unrecorded until
- * mcaq_pipeline_release_a (the caller enqueues the RCCL min/max all-reduce of
- * batch i-1 on mcaq_pipeline_stream(p, 1) first).
- * mcaq_pipeline_fork: every pipeline stream waits for `stream`, and waits on
- * steps issued before the fork are dropped - the caller guarantees those are
- * complete before `stream`'s current position (a graph captured as fork,
- * steps, join and replayed on one stream).  mcaq_pipeline_set_step rewinds or
- * advances the step counter after a capture / replays (waits on steps before
- * it are dropped likewise). */
-typedef struct mcaq_pipeline mcaq_pipeline;
-int mcaq_pipeline_create(const uint32_t* cu_masks, int mask_words, int nplans, mcaq_pipeline** out);
-int mcaq_pipeline_destroy(mcaq_pipeline* p);
-void* mcaq_pipeline_stream(mcaq_pipeline* p, int k);
-int mcaq_pipeline_step(mcaq_pipeline* p,
-                       const mcaq_stats_scale* st, int nst,
-                       const mcaq_morph_scale* ma, int nma, const mcaq_finalize_scale* fz, int nfz,
-                       const mcaq_morph_scale* mb, int nmb,
-                       const mcaq_quant_scale* qs, int nq, int hold_a);
-int mcaq_pipeline_release_a(mcaq_pipeline* p);
-int mcaq_pipeline_fork(mcaq_pipeline* p, hipStream_t stream);
-int mcaq_pipeline_join(mcaq_pipeline* p, hipStream_t stream);
-long long mcaq_pipeline_get_step(mcaq_pipeline* p);
-int mcaq_pipeline_set_step(mcaq_pipeline* p, long long step);
 
 /* Measurement: the calling thread's NEXT mcaq_stats / mcaq_quant launch is
  * issued through hipExtLaunchKernel with these start/stop events (either may

@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libmcaq_hip.so")
-ABI_VERSION = 14
+ABI_VERSION = 15
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -107,9 +107,7 @@ EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats",
            "mcaq_quant",
            "mcaq_qat_forward", "mcaq_qat_backward", "mcaq_qat_work_floats", "mcaq_ema_stats",
            "mcaq_nms", "mcaq_nms_work_floats", "mcaq_time_next_launch", "mcaq_time_launch",
-           "mcaq_morph_pass", "mcaq_pipeline_create", "mcaq_pipeline_destroy", "mcaq_pipeline_stream",
-           "mcaq_pipeline_step", "mcaq_pipeline_release_a", "mcaq_pipeline_join", "mcaq_pipeline_fork",
-           "mcaq_pipeline_get_step", "mcaq_pipeline_set_step",
+           "mcaq_morph_pass",
            "mcaq_mapper_work_floats", "mcaq_mapper_train_forward", "mcaq_mapper_gpart_floats",
            "mcaq_mapper_train_backward", "mcaq_head_gpart_floats", "mcaq_head_train_backward",
            "mcaq_smask_gpart_floats", "mcaq_smask_train_backward", "mcaq_ema_stats_ex", "mcaq_pack",
@@ -139,26 +137,6 @@ def _declare(lib):
     lib.mcaq_morph_finalize.argtypes = [ctypes.POINTER(MorphScale), I, ctypes.POINTER(FinalizeScale), I, P]
     lib.mcaq_morph_pass.restype = I
     lib.mcaq_morph_pass.argtypes = [ctypes.POINTER(MorphScale), I, ctypes.POINTER(FinalizeScale), I, I, P]
-    lib.mcaq_pipeline_create.restype = I
-    lib.mcaq_pipeline_create.argtypes = [ctypes.POINTER(ctypes.c_uint32), I, I, ctypes.POINTER(P)]
-    lib.mcaq_pipeline_destroy.restype = I
-    lib.mcaq_pipeline_destroy.argtypes = [P]
-    lib.mcaq_pipeline_stream.restype = P
-    lib.mcaq_pipeline_stream.argtypes = [P, I]
-    lib.mcaq_pipeline_step.restype = I
-    lib.mcaq_pipeline_step.argtypes = [P, ctypes.POINTER(StatsScale), I, ctypes.POINTER(MorphScale), I,
-                                       ctypes.POINTER(FinalizeScale), I, ctypes.POINTER(MorphScale), I,
-                                       ctypes.POINTER(QuantScale), I, I]
-    lib.mcaq_pipeline_release_a.restype = I
-    lib.mcaq_pipeline_release_a.argtypes = [P]
-    lib.mcaq_pipeline_join.restype = I
-    lib.mcaq_pipeline_join.argtypes = [P, P]
-    lib.mcaq_pipeline_fork.restype = I
-    lib.mcaq_pipeline_fork.argtypes = [P, P]
-    lib.mcaq_pipeline_get_step.restype = ctypes.c_longlong
-    lib.mcaq_pipeline_get_step.argtypes = [P]
-    lib.mcaq_pipeline_set_step.restype = I
-    lib.mcaq_pipeline_set_step.argtypes = [P, ctypes.c_longlong]
     lib.mcaq_stats_units.restype = I
     lib.mcaq_stats_units.argtypes = [I, I, I, I]
     lib.mcaq_morph_scratch_bytes.restype = ctypes.c_size_t

@@ -1718,7 +1718,6 @@ int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream) 
 
 #include "mcaq_qat.h"
 #include "mcaq_nms.h"
-#include "mcaq_pipeline.h"
 #include "mcaq_train.h"
 
 // C++-linkage drop-in for the reference's declaration (include/mcaq_hip.h):

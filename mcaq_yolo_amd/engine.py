@@ -10,9 +10,9 @@ HIP stream:
     mcaq_quant            HBM pass 2: y = dequant(quant_b(x)) * m
 
 All buffers of a `HookPlan` are allocated once, so `HookPlan.run` only
-enqueues launches and can be captured into a HIP graph (torch.cuda.CUDAGraph).
-`HookPipeline` runs many batches software-pipelined over four streams
-(mcaq_pipeline.h) for batched throughput, eagerly or as captured HIP graphs.
+enqueues launches and can be captured into a HIP graph (torch.cuda.CUDAGraph);
+batched throughput comes from several plans' graphs replayed on as many
+streams (bench.py Runner).
 
 This module is the HIP path only: non-CUDA tensors or a missing library
 raise here.  CPU tensors take the pure-PyTorch path (fallback.py), which the
@@ -364,175 +364,3 @@ def sync_channel_minmax(bufs, process_group):
         b["xmin"].copy_(-vec[o:o + C])
         b["xmax"].copy_(vec[o + C:o + 2 * C])
         o += 2 * C
-
-
-class HookPipeline:
-    """Software-pipelined hook path for batched throughput (mcaq_pipeline.h):
-    step i runs pass 1 of batch i, morph pass A (+ channel min/max) of batch
-    i-1, pass B of batch i-2 and pass 2 of batch i-3, each on its own HIP
-    stream and waiting only for the earlier steps' pieces it depends on.
-    `plans` (>= 4 prepared HookPlans of the same shapes) are cycled: batch j
-    uses plans[j % len(plans)].  `submit()` issues one step and returns the
-    plan whose pass 2 it issued (None while filling).  Inputs are written on
-    `in_stream` before a batch's submit, outputs read on `out_stream` after
-    the submit that returns its plan.
-    cu_masks: None, or four lists of CU indices (pass 1, pass A, pass B,
-    pass 2 streams) to pin the streams' workgroups to
-    (hipExtStreamCreateWithCUMask).
-    process_group (N > 1): the channel min/max of batch i-1 is all-reduced on
-    the pass-A stream right after its finalize, before pass 2 reads it.
-
-    capture(n) records n steady-state steps as ONE HIP graph (fork, n steps,
-    join: the four streams become parallel branches with the event edges
-    between them), replay(graph, n) issues it: a step then costs no host
-    work per launch and no cross-stream event round trips."""
-
-    def __init__(self, plans, cu_masks=None, process_group=None, ncus=256):
-        if len(plans) < 4:
-            raise ValueError("the 4-stage pipeline needs >= 4 independent HookPlans")
-        self.plans = list(plans)
-        self.lib = plans[0].lib
-        self.pg = process_group
-        h = ctypes.c_void_p()
-        if cu_masks is None:
-            abi.check(self.lib.mcaq_pipeline_create(None, 0, len(self.plans), ctypes.byref(h)),
-                      "mcaq_pipeline_create")
-        else:
-            if len(cu_masks) != 4:
-                raise ValueError("cu_masks: four CU lists (pass 1, pass A, pass B, pass 2 streams)")
-            words = (ncus + 31) // 32
-            arr = (ctypes.c_uint32 * (4 * words))()
-            for k, cus in enumerate(cu_masks):
-                for c in (cus or ()):
-                    arr[k * words + c // 32] |= 1 << (c % 32)
-            abi.check(self.lib.mcaq_pipeline_create(arr, words, len(self.plans), ctypes.byref(h)),
-                      "mcaq_pipeline_create")
-        self.handle = h
-        self.i = 0
-        self.last = None      # drain(): no new batches from this index on
-        self._a_stream = None
-        self._replayed = False
-        self.in_stream = torch.cuda.ExternalStream(self.lib.mcaq_pipeline_stream(h, 0))
-        self.out_stream = torch.cuda.ExternalStream(self.lib.mcaq_pipeline_stream(h, 3))
-        if process_group is not None:
-            self._a_stream = torch.cuda.ExternalStream(self.lib.mcaq_pipeline_stream(h, 1))
-
-    def _piece(self, j, attr):
-        if j < 0 or (self.last is not None and j >= self.last):
-            return None, 0
-        p = self.plans[j % len(self.plans)]
-        v = getattr(p, attr)
-        return v, (p._n if v is not None else 0)
-
-    def submit(self, _capturing=False):
-        if self._replayed and not _capturing:
-            raise RuntimeError("HookPipeline: eager steps after graph replays need resync(stream) first")
-        i = self.i
-        st, nst = self._piece(i, "_st")
-        ma, nma = self._piece(i - 1, "_mo")
-        fz, nfz = self._piece(i - 1, "_fz")
-        mb, nmb = self._piece(i - 2, "_mo")
-        qs, nq = self._piece(i - 3, "_qs")
-        hold = 1 if (self.pg is not None and nma > 0 and fz is not None) else 0
-        abi.check(self.lib.mcaq_pipeline_step(self.handle, st, nst, ma, nma, fz, nfz, mb, nmb, qs, nq, hold),
-                  "mcaq_pipeline_step")
-        if hold:
-            with torch.cuda.stream(self._a_stream):
-                sync_channel_minmax(self.plans[(i - 1) % len(self.plans)].bufs, self.pg)
-            abi.check(self.lib.mcaq_pipeline_release_a(self.handle), "mcaq_pipeline_release_a")
-        self.i += 1
-        return self.plans[(i - 3) % len(self.plans)] if qs is not None else None
-
-    def drain(self):
-        """Finish every submitted batch: three more steps that start no new
-        batch.  Returns the plans completed by them, in batch order."""
-        self.last = self.i
-        done = []
-        for _ in range(3):
-            p = self.submit()
-            if p is not None:
-                done.append(p)
-        return done
-
-    def join(self, stream=None):
-        """Order `stream` (default: the current one) after everything submitted."""
-        abi.check(self.lib.mcaq_pipeline_join(self.handle, _stream_handle(stream)), "mcaq_pipeline_join")
-
-    def capture(self, nsteps, stream, at=None, pre=None, post=None):
-        """Record `nsteps` steady-state steps starting at step index `at`
-        (default: the next one; >= 3, so the pipeline is full) as one
-        torch.cuda.CUDAGraph captured on `stream`.  Nothing runs and the step
-        counter is left unchanged.  A graph's content depends only on the
-        start's buffer-set phase (at % len(plans)): it replays wherever the
-        pipeline is at that phase.  pre(i) / post(i, plan) are called around
-        the capture of step i (e.g. to capture input writes on in_stream and
-        output reads on out_stream).
-
-        The graph's pieces only wait for pieces inside it (fork at the start,
-        join at the end); the edges from earlier steps are implied by the
-        replay order on one stream.  nsteps <= len(plans) - 4 keeps every
-        buffer-reuse edge (pass 1 of batch j after pass 2 of batch j - NP)
-        outside the graph, so its only cross-stream edges run pass 1 -> A ->
-        B -> pass 2."""
-        if self.pg is not None:
-            raise RuntimeError("graph capture of the pipeline is single-process (N = 1)")
-        i_now = self.i
-        i0 = i_now if at is None else at
-        if i0 < 3 or self.last is not None or nsteps < 1:
-            raise ValueError("capture: steps from index >= 3 of an undrained pipeline")
-        if nsteps > len(self.plans) - 4:
-            # a longer capture would put a buffer-reuse edge (pass 1 of batch
-            # j after pass 2 of batch j - NP) inside the graph: two side
-            # streams waiting on each other's events, the topology whose
-            # hipStreamEndCapture segfaulted (DESIGN.md s.3, capture_probe C2)
-            raise ValueError("capture: nsteps %d > len(plans) - 4 = %d" % (nsteps, len(self.plans) - 4))
-        g = torch.cuda.CUDAGraph()
-        self.i = i0
-        abi.check(self.lib.mcaq_pipeline_set_step(self.handle, i0), "mcaq_pipeline_set_step")
-        try:
-            with torch.cuda.graph(g, stream=stream):
-                abi.check(self.lib.mcaq_pipeline_fork(self.handle, _stream_handle(stream)), "mcaq_pipeline_fork")
-                for _ in range(nsteps):
-                    if pre is not None:
-                        pre(self.i)
-                    done = self.submit(_capturing=True)
-                    if post is not None:
-                        post(self.i - 1, done)
-                self.join(stream)
-        finally:
-            self.i = i_now
-            abi.check(self.lib.mcaq_pipeline_set_step(self.handle, i_now), "mcaq_pipeline_set_step")
-        g.mcaq_phase = i0 % len(self.plans)
-        g.mcaq_steps = nsteps
-        self._replayed = True     # the step events now belong to the graph: eager steps need resync()
-        return g
-
-    def replay(self, graph, stream):
-        """Issue a captured graph on `stream` at the pipeline's current step
-        (which must have the graph's buffer-set phase).  The caller ordered
-        `stream` after any eager steps before the first replay (join(stream))."""
-        if self.i % len(self.plans) != graph.mcaq_phase:
-            raise ValueError("graph captured at phase %d, pipeline at step %d" % (graph.mcaq_phase, self.i))
-        with torch.cuda.stream(stream):
-            graph.replay()
-        self.i += graph.mcaq_steps
-        self._replayed = True
-
-    def resync(self, stream):
-        """Continue with eager steps after a capture / replays issued on
-        `stream`: `stream` joins every pipeline stream, then they fork from it."""
-        self.join(stream)
-        abi.check(self.lib.mcaq_pipeline_set_step(self.handle, self.i), "mcaq_pipeline_set_step")
-        abi.check(self.lib.mcaq_pipeline_fork(self.handle, _stream_handle(stream)), "mcaq_pipeline_fork")
-        self._replayed = False
-
-    def close(self):
-        if self.handle is not None:
-            self.lib.mcaq_pipeline_destroy(self.handle)
-            self.handle = None
-
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass

@@ -187,22 +187,3 @@ def test_plan_descriptor_reuse_equals_rebuild(monkeypatch):
         p.prepare(feats, cm, mm, sms, **kw)          # rebuilt from scratch
         assert id(p._st) != st0
         assert snap() == reused
-
-
-def test_pipeline_capture_rejects_buffer_reuse_edges():
-    """HookPipeline.capture refuses nsteps > len(plans) - 4 (a
-    longer graph would hold a buffer-reuse edge between two side streams, the
-    capture topology that segfaulted in hipStreamEndCapture)
-    and a start before the pipeline is full; both before any HIP call."""
-    from mcaq_yolo_amd.engine import HookPipeline
-    p = HookPipeline.__new__(HookPipeline)
-    p.plans, p.pg, p.i, p.last = [object()] * 6, None, 5, None
-    with pytest.raises(ValueError, match="len\\(plans\\) - 4"):
-        p.capture(3, stream=None)
-    with pytest.raises(ValueError, match="index >= 3"):
-        p.capture(1, stream=None, at=2)
-    with pytest.raises(ValueError, match="index >= 3"):
-        p.capture(0, stream=None)
-    p.last = 7
-    with pytest.raises(ValueError, match="undrained"):
-        p.capture(1, stream=None)

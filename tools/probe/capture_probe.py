@@ -4,8 +4,9 @@ the case that broke).  Cases:
   A  fork origin -> s1, s2 (events), kernels, join
   B  side-to-side edge: s2 waits for an event recorded on s1
   C  one event recorded twice inside the capture (ring reuse)
-  D  HookPipeline.capture(n) for n = 1, 2, 4, 8 (no pre/post)
-  E  HookPipeline.capture(8) with pre/post copies"""
+  C1 one event re-recorded, one direction only
+  C2 both directions between two side streams (the case that segfaulted at
+     hipStreamEndCapture on ROCm 7.0 / torch 2.10, round 3)"""
 import ctypes
 import os
 import sys
@@ -131,36 +132,6 @@ say("torch", torch.__version__, "hip", torch.version.hip)
 run_case("A", case_a)
 run_case("B", case_b)
 
-# D: the bench's staged runner (config 2, 8 buffer sets, 4-step graphs) vs streams
-import time  # noqa: E402
-import bench  # noqa: E402
-from mcaq_yolo_amd.engine import HookPlan, ScaleGeom  # noqa: E402
-dev = torch.device("cuda:0")
-name, B, chans, grid, mapper = bench.CONFIGS[2]
-cm, mm, sm = bench.load_blobs(dev)
-geoms = [ScaleGeom(B, c, h, w, grid) for c, (h, w) in zip(chans, bench.SIZES)]
-plans = []
-for p in range(8):
-    feats = [bench.synth_features(B, c, h, w, 2000 + i + 104729 * p, dev) for i, (c, (h, w)) in enumerate(zip(chans, bench.SIZES))]
-    plan = HookPlan(geoms, dev)
-    plan.prepare(feats, cm, mm, [sm] * 3, mapper_kind=mapper)
-    plan.feats = feats
-    plans.append(plan)
-torch.cuda.synchronize()
-for G in (4, 2, 1):
-    r = bench.StagedRunner(plans, None, group=G)
-    r.run(40); r.sync(); torch.cuda.synchronize()
-    for K in (20, 400, 20, 400):
-        r.prepare(K); r.sync(); torch.cuda.synchronize()
-        t0 = time.perf_counter(); r.run(K); te = time.perf_counter() - t0; r.sync(); torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
-        say("D staged graph G=%d K=%d: %.2f us/step (enqueue %.1f us/step)" % (G, K, dt / K * 1e6, te / K * 1e6))
-    r.pipe.close()
-r = bench.Runner(plans[:3], None, True, 3)
-for K in (20, 400, 20, 400):
-    r.run(20); r.sync(); torch.cuda.synchronize()
-    t0 = time.perf_counter(); r.run(K); r.sync(); torch.cuda.synchronize()
-    say("D streams K=%d: %.2f us/step" % (K, (time.perf_counter() - t0) / K * 1e6))
 run_case("C1", case_c1)
 run_case("C2", case_c2)
 run_case("C", case_c)
