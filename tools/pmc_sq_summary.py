@@ -5,7 +5,7 @@ import glob
 import sys
 from collections import defaultdict
 
-KERNELS = ("stats", "band", "edge", "morph", "tiles", "quant", "finalize")
+KERNELS = ("stats", "band", "edge", "morph", "tiles", "quant_tile", "quant", "finalize")
 
 
 def main(d):
