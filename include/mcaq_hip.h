@@ -41,7 +41,7 @@ typedef void* hipEvent_t;
 extern "C" {
 #endif
 
-#define MCAQ_ABI_VERSION 15
+#define MCAQ_ABI_VERSION 17
 /* largest dynamic LDS request of the morph kernel (gfx950: 160 KiB per CU) */
 #define MCAQ_MORPH_LDS_LIMIT 163840
 
@@ -231,6 +231,17 @@ int mcaq_ema_stats(const float* batch_min, const float* batch_max, float* runnin
 int mcaq_ema_stats_ex(const float* batch_min, const float* batch_max, float* running_min, float* running_max,
                       int C, double momentum, int first, float* copy_min, float* copy_max, long long* num_batches,
                       hipStream_t stream);
+/* mcaq_ema_stats_ex of several quantizers (one per hook scale, <= 3) in ONE
+ * launch: segment k is the argument set of one call. */
+typedef struct {
+  const float* batch_min; const float* batch_max;
+  float* running_min; float* running_max;
+  float* copy_min; float* copy_max;   /* or NULL */
+  int64_t* num_batches;                /* or NULL */
+  int C, first;
+  double momentum;
+} mcaq_ema_seg;
+int mcaq_ema_stats_multi(const mcaq_ema_seg* segs, int nseg, hipStream_t stream);
 
 /* ---- batched NMS of YOLOv8 Detect outputs ----------------------------------
  * pred (B, no, N) fp32 with no = 4 + nc rows (cx, cy, w, h, class scores);
@@ -364,6 +375,18 @@ typedef struct {
 int mcaq_mapper_train_forward_multi(const mcaq_mapper_params* P, const mcaq_mapper_seg* segs, int nseg,
                                     float min_bits, float max_bits, float temperature, float momentum,
                                     int round_bits, int update_stats, hipStream_t stream);
+/* Batch sharded over `world` ranks (process-group BatchNorm): one stage of
+ * every segment per call, as mcaq_mapper_train_forward_stage /
+ * _backward_stage; gathered / gsums / gathered1 hold one pointer per segment
+ * (each that segment's world x 129 gathered entries / 128 summed floats). */
+int mcaq_mapper_train_forward_stage_multi(const mcaq_mapper_params* P, const mcaq_mapper_seg* segs, int nseg,
+                                          float min_bits, float max_bits, float temperature, float momentum,
+                                          int round_bits, int update_stats, int stage, const float* const* gathered,
+                                          int world, hipStream_t stream);
+int mcaq_mapper_train_backward_stage_multi(const mcaq_mapper_params* P, const mcaq_mapper_seg* segs, int nseg,
+                                           float min_bits, float max_bits, float temperature, int stage,
+                                           const float* const* gsums, const float* const* gathered1, int world,
+                                           hipStream_t stream);
 /* 4 launches (no parameter reduction) */
 int mcaq_mapper_train_backward_multi(const mcaq_mapper_params* P, const mcaq_mapper_seg* segs, int nseg,
                                      float min_bits, float max_bits, float temperature, hipStream_t stream);

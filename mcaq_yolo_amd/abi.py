@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libmcaq_hip.so")
-ABI_VERSION = 15
+ABI_VERSION = 17
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -96,6 +96,12 @@ class ReduceSeg(ctypes.Structure):
     _fields_ = [("part", P), ("out", P), ("nparts", I), ("stride", I), ("count", I), ("accumulate", I)]
 
 
+class EmaSeg(ctypes.Structure):
+    """mcaq_ema_seg."""
+    _fields_ = [("batch_min", P), ("batch_max", P), ("running_min", P), ("running_max", P), ("copy_min", P),
+                ("copy_max", P), ("num_batches", P), ("C", I), ("first", I), ("momentum", ctypes.c_double)]
+
+
 # morph stage flags (mcaq_morph.h)
 F_PHI, F_CMLP, F_MAPPER, F_SOFTMASK = 1, 2, 4, 8
 F_CONT, F_HAS_T, F_NORM_C, F_MAP_LINEAR = 16, 32, 64, 128
@@ -114,7 +120,8 @@ EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats",
            "mcaq_mapper_train_forward_stage", "mcaq_mapper_train_backward_stage", "mcaq_mapper_train_reduce",
            "mcaq_mapper_train_grad_reduce", "mcaq_mapper_running_update", "mcaq_head_train_grad_reduce",
            "mcaq_mapper_train_forward_multi", "mcaq_mapper_train_backward_multi", "mcaq_head_train_backward_multi",
-           "mcaq_smask_train_backward_multi", "mcaq_train_reduce_multi")
+           "mcaq_smask_train_backward_multi", "mcaq_train_reduce_multi", "mcaq_ema_stats_multi",
+           "mcaq_mapper_train_forward_stage_multi", "mcaq_mapper_train_backward_stage_multi")
 
 _LIB = None
 
@@ -184,6 +191,13 @@ def _declare(lib):
     lib.mcaq_mapper_train_forward_multi.restype = I
     lib.mcaq_mapper_train_forward_multi.argtypes = [ctypes.POINTER(MapperParams), ctypes.POINTER(MapperSeg), I, Fl, Fl,
                                                     Fl, Fl, I, I, P]
+    lib.mcaq_mapper_train_forward_stage_multi.restype = I
+    lib.mcaq_mapper_train_forward_stage_multi.argtypes = [ctypes.POINTER(MapperParams), ctypes.POINTER(MapperSeg), I,
+                                                          Fl, Fl, Fl, Fl, I, I, I, ctypes.POINTER(P), I, P]
+    lib.mcaq_mapper_train_backward_stage_multi.restype = I
+    lib.mcaq_mapper_train_backward_stage_multi.argtypes = [ctypes.POINTER(MapperParams), ctypes.POINTER(MapperSeg),
+                                                           I, Fl, Fl, Fl, I, ctypes.POINTER(P), ctypes.POINTER(P), I,
+                                                           P]
     lib.mcaq_mapper_train_backward_multi.restype = I
     lib.mcaq_mapper_train_backward_multi.argtypes = [ctypes.POINTER(MapperParams), ctypes.POINTER(MapperSeg), I, Fl,
                                                      Fl, Fl, P]
@@ -191,6 +205,8 @@ def _declare(lib):
     lib.mcaq_head_train_backward_multi.argtypes = [ctypes.POINTER(CmlpParams), ctypes.POINTER(HeadSeg), I, P]
     lib.mcaq_smask_train_backward_multi.restype = I
     lib.mcaq_smask_train_backward_multi.argtypes = [ctypes.POINTER(SmaskSeg), I, P]
+    lib.mcaq_ema_stats_multi.restype = I
+    lib.mcaq_ema_stats_multi.argtypes = [ctypes.POINTER(EmaSeg), I, P]
     lib.mcaq_train_reduce_multi.restype = I
     lib.mcaq_train_reduce_multi.argtypes = [ctypes.POINTER(ReduceSeg), I, I, P]
     lib.mcaq_head_train_backward.restype = I

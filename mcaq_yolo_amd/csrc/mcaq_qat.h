@@ -340,6 +340,30 @@ __global__ __launch_bounds__(256) void mcaq_ema_kernel(const float* bmin, const 
   if (cmax) cmax[c] = hi;
 }
 
+// several EMA updates in one launch: segment of workgroup blockIdx.x by the
+// running workgroup offsets (one per segment, 256 channels per workgroup)
+struct EmaSeg { const float *bmin, *bmax; float *rmin, *rmax, *cmin, *cmax; long long* nbt; int C, first, wg0; float am, cm; };
+struct EmaMulti { EmaSeg s[3]; int nseg; };
+__global__ __launch_bounds__(256) void mcaq_ema_multi_kernel(EmaMulti M) {
+  const int x = (int)blockIdx.x;
+  const EmaSeg& g = (M.nseg > 2 && x >= M.s[2].wg0) ? M.s[2] : ((M.nseg > 1 && x >= M.s[1].wg0) ? M.s[1] : M.s[0]);
+  const int c = (x - g.wg0) * 256 + threadIdx.x;
+  if (c == 0 && g.nbt) g.nbt[0] += 1;
+  if (c >= g.C) return;
+  float lo, hi;
+  if (g.first) {
+    lo = g.bmin[c];
+    hi = g.bmax[c];
+  } else {
+    lo = g.am * g.rmin[c] + g.cm * g.bmin[c];
+    hi = g.am * g.rmax[c] + g.cm * g.bmax[c];
+  }
+  g.rmin[c] = lo;
+  g.rmax[c] = hi;
+  if (g.cmin) g.cmin[c] = lo;
+  if (g.cmax) g.cmax[c] = hi;
+}
+
 }  // namespace mcaq
 
 namespace mcaq {
@@ -424,6 +448,22 @@ int mcaq_ema_stats(const float* batch_min, const float* batch_max, float* runnin
   hipLaunchKernelGGL(mcaq::mcaq_ema_kernel, dim3((C + 255) / 256), dim3(256), 0, stream, batch_min, batch_max,
                      running_min, running_max, C, am, cm, first ? 1 : 0, (float*)nullptr, (float*)nullptr,
                      (long long*)nullptr);
+  return (int)hipGetLastError();
+}
+
+int mcaq_ema_stats_multi(const mcaq_ema_seg* segs, int nseg, hipStream_t stream) {
+  if (!segs || nseg < 1 || nseg > 3) return (int)hipErrorInvalidValue;
+  mcaq::EmaMulti M{};
+  int wg = 0;
+  for (int k = 0; k < nseg; ++k) {
+    const mcaq_ema_seg& e = segs[k];
+    if (e.C < 1 || !e.batch_min || !e.batch_max || !e.running_min || !e.running_max) return (int)hipErrorInvalidValue;
+    M.s[k] = mcaq::EmaSeg{e.batch_min, e.batch_max, e.running_min, e.running_max, e.copy_min, e.copy_max,
+                          reinterpret_cast<long long*>(e.num_batches), e.C, e.first ? 1 : 0, wg, (float)e.momentum, (float)(1.0 - e.momentum)};
+    wg += (e.C + 255) / 256;
+  }
+  M.nseg = nseg;
+  hipLaunchKernelGGL(mcaq::mcaq_ema_multi_kernel, dim3(wg), dim3(256), 0, stream, M);
   return (int)hipGetLastError();
 }
 

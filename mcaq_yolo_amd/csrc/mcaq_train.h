@@ -967,7 +967,21 @@ struct MaskTrainArgs {
   float* gpart;          // [B][SG_SIZE]
   int B, H, W, ht, wt, accumulate;
   int wg0;               // first workgroup of this segment in a multi-segment launch (else 0)
+  int stage;             // 1: |x| mean and m-gradient planes staged in LDS (smask_lds_bytes)
 };
+
+// LDS bytes of the soft-mask backward of one (H, W, ht, wt) image; stage: + the
+// staging plane (16-byte aligned)
+inline size_t smask_lds_bytes(int H, int W, int ht, int wt, bool stage) {
+  const size_t base = ((size_t)20 * ht * wt + 64 + (size_t)H * wt + (size_t)H * W) * sizeof(float) +
+                      (size_t)2 * (ht + wt) * sizeof(int);
+  return stage ? ((base / 4 + 3) & ~(size_t)3) * 4 + (size_t)H * W * sizeof(float) : base;
+}
+// staging applies when it fits and the planes are 16-byte aligned rows of 4
+inline bool smask_stage_ok(const float* absmean, const float* gm, int H, int W, int ht, int wt) {
+  return ((H * W) & 3) == 0 && (((uintptr_t)absmean | (uintptr_t)gm) & 15) == 0 &&
+         smask_lds_bytes(H, W, ht, wt, true) <= 160 * 1024 - 1024;
+}
 
 constexpr int SM_TH = 1024;   // threads per soft-mask backward workgroup (one image)
 
@@ -988,8 +1002,21 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
   int* whi = wlo + wt;
   float* part = (float*)(whi + wt);  // [H][wt] row partials of the upsample adjoint
   float* tv = part + H * wt;         // [H][W] vertical pass of the smoothing adjoint
+  // A.stage: the image's |x| mean plane, then its m(p) gradient plane, are
+  // first copied into LDS ([H][W] after tv) with every load issued at once, so
+  // the per-tile pooling sums and the 5-tap adjoint read LDS instead of
+  // chaining dependent global loads (same values, same order)
+  float* stg = smem_tr + ((int)(tv + H * W - smem_tr) + 3 & ~3);   // 16-byte aligned
   const float* am = A.absmean + (size_t)b * H * W;
   const float* gm = A.gm + (size_t)b * H * W;
+  if (A.stage) {
+    const int n4 = (H * W) >> 2;
+    const float4* s4 = reinterpret_cast<const float4*>(am);
+    for (int e = tid; e < n4; e += SM_TH) reinterpret_cast<float4*>(stg)[e] = s4[e];
+    for (int e = (n4 << 2) + tid; e < H * W; e += SM_TH) stg[e] = am[e];
+    __syncthreads();
+    am = stg;
+  }
   const float sch = (float)ht / (float)H, scw = (float)wt / (float)W;
   // the 5x5 smoothing kernel is the outer product of the 1-D Gaussian
   // (quantization.py:207-209: g1 g1^T): g_d = sqrt(k_dd)
@@ -998,26 +1025,6 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
   for (int d = 0; d < 5; ++d) g1[d] = sqrtf(bits_as_float(k_smooth5_bits[d * 6]));
   for (int i = tid; i < ht; i += SM_TH) { hlo[i] = H; hhi[i] = -1; }
   for (int j = tid; j < wt; j += SM_TH) { wlo[j] = W; whi[j] = -1; }
-  // adjoint of the smoothing (replicate pad), vertical pass:
-  // tv(q, w) = sum_d g_d sum_{p: clamp(p + d - 2) = q} g_m(p, w)
-  for (int e = tid; e < H * W; e += SM_TH) {
-    const int q = e / W, w = e - q * W;
-    float acc = 0.0f;
-    if (q >= 2 && q <= H - 3) {
-#pragma unroll
-      for (int d = 0; d < 5; ++d) acc = fmaf(g1[d], gm[(q - d + 2) * W + w], acc);
-    } else {
-#pragma unroll
-      for (int d = 0; d < 5; ++d) {
-        int p0, p1;
-        tap_range(q, d - 2, H, p0, p1);
-        float r = 0.0f;
-        for (int p = p0; p <= p1; ++p) r += gm[p * W + w];
-        acc = fmaf(g1[d], r, acc);
-      }
-    }
-    tv[e] = acc;
-  }
   __syncthreads();
   // nearest source row / column (floor(o * in / out), clamped) is monotone:
   // every tile's block is a contiguous range
@@ -1055,6 +1062,37 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
   for (int w = 1; w < SM_TH / 64; ++w) amax = fmax_(amax, red[w]);
   const float den = amax + 1e-8f;
   for (int t = tid; t < NT; t += SM_TH) f1[t] = f1[t] / den;
+  if (A.stage) {
+    __syncthreads();   // every pooling read of the staged |x| plane is done
+    const int n4 = (H * W) >> 2;
+    const float4* s4 = reinterpret_cast<const float4*>(gm);
+    for (int e = tid; e < n4; e += SM_TH) reinterpret_cast<float4*>(stg)[e] = s4[e];
+    for (int e = (n4 << 2) + tid; e < H * W; e += SM_TH) stg[e] = gm[e];
+    __syncthreads();
+    gm = stg;
+  }
+  // adjoint of the smoothing (replicate pad), vertical pass:
+  // tv(q, w) = sum_d g_d sum_{p: clamp(p + d - 2) = q} g_m(p, w)
+  for (int e = tid; e < H * W; e += SM_TH) {
+    const int q = e / W, w = e - q * W;
+    float acc = 0.0f;
+    if (q >= 2 && q <= H - 3) {
+#pragma unroll
+      for (int d = 0; d < 5; ++d) acc = fmaf(g1[d], gm[(q - d + 2) * W + w], acc);
+    } else {
+#pragma unroll
+      for (int d = 0; d < 5; ++d) {
+        int p0, p1;
+        tap_range(q, d - 2, H, p0, p1);
+        float r = 0.0f;
+        for (int p = p0; p <= p1; ++p) r += gm[p * W + w];
+        acc = fmaf(g1[d], r, acc);
+      }
+    }
+    tv[e] = acc;
+  }
+  __syncthreads();
+
   // horizontal pass + the nearest-upsample adjoint: one item = one row of one
   // tile column's block, summed into part[h][j]
   for (int it = tid; it < H * wt; it += SM_TH) {
@@ -1456,6 +1494,70 @@ int mcaq_mapper_train_forward_multi(const mcaq_mapper_params* P, const mcaq_mapp
   return (int)hipGetLastError();
 }
 
+int mcaq_mapper_train_forward_stage_multi(const mcaq_mapper_params* P, const mcaq_mapper_seg* segs, int nseg,
+                                          float min_bits, float max_bits, float temperature, float momentum,
+                                          int round_bits, int update_stats, int stage, const float* const* gathered,
+                                          int world, hipStream_t stream) {
+  using namespace mcaq;
+  if (!P || !segs || nseg < 1 || nseg > TR_MAXSEG || (nseg > 1 && update_stats == 1) || stage < 1 || stage > 4 ||
+      world < 1 || (stage >= 2 && !gathered))
+    return (int)hipErrorInvalidValue;
+  TrMulti<MapperTrainArgs> M{};
+  int wg = 0;
+  for (int k = 0; k < nseg; ++k) {
+    const mcaq_mapper_seg& g = segs[k];
+    if (!g.c || !g.bits || !g.work || g.n < 1 || (stage >= 2 && !gathered[k])) return (int)hipErrorInvalidValue;
+    MapperTrainArgs& A = M.s[k];
+    A.P = *P; A.c = g.c; A.bits = g.bits; A.work = g.work; A.n = g.n; A.nwg = (g.n + TR_TPB - 1) / TR_TPB;
+    A.min_bits = min_bits; A.max_bits = max_bits; A.temperature = temperature; A.momentum = momentum;
+    A.round_bits = round_bits; A.update_stats = update_stats; A.wg0 = wg;
+    A.gstat = stage >= 2 ? gathered[k] : nullptr; A.gworld = stage >= 2 ? world : 0;
+    wg += A.nwg;
+  }
+  M.nseg = nseg;
+  const dim3 g(wg), t(MTH);
+  switch (stage) {
+    case 1: hipLaunchKernelGGL(mcaq_mapper_fwd_multi_kernel<1>, g, t, 0, stream, M); break;
+    case 2: hipLaunchKernelGGL(mcaq_mapper_fwd_multi_kernel<2>, g, t, 0, stream, M); break;
+    case 3: hipLaunchKernelGGL(mcaq_mapper_fwd_multi_kernel<3>, g, t, 0, stream, M); break;
+    default: hipLaunchKernelGGL(mcaq_mapper_fwd_multi_kernel<4>, g, t, 0, stream, M); break;
+  }
+  return (int)hipGetLastError();
+}
+
+int mcaq_mapper_train_backward_stage_multi(const mcaq_mapper_params* P, const mcaq_mapper_seg* segs, int nseg,
+                                           float min_bits, float max_bits, float temperature, int stage,
+                                           const float* const* gsums, const float* const* gathered1, int world,
+                                           hipStream_t stream) {
+  using namespace mcaq;
+  if (!P || !segs || nseg < 1 || nseg > TR_MAXSEG || stage < 1 || stage > 4 || world < 1 ||
+      (stage <= 3 && (!gsums || !gathered1)))
+    return (int)hipErrorInvalidValue;
+  TrMulti<MapperTrainArgs> M{};
+  int wg = 0;
+  for (int k = 0; k < nseg; ++k) {
+    const mcaq_mapper_seg& g = segs[k];
+    if (!g.c || !g.gbits || !g.gc || !g.gpart || !g.work || g.n < 1 || (stage <= 3 && (!gsums[k] || !gathered1[k])))
+      return (int)hipErrorInvalidValue;
+    MapperTrainArgs& A = M.s[k];
+    A.P = *P; A.c = g.c; A.gbits = g.gbits; A.gc = g.gc; A.work = g.work; A.gpart = g.gpart; A.n = g.n;
+    A.nwg = (g.n + TR_TPB - 1) / TR_TPB;
+    A.min_bits = min_bits; A.max_bits = max_bits; A.temperature = temperature; A.wg0 = wg;
+    A.gbsum = stage <= 3 ? gsums[k] : nullptr; A.gstat1 = stage <= 3 ? gathered1[k] : nullptr;
+    A.gworld = stage <= 3 ? world : 0;
+    wg += A.nwg;
+  }
+  M.nseg = nseg;
+  const dim3 g(wg), t(MTH);
+  switch (stage) {
+    case 4: hipLaunchKernelGGL(mcaq_mapper_bwd_multi_kernel<4>, g, t, 0, stream, M); break;
+    case 3: hipLaunchKernelGGL(mcaq_mapper_bwd_multi_kernel<3>, g, t, 0, stream, M); break;
+    case 2: hipLaunchKernelGGL(mcaq_mapper_bwd_multi_kernel<2>, g, t, 0, stream, M); break;
+    default: hipLaunchKernelGGL(mcaq_mapper_bwd_multi_kernel<1>, g, t, 0, stream, M); break;
+  }
+  return (int)hipGetLastError();
+}
+
 int mcaq_mapper_train_backward_multi(const mcaq_mapper_params* P, const mcaq_mapper_seg* segs, int nseg,
                                      float min_bits, float max_bits, float temperature, hipStream_t stream) {
   using namespace mcaq;
@@ -1530,10 +1632,9 @@ int mcaq_smask_train_backward_multi(const mcaq_smask_seg* segs, int nseg, hipStr
     MaskTrainArgs& A = M.s[k];
     A.P = g.P; A.bits = g.bits; A.absmean = g.absmean; A.gm = g.gm; A.gbits = g.gbits; A.gpart = g.gpart;
     A.B = g.B; A.H = g.H; A.W = g.W; A.ht = g.ht; A.wt = g.wt; A.accumulate = g.accumulate; A.wg0 = wg;
+    A.stage = smask_stage_ok(g.absmean, g.gm, g.H, g.W, g.ht, g.wt) ? 1 : 0;
     wg += g.B;
-    const int NT = g.ht * g.wt;
-    const size_t l = ((size_t)20 * NT + 64 + (size_t)g.H * g.wt + (size_t)g.H * g.W) * sizeof(float) +
-                     (size_t)2 * (g.ht + g.wt) * sizeof(int);
+    const size_t l = smask_lds_bytes(g.H, g.W, g.ht, g.wt, A.stage != 0);
     if (l > 160 * 1024 - 1024) return (int)hipErrorInvalidValue;
     lb = l > lb ? l : lb;
   }
@@ -1604,9 +1705,8 @@ int mcaq_smask_train_backward(const mcaq_smask_params* P, const float* bits, con
   MaskTrainArgs A{};
   A.P = *P; A.bits = bits; A.absmean = absmean; A.gm = gm; A.gbits = gbits; A.gpart = gpart;
   A.B = B; A.H = H; A.W = W; A.ht = ht; A.wt = wt; A.accumulate = accumulate;
-  const int NT = ht * wt;
-  const size_t lb = ((size_t)20 * NT + 64 + (size_t)H * wt + (size_t)H * W) * sizeof(float) +   // + tv
-                    (size_t)2 * (ht + wt) * sizeof(int);
+  A.stage = smask_stage_ok(absmean, gm, H, W, ht, wt) ? 1 : 0;
+  const size_t lb = smask_lds_bytes(H, W, ht, wt, A.stage != 0);
   if (lb > 160 * 1024 - 1024) return (int)hipErrorInvalidValue;   // m(p) gradient of one image staged in LDS
   static int set = 0;
   if ((int)lb > set) {

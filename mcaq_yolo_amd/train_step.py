@@ -31,6 +31,101 @@ def _cmlp_params(an):
     return list(an.complexity_mlp.parameters())
 
 
+_SM_BLOBS = {"key": None, "blobs": None}
+
+
+def _softmask_blobs(mods):
+    """The soft-mask blobs of every scale's quantizer (core._pack_softmask
+    layout, each padded to a 16-byte multiple) packed by ONE mcaq_pack launch
+    into one buffer; re-packed when a parameter changed (version counters)
+    and always under HIP-graph capture, as core._BlobCache."""
+    ps = [p for m in mods for p in m.net.parameters()]
+    if not all(p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() for p in ps) or \
+            len(ps) > abi.MCAQ_PACK_MAXSEG or any(sum(p.numel() for p in m.net.parameters()) != core._SM_SIZE
+                                                  for m in mods):
+        return [m.blob() for m in mods]
+    key = tuple((p.data_ptr(), p._version) for p in ps)
+    capturing = torch.cuda.is_current_stream_capturing()
+    if capturing or key != _SM_BLOBS["key"]:
+        stride = (core._SM_SIZE + 3) // 4 * 4
+        segs = (abi.PackSeg * len(ps))()
+        k = 0
+        for i, m in enumerate(mods):
+            o = i * stride
+            for p in m.net.parameters():
+                segs[k].src, segs[k].n, segs[k].k, segs[k].mode, segs[k].dst = _p(p.detach()), p.numel(), 1, 0, o
+                o += p.numel()
+                k += 1
+        out = torch.empty(len(mods) * stride, device=ps[0].device)
+        abi.check(abi.lib().mcaq_pack(segs, len(ps), _p(out), out.numel(), _stream()), "mcaq_pack")
+        _SM_BLOBS["blobs"] = [out[i * stride:(i + 1) * stride] for i in range(len(mods))]
+        _SM_BLOBS["key"] = None if capturing else key
+    return _SM_BLOBS["blobs"]
+
+
+def _ema_multi_ok(qs, xs):
+    """Every quantizer in the state the one-launch EMA covers: per-channel
+    running statistics that exist (fp32, contiguous, on the device, C
+    entries), not frozen, unsharded, num_batches_tracked an int64 scalar on
+    the device; otherwise each quantizer runs update_running_stats."""
+    if len({id(q.process_group) for q in qs}) != 1:
+        return False
+    for q, x in zip(qs, xs):
+        if not q.per_channel or q._frozen() or q.running_min is None:
+            return False
+        C = x.shape[1]
+        for t in (q.running_min, q.running_max):
+            if t.dtype != torch.float32 or not t.is_contiguous() or t.device != x.device or t.numel() != C:
+                return False
+        nbt = q.num_batches_tracked
+        if nbt.device != x.device or nbt.dtype != torch.int64 or nbt.numel() != 1:
+            return False
+    return True
+
+
+def _ema_multi(qs, xs, box):
+    """quantization.py:319-353 for every scale's quantizer: the batch min /
+    max from the analyzer's pass-1 partials (one finalize launch for all
+    scales), then the EMA, this step's copies and num_batches_tracked (one
+    launch): the values of q.update_running_stats(x, want_copies=True)."""
+    L = abi.lib()
+    n = len(qs)
+    fz = (abi.FinalizeScale * n)()
+    segs = (abi.EmaSeg * n)()
+    mins, maxs, keep = [], [], []
+    for i, (q, x) in enumerate(zip(qs, xs)):
+        C = x.shape[1]
+        bmin, bmax = torch.empty(C, device=x.device), torch.empty(C, device=x.device)
+        cmin, cmax = torch.empty(C, device=x.device), torch.empty(C, device=x.device)
+        keep += [bmin, bmax]
+        f = fz[i]
+        f.pmin, f.pmax, f.min_out, f.max_out = _p(box[i]["pmin"]), _p(box[i]["pmax"]), _p(bmin), _p(bmax)
+        f.C, f.nunits, f.min_stride = C, box[i]["pmin"].shape[0], 1
+        e = segs[i]
+        e.batch_min, e.batch_max = _p(bmin), _p(bmax)
+        e.running_min, e.running_max = _p(q.running_min), _p(q.running_max)
+        e.copy_min, e.copy_max, e.num_batches = _p(cmin), _p(cmax), _p(q.num_batches_tracked)
+        e.C, e.first, e.momentum = C, 0, float(q.momentum)
+        mins.append(cmin); maxs.append(cmax)
+    abi.check(L.mcaq_finalize(fz, n, _stream()), "mcaq_finalize")
+    pg = qs[0].process_group
+    if pg is not None:
+        # data-parallel QAT: every scale's batch min / max over the global
+        # batch in ONE all-reduce (MAX over [-min, max]; per quantizer the
+        # values of update_running_stats' own all-reduce)
+        import torch.distributed as dist
+        vec = torch.cat([t for i in range(n) for t in (-keep[2 * i], keep[2 * i + 1])])
+        dist.all_reduce(vec, op=dist.ReduceOp.MAX, group=pg)
+        o = 0
+        for i, x in enumerate(xs):
+            C = x.shape[1]
+            keep[2 * i].copy_(-vec[o:o + C])
+            keep[2 * i + 1].copy_(vec[o + C:o + 2 * C])
+            o += 2 * C
+    abi.check(L.mcaq_ema_stats_multi(segs, n, _stream()), "mcaq_ema_stats_multi")
+    return mins, maxs
+
+
 def _run_analyzer_multi(an, xs):
     """Pass 1 (gray, |x| means, channel min/max partials) and the morphology
     (phi, complexity MLP, bilateral -> C) of every scale: 2 launches of
@@ -159,9 +254,31 @@ class _MapperMulti(torch.autograd.Function):
             cfs.append(cf); works.append(w); bits.append(b)
             segs[i].c, segs[i].bits, segs[i].work, segs[i].n = _p(cf), _p(b), _p(w), m
         mom = float(bns[0].momentum)
-        abi.check(L.mcaq_mapper_train_forward_multi(ctypes.byref(q), segs, n, mod.min_bits, mod.max_bits, T, mom,
-                                                    0 if return_continuous else 1, 2, _stream()),
-                  "mcaq_mapper_train_forward_multi")
+        pg = core._mapper_group(net)
+        ctx.pg, ctx.gath1, ctx.world = pg, None, 1
+        if pg is None:
+            abi.check(L.mcaq_mapper_train_forward_multi(ctypes.byref(q), segs, n, mod.min_bits, mod.max_bits, T,
+                                                        mom, 0 if return_continuous else 1, 2, _stream()),
+                      "mcaq_mapper_train_forward_multi")
+        else:
+            # batch sharded (GroupBatchNorm1d): between the stage launches every
+            # scale's (mean, M2, n) of this rank, all-gathered in ONE collective
+            import torch.distributed as dist
+            world = dist.get_world_size(pg)
+            gath = [None] * 4
+            for st in (1, 2, 3, 4):
+                gp = (abi.P * n)(*[_p(t) for t in gath[st - 1]]) if st >= 2 else None
+                abi.check(L.mcaq_mapper_train_forward_stage_multi(
+                    ctypes.byref(q), segs, n, mod.min_bits, mod.max_bits, T, mom, 0 if return_continuous else 1, 2,
+                    st, gp, world, _stream()), "mcaq_mapper_train_forward_stage_multi")
+                if st <= 3:
+                    rk = torch.empty(n, core._RANK_ENT, device=dev)
+                    for i in range(n):
+                        abi.check(L.mcaq_mapper_train_reduce(_p(works[i]), cfs[i].numel(), 0, st, _p(rk[i]), _stream()),
+                                  "mcaq_mapper_train_reduce")
+                    g_all = core._all_gather_flat(rk.reshape(-1), pg, world)
+                    gath[st] = list(g_all.view(world, n, core._RANK_ENT).transpose(0, 1).contiguous())
+            ctx.gath1, ctx.world = gath[1], world
         wa = (abi.P * n)(*[_p(w) for w in works])
         na = (abi.I * n)(*[c.numel() for c in cfs])
         abi.check(L.mcaq_mapper_running_update(ctypes.byref(q), wa, na, n, mom, _stream()),
@@ -190,8 +307,28 @@ class _MapperMulti(torch.autograd.Function):
             gparts.append((gp, (m + 63) // 64))
             s = segs[i]
             s.c, s.work, s.gbits, s.gc, s.gpart, s.n = _p(cfs[i]), _p(works[i]), _p(g), _p(gc), _p(gp), m
-        abi.check(L.mcaq_mapper_train_backward_multi(ctypes.byref(ctx.q), segs, n, mod.min_bits, mod.max_bits, ctx.T,
-                                                     _stream()), "mcaq_mapper_train_backward_multi")
+        if ctx.pg is None:
+            abi.check(L.mcaq_mapper_train_backward_multi(ctypes.byref(ctx.q), segs, n, mod.min_bits, mod.max_bits,
+                                                         ctx.T, _stream()), "mcaq_mapper_train_backward_multi")
+        else:
+            # BN backward sums (S1, S2) of every scale all-reduced in ONE
+            # collective before the stage that consumes them; parameter
+            # gradients stay this rank's own (for the gradient all-reduce)
+            import torch.distributed as dist
+            gs = [None] * 5
+            g1p = (abi.P * n)(*[_p(t) for t in ctx.gath1])
+            for st in (4, 3, 2, 1):
+                gsp = (abi.P * n)(*[_p(t) for t in gs[st]]) if st <= 3 else None
+                abi.check(L.mcaq_mapper_train_backward_stage_multi(
+                    ctypes.byref(ctx.q), segs, n, mod.min_bits, mod.max_bits, ctx.T, st, gsp,
+                    g1p if st <= 3 else None, ctx.world, _stream()), "mcaq_mapper_train_backward_stage_multi")
+                if st >= 2:
+                    bs = torch.empty(n, 128, device=dev)
+                    for i in range(n):
+                        abi.check(L.mcaq_mapper_train_reduce(_p(works[i]), cfs[i].numel(), 1, st - 1, _p(bs[i]),
+                                                             _stream()), "mcaq_mapper_train_reduce")
+                    dist.all_reduce(bs, group=ctx.pg)
+                    gs[st - 1] = list(bs)
         sink = mod._gsink.target(list(mod.mapping_network.parameters()))
         gflat, acc = sink if sink is not None else (torch.empty(core._MAPPER_G_SIZE, device=dev), 0)
         _reduce_chain(gparts, gflat, acc, core._MAPPER_G_SIZE)
@@ -209,6 +346,7 @@ class _SoftMaskMulti(torch.autograd.Function):
         L = abi.lib()
         morphs = (abi.MorphScale * n)()
         ms = []
+        blobs = _softmask_blobs(mods)
         for i in range(n):
             b = _f32c(bits[i]).detach()
             B, H, W = absmeans[i].shape
@@ -218,7 +356,7 @@ class _SoftMaskMulti(torch.autograd.Function):
             m = torch.empty(B, 1, H, W, device=b.device)
             ms.append(m)
             morphs[i] = core._morph_struct(B, H, W, 4, ht, wt, abi.F_SOFTMASK, absmean=absmeans[i], bits_in=b,
-                                           smask=mods[i].blob(), m_out=m)
+                                           smask=blobs[i], m_out=m)
         abi.check(L.mcaq_morph(morphs, n, _stream()), "mcaq_morph(soft mask)")
         ctx.mods, ctx.n = mods, n
         ctx.save_for_backward(*bits, *absmeans)
@@ -323,14 +461,21 @@ def multi_ok(hooks, feats):
         return False
     if len({f.device for f in feats}) != 1 or len(feats) > abi.MCAQ_TRAIN_MAXSEG:
         return False
-    if hooks.process_group is not None or any(q.process_group is not None for q in hooks.quantizers.values()):
+    # data parallel: every quantizer and the mapper's BatchNorm over ONE group
+    pgs = {id(q.process_group) for q in hooks.quantizers.values()}
+    if len(pgs) != 1:
         return False
+    qpg = next(iter(hooks.quantizers.values())).process_group
     an = hooks.complexity_analyzer
     if any(not core._head_bwd_fits(*core._tile_grid(f.shape[2], f.shape[3], an.grid_size)) for f in feats):
         return False
     if isinstance(hooks.bit_mapper, core.ComplexityToBitMappingNetwork):
-        if not hooks.bit_mapper._fusable() or core._mapper_group(hooks.bit_mapper.mapping_network) is not None:
+        if not hooks.bit_mapper._fusable():
             return False
+        if getattr(hooks.bit_mapper.mapping_network[1], "process_group", None) is not qpg:
+            return False
+    elif qpg is not None:
+        return False
     for idx, f in zip(hooks.backbone_out_indices, feats):
         q = hooks.quantizers[str(idx)]
         if q.smooth_transitions and q.soft_mask is not None:
@@ -371,10 +516,14 @@ def forward_features(hooks, feats, state):
         return list(feats)
     qs = [hooks.quantizers[str(i)] for i in idxs]
     mins, maxs = [], []
-    for i, (q, x) in enumerate(zip(qs, xs)):
+    for i, x in enumerate(xs):
+        if bits[i].dim() != 3 or bits[i].shape[0] != x.shape[0]:
+            raise AssertionError(f"Batch size mismatch: {x.shape[0]} vs {bits[i].shape[0]}")
+    per_quantizer = not _ema_multi_ok(qs, xs)
+    if not per_quantizer:
+        mins, maxs = _ema_multi(qs, xs, box)
+    for i, (q, x) in enumerate(zip(qs, xs) if per_quantizer else ()):
         B, C, H, W = x.shape
-        if bits[i].dim() != 3 or bits[i].shape[0] != B:
-            raise AssertionError(f"Batch size mismatch: {B} vs {bits[i].shape[0]}")
         p1 = box[i]
         copies = None
         frozen = q._frozen()

@@ -13,9 +13,13 @@ DEPS = [SRC] + [os.path.join(HERE, "..", "..", "mcaq_yolo_amd", "csrc", f)
 def build(force=False):
     if not force and os.path.exists(LIB) and all(os.path.getmtime(LIB) >= os.path.getmtime(d) for d in DEPS):
         return LIB
+    # private output, then an atomic rename: parallel test workers that find
+    # the library stale each build their own copy and never load a partial file
+    tmp = "%s.%d.tmp" % (LIB, os.getpid())
     cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
-           "-o", LIB, SRC, "-lm"]
+           "-o", tmp, SRC, "-lm"]
     subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
     return LIB
 
 

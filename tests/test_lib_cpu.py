@@ -35,7 +35,7 @@ def test_struct_layouts_match_header():
                       ("mcaq_morph_scale", abi.MorphScale), ("mcaq_quant_scale", abi.QuantScale),
                       ("mcaq_qat_scale", abi.QatScale), ("mcaq_mapper_seg", abi.MapperSeg),
                       ("mcaq_head_seg", abi.HeadSeg), ("mcaq_smask_seg", abi.SmaskSeg),
-                      ("mcaq_reduce_seg", abi.ReduceSeg)):
+                      ("mcaq_reduce_seg", abi.ReduceSeg), ("mcaq_ema_seg", abi.EmaSeg)):
         body = re.search(r"typedef struct \{([^{}]*)\} %s;" % cname, src).group(1)
         body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
         fields = []
