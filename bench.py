@@ -127,7 +127,7 @@ def main_qat(args, world, rank, dev, pg):
     mask, fractional-bit quantizer forward; backward from the upstream feature
     gradients the YOLOv8 neck would return (synthetic, fixed), straight-through
     into the backbone features and into the hook parameters; gradient
-    all-reduce (N > 1), clip 1.0, SGD step, |W| projection (train.py:615-641)."""
+    all-reduce (N > 1), clip 1.0, AdamW step, |W| projection (train.py:615-641)."""
     from mcaq_yolo_amd import abi, core
     from mcaq_yolo_amd.hooks import MCAQHooks
     name, B, chans, grid, mapper = QAT_CONFIG
@@ -144,17 +144,33 @@ def main_qat(args, world, rank, dev, pg):
     gen = torch.Generator(device="cpu").manual_seed(77 + rank)
     G = [(1e-3 * torch.randn(f.shape, generator=gen)).to(dev) for f in feats]
     params_ = [p for p in h.parameters() if p.requires_grad]
-    opt = torch.optim.SGD(params_, lr=1e-3, momentum=0.9)
+    # the reference's optimizer (train.py:140-150: AdamW, lr 1e-3, weight decay
+    # 0.05, betas 0.9 / 0.999) as torch's fused multi-tensor kernel, capturable
+    # (its step counters on the device) so the whole step replays as a graph
+    try:
+        opt = torch.optim.AdamW(params_, lr=1e-3, weight_decay=0.05, betas=(0.9, 0.999), fused=True,
+                                capturable=True)
+        opt_kind = "AdamW (fused, capturable)"
+    except (RuntimeError, TypeError, ValueError):
+        opt = torch.optim.AdamW(params_, lr=1e-3, weight_decay=0.05, betas=(0.9, 0.999), foreach=True,
+                                capturable=True)
+        opt_kind = "AdamW (foreach, capturable)"
     target_bits = 4.0
 
     # how the train-mode mapper ran (fused kernels, or the torch autograd path)
+    from mcaq_yolo_amd import train_step
     fused = {"calls": 0}
-    orig_apply = core._MapperTrainFn.apply
+    orig_apply, orig_multi = core._MapperTrainFn.apply, train_step._MapperMulti.apply
 
     def counted(*a, **k):
         fused["calls"] += 1
         return orig_apply(*a, **k)
+
+    def counted_multi(*a, **k):          # one call for every hook scale
+        fused["calls"] += a[3]
+        return orig_multi(*a, **k)
     core._MapperTrainFn.apply = counted
+    train_step._MapperMulti.apply = counted_multi
 
     def step():
         opt.zero_grad(set_to_none=True)
@@ -171,7 +187,7 @@ def main_qat(args, world, rank, dev, pg):
         h.bit_mapper.enforce_weight_constraints()
 
     # warm up on a side stream (lazy state: running stats, momentum buffers),
-    # then (N = 1) capture the whole step - forward, backward, clip, SGD,
+    # then (N = 1) capture the whole step - forward, backward, clip, AdamW,
     # projection - as one HIP graph: ~300 small launches replayed at once
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
@@ -255,6 +271,7 @@ def main_qat(args, world, rank, dev, pg):
     torch.cuda.synchronize()
     step_s = (time.perf_counter() - t0) / args.steps
     core._MapperTrainFn.apply = orig_apply
+    train_step._MapperMulti.apply = orig_multi
     # one step alone (device idle before it): its latency, and how long the
     # host takes to issue it
     torch.cuda.synchronize()
@@ -293,7 +310,8 @@ def main_qat(args, world, rank, dev, pg):
                                    "continuous bits, STE, stage-3 temperature 1); YOLOv8 network excluded"
                                    % (name, B, grid, mapper),
                        "global_batch": world * B, "parallelism": "dp%d" % world, "hip_graph": use_graph,
-                       "scales": _qat_scales_mode(pg),
+                       "scales": _qat_scales_mode(h, feats),
+                       "optimizer": opt_kind + ", clip_grad_norm 1.0, |W| projection (train.py:626-641)",
                        "host_enqueue_us_per_step": round(t_enq / args.steps * 1e6, 1),
                        "single_step_latency_us": round(t_one * 1e6, 1),
                        "single_step_enqueue_us": round(t_one_enq * 1e6, 1)},
@@ -523,11 +541,13 @@ def cpu_baseline(cfg_id, budget_s=10.0):
                       % (n, B, name, "x".join(map(str, chans)), grid, mapper, torch.get_num_threads(), dt)}
 
 
-def _qat_scales_mode(pg):
+def _qat_scales_mode(h, feats):
+    """How MCAQHooks.forward_features runs this train step (the order it tries)."""
+    from mcaq_yolo_amd import train_step
     hk = _hooks_mod()
-    if pg is None and hk.MULTI_SCALE_TRAIN:
+    if hk.MULTI_SCALE_TRAIN and train_step.multi_ok(h, feats):
         return "multi-segment launches (one per stage for all scales, one stream)"
-    if pg is None and hk.CONCURRENT_TRAIN_SCALES:
+    if hk.CONCURRENT_TRAIN_SCALES and h._concurrent_ok(feats):
         return "per-scale modules on concurrent streams"
     return "per-scale modules, one stream"
 
