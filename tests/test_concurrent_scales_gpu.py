@@ -27,14 +27,24 @@ def _feats(B=4, seed=5, shapes=((64, 80), (128, 40), (256, 20))):
     return feats, gens
 
 
-def _run(concurrent, steps=3, graph=False, mapper="mlp", multi=False):
+def _run(concurrent, steps=3, graph=False, mapper="mlp", multi=False, variant=None):
     """concurrent / multi select the train path (hooks.CONCURRENT_TRAIN_SCALES,
-    hooks.MULTI_SCALE_TRAIN); both False: per-scale modules on one stream."""
+    hooks.MULTI_SCALE_TRAIN); both False: per-scale modules on one stream.
+    variant: None, "normalize" (normalize_complexity), "per_tensor" (every
+    quantizer per_channel=False) or "no_mask" (the C4 quantizer without
+    smooth transitions)."""
     from mcaq_yolo_amd import hooks
     old = hooks.CONCURRENT_TRAIN_SCALES, hooks.MULTI_SCALE_TRAIN
     hooks.CONCURRENT_TRAIN_SCALES, hooks.MULTI_SCALE_TRAIN = concurrent, multi
     try:
         h = _hooks(mapper)
+        if variant == "normalize":
+            h.normalize_complexity = True
+        elif variant == "per_tensor":
+            for q in h.quantizers.values():
+                q.per_channel = False
+        elif variant == "no_mask":
+            h.quantizers["6"].smooth_transitions = False
         feats, gens = _feats()
         params = [p for p in h.parameters() if p.requires_grad]
         opt = torch.optim.SGD(params, lr=1e-2, momentum=0.9)

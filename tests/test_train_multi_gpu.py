@@ -20,6 +20,15 @@ def test_multi_scale_step_equals_per_scale_eager(mapper):
     _same(_run(False, mapper=mapper, multi=True), _run(False, mapper=mapper))
 
 
+@pytest.mark.parametrize("variant", ["normalize", "per_tensor", "no_mask"])
+def test_multi_scale_step_equals_per_scale_variants(variant):
+    """The module options the multi-segment step keeps per-scale pieces for:
+    normalize_complexity (torch quantile ops between analyzer and mapper),
+    per-tensor quantizers (their EMA per quantizer), a quantizer without the
+    soft mask (its QAT segment without m)."""
+    _same(_run(False, multi=True, variant=variant), _run(False, variant=variant))
+
+
 def test_multi_scale_step_equals_per_scale_graph():
     _same(_run(False, steps=3, graph=True, multi=True), _run(False, steps=4))
 
