@@ -21,6 +21,7 @@
 //   quantization.py:213-239 (LearnedSoftMask),
 //   models/mcaq_yolo.py:426-442 (hook: analyzer -> normalize -> mapper).
 #pragma once
+#include <utility>
 #include "../../include/mcaq_hip.h"
 #include "mcaq_math.h"
 #include "mcaq_tables.h"
@@ -114,9 +115,13 @@ struct Ctx { int tid, nthr; };
 #if defined(__HIP_DEVICE_COMPILE__)
 #define MSYNC() __syncthreads()
 #define MATOMIC_ADD(p, v) atomicAdd((p), (v))
+#define MATOMIC_FETCH_ADD(p, v) atomicAdd((p), (v))
+#define MATOMIC_OR(p, v) atomicOr((p), (v))
 #else
 #define MSYNC() do {} while (0)
 #define MATOMIC_ADD(p, v) (*(p) += (v))
+#define MATOMIC_FETCH_ADD(p, v) ((*(p) += (v)) - (v))
+#define MATOMIC_OR(p, v) (*(p) |= (v))
 #endif
 #define MFOR(i, n) for (int i = ctx.tid; i < (n); i += ctx.nthr)
 
@@ -612,6 +617,17 @@ MCAQ_HD float exact_g11(const float* G, int Hc, int Wc, int h, int w) {
   return acc;
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// acc = fma(k[O + i], tap O + i, acc) for i = 0, 1, ..., tap O + i in lane i
+// of v: exact_g11's FMA order with every weight an immediate (I are
+// compile-time indices)
+template <int... I, int O>
+__device__ __forceinline__ void g11_chain(float& acc, float v, std::integer_sequence<int, I...>,
+                                          std::integral_constant<int, O>) {
+  ((acc = fmaf(bits_as_float(k_gauss11_bits[O + I]), __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), I)), acc)), ...);
+}
+#endif
+
 // row_field without a branch around the second word (loads issue together)
 MCAQ_HD uint32_t row_field_bf(const uint32_t* row, int x0, int n, int WPR) {
   const int k = x0 >> 5, sft = x0 & 31;
@@ -910,7 +926,9 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, P
             for (int j = 0; j < 5; ++j) acc = fmaf(bits_as_float(k_gauss5_bits[i * 5 + j]), v[r + i][j], acc);
           if (r0 + r < Hc) {
             pl.A[(r0 + r) * Wc + w] = acc;
+#ifndef MCAQ_PROBE_NO_HIST   // timing probe only (wrong Otsu threshold)
             if (!legacy) otsu_hist_add(sh, acc);
+#endif
           }
         }
       }
@@ -1023,6 +1041,13 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, P
       // g255 = G * 255 is recomputed where read (same rounding as a stored plane).
       float* rowp = pl.Bf;    // horizontal 11-tap pass, column strips, loads issued together
       const int nsr = (Hc + SR - 1) / SR;
+      // pixels within the margin are listed (in the blur plane A, free in
+      // this role until the Sobel stage) and get their exact sums after the
+      // vertical pass, one pixel per thread, instead of a divergent 121-tap
+      // chain inside each wave that meets one
+      int* xlist = reinterpret_cast<int*>(pl.A);
+      int* nx = sh.flags + 9;
+      if (ctx.tid == 0) *nx = 0;
       MFOR2(st, w, nsr, Wc) {
         const int r0 = st * SR;
         float v[SR][11];
@@ -1041,6 +1066,7 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, P
         }
       }
       MSYNC();
+      MSTAMP(2);
       const float marg = bits_as_float(k_g11_margin_bits[0]);
       MFOR2(st, sl, nsr, RS) {   // vertical pass: column strips of SR rows, word-aligned lanes
         const int k = sl >> 5, bit = sl & 31, w = sl;
@@ -1061,16 +1087,48 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, P
             for (int i = 0; i < 11; ++i) m = fmaf(bits_as_float(k_g11_sep_bits[i]), v[r + i], m);
             const float g = pl.G[h * Wc + w] * 255.0f;
             const float t = m - 2.0f;
+#ifdef MCAQ_PROBE_NO_EXACT_G11   // timing probe only (separable estimate everywhere)
+            if (true) {
+#else
             if (fabsf(g - t) > marg) {
+#endif
               on[r] = g > t;
             } else {
-              on[r] = g > exact_g11(pl.G, Hc, Wc, h, w) - 2.0f;
+              xlist[MATOMIC_FETCH_ADD(nx, 1)] = h * Wc + w;   // decided below
             }
           }
         }
 #pragma unroll
         for (int r = 0; r < SR; ++r) if (r0 + r < Hc) put_bits(BIN, (r0 + r) * WPR + k, bit, on[r]);
       }
+      MSYNC();
+      MSTAMP(3);
+      const int nxs = *nx;
+#if defined(__HIP_DEVICE_COMPILE__)
+      // one wave per listed pixel: its lanes load the 121 taps at once (lane
+      // l: taps l and l + 64), then the FMA chain of exact_g11 runs in that
+      // order on the taps read back lane by lane (a single-lane chain waits
+      // on 11 LDS round trips: ~5.5 k cycles per pixel, stage stamps)
+      {
+        const int lane = ctx.tid & 63;
+        for (int i = ctx.tid >> 6; i < nxs; i += ctx.nthr >> 6) {
+          const int p = xlist[i], h = p / Wc, w = p - (p / Wc) * Wc;
+          const int ta = lane, tb = imin_(lane + 64, 120);
+          const int ia = ta / 11, ib = tb / 11;
+          const float va = pl.G[imin_(imax_(h + ia - 5, 0), Hc - 1) * Wc + imin_(imax_(w + (ta - 11 * ia) - 5, 0), Wc - 1)] * 255.0f;
+          const float vb = pl.G[imin_(imax_(h + ib - 5, 0), Hc - 1) * Wc + imin_(imax_(w + (tb - 11 * ib) - 5, 0), Wc - 1)] * 255.0f;
+          float acc = 0.0f;
+          g11_chain(acc, va, std::make_integer_sequence<int, 64>{}, std::integral_constant<int, 0>{});
+          g11_chain(acc, vb, std::make_integer_sequence<int, 57>{}, std::integral_constant<int, 64>{});
+          if (lane == 0 && pl.G[p] * 255.0f > acc - 2.0f) MATOMIC_OR(&BIN[h * WPR + (w >> 5)], 1u << (w & 31));
+        }
+      }
+#else
+      MFOR(i, nxs) {
+        const int p = xlist[i], h = p / Wc, w = p - (p / Wc) * Wc;
+        if (pl.G[p] * 255.0f > exact_g11(pl.G, Hc, Wc, h, w) - 2.0f) MATOMIC_OR(&BIN[h * WPR + (w >> 5)], 1u << (w & 31));
+      }
+#endif
     }
     MSYNC();
     MSTAMP(7);

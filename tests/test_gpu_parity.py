@@ -116,6 +116,41 @@ def test_random_shapes_vs_oracle(dev, blobs, shape, grid):
     check_against_oracle(out, x, blobs[0], grid, "linear")
 
 
+def _near_tie_image(H, Wd, step, seed):
+    """x (1, 1, H, W) whose pixels on a `step` lattice sit within the adaptive
+    threshold's separable-estimate margin (g255 ~ mean(g255) - 2)."""
+    rng = np.random.default_rng(seed)
+    x = rng.uniform(0.2, 0.8, size=(1, 1, H, Wd)).astype(f32)
+    x[0, 0, 0, 0], x[0, 0, -1, -1] = 0.0, 1.0          # normalize01 is then the identity
+    k = O.K["gauss11_adaptive"].astype(np.float64)
+    kc = k[5, 5]
+    for _ in range(40 if step < 11 else 1):   # Gauss-Seidel when the windows overlap
+        for i, h in enumerate(range(8, H - 8, step)):
+            for j, w in enumerate(range(8, Wd - 8, step)):
+                g = x[0, 0].astype(np.float64) * 255.0
+                others = float((k * g[h - 5:h + 6, w - 5:w + 6]).sum() - kc * g[h, w])
+                delta = (-1.5e-3, 0.0, 1.5e-3, 4e-4)[(i + j) % 4]
+                x[0, 0, h, w] = f32((others - 2.0 + delta) / (1.0 - kc) / 255.0)
+    return x
+
+
+@pytest.mark.parametrize("H,step", [(64, 12), (80, 4)])
+def test_adaptive_threshold_near_ties(dev, blobs, H, step):
+    """Pixels within the margin take the exact 121-tap sum (listed, one wave
+    per pixel); a few per image and several hundred (more than the
+    workgroup's waves) - the mask equals the oracle's bit for bit."""
+    x = _near_tie_image(H, H, step, 7 + step)
+    gray = O.normalize01(O.channel_mean(x, H, H))
+    g255 = (gray * f32(255.0)).astype(f32)
+    mean = O.conv2d(g255, O.K["gauss11_adaptive"], pad="replicate")
+    marg = float(np.frombuffer(np.uint32(0x3B926590).tobytes(), f32)[0])
+    near = int((np.abs(g255 - (mean - f32(2.0))) <= marg).sum())
+    assert near >= (4 if step > 4 else 200), near
+    out = run_plan(dev, blobs, [x], 8, "mlp")[0]
+    assert np.array_equal(out["binmask"], O.adaptive_binarize(gray))
+    check_against_oracle(out, x, blobs[0], 8, "mlp")
+
+
 def test_three_scales_global_planes(dev, blobs):
     """A launch whose largest scale does not fit the LDS (160x160 at grid 8)
     runs every scale with planes in global scratch, each at its own stride."""
