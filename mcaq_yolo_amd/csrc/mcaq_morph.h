@@ -687,6 +687,27 @@ constexpr int SR = 8;
 template <int T, bool SQ>
 MCAQ_HD float tile_sum_t(const float* plane, int Wc, int h0, int w0) {
   float acc = 0.0f;
+#if defined(__HIP_DEVICE_COMPILE__)
+  if constexpr (T % 4 == 0) {
+    // 16-byte row loads (Wc and w0 are multiples of T, the planes 16-byte
+    // aligned): lanes take consecutive tiles, T floats apart, so 4-byte loads
+    // hit the same LDS bank every 32 / T lanes (8-way at T = 8)
+    typedef float f4v __attribute__((ext_vector_type(4)));
+#pragma unroll
+    for (int yy = 0; yy < T; ++yy) {
+      const f4v* row = reinterpret_cast<const f4v*>(plane + (h0 + yy) * Wc + w0);
+#pragma unroll
+      for (int q = 0; q < T / 4; ++q) {
+        const f4v v = row[q];
+        acc = SQ ? acc + v.x * v.x : acc + v.x;
+        acc = SQ ? acc + v.y * v.y : acc + v.y;
+        acc = SQ ? acc + v.z * v.z : acc + v.z;
+        acc = SQ ? acc + v.w * v.w : acc + v.w;
+      }
+    }
+    return acc;
+  }
+#endif
 #pragma unroll
   for (int yy = 0; yy < T; ++yy) {
     const float* row = plane + (h0 + yy) * Wc + w0;
