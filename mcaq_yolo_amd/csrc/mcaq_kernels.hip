@@ -803,6 +803,9 @@ __global__ __launch_bounds__(256) void mcaq_tb_mplane_kernel(MorphArgs a, int to
 // pass B: image group g of a workgroup owns threads [g*G, (g+1)*G) and its own
 // LDS tile arrays; the staged weights are shared by the workgroup.  A group
 // past the batch end recomputes the last image (identical values written twice).
+// TS: floats per tile row of the LDS tile arrays (TILE_FLOATS_PAD when the
+// launch's images fit that way, else TILE_FLOATS; mcaq_morph.h)
+template <int TS>
 __global__ __launch_bounds__(TILES_THREADS, MCAQ_TILES_MINW) void mcaq_tiles_kernel(MorphArgs a, int wlds) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __builtin_amdgcn_s_setprio(MCAQ_MORPH_PRIO);
@@ -818,7 +821,7 @@ __global__ __launch_bounds__(TILES_THREADS, MCAQ_TILES_MINW) void mcaq_tiles_ker
   Ctx ctx{(int)threadIdx.x - g * G, G};
   Shared sh;
   carve_shared(base, sh);
-  morph_tiles(ctx, S, b, sh, wl, (int)threadIdx.x, TILES_THREADS, xs);
+  morph_tiles<TS>(ctx, S, b, sh, wl, (int)threadIdx.x, TILES_THREADS, xs);
 }
 
 // ---------------------------------------------------------------------------
@@ -1369,6 +1372,7 @@ struct MorphLaunch {
   int grid_a, var_a;       // pass A grid (0: no pass A) and kernel variant (2 * legacy + lds mode)
   size_t dyn_a;
   int grid_b, wlds;        // pass B grid (0: no pass B), weights staged in LDS
+  int ts;                  // pass B tile row floats (TILE_FLOATS_PAD or TILE_FLOATS)
   size_t dyn_b;
   int band, grid_e;        // pass A in band mode: band grid = grid_a, edge grid
   size_t dyn_e;
@@ -1467,7 +1471,7 @@ static int morph_launch_config(const mcaq_morph_scale* scales, int nscales, cons
     L.var_a = 2 * leg + mode;
     L.dyn_a = dyn;
   }
-  L.tb = 0; L.any_mask = 0;
+  L.tb = 0; L.any_mask = 0; L.ts = TILE_FLOATS_PAD;
   bool tb = any_tiles != 0;
   for (int i = 0; i < nscales; ++i) {
     const int tf = a.s[i].flags & (F_PHI | F_CMLP | F_MAPPER | F_SOFTMASK);
@@ -1491,21 +1495,26 @@ static int morph_launch_config(const mcaq_morph_scale* scales, int nscales, cons
   } else if (any_tiles) {
     // pass B packing: the waves an image needs for one MLP block of MLP_TPW
     // tiles each (at most the whole workgroup); small images share a workgroup
+    const int lim = MCAQ_MORPH_LDS_LIMIT - 1024;
     int twg = 0, per = 0;
-    for (int i = 0; i < nscales; ++i) {
-      const MorphScale& S = a.s[i];
-      a.twg_begin[i] = twg;
-      a.tipw[i] = 1; a.tgstride[i] = 0;
-      if (!(S.flags & (F_PHI | F_CMLP | F_MAPPER | F_SOFTMASK))) continue;
-      const int NT = S.ht * S.wt;
-      const int G = imin_(TILES_THREADS, 64 * ((NT + MLP_TPW - 1) / MLP_TPW));
-      a.tipw[i] = TILES_THREADS / G;
-      a.tgstride[i] = (tiles_lds_bytes(S.H, S.W, NT) + 15) & ~15;
-      per = imax_(per, a.tipw[i] * a.tgstride[i]);
-      twg += (S.B + a.tipw[i] - 1) / a.tipw[i];
+    for (int ts : {(int)TILE_FLOATS_PAD, (int)TILE_FLOATS}) {   // padded rows when they fit
+      twg = 0; per = 0;
+      for (int i = 0; i < nscales; ++i) {
+        const MorphScale& S = a.s[i];
+        a.twg_begin[i] = twg;
+        a.tipw[i] = 1; a.tgstride[i] = 0;
+        if (!(S.flags & (F_PHI | F_CMLP | F_MAPPER | F_SOFTMASK))) continue;
+        const int NT = S.ht * S.wt;
+        const int G = imin_(TILES_THREADS, 64 * ((NT + MLP_TPW - 1) / MLP_TPW));
+        a.tipw[i] = TILES_THREADS / G;
+        a.tgstride[i] = (tiles_lds_bytes(S.H, S.W, NT, ts) + 15) & ~15;
+        per = imax_(per, a.tipw[i] * a.tgstride[i]);
+        twg += (S.B + a.tipw[i] - 1) / a.tipw[i];
+      }
+      L.ts = ts;
+      if (per + TILES_SCRATCH_BYTES <= lim) break;
     }
     a.twg_begin[nscales] = twg;
-    const int lim = MCAQ_MORPH_LDS_LIMIT - 1024;
     if (per + TILES_SCRATCH_BYTES > lim) return (int)hipErrorInvalidValue;
     // stage the weight blobs in LDS when they fit beside the tile arrays and the MLP scratch
     L.wlds = per + TILES_SCRATCH_BYTES + weights_lds_bytes() <= lim;
@@ -1581,11 +1590,17 @@ static int morph_launch(const MorphLaunch& L, int passes, hipStream_t stream) {
     const int lim = MCAQ_MORPH_LDS_LIMIT - 1024;
     static int set_tiles = 0;
     if ((int)L.dyn_b > set_tiles) {
-      hipError_t ae = hipFuncSetAttribute((const void*)mcaq_tiles_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+      hipError_t ae = hipFuncSetAttribute((const void*)mcaq_tiles_kernel<TILE_FLOATS_PAD>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+      if (ae == hipSuccess)
+        ae = hipFuncSetAttribute((const void*)mcaq_tiles_kernel<TILE_FLOATS>, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
       if (ae != hipSuccess) return (int)ae;
       set_tiles = lim;
     }
-    hipLaunchKernelGGL(mcaq_tiles_kernel, dim3(L.grid_b), dim3(TILES_THREADS), L.dyn_b, stream, a, L.wlds);
+    if (L.ts == TILE_FLOATS_PAD)
+      hipLaunchKernelGGL(mcaq_tiles_kernel<TILE_FLOATS_PAD>, dim3(L.grid_b), dim3(TILES_THREADS), L.dyn_b, stream, a, L.wlds);
+    else
+      hipLaunchKernelGGL(mcaq_tiles_kernel<TILE_FLOATS>, dim3(L.grid_b), dim3(TILES_THREADS), L.dyn_b, stream, a, L.wlds);
   }
   return (int)hipGetLastError();
 }

@@ -88,11 +88,16 @@ MCAQ_HD int plane_bytes(int Hc, int Wc) {
   const int P4 = (Hc * Wc + 3) & ~3;
   return 13 * P4 + 4 * BP_COUNT * Hc * words_per_row(Wc);
 }
-// per-image tile storage: fp32 [NT][TILE_FLOATS]
-enum : int { TILE_FLOATS = 48 };
+// per-image tile storage: fp32 [NT][TS] with 48 slots used.  Pass B runs
+// with rows padded to TILE_FLOATS_PAD = 52 floats when the image's tiles fit
+// the LDS that way: per-tile accesses (lane = tile) then spread over 8 of the
+// 32 banks a 4-byte LDS access uses (48: 2 banks, 16-way conflicts); a
+// multiple of 4 keeps the 16-byte staging stores aligned.  Images with more
+// tiles (e.g. 80x80 at grid 16: 400 tiles) keep TILE_FLOATS = 48.
+enum : int { TILE_FLOATS = 48, TILE_FLOATS_PAD = 52 };
 // per-tile partial quantities in the pass A -> pass B buffer (tile_tmp)
 enum : int { TT_STRIDE = 32 };
-MCAQ_HD int tile_bytes(int NT) { return 4 * TILE_FLOATS * NT; }
+MCAQ_HD int tile_bytes(int NT, int TS = TILE_FLOATS_PAD) { return 4 * TS * NT; }
 // fixed shared scratch: 256-int histogram, 2 x 256 doubles, 2 x 64 reduction slots, flags
 MCAQ_HD int fixed_bytes() { return 1024 + 4096 + 512 + 64; }
 // after the tile array: folded mapper BatchNorms (256 floats), two compact
@@ -524,15 +529,16 @@ MCAQ_HD float quantile_sorted(const float* sorted, int stride, int n, float q) {
 }
 
 // sort slot src of the tile array into slot T_SORT (rank sort, exact)
+template <int TS>
 MCAQ_HD void sort_tiles(const Ctx& ctx, float* tiles, int NT, int src) {
   MFOR(t, NT) {
-    const float v = tiles[t * TILE_FLOATS + src];
+    const float v = tiles[t * TS + src];
     int r = 0;
     for (int u = 0; u < NT; ++u) {
-      const float w = tiles[u * TILE_FLOATS + src];
+      const float w = tiles[u * TS + src];
       r += (w < v) || (w == v && u < t);
     }
-    tiles[r * TILE_FLOATS + T_SORT] = v;
+    tiles[r * TS + T_SORT] = v;
   }
   MSYNC();
 }
@@ -1406,11 +1412,12 @@ MCAQ_HD void phi_of_tile(const MorphScale& S, int b, int t, const float* tv, flo
 }
 
 // phi of every tile of image b from the partials staged in tiles[t][T_TMP..] (pass B)
+template <int TS>
 MCAQ_HD void assemble_phi(const Ctx& ctx, const MorphScale& S, int b, float* tiles) {
   const int NT = S.ht * S.wt;
   MFOR(t, NT) {
-    float* tp = tiles + t * TILE_FLOATS + T_PHI;
-    phi_of_tile(S, b, t, tiles + t * TILE_FLOATS + T_TMP, tp);
+    float* tp = tiles + t * TS + T_PHI;
+    phi_of_tile(S, b, t, tiles + t * TS + T_TMP, tp);
     if (S.phi_out) {
       float* o = S.phi_out + ((size_t)b * NT + t) * 8;
       for (int k = 0; k < 8; ++k) o[k] = tp[k];
@@ -1464,6 +1471,7 @@ MCAQ_HD float window_sum_t(const float* a, int W, int h0, int w0) {
 // before the first store; addresses by selects only (no divergent branches
 // between the loads).
 #if defined(__HIP_DEVICE_COMPILE__)
+template <int TS>
 MCAQ_HD void stage_tiles(const Ctx& ctx, const MorphScale& S, int b, float* tiles, float* wl, int wtid, int wnthr) {
   const int NT = S.ht * S.wt;
   // tile partials: NT rows of 8 float4 (tile_tmp rows are contiguous)
@@ -1513,11 +1521,11 @@ MCAQ_HD void stage_tiles(const Ctx& ctx, const MorphScale& S, int b, float* tile
 #pragma unroll
     for (int i = 0; i < KT; ++i) {
       const int u = ctx.tid + i * ctx.nthr;
-      if (u < q_t) reinterpret_cast<float4*>(tiles + (u >> 3) * TILE_FLOATS + T_TMP)[u & 7] = vt[i];
+      if (u < q_t) reinterpret_cast<float4*>(tiles + (u >> 3) * TS + T_TMP)[u & 7] = vt[i];
     }
   } else {
     for (int u = wtid; u < nw; u += wnthr) { const WSrc ws = wsrc(u); wl4[ws.dq] = *ws.p; }
-    MFOR(u, q_t) reinterpret_cast<float4*>(tiles + (u >> 3) * TILE_FLOATS + T_TMP)[u & 7] = tsrc[u];
+    MFOR(u, q_t) reinterpret_cast<float4*>(tiles + (u >> 3) * TS + T_TMP)[u & 7] = tsrc[u];
   }
 }
 #endif
@@ -1528,17 +1536,18 @@ MCAQ_HD void stage_tiles(const Ctx& ctx, const MorphScale& S, int b, float* tile
 // on request).  LDS per image: Shared (fixed + tiles) | extra | bilateral
 // weights (25 NT floats); the staged weight blobs `wl` (or null) belong to the
 // workgroup.
-MCAQ_HD int tiles_lds_bytes(int H, int W, int NT) {
-  return fixed_bytes() + tile_bytes(NT) + extra_bytes(H, W, NT) + 100 * NT;
+MCAQ_HD int tiles_lds_bytes(int H, int W, int NT, int TS = TILE_FLOATS_PAD) {
+  return fixed_bytes() + tile_bytes(NT, TS) + extra_bytes(H, W, NT) + 100 * NT;
 }
 
 // xs: the workgroup's MLP activation scratch (MLP_SCRATCH_FLOATS per wave), device only
+template <int TS = TILE_FLOATS_PAD>
 MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh, float* wl, int wtid, int wnthr,
                          float* xs) {
   const int ht = S.ht, wt = S.wt, NT = ht * wt;
   const float inv_wt = 1.0f / (float)wt;
   float* tiles = sh.tiles;
-  float* extra = tiles + NT * TILE_FLOATS;            // compact per-tile arrays / tables
+  float* extra = tiles + NT * TS;            // compact per-tile arrays / tables
   float* wbuf = (float*)((char*)extra + extra_bytes(S.H, S.W, NT));
   const float* Pc = S.cmlp;
   const float* Pmap = S.mapper;
@@ -1546,7 +1555,7 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
   MSTAMP_INIT(b == 0 ? 0 : -1);
   MSTAMP(10);
 #if defined(__HIP_DEVICE_COMPILE__)
-  stage_tiles(ctx, S, b, tiles, wl, wtid, wnthr);
+  stage_tiles<TS>(ctx, S, b, tiles, wl, wtid, wnthr);
   if (wl && (S.flags & F_CMLP)) Pc = wl + WL_CM;
   if (wl && (S.flags & F_MAPPER) && !(S.flags & F_MAP_LINEAR)) Pmap = wl + WL_MM;
   if (wl && (S.flags & F_SOFTMASK)) Pm = wl + WL_SM;
@@ -1559,18 +1568,18 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
   if (S.flags & F_PHI)
     MFOR(u, NT * NI) {
       const int t = u / NI, it = u - (u / NI) * NI;
-      tiles[t * TILE_FLOATS + T_TMP + it] = ttmp[t * TT_STRIDE + it];
+      tiles[t * TS + T_TMP + it] = ttmp[t * TT_STRIDE + it];
     }
 #endif
   if (S.flags & F_PHI) {
     // partial quantities of the edge and mask workgroups -> phi
     MSYNC();
     MSTAMP(26);
-    assemble_phi(ctx, S, b, tiles);
+    assemble_phi<TS>(ctx, S, b, tiles);
     MSTAMP(27);
   } else if (S.flags & F_CMLP) {
     bcopy<16>(ctx, NT * 8, [&](int u) { return S.phi_out[(size_t)b * NT * 8 + u]; },
-              [&](int u, float v) { tiles[(u >> 3) * TILE_FLOATS + T_PHI + (u & 7)] = v; });
+              [&](int u, float v) { tiles[(u >> 3) * TS + T_PHI + (u & 7)] = v; });
     MSYNC();
   } else {
     MSYNC();   // staged weights visible
@@ -1582,20 +1591,20 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
     for (int blk = ctx.tid >> 6; blk * MLP_TPW < NT; blk += ctx.nthr >> 6) {
       const bool st = b == 0 && blk == 0 && ctx.nthr == MCAQ_TILES_THREADS;
       const lds_f xw = (lds_f)(xs + (threadIdx.x >> 6) * MLP_SCRATCH_FLOATS);
-      if (wl) cmlp_block_mfma<MLP_NH>((lds_cf)Pc, tiles, NT, blk * MLP_TPW, ctx.tid & 63, xw, st);
-      else cmlp_block_mfma<MLP_NH>(Pc, tiles, NT, blk * MLP_TPW, ctx.tid & 63, xw, st);
+      if (wl) cmlp_block_mfma<MLP_NH, lds_cf, TS>((lds_cf)Pc, tiles, NT, blk * MLP_TPW, ctx.tid & 63, xw, st);
+      else cmlp_block_mfma<MLP_NH, const float*, TS>(Pc, tiles, NT, blk * MLP_TPW, ctx.tid & 63, xw, st);
     }
     MSTAMP(28);
 #else
     MFOR(t, NT) {
       float phi[8];
-      for (int k = 0; k < 8; ++k) phi[k] = tiles[t * TILE_FLOATS + T_PHI + k];
-      tiles[t * TILE_FLOATS + T_CMLP] = complexity_mlp_tile(Pc, phi);
+      for (int k = 0; k < 8; ++k) phi[k] = tiles[t * TS + T_PHI + k];
+      tiles[t * TS + T_CMLP] = complexity_mlp_tile(Pc, phi);
     }
 #endif
     MSYNC();
     MFOR(t, NT) {
-      const float v = tiles[t * TILE_FLOATS + T_CMLP];
+      const float v = tiles[t * TS + T_CMLP];
       extra[t] = v;
       if (S.cmlp_out) S.cmlp_out[(size_t)b * NT + t] = v;
     }
@@ -1647,13 +1656,13 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
       if (tail) { num = ((n0 + n1) + n2) + n3; dsum = ((d0 + d1) + d2) + d3; }
       else { num = n0 + n1; dsum = d0 + d1; }
       const float c = clampf_(num / (dsum + 1e-8f), 0.0f, 1.0f);
-      tiles[t * TILE_FLOATS + T_C] = c;
+      tiles[t * TS + T_C] = c;
       if (S.c_out) S.c_out[(size_t)b * NT + t] = c;
     }
     MSYNC();
   } else if (S.c_in) {
     bcopy<16>(ctx, NT, [&](int u) { return S.c_in[(size_t)b * NT + u]; },
-              [&](int u, float v) { tiles[u * TILE_FLOATS + T_C] = v; });
+              [&](int u, float v) { tiles[u * TS + T_C] = v; });
     MSYNC();
   }
   MSTAMP(12);
@@ -1662,30 +1671,30 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
   if (S.flags & F_MAPPER) {
     int csrc = T_C;
     if (S.flags & F_NORM_C) {
-      sort_tiles(ctx, tiles, NT, T_C);
-      const float lo = quantile_sorted(tiles + T_SORT, TILE_FLOATS, NT, 0.02f);
-      const float hi = quantile_sorted(tiles + T_SORT, TILE_FLOATS, NT, 0.98f);
+      sort_tiles<TS>(ctx, tiles, NT, T_C);
+      const float lo = quantile_sorted(tiles + T_SORT, TS, NT, 0.02f);
+      const float hi = quantile_sorted(tiles + T_SORT, TS, NT, 0.98f);
       MSYNC();
       const float den = (hi - lo) + 1e-8f;
       MFOR(t, NT) {
-        const float c = tiles[t * TILE_FLOATS + T_C];
-        tiles[t * TILE_FLOATS + T_CN] = clampf_((c - lo) / den, 0.0f, 1.0f);
+        const float c = tiles[t * TS + T_C];
+        tiles[t * TS + T_CN] = clampf_((c - lo) / den, 0.0f, 1.0f);
       }
       MSYNC();
       csrc = T_CN;
     }
     if (S.flags & F_MAP_LINEAR) {
       // LinearBitMapper (bit_allocation.py:42-80)
-      sort_tiles(ctx, tiles, NT, csrc);
-      const float lo = quantile_sorted(tiles + T_SORT, TILE_FLOATS, NT, 0.02f);
-      const float hi = quantile_sorted(tiles + T_SORT, TILE_FLOATS, NT, 0.98f);
+      sort_tiles<TS>(ctx, tiles, NT, csrc);
+      const float lo = quantile_sorted(tiles + T_SORT, TS, NT, 0.02f);
+      const float hi = quantile_sorted(tiles + T_SORT, TS, NT, 0.98f);
       MSYNC();
       const float spread = hi - lo;
       MFOR(t, NT) {
-        const float c = tiles[t * TILE_FLOATS + csrc];
+        const float c = tiles[t * TS + csrc];
         const float rel = clampf_((c - lo) / (spread + 1e-8f), 0.0f, 1.0f);
         const float cn = spread > 1e-3f ? rel : clampf_(c, 0.0f, 1.0f);
-        tiles[t * TILE_FLOATS + T_AUX] = S.min_bits + (S.max_bits - S.min_bits) * cn;
+        tiles[t * TS + T_AUX] = S.min_bits + (S.max_bits - S.min_bits) * cn;
       }
     } else {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -1706,26 +1715,26 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
       for (int blk = ctx.tid >> 6; blk * MLP_TPW < NT; blk += ctx.nthr >> 6) {
         const bool st = b == 0 && blk == 0 && ctx.nthr == MCAQ_TILES_THREADS;
         const lds_f xw = (lds_f)(xs + (threadIdx.x >> 6) * MLP_SCRATCH_FLOATS);
-        if (wl) mapper_block_mfma<MLP_NH>((lds_cf)Pmap, (lds_cf)ab, tiles, NT, blk * MLP_TPW, ctx.tid & 63, csrc, S.min_bits,
+        if (wl) mapper_block_mfma<MLP_NH, lds_cf, TS>((lds_cf)Pmap, (lds_cf)ab, tiles, NT, blk * MLP_TPW, ctx.tid & 63, csrc, S.min_bits,
                                   S.max_bits, xw, st);
-        else mapper_block_mfma<MLP_NH>((const float*)Pmap, (const float*)ab, tiles, NT, blk * MLP_TPW, ctx.tid & 63, csrc,
+        else mapper_block_mfma<MLP_NH, const float*, TS>((const float*)Pmap, (const float*)ab, tiles, NT, blk * MLP_TPW, ctx.tid & 63, csrc,
                                S.min_bits, S.max_bits, xw, st);
       }
 #else
-      MFOR(t, NT) tiles[t * TILE_FLOATS + T_AUX] =
-          mapper_mlp_tile(Pmap, tiles[t * TILE_FLOATS + csrc], S.min_bits, S.max_bits);
+      MFOR(t, NT) tiles[t * TS + T_AUX] =
+          mapper_mlp_tile(Pmap, tiles[t * TS + csrc], S.min_bits, S.max_bits);
 #endif
     }
     MSYNC();
     MFOR(t, NT) {
-      const float bv = finish_bits(tiles[t * TILE_FLOATS + T_AUX], S);
-      tiles[t * TILE_FLOATS + T_BITS] = bv;
+      const float bv = finish_bits(tiles[t * TS + T_AUX], S);
+      tiles[t * TS + T_BITS] = bv;
       if (S.bits_out) S.bits_out[(size_t)b * NT + t] = bv;
     }
     MSYNC();
   } else if ((S.flags & F_SOFTMASK) && S.bits_in) {
     bcopy<16>(ctx, NT, [&](int u) { return S.bits_in[(size_t)b * NT + u]; },
-              [&](int u, float v) { tiles[u * TILE_FLOATS + T_BITS] = v; });
+              [&](int u, float v) { tiles[u * TS + T_BITS] = v; });
     MSYNC();
   }
   MSTAMP(13);
@@ -1751,7 +1760,7 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
           for (int w = wa; w < wb; ++w) s = s + am[h * W + w];
         a = (s / (float)(hb - ha)) / (float)(wb - wa);
       }
-      tiles[t * TILE_FLOATS + T_ACT] = a;
+      tiles[t * TS + T_ACT] = a;
       lmx = fmaxp(lmx, a);          // torch.amax: a NaN activation makes the image's max NaN
     }
     const float amax = block_max(ctx, sh, lmx);
@@ -1761,8 +1770,8 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
     float* f0a = extra;
     float* f1a = extra + NT;
     MFOR(t, NT) {
-      f0a[t] = clampf_((tiles[t * TILE_FLOATS + T_BITS] - 2.0f) / 6.0f, 0.0f, 1.0f);
-      f1a[t] = tiles[t * TILE_FLOATS + T_ACT] / den;
+      f0a[t] = clampf_((tiles[t * TS + T_BITS] - 2.0f) / 6.0f, 0.0f, 1.0f);
+      f1a[t] = tiles[t * TS + T_ACT] / den;
     }
     MSYNC();
     MFOR(t, NT) {
@@ -1807,7 +1816,7 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
       const float e = vl ? sleef_expf(ea) : cr_exp(ea);
       const float e0 = first ? 1.0f : e, e1 = first ? e : 1.0f;
       const float mtv = e0 / (e0 + e1);
-      tiles[t * TILE_FLOATS + T_MT] = mtv;
+      tiles[t * TS + T_MT] = mtv;
       if (S.mt_out) S.mt_out[(size_t)b * NT + t] = mtv;
     }
     MSYNC();
@@ -1817,7 +1826,7 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
       float* mt = extra;
       int* rsrc = (int*)(extra + NT);
       int* csrc = rsrc + H;
-      MFOR(t, NT) mt[t] = tiles[t * TILE_FLOATS + T_MT];
+      MFOR(t, NT) mt[t] = tiles[t * TS + T_MT];
       MFOR(h, H) rsrc[h] = nearest_src(h, ht, H) * wt;
       MFOR(w, W) csrc[w] = nearest_src(w, wt, W);
       MSYNC();
