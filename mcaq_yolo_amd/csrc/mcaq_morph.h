@@ -877,6 +877,13 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, P
     //    Up to GPT pixels per thread are loaded at once and kept in registers.
     const float* gin = S.gray + (size_t)b * P;
     MFOR(i, 256) sh.hist[i] = 0;          // Otsu histogram, filled by the blur stage
+    // mask role, tiles >= 8 px: per-tile uniform-LBP label counts, counted by
+    // LDS atomics in the Sobel / LBP stage (in the direction byte plane, unused
+    // by this role: 40 NT <= P bytes) instead of 10 label bit planes
+    const bool lbp_cnt = role == 1 && T >= 8;
+    int* lcnt = reinterpret_cast<int*>(pl.dir);
+    const int tsh = __builtin_ctz((unsigned)T);   // tiles are powers of two
+    if (lbp_cnt) MFOR(i, 10 * NT) lcnt[i] = 0;
     float lmn = 3.402823466e38f, lmx = -3.402823466e38f;
     constexpr int GPT = 8;
     const bool greg = P <= GPT * ctx.nthr;
@@ -1196,8 +1203,10 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, P
             gx = fmaf(-1.0f, z20, gx); gx = fmaf(1.0f, z22, gx);
             gy = fmaf(-1.0f, z00, gy); gy = fmaf(-2.0f, z01, gy); gy = fmaf(-1.0f, z02, gy);
             gy = fmaf(1.0f, z20, gy); gy = fmaf(2.0f, z21, gy); gy = fmaf(1.0f, z22, gy);
+#ifndef MCAQ_PROBE_NO_GRAD_PLANES   // timing probe only
             pl.A[h * Wc + w] = gx;
             pl.Bf[h * Wc + w] = gy;
+#endif
             // LBP (morphology.py:630-646): replicate pad, nb >= center, circular order
             int bt[8];
             bt[0] = c[r][0] >= ctr; bt[1] = c[r][1] >= ctr; bt[2] = c[r][2] >= ctr; bt[3] = c[r + 1][2] >= ctr;
@@ -1207,13 +1216,16 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, P
             for (int q = 0; q < 8; ++q) { n1 += bt[q]; tr += bt[q] != bt[(q + 7) & 7]; }
             lab = tr <= 2 ? n1 : 9;
           }
-          if (h < Hc) {
+          if (lbp_cnt) {
+            if (lab >= 0) MATOMIC_ADD(&lcnt[((h >> tsh) * wt + (w >> tsh)) * 10 + lab], 1);
+          } else if (h < Hc) {
 #pragma unroll
             for (int q = 0; q < 10; ++q) put_bits(pl.bits(BP_L0 + q), h * WPR + k, bit, lab == q);
           }
         }
       }
     }
+    MSTAMP(4);
     // boundary (m & ~erode3x3 with in-bounds neighbours) and Euler quad classes
     // of the windows anchored at (h, w) over m[h-1..h][w-1..w] (zero padded)
     MFOR2(h, k, Hc, WPR) {
@@ -1324,7 +1336,8 @@ MCAQ_HD void morph_edges(const Ctx& ctx, const MorphScale& S, int b, int role, P
         const uint32_t* plane = k < 10 ? pl.bits(BP_L0 + k)
                               : (k == 10 ? edge : (k == 11 ? BIN : (k == 12 ? BND : (k == 13 ? Q1 : (k == 14 ? Q3 : QD)))));
         int cnt = 0;
-        if (T == 4) cnt = tile_pop_t<4>(plane, WPR, h0, w0);
+        if (k < 10 && lbp_cnt) cnt = lcnt[t * 10 + k];
+        else if (T == 4) cnt = tile_pop_t<4>(plane, WPR, h0, w0);
         else if (T == 8) cnt = tile_pop_t<8>(plane, WPR, h0, w0);
         else if (T == 16) cnt = tile_pop_t<16>(plane, WPR, h0, w0);
         else for (int yy = 0; yy < T; ++yy) cnt += row_pop(plane + (h0 + yy) * WPR, w0, T, WPR);

@@ -20,8 +20,8 @@ from mcaq_yolo_amd.engine import HookPlan, ScaleGeom  # noqa: E402
 
 NAMES = {1: "E gray+norm", 2: "E blur+hist", 3: "E otsu", 4: "E sobel255+dir", 5: "E nms", 6: "E hysteresis",
          7: "E (7)", 8: "E (8)", 9: "E tile items",
-         17: "M gray+norm", 18: "M binarize: row pass", 19: "M binarize: column pass", 20: "M (20)", 21: "M (21)", 22: "M (22)", 23: "M binarize: exact list",
-         24: "M sobel+lbp+planes", 25: "M tile items",
+         17: "M gray+norm", 18: "M binarize: row pass", 19: "M binarize: column pass", 20: "M sobel+lbp", 21: "M (21)", 22: "M (22)", 23: "M binarize: exact list",
+         24: "M boundary+euler planes", 25: "M tile items",
          10: "B start", 26: "B stage loads", 27: "B assemble phi", 28: "B cmlp mfma", 11: "B cmlp out",
          29: "B bilateral weights", 12: "B bilateral sums", 30: "B mapper BN fold", 13: "B mapper MLP + finish",
          31: "B softmask pool |x| + max", 14: "B softmask net + softmax", 15: "B m plane"}
