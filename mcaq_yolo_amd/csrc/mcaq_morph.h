@@ -174,7 +174,7 @@ struct Shared {
   double* mu;      // 256 (Otsu mu prefix)
   float* redf;     // 64
   int* redi;       // 64
-  int* flags;      // 16
+  int* flags;      // 16: [8] Otsu argmax, [9] adaptive-threshold exact-list length
   float* tiles;    // NT * TILE_FLOATS
 };
 
