@@ -1518,6 +1518,9 @@ static int morph_launch_config(const mcaq_morph_scale* scales, int nscales, cons
     if (per + TILES_SCRATCH_BYTES > lim) return (int)hipErrorInvalidValue;
     // stage the weight blobs in LDS when they fit beside the tile arrays and the MLP scratch
     L.wlds = per + TILES_SCRATCH_BYTES + weights_lds_bytes() <= lim;
+#ifdef MCAQ_TILES_NO_WLDS
+    L.wlds = 0;   // A/B: weights read through the caches (smaller LDS footprint per workgroup)
+#endif
 #ifdef MCAQ_TILES_EXCL
     L.dyn_b = (size_t)lim;   // A/B: one pass-B workgroup per CU (no streaming waves beside it)
 #else
