@@ -1336,7 +1336,10 @@ static int morph_ipw(const MorphScale& S, int mode, int limit) {
   const int per = ((plane_bytes(S.Hc, S.Wc) + 15) & ~15) + fixed_bytes();
   const int P = S.Hc * S.Wc;
   int ipw = 16;
-  while (ipw > 1 && (ipw * per > limit || MORPH_THREADS / ipw < 64 || P > MCAQ_PPT * (MORPH_THREADS / ipw))) ipw >>= 1;
+  // every image group a whole number of waves (ballots / shuffles are per image)
+  while (ipw > 1 && (ipw * per > limit || MORPH_THREADS / ipw < 64 || (MORPH_THREADS / ipw) % 64 != 0 ||
+                     P > MCAQ_PPT * (MORPH_THREADS / ipw)))
+    ipw >>= 1;
   return ipw;
 }
 
