@@ -43,3 +43,8 @@ tot = sum(hist.values())
 print("concurrency:", {k: round(v / tot, 3) for k, v in sorted(hist.items())})
 for c, v in sorted(combo.items(), key=lambda x: -x[1])[:12]:
     print("  %5.1f%%  %s" % (100 * v / tot, "+".join(c) if c else "(idle)"))
+# time with no HBM-streaming kernel (pass 1 / pass 2) running, and with one / two
+nstream = defaultdict(float)
+for c, v in combo.items():
+    nstream[sum(1 for k in c if k in ("stats", "quant"))] += v
+print("streaming kernels active:", {k: round(v / tot, 3) for k, v in sorted(nstream.items())})
