@@ -42,7 +42,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 from mcaq_yolo_amd import params  # noqa: E402
-from mcaq_yolo_amd.engine import HookPlan, ScaleGeom, sync_channel_minmax  # noqa: E402
+from mcaq_yolo_amd.engine import HookPlan, ScaleGeom  # noqa: E402
 
 # BASELINE.json configs that fit this harness: name -> (per-GPU batch, channels, grid, mapper)
 CONFIGS = {
@@ -340,6 +340,10 @@ def main_qat(args, world, rank, dev, pg):
         dist.destroy_process_group()
 
 
+# independent batches per launch set (engine.HookPlan batches): measured
+# DESIGN.md s.3 "Round 5"
+LAUNCH_BATCHES = 2
+
 HOOK_METRIC = ("images/sec @640x640 MCAQ hook path (C3/C4/C5 complexity + bit mapper + 2-8 bit quant), "
                "1/2/4/8 MI355X; % HBM roofline")
 E2E_METRIC = "images/sec @640x640 end-to-end MCAQ infer (YOLOv8 + hooks + NMS), 1/2/4/8 MI355X"
@@ -572,18 +576,23 @@ class _RunMixin:
 
 
 class Runner(_RunMixin):
-    """Issues hook-path steps.  Independent HookPlans (own inputs and
-    buffers) cycled over `depth` HIP streams: step i runs plan i % len(plans)
-    on stream i % depth, so the per-image morphology of one batch
-    (latency-bound) overlaps the HBM passes of the others.  A step is one
-    HIP-graph replay (N = 1), or two replays around the RCCL min/max
-    all-reduce (N > 1)."""
+    """Issues hook-path launch sets.  Independent HookPlans (own inputs and
+    buffers; each a launch set of `batches` batches) cycled over `depth` HIP
+    streams: launch i runs plan i % len(plans) on stream i % depth, so the
+    per-image morphology of one launch set (latency-bound) overlaps the HBM
+    passes of the others.  A launch is one HIP-graph replay - with N > 1 on
+    the nccl (RCCL) backend the min/max all-reduce is captured inside it; on
+    gloo (CPU collectives, the functional rehearsal) it is two replays around
+    the eager all-reduce."""
 
     def __init__(self, plans, pg, use_graph, depth):
         self.plans, self.pg = plans, pg
         self.streams = [torch.cuda.Stream() for _ in range(depth)]
         self.graphs = [None] * len(plans)
         self.i = 0
+        self.batches = plans[0].batches
+        capturable = pg is None or _backend(pg) == "nccl"
+        self.captured_collective = use_graph and pg is not None and capturable
         if use_graph:
             torch.cuda.synchronize()
             for p, plan in enumerate(plans):
@@ -592,7 +601,7 @@ class Runner(_RunMixin):
                     for _ in range(2):          # warm the launchers outside capture
                         plan.launch(st, self.pg)
                 st.synchronize()
-                segs = [lambda pl=plan: pl.launch(torch.cuda.current_stream())] if pg is None else \
+                segs = [lambda pl=plan: pl.launch(torch.cuda.current_stream(), self.pg)] if capturable else \
                     [lambda pl=plan: pl.launch_pre(torch.cuda.current_stream()),
                      lambda pl=plan: pl.launch_quant(torch.cuda.current_stream())]
                 gs = []
@@ -604,6 +613,11 @@ class Runner(_RunMixin):
                 self.graphs[p] = gs
             torch.cuda.synchronize()
 
+    def run(self, steps):
+        """`steps` batches = steps / batches launch sets (steps a multiple)."""
+        for _ in range(steps // self.batches):
+            self.step()
+
     def step(self):
         p = self.i % len(self.plans)
         plan, st, gs = self.plans[p], self.streams[self.i % len(self.streams)], self.graphs[p]
@@ -611,16 +625,21 @@ class Runner(_RunMixin):
         with torch.cuda.stream(st):
             if gs is None:
                 plan.launch(st, self.pg)
-            elif self.pg is None:
+            elif len(gs) == 1:
                 gs[0].replay()
             else:
                 gs[0].replay()
-                sync_channel_minmax(plan.bufs, self.pg)
+                plan.allreduce_stats(self.pg, st)
                 gs[1].replay()
 
     def sync(self):
         for st in self.streams:
             torch.cuda.current_stream().wait_stream(st)
+
+
+def _backend(pg):
+    import torch.distributed as dist
+    return str(dist.get_backend(pg)).lower()
 
 
 def kernel_timing(plans, reps=40, evict=None):
@@ -670,7 +689,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS) + [5],
                     help="2/3/4: inference hook path; 5: QAT hook training step")
-    ap.add_argument("--pipeline", type=int, default=3, help="batches in flight (HIP streams)")
+    ap.add_argument("--pipeline", type=int, default=3, help="launch sets in flight (HIP streams)")
+    ap.add_argument("--launch-batches", type=int, default=LAUNCH_BATCHES,
+                    help="independent batches per launch set (each kernel launch carries that many batches, "
+                         "each with its own statistics and outputs; ms_per_step still counts one batch)")
     ap.add_argument("--inputs", type=int, default=0,
                     help="distinct input batches cycled through (default max(3, pipeline): >= 276 MB of x at "
                          "config 2, more than the 256 MiB Infinity Cache, so no step finds its input cached)")
@@ -694,6 +716,8 @@ def main():
                          "modules on concurrent streams, or one after another (default: hooks')")
     ap.add_argument("--pass-b", choices=("image", "batch"), default=None,
                     help="morphology pass B: per-image workgroups or batch-wide tile kernels (default: engine's)")
+    ap.add_argument("--pass-a", choices=("image", "band"), default=None,
+                    help="morphology pass A: per-image workgroups or 16-row band workgroups (default: engine's)")
     args = ap.parse_args()
     if args.qat_scales is not None:
         from mcaq_yolo_amd import hooks as _hooks
@@ -702,6 +726,9 @@ def main():
     if args.pass_b is not None:
         from mcaq_yolo_amd import engine as _engine
         _engine.TILES_BATCH = args.pass_b == "batch"
+    if args.pass_a is not None:
+        from mcaq_yolo_amd import engine as _engine
+        _engine.BAND_PASS = args.pass_a == "band"
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -730,24 +757,29 @@ def main():
         return main_e2e(args, world, rank, dev, pg)
     name, B, chans, grid, mapper = CONFIGS[args.config]
     depth = max(1, args.pipeline)
+    nbat = max(1, args.launch_batches)
+    # whole launch sets: K (and the warmup) rounded up to a multiple of the batches per launch
+    args.steps = -(-args.steps // nbat) * nbat
+    args.warmup = -(-max(args.warmup, 1) // nbat) * nbat
     cm, mm, sm = load_blobs(dev)
     geoms = [ScaleGeom(B, c, h, w, grid) for c, (h, w) in zip(chans, SIZES)]
     plans = []
     nin = max(args.inputs or max(3, depth), depth)
     for p in range(nin):
         # each batch in flight has its own synthetic input (seeded per rank and slot)
-        feats = [synth_features(B, c, h, w, 1000 * args.config + i + 7919 * rank + 104729 * p, dev)
-                 for i, (c, (h, w)) in enumerate(zip(chans, SIZES))]
-        plan = HookPlan(geoms, dev)
-        plan.prepare(feats, cm, mm, [sm, sm, sm], temperature=1.0, mapper_kind=mapper,
-                     batch_offset=rank * B, batch_total=world * B, m_plane=args.m_plane)
+        feats = [[synth_features(B, c, h, w, 1000 * args.config + i + 7919 * rank + 104729 * (p * nbat + k), dev)
+                  for i, (c, (h, w)) in enumerate(zip(chans, SIZES))] for k in range(nbat)]
+        plan = HookPlan(geoms, dev, batches=nbat)
+        plan.prepare(feats if nbat > 1 else feats[0], cm, mm, [sm, sm, sm], temperature=1.0, mapper_kind=mapper,
+                     batch_offset=rank * B, batch_total=world * B, m_plane=args.m_plane,
+                     shared_stats=pg is not None)
         plan.feats = feats
         plans.append(plan)
     torch.cuda.synchronize()
 
     use_graph = not args.eager
     runner = Runner(plans, pg, use_graph, depth)
-    runner.run(max(args.warmup, 1))
+    runner.run(args.warmup)
     runner.sync()
     torch.cuda.synchronize()
 
@@ -768,7 +800,7 @@ def main():
         torch.cuda.synchronize()
         lat.append(time.perf_counter() - t1)
     latency_ms = sorted(lat)[len(lat) // 2] * 1e3
-    runner.run(4)         # plans[0] was re-run alone: a few more steps to be safe, then settle
+    runner.run(4 * nbat)  # plans[0] was re-run alone: a few more steps to be safe, then settle
     runner.sync()
 
     # ---- timed region: K steps, `depth` batches in flight.  Every window
@@ -812,7 +844,8 @@ def main():
         step_s = wall_k / args.steps
     quant_us = kt["quant"]
 
-    elems = sum(B * c * h * w for c, (h, w) in zip(chans, SIZES))
+    elems = sum(B * c * h * w for c, (h, w) in zip(chans, SIZES))    # per batch (= per step)
+    lelems = nbat * elems                                            # per kernel launch
     alg_bytes = 12 * elems                       # 2 reads of x + 1 write of y, fp32
     # HBM-side bytes per launch from the rocprofv3 PMC passes of tools/pmc_traffic.sh
     # (FETCH_SIZE and WRITE_SIZE in separate runs, FETCH doubled per the gfx950
@@ -827,15 +860,15 @@ def main():
     value = world * B / step_s
     out = None
     if rank == 0:
-        q_gbs = 8 * elems / (quant_us * 1e-6) / 1e9
-        seq = "hipExtLaunchKernel start/stop events of each launch, median of 40 single-batch steps in sequence on " \
-              "one stream over %d input batches, x evicted from the Infinity Cache (384 MiB sweep) before each " \
-              "timed pass" % len(plans)
-        kern = {"quant": {"us": round(quant_us, 2), "alg_bytes": 8 * elems, "GB/s": round(q_gbs, 1),
+        q_gbs = 8 * lelems / (quant_us * 1e-6) / 1e9
+        seq = "hipExtLaunchKernel start/stop events of each launch, median of 40 single-launch steps in sequence " \
+              "on one stream over %d input launch sets (%d batch(es) each), x evicted from the Infinity Cache " \
+              "(384 MiB sweep) before each timed pass" % (len(plans), nbat)
+        kern = {"quant": {"us": round(quant_us, 2), "alg_bytes": 8 * lelems, "GB/s": round(q_gbs, 1),
                           "frac": round(q_gbs / HBM_PEAK_GBS, 4), "timing": seq,
                           "us_in_sequence": round(kt_seq["quant"], 2)}}
-        gbs = 4 * elems / (kt["stats"] * 1e-6) / 1e9
-        kern["stats"] = {"us": round(kt["stats"], 2), "alg_bytes": 4 * elems, "GB/s": round(gbs, 1),
+        gbs = 4 * lelems / (kt["stats"] * 1e-6) / 1e9
+        kern["stats"] = {"us": round(kt["stats"], 2), "alg_bytes": 4 * lelems, "GB/s": round(gbs, 1),
                          "frac": round(gbs / HBM_PEAK_GBS, 4), "timing": seq,
                          "us_in_sequence": round(kt_seq["stats"], 2)}
         kern["morph_finalize"] = {"us": round(kt_seq["morph_finalize"], 2), "bound": "latency (per-image chain)",
@@ -858,12 +891,17 @@ def main():
                                    "quant/dequant; YOLOv8 network excluded (see e2e)" % (name, B, grid, mapper),
                        "global_batch": world * B, "grid_size": grid, "mapper": mapper,
                        "parallelism": "dp%d" % world,
+                       "pass_a": "16-row band workgroups" if _engine_mod().BAND_PASS else "per-image workgroups",
                        "pass_b": "batch-wide tile kernels" if _engine_mod().TILES_BATCH else "per-image workgroups",
                        "hip_graph": use_graph,
-                       "batches_in_flight": depth,
-                       "schedule": "streams: %d batch chains on %d streams, one HIP graph each" % (depth, depth),
-                       "input_batches": len(plans),
-                       "latency_ms_single_batch": round(latency_ms, 4),
+                       "rccl_in_graph": runner.captured_collective,
+                       "batches_per_launch": nbat,
+                       "launch_sets_in_flight": depth,
+                       "batches_in_flight": depth * nbat,
+                       "schedule": "streams: %d launch-set chains (%d independent batch(es) per launch, each with "
+                                   "its own statistics) on %d streams, one HIP graph each" % (depth, nbat, depth),
+                       "input_batches": len(plans) * nbat,
+                       "latency_ms_single_launch": round(latency_ms, 4),
                        "host_enqueue_us_per_step": round(t_enq / args.steps * 1e6, 1),
                        "timing": "steady state: median over %d pairs of (wall(2K steps) - wall(K steps)) / K, "
                                  "each window synchronised on both sides (the pipeline fill and drain cancel)" % npairs,
@@ -885,7 +923,7 @@ def main():
                          "kernel": "%s (pass 2: read x + write y, 8 B per feature element)"
                                    % ("mcaq_quant_tile_kernel" if "mcaq_quant_tile_kernel" in traffic_k
                                       else "mcaq_quant_kernel"),
-                         "alg_bytes_per_launch": 8 * elems, "us_per_launch": kern["quant"]["us"]},
+                         "alg_bytes_per_launch": 8 * lelems, "us_per_launch": kern["quant"]["us"]},
             "kernels": kern,
             "cpu_baseline": None,
         }

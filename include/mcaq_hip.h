@@ -22,7 +22,10 @@
  *       <- ultralytics non_max_suppression + torchvision nms as called by
  *          Predictor.postprocess / predict_batch (mcaq_yolo/inference.py:
  *          213-219, 410-417): the detection postprocess of the e2e path.
- * Up to three hook scales (C3/C4/C5) are processed by one launch.
+ * One launch processes up to MCAQ_MAX_SEGMENTS segments; a segment is one hook
+ * scale (C3/C4/C5) of one batch, each with its own tensors and statistics, so
+ * a launch serves the three scales of one batch or of up to three
+ * independent batches (a "launch set").
  */
 #ifndef MCAQ_HIP_H_
 #define MCAQ_HIP_H_
@@ -41,7 +44,10 @@ typedef void* hipEvent_t;
 extern "C" {
 #endif
 
-#define MCAQ_ABI_VERSION 17
+#define MCAQ_ABI_VERSION 18
+/* segments (hook scale x batch) per mcaq_stats / mcaq_finalize /
+ * mcaq_morph* / mcaq_quant launch */
+#define MCAQ_MAX_SEGMENTS 9
 /* largest dynamic LDS request of the morph kernel (gfx950: 160 KiB per CU) */
 #define MCAQ_MORPH_LDS_LIMIT 163840
 
@@ -90,6 +96,10 @@ typedef struct {
   int block_begin;   /* set by the launcher */
   int per_tensor;    /* 1: ONE min/max over every channel, broadcast to the C
                         outputs (per_channel=False, quantization.py:655-661) */
+  int neg_min;       /* 1: min_out receives -min (so [-min, max] of every
+                        segment can be combined across ranks by ONE MAX
+                        all-reduce in place; mcaq_quant_scale.neg_min reads it
+                        back) */
 } mcaq_finalize_scale;
 int mcaq_finalize(const mcaq_finalize_scale* scales, int nscales, hipStream_t stream);
 
@@ -169,6 +179,7 @@ typedef struct {
                           channels whose statistics are finite hold only
                           finite x and take the shorter arithmetic; 0: any x
                           (frozen / external statistics) */
+  int neg_min;         /* 1: xmin holds -min (mcaq_finalize_scale.neg_min) */
 } mcaq_quant_scale;
 int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream);
 

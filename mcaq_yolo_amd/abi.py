@@ -9,7 +9,8 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libmcaq_hip.so")
-ABI_VERSION = 17
+ABI_VERSION = 18
+MAX_SEGMENTS = 9   # MCAQ_MAX_SEGMENTS: segments (hook scale x batch) per launch
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -23,7 +24,8 @@ class StatsScale(ctypes.Structure):
 
 class FinalizeScale(ctypes.Structure):
     _fields_ = [("pmin", P), ("pmax", P), ("min_in", P), ("max_in", P), ("min_out", P), ("max_out", P),
-                ("C", I), ("nunits", I), ("min_stride", I), ("block_begin", I), ("per_tensor", I)]
+                ("C", I), ("nunits", I), ("min_stride", I), ("block_begin", I), ("per_tensor", I),
+                ("neg_min", I)]
 
 
 class MorphScale(ctypes.Structure):
@@ -40,7 +42,7 @@ class QuantScale(ctypes.Structure):
     _fields_ = [("x", P), ("y", P), ("bits", P), ("m", P), ("mt", P), ("xmin", P), ("xmax", P),
                 ("B", I), ("C", I), ("H", I), ("W", I), ("ht", I), ("wt", I),
                 ("bits_lo", I), ("nbits", I), ("compat_tile_h", I), ("compat_tile_w", I), ("unit_begin", I),
-                ("stats_cover_x", I)]
+                ("stats_cover_x", I), ("neg_min", I)]
 
 
 class QatScale(ctypes.Structure):

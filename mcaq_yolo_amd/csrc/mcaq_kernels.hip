@@ -39,9 +39,11 @@ extern "C" int mcaq_reset_stamps(void) {
 // ---------------------------------------------------------------------------
 // pass 1
 // ---------------------------------------------------------------------------
+constexpr int MAXSEG = MCAQ_MAX_SEGMENTS;   // segments (hook scale x batch) per launch
+
 struct StatsArgs {
-  mcaq_stats_scale s[3];
-  int ppl[3];          // pixels per lane of each scale (1, 2 or 4)
+  mcaq_stats_scale s[MAXSEG];
+  int ppl[MAXSEG];     // pixels per lane of each segment (1, 2 or 4)
   int nscales;
   int units_total;
 };
@@ -440,8 +442,8 @@ __global__ __launch_bounds__(256, MCAQ_STATS_MINW) void mcaq_stats_kernel(StatsA
   int si = 0;
   while (si + 1 < a.nscales && unit >= a.s[si + 1].unit_begin) ++si;
   int lu = unit - a.s[si].unit_begin;
-  const mcaq_stats_scale S = si == 0 ? a.s[0] : si == 1 ? a.s[1] : a.s[2];   // by value: no indexed kernarg copy
-  const int ppl = si == 0 ? a.ppl[0] : si == 1 ? a.ppl[1] : a.ppl[2];
+  const mcaq_stats_scale S = a.s[si];   // wave-uniform index: scalar loads from the kernarg segment
+  const int ppl = a.ppl[si];
 #if MCAQ_STATS_XCD
   {
     const int n = (si + 1 < a.nscales ? a.s[si + 1].unit_begin : a.units_total) - a.s[si].unit_begin;
@@ -466,7 +468,7 @@ __global__ __launch_bounds__(256, MCAQ_STATS_MINW) void mcaq_stats_kernel(StatsA
 // finalize: channel min/max over the partials of pass 1
 // ---------------------------------------------------------------------------
 struct FinalizeArgs {
-  mcaq_finalize_scale s[3];
+  mcaq_finalize_scale s[MAXSEG];
   int nscales;
   int nblocks;
 };
@@ -500,6 +502,7 @@ __device__ __forceinline__ void finalize_body(const FinalizeArgs& a, int blk, fl
     }
     mn = red[0];
     mx = red[nthr];
+    if (S.neg_min) mn = -mn;
     for (int c = tid; c < S.C; c += nthr) { S.min_out[c] = mn; S.max_out[c] = mx; }
     return;
   }
@@ -534,10 +537,13 @@ __device__ __forceinline__ void finalize_body(const FinalizeArgs& a, int blk, fl
   __syncthreads();
   if (part == 0 && cv) {
     for (int k = 1; k < parts; ++k) { mn = vmin_(mn, red[k * 64 + cl]); mx = vmax_(mx, red[nthr + k * 64 + cl]); }
-    S.min_out[c] = mn;
+    S.min_out[c] = S.neg_min ? -mn : mn;
     S.max_out[c] = mx;
   }
 }
+
+// kernel arguments live in the dispatch's kernarg segment (4 KiB)
+static_assert(sizeof(MorphArgs) + sizeof(FinalizeArgs) <= 4096, "morph kernel arguments exceed 4 KiB");
 
 __global__ __launch_bounds__(256) void mcaq_finalize_kernel(FinalizeArgs a) {
   __shared__ float red[2 * 256];
@@ -828,19 +834,22 @@ __global__ __launch_bounds__(TILES_THREADS, MCAQ_TILES_MINW) void mcaq_tiles_ker
 // pass 2: y = dequant(quant_b(x)) * m
 // ---------------------------------------------------------------------------
 struct QuantArgs {
-  mcaq_quant_scale s[3];
+  mcaq_quant_scale s[MAXSEG];
   int nscales;
   int units_total;
   // tile-aligned path (mcaq_quant_tile_kernel): H = ht << sh, W = wt << sw;
   // reciprocals of the slice count, units per image and W for div_small
-  int sh[3], sw[3];
-  float rnsl[3], rupi[3], rw[3];
+  int sh[MAXSEG], sw[MAXSEG];
+  float rnsl[MAXSEG], rupi[MAXSEG], rw[MAXSEG];
 };
 
 #ifndef MCAQ_QSLICE
 #define MCAQ_QSLICE 32
 #endif
 constexpr int QSLICE = MCAQ_QSLICE;   // channels per unit (8 per wave)
+// mcaq_quant_tile_kernel stores one [bits][channel] table entry per thread
+// (bit width tid / 32, channel tid % 32) for 8 widths x QSLICE channels
+static_assert(QSLICE == 32, "the tile-aligned pass 2 assumes 32-channel slices");
 constexpr int QCW = QSLICE / 4;       // channels per wave
 constexpr int QMAXBITS = 15;   // max entries per channel in the LDS table
 constexpr int QMAXNT = 1024;   // max tiles per image whose m values are staged in LDS (more: read from L2)
@@ -902,7 +911,8 @@ __global__ MCAQ_QUANT_LB void mcaq_quant_kernel(QuantArgs a) {
   // table entry's min / max, its m(tile) value, the lane's 4 tile bits (and
   // m(p) values when the plane is given)
   const int tc = imin_(tid / NB, nc - 1);
-  const float tmn = S.xmin[c0 + tc], tmx = S.xmax[c0 + tc];
+  const float tmn0 = S.xmin[c0 + tc], tmx = S.xmax[c0 + tc];
+  const float tmn = S.neg_min ? -tmn0 : tmn0;
   float mtv = 0.0f;
   if (kM == QM_MT_LDS) mtv = S.mt[(size_t)b * NTq + imin_(tid, NTq - 1)];
   const int q0 = chunk * 256 + lane * 4;
@@ -954,9 +964,10 @@ __global__ MCAQ_QUANT_LB void mcaq_quant_kernel(QuantArgs a) {
   if (kBig) {
     for (int i = tid + 256; i < ntab; i += 256) {   // > 256 entries: continuous bit ranges
       const int c = i / NB, k = i - (i / NB) * NB;
-      const QParam q = qparam(S.xmin[c0 + c], S.xmax[c0 + c], S.bits_lo + k);
+      const float mn = S.neg_min ? -S.xmin[c0 + c] : S.xmin[c0 + c];
+      const QParam q = qparam(mn, S.xmax[c0 + c], S.bits_lo + k);
       qt[i] = make_float4(q.scale, q.zp, q.rs, 0.0f);
-      if (k == 0) qany[c] = (!S.stats_cover_x || stats_need_any(S.xmin[c0 + c], S.xmax[c0 + c])) ? 1 : 0;
+      if (k == 0) qany[c] = (!S.stats_cover_x || stats_need_any(mn, S.xmax[c0 + c])) ? 1 : 0;
     }
   }
   if (kM == QM_MT_LDS) {
@@ -1068,11 +1079,8 @@ __global__ MCAQ_QUANT_LB void mcaq_quant_tile_kernel(QuantArgs a) {
   const mcaq_quant_scale& S = a.s[si];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int H = S.H, W = S.W, HW = H * W;
-  const int sh = si == 0 ? a.sh[0] : si == 1 ? a.sh[1] : a.sh[2];
-  const int sw = si == 0 ? a.sw[0] : si == 1 ? a.sw[1] : a.sw[2];
-  const float rnsl = si == 0 ? a.rnsl[0] : si == 1 ? a.rnsl[1] : a.rnsl[2];
-  const float rupi = si == 0 ? a.rupi[0] : si == 1 ? a.rupi[1] : a.rupi[2];
-  const float rw = si == 0 ? a.rw[0] : si == 1 ? a.rw[1] : a.rw[2];
+  const int sh = a.sh[si], sw = a.sw[si];
+  const float rnsl = a.rnsl[si], rupi = a.rupi[si], rw = a.rw[si];
   const int nsl = (S.C + QSLICE - 1) / QSLICE, upi = (HW + 255) >> 8;
   const int lu = unit - S.unit_begin;
   const int q1 = div_small(lu, nsl, rnsl);
@@ -1087,7 +1095,8 @@ __global__ MCAQ_QUANT_LB void mcaq_quant_tile_kernel(QuantArgs a) {
   // channel tid % 32), its m(tile) value, the lane's tile bits (one load: its
   // 4 pixels share the tile)
   const int tc = imin_(tid & (QSLICE - 1), nc - 1);
-  const float tmn = S.xmin[c0 + tc], tmx = S.xmax[c0 + tc];
+  const float tmn0 = S.xmin[c0 + tc], tmx = S.xmax[c0 + tc];
+  const float tmn = S.neg_min ? -tmn0 : tmn0;
   float mtv = 0.0f;
   if (kM == QM_MT_LDS) mtv = S.mt[(size_t)b * NTq + imin_(tid, NTq - 1)];
   const int q0 = chunk * 256 + lane * 4;
@@ -1237,7 +1246,7 @@ int mcaq_launch_spatial_quantization(const float* input, const float* bit_map, c
 }
 
 int mcaq_stats(const mcaq_stats_scale* scales, int nscales, hipStream_t stream) {
-  if (nscales < 1 || nscales > 3) return (int)hipErrorInvalidValue;
+  if (nscales < 1 || nscales > MAXSEG) return (int)hipErrorInvalidValue;
   StatsArgs a;
   int units = 0;
   for (int i = 0; i < nscales; ++i) {
@@ -1267,7 +1276,7 @@ int mcaq_stats_units(int B, int C, int H, int W) {
 }
 
 static int finalize_args(const mcaq_finalize_scale* scales, int nscales, FinalizeArgs& a) {
-  if (nscales < 1 || nscales > 3) return (int)hipErrorInvalidValue;
+  if (nscales < 1 || nscales > MAXSEG) return (int)hipErrorInvalidValue;
   int blocks = 0;
   for (int i = 0; i < nscales; ++i) {
     a.s[i] = scales[i];
@@ -1384,7 +1393,7 @@ struct MorphLaunch {
 
 static int morph_launch_config(const mcaq_morph_scale* scales, int nscales, const mcaq_finalize_scale* fscales,
                                int nfscales, MorphLaunch& L) {
-  if (nscales < 1 || nscales > 3) return (int)hipErrorInvalidValue;
+  if (nscales < 1 || nscales > MAXSEG) return (int)hipErrorInvalidValue;
   FinalizeArgs& fa = L.fa;
   fa = FinalizeArgs{};
   if (nfscales > 0) {
@@ -1628,7 +1637,7 @@ int mcaq_morph_pass(const mcaq_morph_scale* scales, int nscales, const mcaq_fina
 }
 
 int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream) {
-  if (nscales < 1 || nscales > 3) return (int)hipErrorInvalidValue;
+  if (nscales < 1 || nscales > MAXSEG) return (int)hipErrorInvalidValue;
   QuantArgs a;
   int units = 0;
   for (int i = 0; i < nscales; ++i) {

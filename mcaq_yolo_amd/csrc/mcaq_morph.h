@@ -64,19 +64,21 @@ enum : int {
 
 using MorphScale = mcaq_morph_scale;  // include/mcaq_hip.h
 
+constexpr int MORPH_MAXSEG = MCAQ_MAX_SEGMENTS;   // segments (hook scale x batch) per launch
+
 struct MorphArgs {
-  MorphScale s[3];
+  MorphScale s[MORPH_MAXSEG];
   int nscales;
   // pass A packing (set by the launcher): images per workgroup, LDS bytes per
   // image group (planes + shared, or shared only), plane bytes per image, and
-  // the first workgroup of each scale (wg_begin[nscales] = pass A workgroups)
-  int ipw[3], gstride[3], pstride[3], wg_begin[4];
+  // the first workgroup of each segment (wg_begin[nscales] = pass A workgroups)
+  int ipw[MORPH_MAXSEG], gstride[MORPH_MAXSEG], pstride[MORPH_MAXSEG], wg_begin[MORPH_MAXSEG + 1];
   // pass B packing: images per workgroup, LDS bytes per image, first workgroup
-  int tipw[3], tgstride[3], twg_begin[4];
-  // band mode of pass A (mcaq_band.h): first band / edge workgroup of each scale
-  int bwg_begin[4], ewg_begin[4];
-  // batch-wide pass B (mcaq_tiles_batch.h): first 64-tile workgroup of each scale
-  int tb_begin[4];
+  int tipw[MORPH_MAXSEG], tgstride[MORPH_MAXSEG], twg_begin[MORPH_MAXSEG + 1];
+  // band mode of pass A (mcaq_band.h): first band / edge workgroup of each segment
+  int bwg_begin[MORPH_MAXSEG + 1], ewg_begin[MORPH_MAXSEG + 1];
+  // batch-wide pass B (mcaq_tiles_batch.h): first 64-tile workgroup of each segment
+  int tb_begin[MORPH_MAXSEG + 1];
 };
 
 // bit planes

@@ -14,6 +14,19 @@ enqueues launches and can be captured into a HIP graph (torch.cuda.CUDAGraph);
 batched throughput comes from several plans' graphs replayed on as many
 streams (bench.py Runner).
 
+A launch takes up to abi.MAX_SEGMENTS segments, a segment being one hook scale
+of one batch.  `HookPlan(geoms, dev, batches=k)` is a LAUNCH SET: k independent
+batches (each with its own input, statistics, outputs and batch_offset /
+batch_total, exactly as if run alone) in one launch of each kernel, so every
+node of the chain carries k batches of streaming work while the per-image
+morphology latency stays that of one image.
+
+Batch-sharded runs (one process per GPU) keep every segment's channel
+statistics as [-min | max] in ONE contiguous buffer (`HookPlan.mm`): the
+finalize writes the negated min, pass 2 reads it back negated, and the only
+operation between them is one in-place MAX all-reduce of that buffer - an RCCL
+collective that can be captured inside the step's HIP graph.
+
 This module is the HIP path only: non-CUDA tensors or a missing library
 raise here.  CPU tensors take the pure-PyTorch path (fallback.py), which the
 modules in core.py / hooks.py dispatch to, as the reference does.
@@ -82,12 +95,20 @@ class ScaleGeom:
 class HookPlan:
     """Buffers + launch descriptors for a fixed set of hook-scale shapes.
 
-    want: subset of {"phi", "cmlp", "debug"} extra outputs."""
+    want: subset of {"phi", "cmlp", "debug"} extra outputs.
+    batches: independent batches of those shapes per launch (a launch set);
+    segment j is scale j // batches of batch j % batches (scale-major, so the
+    heaviest scale's segments start first in pass 1)."""
 
-    def __init__(self, geoms, device, want=()):
-        if not 1 <= len(geoms) <= 3:
-            raise ValueError("1..3 scales per launch")
-        self.geoms = list(geoms)
+    def __init__(self, geoms, device, want=(), batches=1):
+        nbat = int(batches)
+        if nbat < 1 or not 1 <= len(geoms) or len(geoms) * nbat > abi.MAX_SEGMENTS:
+            raise ValueError("1..%d segments (scales x batches) per launch, got %d x %d"
+                             % (abi.MAX_SEGMENTS, len(geoms), nbat))
+        self.scale_geoms = list(geoms)
+        self.batches = nbat
+        self.seg = [(si, k) for si in range(len(geoms)) for k in range(nbat)]
+        self.geoms = [geoms[si] for si, _ in self.seg]
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise RuntimeError("HookPlan needs a CUDA (HIP) device")
@@ -97,6 +118,12 @@ class HookPlan:
         # planes in global memory for every scale when one scale's planes
         # exceed the LDS budget (the mode is common to a launch's scales)
         glob = any(self.lib.mcaq_morph_scratch_bytes(g.B, g.Hc, g.Wc, g.ht, g.wt) for g in self.geoms)
+        # channel statistics of every segment in one buffer: [min | max] per
+        # segment, or [-min | max] when the plan runs batch-sharded (one MAX
+        # all-reduce of the whole buffer makes them global)
+        self.mm = torch.empty(2 * sum(g.C for g in self.geoms), device=d)
+        self._neg = False
+        mo = 0
         for g in self.geoms:
             units = self.lib.mcaq_stats_units(g.B, g.C, g.H, g.W)
             nb = {}
@@ -105,8 +132,9 @@ class HookPlan:
             nb["absmean"] = torch.empty(g.B, g.H, g.W, device=d)
             nb["pmin"] = torch.empty(units, g.C, device=d)
             nb["pmax"] = torch.empty(units, g.C, device=d)
-            nb["xmin"] = torch.empty(g.C, device=d)
-            nb["xmax"] = torch.empty(g.C, device=d)
+            nb["xmin"] = self.mm[mo:mo + g.C]           # holds -min in sharded runs
+            nb["xmax"] = self.mm[mo + g.C:mo + 2 * g.C]
+            mo += 2 * g.C
             nb["complexity"] = torch.empty(g.B, g.ht, g.wt, device=d)
             nb["bits"] = torch.empty(g.B, g.ht, g.wt, device=d)
             nb["mt"] = torch.empty(g.B, g.ht, g.wt, device=d)          # soft-mask tile values
@@ -129,12 +157,22 @@ class HookPlan:
             self.bufs.append(nb)
 
     # ------------------------------------------------------------------
+    def batch_bufs(self, k=0):
+        """Buffer dicts of batch k, in scale order."""
+        return [b for b, (_, kk) in zip(self.bufs, self.seg) if kk == k]
+
+    def channel_minmax(self, j):
+        """(min, max) of segment j as the quantizer used them."""
+        b = self.bufs[j]
+        return (-b["xmin"] if self._neg else b["xmin"]), b["xmax"]
+
     def run(self, feats, cmlp, mapper, smasks, stream=None, process_group=None, **kw):
         """Enqueue one step (prepare + launch).  feats: list of (B,C,H,W) fp32
-        CUDA tensors matching the plan.  cmlp/mapper: packed blobs (CUDA fp32);
-        smasks: one packed soft-mask blob per scale or None
-        (smooth_transitions=False).  Keyword options: see prepare().  Returns
-        the buffer dicts (overwritten by the next run)."""
+        CUDA tensors matching the plan (batches > 1: one such list per batch).
+        cmlp/mapper: packed blobs (CUDA fp32); smasks: one packed soft-mask
+        blob per scale or None (smooth_transitions=False).  Keyword options:
+        see prepare().  Returns the buffer dicts (overwritten by the next run)."""
+        kw.setdefault("shared_stats", process_group is not None)
         self.prepare(feats, cmlp, mapper, smasks, **kw)
         self.launch(stream, process_group)
         return self.bufs
@@ -142,7 +180,7 @@ class HookPlan:
     def prepare(self, feats, cmlp, mapper, smasks, temperature=1.0, mapper_kind="mlp", continuous=False,
                 normalize=False, minmax=None, batch_offset=0, batch_total=None, binarize_otsu=False,
                 contour_components=True, canny_legacy=False, min_bits=2.0, max_bits=8.0, quantize=True, hysteresis_iters=8,
-                per_tensor=False, softmax_threads=None, m_plane=False):
+                per_tensor=False, softmax_threads=None, m_plane=False, shared_stats=False):
         """Validate inputs and build the launch descriptors (pointers are baked
         in: the tensors must stay alive and in place until the last launch).
         A call with the same blobs, buffers and options as the previous one
@@ -155,7 +193,24 @@ class HookPlan:
         tile by its thread partition); default torch.get_num_threads().
         m_plane: pass B writes the soft-mask plane m(p) and pass 2 reads it,
         instead of pass 2 regenerating m(p) from the tile values per channel
-        slice (+4 B per pixel written, +4 B per pixel per slice read)."""
+        slice (+4 B per pixel written, +4 B per pixel per slice read).
+        shared_stats: the statistics of a batch-sharded run - the finalize
+        writes [-min | max] into `mm` and pass 2 reads the min negated, so
+        launch(process_group=...) combines them with ONE in-place all-reduce.
+        With batches > 1, feats is one list per batch; smasks and minmax are
+        per scale and shared by the batches."""
+        ns = len(self.scale_geoms)
+        if self.batches > 1:
+            if len(feats) != self.batches or any(len(fb) != ns for fb in feats):
+                raise ValueError("expected %d batches of %d feature maps" % (self.batches, ns))
+            feats = [feats[k][si] for si, k in self.seg]
+        if len(smasks) != ns:
+            raise ValueError("expected %d soft-mask blobs" % ns)
+        smasks = [smasks[si] for si, _ in self.seg]
+        if minmax is not None:
+            if len(minmax) != ns:
+                raise ValueError("expected %d minmax entries" % ns)
+            minmax = [minmax[si] for si, _ in self.seg]
         n = len(self.geoms)
         L = self.lib
         if m_plane:
@@ -176,13 +231,15 @@ class HookPlan:
             float(temperature if temperature is not None else 1.0), mapper_kind, bool(continuous), bool(normalize),
             int(batch_offset), batch_total, bool(binarize_otsu), bool(contour_components), bool(canny_legacy),
             float(min_bits), float(max_bits), bool(quantize), int(hysteresis_iters), bool(per_tensor),
-            int(softmax_threads) if softmax_threads else torch.get_num_threads(), bool(m_plane)))
+            int(softmax_threads) if softmax_threads else torch.get_num_threads(), bool(m_plane),
+            bool(shared_stats)))
         if sig is not None and sig == getattr(self, "_sig", None):
             self._rebind(feats)
             self._keep = (list(feats), cmlp, mapper, list(smasks), minmax)
             return
         self._sig = None
         self._keep = (list(feats), cmlp, mapper, list(smasks), minmax)
+        self._neg = bool(shared_stats) and quantize
         with_mask = [sm is not None for sm in smasks]
         # ---- pass 1
         st = (abi.StatsScale * n)()
@@ -204,6 +261,7 @@ class HookPlan:
                 s = fz[i]
                 s.C, s.nunits, s.min_stride = g.C, b["units"], 1
                 s.per_tensor = 1 if per_tensor else 0
+                s.neg_min = 1 if self._neg else 0
                 s.min_out, s.max_out = _p(b["xmin"]), _p(b["xmax"])
                 if minmax is not None and minmax[i] is not None:
                     lo, hi = minmax[i]
@@ -273,6 +331,7 @@ class HookPlan:
                 s.bits_lo, s.nbits = lo_b, nb
                 # batch statistics of this x (pass 1 + finalize, all-reduced or not)
                 s.stats_cover_x = 1 if (minmax is None or minmax[i] is None) else 0
+                s.neg_min = 1 if self._neg else 0
             self._qs = qs
         self._n = n
         self._sig = sig
@@ -332,8 +391,11 @@ class HookPlan:
     def launch(self, stream=None, process_group=None):
         """Enqueue the prepared step on `stream` (default: current stream).
         With a process group (batch sharded over ranks) the per-channel min/max
-        of every scale is combined by ONE all-reduce (max of [-min, max]) so
-        the quantizer sees the global-batch statistics of the reference."""
+        of every segment is combined by ONE all-reduce so the quantizer sees
+        the global-batch statistics of the reference: in place on `mm` when
+        the plan was prepared with shared_stats (no other op, capturable in a
+        HIP graph with the nccl / RCCL backend), else through
+        sync_channel_minmax."""
         L = self.lib
         n = self._n
         sh = _stream_handle(stream)
@@ -343,13 +405,20 @@ class HookPlan:
         nf = n if self._fz is not None else 0
         abi.check(L.mcaq_morph_finalize(self._mo, n, self._fz, nf, sh), "mcaq_morph_finalize")
         if self._fz is not None and process_group is not None:
-            # the collective runs on the launch stream: ordered after the
-            # finalize that writes xmin/xmax and before pass 2 that reads them
-            with torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream()):
-                sync_channel_minmax(self.bufs, process_group)
+            self.allreduce_stats(process_group, stream)
         if self._qs is not None:
             abi.check(L.mcaq_quant(self._qs, n, sh), "mcaq_quant")
         return self.bufs
+
+    def allreduce_stats(self, process_group, stream=None):
+        """The collective between the finalize (which writes the statistics)
+        and pass 2 (which reads them), on the launch stream."""
+        with torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream()):
+            if self._neg:
+                import torch.distributed as dist
+                dist.all_reduce(self.mm, op=dist.ReduceOp.MAX, group=process_group)
+            else:
+                sync_channel_minmax(self.bufs, process_group)
 
 
 def sync_channel_minmax(bufs, process_group):

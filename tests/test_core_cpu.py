@@ -143,6 +143,7 @@ def test_plan_descriptor_reuse_equals_rebuild(monkeypatch):
     shapes = ((2, 16, 80, 80), (2, 32, 40, 40), (2, 64, 20, 20))
     p = HookPlan.__new__(HookPlan)
     p.geoms = [ScaleGeom(*s, 8) for s in shapes]
+    p.scale_geoms, p.batches, p.seg = list(p.geoms), 1, [(i, 0) for i in range(len(shapes))]
     p.device = torch.device("cpu")
     p.lib = None
     p.bufs = []
@@ -173,7 +174,8 @@ def test_plan_descriptor_reuse_equals_rebuild(monkeypatch):
         return feats
 
     keep = []
-    for kw in ({}, {"temperature": 0.5, "per_tensor": True}, {"minmax": [(torch.empty(16), torch.empty(16)), None, None]}):
+    for kw in ({}, {"temperature": 0.5, "per_tensor": True}, {"minmax": [(torch.empty(16), torch.empty(16)), None, None]},
+               {"shared_stats": True}):
         feats = fresh_io()
         keep.append((feats, [dict(b) for b in p.bufs]))
         p.prepare(feats, cm, mm, sms, **kw)

@@ -71,3 +71,22 @@ def test_reference_cpp_linkage_symbol_exported():
     lib = ctypes.CDLL(abi.LIB_PATH)
     mangled = "_Z27launch_spatial_quantizationPKfS0_S0_S0_S0_PfiiiiiiiiP12ihipStream_t"
     assert hasattr(lib, mangled)
+
+
+def test_top_level_mcaq_cuda_ops_importable_fresh_process(tmp_path):
+    """`import mcaq_cuda_ops` - the reference's module name
+    (quantization.py:14-16) - resolves in a fresh process with only the
+    repository on the Python path (no install() call), and spatial_quantize
+    has the argument names / default of the reference's pybind11 binding
+    (ops/src/mcaq_ops.cpp:73-77).  No GPU needed: nothing is launched."""
+    import subprocess
+    import sys
+    code = ("import inspect, mcaq_cuda_ops; s = inspect.signature(mcaq_cuda_ops.spatial_quantize); "
+            "print(list(s.parameters)); print(s.parameters['mask'].default)")
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, "-c", code], cwd=str(tmp_path), env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = r.stdout.strip().splitlines()
+    assert lines[-2] == str(["input", "bit_map", "min_vals", "max_vals", "tile_h", "tile_w", "mask"])
+    assert lines[-1] == "None"
