@@ -282,5 +282,11 @@ class MCAQHooks(nn.Module):
                 outs.append(f if y is None else y)
             for st in streams:
                 main.wait_stream(st)
+            # outputs allocated on the side streams are used on the main one:
+            # the caching allocator must not hand their blocks back to the
+            # side streams' pools before the main stream is done with them
+            for f, y in zip(feats, outs):
+                if y is not f:
+                    y.record_stream(main)
             scope.finish()
         return outs

@@ -158,6 +158,10 @@ def _run_analyzer_multi(an, xs):
         if scratch:
             ptrs["gscratch"] = torch.empty(scratch, device=dev, dtype=torch.uint8)
             keep.append(ptrs["gscratch"])
+        wb = L.mcaq_morph_work_bytes(B, ht * T, wt * T, T) if core._engine.BAND_PASS else 0
+        if wb:
+            ptrs["pwork"] = torch.empty(wb // 4, device=dev)   # pass A as band + edge workgroups, as core.py
+            keep.append(ptrs["pwork"])
         morphs[i] = core._morph_struct(B, H, W, T, ht, wt, flags, **ptrs)
         outs.append(o)
     abi.check(L.mcaq_stats(stats, n, _stream()), "mcaq_stats")
@@ -197,7 +201,7 @@ class _HeadMulti(torch.autograd.Function):
             gcraw = torch.empty(m, device=dev)
             gp = torch.empty(L.mcaq_head_gpart_floats(m), device=dev)
             keep += [g, gcraw]
-            gparts.append((gp, (m + 63) // 64))
+            gparts.append((gp, gp.numel() // core._CM_SIZE))      # one partial per backward workgroup
             sg = segs[i]
             sg.phi, sg.craw, sg.gC, sg.gcraw, sg.gpart = _p(phis[i]), _p(craws[i]), _p(g), _p(gcraw), _p(gp)
             sg.B, sg.ht, sg.wt = B, ht, wt
@@ -304,7 +308,7 @@ class _MapperMulti(torch.autograd.Function):
             gp = torch.empty(L.mcaq_mapper_gpart_floats(m), device=dev)
             keep.append(g)
             gcs.append(gc)
-            gparts.append((gp, (m + 63) // 64))
+            gparts.append((gp, gp.numel() // core._MAPPER_G_SIZE))   # one partial per backward workgroup
             s = segs[i]
             s.c, s.work, s.gbits, s.gc, s.gpart, s.n = _p(cfs[i]), _p(works[i]), _p(g), _p(gc), _p(gp), m
         if ctx.pg is None:
@@ -454,8 +458,14 @@ class _QATMulti(torch.autograd.Function):
 def multi_ok(hooks, feats):
     """The multi-scale step covers train mode with the fused kernels on one
     device, an unsharded batch and the reference modules (mlp or linear mapper,
-    per-channel or per-tensor quantizers)."""
+    per-channel or per-tensor quantizers).  The mapper and every quantizer
+    must be in train mode themselves, as the multi-scale launches assume
+    (batch-statistics BatchNorm with running-stat updates, EMA statistics);
+    a module frozen with .eval() inside a training hook set takes the
+    per-scale modules, which follow each module's own flag."""
     if not (hooks.training and core.FUSED_TRAIN and len(feats) > 1):
+        return False
+    if not hooks.bit_mapper.training or not all(q.training for q in hooks.quantizers.values()):
         return False
     if not all(torch.is_tensor(f) and f.is_cuda and f.dim() == 4 for f in feats):
         return False

@@ -86,3 +86,37 @@ def test_multi_scale_step_quantize_off_and_frozen():
             hooks.MULTI_SCALE_TRAIN, hooks.CONCURRENT_TRAIN_SCALES = old
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+def test_frozen_mapper_in_training_hooks_takes_per_scale_path():
+    """hooks.train() with the bit mapper frozen by .eval(): the
+    multi-scale step must not run the train-mode mapper.  forward_features
+    then takes the per-scale modules, which follow the mapper's own flag
+    (running-statistics BatchNorm, no running-stat update): the bit maps and
+    outputs equal the per-scale path's and running_mean / running_var /
+    num_batches_tracked stay untouched."""
+    from mcaq_yolo_amd import hooks, train_step
+    feats, gens = _feats()
+    res = []
+    for multi in (True, False):
+        old = hooks.MULTI_SCALE_TRAIN, hooks.CONCURRENT_TRAIN_SCALES
+        hooks.MULTI_SCALE_TRAIN, hooks.CONCURRENT_TRAIN_SCALES = multi, False
+        try:
+            h = _hooks()
+            h.bit_mapper.eval()
+            assert not train_step.multi_ok(h, feats)
+            before = {k: v.clone() for k, v in h.bit_mapper.state_dict().items() if "running" in k or "num_batches" in k}
+            outs, aux = h.forward_features(feats, temperature=1.0)
+            sum((o * g).sum() for o, g in zip(outs, gens)).backward()
+            torch.cuda.synchronize()
+            after = h.bit_mapper.state_dict()
+            for k, v in before.items():
+                assert torch.equal(after[k], v), "%s changed with the mapper in eval mode" % k
+            res.append([a["bit_map"].detach().clone() for a in aux] + [o.detach().clone() for o in outs] +
+                       [f.grad.clone() for f in feats])
+            for f in feats:
+                f.grad = None
+        finally:
+            hooks.MULTI_SCALE_TRAIN, hooks.CONCURRENT_TRAIN_SCALES = old
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
