@@ -144,17 +144,26 @@ def main_qat(args, world, rank, dev, pg):
     gen = torch.Generator(device="cpu").manual_seed(77 + rank)
     G = [(1e-3 * torch.randn(f.shape, generator=gen)).to(dev) for f in feats]
     params_ = [p for p in h.parameters() if p.requires_grad]
-    # the reference's optimizer (train.py:140-150: AdamW, lr 1e-3, weight decay
-    # 0.05, betas 0.9 / 0.999) as torch's fused multi-tensor kernel, capturable
-    # (its step counters on the device) so the whole step replays as a graph
-    try:
-        opt = torch.optim.AdamW(params_, lr=1e-3, weight_decay=0.05, betas=(0.9, 0.999), fused=True,
-                                capturable=True)
-        opt_kind = "AdamW (fused, capturable)"
-    except (RuntimeError, TypeError, ValueError):
-        opt = torch.optim.AdamW(params_, lr=1e-3, weight_decay=0.05, betas=(0.9, 0.999), foreach=True,
-                                capturable=True)
-        opt_kind = "AdamW (foreach, capturable)"
+    # the reference's optimizer end of the step (train.py:140-150, 626-641:
+    # clip_grad_norm_ 1.0, AdamW lr 1e-3 weight decay 0.05 betas 0.9 / 0.999,
+    # the mapper's |W| projection): by default optim.ClipAdamW, all three in
+    # ONE launch; --torch-optim: torch's clip + fused capturable AdamW + the
+    # projection as separate kernels (~14 per step)
+    fused_opt = not args.torch_optim
+    if fused_opt:
+        from mcaq_yolo_amd.optim import ClipAdamW
+        opt = ClipAdamW(params_, lr=1e-3, weight_decay=0.05, betas=(0.9, 0.999), max_norm=1.0,
+                        project_abs=h.bit_mapper.constrained_weights())
+        opt_kind = "optim.ClipAdamW (clip_grad_norm 1.0 + AdamW + |W| projection, one launch)"
+    else:
+        try:
+            opt = torch.optim.AdamW(params_, lr=1e-3, weight_decay=0.05, betas=(0.9, 0.999), fused=True,
+                                    capturable=True)
+            opt_kind = "AdamW (fused, capturable) + clip_grad_norm_ 1.0 + enforce_weight_constraints"
+        except (RuntimeError, TypeError, ValueError):
+            opt = torch.optim.AdamW(params_, lr=1e-3, weight_decay=0.05, betas=(0.9, 0.999), foreach=True,
+                                    capturable=True)
+            opt_kind = "AdamW (foreach, capturable) + clip_grad_norm_ 1.0 + enforce_weight_constraints"
     target_bits = 4.0
 
     # how the train-mode mapper ran (fused kernels, or the torch autograd path)
@@ -182,9 +191,12 @@ def main_qat(args, world, rank, dev, pg):
         if pg is not None:
             from mcaq_yolo_amd.dist import allreduce_gradients
             allreduce_gradients(params_, pg)           # one flat bucket over RCCL
-        torch.nn.utils.clip_grad_norm_(params_, max_norm=1.0)
-        opt.step()
-        h.bit_mapper.enforce_weight_constraints()
+        if fused_opt:
+            opt.step()
+        else:
+            torch.nn.utils.clip_grad_norm_(params_, max_norm=1.0)
+            opt.step()
+            h.bit_mapper.enforce_weight_constraints()
 
     # warm up on a side stream (lazy state: running stats, momentum buffers),
     # then (N = 1) capture the whole step - forward, backward, clip, AdamW,
@@ -196,7 +208,10 @@ def main_qat(args, world, rank, dev, pg):
             step()
     torch.cuda.current_stream().wait_stream(side)
     torch.cuda.synchronize()
-    use_graph = pg is None and not args.eager
+    # N > 1 on the nccl (RCCL) backend: the step's collectives (EMA min/max,
+    # the mapper's BatchNorm statistics, the gradient bucket) are captured in
+    # the graph too; gloo (the CPU-collective rehearsal) runs eagerly
+    use_graph = (pg is None or _backend(pg) == "nccl") and not args.eager
     run = step
     if use_graph:
         graph = torch.cuda.CUDAGraph()
@@ -310,8 +325,9 @@ def main_qat(args, world, rank, dev, pg):
                                    "continuous bits, STE, stage-3 temperature 1); YOLOv8 network excluded"
                                    % (name, B, grid, mapper),
                        "global_batch": world * B, "parallelism": "dp%d" % world, "hip_graph": use_graph,
+                       "rccl_in_graph": use_graph and pg is not None,
                        "scales": _qat_scales_mode(h, feats),
-                       "optimizer": opt_kind + ", clip_grad_norm 1.0, |W| projection (train.py:626-641)",
+                       "optimizer": opt_kind + " (train.py:626-641)",
                        "host_enqueue_us_per_step": round(t_enq / args.steps * 1e6, 1),
                        "single_step_latency_us": round(t_one * 1e6, 1),
                        "single_step_enqueue_us": round(t_one_enq * 1e6, 1)},
@@ -501,6 +517,77 @@ def run_e2e(cfg, steps, warmup, world, rank, dev, pg, amp=False, eager=False, fu
                    "hook_share_of_step": round((step_s - net_s) / step_s, 4),
                    "detections_per_image": round(float(cnt.float().mean()), 2)},
     }
+
+
+def main_score(args, world, rank, dev, pg):
+    """Curriculum scoring of a dataset (SURVEY 8(f) rank 4,
+    utils/dataset.py:276-401 tensor path): 640x640 RGB images (0..255
+    values, as a dataset yields them) scored `--score-batch` at a time by
+    mcaq_yolo_amd.dataset.score_batch - per-image /255, phi kernel with every
+    image as its own batch of one, Eq.(8) dot and tile mean - with the images
+    already resident in HBM.  cpu_baseline: the same per-image scores through
+    the pure-PyTorch path (the reference's algorithm, one image per call as
+    the reference loops) on the host's threads."""
+    from mcaq_yolo_amd import core
+    from mcaq_yolo_amd.dataset import score_batch
+    import numpy as np
+    bs = max(1, args.score_batch)
+    torch.manual_seed(0)
+    w = np.load(os.path.join(ROOT, "tests", "golden", "weights.npz"))
+    sd = {k[len("complexity_analyzer."):]: torch.from_numpy(np.array(w[k])) for k in w.files
+          if k.startswith("complexity_analyzer.")}
+    a = core.MorphologicalComplexityAnalyzer(device=dev, grid_size=8)
+    a.load_state_dict(sd)
+    a = a.to(dev).eval()
+    g = torch.Generator(device="cpu").manual_seed(31 + rank)
+    nb = 3
+    xs = [(torch.rand(bs, 3, 640, 640, generator=g) * 255).round().to(dev) for _ in range(nb)]
+    out = torch.empty(args.steps + args.warmup, bs, device=dev)
+    for i in range(max(args.warmup, 1)):
+        out[i % out.shape[0]] = score_batch(a, xs[i % nb])
+    torch.cuda.synchronize()
+    if pg is not None:
+        import torch.distributed as dist
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        out[i] = score_batch(a, xs[i % nb])
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.steps
+    if pg is not None:
+        import torch.distributed as dist
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    res = {"metric": "images/sec curriculum scoring @640x640 (compute_dataset_complexity tensor path), MI355X",
+           "value": round(world * bs / dt, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(dt * 1e3, 4), "higher_is_better": True, "scaling": "weak",
+           "vs_baseline": None, "dtype": "f32", "data": "synthetic 0..255 RGB 640x640 images, seeded analyzer",
+           "config": {"workload": "score_batch of %d images 640x640x3 (grid 8: tile 64, 10x10 tiles; planes in "
+                                  "global scratch), scores kept on the device" % bs,
+                      "global_batch": world * bs, "parallelism": "dp%d" % world},
+           "cpu_baseline": None}
+    if rank == 0 and not args.no_cpu and world == 1:
+        threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+        torch.set_num_threads(threads)
+        ac = core.MorphologicalComplexityAnalyzer(device="cpu", grid_size=8)
+        ac.load_state_dict(sd)
+        ac.eval()
+        xc = xs[0][:4].cpu()
+        t0 = time.perf_counter()
+        n = 0
+        while time.perf_counter() - t0 < 10.0:
+            score_batch(ac, xc[n % 4:n % 4 + 1])
+            n += 1
+        dtc = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": round(n / dtc, 3), "unit": "images/s", "cores": torch.get_num_threads(),
+                               "kind": "port", "sample": "%d images 640x640, one per call (as the reference's loop), "
+                               "pure-PyTorch path (fallback.py), %.1f s" % (n, dtc)}
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if pg is not None:
+        import torch.distributed as dist
+        dist.destroy_process_group()
 
 
 def main_e2e(args, world, rank, dev, pg):
@@ -699,6 +786,11 @@ def main():
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (YOLOv8 + hooks + NMS) leg")
     ap.add_argument("--e2e", action="store_true", help="only the end-to-end line (run_e2e)")
+    ap.add_argument("--torch-optim", action="store_true",
+                    help="--config 5: torch clip_grad_norm_ + fused AdamW + projection instead of optim.ClipAdamW")
+    ap.add_argument("--score", action="store_true",
+                    help="only the curriculum-scoring line (compute_dataset_complexity tensor path, 640x640 images)")
+    ap.add_argument("--score-batch", type=int, default=32, help="--score: images per launch")
     ap.add_argument("--e2e-inflight", type=int, default=2,
                     help="end-to-end leg: batches in flight on as many HIP streams (one graph each)")
     ap.add_argument("--amp", action="store_true", help="--e2e: network under bf16 autocast (hooks stay fp32)")
@@ -743,18 +835,26 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     pg = None
-    if world > 1:
+    # MCAQ_BENCH_SHARDED=1 at N = 1: run the batch-sharded code path anyway
+    # (a world_size 1 process group: the RCCL collectives captured in the
+    # step's graph), to measure what N > 1 adds per step on one GPU
+    if world > 1 or os.environ.get("MCAQ_BENCH_SHARDED") == "1":
         import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29517")
+        os.environ.setdefault("RANK", "0")
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, rank=rank, world_size=world)
         pg = dist.group.WORLD
 
     if args.config == 5:
         return main_qat(args, world, rank, dev, pg)
     if args.e2e:
         return main_e2e(args, world, rank, dev, pg)
+    if args.score:
+        return main_score(args, world, rank, dev, pg)
     name, B, chans, grid, mapper = CONFIGS[args.config]
     depth = max(1, args.pipeline)
     nbat = max(1, args.launch_batches)
@@ -895,6 +995,7 @@ def main():
                        "pass_b": "batch-wide tile kernels" if _engine_mod().TILES_BATCH else "per-image workgroups",
                        "hip_graph": use_graph,
                        "rccl_in_graph": runner.captured_collective,
+                       "sharded_code_path": pg is not None,
                        "batches_per_launch": nbat,
                        "launch_sets_in_flight": depth,
                        "batches_in_flight": depth * nbat,

@@ -106,7 +106,10 @@ int mcaq_finalize(const mcaq_finalize_scale* scales, int nscales, hipStream_t st
 /* ---- morph: one workgroup per image --------------------------------------
  * flags: 1 phi, 2 complexity MLP + bilateral, 4 mapper, 8 soft mask,
  * 16 continuous bits, 32 temperature given, 64 normalise C, 128 linear mapper,
- * 256 Otsu binarize, 512 no Euler correction.  Parameter blobs are the packed
+ * 256 Otsu binarize, 512 no Euler correction, 1024 legacy Canny, 2048 per-image
+ * pass B, 4096 every image its own batch of one (batch_offset / batch_total
+ * ignored: the reference's batch-1 calls, as compute_dataset_complexity
+ * makes them - one launch scores many images).  Parameter blobs are the packed
  * reference state_dict tensors (mcaq_yolo_amd/params.py), 16-byte aligned and
  * zero-padded to a multiple of 4 floats (they are staged with 16-byte loads). */
 typedef struct {
@@ -445,6 +448,27 @@ typedef struct {
   int n, k, mode, dst;
 } mcaq_pack_seg;
 int mcaq_pack(const mcaq_pack_seg* segs, int nseg, float* out, int total, hipStream_t stream);
+
+/* ---- the optimizer end of a QAT step in ONE launch ------------------------
+ * torch.nn.utils.clip_grad_norm_(max_norm) over every segment's gradient
+ * (the norm of the per-tensor 2-norms; .grad scaled in place), then
+ * torch.optim.AdamW (decoupled weight decay, the fused kernel's update
+ * order; *step += 1 first, as a capturable AdamW's step tensor) and, for
+ * segments with project_abs, p <- |p| (the bit mapper's Eq. 18 projection,
+ * bit_allocation.py:186-197) - train.py:626-641.  max_norm <= 0: no clip;
+ * total_norm (1 float) receives the pre-clip norm, or NULL.  One 1024-thread
+ * workgroup (the hook parameters are ~8 k floats). */
+#define MCAQ_OPT_MAXSEG 64
+#define MCAQ_OPT_MAXGROUPS 4
+typedef struct {
+  float* param; float* grad; float* exp_avg; float* exp_avg_sq;
+  int n, project_abs, group;   /* group: index into the hyper-parameter table */
+} mcaq_adamw_seg;
+typedef struct {
+  double lr, weight_decay, beta1, beta2, eps;   /* doubles, as torch's fused AdamW takes them */
+} mcaq_adamw_group;
+int mcaq_clip_adamw(const mcaq_adamw_seg* segs, int nseg, const mcaq_adamw_group* groups, int ngroups,
+                    float* step, float max_norm, float* total_norm, hipStream_t stream);
 
 int mcaq_abi_version(void);
 

@@ -98,6 +98,20 @@ class ReduceSeg(ctypes.Structure):
     _fields_ = [("part", P), ("out", P), ("nparts", I), ("stride", I), ("count", I), ("accumulate", I)]
 
 
+MCAQ_OPT_MAXSEG, MCAQ_OPT_MAXGROUPS = 64, 4
+
+
+class AdamwSeg(ctypes.Structure):
+    """mcaq_adamw_seg."""
+    _fields_ = [("param", P), ("grad", P), ("exp_avg", P), ("exp_avg_sq", P), ("n", I), ("project_abs", I),
+                ("group", I)]
+
+
+class AdamwGroup(ctypes.Structure):
+    """mcaq_adamw_group."""
+    _fields_ = [(k, ctypes.c_double) for k in ("lr", "weight_decay", "beta1", "beta2", "eps")]
+
+
 class EmaSeg(ctypes.Structure):
     """mcaq_ema_seg."""
     _fields_ = [("batch_min", P), ("batch_max", P), ("running_min", P), ("running_max", P), ("copy_min", P),
@@ -109,6 +123,7 @@ F_PHI, F_CMLP, F_MAPPER, F_SOFTMASK = 1, 2, 4, 8
 F_CONT, F_HAS_T, F_NORM_C, F_MAP_LINEAR = 16, 32, 64, 128
 F_BIN_OTSU, F_NO_EULER, F_CANNY_LEGACY = 256, 512, 1024
 F_TILES_IMAGE = 2048   # force the per-image pass B
+F_IMAGE_BATCH = 4096   # each image as its own batch of one (the reference's batch-1 calls)
 
 EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats", "mcaq_stats_units",
            "mcaq_finalize", "mcaq_morph", "mcaq_morph_finalize", "mcaq_morph_scratch_bytes", "mcaq_morph_scratch_bytes_global", "mcaq_morph_work_bytes",
@@ -123,7 +138,7 @@ EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats",
            "mcaq_mapper_train_grad_reduce", "mcaq_mapper_running_update", "mcaq_head_train_grad_reduce",
            "mcaq_mapper_train_forward_multi", "mcaq_mapper_train_backward_multi", "mcaq_head_train_backward_multi",
            "mcaq_smask_train_backward_multi", "mcaq_train_reduce_multi", "mcaq_ema_stats_multi",
-           "mcaq_mapper_train_forward_stage_multi", "mcaq_mapper_train_backward_stage_multi")
+           "mcaq_mapper_train_forward_stage_multi", "mcaq_mapper_train_backward_stage_multi", "mcaq_clip_adamw")
 
 _LIB = None
 
@@ -217,6 +232,8 @@ def _declare(lib):
     lib.mcaq_ema_stats_ex.argtypes = [P, P, P, P, I, ctypes.c_double, I, P, P, P, P]
     lib.mcaq_pack.restype = I
     lib.mcaq_pack.argtypes = [ctypes.POINTER(PackSeg), I, P, I, P]
+    lib.mcaq_clip_adamw.restype = I
+    lib.mcaq_clip_adamw.argtypes = [ctypes.POINTER(AdamwSeg), I, ctypes.POINTER(AdamwGroup), I, P, Fl, P, P]
     lib.mcaq_smask_train_backward.restype = I
     lib.mcaq_smask_train_backward.argtypes = [ctypes.POINTER(SmaskParams), P, P, P, I, I, I, I, I, P, I, P, P, P]
     return lib

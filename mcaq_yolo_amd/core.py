@@ -364,7 +364,7 @@ class MorphologicalComplexityAnalyzer(nn.Module):
         ps = [p for p in self.complexity_mlp.parameters()]
         return self._blob.get(ps, lambda: _pack_cmlp(self.complexity_mlp))
 
-    def _run(self, features, want_c, want_craw=False):
+    def _run(self, features, want_c, want_craw=False, image_batch=False):
         _need_cuda(features, "features")
         if features.dim() != 4:
             raise ValueError("features must be (B, C, H, W)")
@@ -387,7 +387,7 @@ class MorphologicalComplexityAnalyzer(nn.Module):
         else:
             _run_stats(x, gray=gray, Hc=ht * T, Wc=wt * T)
         phi = torch.empty(B, ht, wt, 8, device=dev)
-        flags = abi.F_PHI | self._flags()
+        flags = abi.F_PHI | self._flags() | (abi.F_IMAGE_BATCH if image_batch else 0)
         ptrs = dict(gray=gray, phi_out=phi, tile_tmp=torch.empty(B, ht * wt, 32, device=dev))
         L = abi.lib()
         if want_c:
@@ -413,21 +413,31 @@ class MorphologicalComplexityAnalyzer(nn.Module):
         return {"fractal": phi[..., 0], "texture": phi[..., 1], "gradient": phi[..., 2],
                 "edge": phi[..., 3], "contour": phi[..., 4]}
 
-    def compute_phi_tiles(self, features: torch.Tensor):
-        """morphology.py:798-824: (phi (B,ht,wt,8), detailed dict of phi1..phi5)."""
+    def compute_phi_tiles(self, features: torch.Tensor, image_batch: bool = False):
+        """morphology.py:798-824: (phi (B,ht,wt,8), detailed dict of phi1..phi5).
+        image_batch=True: every image as the reference's batch-1 call would
+        see it (a few ATen reductions follow the tile's position in the whole
+        batch) - one launch for the batch on the GPU."""
         if not features.is_cuda:
-            phi = fallback.phi_tiles(features, self.grid_size, self.canny_impl, self.binarize_impl,
-                                     self.contour_components)
+            if image_batch and features.shape[0] > 1:
+                phi = torch.cat([fallback.phi_tiles(features[i:i + 1], self.grid_size, self.canny_impl,
+                                                    self.binarize_impl, self.contour_components)
+                                 for i in range(features.shape[0])])
+            else:
+                phi = fallback.phi_tiles(features, self.grid_size, self.canny_impl, self.binarize_impl,
+                                         self.contour_components)
         else:
-            phi, _ = self._run(features, want_c=False)
+            phi, _ = self._run(features, want_c=False, image_batch=image_batch)
         return phi, self._detailed(phi)
 
-    def score_image(self, features: torch.Tensor) -> torch.Tensor:
+    def score_image(self, features: torch.Tensor, image_batch: bool = False) -> torch.Tensor:
         """morphology.py:923-937: per-image Eq.(8) score for curriculum sorting,
         mean over tiles of sum_i alpha_i * phi_i (alpha = |feature_weights|
         normalised to sum 1), clamped to [0, 1].  phi comes from the morph
-        kernel; the 5-term dot product is a (B, ht, wt) device reduction."""
-        phi, _ = self.compute_phi_tiles(features)
+        kernel; the 5-term dot product is a (B, ht, wt) device reduction.
+        image_batch: score every image as its own batch-1 call
+        (compute_phi_tiles)."""
+        phi, _ = self.compute_phi_tiles(features, image_batch=image_batch)
         with torch.no_grad():
             alpha = self.feature_weights.detach().abs().to(phi.device)
             alpha = alpha / alpha.sum().clamp(min=1e-8)
@@ -576,6 +586,9 @@ class LinearBitMapper(nn.Module):
             raise NotImplementedError("eps_spread other than the reference default 1e-3")
         self.eps_spread = float(eps_spread)
 
+    def constrained_weights(self):
+        return []
+
     def enforce_weight_constraints(self):
         """No-op (parameter-free), as in the reference."""
 
@@ -641,6 +654,15 @@ class ComplexityToBitMappingNetwork(nn.Module):
                 m.weight.data = torch.abs(m.weight.data)
             if m.bias is not None:
                 nn.init.constant_(m.bias, 0.1)
+
+    def constrained_weights(self):
+        """The parameters enforce_weight_constraints projects onto |W| (Linear
+        weights and BatchNorm gammas; none without enforce_monotonicity) -
+        for optim.ClipAdamW(project_abs=...), which folds the projection into
+        the optimizer launch."""
+        if not self.enforce_monotonicity:
+            return []
+        return [m.weight for m in self.mapping_network.modules() if isinstance(m, (nn.Linear, nn.BatchNorm1d))]
 
     def enforce_weight_constraints(self):
         """Eq.18: |W| for Linear layers and BatchNorm gammas (bit_allocation.py:186-197)."""

@@ -785,7 +785,7 @@ __global__ __launch_bounds__(64) void mcaq_tb_mask_kernel(MorphArgs a) {
   }
   const float den = amax + 1e-8f;
   const float* row = S.tile_tmp + (size_t)b * NT * TT_STRIDE;
-  const bool vl = aten_softmax_vec_lane((long long)(S.batch_offset + b) * NT + t, (long long)S.batch_total * NT, NT,
+  const bool vl = aten_softmax_vec_lane((long long)img_global(S, b) * NT + t, (long long)img_batch_total(S) * NT, NT,
                                         S.softmax_threads);
   const float mtv = smask_tile(
       S.smask, th, tw, S.ht, S.wt,
@@ -1749,6 +1749,7 @@ int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream) 
 #include "mcaq_qat.h"
 #include "mcaq_nms.h"
 #include "mcaq_train.h"
+#include "mcaq_optim.h"
 
 // C++-linkage drop-in for the reference's declaration (include/mcaq_hip.h):
 // same name, argument list and void return as MCAQPlugin.cpp:15-23.  An

@@ -60,9 +60,17 @@ enum : int {
   F_NO_EULER = 512,   // contour_components=False
   F_CANNY_LEGACY = 1024,  // canny_impl='legacy'
   F_TILES_IMAGE = 2048,   // pass B per image (morph_tiles) even where the batch-wide tile kernels apply
+  F_IMAGE_BATCH = 4096,   // every image as its own batch of one (batch_offset 0, batch_total 1): the
+                          // values of the reference's batch-1 calls (compute_dataset_complexity)
 };
 
+
 using MorphScale = mcaq_morph_scale;  // include/mcaq_hip.h
+
+// global position of image b in the batch whose ATen reductions the kernels
+// reproduce, and that batch's size (F_IMAGE_BATCH: each image alone)
+MCAQ_HD int img_global(const MorphScale& S, int b) { return (S.flags & F_IMAGE_BATCH) ? 0 : S.batch_offset + b; }
+MCAQ_HD int img_batch_total(const MorphScale& S) { return (S.flags & F_IMAGE_BATCH) ? 1 : S.batch_total; }
 
 constexpr int MORPH_MAXSEG = MCAQ_MAX_SEGMENTS;   // segments (hook scale x batch) per launch
 
@@ -1374,7 +1382,7 @@ MCAQ_HD void phi_of_tile(const MorphScale& S, int b, int t, const float* tv, flo
   // phi1: weighted log-log regression slope (morphology.py:596-621)
   float p1;
   if (S_ >= 2) {
-    const int ycut = aten_tail_start(S.batch_total * NT);
+    const int ycut = aten_tail_start(img_batch_total(S) * NT);
     float xs[8], ws[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
@@ -1384,7 +1392,7 @@ MCAQ_HD void phi_of_tile(const MorphScale& S, int b, int t, const float* tv, flo
     const float w_sum = bits_as_float(k_frac_st_bits[4 * S_ + 0]);
     const float x_mean = bits_as_float(k_frac_st_bits[4 * S_ + 1]);
     const float var = bits_as_float(k_frac_st_bits[4 * S_ + 2]);
-    const bool tail = ((S.batch_offset + b) * NT + t) >= ycut;
+    const bool tail = (img_global(S, b) * NT + t) >= ycut;
     float ys[8], wy[8], cv[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) ys[i] = i < S_ ? tv[4 + i] : 0.0f;
@@ -1826,8 +1834,8 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
       const float mxl = fmax_(l0, l1);
       const bool first = l0 >= l1;
       const float ea = (first ? l1 : l0) - mxl;
-      const bool vl = aten_softmax_vec_lane((long long)(S.batch_offset + b) * NT + t,
-                                            (long long)S.batch_total * NT, NT, S.softmax_threads);
+      const bool vl = aten_softmax_vec_lane((long long)img_global(S, b) * NT + t,
+                                            (long long)img_batch_total(S) * NT, NT, S.softmax_threads);
       const float e = vl ? sleef_expf(ea) : cr_exp(ea);
       const float e0 = first ? 1.0f : e, e1 = first ? e : 1.0f;
       const float mtv = e0 / (e0 + e1);

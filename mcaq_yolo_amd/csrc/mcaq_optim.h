@@ -1,0 +1,208 @@
+// mcaq_optim.h - the optimizer end of the QAT training step in ONE launch:
+// global gradient-norm clip (torch.nn.utils.clip_grad_norm_), AdamW with
+// decoupled weight decay (torch.optim.AdamW) and the |W| projection of the
+// bit mapper (bit_allocation.py:186-197, Eq. 18) - train.py:626-641 issues
+// them as ~14 small ATen / multi-tensor kernels per step on ~8 k floats of
+// hook parameters.
+//
+// One 1024-thread workgroup over the flat concatenation of the segments
+// (parameter tensors), 4 K elements per chunk: the squared gradients of a
+// chunk are staged in LDS and each wave sums its segments' parts in a fixed
+// order (per-tensor norms; thread 0 combines them in tensor order into the
+// total norm, the norm of the per-tensor norms as clip_grad_norm_ computes
+// it); then every thread loads its 4 elements of a chunk (gradient,
+// parameter, both moments) before clipping, updating and projecting them.  The per-element update is torch's fused AdamW
+// arithmetic (double hyper-parameters); the norm reduces in another order
+// than ATen's, so the values agree with torch's clip + fused AdamW within
+// fp32 rounding (tests/test_optim_gpu.py), not bit for bit.
+#pragma once
+
+namespace mcaq {
+
+static_assert(sizeof(mcaq_adamw_seg) * MCAQ_OPT_MAXSEG + sizeof(mcaq_adamw_group) * MCAQ_OPT_MAXGROUPS + 64 <= 4096,
+              "optimizer kernel arguments exceed 4 KiB");
+
+struct AdamwArgs {
+  mcaq_adamw_seg s[MCAQ_OPT_MAXSEG];
+  mcaq_adamw_group g[MCAQ_OPT_MAXGROUPS];
+  int nseg, total;     // segments; elements over all segments
+  float* step;         // device step counter (float, like torch's capturable AdamW)
+  float max_norm;      // <= 0: no clipping
+  float* total_norm;   // or nullptr
+};
+
+constexpr int OPT_TH = 1024;
+constexpr int OPT_R = 4;                   // elements per thread per chunk
+constexpr int OPT_CH = OPT_TH * OPT_R;     // elements per chunk (staged squares in LDS)
+
+// segment of flat element j: the last segment whose start is <= j (starts in LDS)
+__device__ __forceinline__ int opt_seg_of(const int* st, int nseg, int j) {
+  int lo = 0, hi = nseg - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (st[mid] <= j) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ __launch_bounds__(OPT_TH) void mcaq_clip_adamw_kernel(AdamwArgs a) {
+  __shared__ float sq[OPT_CH];
+  __shared__ float seg_acc[MCAQ_OPT_MAXSEG];
+  __shared__ int st[MCAQ_OPT_MAXSEG + 1];
+  __shared__ mcaq_adamw_seg sg[MCAQ_OPT_MAXSEG];
+  __shared__ float coef_s;
+  __shared__ float g_bc2s[MCAQ_OPT_MAXGROUPS], g_ss[MCAQ_OPT_MAXGROUPS];
+  __shared__ double g_hp[MCAQ_OPT_MAXGROUPS][6];   // lr * wd, beta1, 1 - beta1, beta2, 1 - beta2, eps
+  const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  constexpr int NW = OPT_TH / 64;
+  const int nseg = a.nseg, total = a.total;
+  // the segment table in LDS (per-lane lookups; a per-lane index into the
+  // kernel-argument array would go through scratch)
+  if (tid < nseg) {
+    sg[tid] = a.s[tid];
+    seg_acc[tid] = 0.0f;
+  }
+  if (tid == 0) {
+    int o = 0;
+    for (int k = 0; k < nseg; ++k) { st[k] = o; o += a.s[k].n; }
+    st[nseg] = o;
+  }
+  __syncthreads();
+  const bool clip = a.max_norm > 0.0f;
+  // ---- per-tensor squared-gradient sums, a chunk of 4 K elements at a time:
+  // squares staged in LDS, then each wave sums the parts of its segments
+  // (w, w + 16, ...) in the chunk in a fixed order - deterministic
+  if (clip) {
+    for (int base = 0; base < total; base += OPT_CH) {
+      float v[OPT_R];
+#pragma unroll
+      for (int r = 0; r < OPT_R; ++r) {
+        const int j = base + tid + r * OPT_TH;
+        v[r] = 0.0f;
+        if (j < total) {
+          const int k = opt_seg_of(st, nseg, j);
+          v[r] = sg[k].grad[j - st[k]];
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < OPT_R; ++r) sq[tid + r * OPT_TH] = v[r] * v[r];
+      __syncthreads();
+      for (int k = wv; k < nseg; k += NW) {
+        const int lo = st[k] > base ? st[k] : base;
+        const int hi = st[k + 1] < base + OPT_CH ? st[k + 1] : base + OPT_CH;
+        if (lo >= hi) continue;
+        float acc = 0.0f;
+        for (int i = lo + lane; i < hi; i += 64) acc += sq[i - base];
+        for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+        if (lane == 0) seg_acc[k] += acc;
+      }
+      __syncthreads();
+    }
+    if (tid == 0) {
+      // the norm of the per-tensor norms (clip_grad_norm_), in tensor order
+      float tot = 0.0f;
+      for (int k = 0; k < nseg; ++k) {
+        const float nk = sqrtf(seg_acc[k]);
+        tot = fmaf(nk, nk, tot);
+      }
+      tot = sqrtf(tot);
+      if (a.total_norm) a.total_norm[0] = tot;
+      const float c = a.max_norm / (tot + 1e-6f);
+      coef_s = c < 1.0f ? c : 1.0f;   // clamp(max=1.0); NaN propagates as in torch
+      if (!(c == c)) coef_s = c;
+    }
+  } else if (tid == 0) {
+    coef_s = 1.0f;
+  }
+  const float step = a.step[0] + 1.0f;
+  if (tid < MCAQ_OPT_MAXGROUPS) {
+    // bias corrections of each hyper-parameter group (fused AdamW: fp32
+    // values of the double expressions)
+    const mcaq_adamw_group& G = a.g[tid];
+    const float bc1 = (float)(1.0 - pow(G.beta1, (double)step));
+    g_bc2s[tid] = sqrtf((float)(1.0 - pow(G.beta2, (double)step)));
+    g_ss[tid] = (float)(G.lr / (double)bc1);
+    g_hp[tid][0] = G.lr * G.weight_decay;
+    g_hp[tid][1] = G.beta1; g_hp[tid][2] = 1.0 - G.beta1;
+    g_hp[tid][3] = G.beta2; g_hp[tid][4] = 1.0 - G.beta2;
+    g_hp[tid][5] = G.eps;
+  }
+  __syncthreads();
+  const float coef = coef_s;
+  // ---- AdamW per element, then |W|.  The arithmetic of torch's
+  // _fused_adamw_ (adam_math, fused_adam_utils.cuh): hyper-parameters are
+  // doubles, so the weight decay and both moment updates are evaluated in
+  // double and rounded once to fp32 (an fp32 1 - beta2 alone is 1.3e-5 off);
+  // step size and denominator are fp32 values, the final update fp32.
+  // Every element of a chunk is loaded before any is updated.
+  for (int base = 0; base < total; base += OPT_CH) {
+    float gv[OPT_R], pv[OPT_R], mv[OPT_R], vv[OPT_R];
+    int kk[OPT_R];
+#pragma unroll
+    for (int r = 0; r < OPT_R; ++r) {
+      const int j = base + tid + r * OPT_TH;
+      const int k = opt_seg_of(st, nseg, j < total ? j : total - 1);
+      const int e = (j < total ? j : total - 1) - st[k];
+      kk[r] = k;
+      gv[r] = sg[k].grad[e]; pv[r] = sg[k].param[e]; mv[r] = sg[k].exp_avg[e]; vv[r] = sg[k].exp_avg_sq[e];
+    }
+#pragma unroll
+    for (int r = 0; r < OPT_R; ++r) {
+      const int j = base + tid + r * OPT_TH;
+      if (j >= total) continue;
+      const int k = kk[r], e = j - st[k];
+      const mcaq_adamw_seg& S = sg[k];
+      const int gi = S.group;
+      const float bc2s = g_bc2s[gi], step_size = g_ss[gi];
+      const double* hp = g_hp[gi];
+      float g = gv[r];
+      if (clip) {
+        g = g * coef;
+        S.grad[e] = g;             // clip_grad_norm_ scales .grad in place
+      }
+      float p = pv[r];
+      p = (float)((double)p - hp[0] * (double)p);
+      const float m = (float)(hp[1] * (double)mv[r] + hp[2] * (double)g);
+      const float v = (float)(hp[3] * (double)vv[r] + hp[4] * (double)g * (double)g);
+      const float denom = (float)((double)(sqrtf(v) / bc2s) + hp[5]);
+      p = p - step_size * m / denom;
+      if (S.project_abs) p = fabsf(p);
+      S.exp_avg[e] = m;
+      S.exp_avg_sq[e] = v;
+      S.param[e] = p;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) a.step[0] = step;
+}
+
+}  // namespace mcaq
+
+extern "C" {
+
+int mcaq_clip_adamw(const mcaq_adamw_seg* segs, int nseg, const mcaq_adamw_group* groups, int ngroups,
+                    float* step, float max_norm, float* total_norm, hipStream_t stream) {
+  using namespace mcaq;
+  if (!segs || !groups || !step || nseg < 1 || nseg > MCAQ_OPT_MAXSEG || ngroups < 1 || ngroups > MCAQ_OPT_MAXGROUPS)
+    return (int)hipErrorInvalidValue;
+  AdamwArgs a{};
+  for (int k = 0; k < nseg; ++k) {
+    const mcaq_adamw_seg& g = segs[k];
+    if (!g.param || !g.grad || !g.exp_avg || !g.exp_avg_sq || g.n < 1 || g.group < 0 || g.group >= ngroups)
+      return (int)hipErrorInvalidValue;
+    a.s[k] = g;
+  }
+  for (int k = 0; k < ngroups; ++k) a.g[k] = groups[k];
+  a.nseg = nseg;
+  long long tot = 0;
+  for (int k = 0; k < nseg; ++k) tot += segs[k].n;
+  if (tot > 0x7fffffff) return (int)hipErrorInvalidValue;
+  a.total = (int)tot;
+  a.step = step;
+  a.max_norm = max_norm;
+  a.total_norm = total_norm;
+  hipLaunchKernelGGL(mcaq_clip_adamw_kernel, dim3(1), dim3(OPT_TH), 0, stream, a);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

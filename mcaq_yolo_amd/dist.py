@@ -78,26 +78,47 @@ def sync_mapper_batchnorm(mapper, process_group):
     return mapper
 
 
+from torch.utils.weak import WeakIdKeyDictionary
+
+# per first parameter (by identity; dropped with the model):
+# {(group, params, local pattern): global pattern}
+_UNUSED_CACHE = WeakIdKeyDictionary()
+
+
 def allreduce_gradients(params, process_group, average=True):
     """Average the gradients of `params` over the group with ONE collective:
     every parameter that requires grad goes into a single flat bucket in the
-    order given (a None grad contributes zeros), followed by one "has a
-    gradient" flag per parameter, so every rank reduces buffers of the same
-    length and layout even when ranks disagree on which grads are None.
-    Afterwards every parameter that had a gradient on some rank holds the
-    averaged gradient, and one whose grad was None on every rank keeps None
-    (as DDP leaves globally unused parameters: optimizers then skip them)."""
+    order given (a None grad contributes zeros).  Afterwards every parameter
+    that had a gradient on some rank holds the averaged gradient, and one
+    whose grad was None on every rank keeps None (as DDP leaves globally
+    unused parameters: optimizers then skip them).
+
+    Which parameters have a gradient on SOME rank is a property of the model
+    and the step, not of the data: it is found once per (parameter list,
+    local has-gradient pattern) - one flag per parameter rides along in that
+    first all-reduce and is read back on the host - and reused afterwards, so
+    a steady-state call issues no device-to-host copy, allocates no host
+    tensor and can be captured in a HIP graph with the nccl (RCCL) backend.
+    `reset_unused_cache()` forgets the patterns (e.g. after freezing layers)."""
     import torch.distributed as dist
     ps = [p for p in params if p.requires_grad]
     if not ps:
         return
-    has = [p.grad is not None for p in ps]
-    flags = torch.tensor(has, dtype=ps[0].dtype, device=ps[0].device)
-    flat = torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in ps] + [flags])
+    has = tuple(p.grad is not None for p in ps)
+    key = (id(process_group), tuple(id(p) for p in ps), has)
+    cache = _UNUSED_CACHE.setdefault(ps[0], {})
+    any_grad = cache.get(key)
+    parts = [(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in ps]
+    if any_grad is None:
+        parts.append(torch.tensor(has, dtype=ps[0].dtype, device=ps[0].device))
+    flat = torch.cat(parts)
     dist.all_reduce(flat, group=process_group)
+    if any_grad is None:
+        any_grad = tuple(bool(v) for v in (flat[-len(ps):] > 0).tolist())
+        cache[key] = any_grad
+        flat = flat[:-len(ps)]
     if average:
-        flat[:-len(ps)] /= dist.get_world_size(process_group)
-    any_grad = (flat[-len(ps):] > 0).tolist()
+        flat /= dist.get_world_size(process_group)
     o = 0
     for p, h_any in zip(ps, any_grad):
         n = p.numel()
@@ -109,6 +130,10 @@ def allreduce_gradients(params, process_group, average=True):
         else:
             p.grad.copy_(g)
         o += n
+
+
+def reset_unused_cache():
+    _UNUSED_CACHE.clear()
 
 
 def shard_hooks(hooks, process_group, rank, world, local_batch):

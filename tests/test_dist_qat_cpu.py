@@ -246,3 +246,36 @@ def test_direct_grad_accumulation_off_under_torch_distributed():
     assert core._grads_observed([q])
     res = _run("_sink_worker")
     assert [tuple(res[r]) for r in range(2)] == [(True, True), (True, True)]
+
+
+def test_allreduce_gradients_cached_pattern_no_host_sync():
+    """Second and later calls with the same parameters and local has-grad
+    pattern reuse the global pattern: no device-to-host read (.tolist()),
+    so the call can sit inside a captured step.  World size 1 (gloo)."""
+    import os
+    import torch.distributed as dist
+    from mcaq_yolo_amd import dist as mdist
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ["MASTER_PORT"] = "29611"
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        a = torch.nn.Parameter(torch.ones(3))
+        b = torch.nn.Parameter(torch.ones(2))
+        a.grad = torch.full((3,), 2.0)
+        mdist.allreduce_gradients([a, b], dist.group.WORLD)
+        assert b.grad is None and torch.equal(a.grad, torch.full((3,), 2.0))
+        calls = {"n": 0}
+        orig = torch.Tensor.tolist
+
+        def spy(self):
+            calls["n"] += 1
+            return orig(self)
+        torch.Tensor.tolist = spy
+        try:
+            a.grad = torch.full((3,), 5.0)
+            mdist.allreduce_gradients([a, b], dist.group.WORLD)
+        finally:
+            torch.Tensor.tolist = orig
+        assert calls["n"] == 0 and b.grad is None and torch.equal(a.grad, torch.full((3,), 5.0))
+    finally:
+        dist.destroy_process_group()

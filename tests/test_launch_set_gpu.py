@@ -5,13 +5,9 @@ Every batch of a launch set has its own statistics (quantization.py:650-654:
 the per-channel min/max is over ITS batch), its own outputs and its own
 batch_offset / batch_total, so each must be bit-identical to the same batch
 run alone - bits, complexity, m(tile), channel min/max and y - and to the
-oracle on its first two images.  Also the batch-sharded form of the step:
-statistics as [-min | max] in one buffer, combined by one in-place RCCL
-all-reduce captured inside the step's HIP graph (world_size 1 nccl group on
-cuda:0), equal to the unsharded step.
+oracle on its first two images.  (The batch-sharded form of a launch set,
+with its RCCL all-reduce inside the HIP graph: tests/test_rccl_graph_gpu.py.)
 """
-import socket
-
 import numpy as np
 import pytest
 
@@ -139,85 +135,3 @@ def test_launch_set_segment_limit(dev):
     geoms = [ScaleGeom(*s, 8) for s in CONFIG2]
     with pytest.raises(ValueError):
         HookPlan(geoms, dev, batches=abi.MAX_SEGMENTS // 3 + 1)
-
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
-@pytest.fixture(scope="module")
-def nccl1(dev):
-    """A world_size 1 process group on the nccl (RCCL) backend on cuda:0."""
-    import torch.distributed as dist
-    if dist.is_initialized():
-        pytest.skip("a process group is already initialised")
-    dist.init_process_group("nccl", init_method="tcp://127.0.0.1:%d" % _free_port(), rank=0, world_size=1,
-                            device_id=dev)
-    yield dist.group.WORLD
-    dist.destroy_process_group()
-
-
-@pytest.mark.parametrize("nbat", [1, 2])
-def test_sharded_step_rccl_allreduce_in_graph(dev, blobs, nccl1, nbat):
-    """The batch-sharded step as bench.py runs it with N > 1: the statistics
-    as [-min | max] in one buffer, ONE in-place MAX all-reduce over RCCL
-    between the finalize and pass 2, all captured in one HIP graph.  On one
-    rank it must equal the unsharded step bit for bit (the collective is the
-    identity), for every batch of the launch set."""
-    import torch
-    from mcaq_yolo_amd.engine import HookPlan, ScaleGeom
-    W, cm, mm, sm = blobs
-    geoms = [ScaleGeom(*s, 8) for s in CONFIG2]
-    feats = [_feats(CONFIG2, 500 + k, dev) for k in range(nbat)]
-    arg = feats if nbat > 1 else feats[0]
-    sh = HookPlan(geoms, dev, batches=nbat)
-    sh.prepare(arg, cm, mm, [sm] * 3, shared_stats=True)
-    st = torch.cuda.Stream()
-    with torch.cuda.stream(st):
-        sh.launch(st, nccl1)            # warm-up: communicator setup outside capture
-    st.synchronize()
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, stream=st):
-        sh.launch(torch.cuda.current_stream(), nccl1)
-    for _ in range(2):
-        g.replay()
-    torch.cuda.synchronize()
-    ref = HookPlan(geoms, dev, batches=nbat)
-    ref.run(arg, cm, mm, [sm] * 3)
-    torch.cuda.synchronize()
-    for j in range(len(sh.geoms)):
-        a, b = sh.bufs[j], ref.bufs[j]
-        for key in ("bits", "complexity", "mt", "y"):
-            assert torch.equal(a[key], b[key]), (j, key)
-        mn, mx = sh.channel_minmax(j)
-        assert torch.equal(mn, b["xmin"]) and torch.equal(mx, b["xmax"])
-        assert torch.equal(a["xmin"], -b["xmin"])       # stored negated for the one MAX all-reduce
-
-
-def test_sharded_hooks_eval_nccl_equals_unsharded(dev, nccl1):
-    """MCAQHooks with a process group (dist.shard_hooks, world 1, nccl): the
-    eval-mode hook path runs the shared-statistics plan and its all-reduce;
-    outputs equal the unsharded hooks'."""
-    import torch
-    from mcaq_yolo_amd.dist import shard_hooks
-    from mcaq_yolo_amd.hooks import MCAQHooks
-    import bench
-    feats = _feats(CONFIG2, 700, dev)
-    outs = []
-    for sharded in (False, True):
-        torch.manual_seed(0)
-        h = MCAQHooks(grid_size=8, bit_mapping="mlp", device=dev)
-        h.load_state_dict(bench.hook_state_dict(dev), strict=False)
-        h.eval()
-        if sharded:
-            shard_hooks(h, nccl1, 0, 1, CONFIG2[0][0])
-        with torch.no_grad():
-            y, aux = h.forward_features(feats)
-        torch.cuda.synchronize()
-        outs.append(([t.clone() for t in y], [a["bit_map"].clone() for a in aux]))
-    for a, b in zip(outs[0][0] + outs[0][1], outs[1][0] + outs[1][1]):
-        assert torch.equal(a, b)

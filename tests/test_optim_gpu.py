@@ -1,0 +1,115 @@
+"""optim.ClipAdamW (one launch: clip_grad_norm_ + AdamW + |W| projection,
+train.py:626-641) against torch's own three steps - clip_grad_norm_(1.0),
+torch.optim.AdamW(fused), the mapper's enforce_weight_constraints - over
+several steps on the hook parameters with real QAT gradients.  fp32 sums in
+other orders (the gradient norm): parameters within rtol 1e-5 of the
+largest magnitude per tensor after 5 steps, the clipped gradients and
+exp_avg / exp_avg_sq likewise; the total norm within rtol 1e-6."""
+import pytest
+import torch
+
+from test_concurrent_scales_gpu import _feats
+from test_train_fused_gpu import _hooks
+
+pytestmark = pytest.mark.gpu
+
+
+def _close(a, b, rtol, what):
+    scale = max(float(b.abs().max()), 1e-30)
+    err = float((a - b).abs().max())
+    assert err <= rtol * scale, "%s: max err %g vs scale %g" % (what, err, scale)
+
+
+@pytest.mark.parametrize("max_norm", [1.0, 1e-4, None])
+def test_clip_adamw_matches_torch_steps(max_norm):
+    from mcaq_yolo_amd.optim import ClipAdamW
+    h0, h1 = _hooks(), _hooks()          # identical (seeded, same fixture weights)
+    feats, gens = _feats()
+    p0 = [p for p in h0.parameters() if p.requires_grad]
+    p1 = [p for p in h1.parameters() if p.requires_grad]
+    o0 = torch.optim.AdamW(p0, lr=1e-3, weight_decay=0.05, betas=(0.9, 0.999), fused=True)
+    o1 = ClipAdamW(p1, lr=1e-3, weight_decay=0.05, betas=(0.9, 0.999), max_norm=max_norm,
+                   project_abs=h1.bit_mapper.constrained_weights())
+    for it in range(5):
+        for h, o, ps in ((h0, o0, p0), (h1, o1, p1)):
+            o.zero_grad(set_to_none=True)
+            xs = [f.detach().clone().requires_grad_(True) for f in feats]
+            outs, aux = h.forward_features(xs, temperature=1.0)
+            avg = torch.stack([a["bit_map"].float().mean() for a in aux]).mean()
+            (sum((y * g).sum() for y, g in zip(outs, gens)) + 0.1 * (avg - 4.0) ** 2).backward()
+        # the same gradients go into both optimizers (they only differ after step 1)
+        for a, b in zip(p0, p1):
+            b.grad.copy_(a.grad)
+        tn = torch.nn.utils.clip_grad_norm_(p0, max_norm) if max_norm is not None else None
+        o0.step()
+        h0.bit_mapper.enforce_weight_constraints()
+        o1.step()
+        torch.cuda.synchronize()
+        if max_norm is not None:
+            _close(o1.last_total_norm.reshape(()), tn, 1e-6, "total norm step %d" % it)
+        for (n, a), b in zip([(n, p) for n, p in h0.named_parameters() if p.requires_grad], p1):
+            _close(b.grad, a.grad, 1e-5, "clipped grad %s" % n)
+            _close(b, a, 1e-5, "param %s step %d" % (n, it))
+            _close(o1.state[b]["exp_avg"], o0.state[a]["exp_avg"], 1e-5, "exp_avg %s" % n)
+            _close(o1.state[b]["exp_avg_sq"], o0.state[a]["exp_avg_sq"], 1e-5, "exp_avg_sq %s" % n)
+        # copy torch's parameters over so the steps compare one update at a time
+        with torch.no_grad():
+            for a, b in zip(p0, p1):
+                b.copy_(a)
+                o1.state[b]["exp_avg"].copy_(o0.state[a]["exp_avg"])
+                o1.state[b]["exp_avg_sq"].copy_(o0.state[a]["exp_avg_sq"])
+    for w in h1.bit_mapper.constrained_weights():
+        assert bool((w >= 0).all())
+
+
+def test_clip_adamw_state_dict_roundtrip_with_torch_adamw():
+    from mcaq_yolo_amd.optim import ClipAdamW
+    h = _hooks()
+    ps = [p for p in h.parameters() if p.requires_grad]
+    o = ClipAdamW(ps, lr=1e-3, weight_decay=0.05, max_norm=1.0)
+    for p in ps:
+        p.grad = torch.randn_like(p) * 1e-2
+    o.step()
+    o.step()
+    sd = o.state_dict()
+    t = torch.optim.AdamW(ps, lr=1e-3, weight_decay=0.05)
+    t.load_state_dict(sd)
+    assert float(t.state[ps[0]]["step"]) == 2.0
+    o2 = ClipAdamW(ps, lr=1e-3, weight_decay=0.05, max_norm=1.0)
+    o2.load_state_dict(t.state_dict())
+    for p in ps:
+        assert torch.equal(o2.state[p]["exp_avg"], o.state[p]["exp_avg"])
+        assert torch.equal(o2.state[p]["exp_avg_sq"], o.state[p]["exp_avg_sq"])
+    assert float(o2.state[ps[0]]["step"]) == 2.0
+
+
+def test_clip_adamw_graph_capture():
+    """The step captured in a HIP graph (the bench's QAT step) replays the
+    same updates as eager steps."""
+    from mcaq_yolo_amd.optim import ClipAdamW
+    torch.manual_seed(3)
+    ps = [torch.randn(n, device="cuda", requires_grad=True) for n in (97, 2048, 5)]
+    qs = [p.detach().clone().requires_grad_(True) for p in ps]
+    gs = [torch.randn_like(p) for p in ps]
+    oa = ClipAdamW(ps, lr=1e-2, weight_decay=0.05, max_norm=0.5, project_abs=[ps[1]])
+    ob = ClipAdamW(qs, lr=1e-2, weight_decay=0.05, max_norm=0.5, project_abs=[qs[1]])
+    for p, g in zip(ps, gs):
+        p.grad = g.clone()
+    for q, g in zip(qs, gs):
+        q.grad = g.clone()
+    oa.step()
+    ob.step()          # warm-up (state allocation) outside capture
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        ob.step()
+    for _ in range(3):
+        for p, g in zip(ps, gs):
+            p.grad.copy_(g)
+        oa.step()
+        for q, g in zip(qs, gs):
+            q.grad.copy_(g)
+        graph.replay()
+    torch.cuda.synchronize()
+    for p, q in zip(ps, qs):
+        assert torch.equal(p, q)
+    assert float(oa._step_t) == float(ob._step_t) == 4.0
