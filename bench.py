@@ -165,6 +165,8 @@ def main_qat(args, world, rank, dev, pg):
                                     capturable=True)
             opt_kind = "AdamW (foreach, capturable) + clip_grad_norm_ 1.0 + enforce_weight_constraints"
     target_bits = 4.0
+    h.target_bits = target_bits
+    w_bit = torch.full((), 0.1, device=dev)          # the bit-budget loss weight (loss_weights['bit_budget'])
 
     # how the train-mode mapper ran (fused kernels, or the torch autograd path)
     from mcaq_yolo_amd import train_step
@@ -186,8 +188,9 @@ def main_qat(args, world, rank, dev, pg):
         for f in feats:
             f.grad = None
         outs, aux = h.forward_features(feats, temperature=1.0)   # curriculum stage 3: temperature 1
-        lbit = (MCAQHooks.avg_bits(aux) - target_bits) ** 2
-        torch.autograd.backward(list(outs) + [0.1 * lbit], list(G) + [torch.ones((), device=dev)])
+        # MCAQLoss.compute_bit_budget_loss (models/mcaq_yolo.py:110-118) with weight 0.1
+        lbit = h.bit_budget_loss(aux, target_bits)
+        torch.autograd.backward(list(outs) + [lbit], list(G) + [w_bit])
         if pg is not None:
             from mcaq_yolo_amd.dist import allreduce_gradients
             allreduce_gradients(params_, pg)           # one flat bucket over RCCL

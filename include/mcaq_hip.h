@@ -421,6 +421,36 @@ typedef struct {
 } mcaq_smask_seg;
 /* 1 launch (no reduction) */
 int mcaq_smask_train_backward_multi(const mcaq_smask_seg* segs, int nseg, hipStream_t stream);
+/* The bit budget of a QAT step: avg_bits = mean over the segments of
+ * mean(bits_k) (models/mcaq_yolo.py:572-577) and loss = (avg_bits - target)^2
+ * (MCAQLoss.compute_bit_budget_loss, :110-118), one workgroup. */
+int mcaq_bit_budget_forward(const float* const* bits, const int* n, int nseg, float target, float* avg, float* loss,
+                            hipStream_t stream);
+typedef struct {
+  const float* avg;      /* the forward's avg_bits (device scalar) */
+  const float* g_avg;    /* dL / d avg_bits, or NULL */
+  const float* g_loss;   /* dL / d loss, or NULL */
+  float target;
+  int nscales;           /* scales averaged by avg_bits */
+} mcaq_bit_budget;
+/* The quantizer's fold + the soft-mask backward + the bit-budget gradient of
+ * every scale in ONE launch (one workgroup per image): from the per-slice
+ * partials of mcaq_qat_backward (launched with gm = gb = NULL) grad m(p) and
+ * the quantizer's grad_bits in the fold kernel's order, then gbits =
+ * (c + grad_bits(quantizer)) + grad_bits(soft mask) per tile, c = dL/d avg
+ * / (nscales * B ht wt) - the order autograd adds the three contributions in
+ * the per-scale step.  gpart: the soft-mask parameter partials, as
+ * mcaq_smask_train_backward_multi. */
+typedef struct {
+  mcaq_smask_params P;
+  const float* bits; const float* absmean;
+  const float* qat_work; /* mcaq_qat_work_floats(B, C, H, W) partials of this scale */
+  float* gbits;          /* (B, ht, wt) */
+  float* gpart;          /* mcaq_smask_gpart_floats(B) */
+  int B, C, H, W, ht, wt;
+} mcaq_qat_smask_seg;
+int mcaq_qat_smask_backward_multi(const mcaq_qat_smask_seg* segs, int nseg, const mcaq_bit_budget* bb,
+                                  hipStream_t stream);
 typedef struct {
   const float* part;     /* [nparts][stride] partial sums */
   float* out;            /* count floats (chain: segment 0's only) */

@@ -93,6 +93,17 @@ class SmaskSeg(ctypes.Structure):
                 ("B", I), ("H", I), ("W", I), ("ht", I), ("wt", I), ("accumulate", I)]
 
 
+class BitBudget(ctypes.Structure):
+    """mcaq_bit_budget."""
+    _fields_ = [("avg", P), ("g_avg", P), ("g_loss", P), ("target", Fl), ("nscales", I)]
+
+
+class QatSmaskSeg(ctypes.Structure):
+    """mcaq_qat_smask_seg."""
+    _fields_ = [("P", SmaskParams), ("bits", P), ("absmean", P), ("qat_work", P), ("gbits", P), ("gpart", P),
+                ("B", I), ("C", I), ("H", I), ("W", I), ("ht", I), ("wt", I)]
+
+
 class ReduceSeg(ctypes.Structure):
     """mcaq_reduce_seg."""
     _fields_ = [("part", P), ("out", P), ("nparts", I), ("stride", I), ("count", I), ("accumulate", I)]
@@ -138,7 +149,8 @@ EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats",
            "mcaq_mapper_train_grad_reduce", "mcaq_mapper_running_update", "mcaq_head_train_grad_reduce",
            "mcaq_mapper_train_forward_multi", "mcaq_mapper_train_backward_multi", "mcaq_head_train_backward_multi",
            "mcaq_smask_train_backward_multi", "mcaq_train_reduce_multi", "mcaq_ema_stats_multi",
-           "mcaq_mapper_train_forward_stage_multi", "mcaq_mapper_train_backward_stage_multi", "mcaq_clip_adamw")
+           "mcaq_mapper_train_forward_stage_multi", "mcaq_mapper_train_backward_stage_multi", "mcaq_clip_adamw",
+           "mcaq_bit_budget_forward", "mcaq_qat_smask_backward_multi")
 
 _LIB = None
 
@@ -232,6 +244,10 @@ def _declare(lib):
     lib.mcaq_ema_stats_ex.argtypes = [P, P, P, P, I, ctypes.c_double, I, P, P, P, P]
     lib.mcaq_pack.restype = I
     lib.mcaq_pack.argtypes = [ctypes.POINTER(PackSeg), I, P, I, P]
+    lib.mcaq_bit_budget_forward.restype = I
+    lib.mcaq_bit_budget_forward.argtypes = [ctypes.POINTER(P), ctypes.POINTER(I), I, Fl, P, P, P]
+    lib.mcaq_qat_smask_backward_multi.restype = I
+    lib.mcaq_qat_smask_backward_multi.argtypes = [ctypes.POINTER(QatSmaskSeg), I, ctypes.POINTER(BitBudget), P]
     lib.mcaq_clip_adamw.restype = I
     lib.mcaq_clip_adamw.argtypes = [ctypes.POINTER(AdamwSeg), I, ctypes.POINTER(AdamwGroup), I, P, Fl, P, P]
     lib.mcaq_smask_train_backward.restype = I

@@ -6,12 +6,13 @@
 // hook parameters.
 //
 // One 1024-thread workgroup over the flat concatenation of the segments
-// (parameter tensors), 4 K elements per chunk: the squared gradients of a
-// chunk are staged in LDS and each wave sums its segments' parts in a fixed
-// order (per-tensor norms; thread 0 combines them in tensor order into the
-// total norm, the norm of the per-tensor norms as clip_grad_norm_ computes
-// it); then every thread loads its 4 elements of a chunk (gradient,
-// parameter, both moments) before clipping, updating and projecting them.  The per-element update is torch's fused AdamW
+// (parameter tensors), 4 consecutive elements a thread per 4 K chunk: every
+// load of a phase is issued at once.  The squared gradients of a chunk are
+// staged in LDS and each segment's part summed by one wave in element order
+// (per-tensor norms; thread 0 combines them in tensor order into the total
+// norm, the norm of the per-tensor norms as clip_grad_norm_ computes it);
+// then every thread loads its elements' gradient, parameter and moments
+// before clipping, updating and projecting them.  The per-element update is torch's fused AdamW
 // arithmetic (double hyper-parameters); the norm reduces in another order
 // than ATen's, so the values agree with torch's clip + fused AdamW within
 // fp32 rounding (tests/test_optim_gpu.py), not bit for bit.
@@ -25,76 +26,85 @@ static_assert(sizeof(mcaq_adamw_seg) * MCAQ_OPT_MAXSEG + sizeof(mcaq_adamw_group
 struct AdamwArgs {
   mcaq_adamw_seg s[MCAQ_OPT_MAXSEG];
   mcaq_adamw_group g[MCAQ_OPT_MAXGROUPS];
-  int nseg, total;     // segments; elements over all segments
+  int nseg;
   float* step;         // device step counter (float, like torch's capturable AdamW)
   float max_norm;      // <= 0: no clipping
   float* total_norm;   // or nullptr
 };
 
 constexpr int OPT_TH = 1024;
-constexpr int OPT_R = 4;                   // elements per thread per chunk
-constexpr int OPT_CH = OPT_TH * OPT_R;     // elements per chunk (staged squares in LDS)
-
-// segment of flat element j: the last segment whose start is <= j (starts in LDS)
-__device__ __forceinline__ int opt_seg_of(const int* st, int nseg, int j) {
-  int lo = 0, hi = nseg - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (st[mid] <= j) lo = mid; else hi = mid - 1;
-  }
-  return lo;
-}
+constexpr int OPT_E = 4;                    // consecutive elements per thread per chunk
+constexpr int OPT_CH = OPT_TH * OPT_E;      // elements per chunk (their squares staged in LDS)
 
 __global__ __launch_bounds__(OPT_TH) void mcaq_clip_adamw_kernel(AdamwArgs a) {
+  __shared__ mcaq_adamw_seg sg[MCAQ_OPT_MAXSEG];
+  __shared__ int st[MCAQ_OPT_MAXSEG + 1];     // first flat element of each segment
   __shared__ float sq[OPT_CH];
   __shared__ float seg_acc[MCAQ_OPT_MAXSEG];
-  __shared__ int st[MCAQ_OPT_MAXSEG + 1];
-  __shared__ mcaq_adamw_seg sg[MCAQ_OPT_MAXSEG];
   __shared__ float coef_s;
   __shared__ float g_bc2s[MCAQ_OPT_MAXGROUPS], g_ss[MCAQ_OPT_MAXGROUPS];
   __shared__ double g_hp[MCAQ_OPT_MAXGROUPS][6];   // lr * wd, beta1, 1 - beta1, beta2, 1 - beta2, eps
   const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
   constexpr int NW = OPT_TH / 64;
-  const int nseg = a.nseg, total = a.total;
-  // the segment table in LDS (per-lane lookups; a per-lane index into the
-  // kernel-argument array would go through scratch)
-  if (tid < nseg) {
-    sg[tid] = a.s[tid];
-    seg_acc[tid] = 0.0f;
-  }
+  const int nseg = a.nseg;
+  for (int k = 0; k < nseg; ++k)                 // uniform index: the table in LDS
+    if (tid == k) { sg[k] = a.s[k]; seg_acc[k] = 0.0f; }
   if (tid == 0) {
     int o = 0;
     for (int k = 0; k < nseg; ++k) { st[k] = o; o += a.s[k].n; }
     st[nseg] = o;
   }
+  const float step = a.step[0] + 1.0f;
+  if (tid < MCAQ_OPT_MAXGROUPS) {
+    // bias corrections of each hyper-parameter group (fused AdamW: fp32
+    // values of the double expressions)
+    const mcaq_adamw_group& G = a.g[tid];
+    const float bc1 = (float)(1.0 - pow(G.beta1, (double)step));
+    g_bc2s[tid] = sqrtf((float)(1.0 - pow(G.beta2, (double)step)));
+    g_ss[tid] = (float)(G.lr / (double)bc1);
+    g_hp[tid][0] = G.lr * G.weight_decay;
+    g_hp[tid][1] = G.beta1; g_hp[tid][2] = 1.0 - G.beta1;
+    g_hp[tid][3] = G.beta2; g_hp[tid][4] = 1.0 - G.beta2;
+    g_hp[tid][5] = G.eps;
+  }
   __syncthreads();
+  const int total = st[nseg];
   const bool clip = a.max_norm > 0.0f;
-  // ---- per-tensor squared-gradient sums, a chunk of 4 K elements at a time:
-  // squares staged in LDS, then each wave sums the parts of its segments
-  // (w, w + 16, ...) in the chunk in a fixed order - deterministic
+  // flat elements [e0, e0 + 4) of a chunk per thread: the segment of the
+  // first by binary search, then walked forward
+  auto seg_of = [&](int j) {
+    int lo = 0, hi = nseg - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (st[mid] <= j) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+  };
+  // ---- per-tensor squared-gradient sums: squares staged in LDS, each
+  // segment's part of a chunk summed by one wave in element order, chunks in
+  // order - deterministic
   if (clip) {
     for (int base = 0; base < total; base += OPT_CH) {
-      float v[OPT_R];
+      const int e0 = base + tid * OPT_E;
+      int k = e0 < total ? seg_of(e0) : 0;
+      float v[OPT_E];
 #pragma unroll
-      for (int r = 0; r < OPT_R; ++r) {
-        const int j = base + tid + r * OPT_TH;
-        v[r] = 0.0f;
-        if (j < total) {
-          const int k = opt_seg_of(st, nseg, j);
-          v[r] = sg[k].grad[j - st[k]];
-        }
+      for (int q = 0; q < OPT_E; ++q) {
+        const int j = e0 + q;
+        while (k + 1 < nseg && j >= st[k + 1]) ++k;
+        v[q] = j < total ? sg[k].grad[j - st[k]] : 0.0f;
       }
 #pragma unroll
-      for (int r = 0; r < OPT_R; ++r) sq[tid + r * OPT_TH] = v[r] * v[r];
+      for (int q = 0; q < OPT_E; ++q) sq[tid * OPT_E + q] = v[q] * v[q];
       __syncthreads();
-      for (int k = wv; k < nseg; k += NW) {
-        const int lo = st[k] > base ? st[k] : base;
-        const int hi = st[k + 1] < base + OPT_CH ? st[k + 1] : base + OPT_CH;
+      for (int kk = wv; kk < nseg; kk += NW) {
+        const int lo = st[kk] > base ? st[kk] : base;
+        const int hi = st[kk + 1] < base + OPT_CH ? st[kk + 1] : base + OPT_CH;
         if (lo >= hi) continue;
         float acc = 0.0f;
         for (int i = lo + lane; i < hi; i += 64) acc += sq[i - base];
         for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-        if (lane == 0) seg_acc[k] += acc;
+        if (lane == 0) seg_acc[kk] += acc;
       }
       __syncthreads();
     }
@@ -114,19 +124,6 @@ __global__ __launch_bounds__(OPT_TH) void mcaq_clip_adamw_kernel(AdamwArgs a) {
   } else if (tid == 0) {
     coef_s = 1.0f;
   }
-  const float step = a.step[0] + 1.0f;
-  if (tid < MCAQ_OPT_MAXGROUPS) {
-    // bias corrections of each hyper-parameter group (fused AdamW: fp32
-    // values of the double expressions)
-    const mcaq_adamw_group& G = a.g[tid];
-    const float bc1 = (float)(1.0 - pow(G.beta1, (double)step));
-    g_bc2s[tid] = sqrtf((float)(1.0 - pow(G.beta2, (double)step)));
-    g_ss[tid] = (float)(G.lr / (double)bc1);
-    g_hp[tid][0] = G.lr * G.weight_decay;
-    g_hp[tid][1] = G.beta1; g_hp[tid][2] = 1.0 - G.beta1;
-    g_hp[tid][3] = G.beta2; g_hp[tid][4] = 1.0 - G.beta2;
-    g_hp[tid][5] = G.eps;
-  }
   __syncthreads();
   const float coef = coef_s;
   // ---- AdamW per element, then |W|.  The arithmetic of torch's
@@ -134,38 +131,41 @@ __global__ __launch_bounds__(OPT_TH) void mcaq_clip_adamw_kernel(AdamwArgs a) {
   // doubles, so the weight decay and both moment updates are evaluated in
   // double and rounded once to fp32 (an fp32 1 - beta2 alone is 1.3e-5 off);
   // step size and denominator are fp32 values, the final update fp32.
-  // Every element of a chunk is loaded before any is updated.
+  // A thread loads its 4 elements' gradient, parameter and moments first.
   for (int base = 0; base < total; base += OPT_CH) {
-    float gv[OPT_R], pv[OPT_R], mv[OPT_R], vv[OPT_R];
-    int kk[OPT_R];
+    const int e0 = base + tid * OPT_E;
+    if (e0 >= total) continue;
+    int k = seg_of(e0);
+    int ks[OPT_E];
+    float gv[OPT_E], pv[OPT_E], mv[OPT_E], vv[OPT_E];
 #pragma unroll
-    for (int r = 0; r < OPT_R; ++r) {
-      const int j = base + tid + r * OPT_TH;
-      const int k = opt_seg_of(st, nseg, j < total ? j : total - 1);
-      const int e = (j < total ? j : total - 1) - st[k];
-      kk[r] = k;
-      gv[r] = sg[k].grad[e]; pv[r] = sg[k].param[e]; mv[r] = sg[k].exp_avg[e]; vv[r] = sg[k].exp_avg_sq[e];
+    for (int q = 0; q < OPT_E; ++q) {
+      const int j = e0 + q < total ? e0 + q : total - 1;
+      while (k + 1 < nseg && j >= st[k + 1]) ++k;
+      ks[q] = k;
+      const mcaq_adamw_seg& S = sg[k];
+      const int e = j - st[k];
+      gv[q] = S.grad[e]; pv[q] = S.param[e]; mv[q] = S.exp_avg[e]; vv[q] = S.exp_avg_sq[e];
     }
 #pragma unroll
-    for (int r = 0; r < OPT_R; ++r) {
-      const int j = base + tid + r * OPT_TH;
-      if (j >= total) continue;
-      const int k = kk[r], e = j - st[k];
-      const mcaq_adamw_seg& S = sg[k];
+    for (int q = 0; q < OPT_E; ++q) {
+      const int j = e0 + q;
+      if (j >= total) break;
+      const mcaq_adamw_seg& S = sg[ks[q]];
+      const int e = j - st[ks[q]];
       const int gi = S.group;
-      const float bc2s = g_bc2s[gi], step_size = g_ss[gi];
       const double* hp = g_hp[gi];
-      float g = gv[r];
+      float g = gv[q];
       if (clip) {
         g = g * coef;
         S.grad[e] = g;             // clip_grad_norm_ scales .grad in place
       }
-      float p = pv[r];
+      float p = pv[q];
       p = (float)((double)p - hp[0] * (double)p);
-      const float m = (float)(hp[1] * (double)mv[r] + hp[2] * (double)g);
-      const float v = (float)(hp[3] * (double)vv[r] + hp[4] * (double)g * (double)g);
-      const float denom = (float)((double)(sqrtf(v) / bc2s) + hp[5]);
-      p = p - step_size * m / denom;
+      const float m = (float)(hp[1] * (double)mv[q] + hp[2] * (double)g);
+      const float v = (float)(hp[3] * (double)vv[q] + hp[4] * (double)g * (double)g);
+      const float denom = (float)((double)(sqrtf(v) / g_bc2s[gi]) + hp[5]);
+      p = p - g_ss[gi] * m / denom;
       if (S.project_abs) p = fabsf(p);
       S.exp_avg[e] = m;
       S.exp_avg_sq[e] = v;
@@ -194,10 +194,6 @@ int mcaq_clip_adamw(const mcaq_adamw_seg* segs, int nseg, const mcaq_adamw_group
   }
   for (int k = 0; k < ngroups; ++k) a.g[k] = groups[k];
   a.nseg = nseg;
-  long long tot = 0;
-  for (int k = 0; k < nseg; ++k) tot += segs[k].n;
-  if (tot > 0x7fffffff) return (int)hipErrorInvalidValue;
-  a.total = (int)tot;
   a.step = step;
   a.max_norm = max_norm;
   a.total_norm = total_norm;

@@ -968,14 +968,25 @@ struct MaskTrainArgs {
   int B, H, W, ht, wt, accumulate;
   int wg0;               // first workgroup of this segment in a multi-segment launch (else 0)
   int stage;             // 1: |x| mean and m-gradient planes staged in LDS (smask_lds_bytes)
+  // fold mode (qwork set, gm NULL): the quantizer backward's per-32-channel-
+  // slice partials (mcaq_qat_backward with gm = gb = NULL) are folded here -
+  // grad m(p) straight into the staged plane, the quantizer's grad_bits in
+  // the fold kernel's order - and gbits = (c + grad_bits(quantizer)) +
+  // grad_bits(soft mask), c the bit-budget gradient per tile (bb)
+  const float* qwork;
+  int qC;
+  mcaq_bit_budget bb;
+  float rn;              // 1 / (B * ht * wt) of this scale
 };
 
 // LDS bytes of the soft-mask backward of one (H, W, ht, wt) image; stage: + the
 // staging plane (16-byte aligned)
-inline size_t smask_lds_bytes(int H, int W, int ht, int wt, bool stage) {
+inline size_t smask_lds_bytes(int H, int W, int ht, int wt, bool stage, bool fold = false) {
   const size_t base = ((size_t)20 * ht * wt + 64 + (size_t)H * wt + (size_t)H * W) * sizeof(float) +
                       (size_t)2 * (ht + wt) * sizeof(int);
-  return stage ? ((base / 4 + 3) & ~(size_t)3) * 4 + (size_t)H * W * sizeof(float) : base;
+  const size_t st = stage ? ((base / 4 + 3) & ~(size_t)3) * 4 + (size_t)H * W * sizeof(float) : base;
+  // fold mode: + the grad_bits pixel plane [H][W], band-column sums [ht][W], per-tile sums [NT]
+  return fold ? st + ((size_t)H * W + (size_t)ht * W + (size_t)ht * wt) * sizeof(float) : st;
 }
 // staging applies when it fits and the planes are 16-byte aligned rows of 4
 inline bool smask_stage_ok(const float* absmean, const float* gm, int H, int W, int ht, int wt) {
@@ -1007,8 +1018,12 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
   // the per-tile pooling sums and the 5-tap adjoint read LDS instead of
   // chaining dependent global loads (same values, same order)
   float* stg = smem_tr + ((int)(tv + H * W - smem_tr) + 3 & ~3);   // 16-byte aligned
+  const bool fold = A.qwork != nullptr;
+  float* fpix = stg + H * W;          // fold mode: grad_bits partial sums per pixel
+  float* fcol = fpix + H * W;         //   per (tile row, column)
+  float* fgb = fcol + ht * W;         //   per tile: c + the quantizer's grad_bits
   const float* am = A.absmean + (size_t)b * H * W;
-  const float* gm = A.gm + (size_t)b * H * W;
+  const float* gm = fold ? nullptr : A.gm + (size_t)b * H * W;
   if (A.stage) {
     const int n4 = (H * W) >> 2;
     const float4* s4 = reinterpret_cast<const float4*>(am);
@@ -1062,7 +1077,47 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
   for (int w = 1; w < SM_TH / 64; ++w) amax = fmax_(amax, red[w]);
   const float den = amax + 1e-8f;
   for (int t = tid; t < NT; t += SM_TH) f1[t] = f1[t] / den;
-  if (A.stage) {
+  if (fold) {
+    // the quantizer backward's fold (qat_fold_band's values): per pixel the
+    // slice partials in slice order -> grad m(p) (into the staged plane) and
+    // the grad_bits pixel sum; per (tile row, column) the band's rows in
+    // order; per tile its columns in order
+    __syncthreads();   // every pooling read of the staged |x| plane is done
+    const int nsl = (A.qC + 31) / 32;
+    const size_t plane = (size_t)A.B * H * W;
+    const float* pm = A.qwork + (size_t)b * H * W;
+    const float* pf = A.qwork + (size_t)nsl * plane + (size_t)b * H * W;
+    for (int e = tid; e < H * W; e += SM_TH) {
+      float vm = pm[e], vf = pf[e];
+      for (int k = 1; k < nsl; ++k) { vm = vm + pm[(size_t)k * plane + e]; vf = vf + pf[(size_t)k * plane + e]; }
+      stg[e] = vm;
+      fpix[e] = vf;
+    }
+    __syncthreads();
+    gm = stg;
+    for (int it = tid; it < ht * W; it += SM_TH) {
+      const int th = it / W, w = it - th * W;
+      float t = 0.0f;
+      for (int h = hlo[th]; h <= hhi[th]; ++h) t += fpix[h * W + w];
+      fcol[it] = t;
+    }
+    // the bit-budget gradient of every tile of this scale:
+    // d L / d avg = g_avg + g_loss * 2 (avg - target), through mean(stack(means))
+    float c = 0.0f;
+    const bool has_c = A.bb.g_avg || A.bb.g_loss;
+    if (has_c) {
+      float dA = A.bb.g_avg ? A.bb.g_avg[0] : 0.0f;
+      if (A.bb.g_loss) dA = dA + A.bb.g_loss[0] * (2.0f * (A.bb.avg[0] - A.bb.target));
+      c = (dA * (1.0f / (float)A.bb.nscales)) * A.rn;
+    }
+    __syncthreads();
+    for (int t = tid; t < NT; t += SM_TH) {
+      const int i = t / wt, j = t - i * wt;
+      float g = 0.0f;
+      for (int w = wlo[j]; w <= whi[j]; ++w) g += fcol[i * W + w];
+      fgb[t] = has_c ? c + g : g;
+    }
+  } else if (A.stage) {
     __syncthreads();   // every pooling read of the staged |x| plane is done
     const int n4 = (H * W) >> 2;
     const float4* s4 = reinterpret_cast<const float4*>(gm);
@@ -1175,7 +1230,7 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
     const float f = (bv - 2.0f) / 6.0f;
     const float gb = (f >= 0.0f && f <= 1.0f) ? s / 6.0f : 0.0f;
     float* dst = A.gbits + (size_t)b * NT + u;
-    *dst = A.accumulate ? *dst + gb : gb;
+    *dst = fold ? fgb[u] + gb : (A.accumulate ? *dst + gb : gb);
   }
   // ---- parameter partials of this image
   float* gp = A.gpart + (size_t)b * SG_SIZE;
@@ -1278,6 +1333,34 @@ __global__ __launch_bounds__(64 * CB_NW) void mcaq_cmlp_bwd_multi_kernel(TrMulti
 }
 __global__ __launch_bounds__(SM_TH) void mcaq_smask_bwd_multi_kernel(TrMulti<MaskTrainArgs> M) {
   mcaq_smask_bwd_body(tr_seg(M));
+}
+
+// bit budget forward: per segment the mean of its bits (a fixed-order tree:
+// per thread a strided sum, then the block's halving tree), their mean, and
+// (avg - target)^2 - deterministic; ATen's CUDA mean reduces in another order
+// (fp32 rounding apart)
+struct BitBudgetArgs { const float* bits[TR_MAXSEG]; int n[TR_MAXSEG]; int nseg; float target; float* avg; float* loss; };
+__global__ __launch_bounds__(1024) void mcaq_bit_budget_kernel(BitBudgetArgs a) {
+  __shared__ float red[1024];
+  const int tid = (int)threadIdx.x;
+  float total = 0.0f;
+  for (int k = 0; k < a.nseg; ++k) {
+    float s = 0.0f;
+    for (int i = tid; i < a.n[k]; i += 1024) s += a.bits[k][i];
+    red[tid] = s;
+    __syncthreads();
+    for (int h = 512; h > 0; h >>= 1) {
+      if (tid < h) red[tid] = red[tid] + red[tid + h];
+      __syncthreads();
+    }
+    total = total + red[0] * (1.0f / (float)a.n[k]);
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const float avg = total * (1.0f / (float)a.nseg);
+    a.avg[0] = avg;
+    if (a.loss) a.loss[0] = (avg - a.target) * (avg - a.target);
+  }
 }
 
 // parameter-gradient reductions of several segments.  chain = 0: segment k
@@ -1647,6 +1730,58 @@ int mcaq_smask_train_backward_multi(const mcaq_smask_seg* segs, int nseg, hipStr
     set = 1;
   }
   hipLaunchKernelGGL(mcaq_smask_bwd_multi_kernel, dim3(wg), dim3(SM_TH), lb, stream, M);
+  return (int)hipGetLastError();
+}
+
+int mcaq_qat_smask_backward_multi(const mcaq_qat_smask_seg* segs, int nseg, const mcaq_bit_budget* bb,
+                                  hipStream_t stream) {
+  using namespace mcaq;
+  if (!segs || !bb || nseg < 1 || nseg > TR_MAXSEG || bb->nscales < 1 ||
+      ((bb->g_avg || bb->g_loss) && !bb->avg))
+    return (int)hipErrorInvalidValue;
+  TrMulti<MaskTrainArgs> M{};
+  int wg = 0;
+  size_t lb = 0;
+  for (int k = 0; k < nseg; ++k) {
+    const mcaq_qat_smask_seg& g = segs[k];
+    if (!g.bits || !g.absmean || !g.qat_work || !g.gbits || !g.gpart || g.B < 1 || g.C < 1 || g.ht < 1 ||
+        g.wt < 1 || g.H < g.ht || g.W < g.wt)
+      return (int)hipErrorInvalidValue;
+    MaskTrainArgs& A = M.s[k];
+    A.P = g.P; A.bits = g.bits; A.absmean = g.absmean; A.gm = nullptr; A.gbits = g.gbits; A.gpart = g.gpart;
+    A.B = g.B; A.H = g.H; A.W = g.W; A.ht = g.ht; A.wt = g.wt; A.accumulate = 0; A.wg0 = wg;
+    A.qwork = g.qat_work; A.qC = g.C; A.bb = *bb;
+    A.rn = 1.0f / (float)(g.B * g.ht * g.wt);
+    // the |x| plane staged when it fits (16-byte rows of 4); the fold planes always in LDS
+    A.stage = (((g.H * g.W) & 3) == 0 && ((uintptr_t)g.absmean & 15) == 0) ? 1 : 0;
+    wg += g.B;
+    const size_t l = smask_lds_bytes(g.H, g.W, g.ht, g.wt, true, true);
+    if (l > 160 * 1024 - 1024) return (int)hipErrorInvalidValue;
+    lb = l > lb ? l : lb;
+  }
+  M.nseg = nseg;
+  static int set = 0;
+  if (!set) {
+    const hipError_t e = hipFuncSetAttribute((const void*)mcaq_smask_bwd_multi_kernel,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024);
+    if (e != hipSuccess) return (int)e;
+    set = 1;
+  }
+  hipLaunchKernelGGL(mcaq_smask_bwd_multi_kernel, dim3(wg), dim3(SM_TH), lb, stream, M);
+  return (int)hipGetLastError();
+}
+
+int mcaq_bit_budget_forward(const float* const* bits, const int* n, int nseg, float target, float* avg, float* loss,
+                            hipStream_t stream) {
+  using namespace mcaq;
+  if (!bits || !n || !avg || nseg < 1 || nseg > TR_MAXSEG) return (int)hipErrorInvalidValue;
+  BitBudgetArgs a{};
+  for (int k = 0; k < nseg; ++k) {
+    if (!bits[k] || n[k] < 1) return (int)hipErrorInvalidValue;
+    a.bits[k] = bits[k]; a.n[k] = n[k];
+  }
+  a.nseg = nseg; a.target = target; a.avg = avg; a.loss = loss;
+  hipLaunchKernelGGL(mcaq_bit_budget_kernel, dim3(1), dim3(1024), 0, stream, a);
   return (int)hipGetLastError();
 }
 

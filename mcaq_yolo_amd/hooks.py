@@ -70,6 +70,9 @@ class MCAQHooks(nn.Module):
         # partition); None = torch.get_num_threads() at each call,
         # an int pins it (results then independent of this process's threads)
         self.softmax_threads = None
+        # bit budget target of the QAT loss (MCAQYOLO.target_bits, models/
+        # mcaq_yolo.py:70-77, 333; the curriculum sets it per stage)
+        self.target_bits = 4.0
         self._handles = []
         self._plans = {}
         # buffer set of the per-shape HookPlans: steps captured into HIP graphs
@@ -106,11 +109,38 @@ class MCAQHooks(nn.Module):
         return aux
 
     @staticmethod
+    def _budget(aux):
+        """The bit budget the multi-scale train step computed with these bit
+        maps (train_step._MaskQuantMulti), if aux is exactly that step's."""
+        b = aux[0].get("_bit_budget") if aux else None
+        if b is None or len(aux) != len(b["bits"]):
+            return None
+        if any(a.get("_bit_budget") is not b or a["bit_map"] is not m for a, m in zip(aux, b["bits"])):
+            return None
+        return b
+
+    @staticmethod
     def avg_bits(aux):
-        """models/mcaq_yolo.py:572-577: mean over scales of each bit map's mean."""
+        """models/mcaq_yolo.py:572-577: mean over scales of each bit map's mean.
+        After a multi-scale train step the value its bit-budget launch
+        computed (same definition, a fixed-order device reduction; its
+        gradient is folded into that step's backward launch)."""
         if not aux:
             return None
+        b = MCAQHooks._budget(aux)
+        if b is not None:
+            return b["avg_bits"]
         return torch.stack([a["bit_map"].float().mean() for a in aux]).mean()
+
+    def bit_budget_loss(self, aux, target_bits=None):
+        """MCAQLoss.compute_bit_budget_loss (models/mcaq_yolo.py:110-118):
+        (avg_bits - target)^2, target default self.target_bits.  After a
+        multi-scale train step run with that target: its fused value."""
+        t = float(self.target_bits if target_bits is None else target_bits)
+        b = MCAQHooks._budget(aux)
+        if b is not None and b["target"] == t:
+            return b["loss_bit"]
+        return (MCAQHooks.avg_bits(aux) - t) ** 2
 
     # -- the hook body (models/mcaq_yolo.py:409-455)
     def make_hook(self, layer_idx):

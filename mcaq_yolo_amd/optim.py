@@ -124,6 +124,13 @@ class ClipAdamW(torch.optim.Optimizer):
                                             ctypes.c_void_p(self._step_t.data_ptr()), mn,
                                             ctypes.c_void_p(self._norm_t.data_ptr()), st), "mcaq_clip_adamw")
         self.last_total_norm = self._norm_t[0] if self.max_norm is not None else None
+        # the kernel updated the tensors through raw pointers: bump their
+        # version counters as an in-place torch op would, so caches keyed on
+        # them (the packed weight blobs, core._BlobCache) see the new values
+        for _, p in items:
+            torch.autograd.graph.increment_version(p)
+            if self.max_norm is not None:
+                torch.autograd.graph.increment_version(p.grad)
 
     def _step_torch(self, items):
         """The same step as torch ops (CPU parameters)."""

@@ -93,9 +93,13 @@ def _ema_multi(qs, xs, box):
     fz = (abi.FinalizeScale * n)()
     segs = (abi.EmaSeg * n)()
     mins, maxs, keep = [], [], []
+    fold = all("bmin" in b for b in box[:n])      # reduced by the analyzer's morph launch
     for i, (q, x) in enumerate(zip(qs, xs)):
         C = x.shape[1]
-        bmin, bmax = torch.empty(C, device=x.device), torch.empty(C, device=x.device)
+        if fold:
+            bmin, bmax = box[i]["bmin"], box[i]["bmax"]
+        else:
+            bmin, bmax = torch.empty(C, device=x.device), torch.empty(C, device=x.device)
         cmin, cmax = torch.empty(C, device=x.device), torch.empty(C, device=x.device)
         keep += [bmin, bmax]
         f = fz[i]
@@ -107,7 +111,8 @@ def _ema_multi(qs, xs, box):
         e.copy_min, e.copy_max, e.num_batches = _p(cmin), _p(cmax), _p(q.num_batches_tracked)
         e.C, e.first, e.momentum = C, 0, float(q.momentum)
         mins.append(cmin); maxs.append(cmax)
-    abi.check(L.mcaq_finalize(fz, n, _stream()), "mcaq_finalize")
+    if not fold:
+        abi.check(L.mcaq_finalize(fz, n, _stream()), "mcaq_finalize")
     pg = qs[0].process_group
     if pg is not None:
         # data-parallel QAT: every scale's batch min / max over the global
@@ -164,8 +169,18 @@ def _run_analyzer_multi(an, xs):
             keep.append(ptrs["pwork"])
         morphs[i] = core._morph_struct(B, H, W, T, ht, wt, flags, **ptrs)
         outs.append(o)
+    # the quantizers' batch min / max ride along with the morph launch as its
+    # channel-reduction workgroups (as in inference): the EMA then needs no
+    # finalize launch of its own (_ema_multi)
+    fz = (abi.FinalizeScale * n)()
+    for i, (x, o) in enumerate(zip(xs, outs)):
+        C = x.shape[1]
+        o["bmin"], o["bmax"] = torch.empty(C, device=x.device), torch.empty(C, device=x.device)
+        f = fz[i]
+        f.pmin, f.pmax, f.min_out, f.max_out = _p(o["pmin"]), _p(o["pmax"]), _p(o["bmin"]), _p(o["bmax"])
+        f.C, f.nunits, f.min_stride = C, o["pmin"].shape[0], 1
     abi.check(L.mcaq_stats(stats, n, _stream()), "mcaq_stats")
-    abi.check(L.mcaq_morph(morphs, n, _stream()), "mcaq_morph")
+    abi.check(L.mcaq_morph_finalize(morphs, n, fz, n, _stream()), "mcaq_morph_finalize")
     return outs
 
 
@@ -401,6 +416,122 @@ class _SoftMaskMulti(torch.autograd.Function):
             (None,) * n + tuple(pgrads)
 
 
+# The soft masks, the quantizers and the bit budget of every scale as ONE
+# autograd node (_MaskQuantMulti): the quantizer backward's fold, the soft-mask
+# backward and the bit-budget gradient then meet in one launch, so the bit
+# maps receive ONE gradient (no ATen adds between the quantizer's, the soft
+# mask's and the avg_bits term's contributions) and avg_bits / its loss cost
+# one small launch instead of ~20 ATen kernels.  False: the separate
+# _SoftMaskMulti / _QATMulti nodes and avg_bits as torch ops.
+FUSED_MASK_QAT = True
+
+
+class _MaskQuantMulti(torch.autograd.Function):
+    """LearnedSoftMask + fractional-bit STE quantizer of every scale, plus the
+    bit budget avg_bits = mean_k mean(bits_k) and (avg_bits - target)^2
+    (models/mcaq_yolo.py:572-577, 110-118).  Forward: the soft-mask planes
+    (one morph launch), the quantizer (one launch), the bit budget (one
+    launch).  Backward: the quantizer (one launch, partials only), then fold +
+    soft-mask backward + bit-budget gradient (one launch), the soft-mask
+    parameter reduction (one launch).  Per tile the bit-map gradient is
+    (c + grad_bits(quantizer)) + grad_bits(soft mask), the order autograd
+    sums them in the per-scale step."""
+
+    @staticmethod
+    def forward(ctx, mods, n, target, *args):
+        ctx.set_materialize_grads(False)
+        bits, absmeans, xs, mins, maxs = (args[k * n:(k + 1) * n] for k in range(5))
+        L = abi.lib()
+        st = _stream()
+        blobs = _softmask_blobs(mods)
+        morphs = (abi.MorphScale * n)()
+        ms, bf = [], []
+        for i in range(n):
+            b = _f32c(bits[i]).detach()
+            bf.append(b)
+            B, H, W = absmeans[i].shape
+            _, ht, wt = b.shape
+            if 4 * ht > H or 4 * wt > W:
+                raise NotImplementedError("soft mask on a tile grid finer than 4 pixels per tile")
+            m = torch.empty(B, 1, H, W, device=b.device)
+            ms.append(m)
+            morphs[i] = core._morph_struct(B, H, W, 4, ht, wt, abi.F_SOFTMASK, absmean=absmeans[i], bits_in=b,
+                                           smask=blobs[i], m_out=m)
+        abi.check(L.mcaq_morph(morphs, n, st), "mcaq_morph(soft mask)")
+        xs = [_f32c(x) for x in xs]
+        arr = (abi.QatScale * n)()
+        ys = []
+        for i in range(n):
+            y = torch.empty_like(xs[i])
+            ys.append(y)
+            q = core._qat_struct(xs[i], bf[i], ms[i], mins[i], maxs[i])
+            q.y = _p(y)
+            arr[i] = q
+        abi.check(L.mcaq_qat_forward(arr, n, st), "mcaq_qat_forward")
+        dev = xs[0].device
+        avg = torch.empty((), device=dev)
+        loss = torch.empty((), device=dev)
+        bp = (abi.P * n)(*[_p(b) for b in bf])
+        bn = (abi.I * n)(*[b.numel() for b in bf])
+        abi.check(L.mcaq_bit_budget_forward(bp, bn, n, float(target), _p(avg), _p(loss), st), "mcaq_bit_budget_forward")
+        ctx.mods, ctx.n, ctx.target = mods, n, float(target)
+        ctx.save_for_backward(*xs, *bf, *ms, *absmeans, *mins, *maxs, avg)
+        return tuple(ys) + (avg, loss)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        n = ctx.n
+        sv = ctx.saved_tensors
+        xs, bits, ms, absmeans, mins, maxs = (sv[k * n:(k + 1) * n] for k in range(6))
+        avg = sv[6 * n]
+        gys, g_avg, g_loss = grads[:n], grads[n], grads[n + 1]
+        L = abi.lib()
+        st = _stream()
+        arr = (abi.QatScale * n)()
+        segs = (abi.QatSmaskSeg * n)()
+        rsegs = (abi.ReduceSeg * n)()
+        gxs, gbs, gflats, keep = [], [], [], []
+        for i in range(n):
+            x = xs[i]
+            B, C, H, W = x.shape
+            g = _f32c(gys[i]) if gys[i] is not None else torch.zeros_like(x)
+            gx = torch.empty_like(x)
+            work = torch.empty(L.mcaq_qat_work_floats(B, C, H, W), device=x.device)
+            keep += [g, work]
+            q = core._qat_struct(x, bits[i], ms[i], mins[i], maxs[i])
+            q.g, q.gx, q.work = _p(g), _p(gx), _p(work)     # gm = gb = NULL: partials only, folded below
+            arr[i] = q
+            gxs.append(gx)
+            _, ht, wt = bits[i].shape
+            gb = torch.empty(B, ht, wt, device=x.device)
+            gp = torch.empty(L.mcaq_smask_gpart_floats(B), device=x.device)
+            gf = torch.empty(core._SM_SIZE, device=x.device)
+            keep.append(gp)
+            gbs.append(gb)
+            gflats.append(gf)
+            sg = segs[i]
+            sg.P = abi.SmaskParams(*[_p(p.detach()) for p in ctx.mods[i].net.parameters()])
+            sg.bits, sg.absmean, sg.qat_work, sg.gbits, sg.gpart = _p(bits[i]), _p(absmeans[i]), _p(work), _p(gb), \
+                _p(gp)
+            sg.B, sg.C, sg.H, sg.W, sg.ht, sg.wt = B, C, H, W, ht, wt
+            r = rsegs[i]
+            r.part, r.out, r.nparts, r.stride, r.count, r.accumulate = _p(gp), _p(gf), B, core._SM_SIZE, \
+                core._SM_SIZE, 0
+        abi.check(L.mcaq_qat_backward(arr, n, st), "mcaq_qat_backward")
+        ga = _f32c(g_avg) if g_avg is not None else None
+        gl = _f32c(g_loss) if g_loss is not None else None
+        bb = abi.BitBudget(_p(avg), _p(ga), _p(gl), ctx.target, n)
+        abi.check(L.mcaq_qat_smask_backward_multi(segs, n, ctypes.byref(bb), st), "mcaq_qat_smask_backward_multi")
+        abi.check(L.mcaq_train_reduce_multi(rsegs, n, 0, st), "mcaq_train_reduce_multi")
+        pgrads = []
+        for i in range(n):
+            params = list(ctx.mods[i].net.parameters())
+            pgrads += [gg if p.requires_grad else None for gg, p in zip(core._split_flat(gflats[i], params), params)]
+        nig = ctx.needs_input_grad
+        return (None, None, None) + tuple(gbs[i] if nig[3 + i] else None for i in range(n)) + (None,) * n + \
+            tuple(gxs[i] if nig[3 + 2 * n + i] else None for i in range(n)) + (None,) * (2 * n) + tuple(pgrads)
+
+
 class _QATMulti(torch.autograd.Function):
     """Fractional-bit straight-through quantizer x m(p) of every scale: one
     forward launch, one backward launch (+ its fold)."""
@@ -549,6 +680,15 @@ def forward_features(hooks, feats, state):
             xmin, xmax = q.batch_minmax(x, None)
         mins.append(xmin); maxs.append(xmax)
     want = [q.smooth_transitions and q.soft_mask is not None for q in qs]
+    if FUSED_MASK_QAT and all(want) and n <= abi.MCAQ_TRAIN_MAXSEG:
+        target = float(getattr(hooks, "target_bits", 4.0))
+        res = _MaskQuantMulti.apply([q.soft_mask for q in qs], n, target, *bits, *[b["absmean"] for b in box],
+                                    *feats, *mins, *maxs, *[p for q in qs for p in q.soft_mask.net.parameters()])
+        ys, budget = list(res[:n]), {"avg_bits": res[n], "loss_bit": res[n + 1], "target": target, "bits": bits}
+        for i in range(n):
+            state.setdefault("aux", []).append({"layer": idxs[i], "complexity": cs[i], "bit_map": bits[i],
+                                                "features_q": ys[i], "_bit_budget": budget})
+        return ys
     ms = [None] * n
     if all(want):
         ms = list(_SoftMaskMulti.apply([q.soft_mask for q in qs], n, *bits, *[b["absmean"] for b in box],

@@ -27,15 +27,19 @@ def _feats(B=4, seed=5, shapes=((64, 80), (128, 40), (256, 20))):
     return feats, gens
 
 
-def _run(concurrent, steps=3, graph=False, mapper="mlp", multi=False, variant=None):
+def _run(concurrent, steps=3, graph=False, mapper="mlp", multi=False, variant=None, fused_mq=False, budget=False):
     """concurrent / multi select the train path (hooks.CONCURRENT_TRAIN_SCALES,
     hooks.MULTI_SCALE_TRAIN); both False: per-scale modules on one stream.
     variant: None, "normalize" (normalize_complexity), "per_tensor" (every
     quantizer per_channel=False) or "no_mask" (the C4 quantizer without
-    smooth transitions)."""
-    from mcaq_yolo_amd import hooks
-    old = hooks.CONCURRENT_TRAIN_SCALES, hooks.MULTI_SCALE_TRAIN
+    smooth transitions).  fused_mq: train_step.FUSED_MASK_QAT (the soft
+    masks, quantizers and bit budget as one node); budget: the bit-budget
+    term through MCAQHooks.bit_budget_loss instead of torch ops on the aux
+    bit maps."""
+    from mcaq_yolo_amd import hooks, train_step
+    old = hooks.CONCURRENT_TRAIN_SCALES, hooks.MULTI_SCALE_TRAIN, train_step.FUSED_MASK_QAT
     hooks.CONCURRENT_TRAIN_SCALES, hooks.MULTI_SCALE_TRAIN = concurrent, multi
+    train_step.FUSED_MASK_QAT = fused_mq
     try:
         h = _hooks(mapper)
         if variant == "normalize":
@@ -55,8 +59,11 @@ def _run(concurrent, steps=3, graph=False, mapper="mlp", multi=False, variant=No
             for f in feats:
                 f.grad = None
             outs, aux = h.forward_features(feats, temperature=1.0)
-            avg = torch.stack([a["bit_map"].float().mean() for a in aux]).mean()
-            loss = sum((o * g).sum() for o, g in zip(outs, gens)) + 0.1 * (avg - 4.0) ** 2
+            if budget:
+                lb = h.bit_budget_loss(aux, 4.0)
+            else:
+                lb = (torch.stack([a["bit_map"].float().mean() for a in aux]).mean() - 4.0) ** 2
+            loss = sum((o * g).sum() for o, g in zip(outs, gens)) + 0.1 * lb
             loss.backward()
             rec["outs"] = [o.detach() for o in outs]
             rec["bits"] = [a["bit_map"].detach() for a in aux]
@@ -89,7 +96,33 @@ def _run(concurrent, steps=3, graph=False, mapper="mlp", multi=False, variant=No
         snap["bufs"] = {k: b.detach().clone() for k, b in h.named_buffers() if b is not None}
         return snap
     finally:
-        hooks.CONCURRENT_TRAIN_SCALES, hooks.MULTI_SCALE_TRAIN = old
+        hooks.CONCURRENT_TRAIN_SCALES, hooks.MULTI_SCALE_TRAIN, train_step.FUSED_MASK_QAT = old
+
+
+def _close(a, b, rtol=1e-5):
+    """Within fp32 rounding of the tensor's scale: the fused node sums the
+    bit-map gradient contributions (and the bit budget) in another order."""
+    for k in ("outs", "bits", "cplx", "fgrad"):
+        for i, (x, y) in enumerate(zip(a[k], b[k])):
+            err = float((x - y).abs().max())
+            assert err <= rtol * max(float(y.abs().max()), 1e-30), "%s[%d]: %g" % (k, i, err)
+    # gradients: relative to the module's largest gradient (the Linear layers
+    # feeding a train-mode BatchNorm carry cancelling sums: test_dist_qat_gpu)
+    gmax = {}
+    for n, y in b["grads"].items():
+        mod = ".".join(n.split(".")[:2])
+        gmax[mod] = max(gmax.get(mod, 0.0), float(y.abs().max()))
+    for k in ("grads", "params", "bufs"):
+        assert set(a[k]) == set(b[k]), k
+        for n in a[k]:
+            x, y = a[k][n].float(), b[k][n].float()
+            err = float((x - y).abs().max()) if x.numel() else 0.0
+            scale = max(float(y.abs().max()) if y.numel() else 0.0, 1e-30)
+            if k == "grads":
+                scale, tol = max(gmax[".".join(n.split(".")[:2])], 1e-30), 1e-4
+            else:
+                tol = rtol
+            assert err <= tol * scale, "%s %s: %g vs %g" % (k, n, err, scale)
 
 
 def _same(a, b):

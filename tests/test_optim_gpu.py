@@ -113,3 +113,36 @@ def test_clip_adamw_graph_capture():
     for p, q in zip(ps, qs):
         assert torch.equal(p, q)
     assert float(oa._step_t) == float(ob._step_t) == 4.0
+
+
+def test_clip_adamw_step_reaches_packed_blobs():
+    """The kernel writes the parameters through raw pointers; the optimizer
+    bumps their version counters, so the hooks' packed weight blobs
+    (core._BlobCache) are re-packed and the next eager forward sees the
+    update (equal to the same hooks stepped by torch's optimizer)."""
+    from mcaq_yolo_amd.optim import ClipAdamW
+    feats, gens = _feats()
+    res = []
+    for fused in (True, False):
+        h = _hooks()
+        ps = [p for p in h.parameters() if p.requires_grad]
+        o = ClipAdamW(ps, lr=1e-2, weight_decay=0.05) if fused else torch.optim.AdamW(ps, lr=1e-2, weight_decay=0.05)
+        for it in range(2):
+            o.zero_grad(set_to_none=True)
+            xs = [f.detach().clone().requires_grad_(True) for f in feats]
+            outs, aux = h.forward_features(xs, temperature=1.0)
+            sum((y * g).sum() for y, g in zip(outs, gens)).backward()
+            o.step()
+        with torch.no_grad():
+            h.eval()
+            outs, aux = h.forward_features([f.detach() for f in feats])
+        torch.cuda.synchronize()
+        res.append([a["complexity"].clone() for a in aux])
+    for a, b in zip(*res):
+        err = float((a - b).abs().max())
+        assert err <= 1e-4 * float(b.abs().max()), err
+    # and not equal to the un-stepped hooks'
+    h0 = _hooks().eval()
+    with torch.no_grad():
+        _, aux0 = h0.forward_features([f.detach() for f in feats])
+    assert not torch.equal(aux0[0]["complexity"], res[0][0])

@@ -9,7 +9,7 @@ after SGD steps, every buffer - eager and captured in a HIP graph."""
 import pytest
 import torch
 
-from test_concurrent_scales_gpu import _feats, _run, _same
+from test_concurrent_scales_gpu import _close, _feats, _run, _same
 from test_train_fused_gpu import _hooks
 
 pytestmark = pytest.mark.gpu
@@ -120,3 +120,53 @@ def test_frozen_mapper_in_training_hooks_takes_per_scale_path():
             hooks.MULTI_SCALE_TRAIN, hooks.CONCURRENT_TRAIN_SCALES = old
     for a, b in zip(*res):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("budget", [False, True])
+def test_fused_mask_quant_budget_step_close_to_per_scale(budget):
+    """train_step.FUSED_MASK_QAT (the default): soft masks, quantizers and
+    the bit budget of every scale as one autograd node whose backward folds
+    the quantizer, the soft mask and the bit-budget gradient into one launch.
+    The first forward is bit-identical to the per-scale step; the bit-map
+    gradient sums its contributions in another association, so gradients and
+    later steps agree within fp32 rounding.  budget: the loss's bit-budget
+    term through MCAQHooks.bit_budget_loss (the fused value and gradient on
+    the multi path, torch ops on the per-scale path)."""
+    a = _run(False, steps=1, multi=True, fused_mq=True, budget=budget)
+    b = _run(False, steps=1, budget=budget)
+    for k in ("outs", "bits", "cplx"):
+        for x, y in zip(a[k], b[k]):
+            assert torch.equal(x, y), k
+    _close(a, b)
+    # (one step only: the biases of the Linear layers that feed train-mode
+    # BatchNorm have a mathematically zero gradient, so theirs is rounding
+    # noise in either association - 20-40 % apart here - and SGD steps on it
+    # move the two runs apart along directions the loss does not see
+    # (tools/diag/fused_mq_drift.py); the fused step's determinism is
+    # test_fused_mask_quant_budget_graph's exact graph-vs-eager check)
+
+
+def test_fused_mask_quant_budget_graph():
+    """The fused step captured in a HIP graph == the same step eager, bit
+    for bit (warm-up step + 3 replays vs 4 eager steps)."""
+    _same(_run(False, steps=3, graph=True, multi=True, fused_mq=True, budget=True),
+          _run(False, steps=4, multi=True, fused_mq=True, budget=True))
+
+
+def test_bit_budget_values():
+    """avg_bits / bit_budget_loss of the fused step against the torch
+    expressions on the same bit maps (fp32 reduction order apart)."""
+    from mcaq_yolo_amd import hooks, train_step
+    from test_train_fused_gpu import _hooks
+    assert train_step.FUSED_MASK_QAT and hooks.MULTI_SCALE_TRAIN
+    h = _hooks()
+    feats, _ = _feats()
+    outs, aux = h.forward_features(feats)
+    avg = h.avg_bits(aux)
+    ref = torch.stack([a["bit_map"].float().mean() for a in aux]).mean()
+    assert aux[0]["_bit_budget"]["avg_bits"] is avg
+    assert abs(float(avg) - float(ref)) <= 2e-6 * abs(float(ref))
+    lb = h.bit_budget_loss(aux, 4.0)
+    assert abs(float(lb) - (float(ref) - 4.0) ** 2) <= 1e-5 * max((float(ref) - 4.0) ** 2, 1e-6)
+    lb5 = h.bit_budget_loss(aux, 5.0)          # another target: torch ops on the fused avg
+    assert abs(float(lb5) - (float(avg) - 5.0) ** 2) <= 1e-6
