@@ -33,6 +33,20 @@ struct AdamwArgs {
 };
 
 constexpr int OPT_TH = 1024;
+
+// beta^step for an integer-valued step by binary exponentiation in double (a
+// few multiplies instead of the library pow, whose code the one-shot kernel
+// would fetch cold; within an ulp or two of pow)
+__device__ __forceinline__ double pow_int(double b, float step) {
+  long long e = (long long)step;
+  double r = 1.0;
+  while (e > 0) {
+    if (e & 1) r *= b;
+    b *= b;
+    e >>= 1;
+  }
+  return r;
+}
 constexpr int OPT_E = 4;                    // consecutive elements per thread per chunk
 constexpr int OPT_CH = OPT_TH * OPT_E;      // elements per chunk (their squares staged in LDS)
 
@@ -47,20 +61,38 @@ __global__ __launch_bounds__(OPT_TH) void mcaq_clip_adamw_kernel(AdamwArgs a) {
   const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
   constexpr int NW = OPT_TH / 64;
   const int nseg = a.nseg;
-  for (int k = 0; k < nseg; ++k)                 // uniform index: the table in LDS
-    if (tid == k) { sg[k] = a.s[k]; seg_acc[k] = 0.0f; }
-  if (tid == 0) {
-    int o = 0;
-    for (int k = 0; k < nseg; ++k) { st[k] = o; o += a.s[k].n; }
-    st[nseg] = o;
+  {
+    // the segment table into LDS, a dword per thread (the kernel-argument
+    // segment read through a pointer: no per-lane indexing of the argument)
+    constexpr int SW = (int)(sizeof(mcaq_adamw_seg) / 4);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(&a.s[0]);
+    for (int i = tid; i < nseg * SW; i += OPT_TH) reinterpret_cast<uint32_t*>(sg)[i] = src[i];
+    if (tid < nseg) seg_acc[tid] = 0.0f;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    // segment starts: an exclusive scan of the sizes over one wave (64 per round)
+    int carry = 0;
+    for (int k0 = 0; k0 < nseg; k0 += 64) {
+      const int k = k0 + tid;
+      const int nk = k < nseg ? sg[k].n : 0;
+      int incl = nk;
+      for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(incl, o, 64);
+        if (tid >= o) incl += t;
+      }
+      if (k < nseg) st[k] = carry + incl - nk;
+      carry += __shfl(incl, 63, 64);
+    }
+    if (tid == 0) st[nseg] = carry;
   }
   const float step = a.step[0] + 1.0f;
   if (tid < MCAQ_OPT_MAXGROUPS) {
     // bias corrections of each hyper-parameter group (fused AdamW: fp32
     // values of the double expressions)
     const mcaq_adamw_group& G = a.g[tid];
-    const float bc1 = (float)(1.0 - pow(G.beta1, (double)step));
-    g_bc2s[tid] = sqrtf((float)(1.0 - pow(G.beta2, (double)step)));
+    const float bc1 = (float)(1.0 - pow_int(G.beta1, step));
+    g_bc2s[tid] = sqrtf((float)(1.0 - pow_int(G.beta2, step)));
     g_ss[tid] = (float)(G.lr / (double)bc1);
     g_hp[tid][0] = G.lr * G.weight_decay;
     g_hp[tid][1] = G.beta1; g_hp[tid][2] = 1.0 - G.beta1;
@@ -101,25 +133,35 @@ __global__ __launch_bounds__(OPT_TH) void mcaq_clip_adamw_kernel(AdamwArgs a) {
         const int lo = st[kk] > base ? st[kk] : base;
         const int hi = st[kk + 1] < base + OPT_CH ? st[kk + 1] : base + OPT_CH;
         if (lo >= hi) continue;
-        float acc = 0.0f;
-        for (int i = lo + lane; i < hi; i += 64) acc += sq[i - base];
+        // four independent partial sums per lane (fixed order), then the wave
+        float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+        int i = lo + lane;
+        for (; i + 192 < hi; i += 256) {
+          a0 += sq[i - base]; a1 += sq[i + 64 - base]; a2 += sq[i + 128 - base]; a3 += sq[i + 192 - base];
+        }
+        for (; i < hi; i += 64) a0 += sq[i - base];
+        float acc = (a0 + a1) + (a2 + a3);
         for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
         if (lane == 0) seg_acc[kk] += acc;
       }
       __syncthreads();
     }
-    if (tid == 0) {
-      // the norm of the per-tensor norms (clip_grad_norm_), in tensor order
-      float tot = 0.0f;
-      for (int k = 0; k < nseg; ++k) {
+    if (tid < 64) {
+      // the norm of the per-tensor norms (clip_grad_norm_): squares of the
+      // tensor norms summed over the wave (fixed tree)
+      float t2 = 0.0f;
+      for (int k = tid; k < nseg; k += 64) {
         const float nk = sqrtf(seg_acc[k]);
-        tot = fmaf(nk, nk, tot);
+        t2 = fmaf(nk, nk, t2);
       }
-      tot = sqrtf(tot);
-      if (a.total_norm) a.total_norm[0] = tot;
-      const float c = a.max_norm / (tot + 1e-6f);
-      coef_s = c < 1.0f ? c : 1.0f;   // clamp(max=1.0); NaN propagates as in torch
-      if (!(c == c)) coef_s = c;
+      for (int o = 32; o > 0; o >>= 1) t2 += __shfl_xor(t2, o, 64);
+      const float tot = sqrtf(t2);
+      if (tid == 0) {
+        if (a.total_norm) a.total_norm[0] = tot;
+        const float c = a.max_norm / (tot + 1e-6f);
+        coef_s = c < 1.0f ? c : 1.0f;   // clamp(max=1.0); NaN propagates as in torch
+        if (!(c == c)) coef_s = c;
+      }
     }
   } else if (tid == 0) {
     coef_s = 1.0f;

@@ -1,7 +1,8 @@
-"""Probe: bounds of the pipelined hook step at config 2 (3 batches in flight on
-3 streams, one HIP graph per batch, as bench.Runner): the full chain, the
-streaming passes only (pass 1 + pass 2), the morphology only (pass A + B),
-and pass A / pass B alone - us per step, interleaved repeats."""
+"""Probe: bounds of the pipelined hook step at config 2 (3 launch sets in
+flight on 3 streams, one HIP graph per launch set, as bench.Runner; argv[1]
+= batches per launch set, default 1): the full chain, the streaming passes
+only (pass 1 + pass 2), the morphology only (pass A + B), and pass A / pass B
+alone - us per 32-image batch, interleaved repeats."""
 import os
 import sys
 import time
@@ -17,11 +18,13 @@ dev = torch.device("cuda:0")
 name, B, chans, grid, mapper = bench.CONFIGS[2]
 cm, mm, sm = bench.load_blobs(dev)
 geoms = [ScaleGeom(B, c, h, w, grid) for c, (h, w) in zip(chans, bench.SIZES)]
+K = int(sys.argv[1]) if len(sys.argv) > 1 else 1
 plans = []
 for p in range(3):
-    feats = [bench.synth_features(B, c, h, w, 2000 + i + 104729 * p, dev) for i, (c, (h, w)) in enumerate(zip(chans, bench.SIZES))]
-    plan = HookPlan(geoms, dev)
-    plan.prepare(feats, cm, mm, [sm] * 3, mapper_kind=mapper)
+    feats = [[bench.synth_features(B, c, h, w, 2000 + i + 104729 * (p * K + k), dev)
+              for i, (c, (h, w)) in enumerate(zip(chans, bench.SIZES))] for k in range(K)]
+    plan = HookPlan(geoms, dev, batches=K)
+    plan.prepare(feats if K > 1 else feats[0], cm, mm, [sm] * 3, mapper_kind=mapper)
     plan.feats = feats
     plans.append(plan)
     plan.launch()
@@ -64,6 +67,9 @@ for v, fn in VARIANTS.items():
 torch.cuda.synchronize()
 
 
+NB = K
+
+
 def timeit(v, K=300):
     gs = graphs[v]
     for i in range(30):
@@ -75,8 +81,9 @@ def timeit(v, K=300):
         with torch.cuda.stream(streams[i % 3]):
             gs[i % 3].replay()
     torch.cuda.synchronize()
-    return (time.perf_counter() - t0) / K * 1e6
+    return (time.perf_counter() - t0) / (K * NB) * 1e6
 
 
+print("batches per launch set:", NB)
 for rep in range(3):
     print(" | ".join("%s %.1f" % (v, timeit(v)) for v in VARIANTS), flush=True)
