@@ -44,7 +44,7 @@ typedef void* hipEvent_t;
 extern "C" {
 #endif
 
-#define MCAQ_ABI_VERSION 18
+#define MCAQ_ABI_VERSION 19
 /* segments (hook scale x batch) per mcaq_stats / mcaq_finalize /
  * mcaq_morph* / mcaq_quant launch */
 #define MCAQ_MAX_SEGMENTS 9
@@ -234,6 +234,12 @@ typedef struct {
 } mcaq_qat_scale;
 int mcaq_qat_forward(const mcaq_qat_scale* scales, int nscales, hipStream_t stream);
 int mcaq_qat_backward(const mcaq_qat_scale* scales, int nscales, hipStream_t stream);
+/* mcaq_qat_forward plus the train step's bit budget as one extra workgroup of
+ * the same launch: avg = mean_k mean(bits[k][0 .. n[k])) over nseg <= 3 bit
+ * maps (models/mcaq_yolo.py:572-577) and loss = (avg - target)^2 (NULL: not
+ * written; MCAQLoss.compute_bit_budget_loss, :110-118). */
+int mcaq_qat_forward_budget(const mcaq_qat_scale* scales, int nscales, const float* const* bits, const int* n,
+                            int nseg, float target, float* avg, float* loss, hipStream_t stream);
 size_t mcaq_qat_work_floats(int B, int C, int H, int W);
 /* running <- fp32(momentum) running + fp32(1 - momentum) batch, per channel
  * (first != 0: running <- batch), in place. */
@@ -349,6 +355,13 @@ int mcaq_mapper_train_grad_reduce(int n, const float* gpart, float* gparams, int
  * several streams (the running buffers are shared).  1 launch. */
 int mcaq_mapper_running_update(const mcaq_mapper_params* P, const float* const* works, const int* ns, int count,
                                float momentum, hipStream_t stream);
+/* mcaq_ema_stats_multi(segs, nseg) plus mcaq_mapper_running_update(P, works,
+ * ns, count, momentum) as one extra workgroup of the same launch: the train
+ * step's deferred BatchNorm running-statistics update of the bit mapper rides
+ * on the quantizers' EMA launch that follows it. */
+int mcaq_ema_stats_multi_running(const mcaq_ema_seg* segs, int nseg, const mcaq_mapper_params* P,
+                                 const float* const* works, const int* ns, int count, float momentum,
+                                 hipStream_t stream);
 /* grid_sync: NULL (one launch per batch-statistics barrier), or 2 zeroed
  * uint32 that launches on one stream share (each launch leaves them zeroed):
  * forward and backward then run as ONE launch each, with grid-wide barriers

@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libmcaq_hip.so")
-ABI_VERSION = 18
+ABI_VERSION = 19
 MAX_SEGMENTS = 9   # MCAQ_MAX_SEGMENTS: segments (hook scale x batch) per launch
 
 P = ctypes.c_void_p
@@ -150,7 +150,8 @@ EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats",
            "mcaq_mapper_train_forward_multi", "mcaq_mapper_train_backward_multi", "mcaq_head_train_backward_multi",
            "mcaq_smask_train_backward_multi", "mcaq_train_reduce_multi", "mcaq_ema_stats_multi",
            "mcaq_mapper_train_forward_stage_multi", "mcaq_mapper_train_backward_stage_multi", "mcaq_clip_adamw",
-           "mcaq_bit_budget_forward", "mcaq_qat_smask_backward_multi")
+           "mcaq_bit_budget_forward", "mcaq_qat_smask_backward_multi", "mcaq_qat_forward_budget",
+           "mcaq_ema_stats_multi_running")
 
 _LIB = None
 
@@ -244,6 +245,12 @@ def _declare(lib):
     lib.mcaq_ema_stats_ex.argtypes = [P, P, P, P, I, ctypes.c_double, I, P, P, P, P]
     lib.mcaq_pack.restype = I
     lib.mcaq_pack.argtypes = [ctypes.POINTER(PackSeg), I, P, I, P]
+    lib.mcaq_qat_forward_budget.restype = I
+    lib.mcaq_qat_forward_budget.argtypes = [ctypes.POINTER(QatScale), I, ctypes.POINTER(P), ctypes.POINTER(I), I, Fl,
+                                            P, P, P]
+    lib.mcaq_ema_stats_multi_running.restype = I
+    lib.mcaq_ema_stats_multi_running.argtypes = [ctypes.POINTER(EmaSeg), I, ctypes.POINTER(MapperParams),
+                                                 ctypes.POINTER(P), ctypes.POINTER(I), I, Fl, P]
     lib.mcaq_bit_budget_forward.restype = I
     lib.mcaq_bit_budget_forward.argtypes = [ctypes.POINTER(P), ctypes.POINTER(I), I, Fl, P, P, P]
     lib.mcaq_qat_smask_backward_multi.restype = I

@@ -20,10 +20,14 @@
 
 namespace mcaq {
 
+// the train step's bit budget riding on the QAT forward launch (nseg = 0: none)
+struct QatBudget { const float* bits[3]; int n[3]; int nseg; float target; float* avg; float* loss; };
+
 struct QatArgs {
   mcaq_qat_scale s[3];
   int nscales;
   int units_total;
+  QatBudget bb;
 };
 
 #ifndef MCAQ_QAT_MINW
@@ -142,11 +146,48 @@ constexpr int QAT_FUSED_MAXW = 512;
 // config 5: all loads issued ahead of the table and barrier;
 // two channels at a time under an 8-workgroup/CU register cap; one-wave
 // workgroups walking all 32 channels of a slice (every unit resident at once).
+// the bit budget of the train step (models/mcaq_yolo.py:572-577 avg_bits =
+// mean_k mean(bits_k); MCAQLoss.compute_bit_budget_loss :110-118) as ONE extra
+// workgroup of the QAT forward launch, which reads the same bit maps: per
+// segment 8 loads a thread in flight (clamped index, no load behind a
+// branch), a fixed shuffle tree per wave, the 4 waves summed in order
+__device__ __forceinline__ void qat_budget_block(const QatBudget& B, float* red) {
+  const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  float total = 0.0f;
+  for (int k = 0; k < B.nseg; ++k) {
+    const float* p = k == 0 ? B.bits[0] : (k == 1 ? B.bits[1] : B.bits[2]);
+    const int n = k == 0 ? B.n[0] : (k == 1 ? B.n[1] : B.n[2]);
+    float s = 0.0f;
+    for (int i0 = tid; i0 < n; i0 += 256 * 8) {
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] = p[imin_(i0 + 256 * r, n - 1)];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) s += i0 + 256 * r < n ? v[r] : 0.0f;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (lane == 0) red[wv] = s;
+    __syncthreads();
+    total = total + ((red[0] + red[1]) + (red[2] + red[3])) * (1.0f / (float)n);
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const float avg = total * (1.0f / (float)B.nseg);
+    B.avg[0] = avg;
+    if (B.loss) B.loss[0] = (avg - B.target) * (avg - B.target);
+  }
+}
+
 template <bool kBwd, bool kVec>
 __global__ __launch_bounds__(256, MCAQ_QAT_MINW) void mcaq_qat_kernel(QatArgs a) {
   __shared__ float4 qt[32 * QAT_NB];   // scale, zp, 1/scale
   __shared__ float red[2][4][256];
   __shared__ int s_last;   // bands completed by this unit (bit per band)
+  if (!kBwd && (int)blockIdx.x >= a.units_total) {   // the bit-budget workgroup (forward only)
+    qat_budget_block(a.bb, &red[0][0][0]);
+    return;
+  }
   const int unit = blockIdx.x;
   int si = 0;
   while (si + 1 < a.nscales && unit >= a.s[si + 1].unit_begin) ++si;
@@ -161,12 +202,33 @@ __global__ __launch_bounds__(256, MCAQ_QAT_MINW) void mcaq_qat_kernel(QatArgs a)
   const int b = lu / upi;
   const int c0 = slice * 32;
   const int nc = imin_(32, S.C - c0);
+  const int q0 = chunk * 256 + lane * 4;
+  const int cw = wv * 8;
+  const int ncw = imin_(8, nc - cw);
+  const size_t rowbase = ((size_t)b * S.C + c0 + imax_(0, imin_(cw, nc - 1))) * HW;
+  const float* xb = S.x + rowbase;
+  const int qa = q0 < HW ? q0 : 0;
+  // ---- the wave's 8 x rows first, unconditionally (clamped channel and
+  // pixel indices): in flight through the table build and the per-pixel
+  // prologue, as pass 2 issues them (the backward's g rows follow in the
+  // channel loop: both sets at once spill 84 B a lane at 128 VGPRs)
+  float xv[8][4];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const size_t ro = (size_t)imin_(c, imax_(ncw - 1, 0)) * HW;
+    if (kVec) {
+      const float4 t = *reinterpret_cast<const float4*>(xb + ro + qa);
+      xv[c][0] = t.x; xv[c][1] = t.y; xv[c][2] = t.z; xv[c][3] = t.w;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) xv[c][k] = xb[ro + imin_(q0 + k, HW - 1)];
+    }
+  }
   for (int i = tid; i < nc * QAT_NB; i += 256) {
     const int c = i / QAT_NB, k = i - c * QAT_NB;
     const QParam q = qparam(S.xmin[c0 + c], S.xmax[c0 + c], QAT_LO + k);
     qt[i] = make_float4(q.scale, q.zp, q.rs, 0.0f);
   }
-  const int q0 = chunk * 256 + lane * 4;
   const NearestMap nmh = nearest_map(S.ht, S.H), nmw = nearest_map(S.wt, S.W);
   bool pv[4];
   int kl[4], kh[4];
@@ -186,31 +248,21 @@ __global__ __launch_bounds__(256, MCAQ_QAT_MINW) void mcaq_qat_kernel(QatArgs a)
     mv[k] = S.m ? S.m[(size_t)b * HW + p] : 1.0f;
   }
   const bool has_m = S.m != nullptr;
-  const int cw = wv * 8;
-  const int ncw = imin_(8, nc - cw);
-  const size_t rowbase = ((size_t)b * S.C + c0 + imax_(0, imin_(cw, nc - 1))) * HW;
-  const float* xb = S.x + rowbase;
-  const int qa = pv[0] ? q0 : 0;
   __syncthreads();   // qt ready
   float sgm[4] = {0.f, 0.f, 0.f, 0.f}, sgf[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
     if (c >= ncw) break;
-    const size_t ro = (size_t)c * HW;
-    float v[4], gv[4];
-    if (kVec) {
-      const float4 t = *reinterpret_cast<const float4*>(xb + ro + qa);
-      v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
-      if (kBwd) {
+    const float* v = xv[c];
+    float gv[4];
+    if (kBwd) {
+      const size_t ro = (size_t)c * HW;
+      if (kVec) {
         const float4 u = *reinterpret_cast<const float4*>(S.g + rowbase + ro + qa);
         gv[0] = u.x; gv[1] = u.y; gv[2] = u.z; gv[3] = u.w;
-      }
-    } else {
+      } else {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const size_t o = ro + imin_(q0 + k, HW - 1);
-        v[k] = xb[o];
-        if (kBwd) gv[k] = S.g[rowbase + o];
+        for (int k = 0; k < 4; ++k) gv[k] = S.g[rowbase + ro + imin_(q0 + k, HW - 1)];
       }
     }
     float o[4];
@@ -344,7 +396,7 @@ __global__ __launch_bounds__(256) void mcaq_ema_kernel(const float* bmin, const 
 // running workgroup offsets (one per segment, 256 channels per workgroup)
 struct EmaSeg { const float *bmin, *bmax; float *rmin, *rmax, *cmin, *cmax; long long* nbt; int C, first, wg0; float am, cm; };
 struct EmaMulti { EmaSeg s[3]; int nseg; };
-__global__ __launch_bounds__(256) void mcaq_ema_multi_kernel(EmaMulti M) {
+__device__ __forceinline__ void ema_multi_body(const EmaMulti& M) {
   const int x = (int)blockIdx.x;
   const EmaSeg& g = (M.nseg > 2 && x >= M.s[2].wg0) ? M.s[2] : ((M.nseg > 1 && x >= M.s[1].wg0) ? M.s[1] : M.s[0]);
   const int c = (x - g.wg0) * 256 + threadIdx.x;
@@ -363,11 +415,26 @@ __global__ __launch_bounds__(256) void mcaq_ema_multi_kernel(EmaMulti M) {
   if (g.cmin) g.cmin[c] = lo;
   if (g.cmax) g.cmax[c] = hi;
 }
+__global__ __launch_bounds__(256) void mcaq_ema_multi_kernel(EmaMulti M) { ema_multi_body(M); }
 
 }  // namespace mcaq
 
 namespace mcaq {
 // 16-byte vector rows need 16-byte aligned bases of every per-element array
+// the EMA segments of a launch; returns its workgroup count, or -1
+static inline int ema_multi_args(const mcaq_ema_seg* segs, int nseg, EmaMulti& M) {
+  int wg = 0;
+  for (int k = 0; k < nseg; ++k) {
+    const mcaq_ema_seg& e = segs[k];
+    if (e.C < 1 || !e.batch_min || !e.batch_max || !e.running_min || !e.running_max) return -1;
+    M.s[k] = EmaSeg{e.batch_min, e.batch_max, e.running_min, e.running_max, e.copy_min, e.copy_max,
+                    reinterpret_cast<long long*>(e.num_batches), e.C, e.first ? 1 : 0, wg, (float)e.momentum,
+                    (float)(1.0 - e.momentum)};
+    wg += (e.C + 255) / 256;
+  }
+  M.nseg = nseg;
+  return wg;
+}
 static inline bool qat_aligned16(const mcaq_qat_scale& s, bool bwd) {
   uintptr_t u = (uintptr_t)s.x;
   u |= bwd ? ((uintptr_t)s.g | (uintptr_t)s.gx) : (uintptr_t)s.y;
@@ -402,6 +469,7 @@ static int qat_args(const mcaq_qat_scale* scales, int nscales, bool bwd, mcaq::Q
   }
   a.nscales = nscales;
   a.units_total = units;
+  a.bb = mcaq::QatBudget{};
   return 0;
 }
 
@@ -417,6 +485,29 @@ int mcaq_qat_forward(const mcaq_qat_scale* scales, int nscales, hipStream_t stre
     launch_k((mcaq::mcaq_qat_kernel<false, true>), dim3(a.units_total), dim3(256), 0, stream, a);
   else
     launch_k((mcaq::mcaq_qat_kernel<false, false>), dim3(a.units_total), dim3(256), 0, stream, a);
+  return (int)hipGetLastError();
+}
+
+int mcaq_qat_forward_budget(const mcaq_qat_scale* scales, int nscales, const float* const* bits, const int* n,
+                            int nseg, float target, float* avg, float* loss, hipStream_t stream) {
+  mcaq::QatArgs a;
+  int blocks;
+  const int e = qat_args(scales, nscales, false, a, blocks);
+  if (e) return e;
+  if (!bits || !n || nseg < 1 || nseg > 3 || !avg) return (int)hipErrorInvalidValue;
+  for (int k = 0; k < nseg; ++k) {
+    if (!bits[k] || n[k] < 1) return (int)hipErrorInvalidValue;
+    a.bb.bits[k] = bits[k];
+    a.bb.n[k] = n[k];
+  }
+  a.bb.nseg = nseg; a.bb.target = target; a.bb.avg = avg; a.bb.loss = loss;
+  bool vec = true;
+  for (int i = 0; i < nscales; ++i)
+    vec = vec && ((scales[i].H * scales[i].W) & 3) == 0 && mcaq::qat_aligned16(scales[i], false);
+  if (vec)
+    launch_k((mcaq::mcaq_qat_kernel<false, true>), dim3(a.units_total + 1), dim3(256), 0, stream, a);
+  else
+    launch_k((mcaq::mcaq_qat_kernel<false, false>), dim3(a.units_total + 1), dim3(256), 0, stream, a);
   return (int)hipGetLastError();
 }
 
@@ -454,15 +545,8 @@ int mcaq_ema_stats(const float* batch_min, const float* batch_max, float* runnin
 int mcaq_ema_stats_multi(const mcaq_ema_seg* segs, int nseg, hipStream_t stream) {
   if (!segs || nseg < 1 || nseg > 3) return (int)hipErrorInvalidValue;
   mcaq::EmaMulti M{};
-  int wg = 0;
-  for (int k = 0; k < nseg; ++k) {
-    const mcaq_ema_seg& e = segs[k];
-    if (e.C < 1 || !e.batch_min || !e.batch_max || !e.running_min || !e.running_max) return (int)hipErrorInvalidValue;
-    M.s[k] = mcaq::EmaSeg{e.batch_min, e.batch_max, e.running_min, e.running_max, e.copy_min, e.copy_max,
-                          reinterpret_cast<long long*>(e.num_batches), e.C, e.first ? 1 : 0, wg, (float)e.momentum, (float)(1.0 - e.momentum)};
-    wg += (e.C + 255) / 256;
-  }
-  M.nseg = nseg;
+  const int wg = ema_multi_args(segs, nseg, M);
+  if (wg < 0) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(mcaq::mcaq_ema_multi_kernel, dim3(wg), dim3(256), 0, stream, M);
   return (int)hipGetLastError();
 }

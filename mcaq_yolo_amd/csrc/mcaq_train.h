@@ -217,7 +217,7 @@ struct MapperRunningArgs {
   int count;
   float momentum;
 };
-__global__ __launch_bounds__(64) void mcaq_mapper_running_kernel(MapperRunningArgs A) {
+__device__ __forceinline__ void mapper_running_body(const MapperRunningArgs& A) {
   const int j = threadIdx.x;
   for (int k = 0; k < A.count; ++k) {
 #pragma unroll
@@ -231,6 +231,19 @@ __global__ __launch_bounds__(64) void mcaq_mapper_running_kernel(MapperRunningAr
       }
     }
   }
+}
+__global__ __launch_bounds__(64) void mcaq_mapper_running_kernel(MapperRunningArgs A) { mapper_running_body(A); }
+
+// the quantizers' EMA launch with the mapper's deferred running-statistics
+// update as one extra workgroup (threads 0..63): both are a few hundred
+// floats, and the EMA launch directly follows the mapper in the train step
+struct EmaRunArgs { EmaMulti M; MapperRunningArgs R; int ema_wg; };
+__global__ __launch_bounds__(256) void mcaq_ema_running_kernel(EmaRunArgs a) {
+  if ((int)blockIdx.x >= a.ema_wg) {
+    if (threadIdx.x < 64) mapper_running_body(a.R);
+    return;
+  }
+  ema_multi_body(a.M);
 }
 
 // batch statistics of layer L from the forward partials: mean, rstd of every
@@ -996,6 +1009,20 @@ inline bool smask_stage_ok(const float* absmean, const float* gm, int H, int W, 
 
 constexpr int SM_TH = 1024;   // threads per soft-mask backward workgroup (one image)
 
+// an [n] fp32 plane (16-byte aligned, n % 4 == 0 when staged) into LDS: two
+// 16-byte groups per thread per round, both loads issued before either store
+__device__ __forceinline__ void smask_copy_plane(float* dst, const float* src, int n, int tid) {
+  const int n4 = n >> 2;
+  const float4* s4 = reinterpret_cast<const float4*>(src);
+  for (int e = tid; e < n4; e += 2 * SM_TH) {
+    const int e2 = imin_(e + SM_TH, n4 - 1);
+    const float4 a = s4[e], c = s4[e2];
+    reinterpret_cast<float4*>(dst)[e] = a;
+    if (e + SM_TH < n4) reinterpret_cast<float4*>(dst)[e2] = c;
+  }
+  for (int e = (n4 << 2) + tid; e < n; e += SM_TH) dst[e] = src[e];
+}
+
 __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
   extern __shared__ float smem_tr[];
   const int b = (int)blockIdx.x - A.wg0, H = A.H, W = A.W, ht = A.ht, wt = A.wt, NT = ht * wt;
@@ -1025,10 +1052,7 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
   const float* am = A.absmean + (size_t)b * H * W;
   const float* gm = fold ? nullptr : A.gm + (size_t)b * H * W;
   if (A.stage) {
-    const int n4 = (H * W) >> 2;
-    const float4* s4 = reinterpret_cast<const float4*>(am);
-    for (int e = tid; e < n4; e += SM_TH) reinterpret_cast<float4*>(stg)[e] = s4[e];
-    for (int e = (n4 << 2) + tid; e < H * W; e += SM_TH) stg[e] = am[e];
+    smask_copy_plane(stg, am, H * W, tid);
     __syncthreads();
     am = stg;
   }
@@ -1087,7 +1111,49 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
     const size_t plane = (size_t)A.B * H * W;
     const float* pm = A.qwork + (size_t)b * H * W;
     const float* pf = A.qwork + (size_t)nsl * plane + (size_t)b * H * W;
-    for (int e = tid; e < H * W; e += SM_TH) {
+    // 16-byte groups, two per thread per round, every slice partial of a
+    // round loaded before the first sum (slices KC at a time, the index
+    // clamped: no load behind a branch); summed in slice order as before
+    const bool v4 = ((H * W) & 3) == 0 && (plane & 3) == 0 && ((((uintptr_t)pm) | (uintptr_t)pf) & 15) == 0;
+    const int n4 = v4 ? (H * W) >> 2 : 0;
+    {
+      constexpr int KC = 4;
+      const size_t plane4 = plane >> 2;
+      const float4* pm4 = reinterpret_cast<const float4*>(pm);
+      const float4* pf4 = reinterpret_cast<const float4*>(pf);
+      for (int e4 = tid; e4 < n4; e4 += 2 * SM_TH) {
+        const int e4b = imin_(e4 + SM_TH, n4 - 1);
+        float4 vm = make_float4(0.f, 0.f, 0.f, 0.f), vf = vm, wm = vm, wf = vm;
+        for (int k0 = 0; k0 < nsl; k0 += KC) {
+          float4 lm[KC], lf[KC], km[KC], kf[KC];
+#pragma unroll
+          for (int q = 0; q < KC; ++q) {
+            const size_t o = (size_t)imin_(k0 + q, nsl - 1) * plane4;
+            lm[q] = pm4[o + e4]; lf[q] = pf4[o + e4];
+            km[q] = pm4[o + e4b]; kf[q] = pf4[o + e4b];
+          }
+#pragma unroll
+          for (int q = 0; q < KC; ++q) {
+            if (k0 + q >= nsl) break;
+            if (k0 + q == 0) {
+              vm = lm[0]; vf = lf[0]; wm = km[0]; wf = kf[0];
+            } else {
+              vm.x = vm.x + lm[q].x; vm.y = vm.y + lm[q].y; vm.z = vm.z + lm[q].z; vm.w = vm.w + lm[q].w;
+              vf.x = vf.x + lf[q].x; vf.y = vf.y + lf[q].y; vf.z = vf.z + lf[q].z; vf.w = vf.w + lf[q].w;
+              wm.x = wm.x + km[q].x; wm.y = wm.y + km[q].y; wm.z = wm.z + km[q].z; wm.w = wm.w + km[q].w;
+              wf.x = wf.x + kf[q].x; wf.y = wf.y + kf[q].y; wf.z = wf.z + kf[q].z; wf.w = wf.w + kf[q].w;
+            }
+          }
+        }
+        reinterpret_cast<float4*>(stg)[e4] = vm;
+        reinterpret_cast<float4*>(fpix)[e4] = vf;
+        if (e4 + SM_TH < n4) {
+          reinterpret_cast<float4*>(stg)[e4b] = wm;
+          reinterpret_cast<float4*>(fpix)[e4b] = wf;
+        }
+      }
+    }
+    for (int e = (n4 << 2) + tid; e < H * W; e += SM_TH) {
       float vm = pm[e], vf = pf[e];
       for (int k = 1; k < nsl; ++k) { vm = vm + pm[(size_t)k * plane + e]; vf = vf + pf[(size_t)k * plane + e]; }
       stg[e] = vm;
@@ -1119,10 +1185,7 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
     }
   } else if (A.stage) {
     __syncthreads();   // every pooling read of the staged |x| plane is done
-    const int n4 = (H * W) >> 2;
-    const float4* s4 = reinterpret_cast<const float4*>(gm);
-    for (int e = tid; e < n4; e += SM_TH) reinterpret_cast<float4*>(stg)[e] = s4[e];
-    for (int e = (n4 << 2) + tid; e < H * W; e += SM_TH) stg[e] = gm[e];
+    smask_copy_plane(stg, gm, H * W, tid);
     __syncthreads();
     gm = stg;
   }
@@ -1232,30 +1295,37 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
     float* dst = A.gbits + (size_t)b * NT + u;
     *dst = fold ? fgb[u] + gb : (A.accumulate ? *dst + gb : gb);
   }
-  // ---- parameter partials of this image
+  // ---- parameter partials of this image: element e on wave e % 16, its
+  // tiles over the wave's lanes (tile lane + 64 k), then a fixed shuffle tree
+  // (deterministic; the elements' sums used to run serially over all tiles
+  // on 170 threads)
   float* gp = A.gpart + (size_t)b * SG_SIZE;
-  for (int e = tid; e < SG_SIZE; e += SM_TH) {
+  const int lane = tid & 63, wv = tid >> 6;
+  const float rwt = 1.0f / (float)wt;   // tile row of t: floor((t + 0.5) / wt) is exact for t < 2^14
+  for (int e = wv; e < SG_SIZE; e += SM_TH / 64) {
     float s = 0.0f;
     if (e < SG_B1) {                  // W1[oc][ic][qq]
       const int oc = e / 18, ic = (e / 9) & 1, qq = e % 9;
+      const int di = qq / 3 - 1, dj = qq % 3 - 1;
       const float* f = ic == 0 ? f0 : f1;
-      for (int t = 0; t < NT; ++t) {
-        const int i = t / wt, j = t - i * wt;
-        const int ii = i + qq / 3 - 1, jj = j + qq % 3 - 1;
-        if (ii < 0 || ii >= ht || jj < 0 || jj >= wt) continue;
-        s = fmaf(gpre[t * 8 + oc], f[ii * wt + jj], s);
+      for (int t = lane; t < NT; t += 64) {
+        const int i = (int)(((float)t + 0.5f) * rwt), j = t - i * wt;
+        const int ii = i + di, jj = j + dj;
+        if (ii >= 0 && ii < ht && jj >= 0 && jj < wt) s = fmaf(gpre[t * 8 + oc], f[ii * wt + jj], s);
       }
     } else if (e < SG_W2) {           // b1
       const int oc = e - SG_B1;
-      for (int t = 0; t < NT; ++t) s += gpre[t * 8 + oc];
+      for (int t = lane; t < NT; t += 64) s += gpre[t * 8 + oc];
     } else if (e < SG_B2) {           // W2[o][ic]: g_l(o) relu_ic, g_l1 = -g_l0
       const int o = (e - SG_W2) >> 3, ic = (e - SG_W2) & 7;
-      for (int t = 0; t < NT; ++t) s = fmaf(o == 0 ? gl[t] : -gl[t], rel[t * 8 + ic], s);
+      for (int t = lane; t < NT; t += 64) s = fmaf(o == 0 ? gl[t] : -gl[t], rel[t * 8 + ic], s);
     } else {                          // b2
       const int o = e - SG_B2;
-      for (int t = 0; t < NT; ++t) s += o == 0 ? gl[t] : -gl[t];
+      for (int t = lane; t < NT; t += 64) s += o == 0 ? gl[t] : -gl[t];
     }
-    gp[e] = s;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (lane == 0) gp[e] = s;
   }
 }
 __global__ __launch_bounds__(SM_TH) void mcaq_smask_bwd_kernel(MaskTrainArgs A) { mcaq_smask_bwd_body(A); }
@@ -1452,6 +1522,25 @@ int mcaq_mapper_running_update(const mcaq_mapper_params* P, const float* const* 
     A.rstat[k] = mapper_work(const_cast<float*>(works[k]), ns[k]).rstat;
   }
   hipLaunchKernelGGL(mcaq_mapper_running_kernel, dim3(1), dim3(64), 0, stream, A);
+  return (int)hipGetLastError();
+}
+
+int mcaq_ema_stats_multi_running(const mcaq_ema_seg* segs, int nseg, const mcaq_mapper_params* P,
+                                 const float* const* works, const int* ns, int count, float momentum,
+                                 hipStream_t stream) {
+  using namespace mcaq;
+  if (!segs || nseg < 1 || nseg > 3 || !P || !works || !ns || count < 1 || count > MAPPER_RU_MAX)
+    return (int)hipErrorInvalidValue;
+  EmaRunArgs a{};
+  const int wg = ema_multi_args(segs, nseg, a.M);
+  if (wg < 0) return (int)hipErrorInvalidValue;
+  a.R.P = *P; a.R.count = count; a.R.momentum = momentum;
+  for (int k = 0; k < count; ++k) {
+    if (!works[k] || ns[k] < 1) return (int)hipErrorInvalidValue;
+    a.R.rstat[k] = mapper_work(const_cast<float*>(works[k]), ns[k]).rstat;
+  }
+  a.ema_wg = wg;
+  hipLaunchKernelGGL(mcaq_ema_running_kernel, dim3(wg + 1), dim3(256), 0, stream, a);
   return (int)hipGetLastError();
 }
 

@@ -83,7 +83,7 @@ def _ema_multi_ok(qs, xs):
     return True
 
 
-def _ema_multi(qs, xs, box):
+def _ema_multi(qs, xs, box, running=None):
     """quantization.py:319-353 for every scale's quantizer: the batch min /
     max from the analyzer's pass-1 partials (one finalize launch for all
     scales), then the EMA, this step's copies and num_batches_tracked (one
@@ -127,8 +127,21 @@ def _ema_multi(qs, xs, box):
             keep[2 * i].copy_(-vec[o:o + C])
             keep[2 * i + 1].copy_(vec[o + C:o + 2 * C])
             o += 2 * C
-    abi.check(L.mcaq_ema_stats_multi(segs, n, _stream()), "mcaq_ema_stats_multi")
+    if running is not None:
+        # + the mapper's running-statistics update as one extra workgroup
+        rq, wa, na, cnt, mom = running
+        abi.check(L.mcaq_ema_stats_multi_running(segs, n, ctypes.byref(rq), wa, na, cnt, mom, _stream()),
+                  "mcaq_ema_stats_multi_running")
+    else:
+        abi.check(L.mcaq_ema_stats_multi(segs, n, _stream()), "mcaq_ema_stats_multi")
     return mins, maxs
+
+
+def _flush_running(pending):
+    """The mapper's deferred BatchNorm running-statistics update on its own."""
+    q, wa, na, n, mom = pending
+    abi.check(abi.lib().mcaq_mapper_running_update(ctypes.byref(q), wa, na, n, mom, _stream()),
+              "mcaq_mapper_running_update")
 
 
 def _run_analyzer_multi(an, xs):
@@ -300,8 +313,11 @@ class _MapperMulti(torch.autograd.Function):
             ctx.gath1, ctx.world = gath[1], world
         wa = (abi.P * n)(*[_p(w) for w in works])
         na = (abi.I * n)(*[c.numel() for c in cfs])
-        abi.check(L.mcaq_mapper_running_update(ctypes.byref(q), wa, na, n, mom, _stream()),
-                  "mcaq_mapper_running_update")
+        if pg is None and getattr(mod, "_defer_running", False):
+            # the quantizers' EMA launch that follows applies it (forward_features)
+            mod._pending_running = (q, wa, na, n, mom)
+        else:
+            _flush_running((q, wa, na, n, mom))
         ctx.q, ctx.T, ctx.mod, ctx.n = q, T, mod, n
         ctx.shapes = [c.shape for c in cs]
         ctx.save_for_backward(*cfs, *works, *params)
@@ -467,13 +483,14 @@ class _MaskQuantMulti(torch.autograd.Function):
             q = core._qat_struct(xs[i], bf[i], ms[i], mins[i], maxs[i])
             q.y = _p(y)
             arr[i] = q
-        abi.check(L.mcaq_qat_forward(arr, n, st), "mcaq_qat_forward")
         dev = xs[0].device
         avg = torch.empty((), device=dev)
         loss = torch.empty((), device=dev)
         bp = (abi.P * n)(*[_p(b) for b in bf])
         bn = (abi.I * n)(*[b.numel() for b in bf])
-        abi.check(L.mcaq_bit_budget_forward(bp, bn, n, float(target), _p(avg), _p(loss), st), "mcaq_bit_budget_forward")
+        # the quantizer and the bit budget (one extra workgroup) in one launch
+        abi.check(L.mcaq_qat_forward_budget(arr, n, bp, bn, n, float(target), _p(avg), _p(loss), st),
+                  "mcaq_qat_forward_budget")
         ctx.mods, ctx.n, ctx.target = mods, n, float(target)
         ctx.save_for_backward(*xs, *bf, *ms, *absmeans, *mins, *maxs, avg)
         return tuple(ys) + (avg, loss)
@@ -644,25 +661,43 @@ def forward_features(hooks, feats, state):
             hi = torch.quantile(flat, 0.98, dim=1, keepdim=True).unsqueeze(-1)
             cs[i] = ((c - lo) / (hi - lo + 1e-8)).clamp(0.0, 1.0)
     T = state.get("temperature", 1.0)
-    if isinstance(mapper, core.ComplexityToBitMappingNetwork):
-        ncs = [core._normalize_complexity_shape(c) for c in cs]
-        bits = list(_MapperMulti.apply(mapper, T, True, n, *ncs, *mapper.mapping_network.parameters()))
-    else:
-        bits = [mapper(c, T, return_continuous=True) for c in cs]
+    quantize = state.get("quantize", True)
+    qs = [hooks.quantizers[str(i)] for i in idxs]
+    per_quantizer = not (quantize and _ema_multi_ok(qs, xs))
+    try:
+        if isinstance(mapper, core.ComplexityToBitMappingNetwork):
+            ncs = [core._normalize_complexity_shape(c) for c in cs]
+            # the mapper's running-statistics update rides on the EMA launch
+            mapper._defer_running, mapper._pending_running = not per_quantizer, None
+            bits = list(_MapperMulti.apply(mapper, T, True, n, *ncs, *mapper.mapping_network.parameters()))
+        else:
+            bits = [mapper(c, T, return_continuous=True) for c in cs]
+        return _quantize_multi(hooks, feats, state, n, idxs, xs, box, cs, bits, qs, per_quantizer)
+    finally:
+        pend = getattr(mapper, "_pending_running", None)
+        mapper._defer_running, mapper._pending_running = False, None
+        if pend is not None:
+            _flush_running(pend)
+
+
+def _quantize_multi(hooks, feats, state, n, idxs, xs, box, cs, bits, qs, per_quantizer):
+    """forward_features after the mapper: EMA statistics, soft masks, the
+    quantizers (and the bit budget)."""
+    mapper = hooks.bit_mapper
     quantize = state.get("quantize", True)
     if not quantize:
         for i in range(n):
             state.setdefault("aux", []).append({"layer": idxs[i], "complexity": cs[i], "bit_map": bits[i],
                                                 "features_q": feats[i]})
         return list(feats)
-    qs = [hooks.quantizers[str(i)] for i in idxs]
     mins, maxs = [], []
     for i, x in enumerate(xs):
         if bits[i].dim() != 3 or bits[i].shape[0] != x.shape[0]:
             raise AssertionError(f"Batch size mismatch: {x.shape[0]} vs {bits[i].shape[0]}")
-    per_quantizer = not _ema_multi_ok(qs, xs)
     if not per_quantizer:
-        mins, maxs = _ema_multi(qs, xs, box)
+        running = getattr(mapper, "_pending_running", None)
+        mapper._pending_running = None
+        mins, maxs = _ema_multi(qs, xs, box, running)
     for i, (q, x) in enumerate(zip(qs, xs) if per_quantizer else ()):
         B, C, H, W = x.shape
         p1 = box[i]

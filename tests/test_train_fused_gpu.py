@@ -104,8 +104,21 @@ def _cmp_grads(g1, g0):
 
 @pytest.mark.parametrize("temperature", [1.0, 2.5])
 def test_fused_train_step_matches_torch_path(temperature):
-    o1, a1, gx1, g1, b1 = _step(True, temperature=temperature)
-    o0, a0, gx0, g0, b0 = _step(False, temperature=temperature)
+    _check_step_vs_torch(temperature)
+
+
+def test_fused_train_step_config5_bs16_matches_torch_path():
+    """The whole QAT hook step at BASELINE config 5's per-GPU batch (yolov8n
+    bs16, 640x640: C3 64x80x80, C4 128x40x40, C5 256x20x20) - the multi-scale
+    launches with the fused soft-mask / quantizer / bit-budget node, as
+    bench.py --config 5 runs it - against the reference's per-scale torch
+    path, at the tolerances of the B = 4 test."""
+    _check_step_vs_torch(1.0, B=16)
+
+
+def _check_step_vs_torch(temperature, B=4):
+    o1, a1, gx1, g1, b1 = _step(True, B=B, temperature=temperature)
+    o0, a0, gx0, g0, b0 = _step(False, B=B, temperature=temperature)
     for a, b in zip(a1, a0):
         assert torch.equal(a["complexity"], b["complexity"]), "analyzer forward (morph kernel) differs"
         _rel(a["bit_map"], b["bit_map"], 1e-5)
