@@ -44,7 +44,7 @@ typedef void* hipEvent_t;
 extern "C" {
 #endif
 
-#define MCAQ_ABI_VERSION 19
+#define MCAQ_ABI_VERSION 20
 /* segments (hook scale x batch) per mcaq_stats / mcaq_finalize /
  * mcaq_morph* / mcaq_quant launch */
 #define MCAQ_MAX_SEGMENTS 9
@@ -492,15 +492,17 @@ typedef struct {
 } mcaq_pack_seg;
 int mcaq_pack(const mcaq_pack_seg* segs, int nseg, float* out, int total, hipStream_t stream);
 
-/* ---- the optimizer end of a QAT step in ONE launch ------------------------
+/* ---- the optimizer end of a QAT step in two launches ----------------------
  * torch.nn.utils.clip_grad_norm_(max_norm) over every segment's gradient
  * (the norm of the per-tensor 2-norms; .grad scaled in place), then
  * torch.optim.AdamW (decoupled weight decay, the fused kernel's update
  * order; *step += 1 first, as a capturable AdamW's step tensor) and, for
  * segments with project_abs, p <- |p| (the bit mapper's Eq. 18 projection,
  * bit_allocation.py:186-197) - train.py:626-641.  max_norm <= 0: no clip;
- * total_norm (1 float) receives the pre-clip norm, or NULL.  One 1024-thread
- * workgroup (the hook parameters are ~8 k floats). */
+ * total_norm (1 float) receives the pre-clip norm, or NULL.  work:
+ * mcaq_clip_adamw_work_floats(total elements) floats of device scratch.  Two
+ * launches over 1,024-element chunks (per-chunk squared-norm partials, then
+ * norm + update); capturable. */
 #define MCAQ_OPT_MAXSEG 64
 #define MCAQ_OPT_MAXGROUPS 4
 typedef struct {
@@ -510,8 +512,9 @@ typedef struct {
 typedef struct {
   double lr, weight_decay, beta1, beta2, eps;   /* doubles, as torch's fused AdamW takes them */
 } mcaq_adamw_group;
+size_t mcaq_clip_adamw_work_floats(int total);
 int mcaq_clip_adamw(const mcaq_adamw_seg* segs, int nseg, const mcaq_adamw_group* groups, int ngroups,
-                    float* step, float max_norm, float* total_norm, hipStream_t stream);
+                    float* step, float max_norm, float* total_norm, float* work, hipStream_t stream);
 
 int mcaq_abi_version(void);
 

@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libmcaq_hip.so")
-ABI_VERSION = 19
+ABI_VERSION = 20
 MAX_SEGMENTS = 9   # MCAQ_MAX_SEGMENTS: segments (hook scale x batch) per launch
 
 P = ctypes.c_void_p
@@ -149,7 +149,7 @@ EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats",
            "mcaq_mapper_train_grad_reduce", "mcaq_mapper_running_update", "mcaq_head_train_grad_reduce",
            "mcaq_mapper_train_forward_multi", "mcaq_mapper_train_backward_multi", "mcaq_head_train_backward_multi",
            "mcaq_smask_train_backward_multi", "mcaq_train_reduce_multi", "mcaq_ema_stats_multi",
-           "mcaq_mapper_train_forward_stage_multi", "mcaq_mapper_train_backward_stage_multi", "mcaq_clip_adamw",
+           "mcaq_mapper_train_forward_stage_multi", "mcaq_mapper_train_backward_stage_multi", "mcaq_clip_adamw", "mcaq_clip_adamw_work_floats",
            "mcaq_bit_budget_forward", "mcaq_qat_smask_backward_multi", "mcaq_qat_forward_budget",
            "mcaq_ema_stats_multi_running")
 
@@ -256,7 +256,9 @@ def _declare(lib):
     lib.mcaq_qat_smask_backward_multi.restype = I
     lib.mcaq_qat_smask_backward_multi.argtypes = [ctypes.POINTER(QatSmaskSeg), I, ctypes.POINTER(BitBudget), P]
     lib.mcaq_clip_adamw.restype = I
-    lib.mcaq_clip_adamw.argtypes = [ctypes.POINTER(AdamwSeg), I, ctypes.POINTER(AdamwGroup), I, P, Fl, P, P]
+    lib.mcaq_clip_adamw.argtypes = [ctypes.POINTER(AdamwSeg), I, ctypes.POINTER(AdamwGroup), I, P, Fl, P, P, P]
+    lib.mcaq_clip_adamw_work_floats.restype = ctypes.c_size_t
+    lib.mcaq_clip_adamw_work_floats.argtypes = [I]
     lib.mcaq_smask_train_backward.restype = I
     lib.mcaq_smask_train_backward.argtypes = [ctypes.POINTER(SmaskParams), P, P, P, I, I, I, I, I, P, I, P, P, P]
     return lib

@@ -1,21 +1,24 @@
-// mcaq_optim.h - the optimizer end of the QAT training step in ONE launch:
+// mcaq_optim.h - the optimizer end of the QAT training step in TWO launches:
 // global gradient-norm clip (torch.nn.utils.clip_grad_norm_), AdamW with
 // decoupled weight decay (torch.optim.AdamW) and the |W| projection of the
 // bit mapper (bit_allocation.py:186-197, Eq. 18) - train.py:626-641 issues
 // them as ~14 small ATen / multi-tensor kernels per step on ~8 k floats of
 // hook parameters.
 //
-// One 1024-thread workgroup over the flat concatenation of the segments
-// (parameter tensors), 4 consecutive elements a thread per 4 K chunk: every
-// load of a phase is issued at once.  The squared gradients of a chunk are
-// staged in LDS and each segment's part summed by one wave in element order
-// (per-tensor norms; thread 0 combines them in tensor order into the total
-// norm, the norm of the per-tensor norms as clip_grad_norm_ computes it);
-// then every thread loads its elements' gradient, parameter and moments
-// before clipping, updating and projecting them.  The per-element update is torch's fused AdamW
-// arithmetic (double hyper-parameters); the norm reduces in another order
-// than ATen's, so the values agree with torch's clip + fused AdamW within
-// fp32 rounding (tests/test_optim_gpu.py), not bit for bit.
+// Both launches cut the flat concatenation of the segments (parameter
+// tensors) into 1,024-element chunks, one 256-thread workgroup each, 4
+// consecutive elements a thread.  Launch 1: every chunk's squared gradients
+// staged in LDS, each segment's part summed by one wave in element order ->
+// work[chunk][segment].  Launch 2: every workgroup folds those partials in
+// chunk order into the per-tensor squared norms, combines them in tensor
+// order into the total norm (the norm of the per-tensor norms, as
+// clip_grad_norm_ computes it) and the clip coefficient, then updates its
+// chunk: torch's fused AdamW arithmetic (double hyper-parameters) and |W|.
+// The norm reduces in another order than ATen's, so the values agree with
+// torch's clip + fused AdamW within fp32 rounding (tests/test_optim_gpu.py),
+// not bit for bit.  (Round 5 first ran both phases in ONE 1,024-thread
+// workgroup: 25 us in the graph; two launches over ~9 workgroups each take
+// less: the per-chunk work is one load round trip, not eight.)
 #pragma once
 
 namespace mcaq {
@@ -32,11 +35,13 @@ struct AdamwArgs {
   float* total_norm;   // or nullptr
 };
 
-constexpr int OPT_TH = 1024;
+constexpr int OPT_TH = 256;
+constexpr int OPT_E = 4;                    // consecutive elements per thread
+constexpr int OPT_CH = OPT_TH * OPT_E;      // elements per chunk (one workgroup)
+constexpr int OPT_WORK0 = 4;                // work[0]: the step after this one; partials from work[4]
 
 // beta^step for an integer-valued step by binary exponentiation in double (a
-// few multiplies instead of the library pow, whose code the one-shot kernel
-// would fetch cold; within an ulp or two of pow)
+// few multiplies instead of the library pow; within an ulp or two of pow)
 __device__ __forceinline__ double pow_int(double b, float step) {
   long long e = (long long)step;
   double r = 1.0;
@@ -47,31 +52,17 @@ __device__ __forceinline__ double pow_int(double b, float step) {
   }
   return r;
 }
-constexpr int OPT_E = 4;                    // consecutive elements per thread per chunk
-constexpr int OPT_CH = OPT_TH * OPT_E;      // elements per chunk (their squares staged in LDS)
 
-__global__ __launch_bounds__(OPT_TH) void mcaq_clip_adamw_kernel(AdamwArgs a) {
-  __shared__ mcaq_adamw_seg sg[MCAQ_OPT_MAXSEG];
-  __shared__ int st[MCAQ_OPT_MAXSEG + 1];     // first flat element of each segment
-  __shared__ float sq[OPT_CH];
-  __shared__ float seg_acc[MCAQ_OPT_MAXSEG];
-  __shared__ float coef_s;
-  __shared__ float g_bc2s[MCAQ_OPT_MAXGROUPS], g_ss[MCAQ_OPT_MAXGROUPS];
-  __shared__ double g_hp[MCAQ_OPT_MAXGROUPS][6];   // lr * wd, beta1, 1 - beta1, beta2, 1 - beta2, eps
-  const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  constexpr int NW = OPT_TH / 64;
-  const int nseg = a.nseg;
-  {
-    // the segment table into LDS, a dword per thread (the kernel-argument
-    // segment read through a pointer: no per-lane indexing of the argument)
-    constexpr int SW = (int)(sizeof(mcaq_adamw_seg) / 4);
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(&a.s[0]);
-    for (int i = tid; i < nseg * SW; i += OPT_TH) reinterpret_cast<uint32_t*>(sg)[i] = src[i];
-    if (tid < nseg) seg_acc[tid] = 0.0f;
-  }
+// the segment table into LDS (a dword per thread, from the kernel argument
+// through a pointer: no per-lane indexing of the argument) and the segments'
+// first flat elements (exclusive scan of the sizes over wave 0)
+__device__ __forceinline__ void opt_table(const AdamwArgs& a, mcaq_adamw_seg* sg, int* st) {
+  const int tid = (int)threadIdx.x, nseg = a.nseg;
+  constexpr int SW = (int)(sizeof(mcaq_adamw_seg) / 4);
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(&a.s[0]);
+  for (int i = tid; i < nseg * SW; i += OPT_TH) reinterpret_cast<uint32_t*>(sg)[i] = src[i];
   __syncthreads();
   if (tid < 64) {
-    // segment starts: an exclusive scan of the sizes over one wave (64 per round)
     int carry = 0;
     for (int k0 = 0; k0 < nseg; k0 += 64) {
       const int k = k0 + tid;
@@ -86,7 +77,89 @@ __global__ __launch_bounds__(OPT_TH) void mcaq_clip_adamw_kernel(AdamwArgs a) {
     }
     if (tid == 0) st[nseg] = carry;
   }
-  const float step = a.step[0] + 1.0f;
+  __syncthreads();
+}
+
+// the segment holding flat element j (binary search over the starts)
+__device__ __forceinline__ int opt_seg_of(const int* st, int nseg, int j) {
+  int lo = 0, hi = nseg - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (st[mid] <= j) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+// launch 1: this chunk's squared-gradient sum of every segment (0 where the
+// segment does not overlap the chunk) -> work[OPT_WORK0 + chunk * nseg + k]
+__global__ __launch_bounds__(OPT_TH) void mcaq_adamw_norm_kernel(AdamwArgs a, float* work) {
+  __shared__ mcaq_adamw_seg sg[MCAQ_OPT_MAXSEG];
+  __shared__ int st[MCAQ_OPT_MAXSEG + 1];
+  __shared__ float sq[OPT_CH];
+  const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int nseg = a.nseg;
+  opt_table(a, sg, st);
+  const int total = st[nseg];
+  const int base = (int)blockIdx.x * OPT_CH, e0 = base + tid * OPT_E;
+  int k = opt_seg_of(st, nseg, imin_(e0, total - 1));
+  float v[OPT_E];
+#pragma unroll
+  for (int q = 0; q < OPT_E; ++q) {
+    const int j = imin_(e0 + q, total - 1);
+    while (k + 1 < nseg && j >= st[k + 1]) ++k;
+    v[q] = sg[k].grad[j - st[k]];
+  }
+#pragma unroll
+  for (int q = 0; q < OPT_E; ++q) sq[tid * OPT_E + q] = e0 + q < total ? v[q] * v[q] : 0.0f;
+  __syncthreads();
+  float* out = work + OPT_WORK0 + (size_t)blockIdx.x * nseg;
+  for (int kk = wv; kk < nseg; kk += OPT_TH / 64) {
+    const int lo = imax_(st[kk], base), hi = imin_(st[kk + 1], base + OPT_CH);
+    float acc = 0.0f;
+    if (lo < hi) {
+      // four independent partial sums per lane (fixed order), then the wave
+      float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+      int i = lo + lane;
+      for (; i + 192 < hi; i += 256) {
+        a0 += sq[i - base]; a1 += sq[i + 64 - base]; a2 += sq[i + 128 - base]; a3 += sq[i + 192 - base];
+      }
+      for (; i < hi; i += 64) a0 += sq[i - base];
+      acc = (a0 + a1) + (a2 + a3);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    }
+    if (lane == 0) out[kk] = acc;
+  }
+  if (blockIdx.x == 0 && tid == 0) work[0] = a.step[0] + 1.0f;
+}
+
+// launch 2: the clip coefficient from launch 1's partials (every workgroup
+// the same, in the same order), then AdamW and |W| on this chunk
+__global__ __launch_bounds__(OPT_TH) void mcaq_adamw_update_kernel(AdamwArgs a, const float* work, int nchunk) {
+  __shared__ mcaq_adamw_seg sg[MCAQ_OPT_MAXSEG];
+  __shared__ int st[MCAQ_OPT_MAXSEG + 1];
+  __shared__ float seg_acc[MCAQ_OPT_MAXSEG];
+  __shared__ float coef_s;
+  __shared__ float g_bc2s[MCAQ_OPT_MAXGROUPS], g_ss[MCAQ_OPT_MAXGROUPS];
+  __shared__ double g_hp[MCAQ_OPT_MAXGROUPS][6];   // lr * wd, beta1, 1 - beta1, beta2, 1 - beta2, eps
+  const int tid = (int)threadIdx.x;
+  const int nseg = a.nseg;
+  const bool clip = a.max_norm > 0.0f;
+  const float step = work[0];
+  // per-tensor squared norms: the chunks' partials in chunk order, 8 loads
+  // of a thread in flight (clamped index)
+  if (clip && tid < nseg) {
+    const float* pk = work + OPT_WORK0 + tid;
+    float s = 0.0f;
+    for (int w0 = 0; w0 < nchunk; w0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) v[r] = pk[(size_t)imin_(w0 + r, nchunk - 1) * nseg];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) s = w0 + r < nchunk ? s + v[r] : s;
+    }
+    seg_acc[tid] = s;
+  }
   if (tid < MCAQ_OPT_MAXGROUPS) {
     // bias corrections of each hyper-parameter group (fused AdamW: fp32
     // values of the double expressions)
@@ -99,53 +172,8 @@ __global__ __launch_bounds__(OPT_TH) void mcaq_clip_adamw_kernel(AdamwArgs a) {
     g_hp[tid][3] = G.beta2; g_hp[tid][4] = 1.0 - G.beta2;
     g_hp[tid][5] = G.eps;
   }
-  __syncthreads();
-  const int total = st[nseg];
-  const bool clip = a.max_norm > 0.0f;
-  // flat elements [e0, e0 + 4) of a chunk per thread: the segment of the
-  // first by binary search, then walked forward
-  auto seg_of = [&](int j) {
-    int lo = 0, hi = nseg - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (st[mid] <= j) lo = mid; else hi = mid - 1;
-    }
-    return lo;
-  };
-  // ---- per-tensor squared-gradient sums: squares staged in LDS, each
-  // segment's part of a chunk summed by one wave in element order, chunks in
-  // order - deterministic
+  opt_table(a, sg, st);    // (its barriers also publish seg_acc and the group table)
   if (clip) {
-    for (int base = 0; base < total; base += OPT_CH) {
-      const int e0 = base + tid * OPT_E;
-      int k = e0 < total ? seg_of(e0) : 0;
-      float v[OPT_E];
-#pragma unroll
-      for (int q = 0; q < OPT_E; ++q) {
-        const int j = e0 + q;
-        while (k + 1 < nseg && j >= st[k + 1]) ++k;
-        v[q] = j < total ? sg[k].grad[j - st[k]] : 0.0f;
-      }
-#pragma unroll
-      for (int q = 0; q < OPT_E; ++q) sq[tid * OPT_E + q] = v[q] * v[q];
-      __syncthreads();
-      for (int kk = wv; kk < nseg; kk += NW) {
-        const int lo = st[kk] > base ? st[kk] : base;
-        const int hi = st[kk + 1] < base + OPT_CH ? st[kk + 1] : base + OPT_CH;
-        if (lo >= hi) continue;
-        // four independent partial sums per lane (fixed order), then the wave
-        float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
-        int i = lo + lane;
-        for (; i + 192 < hi; i += 256) {
-          a0 += sq[i - base]; a1 += sq[i + 64 - base]; a2 += sq[i + 128 - base]; a3 += sq[i + 192 - base];
-        }
-        for (; i < hi; i += 64) a0 += sq[i - base];
-        float acc = (a0 + a1) + (a2 + a3);
-        for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-        if (lane == 0) seg_acc[kk] += acc;
-      }
-      __syncthreads();
-    }
     if (tid < 64) {
       // the norm of the per-tensor norms (clip_grad_norm_): squares of the
       // tensor norms summed over the wave (fixed tree)
@@ -154,10 +182,11 @@ __global__ __launch_bounds__(OPT_TH) void mcaq_clip_adamw_kernel(AdamwArgs a) {
         const float nk = sqrtf(seg_acc[k]);
         t2 = fmaf(nk, nk, t2);
       }
+#pragma unroll
       for (int o = 32; o > 0; o >>= 1) t2 += __shfl_xor(t2, o, 64);
       const float tot = sqrtf(t2);
       if (tid == 0) {
-        if (a.total_norm) a.total_norm[0] = tot;
+        if (a.total_norm && blockIdx.x == 0) a.total_norm[0] = tot;
         const float c = a.max_norm / (tot + 1e-6f);
         coef_s = c < 1.0f ? c : 1.0f;   // clamp(max=1.0); NaN propagates as in torch
         if (!(c == c)) coef_s = c;
@@ -168,16 +197,16 @@ __global__ __launch_bounds__(OPT_TH) void mcaq_clip_adamw_kernel(AdamwArgs a) {
   }
   __syncthreads();
   const float coef = coef_s;
+  const int total = st[nseg];
   // ---- AdamW per element, then |W|.  The arithmetic of torch's
   // _fused_adamw_ (adam_math, fused_adam_utils.cuh): hyper-parameters are
   // doubles, so the weight decay and both moment updates are evaluated in
   // double and rounded once to fp32 (an fp32 1 - beta2 alone is 1.3e-5 off);
   // step size and denominator are fp32 values, the final update fp32.
   // A thread loads its 4 elements' gradient, parameter and moments first.
-  for (int base = 0; base < total; base += OPT_CH) {
-    const int e0 = base + tid * OPT_E;
-    if (e0 >= total) continue;
-    int k = seg_of(e0);
+  const int e0 = (int)blockIdx.x * OPT_CH + tid * OPT_E;
+  if (e0 < total) {
+    int k = opt_seg_of(st, nseg, e0);
     int ks[OPT_E];
     float gv[OPT_E], pv[OPT_E], mv[OPT_E], vv[OPT_E];
 #pragma unroll
@@ -214,32 +243,44 @@ __global__ __launch_bounds__(OPT_TH) void mcaq_clip_adamw_kernel(AdamwArgs a) {
       S.param[e] = p;
     }
   }
-  __syncthreads();
-  if (tid == 0) a.step[0] = step;
+  if (blockIdx.x == 0 && tid == 0) a.step[0] = step;   // every workgroup read the step from work[0]
 }
 
 }  // namespace mcaq
 
 extern "C" {
 
+size_t mcaq_clip_adamw_work_floats(int total) {
+  return (size_t)mcaq::OPT_WORK0 + (size_t)((total + mcaq::OPT_CH - 1) / mcaq::OPT_CH) * MCAQ_OPT_MAXSEG;
+}
+
 int mcaq_clip_adamw(const mcaq_adamw_seg* segs, int nseg, const mcaq_adamw_group* groups, int ngroups,
-                    float* step, float max_norm, float* total_norm, hipStream_t stream) {
+                    float* step, float max_norm, float* total_norm, float* work, hipStream_t stream) {
   using namespace mcaq;
-  if (!segs || !groups || !step || nseg < 1 || nseg > MCAQ_OPT_MAXSEG || ngroups < 1 || ngroups > MCAQ_OPT_MAXGROUPS)
+  if (!segs || !groups || !step || !work || nseg < 1 || nseg > MCAQ_OPT_MAXSEG || ngroups < 1 ||
+      ngroups > MCAQ_OPT_MAXGROUPS)
     return (int)hipErrorInvalidValue;
   AdamwArgs a{};
+  long long total = 0;
   for (int k = 0; k < nseg; ++k) {
     const mcaq_adamw_seg& g = segs[k];
     if (!g.param || !g.grad || !g.exp_avg || !g.exp_avg_sq || g.n < 1 || g.group < 0 || g.group >= ngroups)
       return (int)hipErrorInvalidValue;
     a.s[k] = g;
+    total += g.n;
   }
+  if (total > (1LL << 30)) return (int)hipErrorInvalidValue;
   for (int k = 0; k < ngroups; ++k) a.g[k] = groups[k];
   a.nseg = nseg;
   a.step = step;
   a.max_norm = max_norm;
   a.total_norm = total_norm;
-  hipLaunchKernelGGL(mcaq_clip_adamw_kernel, dim3(1), dim3(OPT_TH), 0, stream, a);
+  const int nchunk = (int)((total + OPT_CH - 1) / OPT_CH);
+  // launch 1 also writes work[0] (the next step count) for launch 2
+  hipLaunchKernelGGL(mcaq_adamw_norm_kernel, dim3(nchunk), dim3(OPT_TH), 0, stream, a, work);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(mcaq_adamw_update_kernel, dim3(nchunk), dim3(OPT_TH), 0, stream, a, (const float*)work, nchunk);
   return (int)hipGetLastError();
 }
 

@@ -75,18 +75,18 @@ __device__ __forceinline__ void chan_combine(const float* part, int nwg, int str
 // ---- parameter-gradient reduction ------------------------------------------
 // sum_w part[w * stride + e] in workgroup order; the loads of 8 partials are
 // issued before their adds (the sum is a chain of dependent adds, the loads
-// are not: one memory latency per 8 partials instead of per partial)
+// are not: one memory latency per 8 partials instead of per partial) - the
+// last, partial group too (clamped index, the surplus not added; it used to
+// take one latency per partial)
 __device__ __forceinline__ float tr_ordered_sum(const float* __restrict__ part, int nwg, int stride, int e) {
   float s = 0.0f;
-  int w = 0;
-  for (; w + 8 <= nwg; w += 8) {
+  for (int w = 0; w < nwg; w += 8) {
     float v[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = part[(size_t)(w + k) * stride + e];
+    for (int k = 0; k < 8; ++k) v[k] = part[(size_t)imin_(w + k, nwg - 1) * stride + e];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) s += v[k];
+    for (int k = 0; k < 8; ++k) s = w + k < nwg ? s + v[k] : s;
   }
-  for (; w < nwg; ++w) s += part[(size_t)w * stride + e];
   return s;
 }
 
@@ -329,6 +329,15 @@ __device__ __forceinline__ void mapper_fwd_stage(const MapperTrainArgs& A, MapFw
   const bool valid = t < A.n;
   const int tc = valid ? t : A.n - 1;
   const float nvalid = (float)imin_(TR_TPB, A.n - wgi * TR_TPB);
+  // this lane's previous-layer activations first: in flight through the
+  // batch statistics below
+  constexpr int KP = S == 2 ? 32 : (S == 3 ? 64 : 32);
+  float apv[S >= 2 ? KP / MW : 1];
+  if constexpr (S >= 2) {
+    const float* aprev = S == 2 ? W.a1 : (S == 3 ? W.a2 : W.a3);
+#pragma unroll
+    for (int i = 0; i < KP / MW; ++i) apv[i] = aprev[(size_t)tc * KP + q + i * MW];
+  }
   if constexpr (S >= 2) map_stats<S - 1>(A, W, s_mean, s_rstd, s_tmp);
   // ---- layer inputs of this workgroup's tiles -> s_in
   if constexpr (S == 1) {
@@ -340,14 +349,12 @@ __device__ __forceinline__ void mapper_fwd_stage(const MapperTrainArgs& A, MapFw
   __syncthreads();
   if constexpr (S >= 2) {
     // h = relu(gamma (a - mean) rstd + beta) of the previous layer
-    constexpr int KP = S == 2 ? 32 : (S == 3 ? 64 : 32);
-    const float* aprev = S == 2 ? W.a1 : (S == 3 ? W.a2 : W.a3);
     const float* g = S == 2 ? P.g1 : (S == 3 ? P.g2 : P.g3);
     const float* be = S == 2 ? P.be1 : (S == 3 ? P.be2 : P.be3);
 #pragma unroll
     for (int i = 0; i < KP / MW; ++i) {
       const int k = q + i * MW;
-      const float a = aprev[(size_t)tc * KP + k];
+      const float a = apv[i];
       const float y = g[k] * ((a - s_mean[k]) * s_rstd[k]) + be[k];
       s_in[lane][k] = y > 0.0f ? y : 0.0f;
     }
@@ -473,6 +480,29 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
   const int tc = valid ? t : A.n - 1;
   float* gp = A.gpart + (size_t)wgi * MG_SIZE;
   float* bp = W.bpart_of(S) + (size_t)wgi * 128;   // BN(S-1) partials written here
+  // this lane's per-tile operands first, in flight through the BN sums:
+  // g_y(S) and a(S) of step 1, a(S-1) of steps 2 and 4
+  constexpr int N1 = S == 4 ? 1 : MapL<S == 4 ? 1 : S>::N;
+  constexpr int KI = S == 4 ? 32 : (S == 1 ? 3 : MapL<S>::K);
+  float gyp[S <= 3 ? N1 / MW : 1], asp[S <= 3 ? N1 / MW : 1];
+  float ap2[S >= 2 ? KI / MW : 1], ap4[S >= 2 ? KI / MW : 1];
+  if constexpr (S <= 3) {
+    const float* aS = S == 1 ? W.a1 : (S == 2 ? W.a2 : W.a3);
+#pragma unroll
+    for (int i = 0; i < N1 / MW; ++i) {
+      const int j = q + i * MW;
+      gyp[i] = W.gy[(size_t)tc * 64 + j];
+      asp[i] = aS[(size_t)tc * N1 + j];
+    }
+  }
+  if constexpr (S >= 2) {
+    const float* ap = S == 4 ? W.a3 : (S == 3 ? W.a2 : W.a1);
+#pragma unroll
+    for (int i = 0; i < KI / MW; ++i) {
+      ap2[i] = ap[(size_t)tc * KI + q + i * MW];
+      ap4[i] = ap[(size_t)tc * KI + q * (KI / MW) + i];
+    }
+  }
   // ---- 1. gradient of a(S) for this workgroup's tiles -> s_g
   if constexpr (S == 4) {
     if (q == 0) {
@@ -524,8 +554,8 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
 #pragma unroll
     for (int i = 0; i < N / MW; ++i) {
       const int j = q + i * MW;
-      const float gy = W.gy[(size_t)tc * 64 + j];
-      const float xh = (aS[(size_t)tc * N + j] - s_mean[j]) * s_rstd[j];
+      const float gy = gyp[i];
+      const float xh = (asp[i] - s_mean[j]) * s_rstd[j];
       s_g[lane][j] = valid ? g[j] * s_rstd[j] * (gy - s_sg[j] * inv_n - xh * (s_sgx[j] * inv_n)) : 0.0f;
     }
   }
@@ -537,7 +567,6 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
       s_h[lane][0] = valid ? c : 0.0f; s_h[lane][1] = valid ? c * c : 0.0f; s_h[lane][2] = valid ? log1pf(c) : 0.0f;
     }
   } else {
-    const float* ap = S == 4 ? W.a3 : (S == 3 ? W.a2 : W.a1);
     const float* g = S == 4 ? P.g3 : (S == 3 ? P.g2 : P.g1);
     const float* be = S == 4 ? P.be3 : (S == 3 ? P.be2 : P.be1);
     const int L = S - 1;
@@ -545,7 +574,7 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
     for (int i = 0; i < K / MW; ++i) {
       const int k = q + i * MW;
       const float mean = W.stat[(L - 1) * 128 + k], rstd = W.stat[(L - 1) * 128 + 64 + k];
-      const float y = g[k] * ((ap[(size_t)tc * K + k] - mean) * rstd) + be[k];
+      const float y = g[k] * ((ap2[i] - mean) * rstd) + be[k];
       s_h[lane][k] = valid && y > 0.0f ? y : 0.0f;
     }
   }
@@ -587,7 +616,6 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
     const int L = S - 1;
     constexpr int NQ = K / MW;
     float gyv[NQ], xhv[NQ];
-    const float* ap = S == 4 ? W.a3 : (S == 3 ? W.a2 : W.a1);
     const float* g = S == 4 ? P.g3 : (S == 3 ? P.g2 : P.g1);
     const float* be = S == 4 ? P.be3 : (S == 3 ? P.be2 : P.be1);
 #pragma unroll
@@ -597,7 +625,7 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
 #pragma unroll 16
       for (int j = 0; j < NO; ++j) acc = fmaf(w[j * K + k], s_g[lane][j], acc);
       const float mean = W.stat[(L - 1) * 128 + k], rstd = W.stat[(L - 1) * 128 + 64 + k];
-      const float xh = (ap[(size_t)tc * K + k] - mean) * rstd;
+      const float xh = (ap4[f] - mean) * rstd;
       const float y = g[k] * xh + be[k];
       const float gy = (valid && y > 0.0f) ? acc : 0.0f;
       gyv[f] = gy; xhv[f] = xh;

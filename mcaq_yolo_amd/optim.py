@@ -1,5 +1,5 @@
-"""The optimizer end of the reference's QAT step (train.py:626-641) as ONE
-kernel launch on the GPU:
+"""The optimizer end of the reference's QAT step (train.py:626-641) as two
+kernel launches on the GPU:
 
     torch.nn.utils.clip_grad_norm_(params, max_norm=1.0)   # ~9 ATen kernels
     optimizer.step()                                       # AdamW (train.py:140-150), 4 multi-tensor kernels
@@ -15,6 +15,8 @@ parameters the whole step is `mcaq_clip_adamw` (csrc/mcaq_optim.h): no host
 sync, capturable in a HIP graph.  CPU parameters run the same three steps as
 torch ops.  Values agree with torch's clip + fused AdamW within fp32
 rounding (the norms reduce in another order): tests/test_optim_gpu.py.
+The two launches: per-chunk squared-norm partials, then the norm and the
+update of every chunk (csrc/mcaq_optim.h).
 """
 import ctypes
 
@@ -118,11 +120,14 @@ class ClipAdamW(torch.optim.Optimizer):
             self._groups = (abi.AdamwGroup * len(hps))(*[abi.AdamwGroup(*hp) for hp in hps])
             self._segs, self._seg_key = segs, key
             self._norm_t = torch.empty(1, device=items[0][1].device)
+            total = sum(p.numel() for _, p in items)
+            self._work = torch.empty(abi.lib().mcaq_clip_adamw_work_floats(total), device=items[0][1].device)
         mn = self.max_norm if self.max_norm is not None else 0.0
         st = ctypes.c_void_p(torch.cuda.current_stream(items[0][1].device).cuda_stream)
         abi.check(abi.lib().mcaq_clip_adamw(self._segs, len(items), self._groups, len(self._groups),
                                             ctypes.c_void_p(self._step_t.data_ptr()), mn,
-                                            ctypes.c_void_p(self._norm_t.data_ptr()), st), "mcaq_clip_adamw")
+                                            ctypes.c_void_p(self._norm_t.data_ptr()),
+                                            ctypes.c_void_p(self._work.data_ptr()), st), "mcaq_clip_adamw")
         self.last_total_norm = self._norm_t[0] if self.max_norm is not None else None
         # the kernel updated the tensors through raw pointers: bump their
         # version counters as an in-place torch op would, so caches keyed on
