@@ -618,12 +618,22 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
     float gyv[NQ], xhv[NQ];
     const float* g = S == 4 ? P.g3 : (S == 3 ? P.g2 : P.g1);
     const float* be = S == 4 ? P.be3 : (S == 3 ? P.be2 : P.be1);
+    // rows j outer, the wave's NQ consecutive columns inner: one NQ-wide
+    // scalar load of W per row instead of NQ strided ones (each output's sum
+    // still runs over j in order)
+    float accv[NQ];
+#pragma unroll
+    for (int f = 0; f < NQ; ++f) accv[f] = 0.0f;
+#pragma unroll 8
+    for (int j = 0; j < NO; ++j) {
+      const float ga = s_g[lane][j];
+#pragma unroll
+      for (int f = 0; f < NQ; ++f) accv[f] = fmaf(w[j * K + q * NQ + f], ga, accv[f]);
+    }
 #pragma unroll
     for (int f = 0; f < NQ; ++f) {
       const int k = q * NQ + f;
-      float acc = 0.0f;
-#pragma unroll 16
-      for (int j = 0; j < NO; ++j) acc = fmaf(w[j * K + k], s_g[lane][j], acc);
+      const float acc = accv[f];
       const float mean = W.stat[(L - 1) * 128 + k], rstd = W.stat[(L - 1) * 128 + 64 + k];
       const float xh = (ap4[f] - mean) * rstd;
       const float y = g[k] * xh + be[k];
@@ -932,12 +942,21 @@ __device__ __forceinline__ void mcaq_cmlp_bwd_body(const HeadTrainArgs& A) {
   // layer 2 transpose, LN1 (wave q: inputs F1 q ..)
   float gx1[F1];
   m1 = 0.0f; m2 = 0.0f;
+  // rows j outer, the wave's F1 consecutive columns inner: one F1-wide scalar
+  // load of W2 per row instead of F1 strided ones (each sum still over j in order)
+  float accv[F1];
+#pragma unroll
+  for (int f = 0; f < F1; ++f) accv[f] = 0.0f;
+#pragma unroll 8
+  for (int j = 0; j < 32; ++j) {
+    const float ga = v[CB_GA2 + j];
+#pragma unroll
+    for (int f = 0; f < F1; ++f) accv[f] = fmaf(P.w2[j * 64 + q * F1 + f], ga, accv[f]);
+  }
 #pragma unroll
   for (int f = 0; f < F1; ++f) {
     const int k = q * F1 + f;
-    float acc = 0.0f;
-#pragma unroll 16
-    for (int j = 0; j < 32; ++j) acc = fmaf(P.w2[j * 64 + k], v[CB_GA2 + j], acc);
+    const float acc = accv[f];
     const float y = P.g1[k] * x1[f] + P.be1[k];
     const float gy = y > 0.0f ? acc : 0.0f;
     v[CB_GY1 + k] = gy; v[CB_GYX1 + k] = gy * x1[f];
@@ -1022,8 +1041,10 @@ struct MaskTrainArgs {
 
 // LDS bytes of the soft-mask backward of one (H, W, ht, wt) image; stage: + the
 // staging plane (16-byte aligned)
+constexpr int SM_PCH = 6;      // tile chunks of the parameter partials (SM_PCH x SG_SIZE <= threads)
+constexpr int SM_WS = 176;     // LDS floats of the staged soft-mask parameters
 inline size_t smask_lds_bytes(int H, int W, int ht, int wt, bool stage, bool fold = false) {
-  const size_t base = ((size_t)20 * ht * wt + 64 + (size_t)H * wt + (size_t)H * W) * sizeof(float) +
+  const size_t base = ((size_t)20 * ht * wt + 64 + 1024 + SM_WS + (size_t)H * wt + (size_t)H * W) * sizeof(float) +
                       (size_t)2 * (ht + wt) * sizeof(int);
   const size_t st = stage ? ((base / 4 + 3) & ~(size_t)3) * 4 + (size_t)H * W * sizeof(float) : base;
   // fold mode: + the grad_bits pixel plane [H][W], band-column sums [ht][W], per-tile sums [NT]
@@ -1036,6 +1057,18 @@ inline bool smask_stage_ok(const float* absmean, const float* gm, int H, int W, 
 }
 
 constexpr int SM_TH = 1024;   // threads per soft-mask backward workgroup (one image)
+
+// diagnostic build only (-DMCAQ_STAMPS): stage cycle stamps of the train
+// kernels' workgroup 0 (tools/probe/train_stamps.py), slots 32..63
+#if defined(MCAQ_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
+#define TSTAMP(k)                                                                            \
+  do {                                                                                       \
+    __syncthreads();                                                                         \
+    if (threadIdx.x == 0 && blockIdx.x == 0) g_mcaq_stamps[(k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define TSTAMP(k) do {} while (0)
+#endif
 
 // an [n] fp32 plane (16-byte aligned, n % 4 == 0 when staged) into LDS: two
 // 16-byte groups per thread per round, both loads issued before either store
@@ -1062,7 +1095,9 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
   float* rel = gpre + 8 * NT;        // per tile x 8: relu(hidden)
   float* red = rel + 8 * NT;         // 64 reduction slots
   float* gmt = red + 64;             // per tile: gradient of m(tile)
-  int* hlo = (int*)(gmt + NT);       // rows / columns of every tile's nearest-upsample block
+  float* psc = gmt + NT;             // [SM_PCH][SG_SIZE] parameter partials of tile chunks
+  float* wsm = psc + SM_TH;          // the soft-mask net's parameters (SG_SIZE floats, padded)
+  int* hlo = (int*)(wsm + SM_WS);    // rows / columns of every tile's nearest-upsample block
   int* hhi = hlo + ht;
   int* wlo = hhi + ht;
   int* whi = wlo + wt;
@@ -1079,6 +1114,12 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
   float* fgb = fcol + ht * W;         //   per tile: c + the quantizer's grad_bits
   const float* am = A.absmean + (size_t)b * H * W;
   const float* gm = fold ? nullptr : A.gm + (size_t)b * H * W;
+  TSTAMP(32);
+  // the net's parameters into LDS: W1 (8,2,3,3) | b1 (8) | W2 (2,8) | b2 (2)
+  if (tid < SG_SIZE) {
+    wsm[tid] = tid < SG_B1 ? A.P.w1[tid] : tid < SG_W2 ? A.P.b1[tid - SG_B1]
+                                     : tid < SG_B2 ? A.P.w2[tid - SG_W2] : A.P.b2[tid - SG_B2];
+  }
   if (A.stage) {
     smask_copy_plane(stg, am, H * W, tid);
     __syncthreads();
@@ -1105,19 +1146,30 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
     if (w == 0 || imin_((int)floorf((float)(w - 1) * scw), wt - 1) != j) wlo[j] = w;
     if (w == W - 1 || imin_((int)floorf((float)(w + 1) * scw), wt - 1) != j) whi[j] = w;
   }
+  TSTAMP(33);
   // ---- forward recompute: per-tile activation (adaptive_avg_pool2d), amax
   float lmx = -3.402823466e38f;
   for (int t = tid; t < NT; t += SM_TH) {
+    const float bv = A.bits[(size_t)b * NT + t];   // issued first: in flight through the pooling sums
     const int i = t / wt, j = t - i * wt;
     const int ha = (i * H) / ht, hb = ((i + 1) * H + ht - 1) / ht;
     const int wa = (j * W) / wt, wb = ((j + 1) * W + wt - 1) / wt;
+    // h-major, w ascending (adaptive_avg_pool2d's order), each row's values
+    // loaded 8 at a time before they are added (clamped index)
     float s = 0.0f;
-    for (int h = ha; h < hb; ++h)
-      for (int w = wa; w < wb; ++w) s += am[h * W + w];
+    for (int h = ha; h < hb; ++h) {
+      const float* r = am + h * W;
+      for (int w0 = wa; w0 < wb; w0 += 8) {
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = r[imin_(w0 + k, wb - 1)];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) s = w0 + k < wb ? s + v[k] : s;
+      }
+    }
     const float a = (s / (float)(hb - ha)) / (float)(wb - wa);
     f1[t] = a;
     lmx = fmax_(lmx, a);
-    const float bv = A.bits[(size_t)b * NT + t];
     f0[t] = clampf_((bv - 2.0f) / 6.0f, 0.0f, 1.0f);
   }
 #pragma unroll
@@ -1129,6 +1181,7 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
   for (int w = 1; w < SM_TH / 64; ++w) amax = fmax_(amax, red[w]);
   const float den = amax + 1e-8f;
   for (int t = tid; t < NT; t += SM_TH) f1[t] = f1[t] / den;
+  TSTAMP(34);
   if (fold) {
     // the quantizer backward's fold (qat_fold_band's values): per pixel the
     // slice partials in slice order -> grad m(p) (into the staged plane) and
@@ -1189,6 +1242,7 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
     }
     __syncthreads();
     gm = stg;
+    TSTAMP(41);
     for (int it = tid; it < ht * W; it += SM_TH) {
       const int th = it / W, w = it - th * W;
       float t = 0.0f;
@@ -1217,6 +1271,7 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
     __syncthreads();
     gm = stg;
   }
+  TSTAMP(35);
   // adjoint of the smoothing (replicate pad), vertical pass:
   // tv(q, w) = sum_d g_d sum_{p: clamp(p + d - 2) = q} g_m(p, w)
   for (int e = tid; e < H * W; e += SM_TH) {
@@ -1238,31 +1293,72 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
     tv[e] = acc;
   }
   __syncthreads();
+  TSTAMP(36);
 
-  // horizontal pass + the nearest-upsample adjoint: one item = one row of one
-  // tile column's block, summed into part[h][j]
-  for (int it = tid; it < H * wt; it += SM_TH) {
-    const int h = it / wt, j = it - h * wt;
-    const float* row = tv + h * W;
-    float acc = 0.0f;
-    for (int q = wlo[j]; q <= whi[j]; ++q) {
-      float g = 0.0f;
-      if (q >= 2 && q <= W - 3) {
+  // horizontal pass + the nearest-upsample adjoint: part[h][j] = the sum,
+  // over the columns q of tile column j in order, of the 5-tap value g(q) of
+  // row h.  Staged: g(q) of every pixel first (one item per pixel, into the
+  // staged plane, dead after the vertical pass), then the column sums;
+  // otherwise one item per (row, tile column).  The same values either way.
+  auto htap = [&](const float* row, int q) {
+    float g = 0.0f;
+    if (q >= 2 && q <= W - 3) {
 #pragma unroll
-        for (int d = 0; d < 5; ++d) g = fmaf(g1[d], row[q - d + 2], g);
-      } else {
+      for (int d = 0; d < 5; ++d) g = fmaf(g1[d], row[q - d + 2], g);
+    } else {
 #pragma unroll
-        for (int d = 0; d < 5; ++d) {
-          int p0, p1;
-          tap_range(q, d - 2, W, p0, p1);
-          float r = 0.0f;
-          for (int p = p0; p <= p1; ++p) r += row[p];
-          g = fmaf(g1[d], r, g);
-        }
+      for (int d = 0; d < 5; ++d) {
+        int p0, p1;
+        tap_range(q, d - 2, W, p0, p1);
+        float r = 0.0f;
+        for (int p = p0; p <= p1; ++p) r += row[p];
+        g = fmaf(g1[d], r, g);
       }
-      acc += g;
     }
-    part[it] = acc;
+    return g;
+  };
+  if (A.stage && W >= 8 && H * W <= (1 << 20)) {
+    float* gq = stg;
+    // interior columns 2 .. W-3 (the 5 taps, no branch), then the 4 edge
+    // columns of every row (the replicate-pad ranges) as items of their own,
+    // so no wave runs both paths
+    const int WI = W - 4;
+    const float rWI = 1.0f / (float)WI;   // floor((e + 0.5) / WI) is exact for e < 2^20
+    for (int e = tid; e < H * WI; e += SM_TH) {
+      const int h = (int)(((float)e + 0.5f) * rWI), q = 2 + e - h * WI;
+      const float* row = tv + h * W;
+      float g = 0.0f;
+#pragma unroll
+      for (int d = 0; d < 5; ++d) g = fmaf(g1[d], row[q - d + 2], g);
+      gq[h * W + q] = g;
+    }
+    for (int e = tid; e < H * 4; e += SM_TH) {
+      const int h = e >> 2, k = e & 3, q = k < 2 ? k : W - 4 + k;
+      gq[h * W + q] = htap(tv + h * W, q);
+    }
+    __syncthreads();
+    for (int it = tid; it < H * wt; it += SM_TH) {
+      const int h = it / wt, j = it - h * wt;
+      const float* r = gq + h * W;
+      const int q1 = whi[j];
+      float acc = 0.0f;
+      for (int q0 = wlo[j]; q0 <= q1; q0 += 8) {
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = r[imin_(q0 + k, q1)];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc = q0 + k <= q1 ? acc + v[k] : acc;
+      }
+      part[it] = acc;
+    }
+  } else {
+    for (int it = tid; it < H * wt; it += SM_TH) {
+      const int h = it / wt, j = it - h * wt;
+      const float* row = tv + h * W;
+      float acc = 0.0f;
+      for (int q = wlo[j]; q <= whi[j]; ++q) acc += htap(row, q);
+      part[it] = acc;
+    }
   }
   __syncthreads();
   for (int t = tid; t < NT; t += SM_TH) {
@@ -1272,38 +1368,45 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
     gmt[t] = g;
   }
   __syncthreads();
-  // ---- per tile: hidden layer, logits, m(tile), gradients of the logits
-  for (int t = tid; t < NT; t += SM_TH) {
-    const int i = t / wt, j = t - i * wt;
-    float hid[8];
+  TSTAMP(37);
+  // ---- per tile: hidden layer (one item per (tile, hidden unit)), then
+  // logits, m(tile), gradients of the logits (one item per tile)
+  const float rwt = 1.0f / (float)wt;   // tile row of t: floor((t + 0.5) / wt) is exact for t < 2^14
+  for (int u = tid; u < NT * 8; u += SM_TH) {
+    const int t = u >> 3, oc = u & 7;
+    const int i = (int)(((float)t + 0.5f) * rwt), j = t - i * wt;
+    float acc = wsm[SG_B1 + oc];
 #pragma unroll
-    for (int oc = 0; oc < 8; ++oc) {
-      float acc = A.P.b1[oc];
-#pragma unroll
-      for (int qq = 0; qq < 9; ++qq) {
-        const int ii = i + qq / 3 - 1, jj = j + qq % 3 - 1;
-        if (ii < 0 || ii >= ht || jj < 0 || jj >= wt) continue;
-        const int s = ii * wt + jj;
-        acc = fmaf(A.P.w1[(oc * 2 + 0) * 9 + qq], f0[s], acc);
-        acc = fmaf(A.P.w1[(oc * 2 + 1) * 9 + qq], f1[s], acc);
-      }
-      hid[oc] = acc;
-      rel[t * 8 + oc] = acc > 0.0f ? acc : 0.0f;
+    for (int qq = 0; qq < 9; ++qq) {
+      const int ii = i + qq / 3 - 1, jj = j + qq % 3 - 1;
+      if (ii < 0 || ii >= ht || jj < 0 || jj >= wt) continue;
+      const int s = ii * wt + jj;
+      acc = fmaf(wsm[(oc * 2 + 0) * 9 + qq], f0[s], acc);
+      acc = fmaf(wsm[(oc * 2 + 1) * 9 + qq], f1[s], acc);
     }
-    float l0 = A.P.b2[0], l1 = A.P.b2[1];
+    gpre[u] = acc;                    // the pre-activation until its gradient replaces it
+    rel[u] = acc > 0.0f ? acc : 0.0f;
+  }
+  __syncthreads();
+  for (int t = tid; t < NT; t += SM_TH) {
+    float l0 = wsm[SG_B2], l1 = wsm[SG_B2 + 1];
 #pragma unroll
-    for (int ic = 0; ic < 8; ++ic) { l0 = fmaf(A.P.w2[ic], rel[t * 8 + ic], l0); l1 = fmaf(A.P.w2[8 + ic], rel[t * 8 + ic], l1); }
+    for (int ic = 0; ic < 8; ++ic) {
+      l0 = fmaf(wsm[SG_W2 + ic], rel[t * 8 + ic], l0);
+      l1 = fmaf(wsm[SG_W2 + 8 + ic], rel[t * 8 + ic], l1);
+    }
     const float mt = 1.0f / (1.0f + expf(l1 - l0));
     // softmax (2 classes): d m / d l0 = m (1 - m) = -d m / d l1
     const float g0 = gmt[t] * (mt * (1.0f - mt));
     gl[t] = g0;
 #pragma unroll
     for (int ic = 0; ic < 8; ++ic) {
-      const float gr = A.P.w2[ic] * g0 - A.P.w2[8 + ic] * g0;
-      gpre[t * 8 + ic] = hid[ic] > 0.0f ? gr : 0.0f;
+      const float gr = wsm[SG_W2 + ic] * g0 - wsm[SG_W2 + 8 + ic] * g0;
+      gpre[t * 8 + ic] = gpre[t * 8 + ic] > 0.0f ? gr : 0.0f;
     }
   }
   __syncthreads();
+  TSTAMP(38);
   // ---- gradient of the bits feature: 3x3 transposed conv of gpre, then
   // through the clamp and the affine map
   for (int u = tid; u < NT; u += SM_TH) {
@@ -1315,7 +1418,7 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
       if (ti < 0 || ti >= ht || tj < 0 || tj >= wt) continue;
       const int t = ti * wt + tj;
 #pragma unroll
-      for (int oc = 0; oc < 8; ++oc) s = fmaf(A.P.w1[(oc * 2 + 0) * 9 + qq], gpre[t * 8 + oc], s);
+      for (int oc = 0; oc < 8; ++oc) s = fmaf(wsm[(oc * 2 + 0) * 9 + qq], gpre[t * 8 + oc], s);
     }
     const float bv = A.bits[(size_t)b * NT + u];
     const float f = (bv - 2.0f) / 6.0f;
@@ -1323,38 +1426,46 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
     float* dst = A.gbits + (size_t)b * NT + u;
     *dst = fold ? fgb[u] + gb : (A.accumulate ? *dst + gb : gb);
   }
-  // ---- parameter partials of this image: element e on wave e % 16, its
-  // tiles over the wave's lanes (tile lane + 64 k), then a fixed shuffle tree
-  // (deterministic; the elements' sums used to run serially over all tiles
-  // on 170 threads)
+  TSTAMP(39);
+  // ---- parameter partials of this image: thread (chunk c, element e) sums
+  // e's terms over the tiles of chunk c in tile order; the SM_PCH chunk sums
+  // of each element are then added in chunk order (deterministic)
+  static_assert(SM_PCH * SG_SIZE <= SM_TH, "soft-mask partial chunks exceed the workgroup");
   float* gp = A.gpart + (size_t)b * SG_SIZE;
-  const int lane = tid & 63, wv = tid >> 6;
-  const float rwt = 1.0f / (float)wt;   // tile row of t: floor((t + 0.5) / wt) is exact for t < 2^14
-  for (int e = wv; e < SG_SIZE; e += SM_TH / 64) {
+  if (tid < SM_PCH * SG_SIZE) {
+    const int c = tid / SG_SIZE, e = tid - c * SG_SIZE;
+    const int t0 = (c * NT) / SM_PCH, t1 = ((c + 1) * NT) / SM_PCH;
     float s = 0.0f;
     if (e < SG_B1) {                  // W1[oc][ic][qq]
       const int oc = e / 18, ic = (e / 9) & 1, qq = e % 9;
       const int di = qq / 3 - 1, dj = qq % 3 - 1;
       const float* f = ic == 0 ? f0 : f1;
-      for (int t = lane; t < NT; t += 64) {
-        const int i = (int)(((float)t + 0.5f) * rwt), j = t - i * wt;
+      int i = (int)(((float)t0 + 0.5f) * rwt), j = t0 - i * wt;   // walked forward with t
+      for (int t = t0; t < t1; ++t) {
         const int ii = i + di, jj = j + dj;
         if (ii >= 0 && ii < ht && jj >= 0 && jj < wt) s = fmaf(gpre[t * 8 + oc], f[ii * wt + jj], s);
+        if (++j == wt) { j = 0; ++i; }
       }
     } else if (e < SG_W2) {           // b1
       const int oc = e - SG_B1;
-      for (int t = lane; t < NT; t += 64) s += gpre[t * 8 + oc];
+      for (int t = t0; t < t1; ++t) s += gpre[t * 8 + oc];
     } else if (e < SG_B2) {           // W2[o][ic]: g_l(o) relu_ic, g_l1 = -g_l0
       const int o = (e - SG_W2) >> 3, ic = (e - SG_W2) & 7;
-      for (int t = lane; t < NT; t += 64) s = fmaf(o == 0 ? gl[t] : -gl[t], rel[t * 8 + ic], s);
+      for (int t = t0; t < t1; ++t) s = fmaf(o == 0 ? gl[t] : -gl[t], rel[t * 8 + ic], s);
     } else {                          // b2
       const int o = e - SG_B2;
-      for (int t = lane; t < NT; t += 64) s += o == 0 ? gl[t] : -gl[t];
+      for (int t = t0; t < t1; ++t) s += o == 0 ? gl[t] : -gl[t];
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-    if (lane == 0) gp[e] = s;
+    psc[tid] = s;
   }
+  __syncthreads();
+  if (tid < SG_SIZE) {
+    float s = psc[tid];
+#pragma unroll
+    for (int c = 1; c < SM_PCH; ++c) s += psc[c * SG_SIZE + tid];
+    gp[tid] = s;
+  }
+  TSTAMP(40);
 }
 __global__ __launch_bounds__(SM_TH) void mcaq_smask_bwd_kernel(MaskTrainArgs A) { mcaq_smask_bwd_body(A); }
 

@@ -1,0 +1,48 @@
+"""Diagnostic: stage cycles of the train-step kernels' workgroup 0 (the
+soft-mask backward of scale 0's image 0, slots 32..41) from a -DMCAQ_STAMPS
+build (python tools/build.py --stamps -> lib/libmcaq_hip_stamps.so), one QAT
+step at config 5 (bench.py --config 5 shapes)."""
+import ctypes
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+from mcaq_yolo_amd import abi  # noqa: E402
+
+abi._LIB = abi.load_library(os.path.join(ROOT, "mcaq_yolo_amd", "lib", "libmcaq_hip_stamps.so"))
+L = abi._LIB
+L.mcaq_read_stamps.argtypes = [ctypes.c_void_p]
+from test_train_fused_gpu import _hooks  # noqa: E402
+
+STAGES = [(32, 33, "stage |x| plane + ranges"), (33, 34, "pool |x| per tile + amax"), (34, 41, "fold: slice loads"),
+          (41, 35, "fold: band / tile sums"), (35, 36, "smoothing adjoint, vertical"),
+          (36, 37, "horizontal + upsample adjoint"), (37, 38, "per-tile net + logit grads"),
+          (38, 39, "bits-feature grad (3x3^T)"), (39, 40, "parameter partials")]
+
+
+def main():
+    dev = torch.device("cuda:0")
+    h = _hooks()
+    gen = torch.Generator(device="cpu").manual_seed(5)
+    feats = [torch.randn(16, c, s, s, generator=gen).to(dev).requires_grad_(True)
+             for c, s in ((64, 80), (128, 40), (256, 20))]
+    for _ in range(3):
+        outs, aux = h.forward_features(feats)
+        loss = sum(o.sum() for o in outs) * 1e-3 + h.bit_budget_loss(aux, 4.0)
+        loss.backward()
+        torch.cuda.synchronize()
+    buf = (ctypes.c_ulonglong * 64)()
+    L.mcaq_read_stamps(ctypes.cast(buf, ctypes.c_void_p))
+    st = list(buf)
+    print("soft-mask backward, scale 0 image 0 (80x80, 10x10 tiles): %d s_memtime ticks total"
+          % (st[40] - st[32]))
+    for a, b, name in STAGES:
+        print("   %-34s %8d" % (name, st[b] - st[a]))
+
+
+if __name__ == "__main__":
+    main()
