@@ -23,6 +23,30 @@
 
 namespace mcaq {
 
+// v_mfma_f32_16x16x4_f32 (D = a k-ordered fp32 FMA chain over its 4 k; lane
+// l: A[l & 15][l >> 4], B[l >> 4][l & 15], D rows 4 (l >> 4) + r, column l & 15)
+typedef float tr_f4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ tr_f4 tr_mfma4(float a, float b, tr_f4 c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+#else
+  return c;
+#endif
+}
+
+// diagnostic build only (-DMCAQ_STAMPS): stage cycle stamps of the train
+// kernels' workgroup 0 (tools/probe/train_stamps.py), slots 32..63
+#if defined(MCAQ_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
+#define TSTAMP(k)                                                                            \
+  do {                                                                                       \
+    __syncthreads();                                                                         \
+    if (threadIdx.x == 0 && blockIdx.x == 0) g_mcaq_stamps[(k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define TSTAMP(k) do {} while (0)
+#endif
+
+
 // ---- shared helpers --------------------------------------------------------
 constexpr int TR_TPB = 64;          // tiles per workgroup (one per lane of a wave)
 
@@ -135,7 +159,12 @@ constexpr int RANK_ENT = 129;   // (mean[64], M2[64], n) of one rank
 
 // work layout (floats)
 struct MapperWork {
-  float *a1, *a2, *a3, *o, *gy;   // pre-BN activations (n x 32 / 64 / 32), sigmoid out, gradient scratch (n x 64)
+  // pre-BN activations (32 / 64 / 32 x n), sigmoid out, gradient scratch
+  // (64 x n): feature-major, so a wave's 64 tiles (lanes) of one feature are
+  // 256 contiguous bytes - coalesced loads and stores (tile-major rows made
+  // every access 64 separate lines: the forward layer's stores and the
+  // backward's g_y stores took ~6 us of a stage)
+  float *a1, *a2, *a3, *o, *gy;
   float *part, *cnt;              // per-workgroup (mean[64], M2[64]) and counts
   float *stat;                    // 3 layers x (mean[64], rstd[64])
   float *bpart;                   // backward BN partials [2][nwg][2 x 64]
@@ -313,6 +342,7 @@ struct MapFwdLds {
   float in[TR_TPB][65];     // this workgroup's tiles' layer inputs
   float mean[64], rstd[64];
   float tmp[MW * 192];
+  float w[64 * 32];         // stages 2 / 3: the layer's weights (read as broadcast LDS vectors)
 };
 
 template <int S>
@@ -329,6 +359,19 @@ __device__ __forceinline__ void mapper_fwd_stage(const MapperTrainArgs& A, MapFw
   const bool valid = t < A.n;
   const int tc = valid ? t : A.n - 1;
   const float nvalid = (float)imin_(TR_TPB, A.n - wgi * TR_TPB);
+  if constexpr (S == 2) TSTAMP(50);
+  // stages 2 / 3: the layer's weights (K x N = 2048 floats, 4 a thread,
+  // coalesced) first, into LDS below - the FMA loop then reads broadcast LDS
+  // vectors instead of waiting on ~32 dependent scalar-load batches
+  constexpr bool kWL = S == 2 || S == 3;
+  constexpr int WN = kWL ? MapL<S>::K * MapL<S>::N : MTH;
+  static_assert(WN % MTH == 0 && WN <= 64 * 32, "mapper weight staging");
+  float wst[WN / MTH];
+  if constexpr (kWL) {
+    const float* wsrc = S == 2 ? P.w2 : P.w3;
+#pragma unroll
+    for (int i = 0; i < WN / MTH; ++i) wst[i] = wsrc[tid + i * MTH];
+  }
   // this lane's previous-layer activations first: in flight through the
   // batch statistics below
   constexpr int KP = S == 2 ? 32 : (S == 3 ? 64 : 32);
@@ -336,9 +379,11 @@ __device__ __forceinline__ void mapper_fwd_stage(const MapperTrainArgs& A, MapFw
   if constexpr (S >= 2) {
     const float* aprev = S == 2 ? W.a1 : (S == 3 ? W.a2 : W.a3);
 #pragma unroll
-    for (int i = 0; i < KP / MW; ++i) apv[i] = aprev[(size_t)tc * KP + q + i * MW];
+    for (int i = 0; i < KP / MW; ++i) apv[i] = aprev[(size_t)(q + i * MW) * A.n + tc];
   }
   if constexpr (S >= 2) map_stats<S - 1>(A, W, s_mean, s_rstd, s_tmp);
+  if constexpr (S == 2) TSTAMP(51);
+  if constexpr (S == 2) TSTAMP(52);
   // ---- layer inputs of this workgroup's tiles -> s_in
   if constexpr (S == 1) {
     if (q == 0) {
@@ -358,11 +403,16 @@ __device__ __forceinline__ void mapper_fwd_stage(const MapperTrainArgs& A, MapFw
       const float y = g[k] * ((a - s_mean[k]) * s_rstd[k]) + be[k];
       s_in[lane][k] = y > 0.0f ? y : 0.0f;
     }
+    if constexpr (kWL) {
+#pragma unroll
+      for (int i = 0; i < WN / MTH; ++i) L.w[tid + i * MTH] = wst[i];
+    }
     __syncthreads();
   }
+  if constexpr (S == 2) TSTAMP(53);
   if constexpr (S <= 3) {
     constexpr int K = MapL<S>::K, N = MapL<S>::N, NQ = N / MW;
-    const float* w = S == 1 ? P.w1 : (S == 2 ? P.w2 : P.w3);
+    const float* w = S == 1 ? P.w1 : L.w;
     const float* bb = S == 1 ? P.b1 : (S == 2 ? P.b2 : P.b3);
     float* aout = S == 1 ? W.a1 : (S == 2 ? W.a2 : W.a3);
     float x[K];
@@ -376,10 +426,12 @@ __device__ __forceinline__ void mapper_fwd_stage(const MapperTrainArgs& A, MapFw
 #pragma unroll
       for (int k = 0; k < K; ++k) acc = fmaf(w[j * K + k], x[k], acc);
       o[f] = acc;
-      if (valid) aout[(size_t)t * N + j] = acc;
+      if (valid) aout[(size_t)j * A.n + t] = acc;
     }
+    if constexpr (S == 2) TSTAMP(54);
     wg_moments<NQ>(o, valid, nvalid, q * NQ, W.fpart(S) + (size_t)wgi * 128, N);
     if (tid == 0) W.cnt[wgi] = nvalid;
+    if constexpr (S == 2) TSTAMP(55);
   } else {
     // last layer + sigmoid + bit range, temperature, clamp (+ round)
     if (q == 0 && valid) {
@@ -460,6 +512,7 @@ struct MapBwdLds {
   float g[TR_TPB][65];     // gradient of this layer's pre-activation a(S)
   float mean[64], rstd[64], sg[64], sgx[64];
   float tmp[MW * 128];
+  float w[64 * 32];        // stages 3 / 2: the layer's weights for W^T g_a
 };
 
 template <int S>
@@ -480,6 +533,18 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
   const int tc = valid ? t : A.n - 1;
   float* gp = A.gpart + (size_t)wgi * MG_SIZE;
   float* bp = W.bpart_of(S) + (size_t)wgi * 128;   // BN(S-1) partials written here
+  if constexpr (S == 3) TSTAMP(56);
+  // stages 3 / 2: the layer's weights first (into LDS before the first
+  // barrier; W^T g_a reads them as broadcast LDS vectors)
+  constexpr bool kWL = S == 2 || S == 3;
+  constexpr int WN = kWL ? MapL<S>::K * MapL<S>::N : MTH;
+  static_assert(WN % MTH == 0 && WN <= 64 * 32, "mapper weight staging");
+  float wst[WN / MTH];
+  if constexpr (kWL) {
+    const float* wsrc = S == 2 ? P.w2 : P.w3;
+#pragma unroll
+    for (int i = 0; i < WN / MTH; ++i) wst[i] = wsrc[tid + i * MTH];
+  }
   // this lane's per-tile operands first, in flight through the BN sums:
   // g_y(S) and a(S) of step 1, a(S-1) of steps 2 and 4
   constexpr int N1 = S == 4 ? 1 : MapL<S == 4 ? 1 : S>::N;
@@ -491,18 +556,19 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
 #pragma unroll
     for (int i = 0; i < N1 / MW; ++i) {
       const int j = q + i * MW;
-      gyp[i] = W.gy[(size_t)tc * 64 + j];
-      asp[i] = aS[(size_t)tc * N1 + j];
+      gyp[i] = W.gy[(size_t)j * A.n + tc];
+      asp[i] = aS[(size_t)j * A.n + tc];
     }
   }
   if constexpr (S >= 2) {
     const float* ap = S == 4 ? W.a3 : (S == 3 ? W.a2 : W.a1);
 #pragma unroll
     for (int i = 0; i < KI / MW; ++i) {
-      ap2[i] = ap[(size_t)tc * KI + q + i * MW];
-      ap4[i] = ap[(size_t)tc * KI + q * (KI / MW) + i];
+      ap2[i] = ap[(size_t)(q + i * MW) * A.n + tc];
+      ap4[i] = ap[(size_t)(q * (KI / MW) + i) * A.n + tc];
     }
   }
+  if constexpr (S == 3) TSTAMP(42);
   // ---- 1. gradient of a(S) for this workgroup's tiles -> s_g
   if constexpr (S == 4) {
     if (q == 0) {
@@ -526,6 +592,10 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
         for (int w = part; w < A.nwg; w += MW) { s1 += bq[(size_t)w * 128 + j]; s2 += bq[(size_t)w * 128 + 64 + j]; }
         s_tmp[part * 128 + j] = s1; s_tmp[part * 128 + 64 + j] = s2;
       }
+    }
+    if constexpr (kWL) {
+#pragma unroll
+      for (int i = 0; i < WN / MTH; ++i) L.w[tid + i * MTH] = wst[i];
     }
     __syncthreads();
     if (tid < N) {
@@ -559,6 +629,7 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
       s_g[lane][j] = valid ? g[j] * s_rstd[j] * (gy - s_sg[j] * inv_n - xh * (s_sgx[j] * inv_n)) : 0.0f;
     }
   }
+  if constexpr (S == 3) TSTAMP(43);
   // ---- 2. this layer's input activations h(S-1) -> s_h
   constexpr int K = S == 4 ? 32 : (S == 1 ? 3 : MapL<S>::K);
   if constexpr (S == 1) {
@@ -579,48 +650,55 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
     }
   }
   __syncthreads();
+  if constexpr (S == 3) TSTAMP(44);
   // ---- 3. weight / bias partials of layer S: sum over the tiles of g_a (x) h
   {
     constexpr int NO = S == 4 ? 1 : MapL<S>::N;
     const int ow = S == 4 ? MG_W4 : (S == 3 ? MG_W3 : (S == 2 ? MG_W2 : MG_W1));
     const int ob = S == 4 ? MG_B4 : (S == 3 ? MG_B3 : (S == 2 ? MG_B2 : MG_B1));
     if constexpr (NO * K == 4 * MTH) {
-      // one row x 4 columns per thread: 5 LDS reads per 4 FMAs
-      const int j0 = tid / (K / 4), k0 = (tid % (K / 4)) * 4;
-      float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-      for (int u = 0; u < TR_TPB; ++u) {
-        const float g0 = s_g[u][j0];
+      // the NO x K sums over the 64 tiles as one 16 x 16 block per wave on
+      // v_mfma_f32_16x16x4_f32: a tile-ordered fp32 FMA chain u = 0..63 (the
+      // values of the scalar loop), 2 LDS reads per 4 tiles instead of 5 per tile
+      constexpr int TB = K / 16;              // column blocks; (NO / 16) x TB = MW blocks
+      static_assert((NO / 16) * TB == MW, "one 16 x 16 block per wave");
+      const int jb = q / TB, kb = q - (q / TB) * TB;
+      const int lr = lane & 15, lk = lane >> 4;
+      tr_f4 d = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-        for (int c = 0; c < 4; ++c) acc[c] = fmaf(g0, s_h[u][k0 + c], acc[c]);
-      }
+      for (int st = 0; st < TR_TPB / 4; ++st)
+        d = tr_mfma4(s_g[4 * st + lk][jb * 16 + lr], s_h[4 * st + lk][kb * 16 + lr], d);
 #pragma unroll
-      for (int c = 0; c < 4; ++c) gp[ow + j0 * K + k0 + c] = acc[c];
+      for (int r = 0; r < 4; ++r) gp[ow + (jb * 16 + 4 * lk + r) * K + kb * 16 + lr] = d[r];
     } else {
       for (int e = tid; e < NO * K; e += MTH) {
         const int j = e / K, k = e - (e / K) * K;
         float s = 0.0f;
+#pragma unroll 8
         for (int u = 0; u < TR_TPB; ++u) s = fmaf(s_g[u][j], s_h[u][k], s);
         gp[ow + e] = s;
       }
     }
     for (int j = tid; j < NO; j += MTH) {
       float s = 0.0f;
+#pragma unroll 8
       for (int u = 0; u < TR_TPB; ++u) s += s_g[u][j];
       gp[ob + j] = s;
     }
   }
+  if constexpr (S == 3) TSTAMP(45);
   // ---- 4. gradient of the layer input: g_h = W^T g_a, through ReLU / BN(S-1)
   if constexpr (S >= 2) {
     constexpr int NO = S == 4 ? 1 : MapL<S>::N;
-    const float* w = S == 4 ? P.w4 : (S == 3 ? P.w3 : P.w2);
-    const int L = S - 1;
+    const float* w = S == 4 ? P.w4 : L.w;
+    const int Lp = S - 1;
     constexpr int NQ = K / MW;
     float gyv[NQ], xhv[NQ];
     const float* g = S == 4 ? P.g3 : (S == 3 ? P.g2 : P.g1);
     const float* be = S == 4 ? P.be3 : (S == 3 ? P.be2 : P.be1);
     // rows j outer, the wave's NQ consecutive columns inner: one NQ-wide
-    // scalar load of W per row instead of NQ strided ones (each output's sum
-    // still runs over j in order)
+    // broadcast read of W (LDS, or scalar for the 32-float W4) per row
+    // instead of NQ strided ones (each output's sum still runs over j in order)
     float accv[NQ];
 #pragma unroll
     for (int f = 0; f < NQ; ++f) accv[f] = 0.0f;
@@ -634,14 +712,15 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
     for (int f = 0; f < NQ; ++f) {
       const int k = q * NQ + f;
       const float acc = accv[f];
-      const float mean = W.stat[(L - 1) * 128 + k], rstd = W.stat[(L - 1) * 128 + 64 + k];
+      const float mean = W.stat[(Lp - 1) * 128 + k], rstd = W.stat[(Lp - 1) * 128 + 64 + k];
       const float xh = (ap4[f] - mean) * rstd;
       const float y = g[k] * xh + be[k];
       const float gy = (valid && y > 0.0f) ? acc : 0.0f;
       gyv[f] = gy; xhv[f] = xh;
-      if (valid) W.gy[(size_t)t * 64 + k] = gy;
+      if (valid) W.gy[(size_t)k * A.n + t] = gy;
     }
     __syncthreads();   // every lane has read its W.gy row of this launch's input (S < 4) before it is overwritten
+    if constexpr (S == 3) TSTAMP(46);
     // BN(S-1) partial sums: sum g_y, sum g_y xhat
 #pragma unroll
     for (int f = 0; f < NQ; ++f) {
@@ -662,6 +741,7 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
       A.gc[t] = (craw >= 0.0f && craw <= 1.0f) ? gcv : 0.0f;
     }
   }
+  if constexpr (S == 3) TSTAMP(47);
 }
 
 // sharded mapper: this rank's share of a batch statistic, in workgroup order.
@@ -972,16 +1052,18 @@ __device__ __forceinline__ void mcaq_cmlp_bwd_body(const HeadTrainArgs& A) {
   float* gp = A.gpart + (size_t)wgi * CG_SIZE;
   auto tvec = [&](int u) { return sv + u * CB_ST; };
   {
-    const int j0 = tid >> 4, k0 = (tid & 15) * 4;
-    float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-    for (int u = 0; u < TR_TPB; ++u) {
-      const float* w = tvec(u);
-      const float g0 = w[CB_GA2 + j0];
+    // one 16 x 16 block of W2 per wave on v_mfma_f32_16x16x4_f32: a
+    // tile-ordered fp32 FMA chain u = 0..63 (the scalar loop's values)
+    static_assert(NW == 8, "2 x 4 blocks of 16 x 16");
+    const int jb = q >> 2, kb = q & 3, lr = lane & 15, lk = lane >> 4;
+    tr_f4 d = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-      for (int c = 0; c < 4; ++c) acc[c] = fmaf(g0, w[CB_R1 + k0 + c], acc[c]);
+    for (int st = 0; st < TR_TPB / 4; ++st) {
+      const float* w = tvec(4 * st + lk);
+      d = tr_mfma4(w[CB_GA2 + jb * 16 + lr], w[CB_R1 + kb * 16 + lr], d);
     }
 #pragma unroll
-    for (int c = 0; c < 4; ++c) gp[CG_W2 + j0 * 64 + k0 + c] = acc[c];
+    for (int r = 0; r < 4; ++r) gp[CG_W2 + (jb * 16 + 4 * lk + r) * 64 + kb * 16 + lr] = d[r];
   }
   // the rest: W1 (64 x 8) 512, b1 / LN1 64 + 64 + 64, b2 / LN2 32 + 32 + 32, W3 32, b3 1
   for (int e = tid; e < CG_SIZE; e += NTH) {
@@ -1058,17 +1140,6 @@ inline bool smask_stage_ok(const float* absmean, const float* gm, int H, int W, 
 
 constexpr int SM_TH = 1024;   // threads per soft-mask backward workgroup (one image)
 
-// diagnostic build only (-DMCAQ_STAMPS): stage cycle stamps of the train
-// kernels' workgroup 0 (tools/probe/train_stamps.py), slots 32..63
-#if defined(MCAQ_STAMPS) && defined(__HIP_DEVICE_COMPILE__)
-#define TSTAMP(k)                                                                            \
-  do {                                                                                       \
-    __syncthreads();                                                                         \
-    if (threadIdx.x == 0 && blockIdx.x == 0) g_mcaq_stamps[(k)] = __builtin_amdgcn_s_memtime(); \
-  } while (0)
-#else
-#define TSTAMP(k) do {} while (0)
-#endif
 
 // an [n] fp32 plane (16-byte aligned, n % 4 == 0 when staged) into LDS: two
 // 16-byte groups per thread per round, both loads issued before either store

@@ -1,5 +1,6 @@
 """Diagnostic: stage cycles of the train-step kernels' workgroup 0 (the
-soft-mask backward of scale 0's image 0, slots 32..41) from a -DMCAQ_STAMPS
+soft-mask backward of scale 0's image 0, slots 32..41; the mapper's backward
+stage 3 and forward stage 2, slots 42..56) from a -DMCAQ_STAMPS
 build (python tools/build.py --stamps -> lib/libmcaq_hip_stamps.so), one QAT
 step at config 5 (bench.py --config 5 shapes)."""
 import ctypes
@@ -24,6 +25,13 @@ STAGES = [(32, 33, "stage |x| plane + ranges"), (33, 34, "pool |x| per tile + am
           (38, 39, "bits-feature grad (3x3^T)"), (39, 40, "parameter partials")]
 
 
+MAPPER_BWD = [(56, 42, "operand loads issued + BN sums"), (42, 43, "g_a(S) (BN backward)"),
+              (43, 44, "h(S-1) recompute"), (44, 45, "weight / bias partials"), (45, 46, "W^T g_a, g_y stores"),
+              (46, 47, "BN(S-1) partial sums")]
+MAPPER_FWD = [(50, 51, "batch statistics (map_stats)"), (52, 53, "h(S-1) into LDS"), (53, 54, "layer (FMA)"),
+              (54, 55, "workgroup moments")]
+
+
 def main():
     dev = torch.device("cuda:0")
     h = _hooks()
@@ -41,6 +49,12 @@ def main():
     print("soft-mask backward, scale 0 image 0 (80x80, 10x10 tiles): %d s_memtime ticks total"
           % (st[40] - st[32]))
     for a, b, name in STAGES:
+        print("   %-34s %8d" % (name, st[b] - st[a]))
+    print("mapper backward stage 3, workgroup 0 (64 tiles of scale 0): %d ticks" % (st[47] - st[56]))
+    for a, b, name in MAPPER_BWD:
+        print("   %-34s %8d" % (name, st[b] - st[a]))
+    print("mapper forward stage 2, workgroup 0: %d ticks" % (st[55] - st[50]))
+    for a, b, name in MAPPER_FWD:
         print("   %-34s %8d" % (name, st[b] - st[a]))
 
 
