@@ -247,17 +247,33 @@ struct MapperRunningArgs {
   float momentum;
 };
 __device__ __forceinline__ void mapper_running_body(const MapperRunningArgs& A) {
+  // per layer: the running buffers and every forward's statistics loaded
+  // once, the count updates applied in list order in registers (the values
+  // of map_running_update applied one after another), stored once
   const int j = threadIdx.x;
-  for (int k = 0; k < A.count; ++k) {
 #pragma unroll
-    for (int L = 1; L <= 3; ++L) {
-      const int N = L == 2 ? 64 : 32;
-      if (j < N) {
-        const float* g; const float* be; float* rm; float* rv; long long* nbt;
-        map_bn(A.P, L, g, be, rm, rv, nbt);
-        map_running_update(rm, rv, nbt, j, A.momentum, A.rstat[k][(L - 1) * 128 + j],
-                           A.rstat[k][(L - 1) * 128 + 64 + j]);
+  for (int L = 1; L <= 3; ++L) {
+    const int N = L == 2 ? 64 : 32;
+    if (j < N) {
+      const float* g; const float* be; float* rm; float* rv; long long* nbt;
+      map_bn(A.P, L, g, be, rm, rv, nbt);
+      float mk[MAPPER_RU_MAX], uk[MAPPER_RU_MAX];
+#pragma unroll
+      for (int k = 0; k < MAPPER_RU_MAX; ++k) {
+        const float* r = A.rstat[k < A.count ? k : 0];
+        mk[k] = r[(L - 1) * 128 + j];
+        uk[k] = r[(L - 1) * 128 + 64 + j];
       }
+      float m = rm[j], v = rv[j];
+#pragma unroll
+      for (int k = 0; k < MAPPER_RU_MAX; ++k) {
+        if (k >= A.count) break;
+        m = (1.0f - A.momentum) * m + A.momentum * mk[k];
+        v = (1.0f - A.momentum) * v + A.momentum * uk[k];
+      }
+      rm[j] = m;
+      rv[j] = v;
+      if (j == 0 && nbt) nbt[0] += A.count;
     }
   }
 }
@@ -418,11 +434,16 @@ __device__ __forceinline__ void mapper_fwd_stage(const MapperTrainArgs& A, MapFw
     float x[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) x[k] = s_in[lane][k];
+    // the wave's biases first: inside the loop each load would wait behind
+    // the previous output's store (the compiler cannot tell bb from aout)
+    float bq[NQ];
+#pragma unroll
+    for (int f = 0; f < NQ; ++f) bq[f] = bb[q * NQ + f];
     float o[NQ];
 #pragma unroll
     for (int f = 0; f < NQ; ++f) {
       const int j = q * NQ + f;
-      float acc = bb[j];
+      float acc = bq[f];
 #pragma unroll
       for (int k = 0; k < K; ++k) acc = fmaf(w[j * K + k], x[k], acc);
       o[f] = acc;
@@ -699,6 +720,16 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
     // rows j outer, the wave's NQ consecutive columns inner: one NQ-wide
     // broadcast read of W (LDS, or scalar for the 32-float W4) per row
     // instead of NQ strided ones (each output's sum still runs over j in order)
+    // the BN(S-1) statistics and affine parameters of the wave's columns
+    // first: in the store loop below each load would wait behind the
+    // previous column's g_y store (W.stat and W.gy share the work buffer)
+    float smn[NQ], srs[NQ], sgm[NQ], sbe[NQ];
+#pragma unroll
+    for (int f = 0; f < NQ; ++f) {
+      const int k = q * NQ + f;
+      smn[f] = W.stat[(Lp - 1) * 128 + k]; srs[f] = W.stat[(Lp - 1) * 128 + 64 + k];
+      sgm[f] = g[k]; sbe[f] = be[k];
+    }
     float accv[NQ];
 #pragma unroll
     for (int f = 0; f < NQ; ++f) accv[f] = 0.0f;
@@ -712,9 +743,8 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
     for (int f = 0; f < NQ; ++f) {
       const int k = q * NQ + f;
       const float acc = accv[f];
-      const float mean = W.stat[(Lp - 1) * 128 + k], rstd = W.stat[(Lp - 1) * 128 + 64 + k];
-      const float xh = (ap4[f] - mean) * rstd;
-      const float y = g[k] * xh + be[k];
+      const float xh = (ap4[f] - smn[f]) * srs[f];
+      const float y = sgm[f] * xh + sbe[f];
       const float gy = (valid && y > 0.0f) ? acc : 0.0f;
       gyv[f] = gy; xhv[f] = xh;
       if (valid) W.gy[(size_t)k * A.n + t] = gy;
@@ -845,7 +875,9 @@ __device__ __forceinline__ void tap_range(int u, int o, int n, int& lo, int& hi)
   hi = imin_(hi, n - 1);
 }
 
+constexpr int BL_TH = 1024;   // threads per bilateral-backward workgroup (one image)
 __device__ __forceinline__ void mcaq_bilateral_bwd_body(const HeadTrainArgs& A) {
+  TSTAMP(57);
   extern __shared__ float smem_tr[];
   const int b = (int)blockIdx.x - A.wg0, ht = A.ht, wt = A.wt, NT = ht * wt;
   const int tid = threadIdx.x;
@@ -855,9 +887,9 @@ __device__ __forceinline__ void mcaq_bilateral_bwd_body(const HeadTrainArgs& A) 
   float* wk = gcen + NT;          // [NT][25] range x spatial weights
   float* cf = wk + 25 * NT;       // [NT][25] gd_t * dC_t / dp_k
   const float* crg = A.craw + (size_t)b * NT;
-  for (int t = tid; t < NT; t += 256) cr[t] = crg[t];
+  for (int t = tid; t < NT; t += BL_TH) cr[t] = crg[t];
   __syncthreads();
-  for (int e = tid; e < NT * 25; e += 256) {
+  for (int e = tid; e < NT * 25; e += BL_TH) {
     const int t = e / 25, k = e - t * 25;
     const int th = t / wt, tw = t - th * wt;
     const int hh = imin_(imax_(th + k / 5 - 2, 0), ht - 1), ww = imin_(imax_(tw + k % 5 - 2, 0), wt - 1);
@@ -865,8 +897,9 @@ __device__ __forceinline__ void mcaq_bilateral_bwd_body(const HeadTrainArgs& A) 
     wk[e] = bits_as_float(k_bilat_sp_bits[k]) * expf(-(d * d) / 0.02f);
   }
   __syncthreads();
+  TSTAMP(58);
   // per tile: forward C, g / D, the centre term
-  for (int t = tid; t < NT; t += 256) {
+  for (int t = tid; t < NT; t += BL_TH) {
     const int th = t / wt, tw = t - th * wt;
     const float c = cr[t];
     float num = 0.0f, den = 0.0f, sc = 0.0f;
@@ -892,8 +925,9 @@ __device__ __forceinline__ void mcaq_bilateral_bwd_body(const HeadTrainArgs& A) 
     gcen[t] = gdt * sc;
   }
   __syncthreads();
+  TSTAMP(59);
   // adjoint gather: g_craw[u] = gcen[u] + sum over (k, t) with clamp(t + o_k) = u of cf[t][k]
-  for (int u = tid; u < NT; u += 256) {
+  for (int u = tid; u < NT; u += BL_TH) {
     const int uh = u / wt, uw = u - uh * wt;
     float s = gcen[u];
     for (int k = 0; k < 25; ++k) {
@@ -905,8 +939,9 @@ __device__ __forceinline__ void mcaq_bilateral_bwd_body(const HeadTrainArgs& A) 
     }
     A.gcraw[(size_t)b * NT + u] = s;
   }
+  TSTAMP(60);
 }
-__global__ __launch_bounds__(256) void mcaq_bilateral_bwd_kernel(HeadTrainArgs A) { mcaq_bilateral_bwd_body(A); }
+__global__ __launch_bounds__(BL_TH) void mcaq_bilateral_bwd_kernel(HeadTrainArgs A) { mcaq_bilateral_bwd_body(A); }
 
 // complexity MLP backward (Linear(8,64)-LN-ReLU-Linear(64,32)-LN-ReLU-
 // Linear(32,1)-sigmoid, recomputed): 64 tiles per workgroup, one per lane;
@@ -940,6 +975,7 @@ __device__ __forceinline__ void mcaq_cmlp_bwd_body(const HeadTrainArgs& A) {
     __syncthreads();
     return r;
   };
+  TSTAMP(16);
   float ph[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) ph[k] = A.phi[(size_t)tc * 8 + k];
@@ -972,6 +1008,7 @@ __device__ __forceinline__ void mcaq_cmlp_bwd_body(const HeadTrainArgs& A) {
     v[CB_R1 + j] = y > 0.0f ? y : 0.0f;
   }
   __syncthreads();
+  TSTAMP(17);
   // layer 2 (wave q: outputs F2 q ..)
   float x2[F2];
   s = 0.0f;
@@ -1001,6 +1038,7 @@ __device__ __forceinline__ void mcaq_cmlp_bwd_body(const HeadTrainArgs& A) {
   }
   const float a3 = xsum(a3p) + P.b3[0];
   const float cv = tr_sigmoid(a3);
+  TSTAMP(18);
   // ---- backward: sigmoid, layer 3, LN2
   const float g3 = valid ? A.gcraw[t] * (cv * (1.0f - cv)) : 0.0f;
   if (q == 0) v[CB_GA3] = g3;
@@ -1019,6 +1057,7 @@ __device__ __forceinline__ void mcaq_cmlp_bwd_body(const HeadTrainArgs& A) {
 #pragma unroll
   for (int f = 0; f < F2; ++f) v[CB_GA2 + q * F2 + f] = rs2 * (gx2[f] - m1 - x2[f] * m2);
   __syncthreads();
+  TSTAMP(19);
   // layer 2 transpose, LN1 (wave q: inputs F1 q ..)
   float gx1[F1];
   m1 = 0.0f; m2 = 0.0f;
@@ -1047,6 +1086,7 @@ __device__ __forceinline__ void mcaq_cmlp_bwd_body(const HeadTrainArgs& A) {
 #pragma unroll
   for (int f = 0; f < F1; ++f) v[CB_GA1 + q * F1 + f] = rs1 * (gx1[f] - m1 - x1[f] * m2);
   __syncthreads();
+  TSTAMP(20);
   // ---- weight partials over the workgroup's tiles (invalid lanes carry zero
   // gradients).  W2 (32 x 64): thread = one row x 4 columns.
   float* gp = A.gpart + (size_t)wgi * CG_SIZE;
@@ -1065,6 +1105,7 @@ __device__ __forceinline__ void mcaq_cmlp_bwd_body(const HeadTrainArgs& A) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) gp[CG_W2 + (jb * 16 + 4 * lk + r) * 64 + kb * 16 + lr] = d[r];
   }
+  TSTAMP(21);
   // the rest: W1 (64 x 8) 512, b1 / LN1 64 + 64 + 64, b2 / LN2 32 + 32 + 32, W3 32, b3 1
   for (int e = tid; e < CG_SIZE; e += NTH) {
     if (e >= CG_W2 && e < CG_B2) continue;
@@ -1091,6 +1132,7 @@ __device__ __forceinline__ void mcaq_cmlp_bwd_body(const HeadTrainArgs& A) {
     }
     gp[e] = a;
   }
+  TSTAMP(22);
 }
 __global__ __launch_bounds__(64 * CB_NW) void mcaq_cmlp_bwd_kernel(HeadTrainArgs A) { mcaq_cmlp_bwd_body(A); }
 
@@ -1605,7 +1647,7 @@ __global__ __launch_bounds__(MTH) void mcaq_mapper_bwd_multi_kernel(TrMulti<Mapp
   __shared__ MapBwdLds L;
   mapper_bwd_stage<S>(tr_seg(M), L);
 }
-__global__ __launch_bounds__(256) void mcaq_bilateral_bwd_multi_kernel(TrMulti<HeadTrainArgs> M) {
+__global__ __launch_bounds__(BL_TH) void mcaq_bilateral_bwd_multi_kernel(TrMulti<HeadTrainArgs> M) {
   mcaq_bilateral_bwd_body(tr_seg(M));
 }
 __global__ __launch_bounds__(64 * CB_NW) void mcaq_cmlp_bwd_multi_kernel(TrMulti<HeadTrainArgs> M) {
@@ -1841,7 +1883,7 @@ int mcaq_head_train_backward(const mcaq_cmlp_params* P, const float* phi, const 
     if (e != hipSuccess) return (int)e;
     set = 1;
   }
-  hipLaunchKernelGGL(mcaq_bilateral_bwd_kernel, dim3(B), dim3(256), lb, stream, A);
+  hipLaunchKernelGGL(mcaq_bilateral_bwd_kernel, dim3(B), dim3(BL_TH), lb, stream, A);
   hipLaunchKernelGGL(mcaq_cmlp_bwd_kernel, dim3(A.nwg), dim3(64 * CB_NW), lc, stream, A);
   if (gparams)   // NULL: the caller reduces gpart (mcaq_head_train_grad_reduce)
     hipLaunchKernelGGL(mcaq_tr_reduce_kernel, dim3((CG_SIZE + 255) / 256), dim3(256), 0, stream, (const float*)gpart,
@@ -1995,7 +2037,7 @@ int mcaq_head_train_backward_multi(const mcaq_cmlp_params* P, const mcaq_head_se
     if (e != hipSuccess) return (int)e;
     set = 1;
   }
-  hipLaunchKernelGGL(mcaq_bilateral_bwd_multi_kernel, dim3(wb), dim3(256), lb, stream, Mb);
+  hipLaunchKernelGGL(mcaq_bilateral_bwd_multi_kernel, dim3(wb), dim3(BL_TH), lb, stream, Mb);
   hipLaunchKernelGGL(mcaq_cmlp_bwd_multi_kernel, dim3(wc), dim3(64 * CB_NW), lc, stream, Mc);
   return (int)hipGetLastError();
 }

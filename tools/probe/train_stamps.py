@@ -28,6 +28,10 @@ STAGES = [(32, 33, "stage |x| plane + ranges"), (33, 34, "pool |x| per tile + am
 MAPPER_BWD = [(56, 42, "operand loads issued + BN sums"), (42, 43, "g_a(S) (BN backward)"),
               (43, 44, "h(S-1) recompute"), (44, 45, "weight / bias partials"), (45, 46, "W^T g_a, g_y stores"),
               (46, 47, "BN(S-1) partial sums")]
+BILAT = [(57, 58, "range x spatial weights (exp)"), (58, 59, "per tile: C, g / D, centre"),
+         (59, 60, "adjoint gather")]
+CMLP = [(16, 17, "recompute layer 1 + LN1"), (17, 18, "recompute layer 2 + LN2 + L3"), (18, 19, "sigmoid / L3 / LN2 bwd"),
+        (19, 20, "L2^T + LN1 bwd"), (20, 21, "W2 partials (MFMA)"), (21, 22, "other partials")]
 MAPPER_FWD = [(50, 51, "batch statistics (map_stats)"), (52, 53, "h(S-1) into LDS"), (53, 54, "layer (FMA)"),
               (54, 55, "workgroup moments")]
 
@@ -52,6 +56,12 @@ def main():
         print("   %-34s %8d" % (name, st[b] - st[a]))
     print("mapper backward stage 3, workgroup 0 (64 tiles of scale 0): %d ticks" % (st[47] - st[56]))
     for a, b, name in MAPPER_BWD:
+        print("   %-34s %8d" % (name, st[b] - st[a]))
+    print("bilateral backward, image 0 of scale 0: %d ticks" % (st[60] - st[57]))
+    for a, b, name in BILAT:
+        print("   %-34s %8d" % (name, st[b] - st[a]))
+    print("complexity-MLP backward, workgroup 0: %d ticks" % (st[22] - st[16]))
+    for a, b, name in CMLP:
         print("   %-34s %8d" % (name, st[b] - st[a]))
     print("mapper forward stage 2, workgroup 0: %d ticks" % (st[55] - st[50]))
     for a, b, name in MAPPER_FWD:
