@@ -44,7 +44,7 @@ typedef void* hipEvent_t;
 extern "C" {
 #endif
 
-#define MCAQ_ABI_VERSION 20
+#define MCAQ_ABI_VERSION 21
 /* segments (hook scale x batch) per mcaq_stats / mcaq_finalize /
  * mcaq_morph* / mcaq_quant launch */
 #define MCAQ_MAX_SEGMENTS 9
@@ -473,6 +473,13 @@ typedef struct {
  * = s_0 (+ out if accumulate) + s_1 + s_2 in segment order (the values of
  * one reduction per segment, the later ones accumulating).  1 launch. */
 int mcaq_train_reduce_multi(const mcaq_reduce_seg* segs, int nseg, int chain, hipStream_t stream);
+/* mcaq_head_train_backward_multi with a chain reduction (as
+ * mcaq_train_reduce_multi with chain 1: nr segments into rsegs[0].out)
+ * riding on the bilateral launch as extra workgroups - the bit mapper's
+ * parameter gradients summed beside the head's backward instead of in a
+ * launch of their own (nr = 0: none). */
+int mcaq_head_train_backward_multi_ride(const mcaq_cmlp_params* P, const mcaq_head_seg* segs, int nseg,
+                                        const mcaq_reduce_seg* rsegs, int nr, hipStream_t stream);
 
 /* gparams of the mapper / head backward: accumulate != 0 adds to gparams
  * (the parameters' persistent gradient storage), 0 overwrites it; NULL

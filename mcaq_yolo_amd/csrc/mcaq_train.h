@@ -304,16 +304,29 @@ __device__ void map_stats(const MapperTrainArgs& A, const MapperWork& W, float* 
     const float* fp = W.fpart(L);
     // one process: this launch's workgroup partials; sharded: every rank's
     const int nsrc = A.gworld > 0 ? A.gworld : A.nwg;
-#pragma unroll 4
-    for (int w = part; w < nsrc; w += MW) {
-      const float nb = A.gworld > 0 ? A.gstat[(size_t)w * RANK_ENT + 128] : W.cnt[w];
-      const float mb = A.gworld > 0 ? A.gstat[(size_t)w * RANK_ENT + j] : fp[(size_t)w * 128 + j];
-      const float M2b = A.gworld > 0 ? A.gstat[(size_t)w * RANK_ENT + 64 + j] : fp[(size_t)w * 128 + N + j];
-      if (nb <= 0.0f) continue;
-      const float nn = n + nb, d = mb - m;
-      m = m + d * (nb / nn);
-      M2 = M2 + M2b + d * d * (n * nb / nn);
-      n = nn;
+    const bool gs = A.gworld > 0;
+    // 4 partials of the wave's share loaded before any is combined (clamped
+    // index: no load behind the empty-partial test, which made every
+    // partial a round trip of its own), combined in the same order
+    for (int w0 = part; w0 < nsrc; w0 += 4 * MW) {
+      float nbv[4], mbv[4], m2v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int w = imin_(w0 + r * MW, nsrc - 1);
+        nbv[r] = gs ? A.gstat[(size_t)w * RANK_ENT + 128] : W.cnt[w];
+        mbv[r] = gs ? A.gstat[(size_t)w * RANK_ENT + j] : fp[(size_t)w * 128 + j];
+        m2v[r] = gs ? A.gstat[(size_t)w * RANK_ENT + 64 + j] : fp[(size_t)w * 128 + N + j];
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float nb = w0 + r * MW < nsrc ? nbv[r] : 0.0f;
+        if (nb <= 0.0f) continue;
+        const float mb = mbv[r], M2b = m2v[r];
+        const float nn = n + nb, d = mb - m;
+        m = m + d * (nb / nn);
+        M2 = M2 + M2b + d * d * (n * nb / nn);
+        n = nn;
+      }
     }
     s_tmp[part * 192 + j] = n; s_tmp[part * 192 + 64 + j] = m; s_tmp[part * 192 + 128 + j] = M2;
   }
@@ -926,17 +939,31 @@ __device__ __forceinline__ void mcaq_bilateral_bwd_body(const HeadTrainArgs& A) 
   }
   __syncthreads();
   TSTAMP(59);
-  // adjoint gather: g_craw[u] = gcen[u] + sum over (k, t) with clamp(t + o_k) = u of cf[t][k]
-  for (int u = tid; u < NT; u += BL_TH) {
+  // adjoint gather: g_craw[u] = gcen[u] + sum over (k, t) with clamp(t + o_k)
+  // = u of cf[t][k].  One item per (tile u, tap k) - the tap's terms, tiles
+  // row-major (one term inside the image, up to 9 at a corner) - into the
+  // weight array (dead after the per-tile pass), then per tile gcen + the 25
+  // tap sums in tap order (one tile-serial chain of 25 variable loops before)
+  float* pk = wk;
+  for (int e = tid; e < NT * 25; e += BL_TH) {
+    const int u = e / 25, k = e - u * 25;
     const int uh = u / wt, uw = u - uh * wt;
+    int h0, h1, w0, w1;
+    tap_range(uh, k / 5 - 2, ht, h0, h1);
+    tap_range(uw, k % 5 - 2, wt, w0, w1);
+    float s = 0.0f;
+    for (int th = h0; th <= h1; ++th)
+      for (int tw = w0; tw <= w1; ++tw) s += cf[(th * wt + tw) * 25 + k];
+    pk[e] = s;
+  }
+  __syncthreads();
+  for (int u = tid; u < NT; u += BL_TH) {
+    float v[25];
+#pragma unroll
+    for (int k = 0; k < 25; ++k) v[k] = pk[u * 25 + k];
     float s = gcen[u];
-    for (int k = 0; k < 25; ++k) {
-      int h0, h1, w0, w1;
-      tap_range(uh, k / 5 - 2, ht, h0, h1);
-      tap_range(uw, k % 5 - 2, wt, w0, w1);
-      for (int th = h0; th <= h1; ++th)
-        for (int tw = w0; tw <= w1; ++tw) s += cf[(th * wt + tw) * 25 + k];
-    }
+#pragma unroll
+    for (int k = 0; k < 25; ++k) s += v[k];
     A.gcraw[(size_t)b * NT + u] = s;
   }
   TSTAMP(60);
@@ -958,6 +985,7 @@ __device__ __forceinline__ void mcaq_cmlp_bwd_body(const HeadTrainArgs& A) {
   extern __shared__ float smem_tr[];
   float* sv = smem_tr;                       // [TR_TPB][CB_ST]
   float* red = sv + TR_TPB * CB_ST;          // [NW][TR_TPB] cross-wave partial sums
+  float* w2s = red + NW * TR_TPB;            // W2 (32 x 64), read as broadcast LDS vectors
   const mcaq_cmlp_params& P = A.P;
   const int tid = threadIdx.x, lane = tid & 63, q = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wgi = (int)blockIdx.x - A.wg0;   // workgroup within this segment
@@ -976,6 +1004,9 @@ __device__ __forceinline__ void mcaq_cmlp_bwd_body(const HeadTrainArgs& A) {
     return r;
   };
   TSTAMP(16);
+  // W2 into LDS (4 floats a thread; published by the first cross-wave sum's barrier)
+#pragma unroll
+  for (int i = 0; i < 2048 / NTH; ++i) w2s[tid + i * NTH] = P.w2[tid + i * NTH];
   float ph[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) ph[k] = A.phi[(size_t)tc * 8 + k];
@@ -1017,7 +1048,7 @@ __device__ __forceinline__ void mcaq_cmlp_bwd_body(const HeadTrainArgs& A) {
     const int j = q * F2 + f;
     float acc = P.b2[j];
 #pragma unroll 16
-    for (int k = 0; k < 64; ++k) acc = fmaf(P.w2[j * 64 + k], v[CB_R1 + k], acc);
+    for (int k = 0; k < 64; ++k) acc = fmaf(w2s[j * 64 + k], v[CB_R1 + k], acc);
     x2[f] = acc;
     s += acc;
   }
@@ -1070,7 +1101,7 @@ __device__ __forceinline__ void mcaq_cmlp_bwd_body(const HeadTrainArgs& A) {
   for (int j = 0; j < 32; ++j) {
     const float ga = v[CB_GA2 + j];
 #pragma unroll
-    for (int f = 0; f < F1; ++f) accv[f] = fmaf(P.w2[j * 64 + q * F1 + f], ga, accv[f]);
+    for (int f = 0; f < F1; ++f) accv[f] = fmaf(w2s[j * 64 + q * F1 + f], ga, accv[f]);
   }
 #pragma unroll
   for (int f = 0; f < F1; ++f) {
@@ -1106,31 +1137,56 @@ __device__ __forceinline__ void mcaq_cmlp_bwd_body(const HeadTrainArgs& A) {
     for (int r = 0; r < 4; ++r) gp[CG_W2 + (jb * 16 + 4 * lk + r) * 64 + kb * 16 + lr] = d[r];
   }
   TSTAMP(21);
-  // the rest: W1 (64 x 8) 512, b1 / LN1 64 + 64 + 64, b2 / LN2 32 + 32 + 32, W3 32, b3 1
-  for (int e = tid; e < CG_SIZE; e += NTH) {
-    if (e >= CG_W2 && e < CG_B2) continue;
-    float a = 0.0f;
-    if (e < CG_B1) {                       // W1: ga1 (x) phi
-      const int j = e >> 3, k = e & 7;
-      for (int u = 0; u < TR_TPB; ++u) a = fmaf(tvec(u)[CB_GA1 + j], tvec(u)[CB_PHI + k], a);
-    } else if (e < CG_G1) {                // b1
-      for (int u = 0; u < TR_TPB; ++u) a += tvec(u)[CB_GA1 + e - CG_B1];
-    } else if (e < CG_BE1) {               // LN1 gamma
-      for (int u = 0; u < TR_TPB; ++u) a += tvec(u)[CB_GYX1 + e - CG_G1];
-    } else if (e < CG_W2) {                // LN1 beta
-      for (int u = 0; u < TR_TPB; ++u) a += tvec(u)[CB_GY1 + e - CG_BE1];
-    } else if (e < CG_G2) {                // b2
-      for (int u = 0; u < TR_TPB; ++u) a += tvec(u)[CB_GA2 + e - CG_B2];
-    } else if (e < CG_BE2) {               // LN2 gamma
-      for (int u = 0; u < TR_TPB; ++u) a += tvec(u)[CB_GYX2 + e - CG_G2];
-    } else if (e < CG_W3) {                // LN2 beta
-      for (int u = 0; u < TR_TPB; ++u) a += tvec(u)[CB_GY2 + e - CG_BE2];
-    } else if (e < CG_B3) {                // W3: ga3 * r2
-      for (int u = 0; u < TR_TPB; ++u) a = fmaf(tvec(u)[CB_GA3], tvec(u)[CB_R2 + e - CG_W3], a);
-    } else {                               // b3
-      for (int u = 0; u < TR_TPB; ++u) a += tvec(u)[CB_GA3];
+  // W1 (64 x 8) on MFMA as well: waves 0..3, one 16-row block each, the
+  // B columns 8..15 zero (the same tile-ordered FMA chains)
+  if (q < 4) {
+    const int lr = lane & 15, lk = lane >> 4;
+    tr_f4 d = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int st = 0; st < TR_TPB / 4; ++st) {
+      const float* w = tvec(4 * st + lk);
+      const float ph_k = w[CB_PHI + (lr & 7)];
+      d = tr_mfma4(w[CB_GA1 + q * 16 + lr], lr < 8 ? ph_k : 0.0f, d);
     }
-    gp[e] = a;
+    if (lr < 8) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) gp[CG_W1 + (q * 16 + 4 * lk + r) * 8 + lr] = d[r];
+    }
+  }
+  // the other sums over the tiles - b1 / LN1 (192) and b2 / LN2 / W3 / b3
+  // (129) - one element a thread, waves 4..7 first
+  {
+    const int r = (tid + NTH / 2) % NTH;
+    if (r < 321) {
+      const int e = r < 192 ? CG_B1 + r : CG_B2 + (r - 192);
+      float a = 0.0f;
+      if (e < CG_G1) {                       // b1
+#pragma unroll 8
+        for (int u = 0; u < TR_TPB; ++u) a += tvec(u)[CB_GA1 + e - CG_B1];
+      } else if (e < CG_BE1) {               // LN1 gamma
+#pragma unroll 8
+        for (int u = 0; u < TR_TPB; ++u) a += tvec(u)[CB_GYX1 + e - CG_G1];
+      } else if (e < CG_W2) {                // LN1 beta
+#pragma unroll 8
+        for (int u = 0; u < TR_TPB; ++u) a += tvec(u)[CB_GY1 + e - CG_BE1];
+      } else if (e < CG_G2) {                // b2
+#pragma unroll 8
+        for (int u = 0; u < TR_TPB; ++u) a += tvec(u)[CB_GA2 + e - CG_B2];
+      } else if (e < CG_BE2) {               // LN2 gamma
+#pragma unroll 8
+        for (int u = 0; u < TR_TPB; ++u) a += tvec(u)[CB_GYX2 + e - CG_G2];
+      } else if (e < CG_W3) {                // LN2 beta
+#pragma unroll 8
+        for (int u = 0; u < TR_TPB; ++u) a += tvec(u)[CB_GY2 + e - CG_BE2];
+      } else if (e < CG_B3) {                // W3: ga3 * r2
+#pragma unroll 8
+        for (int u = 0; u < TR_TPB; ++u) a = fmaf(tvec(u)[CB_GA3], tvec(u)[CB_R2 + e - CG_W3], a);
+      } else {                               // b3
+#pragma unroll 8
+        for (int u = 0; u < TR_TPB; ++u) a += tvec(u)[CB_GA3];
+      }
+      gp[e] = a;
+    }
   }
   TSTAMP(22);
 }
@@ -1692,18 +1748,22 @@ __global__ __launch_bounds__(1024) void mcaq_bit_budget_kernel(BitBudgetArgs a) 
 // one reduction launch per segment leaves (the first with `accumulate`, the
 // others accumulating)
 struct TrReduceSeg { const float* part; float* out; int nwg, stride, count, accumulate; };
+// chain mode: element e of segment 0's output = s_0 (+ out) + s_1 + s_2
+__device__ __forceinline__ void tr_chain_elem(const TrMulti<TrReduceSeg>& M, int e) {
+  const TrReduceSeg& s0 = M.s[0];
+  if (e >= s0.count) return;
+  float v = 0.0f;
+  for (int k = 0; k < M.nseg; ++k) {
+    const TrReduceSeg& g = k == 0 ? M.s[0] : (k == 1 ? M.s[1] : M.s[2]);
+    const float sum = tr_ordered_sum(g.part, g.nwg, g.stride, e);
+    v = k == 0 ? (s0.accumulate ? s0.out[e] + sum : sum) : v + sum;
+  }
+  s0.out[e] = v;
+}
 __global__ __launch_bounds__(256) void mcaq_tr_reduce_multi_kernel(TrMulti<TrReduceSeg> M, int chain) {
   const int e = blockIdx.x * 256 + threadIdx.x;
   if (chain) {
-    const TrReduceSeg& s0 = M.s[0];
-    if (e >= s0.count) return;
-    float v = 0.0f;
-    for (int k = 0; k < M.nseg; ++k) {
-      const TrReduceSeg& g = k == 0 ? M.s[0] : (k == 1 ? M.s[1] : M.s[2]);
-      const float sum = tr_ordered_sum(g.part, g.nwg, g.stride, e);
-      v = k == 0 ? (s0.accumulate ? s0.out[e] + sum : sum) : v + sum;
-    }
-    s0.out[e] = v;
+    tr_chain_elem(M, e);
   } else {
     const int k = blockIdx.y;
     const TrReduceSeg& g = k == 0 ? M.s[0] : (k == 1 ? M.s[1] : M.s[2]);
@@ -1711,6 +1771,19 @@ __global__ __launch_bounds__(256) void mcaq_tr_reduce_multi_kernel(TrMulti<TrRed
     const float sum = tr_ordered_sum(g.part, g.nwg, g.stride, e);
     g.out[e] = g.accumulate ? g.out[e] + sum : sum;
   }
+}
+
+// the bilateral backward launch with a chain reduction riding along as
+// workgroups rwg0.. (BL_TH elements each): the bit mapper's parameter
+// gradients, whose partials the mapper's last backward stage left, summed
+// while the analyzer head's backward runs (train_step._HeadMulti)
+__global__ __launch_bounds__(BL_TH) void mcaq_bilateral_bwd_ride_kernel(TrMulti<HeadTrainArgs> M, TrMulti<TrReduceSeg> R,
+                                                                       int rwg0) {
+  if ((int)blockIdx.x >= rwg0) {
+    tr_chain_elem(R, ((int)blockIdx.x - rwg0) * BL_TH + (int)threadIdx.x);
+    return;
+  }
+  mcaq_bilateral_bwd_body(tr_seg(M));
 }
 
 extern "C" {
@@ -1872,7 +1945,7 @@ int mcaq_head_train_backward(const mcaq_cmlp_params* P, const float* phi, const 
   A.B = B; A.ht = ht; A.wt = wt; A.n = B * ht * wt; A.nwg = (A.n + TR_TPB - 1) / TR_TPB;
   const size_t lb = (size_t)53 * ht * wt * sizeof(float);
   if (lb > 160 * 1024 - 1024) return (int)hipErrorInvalidValue;
-  const size_t lc = (size_t)(TR_TPB * CB_ST + CB_NW * TR_TPB) * sizeof(float);
+  const size_t lc = (size_t)(TR_TPB * CB_ST + CB_NW * TR_TPB + 2048) * sizeof(float);
   static int set = 0;
   if (!set) {
     hipError_t e = hipFuncSetAttribute((const void*)mcaq_cmlp_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2006,9 +2079,19 @@ int mcaq_mapper_train_backward_multi(const mcaq_mapper_params* P, const mcaq_map
   return (int)hipGetLastError();
 }
 
-int mcaq_head_train_backward_multi(const mcaq_cmlp_params* P, const mcaq_head_seg* segs, int nseg, hipStream_t stream) {
+int mcaq_head_train_backward_multi_ride(const mcaq_cmlp_params* P, const mcaq_head_seg* segs, int nseg,
+                                        const mcaq_reduce_seg* rsegs, int nr, hipStream_t stream) {
   using namespace mcaq;
-  if (!P || !segs || nseg < 1 || nseg > TR_MAXSEG) return (int)hipErrorInvalidValue;
+  if (!P || !segs || nseg < 1 || nseg > TR_MAXSEG || nr < 0 || nr > TR_MAXSEG || (nr > 0 && !rsegs))
+    return (int)hipErrorInvalidValue;
+  TrMulti<TrReduceSeg> R{};
+  for (int k = 0; k < nr; ++k) {
+    const mcaq_reduce_seg& g = rsegs[k];
+    if (!g.part || (!g.out && k == 0) || g.nparts < 1 || g.stride < g.count || g.count < 1 || g.count != rsegs[0].count)
+      return (int)hipErrorInvalidValue;
+    R.s[k] = TrReduceSeg{g.part, g.out, g.nparts, g.stride, g.count, g.accumulate};
+  }
+  R.nseg = nr;
   TrMulti<HeadTrainArgs> Mb{}, Mc{};
   int wb = 0, wc = 0;
   size_t lb = 0;
@@ -2026,7 +2109,7 @@ int mcaq_head_train_backward_multi(const mcaq_cmlp_params* P, const mcaq_head_se
     Mc.s[k] = A; Mc.s[k].wg0 = wc; wc += A.nwg;    // MLP: 64 tiles per workgroup
   }
   Mb.nseg = Mc.nseg = nseg;
-  const size_t lc = (size_t)(TR_TPB * CB_ST + CB_NW * TR_TPB) * sizeof(float);
+  const size_t lc = (size_t)(TR_TPB * CB_ST + CB_NW * TR_TPB + 2048) * sizeof(float);
   static int set = 0;
   if (!set) {
     hipError_t e = hipFuncSetAttribute((const void*)mcaq_cmlp_bwd_multi_kernel,
@@ -2037,9 +2120,25 @@ int mcaq_head_train_backward_multi(const mcaq_cmlp_params* P, const mcaq_head_se
     if (e != hipSuccess) return (int)e;
     set = 1;
   }
-  hipLaunchKernelGGL(mcaq_bilateral_bwd_multi_kernel, dim3(wb), dim3(BL_TH), lb, stream, Mb);
+  if (nr > 0) {
+    static int set_r = 0;
+    if (!set_r) {
+      const hipError_t e = hipFuncSetAttribute((const void*)mcaq_bilateral_bwd_ride_kernel,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024);
+      if (e != hipSuccess) return (int)e;
+      set_r = 1;
+    }
+    const int rw = (R.s[0].count + BL_TH - 1) / BL_TH;
+    hipLaunchKernelGGL(mcaq_bilateral_bwd_ride_kernel, dim3(wb + rw), dim3(BL_TH), lb, stream, Mb, R, wb);
+  } else {
+    hipLaunchKernelGGL(mcaq_bilateral_bwd_multi_kernel, dim3(wb), dim3(BL_TH), lb, stream, Mb);
+  }
   hipLaunchKernelGGL(mcaq_cmlp_bwd_multi_kernel, dim3(wc), dim3(64 * CB_NW), lc, stream, Mc);
   return (int)hipGetLastError();
+}
+
+int mcaq_head_train_backward_multi(const mcaq_cmlp_params* P, const mcaq_head_seg* segs, int nseg, hipStream_t stream) {
+  return mcaq_head_train_backward_multi_ride(P, segs, nseg, nullptr, 0, stream);
 }
 
 int mcaq_smask_train_backward_multi(const mcaq_smask_seg* segs, int nseg, hipStream_t stream) {

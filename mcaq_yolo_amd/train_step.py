@@ -277,8 +277,14 @@ class _HeadMulti(torch.autograd.Function):
             sg = segs[i]
             sg.phi, sg.craw, sg.gC, sg.gcraw, sg.gpart = _p(phis[i]), _p(craws[i]), _p(g), _p(gcraw), _p(gp)
             sg.B, sg.ht, sg.wt = B, ht, wt
-        abi.check(L.mcaq_head_train_backward_multi(ctypes.byref(q), segs, n, _stream()),
-                  "mcaq_head_train_backward_multi")
+        ride = _PENDING_REDUCE["segs"]
+        _PENDING_REDUCE["segs"] = None
+        if ride is not None:     # the mapper's gradient reduction as extra workgroups of the bilateral launch
+            abi.check(L.mcaq_head_train_backward_multi_ride(ctypes.byref(q), segs, n, ride[0], ride[1], _stream()),
+                      "mcaq_head_train_backward_multi_ride")
+        else:
+            abi.check(L.mcaq_head_train_backward_multi(ctypes.byref(q), segs, n, _stream()),
+                      "mcaq_head_train_backward_multi")
         mod_params = _cmlp_params(ctx.an)
         sink = ctx.an._gsink.target(mod_params) if len(mod_params) == len(params) else None
         gflat, acc = sink if sink is not None else (torch.empty(core._CM_SIZE, device=dev), 0)
@@ -287,15 +293,37 @@ class _HeadMulti(torch.autograd.Function):
         return (None, None, None) + (None,) * n + grads
 
 
-def _reduce_chain(gparts, out, acc, count):
-    """Sum every scale's per-workgroup partials into `out` in the order the
-    per-scale backwards accumulate them (autograd runs the last scale's first)."""
+def _chain_segs(gparts, out, acc, count):
+    """ReduceSeg chain: every scale's per-workgroup partials into `out`, in
+    the order the per-scale backwards accumulate them (autograd runs the last
+    scale's first)."""
     n = len(gparts)
     segs = (abi.ReduceSeg * n)()
     for k, (gp, nparts) in enumerate(reversed(gparts)):
         s = segs[k]
         s.part, s.out, s.nparts, s.stride, s.count, s.accumulate = _p(gp), _p(out), nparts, count, count, acc
-    abi.check(abi.lib().mcaq_train_reduce_multi(segs, n, 1, _stream()), "mcaq_train_reduce_multi")
+    return segs
+
+
+def _reduce_chain(gparts, out, acc, count):
+    abi.check(abi.lib().mcaq_train_reduce_multi(_chain_segs(gparts, out, acc, count), len(gparts), 1, _stream()),
+              "mcaq_train_reduce_multi")
+
+
+# The bit mapper's parameter-gradient reduction, deferred from its backward
+# to ride on the analyzer head's backward launch (the next node autograd runs
+# on this path; the mapper's .grad are views of its _GradSink buffer, which
+# nothing reads before the optimizer).  An engine callback at the end of
+# backward launches it on its own if no head backward took it.
+_PENDING_REDUCE = {"segs": None}
+
+
+def _flush_pending_reduce():
+    p = _PENDING_REDUCE["segs"]
+    _PENDING_REDUCE["segs"] = None
+    if p is not None:
+        segs, n, keep = p
+        abi.check(abi.lib().mcaq_train_reduce_multi(segs, n, 1, _stream()), "mcaq_train_reduce_multi")
 
 
 class _MapperMulti(torch.autograd.Function):
@@ -410,7 +438,11 @@ class _MapperMulti(torch.autograd.Function):
                     gs[st - 1] = list(bs)
         sink = mod._gsink.target(list(mod.mapping_network.parameters()))
         gflat, acc = sink if sink is not None else (torch.empty(core._MAPPER_G_SIZE, device=dev), 0)
-        _reduce_chain(gparts, gflat, acc, core._MAPPER_G_SIZE)
+        if sink is not None and ctx.pg is None and _PENDING_REDUCE["segs"] is None:
+            _PENDING_REDUCE["segs"] = (_chain_segs(gparts, gflat, acc, core._MAPPER_G_SIZE), n, gparts)
+            torch.autograd.Variable._execution_engine.queue_callback(_flush_pending_reduce)
+        else:
+            _reduce_chain(gparts, gflat, acc, core._MAPPER_G_SIZE)
         grads = (None,) * len(params) if sink is not None else tuple(core._split_flat(gflat, params))
         return (None, None, None, None) + tuple(g.view(s) for g, s in zip(gcs, ctx.shapes)) + grads
 
