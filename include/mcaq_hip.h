@@ -44,7 +44,7 @@ typedef void* hipEvent_t;
 extern "C" {
 #endif
 
-#define MCAQ_ABI_VERSION 21
+#define MCAQ_ABI_VERSION 22
 /* segments (hook scale x batch) per mcaq_stats / mcaq_finalize /
  * mcaq_morph* / mcaq_quant launch */
 #define MCAQ_MAX_SEGMENTS 9
@@ -498,6 +498,11 @@ typedef struct {
   int n, k, mode, dst;
 } mcaq_pack_seg;
 int mcaq_pack(const mcaq_pack_seg* segs, int nseg, float* out, int total, hipStream_t stream);
+/* mcaq_stats(scales, nscales) with mcaq_pack(segs, nseg, out, total) riding
+ * on the same launch as extra workgroups (the train step re-packs its blobs
+ * beside pass 1, which reads none of them). */
+int mcaq_stats_pack(const mcaq_stats_scale* scales, int nscales, const mcaq_pack_seg* segs, int nseg, float* out,
+                    int total, hipStream_t stream);
 
 /* ---- the optimizer end of a QAT step in two launches ----------------------
  * torch.nn.utils.clip_grad_norm_(max_norm) over every segment's gradient

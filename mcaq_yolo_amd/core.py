@@ -183,11 +183,15 @@ def _pack_segs(parts, mfma, base=0):
     return segs, o
 
 
-def _launch_pack(segs, out):
+def _pack_array(segs):
     arr = (abi.PackSeg * len(segs))()
     for a, (t, n, k, mode, dst) in zip(arr, segs):
         a.src, a.n, a.k, a.mode, a.dst = _p(t), n, k, mode, dst
-    abi.check(abi.lib().mcaq_pack(arr, len(segs), _p(out), out.numel(), _stream()), "mcaq_pack")
+    return arr
+
+
+def _launch_pack(segs, out):
+    abi.check(abi.lib().mcaq_pack(_pack_array(segs), len(segs), _p(out), out.numel(), _stream()), "mcaq_pack")
 
 
 def _device_pack(parts, mfma, total):

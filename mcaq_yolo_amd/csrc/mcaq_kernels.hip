@@ -435,8 +435,7 @@ __device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, fl
 #endif
 
 template <bool kVec>   // kVec: 8/16-byte row accesses for ppl 2/4 (host checks alignment)
-__global__ __launch_bounds__(256, MCAQ_STATS_MINW) void mcaq_stats_kernel(StatsArgs a) {
-  __shared__ float lds[ST_LDS];
+__device__ __forceinline__ void stats_dispatch(const StatsArgs& a, float* lds) {
   // heaviest (most channels per pixel) scales are the last ones: start them first
   const int unit = a.units_total - 1 - (int)blockIdx.x;
   int si = 0;
@@ -462,6 +461,12 @@ __global__ __launch_bounds__(256, MCAQ_STATS_MINW) void mcaq_stats_kernel(StatsA
     if (ppl == 2) { stats_unit<2, kVec>(S, lu, lds); return; }
   }
   stats_unit<1, kVec>(S, lu, lds);
+}
+
+template <bool kVec>
+__global__ __launch_bounds__(256, MCAQ_STATS_MINW) void mcaq_stats_kernel(StatsArgs a) {
+  __shared__ float lds[ST_LDS];
+  stats_dispatch<kVec>(a, lds);
 }
 
 // ---------------------------------------------------------------------------
@@ -1245,9 +1250,9 @@ int mcaq_launch_spatial_quantization(const float* input, const float* bit_map, c
   return mcaq_quant(&q, 1, stream);
 }
 
-int mcaq_stats(const mcaq_stats_scale* scales, int nscales, hipStream_t stream) {
+// the arguments of a pass-1 launch; returns 0 or a hipError_t (vec: 16-byte rows)
+static int stats_args(const mcaq_stats_scale* scales, int nscales, StatsArgs& a, bool& vec) {
   if (nscales < 1 || nscales > MAXSEG) return (int)hipErrorInvalidValue;
-  StatsArgs a;
   int units = 0;
   for (int i = 0; i < nscales; ++i) {
     a.s[i] = scales[i];
@@ -1261,12 +1266,20 @@ int mcaq_stats(const mcaq_stats_scale* scales, int nscales, hipStream_t stream) 
   a.nscales = nscales;
   a.units_total = units;
   // 16-byte (ppl 4) / 8-byte (ppl 2) rows need 16/8-byte aligned bases
-  bool vec = true;
+  vec = true;
   for (int i = 0; i < nscales; ++i) vec = vec && ((uintptr_t)scales[i].x & 15) == 0;
+  return 0;
+}
+
+int mcaq_stats(const mcaq_stats_scale* scales, int nscales, hipStream_t stream) {
+  StatsArgs a;
+  bool vec;
+  const int e = stats_args(scales, nscales, a, vec);
+  if (e) return e;
   if (vec)
-    launch_k(mcaq_stats_kernel<true>, dim3(units), dim3(256), 0, stream, a);
+    launch_k(mcaq_stats_kernel<true>, dim3(a.units_total), dim3(256), 0, stream, a);
   else
-    launch_k(mcaq_stats_kernel<false>, dim3(units), dim3(256), 0, stream, a);
+    launch_k(mcaq_stats_kernel<false>, dim3(a.units_total), dim3(256), 0, stream, a);
   return (int)hipGetLastError();
 }
 

@@ -452,16 +452,19 @@ __device__ __forceinline__ void mapper_fwd_stage(const MapperTrainArgs& A, MapFw
     float bq[NQ];
 #pragma unroll
     for (int f = 0; f < NQ; ++f) bq[f] = bb[q * NQ + f];
+    // k outer, the NQ outputs' FMA chains interleaved (each still runs over
+    // k in order from its bias)
     float o[NQ];
 #pragma unroll
-    for (int f = 0; f < NQ; ++f) {
-      const int j = q * NQ + f;
-      float acc = bq[f];
+    for (int f = 0; f < NQ; ++f) o[f] = bq[f];
 #pragma unroll
-      for (int k = 0; k < K; ++k) acc = fmaf(w[j * K + k], x[k], acc);
-      o[f] = acc;
-      if (valid) aout[(size_t)j * A.n + t] = acc;
+    for (int k = 0; k < K; ++k) {
+#pragma unroll
+      for (int f = 0; f < NQ; ++f) o[f] = fmaf(w[(q * NQ + f) * K + k], x[k], o[f]);
     }
+#pragma unroll
+    for (int f = 0; f < NQ; ++f)
+      if (valid) aout[(size_t)(q * NQ + f) * A.n + t] = o[f];
     if constexpr (S == 2) TSTAMP(54);
     wg_moments<NQ>(o, valid, nvalid, q * NQ, W.fpart(S) + (size_t)wgi * 128, N);
     if (tid == 0) W.cnt[wgi] = nvalid;
@@ -1018,14 +1021,14 @@ __device__ __forceinline__ void mcaq_cmlp_bwd_body(const HeadTrainArgs& A) {
   float x1[F1];
   float s = 0.0f;
 #pragma unroll
-  for (int f = 0; f < F1; ++f) {
-    const int j = q * F1 + f;
-    float acc = P.b1[j];
+  for (int f = 0; f < F1; ++f) x1[f] = P.b1[q * F1 + f];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) acc = fmaf(P.w1[j * 8 + k], ph[k], acc);
-    x1[f] = acc;
-    s += acc;
+  for (int k = 0; k < 8; ++k) {      // k outer: the F1 chains interleaved, each over k in order
+#pragma unroll
+    for (int f = 0; f < F1; ++f) x1[f] = fmaf(P.w1[(q * F1 + f) * 8 + k], ph[k], x1[f]);
   }
+#pragma unroll
+  for (int f = 0; f < F1; ++f) s += x1[f];
   const float mu1 = xsum(s) / 64.0f;
   s = 0.0f;
 #pragma unroll
@@ -1044,14 +1047,15 @@ __device__ __forceinline__ void mcaq_cmlp_bwd_body(const HeadTrainArgs& A) {
   float x2[F2];
   s = 0.0f;
 #pragma unroll
-  for (int f = 0; f < F2; ++f) {
-    const int j = q * F2 + f;
-    float acc = P.b2[j];
+  for (int f = 0; f < F2; ++f) x2[f] = P.b2[q * F2 + f];
 #pragma unroll 16
-    for (int k = 0; k < 64; ++k) acc = fmaf(w2s[j * 64 + k], v[CB_R1 + k], acc);
-    x2[f] = acc;
-    s += acc;
+  for (int k = 0; k < 64; ++k) {     // k outer: the F2 chains interleaved, each over k in order
+    const float r = v[CB_R1 + k];
+#pragma unroll
+    for (int f = 0; f < F2; ++f) x2[f] = fmaf(w2s[(q * F2 + f) * 64 + k], r, x2[f]);
   }
+#pragma unroll
+  for (int f = 0; f < F2; ++f) s += x2[f];
   const float mu2 = xsum(s) / 32.0f;
   s = 0.0f;
 #pragma unroll
@@ -1650,8 +1654,7 @@ struct PackArgs {
   int nseg, total;
 };
 
-__global__ __launch_bounds__(256) void mcaq_pack_kernel(PackArgs a, float* __restrict__ out) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
+__device__ __forceinline__ void pack_elem(const PackArgs& a, float* __restrict__ out, int e) {
   if (e >= a.total) return;
   float v = 0.0f;
   for (int i = 0; i < a.nseg; ++i) {
@@ -1669,6 +1672,22 @@ __global__ __launch_bounds__(256) void mcaq_pack_kernel(PackArgs a, float* __res
     }
   }
   out[e] = v;
+}
+__global__ __launch_bounds__(256) void mcaq_pack_kernel(PackArgs a, float* __restrict__ out) {
+  pack_elem(a, out, blockIdx.x * 256 + threadIdx.x);
+}
+
+// the train step's blob pack riding on its pass-1 launch as workgroups
+// units_total.. (pass 1 reads no blob; the morph launch that follows does)
+template <bool kVec>
+__global__ __launch_bounds__(256, MCAQ_STATS_MINW) void mcaq_stats_pack_kernel(StatsArgs a, PackArgs p,
+                                                                             float* __restrict__ out) {
+  __shared__ float lds[ST_LDS];
+  if ((int)blockIdx.x >= a.units_total) {
+    pack_elem(p, out, ((int)blockIdx.x - a.units_total) * 256 + (int)threadIdx.x);
+    return;
+  }
+  stats_dispatch<kVec>(a, lds);
 }
 
 }  // namespace mcaq
@@ -1749,6 +1768,8 @@ __global__ __launch_bounds__(1024) void mcaq_bit_budget_kernel(BitBudgetArgs a) 
 // others accumulating)
 struct TrReduceSeg { const float* part; float* out; int nwg, stride, count, accumulate; };
 // chain mode: element e of segment 0's output = s_0 (+ out) + s_1 + s_2
+// (a variant walking all segments' partials as one 16-deep load list was
+// slower: 5.9 -> 10.7 us for the complexity-MLP chain, r05)
 __device__ __forceinline__ void tr_chain_elem(const TrMulti<TrReduceSeg>& M, int e) {
   const TrReduceSeg& s0 = M.s[0];
   if (e >= s0.count) return;
@@ -2255,10 +2276,8 @@ int mcaq_head_train_grad_reduce(int n, const float* gpart, float* gparams, int a
 
 size_t mcaq_smask_gpart_floats(int B) { return (size_t)B * mcaq::SG_SIZE; }
 
-int mcaq_pack(const mcaq_pack_seg* segs, int nseg, float* out, int total, hipStream_t stream) {
-  using namespace mcaq;
+static int pack_args(const mcaq_pack_seg* segs, int nseg, float* out, int total, mcaq::PackArgs& a) {
   if (!segs || !out || nseg < 1 || nseg > MCAQ_PACK_MAXSEG || total < 1) return (int)hipErrorInvalidValue;
-  PackArgs a{};
   for (int i = 0; i < nseg; ++i) {
     const mcaq_pack_seg& g = segs[i];
     if (!g.src || g.n < 1 || g.dst < 0 || (g.mode != 0 && (g.mode != 1 || g.k < 1))) return (int)hipErrorInvalidValue;
@@ -2267,7 +2286,33 @@ int mcaq_pack(const mcaq_pack_seg* segs, int nseg, float* out, int total, hipStr
     a.seg[i] = g;
   }
   a.nseg = nseg; a.total = total;
+  return 0;
+}
+
+int mcaq_pack(const mcaq_pack_seg* segs, int nseg, float* out, int total, hipStream_t stream) {
+  using namespace mcaq;
+  PackArgs a{};
+  const int e = pack_args(segs, nseg, out, total, a);
+  if (e) return e;
   hipLaunchKernelGGL(mcaq_pack_kernel, dim3((total + 255) / 256), dim3(256), 0, stream, a, out);
+  return (int)hipGetLastError();
+}
+
+int mcaq_stats_pack(const mcaq_stats_scale* scales, int nscales, const mcaq_pack_seg* segs, int nseg, float* out,
+                    int total, hipStream_t stream) {
+  using namespace mcaq;
+  StatsArgs a;
+  bool vec;
+  const int e = stats_args(scales, nscales, a, vec);
+  if (e) return e;
+  PackArgs p{};
+  const int pe = pack_args(segs, nseg, out, total, p);
+  if (pe) return pe;
+  const dim3 g(a.units_total + (total + 255) / 256);
+  if (vec)
+    launch_k(mcaq_stats_pack_kernel<true>, g, dim3(256), 0, stream, a, p, out);
+  else
+    launch_k(mcaq_stats_pack_kernel<false>, g, dim3(256), 0, stream, a, p, out);
   return (int)hipGetLastError();
 }
 

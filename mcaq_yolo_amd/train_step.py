@@ -32,6 +32,16 @@ def _cmlp_params(an):
 
 
 _SM_BLOBS = {"key": None, "blobs": None, "primed": False}
+_PREPACK = {"pending": None}
+
+
+def _flush_prepack():
+    """The pending blob pack on its own (when no pass-1 launch took it)."""
+    p = _PREPACK["pending"]
+    _PREPACK["pending"] = None
+    if p is not None:
+        arr, n, out, _ = p
+        abi.check(abi.lib().mcaq_pack(arr, n, _p(out), out.numel(), _stream()), "mcaq_pack")
 
 
 def _prepack(an, mods):
@@ -67,7 +77,8 @@ def _prepack(an, mods):
             segs.append((p.detach(), p.numel(), 1, 0, o))
             o += p.numel()
     out = torch.empty(core._CM_BLOB + len(mods) * stride, device=cps[0].device)
-    core._launch_pack(segs, out)
+    # launched by the analyzer's pass-1 launch as extra workgroups (mcaq_stats_pack)
+    _PREPACK["pending"] = (core._pack_array(segs), len(segs), out, segs)
     an._blob.prime(out[:core._CM_BLOB], None if capturing else ckey)
     _SM_BLOBS["blobs"] = [out[core._CM_BLOB + i * stride:core._CM_BLOB + (i + 1) * stride] for i in range(len(mods))]
     _SM_BLOBS["key"] = None if capturing else skey
@@ -236,7 +247,13 @@ def _run_analyzer_multi(an, xs):
         f = fz[i]
         f.pmin, f.pmax, f.min_out, f.max_out = _p(o["pmin"]), _p(o["pmax"]), _p(o["bmin"]), _p(o["bmax"])
         f.C, f.nunits, f.min_stride = C, o["pmin"].shape[0], 1
-    abi.check(L.mcaq_stats(stats, n, _stream()), "mcaq_stats")
+    pend = _PREPACK["pending"]
+    _PREPACK["pending"] = None
+    if pend is not None:      # the step's blob pack rides on pass 1
+        arr, npk, out, _ = pend
+        abi.check(L.mcaq_stats_pack(stats, n, arr, npk, _p(out), out.numel(), _stream()), "mcaq_stats_pack")
+    else:
+        abi.check(L.mcaq_stats(stats, n, _stream()), "mcaq_stats")
     abi.check(L.mcaq_morph_finalize(morphs, n, fz, n, _stream()), "mcaq_morph_finalize")
     return outs
 
@@ -733,7 +750,10 @@ def forward_features(hooks, feats, state):
     if FUSED_MASK_QAT and state.get("quantize", True) and \
             all(q.smooth_transitions and m is not None for q, m in zip(qs, smods)):
         _prepack(an, smods)          # the step's two blob packs in one launch
-    cs = list(_HeadMulti.apply(an, n, box, *xs, *_cmlp_params(an)))
+    try:
+        cs = list(_HeadMulti.apply(an, n, box, *xs, *_cmlp_params(an)))
+    finally:
+        _flush_prepack()             # normally taken by the pass-1 launch
     if hooks.normalize_complexity:
         for i, c in enumerate(cs):
             B = c.shape[0]
