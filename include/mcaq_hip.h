@@ -44,7 +44,7 @@ typedef void* hipEvent_t;
 extern "C" {
 #endif
 
-#define MCAQ_ABI_VERSION 22
+#define MCAQ_ABI_VERSION 23
 /* segments (hook scale x batch) per mcaq_stats / mcaq_finalize /
  * mcaq_morph* / mcaq_quant launch */
 #define MCAQ_MAX_SEGMENTS 9
@@ -362,6 +362,13 @@ int mcaq_mapper_running_update(const mcaq_mapper_params* P, const float* const* 
 int mcaq_ema_stats_multi_running(const mcaq_ema_seg* segs, int nseg, const mcaq_mapper_params* P,
                                  const float* const* works, const int* ns, int count, float momentum,
                                  hipStream_t stream);
+/* mcaq_morph(scales) of a pass-B-only launch (the train step's soft-mask
+ * planes) with the quantizers' EMA (esegs, as mcaq_ema_stats_multi) and,
+ * count > 0, the mapper's running-statistics update riding along as extra
+ * workgroups; any other morph launch runs first, then the EMA launch. */
+int mcaq_morph_ema(const mcaq_morph_scale* scales, int nscales, const mcaq_ema_seg* esegs, int ne,
+                   const mcaq_mapper_params* P, const float* const* works, const int* ns, int count, float momentum,
+                   hipStream_t stream);
 /* grid_sync: NULL (one launch per batch-statistics barrier), or 2 zeroed
  * uint32 that launches on one stream share (each launch leaves them zeroed):
  * forward and backward then run as ONE launch each, with grid-wide barriers

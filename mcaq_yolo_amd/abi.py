@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libmcaq_hip.so")
-ABI_VERSION = 22
+ABI_VERSION = 23
 MAX_SEGMENTS = 9   # MCAQ_MAX_SEGMENTS: segments (hook scale x batch) per launch
 
 P = ctypes.c_void_p
@@ -152,7 +152,7 @@ EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats",
            "mcaq_mapper_train_forward_stage_multi", "mcaq_mapper_train_backward_stage_multi", "mcaq_clip_adamw", "mcaq_clip_adamw_work_floats",
            "mcaq_bit_budget_forward", "mcaq_qat_smask_backward_multi", "mcaq_qat_forward_budget",
            "mcaq_ema_stats_multi_running", "mcaq_head_train_backward_multi_ride",
-           "mcaq_stats_pack")
+           "mcaq_stats_pack", "mcaq_morph_ema")
 
 _LIB = None
 
@@ -247,6 +247,9 @@ def _declare(lib):
     lib.mcaq_head_train_backward.argtypes = [ctypes.POINTER(CmlpParams), P, P, P, I, I, I, P, P, P, I, P]
     lib.mcaq_ema_stats_ex.restype = I
     lib.mcaq_ema_stats_ex.argtypes = [P, P, P, P, I, ctypes.c_double, I, P, P, P, P]
+    lib.mcaq_morph_ema.restype = I
+    lib.mcaq_morph_ema.argtypes = [ctypes.POINTER(MorphScale), I, ctypes.POINTER(EmaSeg), I,
+                                   ctypes.POINTER(MapperParams), ctypes.POINTER(P), ctypes.POINTER(I), I, Fl, P]
     lib.mcaq_stats_pack.restype = I
     lib.mcaq_stats_pack.argtypes = [ctypes.POINTER(StatsScale), I, ctypes.POINTER(PackSeg), I, P, I, P]
     lib.mcaq_pack.restype = I

@@ -817,7 +817,7 @@ __global__ __launch_bounds__(256) void mcaq_tb_mplane_kernel(MorphArgs a, int to
 // TS: floats per tile row of the LDS tile arrays (TILE_FLOATS_PAD when the
 // launch's images fit that way, else TILE_FLOATS; mcaq_morph.h)
 template <int TS>
-__global__ __launch_bounds__(TILES_THREADS, MCAQ_TILES_MINW) void mcaq_tiles_kernel(MorphArgs a, int wlds) {
+__device__ __forceinline__ void tiles_body(const MorphArgs& a, int wlds) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __builtin_amdgcn_s_setprio(MCAQ_MORPH_PRIO);
   int si = 0;
@@ -833,6 +833,10 @@ __global__ __launch_bounds__(TILES_THREADS, MCAQ_TILES_MINW) void mcaq_tiles_ker
   Shared sh;
   carve_shared(base, sh);
   morph_tiles<TS>(ctx, S, b, sh, wl, (int)threadIdx.x, TILES_THREADS, xs);
+}
+template <int TS>
+__global__ __launch_bounds__(TILES_THREADS, MCAQ_TILES_MINW) void mcaq_tiles_kernel(MorphArgs a, int wlds) {
+  tiles_body<TS>(a, wlds);
 }
 
 // ---------------------------------------------------------------------------

@@ -179,7 +179,10 @@ __device__ __forceinline__ void qat_budget_block(const QatBudget& B, float* red)
   }
 }
 
-template <bool kBwd, bool kVec>
+// kTile: every scale's map is a power-of-two multiple of its tile grid with
+// tiles >= 4 pixels wide (host-checked): a lane's 4 pixels share one tile, so
+// one bit-map load and one (lo, hi) table pair per channel serve all four
+template <bool kBwd, bool kVec, bool kTile = false>
 __global__ __launch_bounds__(256, MCAQ_QAT_MINW) void mcaq_qat_kernel(QatArgs a) {
   __shared__ float4 qt[32 * QAT_NB];   // scale, zp, 1/scale
   __shared__ float red[2][4][256];
@@ -233,6 +236,27 @@ __global__ __launch_bounds__(256, MCAQ_QAT_MINW) void mcaq_qat_kernel(QatArgs a)
   bool pv[4];
   int kl[4], kh[4];
   float fu[4], omf[4], mv[4];
+  const bool has_m = S.m != nullptr;
+  if constexpr (kTile) {
+    // one tile for the lane's 4 pixels: the same values in every k slot
+    // (the channel loop's table reads and parameters fold into one per channel)
+    const int h0 = qa / S.W, w0 = qa - h0 * S.W;
+    const float bv = S.bits[((size_t)b * S.ht + (h0 >> nmh.shift)) * S.wt + (w0 >> nmw.shift)];
+    const float fl = floorf(bv);
+    const float f0 = bv - fl;
+    const int lo = imin_(imax_((int)fl, QAT_LO), QAT_LO + QAT_NB - 1);
+    float4 m4 = make_float4(1.0f, 1.0f, 1.0f, 1.0f);
+    if (has_m) m4 = *reinterpret_cast<const float4*>(S.m + (size_t)b * HW + qa);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      pv[k] = q0 + k < HW;
+      fu[k] = f0;
+      omf[k] = 1.0f - f0;
+      kl[k] = lo - QAT_LO;
+      kh[k] = (lo < 8 ? lo + 1 : lo) - QAT_LO;
+    }
+    mv[0] = m4.x; mv[1] = m4.y; mv[2] = m4.z; mv[3] = m4.w;
+  } else {
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int p = imin_(q0 + k, HW - 1);
@@ -247,7 +271,7 @@ __global__ __launch_bounds__(256, MCAQ_QAT_MINW) void mcaq_qat_kernel(QatArgs a)
     kh[k] = (lo < 8 ? lo + 1 : lo) - QAT_LO;    // Q_hi := Q_lo past 8 bits (frac is 0 there)
     mv[k] = S.m ? S.m[(size_t)b * HW + p] : 1.0f;
   }
-  const bool has_m = S.m != nullptr;
+  }
   __syncthreads();   // qt ready
   float sgm[4] = {0.f, 0.f, 0.f, 0.f}, sgf[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -396,8 +420,7 @@ __global__ __launch_bounds__(256) void mcaq_ema_kernel(const float* bmin, const 
 // running workgroup offsets (one per segment, 256 channels per workgroup)
 struct EmaSeg { const float *bmin, *bmax; float *rmin, *rmax, *cmin, *cmax; long long* nbt; int C, first, wg0; float am, cm; };
 struct EmaMulti { EmaSeg s[3]; int nseg; };
-__device__ __forceinline__ void ema_multi_body(const EmaMulti& M) {
-  const int x = (int)blockIdx.x;
+__device__ __forceinline__ void ema_multi_body(const EmaMulti& M, int x) {
   const EmaSeg& g = (M.nseg > 2 && x >= M.s[2].wg0) ? M.s[2] : ((M.nseg > 1 && x >= M.s[1].wg0) ? M.s[1] : M.s[0]);
   const int c = (x - g.wg0) * 256 + threadIdx.x;
   if (c == 0 && g.nbt) g.nbt[0] += 1;
@@ -415,7 +438,7 @@ __device__ __forceinline__ void ema_multi_body(const EmaMulti& M) {
   if (g.cmin) g.cmin[c] = lo;
   if (g.cmax) g.cmax[c] = hi;
 }
-__global__ __launch_bounds__(256) void mcaq_ema_multi_kernel(EmaMulti M) { ema_multi_body(M); }
+__global__ __launch_bounds__(256) void mcaq_ema_multi_kernel(EmaMulti M) { ema_multi_body(M, (int)blockIdx.x); }
 
 }  // namespace mcaq
 
@@ -434,6 +457,15 @@ static inline int ema_multi_args(const mcaq_ema_seg* segs, int nseg, EmaMulti& M
   }
   M.nseg = nseg;
   return wg;
+}
+// kTile launches: power-of-two tile multiples, tiles >= 4 pixels wide,
+// 16-byte rows (and m plane)
+static inline bool qat_tile_ok(const mcaq_qat_scale* sc, int n) {
+  for (int i = 0; i < n; ++i) {
+    const NearestMap mh = nearest_map(sc[i].ht, sc[i].H), mw = nearest_map(sc[i].wt, sc[i].W);
+    if (mh.shift < 0 || mw.shift < 2 || (sc[i].W & 3) != 0 || (((uintptr_t)sc[i].m) & 15) != 0) return false;
+  }
+  return true;
 }
 static inline bool qat_aligned16(const mcaq_qat_scale& s, bool bwd) {
   uintptr_t u = (uintptr_t)s.x;
@@ -481,7 +513,9 @@ int mcaq_qat_forward(const mcaq_qat_scale* scales, int nscales, hipStream_t stre
   bool vec = true;
   for (int i = 0; i < nscales; ++i)
     vec = vec && ((scales[i].H * scales[i].W) & 3) == 0 && mcaq::qat_aligned16(scales[i], false);
-  if (vec)
+  if (vec && mcaq::qat_tile_ok(scales, nscales))
+    launch_k((mcaq::mcaq_qat_kernel<false, true, true>), dim3(a.units_total), dim3(256), 0, stream, a);
+  else if (vec)
     launch_k((mcaq::mcaq_qat_kernel<false, true>), dim3(a.units_total), dim3(256), 0, stream, a);
   else
     launch_k((mcaq::mcaq_qat_kernel<false, false>), dim3(a.units_total), dim3(256), 0, stream, a);
@@ -504,7 +538,9 @@ int mcaq_qat_forward_budget(const mcaq_qat_scale* scales, int nscales, const flo
   bool vec = true;
   for (int i = 0; i < nscales; ++i)
     vec = vec && ((scales[i].H * scales[i].W) & 3) == 0 && mcaq::qat_aligned16(scales[i], false);
-  if (vec)
+  if (vec && mcaq::qat_tile_ok(scales, nscales))
+    launch_k((mcaq::mcaq_qat_kernel<false, true, true>), dim3(a.units_total + 1), dim3(256), 0, stream, a);
+  else if (vec)
     launch_k((mcaq::mcaq_qat_kernel<false, true>), dim3(a.units_total + 1), dim3(256), 0, stream, a);
   else
     launch_k((mcaq::mcaq_qat_kernel<false, false>), dim3(a.units_total + 1), dim3(256), 0, stream, a);
@@ -519,7 +555,9 @@ int mcaq_qat_backward(const mcaq_qat_scale* scales, int nscales, hipStream_t str
   bool vec = true;
   for (int i = 0; i < nscales; ++i)
     vec = vec && ((scales[i].H * scales[i].W) & 3) == 0 && mcaq::qat_aligned16(scales[i], true);
-  if (vec)
+  if (vec && mcaq::qat_tile_ok(scales, nscales))
+    launch_k((mcaq::mcaq_qat_kernel<true, true, true>), dim3(a.units_total), dim3(256), 0, stream, a);
+  else if (vec)
     launch_k((mcaq::mcaq_qat_kernel<true, true>), dim3(a.units_total), dim3(256), 0, stream, a);
   else
     launch_k((mcaq::mcaq_qat_kernel<true, false>), dim3(a.units_total), dim3(256), 0, stream, a);

@@ -288,7 +288,23 @@ __global__ __launch_bounds__(256) void mcaq_ema_running_kernel(EmaRunArgs a) {
     if (threadIdx.x < 64) mapper_running_body(a.R);
     return;
   }
-  ema_multi_body(a.M);
+  ema_multi_body(a.M, (int)blockIdx.x);
+}
+
+// the soft-mask pass B launch with the quantizers' EMA and the mapper's
+// running-statistics update riding along as workgroups wg0.. (the train
+// step's soft-mask planes do not read them; the quantizer launch after does)
+static_assert(TILES_THREADS == 256, "the EMA workgroups riding on pass B take 256 channels each");
+template <int TS>
+__global__ __launch_bounds__(TILES_THREADS, MCAQ_TILES_MINW) void mcaq_tiles_ema_kernel(MorphArgs a, int wlds,
+                                                                                     EmaRunArgs e, int wg0) {
+  if ((int)blockIdx.x >= wg0) {
+    const int x = (int)blockIdx.x - wg0;
+    if (x < e.ema_wg) ema_multi_body(e.M, x);
+    else if (e.R.count > 0 && threadIdx.x < 64) mapper_running_body(e.R);
+    return;
+  }
+  tiles_body<TS>(a, wlds);
 }
 
 // batch statistics of layer L from the forward partials: mean, rstd of every
@@ -1887,6 +1903,52 @@ int mcaq_ema_stats_multi_running(const mcaq_ema_seg* segs, int nseg, const mcaq_
   }
   a.ema_wg = wg;
   hipLaunchKernelGGL(mcaq_ema_running_kernel, dim3(wg + 1), dim3(256), 0, stream, a);
+  return (int)hipGetLastError();
+}
+
+int mcaq_morph_ema(const mcaq_morph_scale* scales, int nscales, const mcaq_ema_seg* esegs, int ne,
+                   const mcaq_mapper_params* P, const float* const* works, const int* ns, int count, float momentum,
+                   hipStream_t stream) {
+  using namespace mcaq;
+  if (!esegs || ne < 1 || ne > 3 || count < 0 || count > MAPPER_RU_MAX || (count > 0 && (!P || !works || !ns)))
+    return (int)hipErrorInvalidValue;
+  MorphLaunch L;
+  int e = morph_launch_config(scales, nscales, nullptr, 0, L);
+  if (e) return e;
+  EmaRunArgs r{};
+  const int wg = ema_multi_args(esegs, ne, r.M);
+  if (wg < 0) return (int)hipErrorInvalidValue;
+  if (count > 0) {
+    r.R.P = *P; r.R.count = count; r.R.momentum = momentum;
+    for (int k = 0; k < count; ++k) {
+      if (!works[k] || ns[k] < 1) return (int)hipErrorInvalidValue;
+      r.R.rstat[k] = mapper_work(const_cast<float*>(works[k]), ns[k]).rstat;
+    }
+  }
+  r.ema_wg = wg;
+  if (L.grid_a > 0 || L.band || L.tb || L.grid_b <= 0) {
+    // no lone pass-B launch to ride on: the morph launch, then the EMA launch
+    e = morph_launch(L, 3, stream);
+    if (e) return e;
+    return count > 0 ? mcaq_ema_stats_multi_running(esegs, ne, P, works, ns, count, momentum, stream)
+                     : mcaq_ema_stats_multi(esegs, ne, stream);
+  }
+  static int set_te = 0;
+  const int lim = MCAQ_MORPH_LDS_LIMIT - 1024;
+  if ((int)L.dyn_b > set_te) {
+    hipError_t ae = hipFuncSetAttribute((const void*)mcaq_tiles_ema_kernel<TILE_FLOATS_PAD>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+    if (ae == hipSuccess)
+      ae = hipFuncSetAttribute((const void*)mcaq_tiles_ema_kernel<TILE_FLOATS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               lim);
+    if (ae != hipSuccess) return (int)ae;
+    set_te = lim;
+  }
+  const dim3 g(L.grid_b + wg + (count > 0 ? 1 : 0)), t(TILES_THREADS);
+  if (L.ts == TILE_FLOATS_PAD)
+    hipLaunchKernelGGL(mcaq_tiles_ema_kernel<TILE_FLOATS_PAD>, g, t, L.dyn_b, stream, L.a, L.wlds, r, L.grid_b);
+  else
+    hipLaunchKernelGGL(mcaq_tiles_ema_kernel<TILE_FLOATS>, g, t, L.dyn_b, stream, L.a, L.wlds, r, L.grid_b);
   return (int)hipGetLastError();
 }
 

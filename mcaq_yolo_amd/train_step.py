@@ -138,7 +138,30 @@ def _ema_multi_ok(qs, xs):
     return True
 
 
-def _ema_multi(qs, xs, box, running=None):
+# The quantizers' EMA launch (with the mapper's running-statistics update),
+# deferred by _quantize_multi to ride on the soft-mask launch of
+# _MaskQuantMulti (mcaq_morph_ema); flushed on its own if nothing took it.
+_PENDING_EMA = {"args": None}
+
+
+def _flush_ema():
+    p = _PENDING_EMA["args"]
+    _PENDING_EMA["args"] = None
+    if p is not None:
+        _launch_ema(*p)
+
+
+def _launch_ema(segs, n, running, keep):
+    L = abi.lib()
+    if running is not None:
+        rq, wa, na, cnt, mom = running
+        abi.check(L.mcaq_ema_stats_multi_running(segs, n, ctypes.byref(rq), wa, na, cnt, mom, _stream()),
+                  "mcaq_ema_stats_multi_running")
+    else:
+        abi.check(L.mcaq_ema_stats_multi(segs, n, _stream()), "mcaq_ema_stats_multi")
+
+
+def _ema_multi(qs, xs, box, running=None, defer=False):
     """quantization.py:319-353 for every scale's quantizer: the batch min /
     max from the analyzer's pass-1 partials (one finalize launch for all
     scales), then the EMA, this step's copies and num_batches_tracked (one
@@ -182,13 +205,10 @@ def _ema_multi(qs, xs, box, running=None):
             keep[2 * i].copy_(-vec[o:o + C])
             keep[2 * i + 1].copy_(vec[o + C:o + 2 * C])
             o += 2 * C
-    if running is not None:
-        # + the mapper's running-statistics update as one extra workgroup
-        rq, wa, na, cnt, mom = running
-        abi.check(L.mcaq_ema_stats_multi_running(segs, n, ctypes.byref(rq), wa, na, cnt, mom, _stream()),
-                  "mcaq_ema_stats_multi_running")
+    if defer:
+        _PENDING_EMA["args"] = (segs, n, running, keep)
     else:
-        abi.check(L.mcaq_ema_stats_multi(segs, n, _stream()), "mcaq_ema_stats_multi")
+        _launch_ema(segs, n, running, keep)
     return mins, maxs
 
 
@@ -566,7 +586,19 @@ class _MaskQuantMulti(torch.autograd.Function):
             ms.append(m)
             morphs[i] = core._morph_struct(B, H, W, 4, ht, wt, abi.F_SOFTMASK, absmean=absmeans[i], bits_in=b,
                                            smask=blobs[i], m_out=m)
-        abi.check(L.mcaq_morph(morphs, n, st), "mcaq_morph(soft mask)")
+        ema = _PENDING_EMA["args"]
+        _PENDING_EMA["args"] = None
+        if ema is not None:
+            # the quantizers' EMA (+ the mapper's running update) rides on this launch
+            segs_e, ne, running, _ = ema
+            if running is not None:
+                rq, wa, na, cnt, mom = running
+                abi.check(L.mcaq_morph_ema(morphs, n, segs_e, ne, ctypes.byref(rq), wa, na, cnt, mom, st),
+                          "mcaq_morph_ema")
+            else:
+                abi.check(L.mcaq_morph_ema(morphs, n, segs_e, ne, None, None, None, 0, 0.0, st), "mcaq_morph_ema")
+        else:
+            abi.check(L.mcaq_morph(morphs, n, st), "mcaq_morph(soft mask)")
         xs = [_f32c(x) for x in xs]
         arr = (abi.QatScale * n)()
         ys = []
@@ -794,10 +826,13 @@ def _quantize_multi(hooks, feats, state, n, idxs, xs, box, cs, bits, qs, per_qua
     for i, x in enumerate(xs):
         if bits[i].dim() != 3 or bits[i].shape[0] != x.shape[0]:
             raise AssertionError(f"Batch size mismatch: {x.shape[0]} vs {bits[i].shape[0]}")
+    want = [q.smooth_transitions and q.soft_mask is not None for q in qs]
+    fused = FUSED_MASK_QAT and all(want) and n <= abi.MCAQ_TRAIN_MAXSEG
     if not per_quantizer:
         running = getattr(mapper, "_pending_running", None)
         mapper._pending_running = None
-        mins, maxs = _ema_multi(qs, xs, box, running)
+        # on the fused path the EMA launch rides on the soft-mask launch
+        mins, maxs = _ema_multi(qs, xs, box, running, defer=fused)
     for i, (q, x) in enumerate(zip(qs, xs) if per_quantizer else ()):
         B, C, H, W = x.shape
         p1 = box[i]
@@ -814,11 +849,13 @@ def _quantize_multi(hooks, feats, state, n, idxs, xs, box, cs, bits, qs, per_qua
         else:
             xmin, xmax = q.batch_minmax(x, None)
         mins.append(xmin); maxs.append(xmax)
-    want = [q.smooth_transitions and q.soft_mask is not None for q in qs]
-    if FUSED_MASK_QAT and all(want) and n <= abi.MCAQ_TRAIN_MAXSEG:
+    if fused:
         target = float(getattr(hooks, "target_bits", 4.0))
-        res = _MaskQuantMulti.apply([q.soft_mask for q in qs], n, target, *bits, *[b["absmean"] for b in box],
-                                    *feats, *mins, *maxs, *[p for q in qs for p in q.soft_mask.net.parameters()])
+        try:
+            res = _MaskQuantMulti.apply([q.soft_mask for q in qs], n, target, *bits, *[b["absmean"] for b in box],
+                                        *feats, *mins, *maxs, *[p for q in qs for p in q.soft_mask.net.parameters()])
+        finally:
+            _flush_ema()         # normally taken by the soft-mask launch
         ys, budget = list(res[:n]), {"avg_bits": res[n], "loss_bit": res[n + 1], "target": target, "bits": bits}
         for i in range(n):
             state.setdefault("aux", []).append({"layer": idxs[i], "complexity": cs[i], "bit_map": bits[i],

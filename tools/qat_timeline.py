@@ -1,13 +1,13 @@
 """Timeline of one graph-replayed QAT step (bench.py --config 5) from a
 rocprofv3 kernel trace: the kernels between the last two
-mcaq_mapper_running_kernel (or mcaq_ema_running_kernel) dispatches (one per step, issued after the join
+mcaq_mapper_running_kernel (or mcaq_ema_running_kernel, mcaq_tiles_ema_kernel) dispatches (one per step, issued after the join
 of the scale streams), by queue, with start offsets and durations (us)."""
 import csv
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-marks = [i for i, r in enumerate(rows) if "mapper_running_kernel" in r["Kernel_Name"] or "ema_running_kernel" in r["Kernel_Name"]]
+marks = [i for i, r in enumerate(rows) if any(m in r["Kernel_Name"] for m in ("mapper_running_kernel", "ema_running_kernel", "tiles_ema_kernel"))]
 k = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 a, b = marks[-k - 1], marks[-k]
 seg = rows[a + 1:b + 1]
