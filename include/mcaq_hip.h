@@ -44,7 +44,7 @@ typedef void* hipEvent_t;
 extern "C" {
 #endif
 
-#define MCAQ_ABI_VERSION 23
+#define MCAQ_ABI_VERSION 24
 /* segments (hook scale x batch) per mcaq_stats / mcaq_finalize /
  * mcaq_morph* / mcaq_quant launch */
 #define MCAQ_MAX_SEGMENTS 9
@@ -487,6 +487,13 @@ int mcaq_train_reduce_multi(const mcaq_reduce_seg* segs, int nseg, int chain, hi
  * launch of their own (nr = 0: none). */
 int mcaq_head_train_backward_multi_ride(const mcaq_cmlp_params* P, const mcaq_head_seg* segs, int nseg,
                                         const mcaq_reduce_seg* rsegs, int nr, hipStream_t stream);
+/* mcaq_mapper_train_backward_multi with per-segment reductions (as
+ * mcaq_train_reduce_multi with chain 0, segments of equal count) riding on
+ * its first (output-layer) stage launch as extra workgroups - the soft masks'
+ * parameter gradients summed beside the mapper's backward (nr = 0: none). */
+int mcaq_mapper_train_backward_multi_ride(const mcaq_mapper_params* P, const mcaq_mapper_seg* segs, int nseg,
+                                          float min_bits, float max_bits, float temperature,
+                                          const mcaq_reduce_seg* rsegs, int nr, hipStream_t stream);
 
 /* gparams of the mapper / head backward: accumulate != 0 adds to gparams
  * (the parameters' persistent gradient storage), 0 overwrites it; NULL

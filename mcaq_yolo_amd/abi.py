@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libmcaq_hip.so")
-ABI_VERSION = 23
+ABI_VERSION = 24
 MAX_SEGMENTS = 9   # MCAQ_MAX_SEGMENTS: segments (hook scale x batch) per launch
 
 P = ctypes.c_void_p
@@ -152,7 +152,7 @@ EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats",
            "mcaq_mapper_train_forward_stage_multi", "mcaq_mapper_train_backward_stage_multi", "mcaq_clip_adamw", "mcaq_clip_adamw_work_floats",
            "mcaq_bit_budget_forward", "mcaq_qat_smask_backward_multi", "mcaq_qat_forward_budget",
            "mcaq_ema_stats_multi_running", "mcaq_head_train_backward_multi_ride",
-           "mcaq_stats_pack", "mcaq_morph_ema")
+           "mcaq_stats_pack", "mcaq_morph_ema", "mcaq_mapper_train_backward_multi_ride")
 
 _LIB = None
 
@@ -232,6 +232,9 @@ def _declare(lib):
     lib.mcaq_mapper_train_backward_multi.restype = I
     lib.mcaq_mapper_train_backward_multi.argtypes = [ctypes.POINTER(MapperParams), ctypes.POINTER(MapperSeg), I, Fl,
                                                      Fl, Fl, P]
+    lib.mcaq_mapper_train_backward_multi_ride.restype = I
+    lib.mcaq_mapper_train_backward_multi_ride.argtypes = [ctypes.POINTER(MapperParams), ctypes.POINTER(MapperSeg), I,
+                                                          Fl, Fl, Fl, ctypes.POINTER(ReduceSeg), I, P]
     lib.mcaq_head_train_backward_multi_ride.restype = I
     lib.mcaq_head_train_backward_multi_ride.argtypes = [ctypes.POINTER(CmlpParams), ctypes.POINTER(HeadSeg), I,
                                                         ctypes.POINTER(ReduceSeg), I, P]

@@ -789,6 +789,7 @@ class LearnedSoftMask(nn.Module):
         self.register_buffer("smooth_kernel", (g1.unsqueeze(0) * g1.unsqueeze(1)).unsqueeze(0).unsqueeze(0))
         self.kernel_size = k
         self._blob = _BlobCache()
+        self._gsink = _GradSink()
 
     def blob(self):
         return self._blob.get(list(self.net.parameters()), lambda: _pack_softmask(self.net))

@@ -97,19 +97,18 @@ __device__ __forceinline__ void chan_combine(const float* part, int nwg, int str
 }
 
 // ---- parameter-gradient reduction ------------------------------------------
-// sum_w part[w * stride + e] in workgroup order; the loads of 8 partials are
-// issued before their adds (the sum is a chain of dependent adds, the loads
-// are not: one memory latency per 8 partials instead of per partial) - the
-// last, partial group too (clamped index, the surplus not added; it used to
-// take one latency per partial)
+// sum_w part[w * stride + e] in workgroup order; the loads of 16 partials
+// are issued before their adds (the sum is a chain of dependent adds, the
+// loads are not: one memory latency per 16 partials instead of per partial)
+// - the last, partial group too (clamped index, the surplus not added)
 __device__ __forceinline__ float tr_ordered_sum(const float* __restrict__ part, int nwg, int stride, int e) {
   float s = 0.0f;
-  for (int w = 0; w < nwg; w += 8) {
-    float v[8];
+  for (int w = 0; w < nwg; w += 16) {
+    float v[16];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = part[(size_t)imin_(w + k, nwg - 1) * stride + e];
+    for (int k = 0; k < 16; ++k) v[k] = part[(size_t)imin_(w + k, nwg - 1) * stride + e];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) s = w + k < nwg ? s + v[k] : s;
+    for (int k = 0; k < 16; ++k) s = w + k < nwg ? s + v[k] : s;
   }
   return s;
 }
@@ -1810,6 +1809,31 @@ __global__ __launch_bounds__(256) void mcaq_tr_reduce_multi_kernel(TrMulti<TrRed
   }
 }
 
+// per-segment mode as one flat index: element i = (segment i / count, e = i %
+// count) of segments of equal count, each into its own output
+__device__ __forceinline__ void tr_seg_elem(const TrMulti<TrReduceSeg>& M, int i) {
+  const int cnt = M.s[0].count, k = i / cnt, e = i - k * cnt;
+  if (k >= M.nseg) return;
+  const TrReduceSeg& g = k == 0 ? M.s[0] : (k == 1 ? M.s[1] : M.s[2]);
+  const float sum = tr_ordered_sum(g.part, g.nwg, g.stride, e);
+  g.out[e] = g.accumulate ? g.out[e] + sum : sum;
+}
+
+// the mapper's first backward stage with per-segment reductions riding along
+// as workgroups rwg0.. (MTH elements each): the soft masks' parameter
+// gradients, whose partials the soft-mask backward launch before it left
+// (train_step._MaskQuantMulti -> _MapperMulti)
+template <int S>
+__global__ __launch_bounds__(MTH) void mcaq_mapper_bwd_ride_kernel(TrMulti<MapperTrainArgs> M, TrMulti<TrReduceSeg> R,
+                                                                   int rwg0) {
+  __shared__ MapBwdLds L;
+  if ((int)blockIdx.x >= rwg0) {
+    tr_seg_elem(R, ((int)blockIdx.x - rwg0) * MTH + (int)threadIdx.x);
+    return;
+  }
+  mapper_bwd_stage<S>(tr_seg(M), L);
+}
+
 // the bilateral backward launch with a chain reduction riding along as
 // workgroups rwg0.. (BL_TH elements each): the bit mapper's parameter
 // gradients, whose partials the mapper's last backward stage left, summed
@@ -2138,10 +2162,20 @@ int mcaq_mapper_train_backward_stage_multi(const mcaq_mapper_params* P, const mc
   return (int)hipGetLastError();
 }
 
-int mcaq_mapper_train_backward_multi(const mcaq_mapper_params* P, const mcaq_mapper_seg* segs, int nseg,
-                                     float min_bits, float max_bits, float temperature, hipStream_t stream) {
+int mcaq_mapper_train_backward_multi_ride(const mcaq_mapper_params* P, const mcaq_mapper_seg* segs, int nseg,
+                                          float min_bits, float max_bits, float temperature,
+                                          const mcaq_reduce_seg* rsegs, int nr, hipStream_t stream) {
   using namespace mcaq;
-  if (!P || !segs || nseg < 1 || nseg > TR_MAXSEG) return (int)hipErrorInvalidValue;
+  if (!P || !segs || nseg < 1 || nseg > TR_MAXSEG || nr < 0 || nr > TR_MAXSEG || (nr > 0 && !rsegs))
+    return (int)hipErrorInvalidValue;
+  TrMulti<TrReduceSeg> R{};
+  for (int k = 0; k < nr; ++k) {
+    const mcaq_reduce_seg& g = rsegs[k];
+    if (!g.part || !g.out || g.nparts < 1 || g.stride < g.count || g.count < 1 || g.count != rsegs[0].count)
+      return (int)hipErrorInvalidValue;
+    R.s[k] = TrReduceSeg{g.part, g.out, g.nparts, g.stride, g.count, g.accumulate};
+  }
+  R.nseg = nr;
   TrMulti<MapperTrainArgs> M{};
   int wg = 0;
   for (int k = 0; k < nseg; ++k) {
@@ -2155,11 +2189,20 @@ int mcaq_mapper_train_backward_multi(const mcaq_mapper_params* P, const mcaq_map
   }
   M.nseg = nseg;
   const dim3 g(wg), t(MTH);
-  hipLaunchKernelGGL(mcaq_mapper_bwd_multi_kernel<4>, g, t, 0, stream, M);
+  if (nr > 0)
+    hipLaunchKernelGGL(mcaq_mapper_bwd_ride_kernel<4>, dim3(wg + (nr * R.s[0].count + MTH - 1) / MTH), t, 0, stream,
+                       M, R, wg);
+  else
+    hipLaunchKernelGGL(mcaq_mapper_bwd_multi_kernel<4>, g, t, 0, stream, M);
   hipLaunchKernelGGL(mcaq_mapper_bwd_multi_kernel<3>, g, t, 0, stream, M);
   hipLaunchKernelGGL(mcaq_mapper_bwd_multi_kernel<2>, g, t, 0, stream, M);
   hipLaunchKernelGGL(mcaq_mapper_bwd_multi_kernel<1>, g, t, 0, stream, M);
   return (int)hipGetLastError();
+}
+
+int mcaq_mapper_train_backward_multi(const mcaq_mapper_params* P, const mcaq_mapper_seg* segs, int nseg,
+                                     float min_bits, float max_bits, float temperature, hipStream_t stream) {
+  return mcaq_mapper_train_backward_multi_ride(P, segs, nseg, min_bits, max_bits, temperature, nullptr, 0, stream);
 }
 
 int mcaq_head_train_backward_multi_ride(const mcaq_cmlp_params* P, const mcaq_head_seg* segs, int nseg,

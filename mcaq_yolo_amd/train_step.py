@@ -363,6 +363,21 @@ def _flush_pending_reduce():
         abi.check(abi.lib().mcaq_train_reduce_multi(segs, n, 1, _stream()), "mcaq_train_reduce_multi")
 
 
+# The soft masks' parameter-gradient reductions (one per scale, into each
+# net's _GradSink), deferred from _MaskQuantMulti.backward to ride on the
+# bit mapper's first backward launch (the next node on this path) the same
+# way; an engine callback launches them on their own otherwise.
+_PENDING_SM_REDUCE = {"segs": None}
+
+
+def _flush_pending_sm_reduce():
+    p = _PENDING_SM_REDUCE["segs"]
+    _PENDING_SM_REDUCE["segs"] = None
+    if p is not None:
+        segs, n, keep = p
+        abi.check(abi.lib().mcaq_train_reduce_multi(segs, n, 0, _stream()), "mcaq_train_reduce_multi")
+
+
 class _MapperMulti(torch.autograd.Function):
     """Train-mode bit mapper of every scale: 4 forward launches (one per
     batch-statistics barrier) + the running-statistics update in scale order;
@@ -451,7 +466,14 @@ class _MapperMulti(torch.autograd.Function):
             gparts.append((gp, gp.numel() // core._MAPPER_G_SIZE))   # one partial per backward workgroup
             s = segs[i]
             s.c, s.work, s.gbits, s.gc, s.gpart, s.n = _p(cfs[i]), _p(works[i]), _p(g), _p(gc), _p(gp), m
-        if ctx.pg is None:
+        ride = _PENDING_SM_REDUCE["segs"] if ctx.pg is None else None
+        if ride is not None:
+            # the soft masks' gradient reductions as extra workgroups of the first stage launch
+            _PENDING_SM_REDUCE["segs"] = None
+            abi.check(L.mcaq_mapper_train_backward_multi_ride(ctypes.byref(ctx.q), segs, n, mod.min_bits, mod.max_bits,
+                                                              ctx.T, ride[0], ride[1], _stream()),
+                      "mcaq_mapper_train_backward_multi_ride")
+        elif ctx.pg is None:
             abi.check(L.mcaq_mapper_train_backward_multi(ctypes.byref(ctx.q), segs, n, mod.min_bits, mod.max_bits,
                                                          ctx.T, _stream()), "mcaq_mapper_train_backward_multi")
         else:
@@ -664,6 +686,19 @@ class _MaskQuantMulti(torch.autograd.Function):
         gl = _f32c(g_loss) if g_loss is not None else None
         bb = abi.BitBudget(_p(avg), _p(ga), _p(gl), ctx.target, n)
         abi.check(L.mcaq_qat_smask_backward_multi(segs, n, ctypes.byref(bb), st), "mcaq_qat_smask_backward_multi")
+        # every net's gradients straight into its _GradSink (their .grad), the
+        # reduction deferred to the mapper's backward launch; otherwise
+        # reduced here and handed to autograd
+        sinks = [ctx.mods[i]._gsink.target(list(ctx.mods[i].net.parameters())) for i in range(n)]
+        if all(sk is not None for sk in sinks) and _PENDING_SM_REDUCE["segs"] is None:
+            for i, (gf, acc) in enumerate(sinks):
+                rsegs[i].out, rsegs[i].accumulate = _p(gf), acc
+            _PENDING_SM_REDUCE["segs"] = (rsegs, n, keep)
+            torch.autograd.Variable._execution_engine.queue_callback(_flush_pending_sm_reduce)
+            nig = ctx.needs_input_grad
+            return (None, None, None) + tuple(gbs[i] if nig[3 + i] else None for i in range(n)) + (None,) * n + \
+                tuple(gxs[i] if nig[3 + 2 * n + i] else None for i in range(n)) + (None,) * (2 * n) + \
+                (None,) * sum(len(list(m.net.parameters())) for m in ctx.mods)
         abi.check(L.mcaq_train_reduce_multi(rsegs, n, 0, st), "mcaq_train_reduce_multi")
         pgrads = []
         for i in range(n):
