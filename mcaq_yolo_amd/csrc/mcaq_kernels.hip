@@ -816,7 +816,7 @@ __global__ __launch_bounds__(256) void mcaq_tb_mplane_kernel(MorphArgs a, int to
 // past the batch end recomputes the last image (identical values written twice).
 // TS: floats per tile row of the LDS tile arrays (TILE_FLOATS_PAD when the
 // launch's images fit that way, else TILE_FLOATS; mcaq_morph.h)
-template <int TS>
+template <int TS, bool kSmo = false>
 __device__ __forceinline__ void tiles_body(const MorphArgs& a, int wlds) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __builtin_amdgcn_s_setprio(MCAQ_MORPH_PRIO);
@@ -832,7 +832,7 @@ __device__ __forceinline__ void tiles_body(const MorphArgs& a, int wlds) {
   Ctx ctx{(int)threadIdx.x - g * G, G};
   Shared sh;
   carve_shared(base, sh);
-  morph_tiles<TS>(ctx, S, b, sh, wl, (int)threadIdx.x, TILES_THREADS, xs);
+  morph_tiles<TS, kSmo>(ctx, S, b, sh, wl, (int)threadIdx.x, TILES_THREADS, xs);
 }
 template <int TS>
 __global__ __launch_bounds__(TILES_THREADS, MCAQ_TILES_MINW) void mcaq_tiles_kernel(MorphArgs a, int wlds) {

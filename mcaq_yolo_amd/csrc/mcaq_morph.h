@@ -1563,8 +1563,25 @@ MCAQ_HD int tiles_lds_bytes(int H, int W, int NT, int TS = TILE_FLOATS_PAD) {
   return fixed_bytes() + tile_bytes(NT, TS) + extra_bytes(H, W, NT) + 100 * NT;
 }
 
+// per-tile mean |x| activation of the soft mask (adaptive_avg_pool2d windows)
+MCAQ_HD inline float smask_act_tile(const float* am, int H, int W, int ht, int wt, float inv_wt, int t) {
+  const int KH = H / ht, KW = W / wt;
+  const bool even = KH * ht == H && KW * wt == W && KH == KW;
+  const int i = div_small(t, wt, inv_wt), j = t - i * wt;
+  if (even && KH == 4) return (window_sum_t<4>(am, W, i * 4, j * 4) / 4.0f) / 4.0f;
+  if (even && KH == 8) return (window_sum_t<8>(am, W, i * 8, j * 8) / 8.0f) / 8.0f;
+  const int ha = (i * H) / ht, hb = ((i + 1) * H + ht - 1) / ht;
+  const int wa = (j * W) / wt, wb = ((j + 1) * W + wt - 1) / wt;
+  float s = 0.0f;
+  for (int h = ha; h < hb; ++h)
+    for (int w = wa; w < wb; ++w) s = s + am[h * W + w];
+  return (s / (float)(hb - ha)) / (float)(wb - wa);
+}
+
 // xs: the workgroup's MLP activation scratch (MLP_SCRATCH_FLOATS per wave), device only
-template <int TS = TILE_FLOATS_PAD>
+// kSmo: a soft-mask-only launch (every scale F_SOFTMASK with bits_in and at
+// most one tile per thread of its image group; host-checked)
+template <int TS = TILE_FLOATS_PAD, bool kSmo = false>
 MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh, float* wl, int wtid, int wnthr,
                          float* xs) {
   const int ht = S.ht, wt = S.wt, NT = ht * wt;
@@ -1577,33 +1594,15 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
   const float* Pm = S.smask;
   MSTAMP_INIT(b == 0 ? 0 : -1);
   MSTAMP(10);
-  // per-tile mean |x| activation of the soft mask (adaptive_avg_pool2d windows)
-  const int KH = S.H / ht, KW = S.W / wt;
-  const bool even = KH * ht == S.H && KW * wt == S.W && KH == KW;
-  auto act_tile = [&](const float* am, int t) {
-    const int i = div_small(t, wt, inv_wt), j = t - i * wt;
-    float a;
-    if (even && KH == 4) a = (window_sum_t<4>(am, S.W, i * 4, j * 4) / 4.0f) / 4.0f;
-    else if (even && KH == 8) a = (window_sum_t<8>(am, S.W, i * 8, j * 8) / 8.0f) / 8.0f;
-    else {
-      const int ha = (i * S.H) / ht, hb = ((i + 1) * S.H + ht - 1) / ht;
-      const int wa = (j * S.W) / wt, wb = ((j + 1) * S.W + wt - 1) / wt;
-      float s = 0.0f;
-      for (int h = ha; h < hb; ++h)
-        for (int w = wa; w < wb; ++w) s = s + am[h * S.W + w];
-      a = (s / (float)(hb - ha)) / (float)(wb - wa);
-    }
-    return a;
-  };
   // soft-mask-only launch (the train step's m planes, bits given): each
   // thread's tile bits and pooled activation are loaded before the weight
   // staging - one memory latency instead of three, the same values
-  const bool smo = (S.flags & (F_PHI | F_CMLP | F_MAPPER | F_SOFTMASK)) == F_SOFTMASK && S.bits_in &&
-                   NT <= ctx.nthr;
   float pre_b = 0.0f, pre_a = 0.0f;
-  if (smo && ctx.tid < NT) {
-    pre_b = S.bits_in[(size_t)b * NT + ctx.tid];
-    pre_a = act_tile(S.absmean + (size_t)b * S.H * S.W, ctx.tid);
+  if constexpr (kSmo) {
+    if (ctx.tid < NT) {
+      pre_b = S.bits_in[(size_t)b * NT + ctx.tid];
+      pre_a = smask_act_tile(S.absmean + (size_t)b * S.H * S.W, S.H, S.W, ht, wt, inv_wt, ctx.tid);
+    }
   }
 #if defined(__HIP_DEVICE_COMPILE__)
   stage_tiles<TS>(ctx, S, b, tiles, wl, wtid, wnthr);
@@ -1783,7 +1782,7 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
       if (S.bits_out) S.bits_out[(size_t)b * NT + t] = bv;
     }
     MSYNC();
-  } else if (smo) {
+  } else if (kSmo) {
     if (ctx.tid < NT) tiles[ctx.tid * TS + T_BITS] = pre_b;
     MSYNC();
   } else if ((S.flags & F_SOFTMASK) && S.bits_in) {
@@ -1799,7 +1798,7 @@ MCAQ_HD void morph_tiles(const Ctx& ctx, const MorphScale& S, int b, Shared& sh,
     const float* am = S.absmean + (size_t)b * H * W;
     float lmx = -3.402823466e38f;
     MFOR(t, NT) {
-      const float a = smo ? pre_a : act_tile(am, t);
+      const float a = kSmo ? pre_a : smask_act_tile(am, H, W, ht, wt, inv_wt, t);
       tiles[t * TS + T_ACT] = a;
       lmx = fmaxp(lmx, a);          // torch.amax: a NaN activation makes the image's max NaN
     }

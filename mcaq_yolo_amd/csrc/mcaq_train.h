@@ -294,7 +294,7 @@ __global__ __launch_bounds__(256) void mcaq_ema_running_kernel(EmaRunArgs a) {
 // running-statistics update riding along as workgroups wg0.. (the train
 // step's soft-mask planes do not read them; the quantizer launch after does)
 static_assert(TILES_THREADS == 256, "the EMA workgroups riding on pass B take 256 channels each");
-template <int TS>
+template <int TS, bool kSmo>
 __global__ __launch_bounds__(TILES_THREADS, MCAQ_TILES_MINW) void mcaq_tiles_ema_kernel(MorphArgs a, int wlds,
                                                                                      EmaRunArgs e, int wg0) {
   if ((int)blockIdx.x >= wg0) {
@@ -303,7 +303,7 @@ __global__ __launch_bounds__(TILES_THREADS, MCAQ_TILES_MINW) void mcaq_tiles_ema
     else if (e.R.count > 0 && threadIdx.x < 64) mapper_running_body(e.R);
     return;
   }
-  tiles_body<TS>(a, wlds);
+  tiles_body<TS, kSmo>(a, wlds);
 }
 
 // batch statistics of layer L from the forward partials: mean, rstd of every
@@ -1957,22 +1957,34 @@ int mcaq_morph_ema(const mcaq_morph_scale* scales, int nscales, const mcaq_ema_s
     return count > 0 ? mcaq_ema_stats_multi_running(esegs, ne, P, works, ns, count, momentum, stream)
                      : mcaq_ema_stats_multi(esegs, ne, stream);
   }
+  // soft-mask only (the train step's m planes): the tile loads issued up front
+  bool smo = true;
+  for (int i = 0; i < L.a.nscales; ++i) {
+    const MorphScale& S = L.a.s[i];
+    smo = smo && (S.flags & (F_PHI | F_CMLP | F_MAPPER | F_SOFTMASK)) == F_SOFTMASK && S.bits_in && S.absmean &&
+          S.ht * S.wt <= TILES_THREADS / L.a.tipw[i];
+  }
   static int set_te = 0;
   const int lim = MCAQ_MORPH_LDS_LIMIT - 1024;
   if ((int)L.dyn_b > set_te) {
-    hipError_t ae = hipFuncSetAttribute((const void*)mcaq_tiles_ema_kernel<TILE_FLOATS_PAD>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, lim);
-    if (ae == hipSuccess)
-      ae = hipFuncSetAttribute((const void*)mcaq_tiles_ema_kernel<TILE_FLOATS>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               lim);
-    if (ae != hipSuccess) return (int)ae;
+    const void* ks[4] = {(const void*)mcaq_tiles_ema_kernel<TILE_FLOATS_PAD, false>,
+                         (const void*)mcaq_tiles_ema_kernel<TILE_FLOATS, false>,
+                         (const void*)mcaq_tiles_ema_kernel<TILE_FLOATS_PAD, true>,
+                         (const void*)mcaq_tiles_ema_kernel<TILE_FLOATS, true>};
+    for (const void* k : ks) {
+      const hipError_t ae = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lim);
+      if (ae != hipSuccess) return (int)ae;
+    }
     set_te = lim;
   }
   const dim3 g(L.grid_b + wg + (count > 0 ? 1 : 0)), t(TILES_THREADS);
-  if (L.ts == TILE_FLOATS_PAD)
-    hipLaunchKernelGGL(mcaq_tiles_ema_kernel<TILE_FLOATS_PAD>, g, t, L.dyn_b, stream, L.a, L.wlds, r, L.grid_b);
-  else
-    hipLaunchKernelGGL(mcaq_tiles_ema_kernel<TILE_FLOATS>, g, t, L.dyn_b, stream, L.a, L.wlds, r, L.grid_b);
+  if (L.ts == TILE_FLOATS_PAD) {
+    if (smo) hipLaunchKernelGGL((mcaq_tiles_ema_kernel<TILE_FLOATS_PAD, true>), g, t, L.dyn_b, stream, L.a, L.wlds, r, L.grid_b);
+    else hipLaunchKernelGGL((mcaq_tiles_ema_kernel<TILE_FLOATS_PAD, false>), g, t, L.dyn_b, stream, L.a, L.wlds, r, L.grid_b);
+  } else {
+    if (smo) hipLaunchKernelGGL((mcaq_tiles_ema_kernel<TILE_FLOATS, true>), g, t, L.dyn_b, stream, L.a, L.wlds, r, L.grid_b);
+    else hipLaunchKernelGGL((mcaq_tiles_ema_kernel<TILE_FLOATS, false>), g, t, L.dyn_b, stream, L.a, L.wlds, r, L.grid_b);
+  }
   return (int)hipGetLastError();
 }
 
