@@ -1564,7 +1564,7 @@ MCAQ_HD int tiles_lds_bytes(int H, int W, int NT, int TS = TILE_FLOATS_PAD) {
 }
 
 // per-tile mean |x| activation of the soft mask (adaptive_avg_pool2d windows)
-MCAQ_HD inline float smask_act_tile(const float* am, int H, int W, int ht, int wt, float inv_wt, int t) {
+MCAQ_HD float smask_act_tile(const float* am, int H, int W, int ht, int wt, float inv_wt, int t) {
   const int KH = H / ht, KW = W / wt;
   const bool even = KH * ht == H && KW * wt == W && KH == KW;
   const int i = div_small(t, wt, inv_wt), j = t - i * wt;
