@@ -1178,31 +1178,25 @@ __device__ __forceinline__ void mcaq_cmlp_bwd_body(const HeadTrainArgs& A) {
     const int r = (tid + NTH / 2) % NTH;
     if (r < 321) {
       const int e = r < 192 ? CG_B1 + r : CG_B2 + (r - 192);
+      // every element's term is one FMA A(u) B(u) + a - the bias / LN sums
+      // with B = 1 (exactly their adds), W3 ga3 * r2 - as one loop: a wave
+      // holding two element types no longer runs two loops one after another
+      int oa, ob = -1;
+      if (e < CG_G1) oa = CB_GA1 + e - CG_B1;            // b1
+      else if (e < CG_BE1) oa = CB_GYX1 + e - CG_G1;     // LN1 gamma
+      else if (e < CG_W2) oa = CB_GY1 + e - CG_BE1;      // LN1 beta
+      else if (e < CG_G2) oa = CB_GA2 + e - CG_B2;       // b2
+      else if (e < CG_BE2) oa = CB_GYX2 + e - CG_G2;     // LN2 gamma
+      else if (e < CG_W3) oa = CB_GY2 + e - CG_BE2;      // LN2 beta
+      else if (e < CG_B3) { oa = CB_GA3; ob = CB_R2 + e - CG_W3; }   // W3: ga3 * r2
+      else oa = CB_GA3;                                  // b3
+      const int obc = ob >= 0 ? ob : 0;
       float a = 0.0f;
-      if (e < CG_G1) {                       // b1
 #pragma unroll 8
-        for (int u = 0; u < TR_TPB; ++u) a += tvec(u)[CB_GA1 + e - CG_B1];
-      } else if (e < CG_BE1) {               // LN1 gamma
-#pragma unroll 8
-        for (int u = 0; u < TR_TPB; ++u) a += tvec(u)[CB_GYX1 + e - CG_G1];
-      } else if (e < CG_W2) {                // LN1 beta
-#pragma unroll 8
-        for (int u = 0; u < TR_TPB; ++u) a += tvec(u)[CB_GY1 + e - CG_BE1];
-      } else if (e < CG_G2) {                // b2
-#pragma unroll 8
-        for (int u = 0; u < TR_TPB; ++u) a += tvec(u)[CB_GA2 + e - CG_B2];
-      } else if (e < CG_BE2) {               // LN2 gamma
-#pragma unroll 8
-        for (int u = 0; u < TR_TPB; ++u) a += tvec(u)[CB_GYX2 + e - CG_G2];
-      } else if (e < CG_W3) {                // LN2 beta
-#pragma unroll 8
-        for (int u = 0; u < TR_TPB; ++u) a += tvec(u)[CB_GY2 + e - CG_BE2];
-      } else if (e < CG_B3) {                // W3: ga3 * r2
-#pragma unroll 8
-        for (int u = 0; u < TR_TPB; ++u) a = fmaf(tvec(u)[CB_GA3], tvec(u)[CB_R2 + e - CG_W3], a);
-      } else {                               // b3
-#pragma unroll 8
-        for (int u = 0; u < TR_TPB; ++u) a += tvec(u)[CB_GA3];
+      for (int u = 0; u < TR_TPB; ++u) {
+        const float* w = tvec(u);
+        const float bv = w[obc];
+        a = fmaf(w[oa], ob >= 0 ? bv : 1.0f, a);
       }
       gp[e] = a;
     }
@@ -1308,6 +1302,7 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
     wsm[tid] = tid < SG_B1 ? A.P.w1[tid] : tid < SG_W2 ? A.P.b1[tid - SG_B1]
                                      : tid < SG_B2 ? A.P.w2[tid - SG_W2] : A.P.b2[tid - SG_B2];
   }
+  if (tid == SM_TH - 1) red[63] = 1.0f;   // the constant operand of the bias partials
   if (A.stage) {
     smask_copy_plane(stg, am, H * W, tid);
     __syncthreads();
@@ -1617,32 +1612,45 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
   TSTAMP(39);
   // ---- parameter partials of this image: thread (chunk c, element e) sums
   // e's terms over the tiles of chunk c in tile order; the SM_PCH chunk sums
-  // of each element are then added in chunk order (deterministic)
+  // of each element are then added in chunk order (deterministic).  Every
+  // element's term is one FMA a(t) b(t) (+ s): W1 gpre(t, oc) f(neighbour),
+  // b1 gpre(t, oc) x 1, W2 (+-gl(t)) rel(t, ic), b2 (+-gl(t)) x 1 - exactly
+  // the sums / FMAs of the per-type loops, as one branch-free loop (a wave
+  // holds several element types; per-type loops ran one after another)
   static_assert(SM_PCH * SG_SIZE <= SM_TH, "soft-mask partial chunks exceed the workgroup");
   float* gp = A.gpart + (size_t)b * SG_SIZE;
   if (tid < SM_PCH * SG_SIZE) {
     const int c = tid / SG_SIZE, e = tid - c * SG_SIZE;
     const int t0 = (c * NT) / SM_PCH, t1 = ((c + 1) * NT) / SM_PCH;
-    float s = 0.0f;
-    if (e < SG_B1) {                  // W1[oc][ic][qq]
+    const bool w1 = e < SG_B1;
+    // a(t) = sa * pa[t * da]; b(t) = pb[t * db] (W1: a neighbour tap of f0 / f1,
+    // masked outside the tile grid; b1 / b2: the constant 1 in red[63])
+    const float* pa; const float* pb;
+    int da, db, di = 0, dj = 0;
+    float sa = 1.0f;
+    if (w1) {
       const int oc = e / 18, ic = (e / 9) & 1, qq = e % 9;
-      const int di = qq / 3 - 1, dj = qq % 3 - 1;
-      const float* f = ic == 0 ? f0 : f1;
-      int i = (int)(((float)t0 + 0.5f) * rwt), j = t0 - i * wt;   // walked forward with t
-      for (int t = t0; t < t1; ++t) {
-        const int ii = i + di, jj = j + dj;
-        if (ii >= 0 && ii < ht && jj >= 0 && jj < wt) s = fmaf(gpre[t * 8 + oc], f[ii * wt + jj], s);
-        if (++j == wt) { j = 0; ++i; }
-      }
-    } else if (e < SG_W2) {           // b1
-      const int oc = e - SG_B1;
-      for (int t = t0; t < t1; ++t) s += gpre[t * 8 + oc];
-    } else if (e < SG_B2) {           // W2[o][ic]: g_l(o) relu_ic, g_l1 = -g_l0
+      di = qq / 3 - 1; dj = qq % 3 - 1;
+      pa = gpre + oc; da = 8;
+      pb = (ic == 0 ? f0 : f1) + di * wt + dj; db = 1;
+    } else if (e < SG_W2) {
+      pa = gpre + (e - SG_B1); da = 8; pb = red + 63; db = 0;
+    } else if (e < SG_B2) {
       const int o = (e - SG_W2) >> 3, ic = (e - SG_W2) & 7;
-      for (int t = t0; t < t1; ++t) s = fmaf(o == 0 ? gl[t] : -gl[t], rel[t * 8 + ic], s);
-    } else {                          // b2
-      const int o = e - SG_B2;
-      for (int t = t0; t < t1; ++t) s += o == 0 ? gl[t] : -gl[t];
+      pa = gl; da = 1; sa = o == 0 ? 1.0f : -1.0f; pb = rel + ic; db = 8;
+    } else {
+      pa = gl; da = 1; sa = e == SG_B2 ? 1.0f : -1.0f; pb = red + 63; db = 0;
+    }
+    int i = (int)(((float)t0 + 0.5f) * rwt), j = t0 - i * wt;   // walked forward with t
+    float s = 0.0f;
+#pragma unroll 4
+    for (int t = t0; t < t1; ++t) {
+      const bool ok = !w1 || (i + di >= 0 && i + di < ht && j + dj >= 0 && j + dj < wt);
+      const float av = sa * pa[t * da];
+      const float bv = ok ? pb[t * db] : 0.0f;
+      const float v = fmaf(av, bv, s);
+      s = ok ? v : s;
+      if (++j == wt) { j = 0; ++i; }
     }
     psc[tid] = s;
   }

@@ -170,3 +170,43 @@ def test_bit_budget_values():
     assert abs(float(lb) - (float(ref) - 4.0) ** 2) <= 1e-5 * max((float(ref) - 4.0) ** 2, 1e-6)
     lb5 = h.bit_budget_loss(aux, 5.0)          # another target: torch ops on the fused avg
     assert abs(float(lb5) - (float(avg) - 5.0) ** 2) <= 1e-6
+
+
+@pytest.mark.parametrize("frozen_head", [False, True])
+def test_fused_soft_mask_grad_sinks(frozen_head):
+    """The soft masks' parameter gradients go straight into per-net gradient
+    sinks, reduced as extra workgroups of the mapper's first backward launch
+    (frozen_head: analyzer and mapper frozen, so no mapper backward runs and
+    the engine callback at the end of backward launches the reduction).
+    Against the same step with the gradients returned through autograd
+    (core.DIRECT_GRAD_ACCUM off), bit for bit, over two backwards without
+    zero_grad (the sinks' accumulate path)."""
+    from mcaq_yolo_amd import core, train_step
+    assert train_step.FUSED_MASK_QAT
+    feats, gens = _feats()
+    res = []
+    old = core.DIRECT_GRAD_ACCUM
+    for direct in (True, False):
+        core.DIRECT_GRAD_ACCUM = direct
+        try:
+            h = _hooks()
+            if frozen_head:
+                for p in list(h.complexity_analyzer.parameters()) + list(h.bit_mapper.parameters()):
+                    p.requires_grad_(False)
+            for _ in range(2):
+                for f in feats:
+                    f.grad = None
+                outs, aux = h.forward_features(feats, temperature=1.0)
+                loss = sum((o * g).sum() for o, g in zip(outs, gens)) + 0.1 * h.bit_budget_loss(aux, 4.0)
+                loss.backward()
+            torch.cuda.synchronize()
+            sm = {n: p.grad.clone() for n, p in h.named_parameters() if "soft_mask" in n}
+            assert len(sm) == 12 and all(g is not None for g in sm.values())
+            res.append((sm, [f.grad.clone() for f in feats]))
+        finally:
+            core.DIRECT_GRAD_ACCUM = old
+    (a, fa), (b, fb) = res
+    for n in a:
+        assert torch.equal(a[n], b[n]), n
+    for x, y in zip(fa, fb):
+        assert torch.equal(x, y)
