@@ -612,12 +612,24 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
       asp[i] = aS[(size_t)j * A.n + tc];
     }
   }
+  // ... and the BN(S-1) statistics and affine parameters of the wave's step-4
+  // columns (read after the W^T g_a loop, which did not hide their latency)
+  float smn[S >= 2 ? KI / MW : 1], srs[S >= 2 ? KI / MW : 1], sgm[S >= 2 ? KI / MW : 1], sbe[S >= 2 ? KI / MW : 1];
   if constexpr (S >= 2) {
     const float* ap = S == 4 ? W.a3 : (S == 3 ? W.a2 : W.a1);
 #pragma unroll
     for (int i = 0; i < KI / MW; ++i) {
       ap2[i] = ap[(size_t)(q + i * MW) * A.n + tc];
       ap4[i] = ap[(size_t)(q * (KI / MW) + i) * A.n + tc];
+    }
+    const float* g = S == 4 ? P.g3 : (S == 3 ? P.g2 : P.g1);
+    const float* be = S == 4 ? P.be3 : (S == 3 ? P.be2 : P.be1);
+    constexpr int Lp = S - 1;
+#pragma unroll
+    for (int f = 0; f < KI / MW; ++f) {
+      const int k = q * (KI / MW) + f;
+      smn[f] = W.stat[(Lp - 1) * 128 + k]; srs[f] = W.stat[(Lp - 1) * 128 + 64 + k];
+      sgm[f] = g[k]; sbe[f] = be[k];
     }
   }
   if constexpr (S == 3) TSTAMP(42);
@@ -743,24 +755,15 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
   if constexpr (S >= 2) {
     constexpr int NO = S == 4 ? 1 : MapL<S>::N;
     const float* w = S == 4 ? P.w4 : L.w;
-    const int Lp = S - 1;
     constexpr int NQ = K / MW;
+    static_assert(NQ == KI / MW, "step-4 columns");
     float gyv[NQ], xhv[NQ];
-    const float* g = S == 4 ? P.g3 : (S == 3 ? P.g2 : P.g1);
-    const float* be = S == 4 ? P.be3 : (S == 3 ? P.be2 : P.be1);
     // rows j outer, the wave's NQ consecutive columns inner: one NQ-wide
     // broadcast read of W (LDS, or scalar for the 32-float W4) per row
-    // instead of NQ strided ones (each output's sum still runs over j in order)
-    // the BN(S-1) statistics and affine parameters of the wave's columns
-    // first: in the store loop below each load would wait behind the
-    // previous column's g_y store (W.stat and W.gy share the work buffer)
-    float smn[NQ], srs[NQ], sgm[NQ], sbe[NQ];
-#pragma unroll
-    for (int f = 0; f < NQ; ++f) {
-      const int k = q * NQ + f;
-      smn[f] = W.stat[(Lp - 1) * 128 + k]; srs[f] = W.stat[(Lp - 1) * 128 + 64 + k];
-      sgm[f] = g[k]; sbe[f] = be[k];
-    }
+    // instead of NQ strided ones (each output's sum still runs over j in order);
+    // the BN(S-1) statistics / affine parameters (smn, srs, sgm, sbe) were
+    // loaded at the top (in the store loop each load would wait behind the
+    // previous column's g_y store: W.stat and W.gy share the work buffer)
     float accv[NQ];
 #pragma unroll
     for (int f = 0; f < NQ; ++f) accv[f] = 0.0f;
