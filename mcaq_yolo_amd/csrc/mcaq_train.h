@@ -646,7 +646,6 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
     // over the workgroups' partials, MW interleaved subsets in parallel
     constexpr int N = MapL<S>::N;
     const float* g = S == 1 ? P.g1 : (S == 2 ? P.g2 : P.g3);
-    const float* aS = S == 1 ? W.a1 : (S == 2 ? W.a2 : W.a3);
     {
       const int j = tid & 63, part = tid >> 6;
       if (j < N) {

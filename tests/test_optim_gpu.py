@@ -1,4 +1,4 @@
-"""optim.ClipAdamW (one launch: clip_grad_norm_ + AdamW + |W| projection,
+"""optim.ClipAdamW (two launches: clip_grad_norm_ + AdamW + |W| projection,
 train.py:626-641) against torch's own three steps - clip_grad_norm_(1.0),
 torch.optim.AdamW(fused), the mapper's enforce_weight_constraints - over
 several steps on the hook parameters with real QAT gradients.  fp32 sums in
@@ -146,3 +146,39 @@ def test_clip_adamw_step_reaches_packed_blobs():
     with torch.no_grad():
         _, aux0 = h0.forward_features([f.detach() for f in feats])
     assert not torch.equal(aux0[0]["complexity"], res[0][0])
+
+
+@pytest.mark.parametrize("sizes", [(97, 2048, 5), (97, 20000, 5, 3000)])
+def test_clip_adamw_chunked_lists_match_torch(sizes):
+    """Parameter lists of 3 and 24 1,024-element chunks (tensors spanning
+    chunk boundaries) against torch's clip_grad_norm_ + fused AdamW + abs,
+    over 4 steps with fresh gradients, and the device step counter."""
+    from mcaq_yolo_amd.optim import ClipAdamW
+    torch.manual_seed(11)
+    ps = [torch.randn(n, device="cuda", requires_grad=True) for n in sizes]
+    qs = [p.detach().clone().requires_grad_(True) for p in ps]
+    o0 = torch.optim.AdamW(ps, lr=1e-2, weight_decay=0.05, betas=(0.9, 0.999), fused=True)
+    o1 = ClipAdamW(qs, lr=1e-2, weight_decay=0.05, betas=(0.9, 0.999), max_norm=0.5, project_abs=[qs[1]])
+    for it in range(4):
+        gs = [torch.randn_like(p) for p in ps]
+        for p, q, g in zip(ps, qs, gs):
+            p.grad = g.clone()
+            q.grad = g.clone()
+        tn = torch.nn.utils.clip_grad_norm_(ps, 0.5)
+        o0.step()
+        with torch.no_grad():
+            ps[1].abs_()
+        o1.step()
+        torch.cuda.synchronize()
+        _close(o1.last_total_norm.reshape(()), tn, 1e-6, "total norm step %d" % it)
+        for k, (p, q) in enumerate(zip(ps, qs)):
+            _close(q.grad, p.grad, 1e-6, "clipped grad %d step %d" % (k, it))
+            _close(q, p, 1e-5, "param %d step %d" % (k, it))
+            _close(o1.state[q]["exp_avg"], o0.state[p]["exp_avg"], 1e-5, "exp_avg %d" % k)
+            _close(o1.state[q]["exp_avg_sq"], o0.state[p]["exp_avg_sq"], 1e-5, "exp_avg_sq %d" % k)
+        with torch.no_grad():
+            for p, q in zip(ps, qs):
+                q.copy_(p)
+                o1.state[q]["exp_avg"].copy_(o0.state[p]["exp_avg"])
+                o1.state[q]["exp_avg_sq"].copy_(o0.state[p]["exp_avg_sq"])
+    assert float(o1._step_t) == 4.0
