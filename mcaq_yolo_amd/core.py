@@ -981,7 +981,9 @@ class _GradSink:
         self.flat = None
         self.views = None
 
-    def target(self, params):
+    def _plan(self, params):
+        """1 (accumulate into the sink), 0 (fresh: .grad to become the
+        sink's views) or None (autograd); no .grad is touched."""
         if not DIRECT_GRAD_ACCUM or not all(p.requires_grad for p in params):
             return None
         if _grads_observed(params):
@@ -996,12 +998,29 @@ class _GradSink:
         mine = [p.grad is not None and p.grad.data_ptr() == v.data_ptr() and p.grad.shape == v.shape
                 for p, v in zip(params, self.views)]
         if all(mine):
-            return self.flat, 1
+            return 1
         if any(p.grad is not None for p in params):
             return None
-        for p, v in zip(params, self.views):
-            p.grad = v
-        return self.flat, 0
+        return 0
+
+    def _take(self, params, acc):
+        if acc == 0:
+            for p, v in zip(params, self.views):
+                p.grad = v
+        return self.flat, acc
+
+    def target(self, params):
+        acc = self._plan(params)
+        return None if acc is None else self._take(params, acc)
+
+    @staticmethod
+    def target_all(pairs):
+        """[(sink, params), ...] -> every sink's (flat, accumulate), or None
+        (and no .grad touched) when any of them must go through autograd."""
+        plans = [sk._plan(ps) for sk, ps in pairs]
+        if any(a is None for a in plans):
+            return None
+        return [sk._take(ps, a) for (sk, ps), a in zip(pairs, plans)]
 
 
 class _HeadTrainFn(torch.autograd.Function):

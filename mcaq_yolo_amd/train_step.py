@@ -689,8 +689,11 @@ class _MaskQuantMulti(torch.autograd.Function):
         # every net's gradients straight into its _GradSink (their .grad), the
         # reduction deferred to the mapper's backward launch; otherwise
         # reduced here and handed to autograd
-        sinks = [ctx.mods[i]._gsink.target(list(ctx.mods[i].net.parameters())) for i in range(n)]
-        if all(sk is not None for sk in sinks) and _PENDING_SM_REDUCE["segs"] is None:
+        sinks = None
+        if _PENDING_SM_REDUCE["segs"] is None:
+            sinks = core._GradSink.target_all([(ctx.mods[i]._gsink, list(ctx.mods[i].net.parameters()))
+                                               for i in range(n)])
+        if sinks is not None:
             for i, (gf, acc) in enumerate(sinks):
                 rsegs[i].out, rsegs[i].accumulate = _p(gf), acc
             _PENDING_SM_REDUCE["segs"] = (rsegs, n, keep)
