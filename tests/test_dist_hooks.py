@@ -1,4 +1,4 @@
-"""Value-level test of the batch-sharded hook path: two ranks,
+"""Value-level test of the batch-sharded hook path: two (and four) ranks,
 each running `dist.shard_hooks(MCAQHooks(...))` on its half of a batch, must
 give exactly the bits, complexity and quantized y of ONE process running the
 whole batch (and of the oracle on the whole batch).
@@ -114,23 +114,23 @@ def _entry(rank, world, port, dev, q):
         dist.destroy_process_group()
 
 
-def _sharded(dev):
+def _sharded(dev, world=WORLD):
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_entry, args=(r, WORLD, port, dev, q)) for r in range(WORLD)]
+    ps = [ctx.Process(target=_entry, args=(r, world, port, dev, q)) for r in range(world)]
     for p in ps:
         p.start()
-    res = dict(q.get(timeout=240) for _ in range(WORLD))
+    res = dict(q.get(timeout=240) for _ in range(world))
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
     return res
 
 
-def _check(res, full):
-    B = SHAPES[0][0] // WORLD
-    for r in range(WORLD):
+def _check(res, full, world=WORLD):
+    B = SHAPES[0][0] // world
+    for r in range(world):
         sl = slice(r * B, (r + 1) * B)
         for s, ((y, bits, c), (fy, fbits, fc)) in enumerate(zip(res[r], full)):
             assert np.array_equal(bits, fbits[sl]), (r, s)
@@ -151,9 +151,10 @@ def test_fractal_order_depends_on_global_position():
     assert not np.array_equal(loc, g)
 
 
-def test_sharded_hooks_cpu_equal_single_process():
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_hooks_cpu_equal_single_process(world):
     full = _run_hooks(_hooks("cpu"), _feats(), "cpu")
-    _check(_sharded("cpu"), full)
+    _check(_sharded("cpu", world), full, world)
 
 
 @pytest.mark.gpu
@@ -170,3 +171,11 @@ def test_sharded_hooks_gpu_equal_single_process_and_oracle():
         assert np.array_equal(bits, ref["bits"]) and np.array_equal(y, ref["y"])
         assert np.array_equal(bits, cbits) and np.array_equal(y, cy)
     _check(_sharded("cuda:0"), full)
+
+
+@pytest.mark.gpu
+def test_sharded_hooks_gpu_four_ranks():
+    """Four ranks (one image each) on the one GPU (gloo): the statistics
+    exchange and the global fractal column order at world size 4."""
+    full = _run_hooks(_hooks("cuda:0"), _feats(), "cuda:0")
+    _check(_sharded("cuda:0", 4), full, 4)
