@@ -48,7 +48,13 @@ def main():
                              "launches": max(len(fetch.get(name, [])), len(write.get(name, [])))}
         if k.startswith("mcaq_"):
             step += f + w
-    out["step_total"] = round(step)
+    # per-launch sums of the hook kernels = one launch set of `batches`
+    # batches (bench.py --launch-batches, the default 2 since round 5);
+    # step_total is per batch, as the bench's step
+    nb = int(os.environ.get("MCAQ_PMC_BATCHES", "1"))
+    out["batches_per_launch"] = nb
+    out["launch_total"] = round(step)
+    out["step_total"] = round(step / nb)
     print(json.dumps(out, indent=1))
 
 
