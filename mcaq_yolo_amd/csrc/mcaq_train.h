@@ -602,7 +602,7 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
   constexpr int N1 = S == 4 ? 1 : MapL<S == 4 ? 1 : S>::N;
   constexpr int KI = S == 4 ? 32 : (S == 1 ? 3 : MapL<S>::K);
   float gyp[S <= 3 ? N1 / MW : 1], asp[S <= 3 ? N1 / MW : 1];
-  float ap2[S >= 2 ? KI / MW : 1], ap4[S >= 2 ? KI / MW : 1];
+  float ap2[S >= 2 ? KI / MW : 1], ap4[S >= 2 ? KI / MW : 1];   // ap4: SQ x SR values (below)
   if constexpr (S <= 3) {
     const float* aS = S == 1 ? W.a1 : (S == 2 ? W.a2 : W.a3);
 #pragma unroll
@@ -612,22 +612,31 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
       asp[i] = aS[(size_t)j * A.n + tc];
     }
   }
-  // ... and the BN(S-1) statistics and affine parameters of the wave's step-4
-  // columns (read after the W^T g_a loop, which did not hide their latency)
-  float smn[S >= 2 ? KI / MW : 1], srs[S >= 2 ? KI / MW : 1], sgm[S >= 2 ? KI / MW : 1], sbe[S >= 2 ? KI / MW : 1];
+  // ... and the BN(S-1) statistics and affine parameters of the step-4
+  // columns with that step's a(S-1) values (read after the W^T g_a loop, which
+  // did not hide their latency).  Stages 3 / 2 run step 4 on MFMA: wave q
+  // owns tile block q & 3 (16 tiles) and column blocks (q >> 2) + 2 i of
+  // g_h; a lane holds 4 tiles (rows 4 lk + r) of column 16 kb + lr
+  constexpr bool kMF = S == 2 || S == 3;
+  constexpr int SQ = kMF ? (KI / 16) / 2 : (KI / MW > 0 ? KI / MW : 1);   // step-4 column sets of this lane
+  constexpr int SR = kMF ? 4 : 1;                     // tiles per column set
+  const int lr = lane & 15, lk = lane >> 4, mtb = q & 3;
+  float smn[SQ], srs[SQ], sgm[SQ], sbe[SQ];
   if constexpr (S >= 2) {
     const float* ap = S == 4 ? W.a3 : (S == 3 ? W.a2 : W.a1);
 #pragma unroll
-    for (int i = 0; i < KI / MW; ++i) {
-      ap2[i] = ap[(size_t)(q + i * MW) * A.n + tc];
-      ap4[i] = ap[(size_t)(q * (KI / MW) + i) * A.n + tc];
-    }
+    for (int i = 0; i < KI / MW; ++i) ap2[i] = ap[(size_t)(q + i * MW) * A.n + tc];
     const float* g = S == 4 ? P.g3 : (S == 3 ? P.g2 : P.g1);
     const float* be = S == 4 ? P.be3 : (S == 3 ? P.be2 : P.be1);
     constexpr int Lp = S - 1;
 #pragma unroll
-    for (int f = 0; f < KI / MW; ++f) {
-      const int k = q * (KI / MW) + f;
+    for (int f = 0; f < SQ; ++f) {
+      const int k = kMF ? ((q >> 2) + 2 * f) * 16 + lr : q * SQ + f;
+#pragma unroll
+      for (int r = 0; r < SR; ++r) {
+        const int tt = kMF ? imin_(wgi * TR_TPB + mtb * 16 + 4 * lk + r, A.n - 1) : tc;
+        ap4[f * SR + r] = ap[(size_t)k * A.n + tt];
+      }
       smn[f] = W.stat[(Lp - 1) * 128 + k]; srs[f] = W.stat[(Lp - 1) * 128 + 64 + k];
       sgm[f] = g[k]; sbe[f] = be[k];
     }
@@ -751,11 +760,48 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
   }
   if constexpr (S == 3) TSTAMP(45);
   // ---- 4. gradient of the layer input: g_h = W^T g_a, through ReLU / BN(S-1)
-  if constexpr (S >= 2) {
+  if constexpr (kMF) {
+    // g_h (64 tiles x K) = g_a (64 x N) W (N x K) as 16 x 16 blocks on
+    // v_mfma_f32_16x16x4_f32 (j in steps of 4 from 0), then per element
+    // through ReLU / BN(S-1) as the scalar path below; the BN(S-1) partial
+    // sums over the tiles: a lane's 4 tiles in order, the 4 lanes of a column
+    // (xor 16, xor 32), the 4 tile blocks in order
+    constexpr int NO = MapL<S>::N;
+    static_assert(SQ * SR <= KI / MW, "step-4 operands");
+    float* red4 = s_tmp;                 // [2][4 tile blocks][64]
+#pragma unroll
+    for (int f = 0; f < SQ; ++f) {
+      const int kb = (q >> 2) + 2 * f, k = kb * 16 + lr;
+      tr_f4 d = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int st = 0; st < NO / 4; ++st)
+        d = tr_mfma4(s_g[mtb * 16 + lr][4 * st + lk], L.w[(4 * st + lk) * K + k], d);
+      float s1 = 0.0f, s2 = 0.0f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int tg = wgi * TR_TPB + mtb * 16 + 4 * lk + r;
+        const float xh = (ap4[f * SR + r] - smn[f]) * srs[f];
+        const float y = sgm[f] * xh + sbe[f];
+        const float gy = (tg < A.n && y > 0.0f) ? d[r] : 0.0f;
+        if (tg < A.n) W.gy[(size_t)k * A.n + tg] = gy;
+        s1 += gy; s2 += gy * xh;
+      }
+      s1 += __shfl_xor(s1, 16, 64); s2 += __shfl_xor(s2, 16, 64);
+      s1 += __shfl_xor(s1, 32, 64); s2 += __shfl_xor(s2, 32, 64);
+      if (lk == 0) { red4[mtb * 64 + k] = s1; red4[256 + mtb * 64 + k] = s2; }
+    }
+    if constexpr (S == 3) TSTAMP(48);
+    __syncthreads();
+    if constexpr (S == 3) TSTAMP(46);
+    if (tid < K) {
+      bp[tid] = ((red4[tid] + red4[64 + tid]) + red4[128 + tid]) + red4[192 + tid];
+      bp[64 + tid] = ((red4[256 + tid] + red4[320 + tid]) + red4[384 + tid]) + red4[448 + tid];
+    }
+  } else if constexpr (S >= 2) {
     constexpr int NO = S == 4 ? 1 : MapL<S>::N;
     const float* w = S == 4 ? P.w4 : L.w;
     constexpr int NQ = K / MW;
-    static_assert(NQ == KI / MW, "step-4 columns");
+    static_assert(NQ == KI / MW && NQ == SQ, "step-4 columns");
     float gyv[NQ], xhv[NQ];
     // rows j outer, the wave's NQ consecutive columns inner: one NQ-wide
     // broadcast read of W (LDS, or scalar for the 32-float W4) per row
@@ -772,6 +818,7 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
 #pragma unroll
       for (int f = 0; f < NQ; ++f) accv[f] = fmaf(w[j * K + q * NQ + f], ga, accv[f]);
     }
+    if constexpr (S == 3) TSTAMP(48);
 #pragma unroll
     for (int f = 0; f < NQ; ++f) {
       const int k = q * NQ + f;

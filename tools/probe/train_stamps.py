@@ -26,7 +26,7 @@ STAGES = [(32, 33, "stage |x| plane + ranges"), (33, 34, "pool |x| per tile + am
 
 
 MAPPER_BWD = [(56, 42, "operand loads issued + BN sums"), (42, 43, "g_a(S) (BN backward)"),
-              (43, 44, "h(S-1) recompute"), (44, 45, "weight / bias partials"), (45, 46, "W^T g_a, g_y stores"),
+              (43, 44, "h(S-1) recompute"), (44, 45, "weight / bias partials"), (45, 48, "W^T g_a (FMA)"), (48, 46, "g_y stores"),
               (46, 47, "BN(S-1) partial sums")]
 BILAT = [(57, 58, "range x spatial weights (exp)"), (58, 59, "per tile: C, g / D, centre"),
          (59, 60, "adjoint gather")]
