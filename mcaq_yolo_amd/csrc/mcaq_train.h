@@ -454,7 +454,65 @@ __device__ __forceinline__ void mapper_fwd_stage(const MapperTrainArgs& A, MapFw
     __syncthreads();
   }
   if constexpr (S == 2) TSTAMP(53);
-  if constexpr (S <= 3) {
+  if constexpr (S == 2 || S == 3) {
+    // the layer (64 tiles x N) = h (64 x K) W^T (K x N) + b as 16 x 16 blocks
+    // on v_mfma_f32_16x16x4_f32 (k in steps of 4, the bias as the initial
+    // accumulator): wave q owns tile block q & 3 and feature blocks
+    // (q >> 2) + 2 i; a lane holds 4 tiles (rows 4 lk + r) of feature 16 fb + lr.
+    // The workgroup moments: sums over a lane's 4 tiles in order, the column's
+    // 4 lanes (xor 16, xor 32), the 4 tile blocks in order - mean, then M2
+    constexpr int K = MapL<S>::K, N = MapL<S>::N, FPW = (N / 16) / 2;
+    const int lr = lane & 15, lk = lane >> 4, mtb = q & 3;
+    const float* bb = S == 2 ? P.b2 : P.b3;
+    float* aout = S == 2 ? W.a2 : W.a3;
+    float* red1 = s_tmp;                 // [4 tile blocks][64] sums
+    float* red2 = s_tmp + 256;           //   ... squared deviations
+    float bq[FPW];
+#pragma unroll
+    for (int i = 0; i < FPW; ++i) bq[i] = bb[((q >> 2) + 2 * i) * 16 + lr];
+    tr_f4 d[FPW];
+#pragma unroll
+    for (int i = 0; i < FPW; ++i) {
+      const int f = ((q >> 2) + 2 * i) * 16 + lr;
+      d[i] = tr_f4{bq[i], bq[i], bq[i], bq[i]};
+#pragma unroll
+      for (int st = 0; st < K / 4; ++st) d[i] = tr_mfma4(s_in[mtb * 16 + lr][4 * st + lk], L.w[f * K + 4 * st + lk], d[i]);
+      float sm = 0.0f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int tg = wgi * TR_TPB + mtb * 16 + 4 * lk + r;
+        if (tg < A.n) { aout[(size_t)f * A.n + tg] = d[i][r]; sm += d[i][r]; }
+      }
+      sm += __shfl_xor(sm, 16, 64);
+      sm += __shfl_xor(sm, 32, 64);
+      if (lk == 0) red1[mtb * 64 + f] = sm;
+    }
+    if constexpr (S == 2) TSTAMP(54);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < FPW; ++i) {
+      const int f = ((q >> 2) + 2 * i) * 16 + lr;
+      const float mean = (((red1[f] + red1[64 + f]) + red1[128 + f]) + red1[192 + f]) / nvalid;
+      float s2 = 0.0f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int tg = wgi * TR_TPB + mtb * 16 + 4 * lk + r;
+        const float dv = tg < A.n ? d[i][r] - mean : 0.0f;
+        s2 += dv * dv;
+      }
+      s2 += __shfl_xor(s2, 16, 64);
+      s2 += __shfl_xor(s2, 32, 64);
+      if (lk == 0) red2[mtb * 64 + f] = s2;
+    }
+    __syncthreads();
+    if (tid < N) {
+      float* part = W.fpart(S) + (size_t)wgi * 128;
+      part[tid] = (((red1[tid] + red1[64 + tid]) + red1[128 + tid]) + red1[192 + tid]) / nvalid;
+      part[N + tid] = ((red2[tid] + red2[64 + tid]) + red2[128 + tid]) + red2[192 + tid];
+    }
+    if (tid == 0) W.cnt[wgi] = nvalid;
+    if constexpr (S == 2) TSTAMP(55);
+  } else if constexpr (S <= 3) {
     constexpr int K = MapL<S>::K, N = MapL<S>::N, NQ = N / MW;
     const float* w = S == 1 ? P.w1 : L.w;
     const float* bb = S == 1 ? P.b1 : (S == 2 ? P.b2 : P.b3);
