@@ -386,7 +386,7 @@ struct MapFwdLds {
   float in[TR_TPB][65];     // this workgroup's tiles' layer inputs
   float mean[64], rstd[64];
   float tmp[MW * 192];
-  float w[64 * 32];         // stages 2 / 3: the layer's weights (read as broadcast LDS vectors)
+  float w[64 * 34];         // stages 2 / 3: the layer's weights W[f][k] at f * (K + 2) + k (conflict-free MFMA B reads)
 };
 
 template <int S>
@@ -448,8 +448,14 @@ __device__ __forceinline__ void mapper_fwd_stage(const MapperTrainArgs& A, MapFw
       s_in[lane][k] = y > 0.0f ? y : 0.0f;
     }
     if constexpr (kWL) {
+      // rows padded to K + 2 floats: the MFMA B reads (16 rows x 2 columns a
+      // half-wave) hit 32 different banks
+      constexpr int KL = MapL<S>::K;
 #pragma unroll
-      for (int i = 0; i < WN / MTH; ++i) L.w[tid + i * MTH] = wst[i];
+      for (int i = 0; i < WN / MTH; ++i) {
+        const int e = tid + i * MTH;
+        L.w[(e / KL) * (KL + 2) + (e % KL)] = wst[i];
+      }
     }
     __syncthreads();
   }
@@ -476,7 +482,7 @@ __device__ __forceinline__ void mapper_fwd_stage(const MapperTrainArgs& A, MapFw
       const int f = ((q >> 2) + 2 * i) * 16 + lr;
       d[i] = tr_f4{bq[i], bq[i], bq[i], bq[i]};
 #pragma unroll
-      for (int st = 0; st < K / 4; ++st) d[i] = tr_mfma4(s_in[mtb * 16 + lr][4 * st + lk], L.w[f * K + 4 * st + lk], d[i]);
+      for (int st = 0; st < K / 4; ++st) d[i] = tr_mfma4(s_in[mtb * 16 + lr][4 * st + lk], L.w[f * (K + 2) + 4 * st + lk], d[i]);
       float sm = 0.0f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -622,7 +628,7 @@ struct MapBwdLds {
   float g[TR_TPB][65];     // gradient of this layer's pre-activation a(S)
   float mean[64], rstd[64], sg[64], sgx[64];
   float tmp[MW * 128];
-  float w[64 * 32];        // stages 3 / 2: the layer's weights for W^T g_a
+  float w[64 * 48];        // stages 3 / 2: the layer's weights W[j][k] at j * (K + 16) + k, for W^T g_a
 };
 
 template <int S>
@@ -724,8 +730,14 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
       }
     }
     if constexpr (kWL) {
+      // rows padded to K + 16 floats: the MFMA B reads (2 rows x 16 columns a
+      // half-wave) hit 32 different banks
+      constexpr int KL = MapL<S>::K;
 #pragma unroll
-      for (int i = 0; i < WN / MTH; ++i) L.w[tid + i * MTH] = wst[i];
+      for (int i = 0; i < WN / MTH; ++i) {
+        const int e = tid + i * MTH;
+        L.w[(e / KL) * (KL + 16) + (e % KL)] = wst[i];
+      }
     }
     __syncthreads();
     if (tid < N) {
@@ -833,7 +845,7 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
       tr_f4 d = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
       for (int st = 0; st < NO / 4; ++st)
-        d = tr_mfma4(s_g[mtb * 16 + lr][4 * st + lk], L.w[(4 * st + lk) * K + k], d);
+        d = tr_mfma4(s_g[mtb * 16 + lr][4 * st + lk], L.w[(4 * st + lk) * (K + 16) + k], d);
       float s1 = 0.0f, s2 = 0.0f;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
