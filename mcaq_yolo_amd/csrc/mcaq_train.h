@@ -1371,6 +1371,22 @@ inline bool smask_stage_ok(const float* absmean, const float* gm, int H, int W, 
 constexpr int SM_TH = 1024;   // threads per soft-mask backward workgroup (one image)
 
 
+// s + r[a] + ... + r[b - 1] in order, for 16-byte rows (r + a 16-byte
+// aligned, b - a a multiple of 4): float4 LDS reads, two in flight.  The
+// scalar reads of a tile row hit 4 banks across a wave (tile origins are
+// multiples of 8 floats, every lane at the same column offset: 16-way
+// conflicts); a float4 read per lane spreads them
+__device__ __forceinline__ float smask_row_sum4(const float* r, int a, int b, float s) {
+  const float4* r4 = reinterpret_cast<const float4*>(r + a);
+  const int n4 = (b - a) >> 2;
+  for (int c = 0; c < n4; c += 2) {
+    const float4 x = r4[c], y = r4[imin_(c + 1, n4 - 1)];
+    s = s + x.x; s = s + x.y; s = s + x.z; s = s + x.w;
+    if (c + 1 < n4) { s = s + y.x; s = s + y.y; s = s + y.z; s = s + y.w; }
+  }
+  return s;
+}
+
 // an [n] fp32 plane (16-byte aligned, n % 4 == 0 when staged) into LDS: two
 // 16-byte groups per thread per round, both loads issued before either store
 __device__ __forceinline__ void smask_copy_plane(float* dst, const float* src, int n, int tid) {
@@ -1459,14 +1475,18 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
     // h-major, w ascending (adaptive_avg_pool2d's order), each row's values
     // loaded 8 at a time before they are added (clamped index)
     float s = 0.0f;
-    for (int h = ha; h < hb; ++h) {
-      const float* r = am + h * W;
-      for (int w0 = wa; w0 < wb; w0 += 8) {
-        float v[8];
+    if (A.stage && ((W | wa | (wb - wa)) & 3) == 0) {
+      for (int h = ha; h < hb; ++h) s = smask_row_sum4(am + h * W, wa, wb, s);
+    } else {
+      for (int h = ha; h < hb; ++h) {
+        const float* r = am + h * W;
+        for (int w0 = wa; w0 < wb; w0 += 8) {
+          float v[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = r[imin_(w0 + k, wb - 1)];
+          for (int k = 0; k < 8; ++k) v[k] = r[imin_(w0 + k, wb - 1)];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) s = w0 + k < wb ? s + v[k] : s;
+          for (int k = 0; k < 8; ++k) s = w0 + k < wb ? s + v[k] : s;
+        }
       }
     }
     const float a = (s / (float)(hb - ha)) / (float)(wb - wa);
@@ -1643,6 +1663,10 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
       const int h = it / wt, j = it - h * wt;
       const float* r = gq + h * W;
       const int q1 = whi[j];
+      if (((W | wlo[j] | (q1 + 1 - wlo[j])) & 3) == 0) {
+        part[it] = smask_row_sum4(r, wlo[j], q1 + 1, 0.0f);
+        continue;
+      }
       float acc = 0.0f;
       for (int q0 = wlo[j]; q0 <= q1; q0 += 8) {
         float v[8];
