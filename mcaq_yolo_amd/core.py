@@ -928,7 +928,7 @@ def _head_bwd_fits(ht, wt):
 def _smask_bwd_fits(H, W, ht, wt):
     """mcaq_smask_train_backward: one image's m(p) gradient plus tile and
     row tables."""
-    return (20 * ht * wt + 64 + 1024 + 176 + H * wt + H * W) * 4 + 2 * (ht + wt) * 4 <= _TRAIN_LDS_LIMIT
+    return (22 * ht * wt + 64 + 1024 + 176 + H * wt + H * W) * 4 + 2 * (ht + wt) * 4 <= _TRAIN_LDS_LIMIT
 
 
 def _tile_grid(H, W, grid_size):

@@ -1354,9 +1354,10 @@ struct MaskTrainArgs {
 // LDS bytes of the soft-mask backward of one (H, W, ht, wt) image; stage: + the
 // staging plane (16-byte aligned)
 constexpr int SM_PCH = 6;      // tile chunks of the parameter partials (SM_PCH x SG_SIZE <= threads)
+constexpr int SM_HS = 9;       // LDS floats per tile of the 8-wide hidden-layer rows
 constexpr int SM_WS = 176;     // LDS floats of the staged soft-mask parameters
 inline size_t smask_lds_bytes(int H, int W, int ht, int wt, bool stage, bool fold = false) {
-  const size_t base = ((size_t)20 * ht * wt + 64 + 1024 + SM_WS + (size_t)H * wt + (size_t)H * W) * sizeof(float) +
+  const size_t base = ((size_t)(4 + 2 * SM_HS) * ht * wt + 64 + 1024 + SM_WS + (size_t)H * wt + (size_t)H * W) * sizeof(float) +
                       (size_t)2 * (ht + wt) * sizeof(int);
   const size_t st = stage ? ((base / 4 + 3) & ~(size_t)3) * 4 + (size_t)H * W * sizeof(float) : base;
   // fold mode: + the grad_bits pixel plane [H][W], band-column sums [ht][W], per-tile sums [NT]
@@ -1408,9 +1409,11 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
   float* f0 = smem_tr;               // bits feature, clamp((b - 2) / 6, 0, 1)
   float* f1 = f0 + NT;               // activation feature
   float* gl = f1 + NT;               // per tile: gradient of logit 0 (logit 1 gets -gl)
+  // per-tile rows of 8 at a stride of SM_HS = 9 floats: a wave's per-tile
+  // reads of one hidden unit then hit 32 banks (at stride 8 they hit 4)
   float* gpre = gl + NT;             // per tile x 8: gradient of the hidden pre-activation
-  float* rel = gpre + 8 * NT;        // per tile x 8: relu(hidden)
-  float* red = rel + 8 * NT;         // 64 reduction slots
+  float* rel = gpre + SM_HS * NT;    // per tile x 8: relu(hidden)
+  float* red = rel + SM_HS * NT;     // 64 reduction slots
   float* gmt = red + 64;             // per tile: gradient of m(tile)
   float* psc = gmt + NT;             // [SM_PCH][SG_SIZE] parameter partials of tile chunks
   float* wsm = psc + SM_TH;          // the soft-mask net's parameters (SG_SIZE floats, padded)
@@ -1710,16 +1713,16 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
       acc = fmaf(wsm[(oc * 2 + 0) * 9 + qq], f0[s], acc);
       acc = fmaf(wsm[(oc * 2 + 1) * 9 + qq], f1[s], acc);
     }
-    gpre[u] = acc;                    // the pre-activation until its gradient replaces it
-    rel[u] = acc > 0.0f ? acc : 0.0f;
+    gpre[t * SM_HS + oc] = acc;       // the pre-activation until its gradient replaces it
+    rel[t * SM_HS + oc] = acc > 0.0f ? acc : 0.0f;
   }
   __syncthreads();
   for (int t = tid; t < NT; t += SM_TH) {
     float l0 = wsm[SG_B2], l1 = wsm[SG_B2 + 1];
 #pragma unroll
     for (int ic = 0; ic < 8; ++ic) {
-      l0 = fmaf(wsm[SG_W2 + ic], rel[t * 8 + ic], l0);
-      l1 = fmaf(wsm[SG_W2 + 8 + ic], rel[t * 8 + ic], l1);
+      l0 = fmaf(wsm[SG_W2 + ic], rel[t * SM_HS + ic], l0);
+      l1 = fmaf(wsm[SG_W2 + 8 + ic], rel[t * SM_HS + ic], l1);
     }
     const float mt = 1.0f / (1.0f + expf(l1 - l0));
     // softmax (2 classes): d m / d l0 = m (1 - m) = -d m / d l1
@@ -1728,7 +1731,7 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
 #pragma unroll
     for (int ic = 0; ic < 8; ++ic) {
       const float gr = wsm[SG_W2 + ic] * g0 - wsm[SG_W2 + 8 + ic] * g0;
-      gpre[t * 8 + ic] = gpre[t * 8 + ic] > 0.0f ? gr : 0.0f;
+      gpre[t * SM_HS + ic] = gpre[t * SM_HS + ic] > 0.0f ? gr : 0.0f;
     }
   }
   __syncthreads();
@@ -1744,7 +1747,7 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
       if (ti < 0 || ti >= ht || tj < 0 || tj >= wt) continue;
       const int t = ti * wt + tj;
 #pragma unroll
-      for (int oc = 0; oc < 8; ++oc) s = fmaf(wsm[(oc * 2 + 0) * 9 + qq], gpre[t * 8 + oc], s);
+      for (int oc = 0; oc < 8; ++oc) s = fmaf(wsm[(oc * 2 + 0) * 9 + qq], gpre[t * SM_HS + oc], s);
     }
     const float bv = A.bits[(size_t)b * NT + u];
     const float f = (bv - 2.0f) / 6.0f;
@@ -1774,13 +1777,13 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
     if (w1) {
       const int oc = e / 18, ic = (e / 9) & 1, qq = e % 9;
       di = qq / 3 - 1; dj = qq % 3 - 1;
-      pa = gpre + oc; da = 8;
+      pa = gpre + oc; da = SM_HS;
       pb = (ic == 0 ? f0 : f1) + di * wt + dj; db = 1;
     } else if (e < SG_W2) {
-      pa = gpre + (e - SG_B1); da = 8; pb = red + 63; db = 0;
+      pa = gpre + (e - SG_B1); da = SM_HS; pb = red + 63; db = 0;
     } else if (e < SG_B2) {
       const int o = (e - SG_W2) >> 3, ic = (e - SG_W2) & 7;
-      pa = gl; da = 1; sa = o == 0 ? 1.0f : -1.0f; pb = rel + ic; db = 8;
+      pa = gl; da = 1; sa = o == 0 ? 1.0f : -1.0f; pb = rel + ic; db = SM_HS;
     } else {
       pa = gl; da = 1; sa = e == SG_B2 ? 1.0f : -1.0f; pb = red + 63; db = 0;
     }
