@@ -1587,7 +1587,10 @@ __device__ __forceinline__ void mcaq_smask_bwd_body(const MaskTrainArgs& A) {
     for (int t = tid; t < NT; t += SM_TH) {
       const int i = t / wt, j = t - i * wt;
       float g = 0.0f;
-      for (int w = wlo[j]; w <= whi[j]; ++w) g += fcol[i * W + w];
+      if ((((H * W) | W | wlo[j] | (whi[j] + 1 - wlo[j])) & 3) == 0)
+        g = smask_row_sum4(fcol + i * W, wlo[j], whi[j] + 1, 0.0f);   // 16-byte rows
+      else
+        for (int w = wlo[j]; w <= whi[j]; ++w) g += fcol[i * W + w];
       fgb[t] = has_c ? c + g : g;
     }
   } else if (A.stage) {
