@@ -1123,6 +1123,7 @@ __device__ __forceinline__ void mcaq_cmlp_bwd_body(const HeadTrainArgs& A) {
   float* sv = smem_tr;                       // [TR_TPB][CB_ST]
   float* red = sv + TR_TPB * CB_ST;          // [NW][TR_TPB] cross-wave partial sums
   float* w2s = red + NW * TR_TPB;            // W2 (32 x 64), read as broadcast LDS vectors
+  float* w2t = w2s + 2048;                   // W2 transposed (64 x 32): a wave's 4 layer-2 outputs of one k in one 16-byte read
   const mcaq_cmlp_params& P = A.P;
   const int tid = threadIdx.x, lane = tid & 63, q = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wgi = (int)blockIdx.x - A.wg0;   // workgroup within this segment
@@ -1143,7 +1144,12 @@ __device__ __forceinline__ void mcaq_cmlp_bwd_body(const HeadTrainArgs& A) {
   TSTAMP(16);
   // W2 into LDS (4 floats a thread; published by the first cross-wave sum's barrier)
 #pragma unroll
-  for (int i = 0; i < 2048 / NTH; ++i) w2s[tid + i * NTH] = P.w2[tid + i * NTH];
+  for (int i = 0; i < 2048 / NTH; ++i) {
+    const int e = tid + i * NTH;
+    const float wv = P.w2[e];
+    w2s[e] = wv;
+    w2t[(e & 63) * 32 + (e >> 6)] = wv;
+  }
   float ph[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) ph[k] = A.phi[(size_t)tc * 8 + k];
@@ -1182,11 +1188,13 @@ __device__ __forceinline__ void mcaq_cmlp_bwd_body(const HeadTrainArgs& A) {
   s = 0.0f;
 #pragma unroll
   for (int f = 0; f < F2; ++f) x2[f] = P.b2[q * F2 + f];
+  static_assert(F2 == 4, "one float4 of W2^T per k");
 #pragma unroll 16
   for (int k = 0; k < 64; ++k) {     // k outer: the F2 chains interleaved, each over k in order
     const float r = v[CB_R1 + k];
-#pragma unroll
-    for (int f = 0; f < F2; ++f) x2[f] = fmaf(w2s[(q * F2 + f) * 64 + k], r, x2[f]);
+    const float4 w4 = *reinterpret_cast<const float4*>(w2t + k * 32 + q * F2);
+    x2[0] = fmaf(w4.x, r, x2[0]); x2[1] = fmaf(w4.y, r, x2[1]);
+    x2[2] = fmaf(w4.z, r, x2[2]); x2[3] = fmaf(w4.w, r, x2[3]);
   }
 #pragma unroll
   for (int f = 0; f < F2; ++f) s += x2[f];
@@ -2221,7 +2229,7 @@ int mcaq_head_train_backward(const mcaq_cmlp_params* P, const float* phi, const 
   A.B = B; A.ht = ht; A.wt = wt; A.n = B * ht * wt; A.nwg = (A.n + TR_TPB - 1) / TR_TPB;
   const size_t lb = (size_t)53 * ht * wt * sizeof(float);
   if (lb > 160 * 1024 - 1024) return (int)hipErrorInvalidValue;
-  const size_t lc = (size_t)(TR_TPB * CB_ST + CB_NW * TR_TPB + 2048) * sizeof(float);
+  const size_t lc = (size_t)(TR_TPB * CB_ST + CB_NW * TR_TPB + 4096) * sizeof(float);
   static int set = 0;
   if (!set) {
     hipError_t e = hipFuncSetAttribute((const void*)mcaq_cmlp_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2404,7 +2412,7 @@ int mcaq_head_train_backward_multi_ride(const mcaq_cmlp_params* P, const mcaq_he
     Mc.s[k] = A; Mc.s[k].wg0 = wc; wc += A.nwg;    // MLP: 64 tiles per workgroup
   }
   Mb.nseg = Mc.nseg = nseg;
-  const size_t lc = (size_t)(TR_TPB * CB_ST + CB_NW * TR_TPB + 2048) * sizeof(float);
+  const size_t lc = (size_t)(TR_TPB * CB_ST + CB_NW * TR_TPB + 4096) * sizeof(float);
   static int set = 0;
   if (!set) {
     hipError_t e = hipFuncSetAttribute((const void*)mcaq_cmlp_bwd_multi_kernel,
