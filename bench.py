@@ -193,7 +193,7 @@ def main_qat(args, world, rank, dev, pg):
         torch.autograd.backward(list(outs) + [lbit], list(G) + [w_bit])
         if pg is not None:
             from mcaq_yolo_amd.dist import allreduce_gradients
-            allreduce_gradients(params_, pg)           # one flat bucket over RCCL
+            allreduce_gradients(params_, pg, static_pattern=True)   # the sink arena, in place over RCCL
         if fused_opt:
             opt.step()
         else:
@@ -446,7 +446,11 @@ def run_e2e(cfg, steps, warmup, world, rank, dev, pg, amp=False, eager=False, fu
             dt = float(t.item())
         return dt
 
-    nin = max(1, inflight) if (pg is None and not eager) else 1
+    # N > 1 on RCCL: the hook all-reduce and the detections' all-gather are
+    # captured in the step's graph; one batch in flight (one stream), so the
+    # replays issue the communicator's collectives in order on every rank
+    use_graph = not eager and (pg is None or _backend(pg) == "nccl")
+    nin = max(1, inflight) if (pg is None and use_graph) else 1
     fmt = torch.channels_last if channels_last else torch.contiguous_format
     inputs = [imgs] + [torch.rand(imgs.shape, generator=g).to(dev).contiguous(memory_format=fmt) for _ in range(nin - 1)]
 
@@ -467,7 +471,7 @@ def run_e2e(cfg, steps, warmup, world, rank, dev, pg, amp=False, eager=False, fu
                         step_on(k, hooks)
             torch.cuda.current_stream().wait_stream(side)
             torch.cuda.synchronize()
-            if pg is None and not eager:
+            if use_graph:
                 streams = [torch.cuda.Stream() for _ in range(nin)]
                 graphs = []
                 for k in range(nin):
@@ -512,7 +516,8 @@ def run_e2e(cfg, steps, warmup, world, rank, dev, pg, amp=False, eager=False, fu
                                % (name, B, E2E_CONF, E2E_IOU, E2E_MAX_DET,
                                   " + RCCL detection all-gather" if pg is not None else ""),
                    "global_batch": world * B, "grid_size": grid, "mapper": mapper,
-                   "parallelism": "dp%d" % world, "hip_graph": pg is None and not eager,
+                   "parallelism": "dp%d" % world, "hip_graph": use_graph,
+                   "rccl_in_graph": use_graph and pg is not None,
                    "conv_bn_fused": fuse, "channels_last": channels_last, "batches_in_flight": nin,
                    "network_only_ms_per_step": round(net_s * 1e3, 4),
                    # both legs run NMS: the difference is the hooks' cost per step
@@ -681,7 +686,14 @@ class Runner(_RunMixin):
         self.graphs = [None] * len(plans)
         self.i = 0
         self.batches = plans[0].batches
-        capturable = pg is None or _backend(pg) == "nccl"
+        # RCCL inside the graphs only where the replays cannot run two
+        # collectives of the communicator at once: one rank (no peers), or one
+        # stream.  With peers and several streams in flight, graphs replayed
+        # on different streams would put their all-reduce kernels on the GPU
+        # concurrently, in an order that can differ between ranks; there the
+        # all-reduce is issued eagerly between two replays - on the process
+        # group's own stream, in the host's (rank-identical) order.
+        capturable = pg is None or (_backend(pg) == "nccl" and (_world(pg) == 1 or depth == 1))
         self.captured_collective = use_graph and pg is not None and capturable
         if use_graph:
             torch.cuda.synchronize()
@@ -730,6 +742,45 @@ class Runner(_RunMixin):
 def _backend(pg):
     import torch.distributed as dist
     return str(dist.get_backend(pg)).lower()
+
+
+def _world(pg):
+    import torch.distributed as dist
+    return dist.get_world_size(pg)
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` without a launcher: start N rank processes of this
+    same command (one per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set
+    as torch.distributed.run sets them) and wait for them.  This process
+    never touches the GPU; rank 0's one JSON line is passed through."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out = procs[0].communicate()[0]
+    rcs = [procs[0].returncode]
+    for p_ in procs[1:]:
+        try:
+            rcs.append(p_.wait(timeout=600))
+        except subprocess.TimeoutExpired:
+            p_.kill()
+            rcs.append(-9)
+    if any(rcs):
+        for p_ in procs:
+            if p_.poll() is None:
+                p_.kill()
+        raise SystemExit("bench.py --gpus %d: rank exit codes %s" % (n, rcs))
+    sys.stdout.write(out.decode())
+    sys.stdout.flush()
 
 
 def kernel_timing(plans, reps=40, evict=None):
@@ -813,6 +864,9 @@ def main():
                     help="morphology pass B: per-image workgroups or batch-wide tile kernels (default: engine's)")
     ap.add_argument("--pass-a", choices=("image", "band"), default=None,
                     help="morphology pass A: per-image workgroups or 16-row band workgroups (default: engine's)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="launcher rehearsal without a GPU: the ranks rendezvous over gloo, all-reduce their ranks "
+                         "and rank 0 prints one JSON line (tests/test_bench_cpu.py)")
     args = ap.parse_args()
     if args.qat_scales is not None:
         from mcaq_yolo_amd import hooks as _hooks
@@ -825,11 +879,24 @@ def main():
         from mcaq_yolo_amd import engine as _engine
         _engine.BAND_PASS = args.pass_a == "band"
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(args.gpus)          # self-launched: one process per GPU
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    if args.launch_check:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        t = torch.tensor([float(rank)])
+        dist.all_reduce(t)
+        if rank == 0:
+            print(json.dumps({"metric": "launch check", "n_gpus": world, "rank_sum": float(t[0]),
+                              "pid_differs": os.getpid() != os.getppid()}), flush=True)
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     # MCAQ_BENCH_BACKEND=gloo + more ranks than GPUs: functional rehearsal of
     # the N > 1 path on a one-GPU box (never a measurement)
     backend = os.environ.get("MCAQ_BENCH_BACKEND", "nccl")
@@ -1031,7 +1098,7 @@ def main():
             "kernels": kern,
             "cpu_baseline": None,
         }
-    if not args.no_e2e and world == 1:
+    if not args.no_e2e:
         for p_ in plans:
             p_.feats = None
         del runner

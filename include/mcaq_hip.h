@@ -44,7 +44,7 @@ typedef void* hipEvent_t;
 extern "C" {
 #endif
 
-#define MCAQ_ABI_VERSION 24
+#define MCAQ_ABI_VERSION 25
 /* segments (hook scale x batch) per mcaq_stats / mcaq_finalize /
  * mcaq_morph* / mcaq_quant launch */
 #define MCAQ_MAX_SEGMENTS 9
@@ -522,7 +522,9 @@ int mcaq_stats_pack(const mcaq_stats_scale* scales, int nscales, const mcaq_pack
  * torch.nn.utils.clip_grad_norm_(max_norm) over every segment's gradient
  * (the norm of the per-tensor 2-norms; .grad scaled in place), then
  * torch.optim.AdamW (decoupled weight decay, the fused kernel's update
- * order; *step += 1 first, as a capturable AdamW's step tensor) and, for
+ * order; each segment's steps[step_idx] += 1 first, as a capturable AdamW's
+ * per-parameter step tensors: a parameter without a gradient this step is
+ * not a segment and keeps its count) and, for
  * segments with project_abs, p <- |p| (the bit mapper's Eq. 18 projection,
  * bit_allocation.py:186-197) - train.py:626-641.  max_norm <= 0: no clip;
  * total_norm (1 float) receives the pre-clip norm, or NULL.  work:
@@ -533,14 +535,32 @@ int mcaq_stats_pack(const mcaq_stats_scale* scales, int nscales, const mcaq_pack
 #define MCAQ_OPT_MAXGROUPS 4
 typedef struct {
   float* param; float* grad; float* exp_avg; float* exp_avg_sq;
-  int n, project_abs, group;   /* group: index into the hyper-parameter table */
+  int n, project_abs, group;   /* group: row of the hyper-parameter table */
+  int step_idx;                /* this parameter's entry of `steps` (distinct per segment) */
 } mcaq_adamw_seg;
 typedef struct {
   double lr, weight_decay, beta1, beta2, eps;   /* doubles, as torch's fused AdamW takes them */
 } mcaq_adamw_group;
+/* groups: DEVICE table of ngroups rows, read when the kernels run - a
+ * captured step uses the values last written there (an lr schedule writes
+ * the table between replays); steps: device float counters. */
 size_t mcaq_clip_adamw_work_floats(int total);
 int mcaq_clip_adamw(const mcaq_adamw_seg* segs, int nseg, const mcaq_adamw_group* groups, int ngroups,
-                    float* step, float max_norm, float* total_norm, float* work, hipStream_t stream);
+                    float* steps, float max_norm, float* total_norm, float* work, hipStream_t stream);
+
+/* ---- data-parallel QAT step: unpack one all-gather ------------------------
+ * g: every rank's send buffer back to back, [world][stride] floats
+ * (all_gather_into_tensor).  Segment i, mode 0: out[r * n + j] =
+ * g[r * stride + off + j] for every rank r (one hook scale's global batch in
+ * rank order = image order); mode 1 / 2: out[j] = min / max over the ranks
+ * of g[r * stride + off + j] (NaN propagating).  One launch (csrc/mcaq_dp.h,
+ * dist.shard_hooks: the train-mode bit mapper on the global batch). */
+#define MCAQ_DP_MAXSEG 16
+typedef struct {
+  float* out;
+  int off, n, mode;
+} mcaq_dp_seg;
+int mcaq_dp_unpack(const float* g, int world, int stride, const mcaq_dp_seg* segs, int nseg, hipStream_t stream);
 
 int mcaq_abi_version(void);
 

@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libmcaq_hip.so")
-ABI_VERSION = 24
+ABI_VERSION = 25
 MAX_SEGMENTS = 9   # MCAQ_MAX_SEGMENTS: segments (hook scale x batch) per launch
 
 P = ctypes.c_void_p
@@ -115,7 +115,7 @@ MCAQ_OPT_MAXSEG, MCAQ_OPT_MAXGROUPS = 64, 4
 class AdamwSeg(ctypes.Structure):
     """mcaq_adamw_seg."""
     _fields_ = [("param", P), ("grad", P), ("exp_avg", P), ("exp_avg_sq", P), ("n", I), ("project_abs", I),
-                ("group", I)]
+                ("group", I), ("step_idx", I)]
 
 
 class AdamwGroup(ctypes.Structure):
@@ -127,6 +127,14 @@ class EmaSeg(ctypes.Structure):
     """mcaq_ema_seg."""
     _fields_ = [("batch_min", P), ("batch_max", P), ("running_min", P), ("running_max", P), ("copy_min", P),
                 ("copy_max", P), ("num_batches", P), ("C", I), ("first", I), ("momentum", ctypes.c_double)]
+
+
+MCAQ_DP_MAXSEG = 16
+
+
+class DpSeg(ctypes.Structure):
+    """mcaq_dp_seg."""
+    _fields_ = [("out", P), ("off", I), ("n", I), ("mode", I)]
 
 
 # morph stage flags (mcaq_morph.h)
@@ -152,7 +160,7 @@ EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats",
            "mcaq_mapper_train_forward_stage_multi", "mcaq_mapper_train_backward_stage_multi", "mcaq_clip_adamw", "mcaq_clip_adamw_work_floats",
            "mcaq_bit_budget_forward", "mcaq_qat_smask_backward_multi", "mcaq_qat_forward_budget",
            "mcaq_ema_stats_multi_running", "mcaq_head_train_backward_multi_ride",
-           "mcaq_stats_pack", "mcaq_morph_ema", "mcaq_mapper_train_backward_multi_ride")
+           "mcaq_stats_pack", "mcaq_morph_ema", "mcaq_mapper_train_backward_multi_ride", "mcaq_dp_unpack")
 
 _LIB = None
 
@@ -268,9 +276,11 @@ def _declare(lib):
     lib.mcaq_qat_smask_backward_multi.restype = I
     lib.mcaq_qat_smask_backward_multi.argtypes = [ctypes.POINTER(QatSmaskSeg), I, ctypes.POINTER(BitBudget), P]
     lib.mcaq_clip_adamw.restype = I
-    lib.mcaq_clip_adamw.argtypes = [ctypes.POINTER(AdamwSeg), I, ctypes.POINTER(AdamwGroup), I, P, Fl, P, P, P]
+    lib.mcaq_clip_adamw.argtypes = [ctypes.POINTER(AdamwSeg), I, P, I, P, Fl, P, P, P]
     lib.mcaq_clip_adamw_work_floats.restype = ctypes.c_size_t
     lib.mcaq_clip_adamw_work_floats.argtypes = [I]
+    lib.mcaq_dp_unpack.restype = I
+    lib.mcaq_dp_unpack.argtypes = [P, I, I, ctypes.POINTER(DpSeg), I, P]
     lib.mcaq_smask_train_backward.restype = I
     lib.mcaq_smask_train_backward.argtypes = [ctypes.POINTER(SmaskParams), P, P, P, I, I, I, I, I, P, I, P, P, P]
     return lib

@@ -958,17 +958,44 @@ DIRECT_GRAD_ACCUM = True
 
 def _grads_observed(params):
     """True when something outside backward() must see these parameters'
-    gradients as autograd results: torch DDP's reducer (BASELINE config 5 is
-    DDP; it hooks every parameter's AccumulateGrad and would never see a
-    gradient written straight into .grad) or any parameter hook.  Direct
-    accumulation is then off and the gradients go back to autograd."""
-    import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized():
-        return True
+    gradients as autograd results: torch DDP's reducer (it hooks every
+    parameter's AccumulateGrad and would never see a gradient written straight
+    into .grad) or any parameter hook.  Direct accumulation is then off and the
+    gradients go back to autograd.  A torch.distributed process group alone
+    counts as observed (a DDP wrapper may hold the parameters) - unless every
+    parameter is marked as synchronised by this package's own data-parallel
+    step (dist.shard_hooks: dist.allreduce_gradients reads the sinks, no
+    reducer is involved)."""
     for p in params:
         if getattr(p, "_backward_hooks", None) or getattr(p, "_post_accumulate_grad_hooks", None):
             return True
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        return not all(getattr(p, "_mcaq_dp_manual", False) for p in params)
     return False
+
+
+class _GradArena:
+    """The gradient sinks of several nets as consecutive slices of ONE flat
+    device buffer (dist.shard_hooks), so the data-parallel step's gradient
+    bucket is that buffer, all-reduced in place (dist.allreduce_gradients)."""
+
+    def __init__(self, pairs, device):
+        n = sum(p.numel() for _, ps in pairs for p in ps)
+        self.flat = torch.zeros(n, device=device)
+        o = 0
+        for sk, ps in pairs:
+            k = sum(p.numel() for p in ps)
+            old = sk.views
+            sk.flat = self.flat[o:o + k]
+            sk.views = _split_flat(sk.flat, ps)
+            for i, (p, v) in enumerate(zip(ps, sk.views)):
+                # a .grad that was the old sink's view moves into the arena
+                if old is not None and i < len(old) and p.grad is not None and \
+                        p.grad.data_ptr() == old[i].data_ptr() and p.grad.shape == v.shape:
+                    v.copy_(p.grad)
+                    p.grad = v
+            o += k
 
 
 class _GradSink:
@@ -991,7 +1018,7 @@ class _GradSink:
         n = sum(p.numel() for p in params)
         dev = params[0].device
         if self.flat is None or self.flat.numel() != n or self.flat.device != dev:
-            if torch.cuda.is_current_stream_capturing():
+            if dev.type == "cuda" and torch.cuda.is_current_stream_capturing():
                 return None          # first use must happen outside capture (warm-up step)
             self.flat = torch.zeros(n, device=dev)
             self.views = _split_flat(self.flat, params)

@@ -433,11 +433,19 @@ __device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, fl
 #ifndef MCAQ_STATS_XCD
 #define MCAQ_STATS_XCD 1
 #endif
+// > 0: pass 1 and pass 2 (tile kernel) launch at most MCAQ_STREAM_CAP
+// workgroups per CU (x 256 CUs, a multiple of 8: the XCD order holds) that
+// loop over their units, so the streaming passes never hold more than that
+// share of a CU and the latency-bound morphology of other batches in flight
+// finds room beside them.  0: one workgroup per unit (A/B).
+#ifndef MCAQ_STREAM_CAP
+#define MCAQ_STREAM_CAP 0
+#endif
 
 template <bool kVec>   // kVec: 8/16-byte row accesses for ppl 2/4 (host checks alignment)
-__device__ __forceinline__ void stats_dispatch(const StatsArgs& a, float* lds) {
+__device__ __forceinline__ void stats_dispatch(const StatsArgs& a, float* lds, const int bid) {
   // heaviest (most channels per pixel) scales are the last ones: start them first
-  const int unit = a.units_total - 1 - (int)blockIdx.x;
+  const int unit = a.units_total - 1 - bid;
   int si = 0;
   while (si + 1 < a.nscales && unit >= a.s[si + 1].unit_begin) ++si;
   int lu = unit - a.s[si].unit_begin;
@@ -449,7 +457,7 @@ __device__ __forceinline__ void stats_dispatch(const StatsArgs& a, float* lds) {
     const int x0 = a.units_total - a.s[si].unit_begin - n;     // first blockIdx of this scale
     const int upi = (S.H * S.W + 64 * ppl - 1) / (64 * ppl);   // units per image
     if ((x0 & 7) == 0 && (S.B & 7) == 0) {
-      const int j = (int)blockIdx.x - x0, slot = j >> 3, q = slot / upi;
+      const int j = bid - x0, slot = j >> 3, q = slot / upi;
       lu = ((j & 7) + 8 * q) * upi + (slot - q * upi);
     }
   }
@@ -466,7 +474,14 @@ __device__ __forceinline__ void stats_dispatch(const StatsArgs& a, float* lds) {
 template <bool kVec>
 __global__ __launch_bounds__(256, MCAQ_STATS_MINW) void mcaq_stats_kernel(StatsArgs a) {
   __shared__ float lds[ST_LDS];
-  stats_dispatch<kVec>(a, lds);
+#if MCAQ_STREAM_CAP > 0
+  for (int u = (int)blockIdx.x; u < a.units_total; u += (int)gridDim.x) {
+    stats_dispatch<kVec>(a, lds, u);
+    __syncthreads();    // the LDS of this unit is free for the next
+  }
+#else
+  stats_dispatch<kVec>(a, lds, (int)blockIdx.x);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -1076,13 +1091,9 @@ __global__ MCAQ_QUANT_LB void mcaq_quant_kernel(QuantArgs a) {
 // rocprofv3 SQ_INSTS_VALU, profiles/r04_sq/).  Soft mask: none or m(tile)
 // values (QM_NONE / QM_MT_LDS); at most 8 bit widths.
 template <bool kNTL, bool kNTS, int kM>
-__global__ MCAQ_QUANT_LB void mcaq_quant_tile_kernel(QuantArgs a) {
-  __shared__ float4 qt[8 * QSLICE];           // [kb][c]: scale, zp, 1/scale
-  __shared__ float mts[kM == QM_MT_LDS ? QMAXNT : 1];
-  __shared__ float4 mq4[64];                  // m(p) of each lane's 4 pixels
-  __shared__ int qany[QSLICE];
+__device__ __forceinline__ void quant_tile_unit(const QuantArgs& a, const int unit, float4* qt, float* mts, float4* mq4,
+                                                int* qany) {
   typedef float f2 __attribute__((ext_vector_type(2)));
-  const int unit = blockIdx.x;
   int si = 0;
   while (si + 1 < a.nscales && unit >= a.s[si + 1].unit_begin) ++si;
   const mcaq_quant_scale& S = a.s[si];
@@ -1205,6 +1216,22 @@ __global__ MCAQ_QUANT_LB void mcaq_quant_tile_kernel(QuantArgs a) {
   }
 }
 
+template <bool kNTL, bool kNTS, int kM>
+__global__ MCAQ_QUANT_LB void mcaq_quant_tile_kernel(QuantArgs a) {
+  __shared__ float4 qt[8 * QSLICE];           // [kb][c]: scale, zp, 1/scale
+  __shared__ float mts[kM == QM_MT_LDS ? QMAXNT : 1];
+  __shared__ float4 mq4[64];                  // m(p) of each lane's 4 pixels
+  __shared__ int qany[QSLICE];
+#if MCAQ_STREAM_CAP > 0
+  for (int u = (int)blockIdx.x; u < a.units_total; u += (int)gridDim.x) {
+    quant_tile_unit<kNTL, kNTS, kM>(a, u, qt, mts, mq4, qany);
+    __syncthreads();    // LDS of this unit free for the next
+  }
+#else
+  quant_tile_unit<kNTL, kNTS, kM>(a, (int)blockIdx.x, qt, mts, mq4, qany);
+#endif
+}
+
 // ---------------------------------------------------------------------------
 // extern "C" launchers
 // ---------------------------------------------------------------------------
@@ -1280,10 +1307,11 @@ int mcaq_stats(const mcaq_stats_scale* scales, int nscales, hipStream_t stream) 
   bool vec;
   const int e = stats_args(scales, nscales, a, vec);
   if (e) return e;
+  const dim3 g(MCAQ_STREAM_CAP > 0 ? imin_(a.units_total, MCAQ_STREAM_CAP * 256) : a.units_total);
   if (vec)
-    launch_k(mcaq_stats_kernel<true>, dim3(a.units_total), dim3(256), 0, stream, a);
+    launch_k(mcaq_stats_kernel<true>, g, dim3(256), 0, stream, a);
   else
-    launch_k(mcaq_stats_kernel<false>, dim3(a.units_total), dim3(256), 0, stream, a);
+    launch_k(mcaq_stats_kernel<false>, g, dim3(256), 0, stream, a);
   return (int)hipGetLastError();
 }
 
@@ -1727,6 +1755,7 @@ int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream) 
   tile_ok = false;   // A/B: the general kernel
 #endif
   if (tile_ok) {
+    const dim3 g(MCAQ_STREAM_CAP > 0 ? imin_(units, MCAQ_STREAM_CAP * 256) : units);
     switch ((kind == QM_NONE ? 0 : 4) + (nt & 3)) {
       case 0: launch_k(mcaq_quant_tile_kernel<false, false, QM_NONE>, g, t, 0, stream, a); break;
       case 1: launch_k(mcaq_quant_tile_kernel<false, true, QM_NONE>, g, t, 0, stream, a); break;
@@ -1767,6 +1796,7 @@ int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream) 
 #include "mcaq_nms.h"
 #include "mcaq_train.h"
 #include "mcaq_optim.h"
+#include "mcaq_dp.h"
 
 // C++-linkage drop-in for the reference's declaration (include/mcaq_hip.h):
 // same name, argument list and void return as MCAQPlugin.cpp:15-23.  An

@@ -23,14 +23,13 @@
 
 namespace mcaq {
 
-static_assert(sizeof(mcaq_adamw_seg) * MCAQ_OPT_MAXSEG + sizeof(mcaq_adamw_group) * MCAQ_OPT_MAXGROUPS + 64 <= 4096,
-              "optimizer kernel arguments exceed 4 KiB");
+static_assert(sizeof(mcaq_adamw_seg) * MCAQ_OPT_MAXSEG + 64 <= 4096, "optimizer kernel arguments exceed 4 KiB");
 
 struct AdamwArgs {
   mcaq_adamw_seg s[MCAQ_OPT_MAXSEG];
-  mcaq_adamw_group g[MCAQ_OPT_MAXGROUPS];
-  int nseg;
-  float* step;         // device step counter (float, like torch's capturable AdamW)
+  const mcaq_adamw_group* g;   // device table, read at run time (a captured step follows lr changes)
+  int nseg, ngroups;
+  float* steps;        // device per-parameter step counters (float, like torch's capturable AdamW)
   float max_norm;      // <= 0: no clipping
   float* total_norm;   // or nullptr
 };
@@ -38,7 +37,7 @@ struct AdamwArgs {
 constexpr int OPT_TH = 256;
 constexpr int OPT_E = 4;                    // consecutive elements per thread
 constexpr int OPT_CH = OPT_TH * OPT_E;      // elements per chunk (one workgroup)
-constexpr int OPT_WORK0 = 4;                // work[0]: the step after this one; partials from work[4]
+constexpr int OPT_WORK0 = MCAQ_OPT_MAXSEG;  // work[k < nseg]: segment k's step after this one; partials from here
 
 // beta^step for an integer-valued step by binary exponentiation in double (a
 // few multiplies instead of the library pow; within an ulp or two of pow)
@@ -130,7 +129,7 @@ __global__ __launch_bounds__(OPT_TH) void mcaq_adamw_norm_kernel(AdamwArgs a, fl
     }
     if (lane == 0) out[kk] = acc;
   }
-  if (blockIdx.x == 0 && tid == 0) work[0] = a.step[0] + 1.0f;
+  if (blockIdx.x == 0 && tid < nseg) work[tid] = a.steps[sg[tid].step_idx] + 1.0f;
 }
 
 // launch 2: the clip coefficient from launch 1's partials (every workgroup
@@ -140,12 +139,11 @@ __global__ __launch_bounds__(OPT_TH) void mcaq_adamw_update_kernel(AdamwArgs a, 
   __shared__ int st[MCAQ_OPT_MAXSEG + 1];
   __shared__ float seg_acc[MCAQ_OPT_MAXSEG];
   __shared__ float coef_s;
-  __shared__ float g_bc2s[MCAQ_OPT_MAXGROUPS], g_ss[MCAQ_OPT_MAXGROUPS];
-  __shared__ double g_hp[MCAQ_OPT_MAXGROUPS][6];   // lr * wd, beta1, 1 - beta1, beta2, 1 - beta2, eps
+  __shared__ float s_bc2s[MCAQ_OPT_MAXSEG], s_ss[MCAQ_OPT_MAXSEG];
+  __shared__ double g_hp[MCAQ_OPT_MAXGROUPS][7];   // lr * wd, beta1, 1 - beta1, beta2, 1 - beta2, eps, lr
   const int tid = (int)threadIdx.x;
   const int nseg = a.nseg;
   const bool clip = a.max_norm > 0.0f;
-  const float step = work[0];
   // per-tensor squared norms: the chunks' partials in chunk order, 8 loads
   // of a thread in flight (clamped index)
   if (clip && tid < nseg) {
@@ -160,19 +158,26 @@ __global__ __launch_bounds__(OPT_TH) void mcaq_adamw_update_kernel(AdamwArgs a, 
     }
     seg_acc[tid] = s;
   }
-  if (tid < MCAQ_OPT_MAXGROUPS) {
-    // bias corrections of each hyper-parameter group (fused AdamW: fp32
-    // values of the double expressions)
-    const mcaq_adamw_group& G = a.g[tid];
-    const float bc1 = (float)(1.0 - pow_int(G.beta1, step));
-    g_bc2s[tid] = sqrtf((float)(1.0 - pow_int(G.beta2, step)));
-    g_ss[tid] = (float)(G.lr / (double)bc1);
+  if (tid < a.ngroups) {
+    // the hyper-parameter table as the host last wrote it
+    const mcaq_adamw_group G = a.g[tid];
     g_hp[tid][0] = G.lr * G.weight_decay;
     g_hp[tid][1] = G.beta1; g_hp[tid][2] = 1.0 - G.beta1;
     g_hp[tid][3] = G.beta2; g_hp[tid][4] = 1.0 - G.beta2;
-    g_hp[tid][5] = G.eps;
+    g_hp[tid][5] = G.eps; g_hp[tid][6] = G.lr;
   }
   opt_table(a, sg, st);    // (its barriers also publish seg_acc and the group table)
+  if (tid >= 64 && tid < 64 + nseg) {
+    // bias corrections of each parameter at its own step (fused AdamW: fp32
+    // values of the double expressions; torch keeps a step per parameter)
+    const int k = tid - 64;
+    const float step = work[k];
+    const double* hp = g_hp[sg[k].group];
+    const float bc1 = (float)(1.0 - pow_int(hp[1], step));
+    s_bc2s[k] = sqrtf((float)(1.0 - pow_int(hp[3], step)));
+    s_ss[k] = (float)(hp[6] / (double)bc1);
+    if (blockIdx.x == 0) a.steps[sg[k].step_idx] = step;   // every workgroup reads the steps from work
+  }
   if (clip) {
     if (tid < 64) {
       // the norm of the per-tensor norms (clip_grad_norm_): squares of the
@@ -235,15 +240,14 @@ __global__ __launch_bounds__(OPT_TH) void mcaq_adamw_update_kernel(AdamwArgs a, 
       p = (float)((double)p - hp[0] * (double)p);
       const float m = (float)(hp[1] * (double)mv[q] + hp[2] * (double)g);
       const float v = (float)(hp[3] * (double)vv[q] + hp[4] * (double)g * (double)g);
-      const float denom = (float)((double)(sqrtf(v) / g_bc2s[gi]) + hp[5]);
-      p = p - g_ss[gi] * m / denom;
+      const float denom = (float)((double)(sqrtf(v) / s_bc2s[ks[q]]) + hp[5]);
+      p = p - s_ss[ks[q]] * m / denom;
       if (S.project_abs) p = fabsf(p);
       S.exp_avg[e] = m;
       S.exp_avg_sq[e] = v;
       S.param[e] = p;
     }
   }
-  if (blockIdx.x == 0 && tid == 0) a.step[0] = step;   // every workgroup read the step from work[0]
 }
 
 }  // namespace mcaq
@@ -255,28 +259,32 @@ size_t mcaq_clip_adamw_work_floats(int total) {
 }
 
 int mcaq_clip_adamw(const mcaq_adamw_seg* segs, int nseg, const mcaq_adamw_group* groups, int ngroups,
-                    float* step, float max_norm, float* total_norm, float* work, hipStream_t stream) {
+                    float* steps, float max_norm, float* total_norm, float* work, hipStream_t stream) {
   using namespace mcaq;
-  if (!segs || !groups || !step || !work || nseg < 1 || nseg > MCAQ_OPT_MAXSEG || ngroups < 1 ||
+  if (!segs || !groups || !steps || !work || nseg < 1 || nseg > MCAQ_OPT_MAXSEG || ngroups < 1 ||
       ngroups > MCAQ_OPT_MAXGROUPS)
     return (int)hipErrorInvalidValue;
   AdamwArgs a{};
   long long total = 0;
   for (int k = 0; k < nseg; ++k) {
     const mcaq_adamw_seg& g = segs[k];
-    if (!g.param || !g.grad || !g.exp_avg || !g.exp_avg_sq || g.n < 1 || g.group < 0 || g.group >= ngroups)
+    if (!g.param || !g.grad || !g.exp_avg || !g.exp_avg_sq || g.n < 1 || g.group < 0 || g.group >= ngroups ||
+        g.step_idx < 0)
       return (int)hipErrorInvalidValue;
+    for (int j = 0; j < k; ++j)
+      if (segs[j].step_idx == g.step_idx) return (int)hipErrorInvalidValue;   // one step counter per parameter
     a.s[k] = g;
     total += g.n;
   }
   if (total > (1LL << 30)) return (int)hipErrorInvalidValue;
-  for (int k = 0; k < ngroups; ++k) a.g[k] = groups[k];
+  a.g = groups;
+  a.ngroups = ngroups;
   a.nseg = nseg;
-  a.step = step;
+  a.steps = steps;
   a.max_norm = max_norm;
   a.total_norm = total_norm;
   const int nchunk = (int)((total + OPT_CH - 1) / OPT_CH);
-  // launch 1 also writes work[0] (the next step count) for launch 2
+  // launch 1 also writes work[0 .. nseg) (the next step counts) for launch 2
   hipLaunchKernelGGL(mcaq_adamw_norm_kernel, dim3(nchunk), dim3(OPT_TH), 0, stream, a, work);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return (int)e;

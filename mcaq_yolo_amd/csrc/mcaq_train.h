@@ -1867,7 +1867,7 @@ __global__ __launch_bounds__(256, MCAQ_STATS_MINW) void mcaq_stats_pack_kernel(S
     pack_elem(p, out, ((int)blockIdx.x - a.units_total) * 256 + (int)threadIdx.x);
     return;
   }
-  stats_dispatch<kVec>(a, lds);
+  stats_dispatch<kVec>(a, lds, (int)blockIdx.x);
 }
 
 }  // namespace mcaq

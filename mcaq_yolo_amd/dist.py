@@ -81,42 +81,105 @@ def sync_mapper_batchnorm(mapper, process_group):
 from torch.utils.weak import WeakIdKeyDictionary
 
 # per first parameter (by identity; dropped with the model):
-# {(group, params, local pattern): global pattern}
+# {(group, params): global has-gradient pattern}
 _UNUSED_CACHE = WeakIdKeyDictionary()
 
 
-def allreduce_gradients(params, process_group, average=True):
-    """Average the gradients of `params` over the group with ONE collective:
-    every parameter that requires grad goes into a single flat bucket in the
-    order given (a None grad contributes zeros).  Afterwards every parameter
-    that had a gradient on some rank holds the averaged gradient, and one
-    whose grad was None on every rank keeps None (as DDP leaves globally
-    unused parameters: optimizers then skip them).
+def _flat_span(grads):
+    """The one contiguous fp32 span of storage the gradient views tile exactly
+    (no gap, no overlap), or None.  _GradArena lays the hook nets' gradient
+    sinks out that way, so their bucket is reduced in place."""
+    if not grads or any(g is None or not g.is_contiguous() or g.dtype != torch.float32 for g in grads):
+        return None
+    base = grads[0].untyped_storage()
+    if any(g.untyped_storage().data_ptr() != base.data_ptr() for g in grads):
+        return None
+    runs = sorted((g.storage_offset(), g.numel()) for g in grads)
+    o = runs[0][0]
+    for off, n in runs:
+        if off != o:
+            return None
+        o += n
+    t = torch.empty(0, dtype=torch.float32, device=grads[0].device)
+    t.set_(base, runs[0][0], (o - runs[0][0],))
+    return t
 
-    Which parameters have a gradient on SOME rank is a property of the model
-    and the step, not of the data: it is found once per (parameter list,
-    local has-gradient pattern) - one flag per parameter rides along in that
-    first all-reduce and is read back on the host - and reused afterwards, so
-    a steady-state call issues no device-to-host copy, allocates no host
-    tensor and can be captured in a HIP graph with the nccl (RCCL) backend.
-    `reset_unused_cache()` forgets the patterns (e.g. after freezing layers)."""
+
+def _reduce_in_place(t, process_group, average):
+    import torch.distributed as dist
+    world = dist.get_world_size(process_group)
+    if average and world > 1 and dist.get_backend(process_group) == "nccl":
+        dist.all_reduce(t, op=dist.ReduceOp.AVG, group=process_group)   # RCCL ncclAvg: no extra launch
+        return
+    dist.all_reduce(t, group=process_group)
+    if average and world > 1:
+        t /= world
+
+
+def allreduce_gradients(params, process_group, average=True, static_pattern=False):
+    """Average (or sum) the gradients of `params` over the group as ONE flat
+    bucket (train.py:626-641 under DDP).  Afterwards every parameter that had
+    a gradient on some rank holds the reduced gradient (a None grad
+    contributes zeros), and one whose grad was None on every rank keeps None,
+    as DDP leaves globally unused parameters (optimizers then skip them).
+
+    static_pattern=False (default): one flag per parameter rides along in the
+    bucket and is read back, so ranks whose has-gradient patterns differ or
+    change between calls stay consistent - at the cost of a device-to-host
+    read per call (not capturable).
+
+    static_pattern=True: the caller guarantees that the set of parameters
+    with a gradient on SOME rank is fixed (a captured step, the hook step of
+    dist.shard_hooks).  The pattern is agreed collectively on the first call
+    (flags in the bucket, one read-back) and cached per (group, parameters);
+    later calls move exactly the cached parameters on every rank, whatever the
+    local pattern, so bucket sizes always match across ranks (a local None
+    sends zeros; a parameter that became globally unused then ends with a
+    zero gradient instead of None).  A local gradient on a parameter the
+    cached pattern says no rank uses raises ValueError: call
+    reset_unused_cache() on every rank when the model changes.  When the
+    gradients tile one contiguous buffer (the hook nets' sinks, _GradArena),
+    the bucket is that buffer, reduced in place: no concatenation, no copies,
+    no host sync - capturable in a HIP graph with RCCL."""
     import torch.distributed as dist
     ps = [p for p in params if p.requires_grad]
     if not ps:
         return
     has = tuple(p.grad is not None for p in ps)
-    key = (id(process_group), tuple(id(p) for p in ps), has)
+    key = (id(process_group), tuple(id(p) for p in ps))
     cache = _UNUSED_CACHE.setdefault(ps[0], {})
-    any_grad = cache.get(key)
+    any_grad = cache.get(key) if static_pattern else None
+    if any_grad is not None:
+        for p, h, a in zip(ps, has, any_grad):
+            if h and not a:
+                raise ValueError("allreduce_gradients(static_pattern=True): a parameter that no rank had a "
+                                 "gradient for when the pattern was cached has one now; call "
+                                 "dist.reset_unused_cache() on every rank")
+        live = [p for p, a in zip(ps, any_grad) if a]
+        for p in live:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        span = _flat_span([p.grad for p in live])
+        if span is not None:
+            _reduce_in_place(span, process_group, average)
+            return
+        flat = torch.cat([p.grad.reshape(-1) for p in live])
+        _reduce_in_place(flat, process_group, average)
+        o = 0
+        for p in live:
+            n = p.numel()
+            p.grad.copy_(flat[o:o + n].view_as(p))
+            o += n
+        return
+    # flags ride along; read back to decide None vs reduced on every rank alike
     parts = [(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1) for p in ps]
-    if any_grad is None:
-        parts.append(torch.tensor(has, dtype=ps[0].dtype, device=ps[0].device))
+    parts.append(torch.tensor(has, dtype=ps[0].dtype, device=ps[0].device))
     flat = torch.cat(parts)
     dist.all_reduce(flat, group=process_group)
-    if any_grad is None:
-        any_grad = tuple(bool(v) for v in (flat[-len(ps):] > 0).tolist())
+    any_grad = tuple(bool(v) for v in (flat[-len(ps):] > 0).tolist())
+    if static_pattern:
         cache[key] = any_grad
-        flat = flat[:-len(ps)]
+    flat = flat[:-len(ps)]
     if average:
         flat /= dist.get_world_size(process_group)
     o = 0
@@ -139,10 +202,34 @@ def reset_unused_cache():
 def shard_hooks(hooks, process_group, rank, world, local_batch):
     """Configure an MCAQHooks / MCAQYOLO for batch-sharded data parallelism:
     min/max all-reduce in every quantizer, global-batch tile order for the
-    fractal regression, synced mapper BatchNorm for QAT."""
+    fractal regression, synced mapper BatchNorm for QAT.
+
+    The hook parameters' gradients are then this package's to synchronise
+    (`allreduce_gradients`, not a DDP reducer): they are marked so the fused
+    backwards keep writing them into their flat sinks, and the sinks of the
+    complexity MLP, the bit mapper and every soft mask are laid out back to
+    back in ONE device buffer (core._GradArena) - the step's gradient bucket,
+    reduced in place by allreduce_gradients(..., static_pattern=True)."""
+    from . import core
     hooks.process_group = process_group
     hooks.batch_offset, hooks.batch_total = rank * local_batch, world * local_batch
     for q in hooks.quantizers.values():
         q.process_group = process_group
     sync_mapper_batchnorm(hooks.bit_mapper, process_group)
+    pairs = []
+    an = getattr(hooks, "complexity_analyzer", None)
+    if an is not None and hasattr(an, "_gsink"):
+        pairs.append((an._gsink, list(an.complexity_mlp.parameters())))
+    bm = hooks.bit_mapper
+    if hasattr(bm, "_gsink") and hasattr(bm, "mapping_network"):
+        pairs.append((bm._gsink, list(bm.mapping_network.parameters())))
+    for q in hooks.quantizers.values():
+        sm = getattr(q, "soft_mask", None)
+        if sm is not None and hasattr(sm, "_gsink"):
+            pairs.append((sm._gsink, list(sm.net.parameters())))
+    params = [p for _, ps in pairs for p in ps]
+    for p in params:
+        p._mcaq_dp_manual = True
+    if params:
+        hooks._grad_arena = core._GradArena(pairs, params[0].device)
     return hooks

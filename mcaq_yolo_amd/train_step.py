@@ -192,7 +192,7 @@ def _ema_multi(qs, xs, box, running=None, defer=False):
     if not fold:
         abi.check(L.mcaq_finalize(fz, n, _stream()), "mcaq_finalize")
     pg = qs[0].process_group
-    if pg is not None:
+    if pg is not None and not (fold and all(b.get("bglobal") for b in box[:n])):
         # data-parallel QAT: every scale's batch min / max over the global
         # batch in ONE all-reduce (MAX over [-min, max]; per quantizer the
         # values of update_running_stats' own all-reduce)
@@ -378,6 +378,93 @@ def _flush_pending_sm_reduce():
         abi.check(abi.lib().mcaq_train_reduce_multi(segs, n, 0, _stream()), "mcaq_train_reduce_multi")
 
 
+# ---------------------------------------------------------------------------
+# batch-sharded step (dist.shard_hooks): the bit mapper on the global batch
+# ---------------------------------------------------------------------------
+# The mapper's train-mode BatchNorm statistics span the global batch
+# (bit_allocation.py:126 on the single process).  Instead of one collective
+# per batch-statistics stage in each direction (3 + 3), every rank
+# all-gathers the mapper's inputs once - with the quantizers' batch channel
+# min / max riding along - runs the mapper on the GLOBAL batch of tiles (a
+# few thousand tiles: the stage launches' cost is their latency, not the
+# tile count) and keeps its own slice; the backward all-gathers the bits'
+# gradients once and runs the mapper's backward on the global batch, each
+# rank reducing only its own tiles' parameter-gradient partials (the
+# gradient all-reduce then sums the ranks' shares).  Bits, BatchNorm batch
+# and running statistics, EMA min / max and the mapper's input gradients are
+# the single-process values bit for bit; 2 collectives instead of 7.
+# False: the staged per-layer collectives (also taken when a rank's tile
+# count of a scale is not a multiple of the kernels' 64-tile workgroups).
+DP_GLOBAL_MAPPER = True
+_TR_TPB = 64            # tiles per mapper workgroup (csrc/mcaq_train.h TR_TPB)
+
+
+def _consecutive(ts):
+    """The flat concatenation of ts when they already lie back to back in one
+    buffer (no copy), else None."""
+    if not all(t.is_contiguous() and t.dtype == torch.float32 for t in ts):
+        return None
+    st = ts[0].untyped_storage()
+    o = ts[0].storage_offset()
+    for t in ts:
+        if t.untyped_storage().data_ptr() != st.data_ptr() or t.storage_offset() != o:
+            return None
+        o += t.numel()
+    out = torch.empty(0, dtype=torch.float32, device=ts[0].device)
+    out.set_(st, ts[0].storage_offset(), (o - ts[0].storage_offset(),))
+    return out
+
+
+def _dp_exchange(parts, specs, pg):
+    """all-gather the concatenation of `parts` (this rank's flat fp32 pieces)
+    over pg in ONE collective and unpack it in ONE launch: specs are
+    (out, offset in the send buffer, n, mode) - mode 0 writes the pieces of
+    every rank back to back (world * n), mode 1 / 2 the min / max over ranks."""
+    import torch.distributed as dist
+    world = dist.get_world_size(pg)
+    send = _consecutive(parts)
+    if send is None:
+        send = torch.cat(parts)
+    g = core._all_gather_flat(send, pg, world)
+    arr = (abi.DpSeg * len(specs))()
+    for a, (out, off, n, mode) in zip(arr, specs):
+        a.out, a.off, a.n, a.mode = _p(out), off, n, mode
+    abi.check(abi.lib().mcaq_dp_unpack(_p(g), world, send.numel(), arr, len(specs), _stream()), "mcaq_dp_unpack")
+    return g
+
+
+def _dp_mapper_inputs(mapper, ncs, box, with_minmax):
+    """The global-batch mapper inputs of every scale (and, riding along, the
+    quantizers' global batch min / max written into box) - or None when the
+    sharded step keeps the staged collectives."""
+    if not DP_GLOBAL_MAPPER or not isinstance(mapper, core.ComplexityToBitMappingNetwork):
+        return None
+    pg = core._mapper_group(mapper.mapping_network)
+    if pg is None or any(c.numel() % _TR_TPB for c in ncs):
+        return None
+    if len(ncs) * 3 > abi.MCAQ_DP_MAXSEG:
+        return None
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(pg), dist.get_rank(pg)
+    cf = [_f32c(c).reshape(-1) for c in ncs]
+    parts, specs, cg, o = list(cf), [], [], 0
+    for c in cf:
+        g = torch.empty(world * c.numel(), device=c.device)
+        cg.append(g)
+        specs.append((g, o, c.numel(), 0))
+        o += c.numel()
+    if with_minmax:
+        for b in box[:len(ncs)]:
+            for key, mode in (("bmin", 1), ("bmax", 2)):
+                t = b[key]
+                parts.append(t)
+                specs.append((t, o, t.numel(), mode))      # written in place: the global batch's
+                o += t.numel()
+            b["bglobal"] = True
+    _dp_exchange(parts, specs, pg)
+    return {"cg": cg, "rank": rank, "world": world, "pg": pg}
+
+
 class _MapperMulti(torch.autograd.Function):
     """Train-mode bit mapper of every scale: 4 forward launches (one per
     batch-statistics barrier) + the running-statistics update in scale order;
@@ -402,16 +489,17 @@ class _MapperMulti(torch.autograd.Function):
         T = max(float(temperature), 0.1) if temperature is not None else 0.0
         segs = (abi.MapperSeg * n)()
         cfs, works, bits = [], [], []
+        dp = getattr(mod, "_dp", None)       # batch sharded: the global batch (_dp_mapper_inputs)
         for i, c in enumerate(cs):
-            cf = _f32c(c).reshape(-1)
+            cf = _f32c(c).reshape(-1) if dp is None else dp["cg"][i]
             m = cf.numel()
             w = torch.empty(L.mcaq_mapper_work_floats(m), device=dev)
             b = torch.empty(m, device=dev)
             cfs.append(cf); works.append(w); bits.append(b)
             segs[i].c, segs[i].bits, segs[i].work, segs[i].n = _p(cf), _p(b), _p(w), m
         mom = float(bns[0].momentum)
-        pg = core._mapper_group(net)
-        ctx.pg, ctx.gath1, ctx.world = pg, None, 1
+        pg = core._mapper_group(net) if dp is None else None
+        ctx.pg, ctx.gath1, ctx.world, ctx.dp = pg, None, 1, dp
         if pg is None:
             abi.check(L.mcaq_mapper_train_forward_multi(ctypes.byref(q), segs, n, mod.min_bits, mod.max_bits, T,
                                                         mom, 0 if return_continuous else 1, 2, _stream()),
@@ -437,7 +525,7 @@ class _MapperMulti(torch.autograd.Function):
             ctx.gath1, ctx.world = gath[1], world
         wa = (abi.P * n)(*[_p(w) for w in works])
         na = (abi.I * n)(*[c.numel() for c in cfs])
-        if pg is None and getattr(mod, "_defer_running", False):
+        if pg is None and getattr(mod, "_defer_running", False):    # (sharded on the global batch too)
             # the quantizers' EMA launch that follows applies it (forward_features)
             mod._pending_running = (q, wa, na, n, mom)
         else:
@@ -445,6 +533,9 @@ class _MapperMulti(torch.autograd.Function):
         ctx.q, ctx.T, ctx.mod, ctx.n = q, T, mod, n
         ctx.shapes = [c.shape for c in cs]
         ctx.save_for_backward(*cfs, *works, *params)
+        if dp is not None:       # this rank's tiles of the global batch
+            r = dp["rank"]
+            return tuple(b[r * c.numel():(r + 1) * c.numel()].view(c.shape) for b, c in zip(bits, cs))
         return tuple(b.view(c.shape) for b, c in zip(bits, cs))
 
     @staticmethod
@@ -456,14 +547,38 @@ class _MapperMulti(torch.autograd.Function):
         dev = cfs[0].device
         segs = (abi.MapperSeg * n)()
         gcs, gparts, keep = [], [], []
+        dp = ctx.dp
+        gls = [(_f32c(gbits[i]).reshape(-1) if gbits[i] is not None else
+                torch.zeros(ctx.shapes[i].numel(), device=dev)) for i in range(n)]
+        if dp is not None:
+            # every rank's bit gradients of every scale: ONE all-gather
+            r, world = dp["rank"], dp["world"]
+            ggs, specs, o = [], [], 0
+            for g in gls:
+                gg = torch.empty(world * g.numel(), device=dev)
+                ggs.append(gg)
+                specs.append((gg, o, g.numel(), 0))
+                o += g.numel()
+            keep.append(_dp_exchange(gls, specs, dp["pg"]))
+            gls = ggs
         for i in range(n):
             m = cfs[i].numel()
-            g = _f32c(gbits[i]).reshape(-1) if gbits[i] is not None else torch.zeros(m, device=dev)
+            g = gls[i]
             gc = torch.empty(m, device=dev)
             gp = torch.empty(L.mcaq_mapper_gpart_floats(m), device=dev)
             keep.append(g)
-            gcs.append(gc)
-            gparts.append((gp, gp.numel() // core._MAPPER_G_SIZE))   # one partial per backward workgroup
+            npart = gp.numel() // core._MAPPER_G_SIZE             # one partial per backward workgroup
+            if dp is not None:
+                # this rank's share of the parameter gradients: its own tiles'
+                # workgroups (whole workgroups: _TR_TPB divides its tile count)
+                ml = ctx.shapes[i].numel()
+                gcs.append(gc[r * ml:(r + 1) * ml])
+                nl = ml // _TR_TPB
+                gparts.append((gp[r * nl * core._MAPPER_G_SIZE:(r + 1) * nl * core._MAPPER_G_SIZE], nl))
+                keep.append(gp)
+            else:
+                gcs.append(gc)
+                gparts.append((gp, npart))
             s = segs[i]
             s.c, s.work, s.gbits, s.gc, s.gpart, s.n = _p(cfs[i]), _p(works[i]), _p(g), _p(gc), _p(gp), m
         ride = _PENDING_SM_REDUCE["segs"] if ctx.pg is None else None
@@ -498,7 +613,7 @@ class _MapperMulti(torch.autograd.Function):
         sink = mod._gsink.target(list(mod.mapping_network.parameters()))
         gflat, acc = sink if sink is not None else (torch.empty(core._MAPPER_G_SIZE, device=dev), 0)
         if sink is not None and ctx.pg is None and _PENDING_REDUCE["segs"] is None:
-            _PENDING_REDUCE["segs"] = (_chain_segs(gparts, gflat, acc, core._MAPPER_G_SIZE), n, gparts)
+            _PENDING_REDUCE["segs"] = (_chain_segs(gparts, gflat, acc, core._MAPPER_G_SIZE), n, (gparts, keep))
             torch.autograd.Variable._execution_engine.queue_callback(_flush_pending_reduce)
         else:
             _reduce_chain(gparts, gflat, acc, core._MAPPER_G_SIZE)
@@ -655,6 +770,10 @@ class _MaskQuantMulti(torch.autograd.Function):
         segs = (abi.QatSmaskSeg * n)()
         rsegs = (abi.ReduceSeg * n)()
         gxs, gbs, gflats, keep = [], [], [], []
+        # the scales' bit-map gradients back to back in one buffer (a sharded
+        # step all-gathers them as they are, _MapperMulti.backward)
+        gb_all = torch.empty(sum(b.numel() for b in bits), device=xs[0].device)
+        gbo = 0
         for i in range(n):
             x = xs[i]
             B, C, H, W = x.shape
@@ -667,7 +786,8 @@ class _MaskQuantMulti(torch.autograd.Function):
             arr[i] = q
             gxs.append(gx)
             _, ht, wt = bits[i].shape
-            gb = torch.empty(B, ht, wt, device=x.device)
+            gb = gb_all[gbo:gbo + B * ht * wt].view(B, ht, wt)
+            gbo += B * ht * wt
             gp = torch.empty(L.mcaq_smask_gpart_floats(B), device=x.device)
             gf = torch.empty(core._SM_SIZE, device=x.device)
             keep.append(gp)
@@ -839,13 +959,15 @@ def forward_features(hooks, feats, state):
             ncs = [core._normalize_complexity_shape(c) for c in cs]
             # the mapper's running-statistics update rides on the EMA launch
             mapper._defer_running, mapper._pending_running = not per_quantizer, None
+            # batch sharded: the mapper on the global batch, EMA min / max riding along
+            mapper._dp = _dp_mapper_inputs(mapper, ncs, box, with_minmax=not per_quantizer)
             bits = list(_MapperMulti.apply(mapper, T, True, n, *ncs, *mapper.mapping_network.parameters()))
         else:
             bits = [mapper(c, T, return_continuous=True) for c in cs]
         return _quantize_multi(hooks, feats, state, n, idxs, xs, box, cs, bits, qs, per_quantizer)
     finally:
         pend = getattr(mapper, "_pending_running", None)
-        mapper._defer_running, mapper._pending_running = False, None
+        mapper._defer_running, mapper._pending_running, mapper._dp = False, None, None
         if pend is not None:
             _flush_running(pend)
 

@@ -229,7 +229,12 @@ def test_group_batchnorm_large_mean_two_ranks():
 def _sink_worker(rank, world):
     from mcaq_yolo_amd import core
     p = torch.nn.Parameter(torch.zeros(3))
-    return core._grads_observed([p]), core._GradSink().target([p]) is None
+    r = (core._grads_observed([p]), core._GradSink().target([p]) is None)
+    # marked by dist.shard_hooks (this package's own gradient all-reduce, no
+    # DDP reducer): the sinks stay on
+    q = torch.nn.Parameter(torch.zeros(3))
+    q._mcaq_dp_manual = True
+    return r + (core._grads_observed([q]), core._GradSink().target([q]) is None)
 
 
 def test_direct_grad_accumulation_off_under_torch_distributed():
@@ -245,13 +250,13 @@ def test_direct_grad_accumulation_off_under_torch_distributed():
     q.register_post_accumulate_grad_hook(lambda t: None)
     assert core._grads_observed([q])
     res = _run("_sink_worker")
-    assert [tuple(res[r]) for r in range(2)] == [(True, True), (True, True)]
+    assert [tuple(res[r]) for r in range(2)] == [(True, True, False, False), (True, True, False, False)]
 
 
 def test_allreduce_gradients_cached_pattern_no_host_sync():
-    """Second and later calls with the same parameters and local has-grad
-    pattern reuse the global pattern: no device-to-host read (.tolist()),
-    so the call can sit inside a captured step.  World size 1 (gloo)."""
+    """static_pattern=True: second and later calls reuse the global pattern
+    agreed on the first: no device-to-host read (.tolist()), so the call can
+    sit inside a captured step.  World size 1 (gloo)."""
     import os
     import torch.distributed as dist
     from mcaq_yolo_amd import dist as mdist
@@ -262,7 +267,7 @@ def test_allreduce_gradients_cached_pattern_no_host_sync():
         a = torch.nn.Parameter(torch.ones(3))
         b = torch.nn.Parameter(torch.ones(2))
         a.grad = torch.full((3,), 2.0)
-        mdist.allreduce_gradients([a, b], dist.group.WORLD)
+        mdist.allreduce_gradients([a, b], dist.group.WORLD, static_pattern=True)
         assert b.grad is None and torch.equal(a.grad, torch.full((3,), 2.0))
         calls = {"n": 0}
         orig = torch.Tensor.tolist
@@ -273,9 +278,70 @@ def test_allreduce_gradients_cached_pattern_no_host_sync():
         torch.Tensor.tolist = spy
         try:
             a.grad = torch.full((3,), 5.0)
-            mdist.allreduce_gradients([a, b], dist.group.WORLD)
+            mdist.allreduce_gradients([a, b], dist.group.WORLD, static_pattern=True)
         finally:
             torch.Tensor.tolist = orig
         assert calls["n"] == 0 and b.grad is None and torch.equal(a.grad, torch.full((3,), 5.0))
     finally:
         dist.destroy_process_group()
+
+
+def _changing_pattern_worker(rank, world, static):
+    """ADVICE r5: rank 1 leaves b's gradient None on the second call only;
+    the ranks' buckets must still match (gloo aborts on a size mismatch)."""
+    from mcaq_yolo_amd import dist as mdist
+    a = torch.nn.Parameter(torch.zeros(3))
+    b = torch.nn.Parameter(torch.zeros(2))
+    out = []
+    for call in range(3):
+        a.grad = torch.full((3,), float(rank + 1))
+        b.grad = None if (rank == 1 and call == 1) else torch.full((2,), 10.0 * (rank + 1))
+        mdist.allreduce_gradients([a, b], dist.group.WORLD, static_pattern=static)
+        out.append((a.grad.numpy().copy(), None if b.grad is None else b.grad.numpy().copy()))
+    return out
+
+
+@pytest.mark.parametrize("static", [False, True])
+def test_allreduce_gradients_local_pattern_changes(static):
+    res = _run("_changing_pattern_worker", 2, static)
+    for r in range(2):
+        for call in range(3):
+            a, b = res[r][call]
+            assert np.array_equal(a, np.full(3, 1.5, np.float32))
+            # call 1: only rank 0 contributes b (a None sends zeros): (10 + 0) / 2
+            assert np.array_equal(b, np.full(2, 5.0 if call == 1 else 15.0, np.float32))
+
+
+def _static_unused_worker(rank, world):
+    from mcaq_yolo_amd import dist as mdist
+    a = torch.nn.Parameter(torch.zeros(3))
+    b = torch.nn.Parameter(torch.zeros(2))
+    a.grad = torch.ones(3)
+    mdist.allreduce_gradients([a, b], dist.group.WORLD, static_pattern=True)     # b unused everywhere: cached
+    first = b.grad is None
+    b.grad = torch.ones(2)
+    try:
+        mdist.allreduce_gradients([a, b], dist.group.WORLD, static_pattern=True)
+        raised = False
+    except ValueError:
+        raised = True
+    return first, raised
+
+
+def test_allreduce_gradients_static_pattern_rejects_new_gradient():
+    res = _run("_static_unused_worker")
+    assert [tuple(res[r]) for r in range(2)] == [(True, True), (True, True)]
+
+
+def test_flat_span_in_place_bucket():
+    """Gradients tiling one buffer (the hook nets' sink arena) are reduced in
+    place as that buffer; anything else is not a span."""
+    from mcaq_yolo_amd.dist import _flat_span
+    buf = torch.arange(10, dtype=torch.float32)
+    g = [buf[4:10], buf[0:3], buf[3:4]]
+    sp = _flat_span(g)
+    assert sp is not None and sp.data_ptr() == buf.data_ptr() and sp.numel() == 10
+    assert _flat_span([buf[0:3], buf[4:10]]) is None          # gap
+    assert _flat_span([buf[0:3], torch.zeros(2)]) is None      # two buffers
+    sp.mul_(2)
+    assert torch.equal(buf, 2 * torch.arange(10, dtype=torch.float32))

@@ -4,16 +4,18 @@ test_dist_hooks.py does for inference) against the single-process step on the
 global batch.
 
 dist.shard_hooks swaps the mapper's BatchNorm1d layers for GroupBatchNorm1d;
-the fused train-mode kernels run them (statistics over every rank's tiles,
-collectives between the stage launches, csrc/mcaq_train.h), the quantizers'
-EMA min/max are all-reduced, and dist.allreduce_gradients sums the hook
-parameters' gradients.  The loss is a sum over samples, so the ranks' losses
+the fused train-mode kernels run the mapper on the GLOBAL batch of tiles (one
+all-gather of its inputs with the quantizers' EMA min/max riding along, one
+of the bit gradients in the backward: train_step.DP_GLOBAL_MAPPER), and
+dist.allreduce_gradients sums the hook parameters' gradients (the ranks'
+shares of the mapper's).  The loss is a sum over samples, so the ranks' losses
 add up to the single-process loss and the summed gradients must equal its
 gradients.
 
-Tolerances (fp32 sums in other orders; the BatchNorm statistics combine
-per-rank partials instead of per-workgroup ones): bits and y 1e-5 / 1e-4
-relative, running statistics 1e-5, gradients as test_train_fused_gpu.py
+Bits, y, feature gradients and every buffer (EMA and BatchNorm running
+statistics) are bit-identical to the single process.  Parameter gradients
+are fp32 sums in other orders (the ranks' shares added by the all-reduce):
+as test_train_fused_gpu.py
 (1e-3 of the tensor's largest magnitude; the Linear layers feeding a
 train-mode BatchNorm 1e-4 of the module's largest gradient)."""
 import os
@@ -165,10 +167,12 @@ def test_sharded_qat_step_equals_single_process():
         r_outs, r_bits, r_gx, r_grads, r_bufs, r_nfused = res[r]
         assert r_nfused == 3, "the sharded step must run the fused mapper kernels"
         sl = slice(r * n, (r + 1) * n)
+        # the mapper runs on the global batch (train_step.DP_GLOBAL_MAPPER):
+        # bits, y, feature gradients and buffers are the single process's
         for s in range(3):
-            _rel(r_bits[s], bits[s][sl], 1e-5, what="bits %d" % s)
-            _rel(r_outs[s], outs[s][sl], 1e-4, what="y %d" % s)
-            _rel(r_gx[s], gx[s][sl], 1e-3, floor=1e-12, what="grad x %d" % s)
+            assert np.array_equal(r_bits[s], bits[s][sl]), "bits %d" % s
+            assert np.array_equal(r_outs[s], outs[s][sl]), "y %d" % s
+            assert np.array_equal(r_gx[s], gx[s][sl]), "grad x %d" % s
         assert set(r_grads) == set(grads)
         for k, v in grads.items():
             mod = k.rsplit(".", 2)[0]
@@ -178,4 +182,4 @@ def test_sharded_qat_step_equals_single_process():
             else:
                 _rel(r_grads[k], v, 1e-3, floor=1e-3 * gmax[mod], what=k)
         for k, v in bufs.items():
-            _rel(r_bufs[k], v, 1e-5, floor=1e-6, what=k)
+            assert np.array_equal(r_bufs[k], v), k

@@ -112,7 +112,7 @@ def test_clip_adamw_graph_capture():
     torch.cuda.synchronize()
     for p, q in zip(ps, qs):
         assert torch.equal(p, q)
-    assert float(oa._step_t) == float(ob._step_t) == 4.0
+    assert all(float(oa.state[p]["step"]) == float(ob.state[q]["step"]) == 4.0 for p, q in zip(ps, qs))
 
 
 def test_clip_adamw_step_reaches_packed_blobs():
@@ -181,4 +181,65 @@ def test_clip_adamw_chunked_lists_match_torch(sizes):
                 q.copy_(p)
                 o1.state[q]["exp_avg"].copy_(o0.state[p]["exp_avg"])
                 o1.state[q]["exp_avg_sq"].copy_(o0.state[p]["exp_avg_sq"])
-    assert float(o1._step_t) == 4.0
+    assert all(float(o1.state[q]["step"]) == 4.0 for q in qs)
+
+
+def test_clip_adamw_step_after_load_state_dict_matches_torch():
+    """a GPU step after load_state_dict (following earlier steps)
+    rebuilds its launch descriptors against the re-homed moment buffers; the
+    run step, load, step equals torch's fused AdamW over the same three steps."""
+    from mcaq_yolo_amd.optim import ClipAdamW
+    torch.manual_seed(5)
+    ps = [torch.randn(n, device="cuda", requires_grad=True) for n in (97, 2048, 5)]
+    qs = [p.detach().clone().requires_grad_(True) for p in ps]
+    o0 = torch.optim.AdamW(ps, lr=1e-2, weight_decay=0.05, fused=True)
+    o1 = ClipAdamW(qs, lr=1e-2, weight_decay=0.05)
+    gs = [[torch.randn_like(p) for p in ps] for _ in range(3)]
+    for it in range(3):
+        for p, q, g in zip(ps, qs, gs[it]):
+            p.grad, q.grad = g.clone(), g.clone()
+        o0.step()
+        o1.step()
+        if it == 1:
+            o1.load_state_dict(o1.state_dict())
+    torch.cuda.synchronize()
+    for k, (p, q) in enumerate(zip(ps, qs)):
+        _close(q, p, 1e-5, "param %d" % k)
+        assert float(o1.state[q]["step"]) == 3.0
+
+
+def test_clip_adamw_per_parameter_steps_and_lr_table():
+    """a parameter without a gradient keeps its step (torch's
+    per-parameter counters), and an lr change reaches a captured step through
+    the device hyper-parameter table (sync_hyperparameters)."""
+    from mcaq_yolo_amd.optim import ClipAdamW
+    torch.manual_seed(6)
+    ps = [torch.randn(n, device="cuda", requires_grad=True) for n in (33, 700)]
+    qs = [p.detach().clone().requires_grad_(True) for p in ps]
+    o0 = torch.optim.AdamW(ps, lr=1e-2, weight_decay=0.05, fused=True)
+    o1 = ClipAdamW(qs, lr=1e-2, weight_decay=0.05)
+    g = [torch.randn_like(p) for p in ps]
+    # step 1: both; step 2: only the second parameter has a gradient
+    for p, q, gg in zip(ps, qs, g):
+        p.grad, q.grad = gg.clone(), gg.clone()
+    o0.step(); o1.step()
+    ps[0].grad = qs[0].grad = None
+    o0.step(); o1.step()
+    torch.cuda.synchronize()
+    assert float(o1.state[qs[0]]["step"]) == 1.0 and float(o1.state[qs[1]]["step"]) == 2.0
+    for k, (p, q) in enumerate(zip(ps, qs)):
+        _close(q, p, 1e-5, "param %d" % k)
+    # captured step, then lr halved between replays
+    qs[0].grad = g[0].clone()
+    ps[0].grad = g[0].clone()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        o1.step()
+    for gr in (o0.param_groups[0], o1.param_groups[0]):
+        gr["lr"] = 5e-3
+    o1.sync_hyperparameters()
+    o0.step()
+    graph.replay()
+    torch.cuda.synchronize()
+    for k, (p, q) in enumerate(zip(ps, qs)):
+        _close(q, p, 1e-5, "param %d after lr change" % k)

@@ -136,7 +136,7 @@ def test_sharded_qat_step_nccl_graph_equals_unsharded(dev, nccl1):
             loss = sum((o * g).sum() for o, g in zip(outs, G)) + sum((a["bit_map"] * gb).sum() for a, gb in zip(aux, GB))
             loss.backward()
             if sharded:
-                allreduce_gradients(params, nccl1, average=True)
+                allreduce_gradients(params, nccl1, average=True, static_pattern=True)
             rec["outs"] = [o.detach() for o in outs]
             rec["bits"] = [a["bit_map"].detach() for a in aux]
             rec["gx"] = [x.grad for x in xs]
@@ -159,9 +159,11 @@ def test_sharded_qat_step_nccl_graph_equals_unsharded(dev, nccl1):
     for _ in range(2):
         g.replay()
     torch.cuda.synchronize()
+    # the mapper runs on the global batch (train_step.DP_GLOBAL_MAPPER): at
+    # world 1 the forward values and feature gradients are the unsharded ones
     for k in ("outs", "bits", "gx"):
         for i, (a, b) in enumerate(zip(rec1[k], rec0[k])):
-            _rel(a.cpu().numpy(), b.cpu().numpy(), 1e-4, floor=1e-12, what="%s %d" % (k, i))
+            assert torch.equal(a, b), "%s %d" % (k, i)
     assert set(rec1["grads"]) == set(rec0["grads"])
     for k, v in rec0["grads"].items():
         _rel(rec1["grads"][k].cpu().numpy(), v.cpu().numpy(), 1e-3, floor=1e-3 * float(v.abs().max()) + 1e-30,
@@ -171,3 +173,51 @@ def test_sharded_qat_step_nccl_graph_equals_unsharded(dev, nccl1):
     assert set(b0) == set(b1)
     for k in b0:
         _rel(b1[k].cpu().numpy(), b0[k].cpu().numpy(), 1e-5, floor=1e-6, what=k)
+
+
+def test_sharded_qat_step_issues_three_collectives(dev, nccl1):
+    """the batch-sharded QAT step (dist.shard_hooks) keeps the
+    fused fast path - gradient sinks in one arena, the mapper on the global
+    batch - and issues 3 collectives per step: the forward all-gather (mapper
+    inputs + EMA min / max), the backward all-gather (bit gradients) and ONE
+    in-place gradient all-reduce over the arena (no concatenation)."""
+    import torch
+    import torch.distributed as dist
+    from mcaq_yolo_amd.dist import allreduce_gradients, shard_hooks
+    from test_dist_qat_gpu import B, _hooks, _inputs
+    feats, G, _ = _inputs()
+    G = [g.to(dev) for g in G]
+    h = shard_hooks(_hooks(dev), nccl1, 0, 1, B)
+    xs = [f.to(dev).requires_grad_(True) for f in feats]
+    params = [p for p in h.parameters() if p.requires_grad]
+    arena = h._grad_arena.flat
+
+    def step():
+        for p in params:
+            p.grad = None
+        outs, aux = h.forward_features(xs, temperature=1.0)
+        torch.autograd.backward(list(outs) + [h.bit_budget_loss(aux, 4.0)],
+                                list(G) + [torch.full((), 0.1, device=dev)])
+        allreduce_gradients(params, nccl1, static_pattern=True)
+    step()
+    calls = []
+    names = ("all_reduce", "all_gather", "all_gather_into_tensor", "broadcast", "reduce_scatter_tensor")
+    orig = {n: getattr(dist, n) for n in names}
+
+    def spy(n):
+        def f(t, *a, **k):
+            calls.append((n, t))
+            return orig[n](t, *a, **k)
+        return f
+    for n in names:
+        setattr(dist, n, spy(n))
+    try:
+        step()
+    finally:
+        for n in names:
+            setattr(dist, n, orig[n])
+    torch.cuda.synchronize()
+    assert [c[0] for c in calls] == ["all_gather_into_tensor", "all_gather_into_tensor", "all_reduce"], calls
+    red = calls[-1][1]
+    assert red.data_ptr() == arena.data_ptr() and red.numel() == arena.numel()
+    assert all(p.grad.untyped_storage().data_ptr() == arena.untyped_storage().data_ptr() for p in params)

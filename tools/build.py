@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "mcaq_yolo_amd", "csrc")
 OUT = os.path.join(ROOT, "mcaq_yolo_amd", "lib", "libmcaq_hip.so")
 SRCS = [os.path.join(CSRC, "mcaq_kernels.hip")]
-DEPS = SRCS + [os.path.join(CSRC, f) for f in ("mcaq_math.h", "mcaq_morph.h", "mcaq_band.h", "mcaq_tiles_batch.h", "mcaq_tables.h", "mcaq_mlp_mfma.h", "mcaq_qat.h", "mcaq_nms.h", "mcaq_train.h", "mcaq_optim.h")] + \
+DEPS = SRCS + [os.path.join(CSRC, f) for f in ("mcaq_math.h", "mcaq_morph.h", "mcaq_band.h", "mcaq_tiles_batch.h", "mcaq_tables.h", "mcaq_mlp_mfma.h", "mcaq_qat.h", "mcaq_nms.h", "mcaq_train.h", "mcaq_optim.h", "mcaq_dp.h")] + \
     [os.path.join(ROOT, "include", "mcaq_hip.h")]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
