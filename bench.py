@@ -94,30 +94,50 @@ def hook_state_dict(device):
 
 
 def cpu_baseline_qat(budget_s=12.0):
-    """Oracle QAT quantizer (EMA + fractional-bit forward + STE backward, the
-    per-element part of the step) on one image per scale, ~budget_s seconds."""
-    import numpy as np
-    from oracle import mcaq_oracle as O
+    """The same QAT step on the host: this package's pure-PyTorch CPU path
+    (core / fallback.py modules in train mode - the reference's own
+    _forward_pytorch training branch, EMA statistics, train-mode mapper,
+    soft mask, fractional-bit STE quantizer), the bit-budget loss, backward,
+    and optim.ClipAdamW's torch-op step, at config 5's per-GPU batch, on the
+    process's torch threads; whole steps repeated for ~budget_s seconds."""
+    from mcaq_yolo_amd.hooks import MCAQHooks
+    from mcaq_yolo_amd.optim import ClipAdamW
     name, B, chans, grid, mapper = QAT_CONFIG
-    rng = np.random.default_rng(0)
-    xs = [synth_features(1, c, h, wd, 5000 + i, "cpu").numpy() for i, (c, (h, wd)) in enumerate(zip(chans, SIZES))]
-    gs = [rng.standard_normal(x.shape).astype(np.float32) for x in xs]
-    bs = [rng.uniform(2, 8, (1, h // 8, wd // 8)).astype(np.float32) for (h, wd) in SIZES]
-    ms = [rng.uniform(0.9, 1.0, (1, h, wd)).astype(np.float32) for (h, wd) in SIZES]
+    cpu = torch.device("cpu")
+    torch.manual_seed(0)
+    h = MCAQHooks(grid_size=grid, bit_mapping=mapper, device=cpu)
+    h.load_state_dict(hook_state_dict(cpu), strict=False)
+    h.train()
+    feats = [synth_features(B, c, hh, ww, 5000 + i, "cpu").requires_grad_(True)
+             for i, (c, (hh, ww)) in enumerate(zip(chans, SIZES))]
+    gen = torch.Generator(device="cpu").manual_seed(77)
+    G = [1e-3 * torch.randn(f.shape, generator=gen) for f in feats]
+    ps = [p for p in h.parameters() if p.requires_grad]
+    opt = ClipAdamW(ps, lr=1e-3, weight_decay=0.05, betas=(0.9, 0.999), max_norm=1.0,
+                    project_abs=h.bit_mapper.constrained_weights())
+    w_bit = torch.full((), 0.1)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        for f in feats:
+            f.grad = None
+        outs, aux = h.forward_features(feats, temperature=1.0)
+        torch.autograd.backward(list(outs) + [h.bit_budget_loss(aux, 4.0)], list(G) + [w_bit])
+        opt.step()
+    step()              # warm-up (lazy state)
     t0 = time.perf_counter()
     n = 0
     while True:
-        for x, g, b, m in zip(xs, gs, bs, ms):
-            rmin, rmax = O.ema_running_stats(x)
-            O.qat_forward(x, b, rmin, rmax, m)
-            O.qat_backward(g, x, b, rmin, rmax, m)
+        step()
         n += 1
         if time.perf_counter() - t0 > budget_s:
             break
     dt = time.perf_counter() - t0
-    return {"value": round(n / dt, 4), "unit": "images/s", "cores": 1, "kind": "port",
-            "sample": "%d images x 3 hook scales (%s, batch 1): EMA stats + QAT forward + STE backward through "
-                      "oracle/mcaq_oracle.py, single-threaded numpy, %.1f s (quantizer only)" % (n, name, dt)}
+    return {"value": round(n * B / dt, 3), "unit": "images/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": "%d whole QAT steps of %s bs%d (3 hook scales, train mode, bit-budget loss, backward, "
+                      "clip + AdamW + |W|) on this package's pure-PyTorch CPU path (the reference's "
+                      "_forward_pytorch training branch), %d torch threads, %.1f s"
+                      % (n, name, B, torch.get_num_threads(), dt)}
 
 
 def main_qat(args, world, rank, dev, pg):

@@ -44,7 +44,11 @@ typedef void* hipEvent_t;
 extern "C" {
 #endif
 
-#define MCAQ_ABI_VERSION 25
+#define MCAQ_ABI_VERSION 27
+/* feature-map element types (mcaq_stats_scale.dtype, mcaq_quant_scale.dtype) */
+#define MCAQ_DTYPE_F32 0
+#define MCAQ_DTYPE_F16 1
+#define MCAQ_DTYPE_BF16 2
 /* segments (hook scale x batch) per mcaq_stats / mcaq_finalize /
  * mcaq_morph* / mcaq_quant launch */
 #define MCAQ_MAX_SEGMENTS 9
@@ -73,13 +77,15 @@ int mcaq_launch_spatial_quantization(const float* input, const float* bit_map,
  *                  pixels of one image: mcaq_stats_units(B,C,H,W) x C floats
  *                  each (NULL to skip). */
 typedef struct {
-  const float* x;  /* (B, C, H, W) fp32 contiguous */
+  const float* x;  /* (B, C, H, W) contiguous, of element type `dtype` */
   float* gray;     /* (B, Hc, Wc) */
   float* absmean;  /* (B, H, W) */
   float* pmin;
   float* pmax;
   int B, C, H, W, Hc, Wc;
   int unit_begin;  /* set by the launcher */
+  int dtype;       /* element type of x: MCAQ_DTYPE_F32 / _F16 / _BF16 (one per launch);
+                      fp16 / bf16 widen exactly, every sum stays fp32 */
 } mcaq_stats_scale;
 int mcaq_stats(const mcaq_stats_scale* scales, int nscales, hipStream_t stream);
 int mcaq_stats_units(int B, int C, int H, int W);
@@ -163,8 +169,8 @@ size_t mcaq_morph_work_bytes(int B, int Hc, int Wc, int tile);
 
 /* ---- pass 2: y = dequant(quant_b(x)) * m ----------------------------------- */
 typedef struct {
-  const float* x;      /* (B, C, H, W) */
-  float* y;            /* (B, C, H, W) */
+  const float* x;      /* (B, C, H, W), element type `dtype` */
+  float* y;            /* (B, C, H, W), element type `ydtype` */
   const float* bits;   /* (B, ht, wt) integer-valued */
   const float* m;      /* (B, H, W) or NULL */
   const float* mt;     /* (B, ht, wt) soft-mask tile values: when set, m(p) is
@@ -183,6 +189,12 @@ typedef struct {
                           finite x and take the shorter arithmetic; 0: any x
                           (frozen / external statistics) */
   int neg_min;         /* 1: xmin holds -min (mcaq_finalize_scale.neg_min) */
+  int dtype;           /* element type of x (MCAQ_DTYPE_*, one per launch): fp16 / bf16
+                          maps widen exactly and the arithmetic is fp32; they take
+                          the tile-aligned kernel only (otherwise hipErrorNotSupported) */
+  int ydtype;          /* element type of y: dtype, or MCAQ_DTYPE_F32 (the reference's
+                          promotion: an fp16 map times the fp32 soft mask is fp32,
+                          quantization.py:742-744); rounded to nearest even */
 } mcaq_quant_scale;
 int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream);
 
@@ -475,6 +487,9 @@ typedef struct {
   const float* part;     /* [nparts][stride] partial sums */
   float* out;            /* count floats (chain: segment 0's only) */
   int nparts, stride, count, accumulate;
+  float scale;           /* 0 or 1: none; else the launch's sum times scale, then
+                            accumulated (chain: segment 0's applies) - a data-parallel
+                            rank's 1 / world share of a gradient it computed whole */
 } mcaq_reduce_seg;
 /* chain 0: out_k (+)= sum of segment k's partials; chain 1: segment 0's out
  * = s_0 (+ out if accumulate) + s_1 + s_2 in segment order (the values of

@@ -9,7 +9,8 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libmcaq_hip.so")
-ABI_VERSION = 25
+ABI_VERSION = 27
+DTYPE_F32, DTYPE_F16, DTYPE_BF16 = 0, 1, 2   # MCAQ_DTYPE_*
 MAX_SEGMENTS = 9   # MCAQ_MAX_SEGMENTS: segments (hook scale x batch) per launch
 
 P = ctypes.c_void_p
@@ -19,7 +20,7 @@ Fl = ctypes.c_float
 
 class StatsScale(ctypes.Structure):
     _fields_ = [("x", P), ("gray", P), ("absmean", P), ("pmin", P), ("pmax", P),
-                ("B", I), ("C", I), ("H", I), ("W", I), ("Hc", I), ("Wc", I), ("unit_begin", I)]
+                ("B", I), ("C", I), ("H", I), ("W", I), ("Hc", I), ("Wc", I), ("unit_begin", I), ("dtype", I)]
 
 
 class FinalizeScale(ctypes.Structure):
@@ -42,7 +43,7 @@ class QuantScale(ctypes.Structure):
     _fields_ = [("x", P), ("y", P), ("bits", P), ("m", P), ("mt", P), ("xmin", P), ("xmax", P),
                 ("B", I), ("C", I), ("H", I), ("W", I), ("ht", I), ("wt", I),
                 ("bits_lo", I), ("nbits", I), ("compat_tile_h", I), ("compat_tile_w", I), ("unit_begin", I),
-                ("stats_cover_x", I), ("neg_min", I)]
+                ("stats_cover_x", I), ("neg_min", I), ("dtype", I), ("ydtype", I)]
 
 
 class QatScale(ctypes.Structure):
@@ -106,7 +107,8 @@ class QatSmaskSeg(ctypes.Structure):
 
 class ReduceSeg(ctypes.Structure):
     """mcaq_reduce_seg."""
-    _fields_ = [("part", P), ("out", P), ("nparts", I), ("stride", I), ("count", I), ("accumulate", I)]
+    _fields_ = [("part", P), ("out", P), ("nparts", I), ("stride", I), ("count", I), ("accumulate", I),
+                ("scale", Fl)]
 
 
 MCAQ_OPT_MAXSEG, MCAQ_OPT_MAXGROUPS = 64, 4

@@ -117,6 +117,61 @@ __device__ __forceinline__ void wave_minmax16(float (&mn)[ST_CG], float (&mx)[ST
   omn = a; omx = b;
 }
 
+// ---- feature element types (MCAQ_DTYPE_*): fp32, or the fp16 / bf16 maps an
+// autocast region hands the hooks.  Loads widen exactly to fp32 (all
+// arithmetic stays fp32: the analyzer's gray / |x| sums are those of
+// x.float(), morphology.py:834-837); stores round to nearest even.
+typedef float mcaq_f4v __attribute__((ext_vector_type(4)));
+typedef _Float16 mcaq_h4v __attribute__((ext_vector_type(4)));
+typedef unsigned short mcaq_u4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float bf16_f(unsigned short u) { return __uint_as_float((unsigned)u << 16); }
+__device__ __forceinline__ unsigned short f_bf16(float f) {
+  const unsigned u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (unsigned short)((u >> 16) | 0x40u);   // quiet NaN
+  return (unsigned short)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+template <typename T> struct ElemIO;
+template <> struct ElemIO<float> {
+  static __device__ __forceinline__ float ld(const float* p) { return *p; }
+  static __device__ __forceinline__ mcaq_f4v ld4(const float* p, bool nt) {
+    return nt ? __builtin_nontemporal_load(reinterpret_cast<const mcaq_f4v*>(p)) : *reinterpret_cast<const mcaq_f4v*>(p);
+  }
+  static __device__ __forceinline__ float2 ld2(const float* p) { return *reinterpret_cast<const float2*>(p); }
+  static __device__ __forceinline__ void st4(float* p, mcaq_f4v v, bool nt) {
+    if (nt) __builtin_nontemporal_store(v, reinterpret_cast<mcaq_f4v*>(p));
+    else *reinterpret_cast<mcaq_f4v*>(p) = v;
+  }
+};
+template <> struct ElemIO<_Float16> {
+  static __device__ __forceinline__ float ld(const _Float16* p) { return (float)*p; }
+  static __device__ __forceinline__ mcaq_f4v ld4(const _Float16* p, bool nt) {
+    const mcaq_h4v h = nt ? __builtin_nontemporal_load(reinterpret_cast<const mcaq_h4v*>(p))
+                          : *reinterpret_cast<const mcaq_h4v*>(p);
+    return __builtin_convertvector(h, mcaq_f4v);
+  }
+  static __device__ __forceinline__ float2 ld2(const _Float16* p) { return make_float2((float)p[0], (float)p[1]); }
+  static __device__ __forceinline__ void st4(_Float16* p, mcaq_f4v v, bool nt) {
+    const mcaq_h4v h = __builtin_convertvector(v, mcaq_h4v);
+    if (nt) __builtin_nontemporal_store(h, reinterpret_cast<mcaq_h4v*>(p));
+    else *reinterpret_cast<mcaq_h4v*>(p) = h;
+  }
+};
+struct Bf16 { unsigned short u; };
+template <> struct ElemIO<Bf16> {
+  static __device__ __forceinline__ float ld(const Bf16* p) { return bf16_f(p->u); }
+  static __device__ __forceinline__ mcaq_f4v ld4(const Bf16* p, bool nt) {
+    const mcaq_u4v u = nt ? __builtin_nontemporal_load(reinterpret_cast<const mcaq_u4v*>(p))
+                          : *reinterpret_cast<const mcaq_u4v*>(p);
+    return mcaq_f4v{bf16_f(u.x), bf16_f(u.y), bf16_f(u.z), bf16_f(u.w)};
+  }
+  static __device__ __forceinline__ float2 ld2(const Bf16* p) { return make_float2(bf16_f(p[0].u), bf16_f(p[1].u)); }
+  static __device__ __forceinline__ void st4(Bf16* p, mcaq_f4v v, bool nt) {
+    const mcaq_u4v u = mcaq_u4v{f_bf16(v.x), f_bf16(v.y), f_bf16(v.z), f_bf16(v.w)};
+    if (nt) __builtin_nontemporal_store(u, reinterpret_cast<mcaq_u4v*>(p));
+    else *reinterpret_cast<mcaq_u4v*>(p) = u;
+  }
+};
+
 // Fold one 16-row block sum into cascade levels a1..a3 (Cascade::push at i % 16 == 0).
 struct Fold {
   float a0, a1, a2, a3;
@@ -136,7 +191,8 @@ struct Fold {
 // Tail-column order (ATen row_sum: 4 interleaved cascades over channels
 // c = 4r + k, leftovers into partial 0) of pixel p, for x and |x| at once;
 // the per-pixel slow path (C > 1024).
-__device__ __noinline__ void tail_sums(const float* xb, int HW, int p, int C, float& og, float& oa) {
+template <typename T>
+__device__ __noinline__ void tail_sums(const T* xb, int HW, int p, int C, float& og, float& oa) {
   Cascade cg[4], ca[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) { cg[k].init(); ca[k].init(); }
@@ -145,7 +201,7 @@ __device__ __noinline__ void tail_sums(const float* xb, int HW, int p, int C, fl
     const int n = imin_(16, n4 - c0);
     float v[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) v[i] = xb[(size_t)(c0 + (i < n ? i : 0)) * HW + p];
+    for (int i = 0; i < 16; ++i) v[i] = ElemIO<T>::ld(xb + (size_t)(c0 + (i < n ? i : 0)) * HW + p);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       if (i < n) { cg[i & 3].push(v[i]); ca[i & 3].push(fabsf(v[i])); }
@@ -153,7 +209,7 @@ __device__ __noinline__ void tail_sums(const float* xb, int HW, int p, int C, fl
   }
   float g0 = cg[0].result(), a0 = ca[0].result();
   for (int r = n4; r < C; ++r) {
-    const float v = xb[(size_t)r * HW + p];
+    const float v = ElemIO<T>::ld(xb + (size_t)r * HW + p);
     g0 = g0 + v; a0 = a0 + fabsf(v);
   }
   og = ((g0 + cg[1].result()) + cg[2].result()) + cg[3].result();
@@ -161,13 +217,14 @@ __device__ __noinline__ void tail_sums(const float* xb, int HW, int p, int C, fl
 }
 
 // sequential channel sum of pixel p (the order of a cropped view's mean)
-__device__ __noinline__ float seq_sum(const float* xb, int HW, int p, int C) {
+template <typename T>
+__device__ __noinline__ float seq_sum(const T* xb, int HW, int p, int C) {
   float sq = 0.0f;
   for (int c0 = 0; c0 < C; c0 += 16) {
     const int n = imin_(16, C - c0);
     float v[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) v[i] = xb[(size_t)(c0 + (i < n ? i : 0)) * HW + p];
+    for (int i = 0; i < 16; ++i) v[i] = ElemIO<T>::ld(xb + (size_t)(c0 + (i < n ? i : 0)) * HW + p);
 #pragma unroll
     for (int i = 0; i < 16; ++i) if (i < n) sq = sq + v[i];
   }
@@ -185,7 +242,7 @@ __device__ __noinline__ float seq_sum(const float* xb, int HW, int p, int C) {
 // registers.  The last (< 32) pixels of an image reduce in ATen's row_sum
 // order instead: their 4 x ceil(C/64) independent 16-row block sums are spread
 // over the workgroup (one load round trip), then folded per pixel.
-template <int PPL, bool kVec>
+template <int PPL, bool kVec, typename T>
 __device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, float* lds) {
   float (*bsg)[256] = reinterpret_cast<float (*)[256]>(lds);
   float (*bsa)[256] = reinterpret_cast<float (*)[256]>(lds + ST_WAVES * 256);
@@ -195,7 +252,7 @@ __device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, fl
   const int upi = (HW + UPIX - 1) / UPIX;
   const int b = lu / upi, chunk = lu - b * upi;
   const int C = S.C;
-  const float* xb = S.x + (size_t)b * C * HW;
+  const T* xb = reinterpret_cast<const T*>(S.x) + (size_t)b * C * HW;
   const bool cropped = (S.Hc != S.H) || (S.Wc != S.W);
 #ifdef MCAQ_PROBE_STATS_NO_MINMAX   // timing probe only (no min/max partials)
   const bool want_g = S.gray != nullptr, want_a = S.absmean != nullptr, want_m = false;
@@ -238,7 +295,7 @@ __device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, fl
       const int p = tstart + i;
       const int r0 = 16 * j, n = imin_(16, nilp - r0);
 #pragma unroll
-      for (int e = 0; e < 16; ++e) tv[e2][e] = xb[(size_t)(4 * (r0 + (e < n ? e : 0)) + k) * HW + p];
+      for (int e = 0; e < 16; ++e) tv[e2][e] = ElemIO<T>::ld(xb + (size_t)(4 * (r0 + (e < n ? e : 0)) + k) * HW + p);
     }
   }
 #else
@@ -262,24 +319,23 @@ __device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, fl
       const int nc = imin_(ST_CG, C - c0);
 #pragma unroll
       for (int i = 0; i < ST_CG; ++i) {
-        const float* row = xb + (size_t)(c0 + (i < nc ? i : 0)) * HW;
+        const T* row = xb + (size_t)(c0 + (i < nc ? i : 0)) * HW;
         if (kVec && PPL == 4) {
           // streaming load: x is far larger than L2, and leaving L2 to the
           // morphology of the other in-flight batches gains ~3 % per step
           // (profiles/r01_stats_ntl_ab/)
-          typedef float f4v __attribute__((ext_vector_type(4)));
 #if defined(MCAQ_STATS_PLAIN_LOADS)
-          const f4v t = *reinterpret_cast<const f4v*>(row + qa);
+          const mcaq_f4v t = ElemIO<T>::ld4(row + qa, false);
 #else
-          const f4v t = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(row + qa));
+          const mcaq_f4v t = ElemIO<T>::ld4(row + qa, true);
 #endif
           v[rr][i][0] = t.x; v[rr][i][1 % PPL] = t.y; v[rr][i][2 % PPL] = t.z; v[rr][i][3 % PPL] = t.w;
         } else if (kVec && PPL == 2) {
-          const float2 t = *reinterpret_cast<const float2*>(row + qa);
+          const float2 t = ElemIO<T>::ld2(row + qa);
           v[rr][i][0] = t.x; v[rr][i][1 % PPL] = t.y;
         } else {
 #pragma unroll
-          for (int k = 0; k < PPL; ++k) v[rr][i][k] = row[imin_(q0 + k, HW - 1)];
+          for (int k = 0; k < PPL; ++k) v[rr][i][k] = ElemIO<T>::ld(row + imin_(q0 + k, HW - 1));
         }
       }
     }
@@ -368,7 +424,7 @@ __device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, fl
       const int r0 = 16 * j, n = imin_(16, nilp - r0);
       float v[16];
 #pragma unroll
-      for (int e = 0; e < 16; ++e) v[e] = xb[(size_t)(4 * (r0 + (e < n ? e : 0)) + k) * HW + p];
+      for (int e = 0; e < 16; ++e) v[e] = ElemIO<T>::ld(xb + (size_t)(4 * (r0 + (e < n ? e : 0)) + k) * HW + p);
       float sg = 0.0f, sa = 0.0f;
 #pragma unroll
       for (int e = 0; e < 16; ++e) if (e < n) { sg = sg + v[e]; sa = sa + fabsf(v[e]); }
@@ -390,7 +446,7 @@ __device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, fl
         rg[k] = cg.result(); ra[k] = ca.result();
       }
       for (int rr = 4 * nilp; rr < C; ++rr) {      // leftover rows into partial 0
-        const float v = xb[(size_t)rr * HW + p];
+        const float v = ElemIO<T>::ld(xb + (size_t)rr * HW + p);
         rg[0] = rg[0] + v; ra[0] = ra[0] + fabsf(v);
       }
       tg = ((rg[0] + rg[1]) + rg[2]) + rg[3];
@@ -442,7 +498,7 @@ __device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, fl
 #define MCAQ_STREAM_CAP 0
 #endif
 
-template <bool kVec>   // kVec: 8/16-byte row accesses for ppl 2/4 (host checks alignment)
+template <bool kVec, typename T = float>   // kVec: 8/16-byte row accesses for ppl 2/4 (host checks alignment)
 __device__ __forceinline__ void stats_dispatch(const StatsArgs& a, float* lds, const int bid) {
   // heaviest (most channels per pixel) scales are the last ones: start them first
   const int unit = a.units_total - 1 - bid;
@@ -463,24 +519,24 @@ __device__ __forceinline__ void stats_dispatch(const StatsArgs& a, float* lds, c
   }
 #endif
   if constexpr (MCAQ_STATS_MAXPPL >= 4) {
-    if (ppl == 4) { stats_unit<4, kVec>(S, lu, lds); return; }
+    if (ppl == 4) { stats_unit<4, kVec, T>(S, lu, lds); return; }
   }
   if constexpr (MCAQ_STATS_MAXPPL >= 2) {
-    if (ppl == 2) { stats_unit<2, kVec>(S, lu, lds); return; }
+    if (ppl == 2) { stats_unit<2, kVec, T>(S, lu, lds); return; }
   }
-  stats_unit<1, kVec>(S, lu, lds);
+  stats_unit<1, kVec, T>(S, lu, lds);
 }
 
-template <bool kVec>
+template <bool kVec, typename T = float>
 __global__ __launch_bounds__(256, MCAQ_STATS_MINW) void mcaq_stats_kernel(StatsArgs a) {
   __shared__ float lds[ST_LDS];
 #if MCAQ_STREAM_CAP > 0
   for (int u = (int)blockIdx.x; u < a.units_total; u += (int)gridDim.x) {
-    stats_dispatch<kVec>(a, lds, u);
+    stats_dispatch<kVec, T>(a, lds, u);
     __syncthreads();    // the LDS of this unit is free for the next
   }
 #else
-  stats_dispatch<kVec>(a, lds, (int)blockIdx.x);
+  stats_dispatch<kVec, T>(a, lds, (int)blockIdx.x);
 #endif
 }
 
@@ -1090,7 +1146,7 @@ __global__ MCAQ_QUANT_LB void mcaq_quant_kernel(QuantArgs a) {
 // VALU instructions per wave on index arithmetic and its integer divisions:
 // rocprofv3 SQ_INSTS_VALU, profiles/r04_sq/).  Soft mask: none or m(tile)
 // values (QM_NONE / QM_MT_LDS); at most 8 bit widths.
-template <bool kNTL, bool kNTS, int kM>
+template <bool kNTL, bool kNTS, int kM, typename T, typename TO>
 __device__ __forceinline__ void quant_tile_unit(const QuantArgs& a, const int unit, float4* qt, float* mts, float4* mq4,
                                                 int* qany) {
   typedef float f2 __attribute__((ext_vector_type(2)));
@@ -1128,15 +1184,12 @@ __device__ __forceinline__ void quant_tile_unit(const QuantArgs& a, const int un
   const int cw = wv * QCW;
   const int ncw = imin_(QCW, nc - cw);
   const size_t rowbase = ((size_t)b * S.C + c0 + imax_(imin_(cw, nc - 1), 0)) * HW;
-  const float* xb = S.x + rowbase;
-  float* yb = S.y + rowbase;
+  const T* xb = reinterpret_cast<const T*>(S.x) + rowbase;
+  TO* yb = reinterpret_cast<TO*>(S.y) + rowbase;
   typedef float f4v __attribute__((ext_vector_type(4)));
   f4v v[QCW];
 #pragma unroll
-  for (int c = 0; c < QCW; ++c) {
-    const f4v* row = reinterpret_cast<const f4v*>(xb + (size_t)imin_(c, imax_(ncw - 1, 0)) * HW + qa);
-    v[c] = kNTL ? __builtin_nontemporal_load(row) : *row;
-  }
+  for (int c = 0; c < QCW; ++c) v[c] = ElemIO<T>::ld4(xb + (size_t)imin_(c, imax_(ncw - 1, 0)) * HW + qa, kNTL);
   // ---- 3. the table (IEEE divisions of QuantizationParameters), staged m(tile)
   {
     const int kq = imin_(tid >> 5, NB - 1);     // every thread stores an entry (unused rows harmless)
@@ -1208,15 +1261,11 @@ __device__ __forceinline__ void quant_tile_unit(const QuantArgs& a, const int un
               quant_dequant_any(v[c].w, q)};
       if (kM != QM_NONE) o = o * f4v{m01.x, m01.y, m23.x, m23.y};
     }
-    if (pv) {
-      f4v* orow = reinterpret_cast<f4v*>(yb + (size_t)c * HW + q0);
-      if (kNTS) __builtin_nontemporal_store(o, orow);
-      else *orow = o;
-    }
+    if (pv) ElemIO<TO>::st4(yb + (size_t)c * HW + q0, o, kNTS);
   }
 }
 
-template <bool kNTL, bool kNTS, int kM>
+template <bool kNTL, bool kNTS, int kM, typename T = float, typename TO = T>
 __global__ MCAQ_QUANT_LB void mcaq_quant_tile_kernel(QuantArgs a) {
   __shared__ float4 qt[8 * QSLICE];           // [kb][c]: scale, zp, 1/scale
   __shared__ float mts[kM == QM_MT_LDS ? QMAXNT : 1];
@@ -1224,11 +1273,11 @@ __global__ MCAQ_QUANT_LB void mcaq_quant_tile_kernel(QuantArgs a) {
   __shared__ int qany[QSLICE];
 #if MCAQ_STREAM_CAP > 0
   for (int u = (int)blockIdx.x; u < a.units_total; u += (int)gridDim.x) {
-    quant_tile_unit<kNTL, kNTS, kM>(a, u, qt, mts, mq4, qany);
+    quant_tile_unit<kNTL, kNTS, kM, T, TO>(a, u, qt, mts, mq4, qany);
     __syncthreads();    // LDS of this unit free for the next
   }
 #else
-  quant_tile_unit<kNTL, kNTS, kM>(a, (int)blockIdx.x, qt, mts, mq4, qany);
+  quant_tile_unit<kNTL, kNTS, kM, T, TO>(a, (int)blockIdx.x, qt, mts, mq4, qany);
 #endif
 }
 
@@ -1291,6 +1340,8 @@ static int stats_args(const mcaq_stats_scale* scales, int nscales, StatsArgs& a,
     const int HW = scales[i].H * scales[i].W;
     if (scales[i].B < 1 || scales[i].C < 1 || HW < 1 || !scales[i].x) return (int)hipErrorInvalidValue;
     if ((scales[i].pmin == nullptr) != (scales[i].pmax == nullptr)) return (int)hipErrorInvalidValue;
+    if (scales[i].dtype != scales[0].dtype || scales[i].dtype < MCAQ_DTYPE_F32 || scales[i].dtype > MCAQ_DTYPE_BF16)
+      return (int)hipErrorInvalidValue;    // one element type per launch
     a.ppl[i] = stats_ppl(scales[i].C, HW);
     units += mcaq_stats_units(scales[i].B, scales[i].C, scales[i].H, scales[i].W);
   }
@@ -1308,10 +1359,14 @@ int mcaq_stats(const mcaq_stats_scale* scales, int nscales, hipStream_t stream) 
   const int e = stats_args(scales, nscales, a, vec);
   if (e) return e;
   const dim3 g(MCAQ_STREAM_CAP > 0 ? imin_(a.units_total, MCAQ_STREAM_CAP * 256) : a.units_total);
-  if (vec)
-    launch_k(mcaq_stats_kernel<true>, g, dim3(256), 0, stream, a);
-  else
-    launch_k(mcaq_stats_kernel<false>, g, dim3(256), 0, stream, a);
+  switch (scales[0].dtype * 2 + (vec ? 1 : 0)) {
+    case 0: launch_k(mcaq_stats_kernel<false>, g, dim3(256), 0, stream, a); break;
+    case 1: launch_k(mcaq_stats_kernel<true>, g, dim3(256), 0, stream, a); break;
+    case 2: launch_k(mcaq_stats_kernel<false, _Float16>, g, dim3(256), 0, stream, a); break;
+    case 3: launch_k(mcaq_stats_kernel<true, _Float16>, g, dim3(256), 0, stream, a); break;
+    case 4: launch_k(mcaq_stats_kernel<false, Bf16>, g, dim3(256), 0, stream, a); break;
+    default: launch_k(mcaq_stats_kernel<true, Bf16>, g, dim3(256), 0, stream, a); break;
+  }
   return (int)hipGetLastError();
 }
 
@@ -1692,7 +1747,10 @@ int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream) 
     if (scales[i].nbits < 1 || scales[i].nbits > QMAXBITS || scales[i].bits_lo < 1 ||
         scales[i].bits_lo + scales[i].nbits - 1 > 16 || HW < 1 || scales[i].C < 1 ||
         scales[i].ht < 1 || scales[i].wt < 1 || !scales[i].x || !scales[i].y || !scales[i].bits ||
-        !scales[i].xmin || !scales[i].xmax)
+        !scales[i].xmin || !scales[i].xmax || scales[i].dtype != scales[0].dtype ||
+        scales[i].dtype < MCAQ_DTYPE_F32 || scales[i].dtype > MCAQ_DTYPE_BF16 ||
+        scales[i].ydtype != scales[0].ydtype ||
+        (scales[i].ydtype != scales[i].dtype && scales[i].ydtype != MCAQ_DTYPE_F32))
       return (int)hipErrorInvalidValue;
     units += scales[i].B * ((HW + 255) / 256) * ((scales[i].C + QSLICE - 1) / QSLICE);
   }
@@ -1712,7 +1770,7 @@ int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream) 
 #else
   size_t xbytes = 0;
   for (int i = 0; i < nscales; ++i)
-    xbytes += (size_t)scales[i].B * scales[i].C * scales[i].H * scales[i].W * sizeof(float);
+    xbytes += (size_t)scales[i].B * scales[i].C * scales[i].H * scales[i].W * (scales[0].dtype ? 2 : sizeof(float));
   const int nt = xbytes > ((size_t)256 << 20) ? 3 : 1;
 #endif
   // m(p) source: one kind for every scale of the launch (the hook always
@@ -1754,6 +1812,25 @@ int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream) 
 #ifdef MCAQ_NO_QUANT_TILE
   tile_ok = false;   // A/B: the general kernel
 #endif
+  const int dt = scales[0].dtype;
+  if (dt != MCAQ_DTYPE_F32) {
+    // fp16 / bf16 maps: the tile-aligned kernel only (any nontemporal policy:
+    // NT loads and stores)
+    if (!tile_ok) return (int)hipErrorNotSupported;
+    const dim3 g(MCAQ_STREAM_CAP > 0 ? imin_(units, MCAQ_STREAM_CAP * 256) : units);
+    const bool yf = scales[0].ydtype == MCAQ_DTYPE_F32;
+    switch ((kind == QM_NONE ? 0 : 1) + (dt == MCAQ_DTYPE_BF16 ? 2 : 0) + (yf ? 4 : 0)) {
+      case 0: launch_k(mcaq_quant_tile_kernel<true, true, QM_NONE, _Float16>, g, t, 0, stream, a); break;
+      case 1: launch_k(mcaq_quant_tile_kernel<true, true, QM_MT_LDS, _Float16>, g, t, 0, stream, a); break;
+      case 2: launch_k(mcaq_quant_tile_kernel<true, true, QM_NONE, Bf16>, g, t, 0, stream, a); break;
+      case 3: launch_k(mcaq_quant_tile_kernel<true, true, QM_MT_LDS, Bf16>, g, t, 0, stream, a); break;
+      case 4: launch_k(mcaq_quant_tile_kernel<true, true, QM_NONE, _Float16, float>, g, t, 0, stream, a); break;
+      case 5: launch_k(mcaq_quant_tile_kernel<true, true, QM_MT_LDS, _Float16, float>, g, t, 0, stream, a); break;
+      case 6: launch_k(mcaq_quant_tile_kernel<true, true, QM_NONE, Bf16, float>, g, t, 0, stream, a); break;
+      default: launch_k(mcaq_quant_tile_kernel<true, true, QM_MT_LDS, Bf16, float>, g, t, 0, stream, a); break;
+    }
+    return (int)hipGetLastError();
+  }
   if (tile_ok) {
     const dim3 g(MCAQ_STREAM_CAP > 0 ? imin_(units, MCAQ_STREAM_CAP * 256) : units);
     switch ((kind == QM_NONE ? 0 : 4) + (nt & 3)) {
@@ -1769,6 +1846,7 @@ int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream) 
     return (int)hipGetLastError();
   }
 #endif
+  if (scales[0].dtype != MCAQ_DTYPE_F32) return (int)hipErrorNotSupported;   // fp16 / bf16: tile kernel only
 #define MCAQ_Q_LAUNCH(V, L, S_)                                                                              \
   do {                                                                                                       \
     switch (kind * 2 + (big ? 1 : 0)) {                                                                      \

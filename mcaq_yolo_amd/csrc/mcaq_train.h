@@ -1946,7 +1946,7 @@ __global__ __launch_bounds__(1024) void mcaq_bit_budget_kernel(BitBudgetArgs a) 
 // segment order - v = s0 (+ out if accumulate), v += s1, v += s2 - the values
 // one reduction launch per segment leaves (the first with `accumulate`, the
 // others accumulating)
-struct TrReduceSeg { const float* part; float* out; int nwg, stride, count, accumulate; };
+struct TrReduceSeg { const float* part; float* out; int nwg, stride, count, accumulate; float scale; };
 // chain mode: element e of segment 0's output = s_0 (+ out) + s_1 + s_2
 // (a variant walking all segments' partials as one 16-deep load list was
 // slower: 5.9 -> 10.7 us for the complexity-MLP chain, r05)
@@ -1954,11 +1954,15 @@ __device__ __forceinline__ void tr_chain_elem(const TrMulti<TrReduceSeg>& M, int
   const TrReduceSeg& s0 = M.s[0];
   if (e >= s0.count) return;
   float v = 0.0f;
+  const bool sc = s0.scale != 0.0f && s0.scale != 1.0f;
   for (int k = 0; k < M.nseg; ++k) {
     const TrReduceSeg& g = k == 0 ? M.s[0] : (k == 1 ? M.s[1] : M.s[2]);
     const float sum = tr_ordered_sum(g.part, g.nwg, g.stride, e);
-    v = k == 0 ? (s0.accumulate ? s0.out[e] + sum : sum) : v + sum;
+    v = k == 0 ? ((s0.accumulate && !sc) ? s0.out[e] + sum : sum) : v + sum;
   }
+  // scaled (a data-parallel rank's share of a gradient it computed whole):
+  // this launch's sum times the scale, then accumulated
+  if (sc) v = s0.accumulate ? s0.out[e] + v * s0.scale : v * s0.scale;
   s0.out[e] = v;
 }
 __global__ __launch_bounds__(256) void mcaq_tr_reduce_multi_kernel(TrMulti<TrReduceSeg> M, int chain) {
@@ -1969,7 +1973,8 @@ __global__ __launch_bounds__(256) void mcaq_tr_reduce_multi_kernel(TrMulti<TrRed
     const int k = blockIdx.y;
     const TrReduceSeg& g = k == 0 ? M.s[0] : (k == 1 ? M.s[1] : M.s[2]);
     if (k >= M.nseg || e >= g.count) return;
-    const float sum = tr_ordered_sum(g.part, g.nwg, g.stride, e);
+    float sum = tr_ordered_sum(g.part, g.nwg, g.stride, e);
+    if (g.scale != 0.0f) sum = sum * g.scale;
     g.out[e] = g.accumulate ? g.out[e] + sum : sum;
   }
 }
@@ -1980,7 +1985,8 @@ __device__ __forceinline__ void tr_seg_elem(const TrMulti<TrReduceSeg>& M, int i
   const int cnt = M.s[0].count, k = i / cnt, e = i - k * cnt;
   if (k >= M.nseg) return;
   const TrReduceSeg& g = k == 0 ? M.s[0] : (k == 1 ? M.s[1] : M.s[2]);
-  const float sum = tr_ordered_sum(g.part, g.nwg, g.stride, e);
+  float sum = tr_ordered_sum(g.part, g.nwg, g.stride, e);
+  if (g.scale != 0.0f) sum = sum * g.scale;
   g.out[e] = g.accumulate ? g.out[e] + sum : sum;
 }
 
@@ -2350,7 +2356,7 @@ int mcaq_mapper_train_backward_multi_ride(const mcaq_mapper_params* P, const mca
     const mcaq_reduce_seg& g = rsegs[k];
     if (!g.part || !g.out || g.nparts < 1 || g.stride < g.count || g.count < 1 || g.count != rsegs[0].count)
       return (int)hipErrorInvalidValue;
-    R.s[k] = TrReduceSeg{g.part, g.out, g.nparts, g.stride, g.count, g.accumulate};
+    R.s[k] = TrReduceSeg{g.part, g.out, g.nparts, g.stride, g.count, g.accumulate, g.scale};
   }
   R.nseg = nr;
   TrMulti<MapperTrainArgs> M{};
@@ -2392,7 +2398,7 @@ int mcaq_head_train_backward_multi_ride(const mcaq_cmlp_params* P, const mcaq_he
     const mcaq_reduce_seg& g = rsegs[k];
     if (!g.part || (!g.out && k == 0) || g.nparts < 1 || g.stride < g.count || g.count < 1 || g.count != rsegs[0].count)
       return (int)hipErrorInvalidValue;
-    R.s[k] = TrReduceSeg{g.part, g.out, g.nparts, g.stride, g.count, g.accumulate};
+    R.s[k] = TrReduceSeg{g.part, g.out, g.nparts, g.stride, g.count, g.accumulate, g.scale};
   }
   R.nseg = nr;
   TrMulti<HeadTrainArgs> Mb{}, Mc{};
@@ -2538,7 +2544,7 @@ int mcaq_train_reduce_multi(const mcaq_reduce_seg* segs, int nseg, int chain, hi
     if (!g.part || (!g.out && !(chain && k > 0)) || g.nparts < 1 || g.stride < g.count || g.count < 1)
       return (int)hipErrorInvalidValue;
     if (chain && g.count != segs[0].count) return (int)hipErrorInvalidValue;
-    M.s[k] = TrReduceSeg{g.part, g.out, g.nparts, g.stride, g.count, g.accumulate};
+    M.s[k] = TrReduceSeg{g.part, g.out, g.nparts, g.stride, g.count, g.accumulate, g.scale};
     cmax = g.count > cmax ? g.count : cmax;
   }
   M.nseg = nseg;
@@ -2587,6 +2593,7 @@ int mcaq_stats_pack(const mcaq_stats_scale* scales, int nscales, const mcaq_pack
   bool vec;
   const int e = stats_args(scales, nscales, a, vec);
   if (e) return e;
+  if (scales[0].dtype != MCAQ_DTYPE_F32) return (int)hipErrorNotSupported;   // the train step's x is fp32
   PackArgs p{};
   const int pe = pack_args(segs, nseg, out, total, p);
   if (pe) return pe;

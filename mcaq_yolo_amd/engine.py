@@ -54,6 +54,32 @@ def _require_cuda(*ts):
             raise RuntimeError("mcaq_yolo_amd runs on MI355X (HIP) only; got a %s tensor" % t.device)
 
 
+# feature-map element types the kernels read natively (include/mcaq_hip.h
+# MCAQ_DTYPE_*): fp32, and the fp16 / bf16 maps an autocast region hands the
+# hooks (train.py:582-585, 748-749).  fp16 / bf16 widen exactly in pass 1 and
+# pass 2, all arithmetic is fp32 (the analyzer's gray / |x| sums are those of
+# x.float(), morphology.py:834-837).  y takes the reference's result type: the
+# input's dtype, or fp32 where the fp32 soft mask multiplies it
+# (quantization.py:742-744 promotes fp16 * fp32 to fp32).
+_DTYPES = {torch.float32: abi.DTYPE_F32, torch.float16: abi.DTYPE_F16, torch.bfloat16: abi.DTYPE_BF16}
+
+
+def half_native_ok(geom, min_bits=2.0, max_bits=8.0):
+    """True when pass 2 takes an fp16 / bf16 map of this geometry natively
+    (the tile-aligned kernel: the map a power-of-two multiple of the tile
+    grid, tiles >= 4 pixels wide, H*W % 4 == 0, <= 1024 tiles, <= 8 widths);
+    otherwise callers quantize x.float()."""
+    def pow2_mult(n, t):
+        k = 0
+        while (t << k) < n:
+            k += 1
+        return (t << k) == n, k
+    okh, _ = pow2_mult(geom.H, geom.ht)
+    okw, sw = pow2_mult(geom.W, geom.wt)
+    return okh and okw and sw >= 2 and (geom.H * geom.W) % 4 == 0 and geom.ht * geom.wt <= 1024 and \
+        int(max_bits) - int(min_bits) + 1 <= 8
+
+
 def _stream_handle(stream):
     s = stream if stream is not None else torch.cuda.current_stream()
     return ctypes.c_void_p(s.cuda_stream)
@@ -168,7 +194,8 @@ class HookPlan:
 
     def run(self, feats, cmlp, mapper, smasks, stream=None, process_group=None, **kw):
         """Enqueue one step (prepare + launch).  feats: list of (B,C,H,W) fp32
-        CUDA tensors matching the plan (batches > 1: one such list per batch).
+        (or fp16 / bf16, see half_native_ok) CUDA tensors matching the plan
+        (batches > 1: one such list per batch).
         cmlp/mapper: packed blobs (CUDA fp32); smasks: one packed soft-mask
         blob per scale or None (smooth_transitions=False).  Keyword options:
         see prepare().  Returns the buffer dicts (overwritten by the next run)."""
@@ -221,9 +248,19 @@ class HookPlan:
             raise ValueError("expected %d feature maps" % n)
         for f, g in zip(feats, self.geoms):
             _require_cuda(f)
-            if f.dtype != torch.float32 or not f.is_contiguous() or tuple(f.shape) != (g.B, g.C, g.H, g.W):
-                raise ValueError("feature map must be contiguous fp32 %s, got %s %s"
+            if f.dtype not in _DTYPES or not f.is_contiguous() or tuple(f.shape) != (g.B, g.C, g.H, g.W):
+                raise ValueError("feature map must be contiguous fp32 / fp16 / bf16 %s, got %s %s"
                                  % ((g.B, g.C, g.H, g.W), tuple(f.shape), f.dtype))
+        dtype = feats[0].dtype
+        if any(f.dtype != dtype for f in feats):
+            raise ValueError("one feature-map dtype per launch, got %s" % sorted({str(f.dtype) for f in feats}))
+        if dtype != torch.float32:
+            if m_plane or not all(half_native_ok(g, min_bits, max_bits) for g in self.geoms):
+                raise ValueError("%s feature maps need the tile-aligned quantizer (engine.half_native_ok)" % dtype)
+        ydt = [torch.float32 if (sm is not None and quantize) else dtype for sm in smasks]
+        for b, g, yd in zip(self.bufs, self.geoms, ydt):
+            if b["y"].dtype != yd:          # y in the reference's result type
+                b["y"] = torch.empty(g.B, g.C, g.H, g.W, device=self.device, dtype=yd)
         # descriptor reuse: an eager hook calls prepare once per forward with
         # new x / output tensors and otherwise the same blobs, buffers and
         # options; then only those pointers are patched into the structs
@@ -232,7 +269,7 @@ class HookPlan:
             int(batch_offset), batch_total, bool(binarize_otsu), bool(contour_components), bool(canny_legacy),
             float(min_bits), float(max_bits), bool(quantize), int(hysteresis_iters), bool(per_tensor),
             int(softmax_threads) if softmax_threads else torch.get_num_threads(), bool(m_plane),
-            bool(shared_stats)))
+            bool(shared_stats), str(dtype)))
         if sig is not None and sig == getattr(self, "_sig", None):
             self._rebind(feats)
             self._keep = (list(feats), cmlp, mapper, list(smasks), minmax)
@@ -252,6 +289,7 @@ class HookPlan:
             s.pmin = _p(b["pmin"]) if need_mm else None
             s.pmax = _p(b["pmax"]) if need_mm else None
             s.B, s.C, s.H, s.W, s.Hc, s.Wc = g.B, g.C, g.H, g.W, g.Hc, g.Wc
+            s.dtype = _DTYPES[dtype]
         self._st = st
         self._fz = self._qs = None
         # ---- channel min/max
@@ -332,6 +370,8 @@ class HookPlan:
                 # batch statistics of this x (pass 1 + finalize, all-reduced or not)
                 s.stats_cover_x = 1 if (minmax is None or minmax[i] is None) else 0
                 s.neg_min = 1 if self._neg else 0
+                s.dtype = _DTYPES[dtype]
+                s.ydtype = _DTYPES[b["y"].dtype]
             self._qs = qs
         self._n = n
         self._sig = sig

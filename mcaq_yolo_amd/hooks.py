@@ -21,7 +21,7 @@ import torch.nn as nn
 
 from .core import (ComplexityToBitMappingNetwork, LinearBitMapper, MorphologicalComplexityAnalyzer,
                    SpatialAdaptiveQuantization)
-from . import core, train_step
+from . import core, engine, train_step
 from .engine import HookPlan, ScaleGeom
 
 DEFAULT_INDICES = (4, 6, 9)   # models/mcaq_yolo.py:361 fallback (C3/C4/C5 of YOLOv8)
@@ -233,10 +233,17 @@ class MCAQHooks(nn.Module):
             return self._run_scale_modules(layer_idx, feat, state)
         quantize = state.get("quantize", True)
         quantizer = self.quantizers[str(layer_idx)]
-        x = feat.float().contiguous()
-        if state.get("calibrating", False) and quantize:
-            quantizer.update_running_stats(x)
+        # fp16 / bf16 maps (an autocast region) are read natively by pass 1 and
+        # pass 2 (fp32 arithmetic, y in the input's dtype) where the quantizer's
+        # tile-aligned kernel takes the shape; otherwise quantized as x.float()
+        half = feat.dtype in (torch.float16, torch.bfloat16)
+        x = feat.contiguous() if half else feat.float().contiguous()
         plan = self._plan(x)
+        if half and not all(engine.half_native_ok(g, self.bit_mapper.min_bits, self.bit_mapper.max_bits)
+                            for g in plan.geoms):
+            x = x.float()
+        if state.get("calibrating", False) and quantize:
+            quantizer.update_running_stats(x.float())
         b = plan.bufs[0]
         for k in ("y", "complexity", "bits"):      # fresh outputs: the caller keeps them
             b[k] = torch.empty_like(b[k])

@@ -28,19 +28,34 @@ import torch
 from . import abi
 
 
-def _check(t, what):
+_HALF = (torch.float16, torch.bfloat16)
+
+
+def _check(t, what, half_ok=False):
     if not torch.is_tensor(t):
         raise TypeError("%s must be a Tensor" % what)
     if not t.is_cuda:
         raise RuntimeError("%s must be a CUDA (HIP) tensor, got %s" % (what, t.device))
-    if t.dtype != torch.float32:
-        raise RuntimeError("%s must be float32, got %s" % (what, t.dtype))
+    if t.dtype != torch.float32 and not (half_ok and t.dtype in _HALF):
+        raise RuntimeError("%s must be float32%s, got %s" % (what, " (or float16 / bfloat16)" if half_ok else "",
+                                                             t.dtype))
     if not t.is_contiguous():
         raise RuntimeError("%s must be contiguous" % what)
 
 
 def spatial_quantize(input, bit_map, min_vals, max_vals, tile_h, tile_w, mask=None):
-    for t, n in ((input, "input"), (bit_map, "bit_map"), (min_vals, "min_vals"), (max_vals, "max_vals")):
+    """input may also be fp16 / bf16 (an autocast region; the reference op
+    raises there, data_ptr<float>): quantized in fp32 arithmetic on
+    input.float() (exact); the result takes torch's type promotion of
+    input x mask (fp32 with an fp32 mask, as the reference's _forward_pytorch
+    returns x_quantized * m, quantization.py:742-744; else the input's dtype,
+    rounded to nearest even)."""
+    _check(input, "input", half_ok=True)
+    if input.dtype in _HALF:
+        out_dt = input.dtype if mask is None else torch.promote_types(input.dtype, mask.dtype)
+        return spatial_quantize(input.float(), bit_map, min_vals, max_vals, tile_h, tile_w,
+                                None if mask is None else mask.float().contiguous()).to(out_dt)
+    for t, n in ((bit_map, "bit_map"), (min_vals, "min_vals"), (max_vals, "max_vals")):
         _check(t, n)
     if input.dim() != 4:
         raise RuntimeError("input must be (N, C, H, W)")

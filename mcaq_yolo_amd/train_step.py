@@ -330,21 +330,22 @@ class _HeadMulti(torch.autograd.Function):
         return (None, None, None) + (None,) * n + grads
 
 
-def _chain_segs(gparts, out, acc, count):
+def _chain_segs(gparts, out, acc, count, scale=0.0):
     """ReduceSeg chain: every scale's per-workgroup partials into `out`, in
     the order the per-scale backwards accumulate them (autograd runs the last
-    scale's first)."""
+    scale's first); scale (0: none) multiplies the launch's sum."""
     n = len(gparts)
     segs = (abi.ReduceSeg * n)()
     for k, (gp, nparts) in enumerate(reversed(gparts)):
         s = segs[k]
         s.part, s.out, s.nparts, s.stride, s.count, s.accumulate = _p(gp), _p(out), nparts, count, count, acc
+        s.scale = scale
     return segs
 
 
-def _reduce_chain(gparts, out, acc, count):
-    abi.check(abi.lib().mcaq_train_reduce_multi(_chain_segs(gparts, out, acc, count), len(gparts), 1, _stream()),
-              "mcaq_train_reduce_multi")
+def _reduce_chain(gparts, out, acc, count, scale=0.0):
+    abi.check(abi.lib().mcaq_train_reduce_multi(_chain_segs(gparts, out, acc, count, scale), len(gparts), 1,
+                                                _stream()), "mcaq_train_reduce_multi")
 
 
 # The bit mapper's parameter-gradient reduction, deferred from its backward
@@ -388,15 +389,13 @@ def _flush_pending_sm_reduce():
 # min / max riding along - runs the mapper on the GLOBAL batch of tiles (a
 # few thousand tiles: the stage launches' cost is their latency, not the
 # tile count) and keeps its own slice; the backward all-gathers the bits'
-# gradients once and runs the mapper's backward on the global batch, each
-# rank reducing only its own tiles' parameter-gradient partials (the
-# gradient all-reduce then sums the ranks' shares).  Bits, BatchNorm batch
-# and running statistics, EMA min / max and the mapper's input gradients are
-# the single-process values bit for bit; 2 collectives instead of 7.
-# False: the staged per-layer collectives (also taken when a rank's tile
-# count of a scale is not a multiple of the kernels' 64-tile workgroups).
+# gradients once and runs the mapper's backward on the global batch: every
+# rank then holds the WHOLE mapper gradient and contributes 1 / world of it
+# to the gradient all-reduce (whose sum is that gradient again).  Bits,
+# BatchNorm batch and running statistics, EMA min / max and the mapper's
+# input gradients are the single-process values bit for bit; 2 collectives
+# instead of 7.  False: the staged per-layer collectives.
 DP_GLOBAL_MAPPER = True
-_TR_TPB = 64            # tiles per mapper workgroup (csrc/mcaq_train.h TR_TPB)
 
 
 def _consecutive(ts):
@@ -440,7 +439,7 @@ def _dp_mapper_inputs(mapper, ncs, box, with_minmax):
     if not DP_GLOBAL_MAPPER or not isinstance(mapper, core.ComplexityToBitMappingNetwork):
         return None
     pg = core._mapper_group(mapper.mapping_network)
-    if pg is None or any(c.numel() % _TR_TPB for c in ncs):
+    if pg is None:
         return None
     if len(ncs) * 3 > abi.MCAQ_DP_MAXSEG:
         return None
@@ -569,16 +568,11 @@ class _MapperMulti(torch.autograd.Function):
             keep.append(g)
             npart = gp.numel() // core._MAPPER_G_SIZE             # one partial per backward workgroup
             if dp is not None:
-                # this rank's share of the parameter gradients: its own tiles'
-                # workgroups (whole workgroups: _TR_TPB divides its tile count)
                 ml = ctx.shapes[i].numel()
-                gcs.append(gc[r * ml:(r + 1) * ml])
-                nl = ml // _TR_TPB
-                gparts.append((gp[r * nl * core._MAPPER_G_SIZE:(r + 1) * nl * core._MAPPER_G_SIZE], nl))
-                keep.append(gp)
+                gcs.append(gc[r * ml:(r + 1) * ml])               # this rank's tiles
             else:
                 gcs.append(gc)
-                gparts.append((gp, npart))
+            gparts.append((gp, npart))
             s = segs[i]
             s.c, s.work, s.gbits, s.gc, s.gpart, s.n = _p(cfs[i]), _p(works[i]), _p(g), _p(gc), _p(gp), m
         ride = _PENDING_SM_REDUCE["segs"] if ctx.pg is None else None
@@ -612,11 +606,15 @@ class _MapperMulti(torch.autograd.Function):
                     gs[st - 1] = list(bs)
         sink = mod._gsink.target(list(mod.mapping_network.parameters()))
         gflat, acc = sink if sink is not None else (torch.empty(core._MAPPER_G_SIZE, device=dev), 0)
+        # batch sharded on the global batch: every rank computed the WHOLE
+        # mapper gradient (all ranks' tiles); it contributes 1 / world of it
+        # to the gradient all-reduce, whose sum is then that gradient
+        sc = 1.0 / dp["world"] if dp is not None else 0.0
         if sink is not None and ctx.pg is None and _PENDING_REDUCE["segs"] is None:
-            _PENDING_REDUCE["segs"] = (_chain_segs(gparts, gflat, acc, core._MAPPER_G_SIZE), n, (gparts, keep))
+            _PENDING_REDUCE["segs"] = (_chain_segs(gparts, gflat, acc, core._MAPPER_G_SIZE, sc), n, (gparts, keep))
             torch.autograd.Variable._execution_engine.queue_callback(_flush_pending_reduce)
         else:
-            _reduce_chain(gparts, gflat, acc, core._MAPPER_G_SIZE)
+            _reduce_chain(gparts, gflat, acc, core._MAPPER_G_SIZE, sc)
         grads = (None,) * len(params) if sink is not None else tuple(core._split_flat(gflat, params))
         return (None, None, None, None) + tuple(g.view(s) for g, s in zip(gcs, ctx.shapes)) + grads
 

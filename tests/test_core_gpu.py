@@ -205,8 +205,8 @@ def test_spatial_quantize_errors():
     with pytest.raises(RuntimeError, match="mask"):
         mcaq_cuda_ops.spatial_quantize(x, b, torch.zeros(4, device=DEV), torch.ones(4, device=DEV), 4, 4,
                                        torch.ones(1, 1, 4, 4, device=DEV))
-    with pytest.raises(RuntimeError, match="float32"):
-        mcaq_cuda_ops.spatial_quantize(x.half(), b, torch.zeros(4, device=DEV), torch.ones(4, device=DEV), 4, 4)
+    with pytest.raises(RuntimeError, match="float32"):     # fp16 / bf16 are taken (test_amp_gpu.py)
+        mcaq_cuda_ops.spatial_quantize(x.double(), b, torch.zeros(4, device=DEV), torch.ones(4, device=DEV), 4, 4)
 
 
 # ---- module-level parity vs the oracle --------------------------------------

@@ -8,7 +8,7 @@ T=${1:-r06_dp}
 OUT=$R/gpurun_out/$T
 mkdir -p $OUT
 cd $R
-timeout -k 10 600 python -u -m pytest tests/test_optim_gpu.py tests/test_rccl_graph_gpu.py tests/test_dist_qat_gpu.py tests/test_train_multi_gpu.py tests/test_qat_gpu.py -x -v --timeout 200 --timeout-method thread > $OUT/pytest.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_amp_gpu.py tests/test_core_gpu.py tests/test_optim_gpu.py tests/test_rccl_graph_gpu.py tests/test_dist_qat_gpu.py tests/test_train_multi_gpu.py tests/test_qat_gpu.py -v --timeout 200 --timeout-method thread > $OUT/pytest.log 2>&1
 rc=$?; grep -E "passed|failed|error" $OUT/pytest.log | tail -1; [ $rc -eq 0 ] || { grep -E "FAIL|Error|assert" $OUT/pytest.log | head -30; exit $rc; }
 timeout -k 10 300 python bench.py --config 5 > $OUT/b_c5.json 2> $OUT/b_c5.err || { tail -5 $OUT/b_c5.err; exit 1; }
 MCAQ_BENCH_SHARDED=1 timeout -k 10 300 python bench.py --config 5 > $OUT/b_c5_sharded.json 2> $OUT/b_c5_sharded.err || { tail -5 $OUT/b_c5_sharded.err; exit 1; }
