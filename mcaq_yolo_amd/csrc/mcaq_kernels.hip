@@ -89,6 +89,13 @@ static inline int stats_ppl(int C, int HW) {
 // ATen's amin/amax propagate NaN): unlike fminf/fmaxf in IEEE mode they need
 // no v_max_f32 canonicalisation of loaded or DPP-moved operands, which was a
 // third of pass 1's min/max VALU work.  Exact in any order.
+#ifndef MCAQ_STATS_PERMLANE
+#define MCAQ_STATS_PERMLANE 0
+#endif
+#ifndef MCAQ_STATS_TAIL_PXMAJOR   // tail items pixel-major over the lanes (A/B)
+#define MCAQ_STATS_TAIL_PXMAJOR 0
+#endif
+
 __device__ __forceinline__ float vmin_(float a, float b) { return __builtin_elementwise_minimum(a, b); }
 __device__ __forceinline__ float vmax_(float a, float b) { return __builtin_elementwise_maximum(a, b); }
 template <int CTRL>
@@ -112,8 +119,26 @@ __device__ __forceinline__ void wave_minmax16(float (&mn)[ST_CG], float (&mx)[ST
   rs_step<2, 0x4E>(mn, mx, (lane & 2) != 0);    // quad_perm 2301 (l ^ 2)
   rs_step<1, 0xB1>(mn, mx, (lane & 1) != 0);    // quad_perm 1032 (l ^ 1)
   float a = mn[0], b = mx[0];
+#if MCAQ_STATS_PERMLANE
+  // cross-row exchanges on the VALU (gfx950 v_permlane16_swap / 32_swap with
+  // the value as both operands: each lane sees its own value and lane l ^ 16
+  // (l ^ 32) among the two results) instead of two LDS bpermutes per step
+  {
+    const auto pa = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(a), false, false);
+    const auto pb = __builtin_amdgcn_permlane16_swap(__float_as_uint(b), __float_as_uint(b), false, false);
+    a = vmin_(vmin_(a, __uint_as_float(pa[0])), __uint_as_float(pa[1]));
+    b = vmax_(vmax_(b, __uint_as_float(pb[0])), __uint_as_float(pb[1]));
+  }
+  {
+    const auto pa = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(a), false, false);
+    const auto pb = __builtin_amdgcn_permlane32_swap(__float_as_uint(b), __float_as_uint(b), false, false);
+    a = vmin_(vmin_(a, __uint_as_float(pa[0])), __uint_as_float(pa[1]));
+    b = vmax_(vmax_(b, __uint_as_float(pb[0])), __uint_as_float(pb[1]));
+  }
+#else
   a = vmin_(a, __shfl_xor(a, 16, 64)); b = vmax_(b, __shfl_xor(b, 16, 64));
   a = vmin_(a, __shfl_xor(a, 32, 64)); b = vmax_(b, __shfl_xor(b, 32, 64));
+#endif
   omn = a; omx = b;
 }
 
@@ -418,8 +443,17 @@ __device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, fl
     }
 #endif
     for (int it = early ? items : tid; it < items; it += 256) {
+#if MCAQ_STATS_TAIL_PXMAJOR
+      // consecutive lanes on consecutive tail pixels of one (cascade, block):
+      // each load instruction touches a few rows, not one row per lane
+      const int i = it % ntail, rem = it / ntail;
+      const int k = rem / nbt, j = rem - k * nbt;
+      const int slot = (i * 4 + k) * nbt + j;
+#else
       const int i = it / (4 * nbt), rem = it - i * (4 * nbt);
       const int k = rem / nbt, j = rem - k * nbt;
+      const int slot = it;
+#endif
       const int p = tstart + i;
       const int r0 = 16 * j, n = imin_(16, nilp - r0);
       float v[16];
@@ -428,7 +462,7 @@ __device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, fl
       float sg = 0.0f, sa = 0.0f;
 #pragma unroll
       for (int e = 0; e < 16; ++e) if (e < n) { sg = sg + v[e]; sa = sa + fabsf(v[e]); }
-      tsg[it] = sg; tsa[it] = sa;
+      tsg[slot] = sg; tsa[slot] = sa;
     }
     __syncthreads();
     const int i = tid - (tstart - base);
