@@ -155,45 +155,51 @@ __device__ __forceinline__ unsigned short f_bf16(float f) {
   if ((u & 0x7fffffffu) > 0x7f800000u) return (unsigned short)((u >> 16) | 0x40u);   // quiet NaN
   return (unsigned short)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
 }
+// The nontemporal choice is a template argument: a runtime `nt ? ntload(p)
+// : *p` lets LLVM merge the two loads of one address and drop the
+// nontemporal bit (round 6: pass 1's x loads lost `nt` that way, -10 % on
+// the config-2 step until caught by an ISA diff).
+template <bool NT, typename V>
+__device__ __forceinline__ V ld_v(const V* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <bool NT, typename V>
+__device__ __forceinline__ void st_v(V* p, V v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
 template <typename T> struct ElemIO;
 template <> struct ElemIO<float> {
   static __device__ __forceinline__ float ld(const float* p) { return *p; }
-  static __device__ __forceinline__ mcaq_f4v ld4(const float* p, bool nt) {
-    return nt ? __builtin_nontemporal_load(reinterpret_cast<const mcaq_f4v*>(p)) : *reinterpret_cast<const mcaq_f4v*>(p);
+  template <bool NT> static __device__ __forceinline__ mcaq_f4v ld4(const float* p) {
+    return ld_v<NT>(reinterpret_cast<const mcaq_f4v*>(p));
   }
   static __device__ __forceinline__ float2 ld2(const float* p) { return *reinterpret_cast<const float2*>(p); }
-  static __device__ __forceinline__ void st4(float* p, mcaq_f4v v, bool nt) {
-    if (nt) __builtin_nontemporal_store(v, reinterpret_cast<mcaq_f4v*>(p));
-    else *reinterpret_cast<mcaq_f4v*>(p) = v;
+  template <bool NT> static __device__ __forceinline__ void st4(float* p, mcaq_f4v v) {
+    st_v<NT>(reinterpret_cast<mcaq_f4v*>(p), v);
   }
 };
 template <> struct ElemIO<_Float16> {
   static __device__ __forceinline__ float ld(const _Float16* p) { return (float)*p; }
-  static __device__ __forceinline__ mcaq_f4v ld4(const _Float16* p, bool nt) {
-    const mcaq_h4v h = nt ? __builtin_nontemporal_load(reinterpret_cast<const mcaq_h4v*>(p))
-                          : *reinterpret_cast<const mcaq_h4v*>(p);
-    return __builtin_convertvector(h, mcaq_f4v);
+  template <bool NT> static __device__ __forceinline__ mcaq_f4v ld4(const _Float16* p) {
+    return __builtin_convertvector(ld_v<NT>(reinterpret_cast<const mcaq_h4v*>(p)), mcaq_f4v);
   }
   static __device__ __forceinline__ float2 ld2(const _Float16* p) { return make_float2((float)p[0], (float)p[1]); }
-  static __device__ __forceinline__ void st4(_Float16* p, mcaq_f4v v, bool nt) {
-    const mcaq_h4v h = __builtin_convertvector(v, mcaq_h4v);
-    if (nt) __builtin_nontemporal_store(h, reinterpret_cast<mcaq_h4v*>(p));
-    else *reinterpret_cast<mcaq_h4v*>(p) = h;
+  template <bool NT> static __device__ __forceinline__ void st4(_Float16* p, mcaq_f4v v) {
+    st_v<NT>(reinterpret_cast<mcaq_h4v*>(p), __builtin_convertvector(v, mcaq_h4v));
   }
 };
 struct Bf16 { unsigned short u; };
 template <> struct ElemIO<Bf16> {
   static __device__ __forceinline__ float ld(const Bf16* p) { return bf16_f(p->u); }
-  static __device__ __forceinline__ mcaq_f4v ld4(const Bf16* p, bool nt) {
-    const mcaq_u4v u = nt ? __builtin_nontemporal_load(reinterpret_cast<const mcaq_u4v*>(p))
-                          : *reinterpret_cast<const mcaq_u4v*>(p);
+  template <bool NT> static __device__ __forceinline__ mcaq_f4v ld4(const Bf16* p) {
+    const mcaq_u4v u = ld_v<NT>(reinterpret_cast<const mcaq_u4v*>(p));
     return mcaq_f4v{bf16_f(u.x), bf16_f(u.y), bf16_f(u.z), bf16_f(u.w)};
   }
   static __device__ __forceinline__ float2 ld2(const Bf16* p) { return make_float2(bf16_f(p[0].u), bf16_f(p[1].u)); }
-  static __device__ __forceinline__ void st4(Bf16* p, mcaq_f4v v, bool nt) {
-    const mcaq_u4v u = mcaq_u4v{f_bf16(v.x), f_bf16(v.y), f_bf16(v.z), f_bf16(v.w)};
-    if (nt) __builtin_nontemporal_store(u, reinterpret_cast<mcaq_u4v*>(p));
-    else *reinterpret_cast<mcaq_u4v*>(p) = u;
+  template <bool NT> static __device__ __forceinline__ void st4(Bf16* p, mcaq_f4v v) {
+    st_v<NT>(reinterpret_cast<mcaq_u4v*>(p), mcaq_u4v{f_bf16(v.x), f_bf16(v.y), f_bf16(v.z), f_bf16(v.w)});
   }
 };
 
@@ -268,7 +274,7 @@ __device__ __noinline__ float seq_sum(const T* xb, int HW, int p, int C) {
 // order instead: their 4 x ceil(C/64) independent 16-row block sums are spread
 // over the workgroup (one load round trip), then folded per pixel.
 template <int PPL, bool kVec, typename T>
-__device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, float* lds) {
+__device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, float* lds, const int only_round = -1) {
   float (*bsg)[256] = reinterpret_cast<float (*)[256]>(lds);
   float (*bsa)[256] = reinterpret_cast<float (*)[256]>(lds + ST_WAVES * 256);
   constexpr int UPIX = 64 * PPL;
@@ -333,6 +339,54 @@ __device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, fl
   // * PPL = 64 floats per lane), so a unit with several channel rounds still
   // pays about one memory latency per MR rounds
   constexpr int MR = MCAQ_STATS_LANE_FLOATS / (ST_CG * PPL) > 0 ? MCAQ_STATS_LANE_FLOATS / (ST_CG * PPL) : 1;
+#ifdef MCAQ_PROBE_STATS_SPLIT
+  // timing probe only (wrong outputs): this workgroup loads one channel round
+  // of the unit and stores its block sums, no fold, no tail
+  if (only_round >= 0) {
+    const int r = only_round;
+    const int blk = imin_(r * ST_WAVES + wv, nblk - 1);
+    const int c0 = blk * ST_CG, nc = imin_(ST_CG, C - c0);
+    const int qa = pv[0] ? q0 : 0;
+    float v[ST_CG][PPL];
+#pragma unroll
+    for (int i = 0; i < ST_CG; ++i) {
+      const T* row = xb + (size_t)(c0 + (i < nc ? i : 0)) * HW;
+      if (kVec && PPL == 4) {
+        const mcaq_f4v t = ElemIO<T>::template ld4<true>(row + qa);
+        v[i][0] = t.x; v[i][1 % PPL] = t.y; v[i][2 % PPL] = t.z; v[i][3 % PPL] = t.w;
+      } else {
+#pragma unroll
+        for (int k = 0; k < PPL; ++k) v[i][k] = ElemIO<T>::ld(row + imin_(q0 + k, HW - 1));
+      }
+    }
+    float gb[PPL], ab[PPL];
+#pragma unroll
+    for (int k = 0; k < PPL; ++k) { gb[k] = 0.0f; ab[k] = 0.0f; }
+#pragma unroll
+    for (int i = 0; i < ST_CG; ++i)
+      if (i < nc) {
+#pragma unroll
+        for (int k = 0; k < PPL; ++k) { gb[k] = gb[k] + v[i][k]; ab[k] = ab[k] + fabsf(v[i][k]); }
+      }
+    if (want_m) {
+      float mn[ST_CG], mx[ST_CG];
+#pragma unroll
+      for (int i = 0; i < ST_CG; ++i) {
+        float lo = v[i][0], hi = v[i][0];
+#pragma unroll
+        for (int k = 1; k < PPL; ++k) { lo = vmin_(lo, v[i][k]); hi = vmax_(hi, v[i][k]); }
+        mn[i] = lo; mx[i] = hi;
+      }
+      float omn, omx;
+      wave_minmax16(mn, mx, lane, omn, omx);
+      if (lane < 16 && lane < nc) { S.pmin[(size_t)lu * C + c0 + lane] = omn; S.pmax[(size_t)lu * C + c0 + lane] = omx; }
+    }
+#pragma unroll
+    for (int k = 0; k < PPL; ++k)
+      if (pv[k] && want_g) S.gray[(size_t)b * HW + q0 + k] = gb[k] + ab[k];
+    return;
+  }
+#endif
   for (int r0 = 0; r0 < rounds; r0 += MR) {
     float v[MR][ST_CG][PPL];
     const int qa = pv[0] ? q0 : 0;
@@ -350,9 +404,9 @@ __device__ __forceinline__ void stats_unit(const mcaq_stats_scale& S, int lu, fl
           // morphology of the other in-flight batches gains ~3 % per step
           // (profiles/r01_stats_ntl_ab/)
 #if defined(MCAQ_STATS_PLAIN_LOADS)
-          const mcaq_f4v t = ElemIO<T>::ld4(row + qa, false);
+          const mcaq_f4v t = ElemIO<T>::template ld4<false>(row + qa);
 #else
-          const mcaq_f4v t = ElemIO<T>::ld4(row + qa, true);
+          const mcaq_f4v t = ElemIO<T>::template ld4<true>(row + qa);
 #endif
           v[rr][i][0] = t.x; v[rr][i][1 % PPL] = t.y; v[rr][i][2 % PPL] = t.z; v[rr][i][3 % PPL] = t.w;
         } else if (kVec && PPL == 2) {
@@ -541,7 +595,7 @@ __device__ __forceinline__ void stats_dispatch(const StatsArgs& a, float* lds, c
   int lu = unit - a.s[si].unit_begin;
   const mcaq_stats_scale S = a.s[si];   // wave-uniform index: scalar loads from the kernarg segment
   const int ppl = a.ppl[si];
-#if MCAQ_STATS_XCD
+#if MCAQ_STATS_XCD && !defined(MCAQ_PROBE_STATS_SPLIT)
   {
     const int n = (si + 1 < a.nscales ? a.s[si + 1].unit_begin : a.units_total) - a.s[si].unit_begin;
     const int x0 = a.units_total - a.s[si].unit_begin - n;     // first blockIdx of this scale
@@ -552,13 +606,22 @@ __device__ __forceinline__ void stats_dispatch(const StatsArgs& a, float* lds, c
     }
   }
 #endif
+#ifdef MCAQ_PROBE_STATS_SPLIT
+  int rnd = -1;
+  {
+    const int nb = (S.C + ST_CG - 1) / ST_CG, R = (nb + ST_WAVES - 1) / ST_WAVES;
+    if (R >= 2) { rnd = lu % R; lu /= R; }
+  }
+#else
+  const int rnd = -1;
+#endif
   if constexpr (MCAQ_STATS_MAXPPL >= 4) {
-    if (ppl == 4) { stats_unit<4, kVec, T>(S, lu, lds); return; }
+    if (ppl == 4) { stats_unit<4, kVec, T>(S, lu, lds, rnd); return; }
   }
   if constexpr (MCAQ_STATS_MAXPPL >= 2) {
-    if (ppl == 2) { stats_unit<2, kVec, T>(S, lu, lds); return; }
+    if (ppl == 2) { stats_unit<2, kVec, T>(S, lu, lds, rnd); return; }
   }
-  stats_unit<1, kVec, T>(S, lu, lds);
+  stats_unit<1, kVec, T>(S, lu, lds, rnd);
 }
 
 template <bool kVec, typename T = float>
@@ -1223,7 +1286,7 @@ __device__ __forceinline__ void quant_tile_unit(const QuantArgs& a, const int un
   typedef float f4v __attribute__((ext_vector_type(4)));
   f4v v[QCW];
 #pragma unroll
-  for (int c = 0; c < QCW; ++c) v[c] = ElemIO<T>::ld4(xb + (size_t)imin_(c, imax_(ncw - 1, 0)) * HW + qa, kNTL);
+  for (int c = 0; c < QCW; ++c) v[c] = ElemIO<T>::template ld4<kNTL>(xb + (size_t)imin_(c, imax_(ncw - 1, 0)) * HW + qa);
   // ---- 3. the table (IEEE divisions of QuantizationParameters), staged m(tile)
   {
     const int kq = imin_(tid >> 5, NB - 1);     // every thread stores an entry (unused rows harmless)
@@ -1295,7 +1358,7 @@ __device__ __forceinline__ void quant_tile_unit(const QuantArgs& a, const int un
               quant_dequant_any(v[c].w, q)};
       if (kM != QM_NONE) o = o * f4v{m01.x, m01.y, m23.x, m23.y};
     }
-    if (pv) ElemIO<TO>::st4(yb + (size_t)c * HW + q0, o, kNTS);
+    if (pv) ElemIO<TO>::template st4<kNTS>(yb + (size_t)c * HW + q0, o);
   }
 }
 
@@ -1378,6 +1441,12 @@ static int stats_args(const mcaq_stats_scale* scales, int nscales, StatsArgs& a,
       return (int)hipErrorInvalidValue;    // one element type per launch
     a.ppl[i] = stats_ppl(scales[i].C, HW);
     units += mcaq_stats_units(scales[i].B, scales[i].C, scales[i].H, scales[i].W);
+#ifdef MCAQ_PROBE_STATS_SPLIT
+    {
+      const int nb = (scales[i].C + ST_CG - 1) / ST_CG, R = (nb + ST_WAVES - 1) / ST_WAVES;
+      if (R >= 2) units += (R - 1) * mcaq_stats_units(scales[i].B, scales[i].C, scales[i].H, scales[i].W);
+    }
+#endif
   }
   a.nscales = nscales;
   a.units_total = units;
