@@ -382,6 +382,10 @@ def main_qat(args, world, rank, dev, pg):
 # independent batches per launch set (engine.HookPlan batches): measured
 # DESIGN.md s.3 "Round 5"
 LAUNCH_BATCHES = 2
+# per config, measured (profiles/r06_configs/): config 3's batch
+# is 1.1 GB of x, two of them per launch lose to one (283.7 vs 271.9 k img/s);
+# configs 2 and 4 gain from two (540 k; 199.3 vs 188.9 k)
+LAUNCH_BATCHES_BY_CONFIG = {2: 2, 3: 1, 4: 2}
 
 HOOK_METRIC = ("images/sec @640x640 MCAQ hook path (C3/C4/C5 complexity + bit mapper + 2-8 bit quant), "
                "1/2/4/8 MI355X; % HBM roofline")
@@ -851,7 +855,7 @@ def main():
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS) + [5],
                     help="2/3/4: inference hook path; 5: QAT hook training step")
     ap.add_argument("--pipeline", type=int, default=3, help="launch sets in flight (HIP streams)")
-    ap.add_argument("--launch-batches", type=int, default=LAUNCH_BATCHES,
+    ap.add_argument("--launch-batches", type=int, default=None,
                     help="independent batches per launch set (each kernel launch carries that many batches, "
                          "each with its own statistics and outputs; ms_per_step still counts one batch)")
     ap.add_argument("--inputs", type=int, default=0,
@@ -947,6 +951,8 @@ def main():
         return main_score(args, world, rank, dev, pg)
     name, B, chans, grid, mapper = CONFIGS[args.config]
     depth = max(1, args.pipeline)
+    if args.launch_batches is None:
+        args.launch_batches = LAUNCH_BATCHES_BY_CONFIG.get(args.config, LAUNCH_BATCHES)
     nbat = max(1, args.launch_batches)
     # whole launch sets: K (and the warmup) rounded up to a multiple of the batches per launch
     args.steps = -(-args.steps // nbat) * nbat
