@@ -532,7 +532,7 @@ def run_e2e(cfg, steps, warmup, world, rank, dev, pg, amp=False, eager=False, fu
     return {
         "metric": E2E_METRIC, "value": round(world * B / step_s, 2), "unit": "images/s", "n_gpus": world,
         "steps": steps, "warmup": warmup, "ms_per_step": round(step_s * 1e3, 4), "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "bf16-net/f32-hooks" if amp else "f32",
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16-net/bf16-maps-f32-math-hooks" if amp else "f32",
         "data": "synthetic torch.rand images 640x640, seeded YOLOv8 + MCAQ weights, class biases shifted "
                 "by %.3f so ~%d anchors/image clear conf %.2f" % (delta, E2E_TARGET_CANDIDATES, E2E_CONF),
         "config": {"workload": "%s bs%d/GPU 640x640 end-to-end: YOLOv8 (MIOpen) + MCAQ hooks C3/C4/C5 (HIP) + "
@@ -871,7 +871,8 @@ def main():
     ap.add_argument("--score-batch", type=int, default=32, help="--score: images per launch")
     ap.add_argument("--e2e-inflight", type=int, default=2,
                     help="end-to-end leg: batches in flight on as many HIP streams (one graph each)")
-    ap.add_argument("--amp", action="store_true", help="--e2e: network under bf16 autocast (hooks stay fp32)")
+    ap.add_argument("--amp", action="store_true",
+                    help="--e2e: network under bf16 autocast (the hooks read the bf16 maps natively, fp32 arithmetic)")
     ap.add_argument("--no-fuse", action="store_true", help="--e2e: keep Conv and BatchNorm separate")
     ap.add_argument("--channels-last", action="store_true", help="--e2e: NHWC network (experiment)")
     ap.add_argument("--find", action="store_true", help="--e2e: MIOpen Find (torch.backends.cudnn.benchmark)")
