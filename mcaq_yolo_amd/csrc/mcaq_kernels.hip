@@ -1243,9 +1243,38 @@ __global__ MCAQ_QUANT_LB void mcaq_quant_kernel(QuantArgs a) {
 // VALU instructions per wave on index arithmetic and its integer divisions:
 // rocprofv3 SQ_INSTS_VALU, profiles/r04_sq/).  Soft mask: none or m(tile)
 // values (QM_NONE / QM_MT_LDS); at most 8 bit widths.
-template <bool kNTL, bool kNTS, int kM, typename T, typename TO>
+typedef float qt_f4v __attribute__((ext_vector_type(4)));
+
+// the x rows of one unit (8 x 16 B per lane) into v: step 2 of quant_tile_unit,
+// issued ahead of time by the pipelined kernel
+template <bool kNTL, typename T>
+__device__ __forceinline__ void quant_tile_load(const QuantArgs& a, const int unit, qt_f4v (&v)[QCW]) {
+  int si = 0;
+  while (si + 1 < a.nscales && unit >= a.s[si + 1].unit_begin) ++si;
+  const mcaq_quant_scale& S = a.s[si];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int HW = S.H * S.W;
+  const int nsl = (S.C + QSLICE - 1) / QSLICE, upi = (HW + 255) >> 8;
+  const int lu = unit - S.unit_begin;
+  const int q1 = div_small(lu, nsl, a.rnsl[si]);
+  const int slice = lu - q1 * nsl;
+  const int b = div_small(q1, upi, a.rupi[si]);
+  const int chunk = q1 - b * upi;
+  const int c0 = slice * QSLICE;
+  const int nc = imin_(QSLICE, S.C - c0);
+  const int q0 = chunk * 256 + lane * 4;
+  const int qa = q0 < HW ? q0 : 0;
+  const int cw = wv * QCW;
+  const int ncw = imin_(QCW, nc - cw);
+  const size_t rowbase = ((size_t)b * S.C + c0 + imax_(imin_(cw, nc - 1), 0)) * HW;
+  const T* xb = reinterpret_cast<const T*>(S.x) + rowbase;
+#pragma unroll
+  for (int c = 0; c < QCW; ++c) v[c] = ElemIO<T>::template ld4<kNTL>(xb + (size_t)imin_(c, imax_(ncw - 1, 0)) * HW + qa);
+}
+
+template <bool kNTL, bool kNTS, int kM, typename T, typename TO, bool kPre = false>
 __device__ __forceinline__ void quant_tile_unit(const QuantArgs& a, const int unit, float4* qt, float* mts, float4* mq4,
-                                                int* qany) {
+                                                int* qany, qt_f4v (*pre)[QCW] = nullptr) {
   typedef float f2 __attribute__((ext_vector_type(2)));
   int si = 0;
   while (si + 1 < a.nscales && unit >= a.s[si + 1].unit_begin) ++si;
@@ -1285,8 +1314,13 @@ __device__ __forceinline__ void quant_tile_unit(const QuantArgs& a, const int un
   TO* yb = reinterpret_cast<TO*>(S.y) + rowbase;
   typedef float f4v __attribute__((ext_vector_type(4)));
   f4v v[QCW];
+  if constexpr (kPre) {
 #pragma unroll
-  for (int c = 0; c < QCW; ++c) v[c] = ElemIO<T>::template ld4<kNTL>(xb + (size_t)imin_(c, imax_(ncw - 1, 0)) * HW + qa);
+    for (int c = 0; c < QCW; ++c) v[c] = (*pre)[c];
+  } else {
+#pragma unroll
+    for (int c = 0; c < QCW; ++c) v[c] = ElemIO<T>::template ld4<kNTL>(xb + (size_t)imin_(c, imax_(ncw - 1, 0)) * HW + qa);
+  }
   // ---- 3. the table (IEEE divisions of QuantizationParameters), staged m(tile)
   {
     const int kq = imin_(tid >> 5, NB - 1);     // every thread stores an entry (unused rows harmless)
@@ -1376,6 +1410,37 @@ __global__ MCAQ_QUANT_LB void mcaq_quant_tile_kernel(QuantArgs a) {
 #else
   quant_tile_unit<kNTL, kNTS, kM, T, TO>(a, (int)blockIdx.x, qt, mts, mq4, qany);
 #endif
+}
+
+// Pipelined persistent form (MCAQ_QUANT_PIPE workgroups per CU, A/B): each
+// workgroup walks units u, u + grid, ...; the x rows of its NEXT unit are in
+// flight while the current one runs its prologue and stores (a 2-deep
+// register pipeline, as tools/probe/narrow_probe.hip's D2 copy).  Same
+// per-element arithmetic as mcaq_quant_tile_kernel.
+#ifndef MCAQ_QUANT_PIPE
+#define MCAQ_QUANT_PIPE 0
+#endif
+template <bool kNTL, bool kNTS, int kM, typename T = float, typename TO = T>
+__global__ __launch_bounds__(256, 2) void mcaq_quant_tile_pipe_kernel(QuantArgs a) {
+  __shared__ float4 qt[8 * QSLICE];
+  __shared__ float mts[kM == QM_MT_LDS ? QMAXNT : 1];
+  __shared__ float4 mq4[64];
+  __shared__ int qany[QSLICE];
+  qt_f4v va[QCW], vb[QCW];
+  const int grid = (int)gridDim.x, total = a.units_total;
+  int u = (int)blockIdx.x;
+  if (u < total) quant_tile_load<kNTL, T>(a, u, va);
+  for (; u < total; u += 2 * grid) {
+    const int un = u + grid;
+    if (un < total) quant_tile_load<kNTL, T>(a, un, vb);
+    quant_tile_unit<kNTL, kNTS, kM, T, TO, true>(a, u, qt, mts, mq4, qany, &va);
+    __syncthreads();
+    if (un >= total) break;
+    const int unn = un + grid;
+    if (unn < total) quant_tile_load<kNTL, T>(a, unn, va);
+    quant_tile_unit<kNTL, kNTS, kM, T, TO, true>(a, un, qt, mts, mq4, qany, &vb);
+    __syncthreads();
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1934,6 +1999,22 @@ int mcaq_quant(const mcaq_quant_scale* scales, int nscales, hipStream_t stream) 
     }
     return (int)hipGetLastError();
   }
+#if MCAQ_QUANT_PIPE > 0
+  if (tile_ok) {
+    const dim3 gp(imin_(units, MCAQ_QUANT_PIPE * 256));
+    switch ((kind == QM_NONE ? 0 : 4) + (nt & 3)) {
+      case 0: launch_k(mcaq_quant_tile_pipe_kernel<false, false, QM_NONE>, gp, t, 0, stream, a); break;
+      case 1: launch_k(mcaq_quant_tile_pipe_kernel<false, true, QM_NONE>, gp, t, 0, stream, a); break;
+      case 2: launch_k(mcaq_quant_tile_pipe_kernel<true, false, QM_NONE>, gp, t, 0, stream, a); break;
+      case 3: launch_k(mcaq_quant_tile_pipe_kernel<true, true, QM_NONE>, gp, t, 0, stream, a); break;
+      case 4: launch_k(mcaq_quant_tile_pipe_kernel<false, false, QM_MT_LDS>, gp, t, 0, stream, a); break;
+      case 5: launch_k(mcaq_quant_tile_pipe_kernel<false, true, QM_MT_LDS>, gp, t, 0, stream, a); break;
+      case 6: launch_k(mcaq_quant_tile_pipe_kernel<true, false, QM_MT_LDS>, gp, t, 0, stream, a); break;
+      default: launch_k(mcaq_quant_tile_pipe_kernel<true, true, QM_MT_LDS>, gp, t, 0, stream, a); break;
+    }
+    return (int)hipGetLastError();
+  }
+#endif
   if (tile_ok) {
     const dim3 g(MCAQ_STREAM_CAP > 0 ? imin_(units, MCAQ_STREAM_CAP * 256) : units);
     switch ((kind == QM_NONE ? 0 : 4) + (nt & 3)) {
