@@ -143,7 +143,8 @@ def _rel(got, ref, rtol, floor=1e-30, what=""):
     assert err <= rtol * scale, "%s: max err %g vs scale %g" % (what, err, scale)
 
 
-def test_sharded_qat_step_equals_single_process():
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_qat_step_equals_single_process(world):
     import torch.multiprocessing as mp
     feats, G, GB = _inputs()
     outs, bits, gx, grads, bufs, nfused = _step(_hooks("cuda:0"), feats, G, GB, "cuda:0")
@@ -151,19 +152,19 @@ def test_sharded_qat_step_equals_single_process():
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_entry, args=(r, WORLD, port, q)) for r in range(WORLD)]
+    ps = [ctx.Process(target=_entry, args=(r, world, port, q)) for r in range(world)]
     for p in ps:
         p.start()
-    res = dict(q.get(timeout=300) for _ in range(WORLD))
+    res = dict(q.get(timeout=300) for _ in range(world))
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    n = B // WORLD
+    n = B // world
     gmax = {}
     for k, v in grads.items():
         mod = k.rsplit(".", 2)[0]
         gmax[mod] = max(gmax.get(mod, 0.0), float(np.abs(v).max()))
-    for r in range(WORLD):
+    for r in range(world):
         r_outs, r_bits, r_gx, r_grads, r_bufs, r_nfused = res[r]
         assert r_nfused == 3, "the sharded step must run the fused mapper kernels"
         sl = slice(r * n, (r + 1) * n)

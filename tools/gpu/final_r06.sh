@@ -19,6 +19,8 @@ timeout -k 10 300 python bench.py --config 5 > $OUT/bench_config5.json 2> $OUT/b
 MCAQ_BENCH_SHARDED=1 timeout -k 10 300 python bench.py --config 5 --no-cpu > $OUT/bench_config5_sharded.json 2> $OUT/bench_config5_sharded.err || { tail -5 $OUT/bench_config5_sharded.err; exit 1; }
 timeout -k 10 300 python bench.py --e2e --amp --steps 20 --warmup 3 > $OUT/bench_e2e_amp.json 2> $OUT/bench_e2e_amp.err || { tail -5 $OUT/bench_e2e_amp.err; exit 1; }
 MCAQ_BENCH_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --no-cpu --steps 20 --warmup 4 > $OUT/bench_gloo_n2.json 2> $OUT/bench_gloo_n2.err || { tail -5 $OUT/bench_gloo_n2.err; exit 1; }
+MCAQ_BENCH_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 4 --no-cpu --no-e2e --steps 20 --warmup 4 > $OUT/bench_gloo_n4.json 2> $OUT/bench_gloo_n4.err || { tail -5 $OUT/bench_gloo_n4.err; exit 1; }
+MCAQ_BENCH_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 4 --config 5 --no-cpu --steps 10 --warmup 3 > $OUT/bench_gloo_n4_c5.json 2> $OUT/bench_gloo_n4_c5.err || { tail -5 $OUT/bench_gloo_n4_c5.err; exit 1; }
 prof() {  # name, bench args...
   local n=$1; shift
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/$n -o run --output-format csv -- python3 $R/bench.py --no-cpu --no-e2e "$@" > $OUT/$n.log 2>&1) || { tail -8 $OUT/$n.log; exit 1; }
@@ -31,7 +33,7 @@ python3 tools/qat_timeline.py $OUT/c5/run_kernel_trace.csv 3 > $OUT/timeline_c5.
 python3 tools/trace_analyze.py $OUT/c2_p3_k2/run_kernel_trace.csv 600 > $OUT/trace_p3_k2.txt
 python3 - <<PY
 import json, csv
-for k in ("bench_default", "bench_config5", "bench_config5_sharded", "bench_e2e_amp", "bench_gloo_n2"):
+for k in ("bench_default", "bench_config5", "bench_config5_sharded", "bench_e2e_amp", "bench_gloo_n2", "bench_gloo_n4", "bench_gloo_n4_c5"):
     d = json.loads([l for l in open("$OUT/%s.json" % k).read().splitlines() if l.startswith("{")][-1])
     r = d.get("path_roofline") or d.get("step_roofline") or {}
     print(k, d["n_gpus"], d["value"], d["ms_per_step"], r.get("frac"), (d.get("roofline") or {}).get("frac"), (d.get("cpu_baseline") or {}).get("value"), (d.get("e2e") or {}).get("value"))
