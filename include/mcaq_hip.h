@@ -44,7 +44,7 @@ typedef void* hipEvent_t;
 extern "C" {
 #endif
 
-#define MCAQ_ABI_VERSION 27
+#define MCAQ_ABI_VERSION 28
 /* feature-map element types (mcaq_stats_scale.dtype, mcaq_quant_scale.dtype) */
 #define MCAQ_DTYPE_F32 0
 #define MCAQ_DTYPE_F16 1
@@ -509,6 +509,28 @@ int mcaq_head_train_backward_multi_ride(const mcaq_cmlp_params* P, const mcaq_he
 int mcaq_mapper_train_backward_multi_ride(const mcaq_mapper_params* P, const mcaq_mapper_seg* segs, int nseg,
                                           float min_bits, float max_bits, float temperature,
                                           const mcaq_reduce_seg* rsegs, int nr, hipStream_t stream);
+/* The mapper's train-mode forward / backward of every segment as ONE launch
+ * each (round 6): the batch statistics between the stages are exchanged
+ * inside the launch through `sync`, a device buffer of
+ * mcaq_mapper_sync_bytes(total workgroups) bytes (workgroups = sum over the
+ * segments of ceil(n / 64), at most mcaq_mapper_fused_max_wg()), zeroed
+ * before its first use and whenever the segments' sizes change, and not used
+ * by two launches at once (one buffer per mapper and layout; forward and
+ * backward of the same segments share it).  Results are bit-identical to
+ * mcaq_mapper_train_forward_multi / _backward_multi_ride.  Word 32 of the
+ * buffer (uint32) is a status word: nonzero after an exchange timed out
+ * (results then invalid).  hipErrorInvalidValue when the buffer is missing or
+ * too small or the workgroups exceed the maximum (use the staged calls). */
+size_t mcaq_mapper_sync_bytes(int total_wg);
+int mcaq_mapper_fused_max_wg(void);
+int mcaq_mapper_train_forward_fused(const mcaq_mapper_params* P, const mcaq_mapper_seg* segs, int nseg,
+                                    float min_bits, float max_bits, float temperature, float momentum,
+                                    int round_bits, int update_stats, void* sync, size_t sync_bytes,
+                                    hipStream_t stream);
+int mcaq_mapper_train_backward_fused(const mcaq_mapper_params* P, const mcaq_mapper_seg* segs, int nseg,
+                                     float min_bits, float max_bits, float temperature,
+                                     const mcaq_reduce_seg* rsegs, int nr, void* sync, size_t sync_bytes,
+                                     hipStream_t stream);
 
 /* gparams of the mapper / head backward: accumulate != 0 adds to gparams
  * (the parameters' persistent gradient storage), 0 overwrites it; NULL

@@ -9,7 +9,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libmcaq_hip.so")
-ABI_VERSION = 27
+ABI_VERSION = 28
 DTYPE_F32, DTYPE_F16, DTYPE_BF16 = 0, 1, 2   # MCAQ_DTYPE_*
 MAX_SEGMENTS = 9   # MCAQ_MAX_SEGMENTS: segments (hook scale x batch) per launch
 
@@ -76,6 +76,7 @@ class SmaskParams(ctypes.Structure):
 
 
 MCAQ_TRAIN_MAXSEG = 3
+MAPPER_SYNC_STATUS_WORD = 32    # uint32 index of the fused mapper sync buffer's status word
 
 
 class MapperSeg(ctypes.Structure):
@@ -162,7 +163,9 @@ EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats",
            "mcaq_mapper_train_forward_stage_multi", "mcaq_mapper_train_backward_stage_multi", "mcaq_clip_adamw", "mcaq_clip_adamw_work_floats",
            "mcaq_bit_budget_forward", "mcaq_qat_smask_backward_multi", "mcaq_qat_forward_budget",
            "mcaq_ema_stats_multi_running", "mcaq_head_train_backward_multi_ride",
-           "mcaq_stats_pack", "mcaq_morph_ema", "mcaq_mapper_train_backward_multi_ride", "mcaq_dp_unpack")
+           "mcaq_stats_pack", "mcaq_morph_ema", "mcaq_mapper_train_backward_multi_ride", "mcaq_dp_unpack",
+           "mcaq_mapper_sync_bytes", "mcaq_mapper_fused_max_wg", "mcaq_mapper_train_forward_fused",
+           "mcaq_mapper_train_backward_fused")
 
 _LIB = None
 
@@ -245,6 +248,16 @@ def _declare(lib):
     lib.mcaq_mapper_train_backward_multi_ride.restype = I
     lib.mcaq_mapper_train_backward_multi_ride.argtypes = [ctypes.POINTER(MapperParams), ctypes.POINTER(MapperSeg), I,
                                                           Fl, Fl, Fl, ctypes.POINTER(ReduceSeg), I, P]
+    lib.mcaq_mapper_sync_bytes.restype = SZ
+    lib.mcaq_mapper_sync_bytes.argtypes = [I]
+    lib.mcaq_mapper_fused_max_wg.restype = I
+    lib.mcaq_mapper_fused_max_wg.argtypes = []
+    lib.mcaq_mapper_train_forward_fused.restype = I
+    lib.mcaq_mapper_train_forward_fused.argtypes = [ctypes.POINTER(MapperParams), ctypes.POINTER(MapperSeg), I, Fl, Fl,
+                                                    Fl, Fl, I, I, P, SZ, P]
+    lib.mcaq_mapper_train_backward_fused.restype = I
+    lib.mcaq_mapper_train_backward_fused.argtypes = [ctypes.POINTER(MapperParams), ctypes.POINTER(MapperSeg), I, Fl,
+                                                     Fl, Fl, ctypes.POINTER(ReduceSeg), I, P, SZ, P]
     lib.mcaq_head_train_backward_multi_ride.restype = I
     lib.mcaq_head_train_backward_multi_ride.argtypes = [ctypes.POINTER(CmlpParams), ctypes.POINTER(HeadSeg), I,
                                                         ctypes.POINTER(ReduceSeg), I, P]

@@ -153,6 +153,12 @@ struct MapperTrainArgs {
   const float* gstat1;
   int gworld;
   int wg0;              // first workgroup of this segment in a multi-segment launch (else 0)
+  // fused launches (mcaq_mapper_train_forward_fused / _backward_fused): this
+  // segment's granule region (3 exchanges x nwg x MAPX_STRIDE), its epoch
+  // word and the buffer's status word (mapx_* below)
+  unsigned long long* gx;
+  unsigned* gep;
+  unsigned* gst;
 };
 constexpr int RANK_ENT = 129;   // (mean[64], M2[64], n) of one rank
 
@@ -212,18 +218,75 @@ constexpr int MW = 8;               // waves per mapper workgroup (lane = tile, 
 constexpr int MAPPER_COOP_MAX_WG = 256;   // one-launch (grid-barrier) mapper up to this many workgroups
 constexpr int MTH = 64 * MW;
 
+// ---- fused mapper launches: the batch-statistic partials exchanged inside
+// the launch.  Each of the three exchanges per direction (forward: layer
+// moments of stages 1..3; backward: BN sums of stages 4..2) is a region of
+// nwg x MAPX_STRIDE 8-byte granules {tag, value}: the data is the flag
+// (cdna_hip_programming.md s.6 Guideline 16, R2) - every producer store and
+// every consumer load of a granule is an agent-scope (write-through, sc1)
+// access and the consumer re-reads until every tag matches, so neither side
+// takes a fence or a counter.  tag = epoch * 8 + exchange: the segment's
+// epoch word is read by every wave at launch and advanced by the segment's
+// first workgroup after its last exchange (every workgroup of the segment has
+// read it by then), so granules of earlier launches never match.  The buffer
+// is zeroed whenever its segment layout changes (train_step._mapx_buffer).
+// Bounded spins: a timeout sets the status word and goes on (tests check it).
+typedef unsigned long long mapx_t;
+constexpr int MAPX_STRIDE = 129;   // granules per workgroup per exchange: [0, 128) partials, 128 count
+constexpr int MAPX_HDR = 64;       // header words (epochs of the segments, status at MAPX_STATUS)
+constexpr int MAPX_STATUS = 32;
+
+__device__ __forceinline__ void mapx_put(mapx_t* g, unsigned tag, float v) {
+  __hip_atomic_store(g, ((mapx_t)tag << 32) | (mapx_t)__float_as_uint(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+template <int R>
+__device__ __forceinline__ void mapx_get(mapx_t* const (&g)[R], unsigned tag, float (&v)[R], unsigned* status) {
+  for (unsigned spins = 0;; ++spins) {
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const mapx_t x = __hip_atomic_load(g[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      v[r] = __uint_as_float((unsigned)x);
+      ok = ok && (unsigned)(x >> 32) == tag;
+    }
+    if (ok) return;
+    if (spins >= (1u << 20)) {
+      __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+// this launch's epoch of the segment, in a register of every wave
+__device__ __forceinline__ unsigned mapx_epoch(const MapperTrainArgs& A) {
+  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(A.gep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ mapx_t* mapx_region(const MapperTrainArgs& A, int x) {
+  return A.gx + (size_t)(x - 1) * A.nwg * MAPX_STRIDE;
+}
+
 // per-workgroup (mean, M2) of feature j over this workgroup's valid tiles;
 // MW waves x 64 tiles, each wave 1/MW of the features.
-// v[f]: this lane's tile's value of feature f0 + f (f < NQ)
-template <int NQ>
-__device__ __forceinline__ void wg_moments(const float (&v)[NQ], bool valid, float nvalid, int f0, float* part, int nfeat) {
+// v[f]: this lane's tile's value of feature f0 + f (f < NQ); kX: published
+// as granules of `gx` with `tag` instead of stored to `part`
+template <int NQ, bool kX = false>
+__device__ __forceinline__ void wg_moments(const float (&v)[NQ], bool valid, float nvalid, int f0, float* part, int nfeat,
+                                           mapx_t* gx = nullptr, unsigned tag = 0) {
 #pragma unroll
   for (int f = 0; f < NQ; ++f) {
     const float s = wave_sum(valid ? v[f] : 0.0f);
     const float mean = s / nvalid;
     const float d = valid ? v[f] - mean : 0.0f;
     const float M2 = wave_sum(d * d);
-    if ((threadIdx.x & 63) == 0) { part[f0 + f] = mean; part[nfeat + f0 + f] = M2; }
+    if ((threadIdx.x & 63) == 0) {
+      if constexpr (kX) {
+        mapx_put(gx + f0 + f, tag, mean);
+        mapx_put(gx + nfeat + f0 + f, tag, M2);
+      } else {
+        part[f0 + f] = mean; part[nfeat + f0 + f] = M2;
+      }
+    }
   }
 }
 
@@ -310,8 +373,9 @@ __global__ __launch_bounds__(TILES_THREADS, MCAQ_TILES_MINW) void mcaq_tiles_ema
 // feature in LDS (and, once per launch, the running-stats update).  The MW
 // waves combine interleaved subsets of the workgroups' partials in parallel
 // (Chan), then one thread per feature combines the MW results.
-template <int L>
-__device__ void map_stats(const MapperTrainArgs& A, const MapperWork& W, float* s_mean, float* s_rstd, float* s_tmp) {
+template <int L, bool kX = false>
+__device__ void map_stats(const MapperTrainArgs& A, const MapperWork& W, float* s_mean, float* s_rstd, float* s_tmp,
+                          unsigned E = 0) {
   constexpr int N = MapL<L>::N;
   const int tid = threadIdx.x, j = tid & 63, part = tid >> 6;
   if (j < N) {
@@ -325,12 +389,27 @@ __device__ void map_stats(const MapperTrainArgs& A, const MapperWork& W, float* 
     // partial a round trip of its own), combined in the same order
     for (int w0 = part; w0 < nsrc; w0 += 4 * MW) {
       float nbv[4], mbv[4], m2v[4];
+      if constexpr (kX) {
+        // fused launch: exchange L's granules (the same values, re-read until published)
+        mapx_t* const gx = mapx_region(A, L);
+        mapx_t* gp[12];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int w = imin_(w0 + r * MW, nsrc - 1);
-        nbv[r] = gs ? A.gstat[(size_t)w * RANK_ENT + 128] : W.cnt[w];
-        mbv[r] = gs ? A.gstat[(size_t)w * RANK_ENT + j] : fp[(size_t)w * 128 + j];
-        m2v[r] = gs ? A.gstat[(size_t)w * RANK_ENT + 64 + j] : fp[(size_t)w * 128 + N + j];
+        for (int r = 0; r < 4; ++r) {
+          mapx_t* const b = gx + (size_t)imin_(w0 + r * MW, nsrc - 1) * MAPX_STRIDE;
+          gp[3 * r] = b + 128; gp[3 * r + 1] = b + j; gp[3 * r + 2] = b + N + j;
+        }
+        float v[12];
+        mapx_get<12>(gp, E * 8u + (unsigned)L, v, A.gst);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { nbv[r] = v[3 * r]; mbv[r] = v[3 * r + 1]; m2v[r] = v[3 * r + 2]; }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int w = imin_(w0 + r * MW, nsrc - 1);
+          nbv[r] = gs ? A.gstat[(size_t)w * RANK_ENT + 128] : W.cnt[w];
+          mbv[r] = gs ? A.gstat[(size_t)w * RANK_ENT + j] : fp[(size_t)w * 128 + j];
+          m2v[r] = gs ? A.gstat[(size_t)w * RANK_ENT + 64 + j] : fp[(size_t)w * 128 + N + j];
+        }
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -389,8 +468,13 @@ struct MapFwdLds {
   float w[64 * 34];         // stages 2 / 3: the layer's weights W[f][k] at f * (K + 2) + k (conflict-free MFMA B reads)
 };
 
-template <int S>
-__device__ __forceinline__ void mapper_fwd_stage(const MapperTrainArgs& A, MapFwdLds& L) {
+// kX (fused launch): the moments published as exchange S's granules, the
+// previous layer's read from exchange S - 1 (epoch E); the workgroup's own
+// activations handed to the next stage in LDS (s_a: [tile][feature]; the
+// global copy stays for the backward launch)
+template <int S, bool kX = false>
+__device__ __forceinline__ void mapper_fwd_stage(const MapperTrainArgs& A, MapFwdLds& L, unsigned E = 0,
+                                                 float (*s_a)[65] = nullptr) {
   float (*s_in)[65] = L.in;
   float* s_mean = L.mean;
   float* s_rstd = L.rstd;
@@ -423,9 +507,10 @@ __device__ __forceinline__ void mapper_fwd_stage(const MapperTrainArgs& A, MapFw
   if constexpr (S >= 2) {
     const float* aprev = S == 2 ? W.a1 : (S == 3 ? W.a2 : W.a3);
 #pragma unroll
-    for (int i = 0; i < KP / MW; ++i) apv[i] = aprev[(size_t)(q + i * MW) * A.n + tc];
+    for (int i = 0; i < KP / MW; ++i)
+      apv[i] = kX ? s_a[tc - wgi * TR_TPB][q + i * MW] : aprev[(size_t)(q + i * MW) * A.n + tc];
   }
-  if constexpr (S >= 2) map_stats<S - 1>(A, W, s_mean, s_rstd, s_tmp);
+  if constexpr (S >= 2) map_stats<S - 1, kX>(A, W, s_mean, s_rstd, s_tmp, E);
   if constexpr (S == 2) TSTAMP(51);
   if constexpr (S == 2) TSTAMP(52);
   // ---- layer inputs of this workgroup's tiles -> s_in
@@ -488,6 +573,7 @@ __device__ __forceinline__ void mapper_fwd_stage(const MapperTrainArgs& A, MapFw
       for (int r = 0; r < 4; ++r) {
         const int tg = wgi * TR_TPB + mtb * 16 + 4 * lk + r;
         if (tg < A.n) { aout[(size_t)f * A.n + tg] = d[i][r]; sm += d[i][r]; }
+        if constexpr (kX) s_a[mtb * 16 + 4 * lk + r][f] = d[i][r];
       }
       sm += __shfl_xor(sm, 16, 64);
       sm += __shfl_xor(sm, 32, 64);
@@ -512,11 +598,22 @@ __device__ __forceinline__ void mapper_fwd_stage(const MapperTrainArgs& A, MapFw
     }
     __syncthreads();
     if (tid < N) {
-      float* part = W.fpart(S) + (size_t)wgi * 128;
-      part[tid] = (((red1[tid] + red1[64 + tid]) + red1[128 + tid]) + red1[192 + tid]) / nvalid;
-      part[N + tid] = ((red2[tid] + red2[64 + tid]) + red2[128 + tid]) + red2[192 + tid];
+      const float pm = (((red1[tid] + red1[64 + tid]) + red1[128 + tid]) + red1[192 + tid]) / nvalid;
+      const float p2 = ((red2[tid] + red2[64 + tid]) + red2[128 + tid]) + red2[192 + tid];
+      if constexpr (kX) {
+        mapx_t* const gx = mapx_region(A, S) + (size_t)wgi * MAPX_STRIDE;
+        mapx_put(gx + tid, E * 8u + S, pm);
+        mapx_put(gx + N + tid, E * 8u + S, p2);
+      } else {
+        float* part = W.fpart(S) + (size_t)wgi * 128;
+        part[tid] = pm;
+        part[N + tid] = p2;
+      }
     }
-    if (tid == 0) W.cnt[wgi] = nvalid;
+    if (tid == 0) {
+      if constexpr (kX) mapx_put(mapx_region(A, S) + (size_t)wgi * MAPX_STRIDE + 128, E * 8u + S, nvalid);
+      else W.cnt[wgi] = nvalid;
+    }
     if constexpr (S == 2) TSTAMP(55);
   } else if constexpr (S <= 3) {
     constexpr int K = MapL<S>::K, N = MapL<S>::N, NQ = N / MW;
@@ -542,11 +639,19 @@ __device__ __forceinline__ void mapper_fwd_stage(const MapperTrainArgs& A, MapFw
       for (int f = 0; f < NQ; ++f) o[f] = fmaf(w[(q * NQ + f) * K + k], x[k], o[f]);
     }
 #pragma unroll
-    for (int f = 0; f < NQ; ++f)
+    for (int f = 0; f < NQ; ++f) {
       if (valid) aout[(size_t)(q * NQ + f) * A.n + t] = o[f];
+      if constexpr (kX) s_a[lane][q * NQ + f] = o[f];
+    }
     if constexpr (S == 2) TSTAMP(54);
-    wg_moments<NQ>(o, valid, nvalid, q * NQ, W.fpart(S) + (size_t)wgi * 128, N);
-    if (tid == 0) W.cnt[wgi] = nvalid;
+    if constexpr (kX) {
+      mapx_t* const gx = mapx_region(A, S) + (size_t)wgi * MAPX_STRIDE;
+      wg_moments<NQ, true>(o, valid, nvalid, q * NQ, nullptr, N, gx, E * 8u + S);
+      if (tid == 0) mapx_put(gx + 128, E * 8u + S, nvalid);
+    } else {
+      wg_moments<NQ>(o, valid, nvalid, q * NQ, W.fpart(S) + (size_t)wgi * 128, N);
+      if (tid == 0) W.cnt[wgi] = nvalid;
+    }
     if constexpr (S == 2) TSTAMP(55);
   } else {
     // last layer + sigmoid + bit range, temperature, clamp (+ round)
@@ -631,8 +736,12 @@ struct MapBwdLds {
   float w[64 * 48];        // stages 3 / 2: the layer's weights W[j][k] at j * (K + 16) + k, for W^T g_a
 };
 
-template <int S>
-__device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBwdLds& L) {
+// kX (fused launch): the BN(S-1) sums published as exchange 5 - S's granules,
+// the BN(S) sums read from exchange 4 - S (epoch E); g_y handed from stage
+// to stage in LDS (s_gy: [tile][feature]) instead of the global scratch
+template <int S, bool kX = false>
+__device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBwdLds& L, unsigned E = 0,
+                                                 float (*s_gy)[65] = nullptr) {
   float (*s_h)[65] = L.h;
   float (*s_g)[65] = L.g;
   float* s_mean = L.mean;
@@ -672,7 +781,7 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
 #pragma unroll
     for (int i = 0; i < N1 / MW; ++i) {
       const int j = q + i * MW;
-      gyp[i] = W.gy[(size_t)j * A.n + tc];
+      gyp[i] = kX ? s_gy[tc - wgi * TR_TPB][j] : W.gy[(size_t)j * A.n + tc];
       asp[i] = aS[(size_t)j * A.n + tc];
     }
   }
@@ -723,9 +832,27 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
       const int j = tid & 63, part = tid >> 6;
       if (j < N) {
         float s1 = 0.0f, s2 = 0.0f;
-        const float* bq = W.bpart_of(S + 1);   // written by the previous launch (stage S + 1)
+        if constexpr (kX) {
+          // fused launch: stage S + 1's sums from its granules, the same order
+          mapx_t* const gx = mapx_region(A, 4 - S);
+          for (int w0 = part; w0 < A.nwg; w0 += 4 * MW) {
+            mapx_t* gp[8];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              mapx_t* const b = gx + (size_t)imin_(w0 + r * MW, A.nwg - 1) * MAPX_STRIDE;
+              gp[2 * r] = b + j; gp[2 * r + 1] = b + 64 + j;
+            }
+            float v[8];
+            mapx_get<8>(gp, E * 8u + (unsigned)(4 - S), v, A.gst);
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (w0 + r * MW < A.nwg) { s1 += v[2 * r]; s2 += v[2 * r + 1]; }
+          }
+        } else {
+          const float* bq = W.bpart_of(S + 1);   // written by the previous launch (stage S + 1)
 #pragma unroll 4
-        for (int w = part; w < A.nwg; w += MW) { s1 += bq[(size_t)w * 128 + j]; s2 += bq[(size_t)w * 128 + 64 + j]; }
+          for (int w = part; w < A.nwg; w += MW) { s1 += bq[(size_t)w * 128 + j]; s2 += bq[(size_t)w * 128 + 64 + j]; }
+        }
         s_tmp[part * 128 + j] = s1; s_tmp[part * 128 + 64 + j] = s2;
       }
     }
@@ -853,7 +980,8 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
         const float xh = (ap4[f * SR + r] - smn[f]) * srs[f];
         const float y = sgm[f] * xh + sbe[f];
         const float gy = (tg < A.n && y > 0.0f) ? d[r] : 0.0f;
-        if (tg < A.n) W.gy[(size_t)k * A.n + tg] = gy;
+        if constexpr (kX) s_gy[mtb * 16 + 4 * lk + r][k] = gy;
+        else if (tg < A.n) W.gy[(size_t)k * A.n + tg] = gy;
         s1 += gy; s2 += gy * xh;
       }
       s1 += __shfl_xor(s1, 16, 64); s2 += __shfl_xor(s2, 16, 64);
@@ -864,8 +992,16 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
     __syncthreads();
     if constexpr (S == 3) TSTAMP(46);
     if (tid < K) {
-      bp[tid] = ((red4[tid] + red4[64 + tid]) + red4[128 + tid]) + red4[192 + tid];
-      bp[64 + tid] = ((red4[256 + tid] + red4[320 + tid]) + red4[384 + tid]) + red4[448 + tid];
+      const float b1 = ((red4[tid] + red4[64 + tid]) + red4[128 + tid]) + red4[192 + tid];
+      const float b2 = ((red4[256 + tid] + red4[320 + tid]) + red4[384 + tid]) + red4[448 + tid];
+      if constexpr (kX) {
+        mapx_t* const gx = mapx_region(A, 5 - S) + (size_t)wgi * MAPX_STRIDE;
+        mapx_put(gx + tid, E * 8u + (5 - S), b1);
+        mapx_put(gx + 64 + tid, E * 8u + (5 - S), b2);
+      } else {
+        bp[tid] = b1;
+        bp[64 + tid] = b2;
+      }
     }
   } else if constexpr (S >= 2) {
     constexpr int NO = S == 4 ? 1 : MapL<S>::N;
@@ -897,7 +1033,8 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
       const float y = sgm[f] * xh + sbe[f];
       const float gy = (valid && y > 0.0f) ? acc : 0.0f;
       gyv[f] = gy; xhv[f] = xh;
-      if (valid) W.gy[(size_t)k * A.n + t] = gy;
+      if constexpr (kX) s_gy[lane][k] = gy;
+      else if (valid) W.gy[(size_t)k * A.n + t] = gy;
     }
     __syncthreads();   // every lane has read its W.gy row of this launch's input (S < 4) before it is overwritten
     if constexpr (S == 3) TSTAMP(46);
@@ -905,7 +1042,15 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
 #pragma unroll
     for (int f = 0; f < NQ; ++f) {
       const float s1 = wave_sum(gyv[f]), s2 = wave_sum(gyv[f] * xhv[f]);
-      if (lane == 0) { bp[q * NQ + f] = s1; bp[64 + q * NQ + f] = s2; }
+      if (lane == 0) {
+        if constexpr (kX) {
+          mapx_t* const gx = mapx_region(A, 5 - S) + (size_t)wgi * MAPX_STRIDE;
+          mapx_put(gx + q * NQ + f, E * 8u + (5 - S), s1);
+          mapx_put(gx + 64 + q * NQ + f, E * 8u + (5 - S), s2);
+        } else {
+          bp[q * NQ + f] = s1; bp[64 + q * NQ + f] = s2;
+        }
+      }
     }
   } else {
     // g_z = W1^T g_a1 -> g_c (through the clamp: torch passes the gradient on [0, 1])
@@ -2005,6 +2150,63 @@ __global__ __launch_bounds__(MTH) void mcaq_mapper_bwd_ride_kernel(TrMulti<Mappe
   mapper_bwd_stage<S>(tr_seg(M), L);
 }
 
+// the four forward stages of every segment in ONE launch, the batch
+// statistics exchanged as granules between them (mapx_*; the arithmetic and
+// its order are the staged launches', so the results are bit-identical).
+// Every workgroup must be resident at once: the launcher admits at most
+// MAPPER_COOP_MAX_WG workgroups (one 512-thread workgroup per CU is enough).
+__global__ __launch_bounds__(MTH) void mcaq_mapper_fwd_fused_kernel(TrMulti<MapperTrainArgs> M) {
+  __shared__ MapFwdLds L;
+  __shared__ float s_a[TR_TPB][65];
+  const MapperTrainArgs& A = tr_seg(M);
+  const unsigned E = mapx_epoch(A);
+  TSTAMP(23);
+  mapper_fwd_stage<1, true>(A, L, E, s_a);
+  __syncthreads();
+  TSTAMP(24);
+  mapper_fwd_stage<2, true>(A, L, E, s_a);
+  __syncthreads();
+  TSTAMP(25);
+  mapper_fwd_stage<3, true>(A, L, E, s_a);
+  __syncthreads();
+  TSTAMP(26);
+  mapper_fwd_stage<4, true>(A, L, E, s_a);
+  TSTAMP(27);
+  // stage 4 read exchange 3, which every workgroup of the segment published
+  // after reading E: the segment's next launch may take the next epoch
+  if ((int)blockIdx.x == A.wg0 && threadIdx.x == 0)
+    __hip_atomic_fetch_add(A.gep, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// the four backward stages in ONE launch (granule exchanges as the forward),
+// with per-segment reductions riding along as workgroups rwg0.. (the soft
+// masks' parameter gradients: mcaq_mapper_bwd_ride_kernel)
+__global__ __launch_bounds__(MTH) void mcaq_mapper_bwd_fused_kernel(TrMulti<MapperTrainArgs> M, TrMulti<TrReduceSeg> R,
+                                                                    int rwg0) {
+  __shared__ MapBwdLds L;
+  __shared__ float s_gy[TR_TPB][65];
+  if ((int)blockIdx.x >= rwg0) {
+    tr_seg_elem(R, ((int)blockIdx.x - rwg0) * MTH + (int)threadIdx.x);
+    return;
+  }
+  const MapperTrainArgs& A = tr_seg(M);
+  const unsigned E = mapx_epoch(A);
+  TSTAMP(28);
+  mapper_bwd_stage<4, true>(A, L, E, s_gy);
+  __syncthreads();
+  TSTAMP(29);
+  mapper_bwd_stage<3, true>(A, L, E, s_gy);
+  __syncthreads();
+  TSTAMP(30);
+  mapper_bwd_stage<2, true>(A, L, E, s_gy);
+  __syncthreads();
+  TSTAMP(31);
+  mapper_bwd_stage<1, true>(A, L, E, s_gy);
+  TSTAMP(49);
+  if ((int)blockIdx.x == A.wg0 && threadIdx.x == 0)
+    __hip_atomic_fetch_add(A.gep, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // the bilateral backward launch with a chain reduction riding along as
 // workgroups rwg0.. (BL_TH elements each): the bit mapper's parameter
 // gradients, whose partials the mapper's last backward stage left, summed
@@ -2386,6 +2588,95 @@ int mcaq_mapper_train_backward_multi_ride(const mcaq_mapper_params* P, const mca
 int mcaq_mapper_train_backward_multi(const mcaq_mapper_params* P, const mcaq_mapper_seg* segs, int nseg,
                                      float min_bits, float max_bits, float temperature, hipStream_t stream) {
   return mcaq_mapper_train_backward_multi_ride(P, segs, nseg, min_bits, max_bits, temperature, nullptr, 0, stream);
+}
+
+size_t mcaq_mapper_sync_bytes(int total_wg) {
+  using namespace mcaq;
+  return total_wg < 1 ? 0 : (size_t)MAPX_HDR * 4 + (size_t)3 * MAPX_STRIDE * 8 * total_wg;
+}
+
+int mcaq_mapper_fused_max_wg(void) { return mcaq::MAPPER_COOP_MAX_WG; }
+
+}  // extern "C"
+
+namespace mcaq {
+// segments of a fused launch over the sync buffer (mcaq_mapper_sync_bytes of
+// the total workgroup count): header words, then per segment 3 exchange
+// regions of nwg x MAPX_STRIDE granules, segments in order
+static int mapx_layout(TrMulti<MapperTrainArgs>& M, int wg, void* sync, size_t sync_bytes) {
+  if (!sync || wg > MAPPER_COOP_MAX_WG || sync_bytes < mcaq_mapper_sync_bytes(wg) ||
+      ((uintptr_t)sync & 7) != 0)
+    return (int)hipErrorInvalidValue;
+  unsigned* hdr = static_cast<unsigned*>(sync);
+  mapx_t* gran = reinterpret_cast<mapx_t*>(hdr + MAPX_HDR);
+  for (int k = 0; k < M.nseg; ++k) {
+    MapperTrainArgs& A = M.s[k];
+    A.gx = gran + (size_t)3 * MAPX_STRIDE * A.wg0;
+    A.gep = hdr + k;
+    A.gst = hdr + MAPX_STATUS;
+  }
+  return 0;
+}
+}  // namespace mcaq
+
+extern "C" {
+
+int mcaq_mapper_train_forward_fused(const mcaq_mapper_params* P, const mcaq_mapper_seg* segs, int nseg,
+                                    float min_bits, float max_bits, float temperature, float momentum,
+                                    int round_bits, int update_stats, void* sync, size_t sync_bytes,
+                                    hipStream_t stream) {
+  using namespace mcaq;
+  if (!P || !segs || nseg < 1 || nseg > TR_MAXSEG || (nseg > 1 && update_stats == 1)) return (int)hipErrorInvalidValue;
+  TrMulti<MapperTrainArgs> M{};
+  int wg = 0;
+  for (int k = 0; k < nseg; ++k) {
+    const mcaq_mapper_seg& g = segs[k];
+    if (!g.c || !g.bits || !g.work || g.n < 1) return (int)hipErrorInvalidValue;
+    MapperTrainArgs& A = M.s[k];
+    A.P = *P; A.c = g.c; A.bits = g.bits; A.work = g.work; A.n = g.n; A.nwg = (g.n + TR_TPB - 1) / TR_TPB;
+    A.min_bits = min_bits; A.max_bits = max_bits; A.temperature = temperature; A.momentum = momentum;
+    A.round_bits = round_bits; A.update_stats = update_stats; A.wg0 = wg;
+    wg += A.nwg;
+  }
+  M.nseg = nseg;
+  const int le = mapx_layout(M, wg, sync, sync_bytes);
+  if (le) return le;
+  hipLaunchKernelGGL(mcaq_mapper_fwd_fused_kernel, dim3(wg), dim3(MTH), 0, stream, M);
+  return (int)hipGetLastError();
+}
+
+int mcaq_mapper_train_backward_fused(const mcaq_mapper_params* P, const mcaq_mapper_seg* segs, int nseg,
+                                     float min_bits, float max_bits, float temperature,
+                                     const mcaq_reduce_seg* rsegs, int nr, void* sync, size_t sync_bytes,
+                                     hipStream_t stream) {
+  using namespace mcaq;
+  if (!P || !segs || nseg < 1 || nseg > TR_MAXSEG || nr < 0 || nr > TR_MAXSEG || (nr > 0 && !rsegs))
+    return (int)hipErrorInvalidValue;
+  TrMulti<TrReduceSeg> R{};
+  for (int k = 0; k < nr; ++k) {
+    const mcaq_reduce_seg& g = rsegs[k];
+    if (!g.part || !g.out || g.nparts < 1 || g.stride < g.count || g.count < 1 || g.count != rsegs[0].count)
+      return (int)hipErrorInvalidValue;
+    R.s[k] = TrReduceSeg{g.part, g.out, g.nparts, g.stride, g.count, g.accumulate, g.scale};
+  }
+  R.nseg = nr;
+  TrMulti<MapperTrainArgs> M{};
+  int wg = 0;
+  for (int k = 0; k < nseg; ++k) {
+    const mcaq_mapper_seg& g = segs[k];
+    if (!g.c || !g.gbits || !g.gc || !g.gpart || !g.work || g.n < 1) return (int)hipErrorInvalidValue;
+    MapperTrainArgs& A = M.s[k];
+    A.P = *P; A.c = g.c; A.gbits = g.gbits; A.gc = g.gc; A.work = g.work; A.gpart = g.gpart; A.n = g.n;
+    A.nwg = (g.n + TR_TPB - 1) / TR_TPB;
+    A.min_bits = min_bits; A.max_bits = max_bits; A.temperature = temperature; A.wg0 = wg;
+    wg += A.nwg;
+  }
+  M.nseg = nseg;
+  const int le = mapx_layout(M, wg, sync, sync_bytes);
+  if (le) return le;
+  const int rwg = nr > 0 ? (nr * R.s[0].count + MTH - 1) / MTH : 0;
+  hipLaunchKernelGGL(mcaq_mapper_bwd_fused_kernel, dim3(wg + rwg), dim3(MTH), 0, stream, M, R, wg);
+  return (int)hipGetLastError();
 }
 
 int mcaq_head_train_backward_multi_ride(const mcaq_cmlp_params* P, const mcaq_head_seg* segs, int nseg,

@@ -20,6 +20,7 @@ _SoftMaskMulti, _QATMulti); LinearBitMapper, normalize_complexity and frozen /
 per-tensor quantizers keep their per-scale pieces in between.
 """
 import ctypes
+import os
 
 import torch
 
@@ -397,6 +398,41 @@ def _flush_pending_sm_reduce():
 # instead of 7.  False: the staged per-layer collectives.
 DP_GLOBAL_MAPPER = True
 
+# The train-mode mapper as ONE launch per direction (mcaq_mapper_train_*_fused):
+# the workgroups exchange the batch statistics between the layers inside the
+# launch (write-through granules, no grid barrier, no fence) instead of
+# ending a launch at each of the 3 + 3 statistics barriers; bit-identical to
+# the staged launches (False), which also serve more workgroups than the
+# chip holds at once.  MCAQ_MAPPER_FUSED=0 selects the staged launches (A/B).
+MAPPER_FUSED = os.environ.get("MCAQ_MAPPER_FUSED", "1") != "0"
+
+
+def _mapx_buffer(mod, dev, ns):
+    """The fused mapper launches' sync buffer for segments of ns tiles: one
+    per mapper module and segment layout (forward and backward share it),
+    zeroed when made; None when the launch would exceed the resident limit."""
+    L = abi.lib()
+    wgs = tuple((int(n) + 63) // 64 for n in ns)
+    total = sum(wgs)
+    if not MAPPER_FUSED or total > L.mcaq_mapper_fused_max_wg():
+        return None
+    cache = mod.__dict__.setdefault("_mapx", {})
+    key = (str(dev), wgs)
+    buf = cache.get(key)
+    if buf is None:
+        buf = torch.zeros((L.mcaq_mapper_sync_bytes(total) + 7) // 8, dtype=torch.int64, device=dev)
+        cache[key] = buf
+    return buf
+
+
+def mapper_sync_status(mod):
+    """Nonzero when an in-launch exchange of a fused mapper launch of `mod`
+    timed out (its results are then invalid); 0 otherwise.  Synchronises."""
+    st = 0
+    for buf in getattr(mod, "_mapx", {}).values():
+        st |= int(buf.view(torch.int32)[abi.MAPPER_SYNC_STATUS_WORD].item())
+    return st
+
 
 def _consecutive(ts):
     """The flat concatenation of ts when they already lie back to back in one
@@ -465,9 +501,10 @@ def _dp_mapper_inputs(mapper, ncs, box, with_minmax):
 
 
 class _MapperMulti(torch.autograd.Function):
-    """Train-mode bit mapper of every scale: 4 forward launches (one per
+    """Train-mode bit mapper of every scale: one forward launch (MAPPER_FUSED:
+    the batch statistics exchanged inside it; else 4 launches, one per
     batch-statistics barrier) + the running-statistics update in scale order;
-    4 backward launches + one parameter reduction."""
+    one backward launch (else 4) + one parameter reduction."""
 
     @staticmethod
     def forward(ctx, mod, temperature, return_continuous, n, *args):
@@ -499,7 +536,14 @@ class _MapperMulti(torch.autograd.Function):
         mom = float(bns[0].momentum)
         pg = core._mapper_group(net) if dp is None else None
         ctx.pg, ctx.gath1, ctx.world, ctx.dp = pg, None, 1, dp
-        if pg is None:
+        sync = _mapx_buffer(mod, dev, [c.numel() for c in cfs]) if pg is None else None
+        ctx.sync = sync
+        if sync is not None:
+            abi.check(L.mcaq_mapper_train_forward_fused(ctypes.byref(q), segs, n, mod.min_bits, mod.max_bits, T, mom,
+                                                        0 if return_continuous else 1, 2, _p(sync),
+                                                        sync.numel() * 8, _stream()),
+                      "mcaq_mapper_train_forward_fused")
+        elif pg is None:
             abi.check(L.mcaq_mapper_train_forward_multi(ctypes.byref(q), segs, n, mod.min_bits, mod.max_bits, T,
                                                         mom, 0 if return_continuous else 1, 2, _stream()),
                       "mcaq_mapper_train_forward_multi")
@@ -576,7 +620,15 @@ class _MapperMulti(torch.autograd.Function):
             s = segs[i]
             s.c, s.work, s.gbits, s.gc, s.gpart, s.n = _p(cfs[i]), _p(works[i]), _p(g), _p(gc), _p(gp), m
         ride = _PENDING_SM_REDUCE["segs"] if ctx.pg is None else None
-        if ride is not None:
+        if ctx.pg is None and ctx.sync is not None:
+            # one launch, the soft masks' reductions (if pending) riding along
+            _PENDING_SM_REDUCE["segs"] = None
+            abi.check(L.mcaq_mapper_train_backward_fused(ctypes.byref(ctx.q), segs, n, mod.min_bits, mod.max_bits,
+                                                         ctx.T, ride[0] if ride is not None else None,
+                                                         ride[1] if ride is not None else 0, _p(ctx.sync),
+                                                         ctx.sync.numel() * 8, _stream()),
+                      "mcaq_mapper_train_backward_fused")
+        elif ride is not None:
             # the soft masks' gradient reductions as extra workgroups of the first stage launch
             _PENDING_SM_REDUCE["segs"] = None
             abi.check(L.mcaq_mapper_train_backward_multi_ride(ctypes.byref(ctx.q), segs, n, mod.min_bits, mod.max_bits,

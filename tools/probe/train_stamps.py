@@ -66,6 +66,15 @@ def main():
     print("mapper forward stage 2, workgroup 0: %d ticks" % (st[55] - st[50]))
     for a, b, name in MAPPER_FWD:
         print("   %-34s %8d" % (name, st[b] - st[a]))
+    # the fused mapper launches (train_step.MAPPER_FUSED), workgroup 0
+    print("mapper forward, one launch: %d ticks" % (st[27] - st[23]))
+    for a, b, name in ((23, 24, "stage 1"), (24, 25, "stage 2 (sweep of exchange 1 + layer)"),
+                       (25, 26, "stage 3 (sweep of exchange 2 + layer)"), (26, 27, "stage 4 (sweep of exchange 3 + bits)")):
+        print("   %-40s %8d" % (name, st[b] - st[a]))
+    print("mapper backward, one launch: %d ticks" % (st[49] - st[28]))
+    for a, b, name in ((28, 29, "stage 4"), (29, 30, "stage 3 (sweep of exchange 1)"),
+                       (30, 31, "stage 2 (sweep of exchange 2)"), (31, 49, "stage 1 (sweep of exchange 3)")):
+        print("   %-40s %8d" % (name, st[b] - st[a]))
 
 
 if __name__ == "__main__":
