@@ -239,7 +239,9 @@ def main_qat(args, world, rank, dev, pg):
     if use_graph:
         graph = torch.cuda.CUDAGraph()
         opt.zero_grad(set_to_none=True)
-        with torch.cuda.graph(graph):
+        # thread_local: the process group's watchdog thread polls its work
+        # events while this thread captures (global mode would fail its calls)
+        with torch.cuda.graph(graph, capture_error_mode="thread_local"):
             step()
         run = graph.replay
         for _ in range(2):
@@ -500,7 +502,7 @@ def run_e2e(cfg, steps, warmup, world, rank, dev, pg, amp=False, eager=False, fu
                 graphs = []
                 for k in range(nin):
                     graph = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(graph, stream=streams[k]):
+                    with torch.cuda.graph(graph, stream=streams[k], capture_error_mode="thread_local"):
                         r = step_on(k, hooks)
                     graphs.append(graph)
                     if k == 0:
@@ -733,7 +735,7 @@ class Runner(_RunMixin):
                 gs = []
                 for seg in segs:
                     g = torch.cuda.CUDAGraph()
-                    with torch.cuda.graph(g, stream=st):
+                    with torch.cuda.graph(g, stream=st, capture_error_mode="thread_local"):
                         seg()
                     gs.append(g)
                 self.graphs[p] = gs

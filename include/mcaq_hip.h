@@ -584,6 +584,17 @@ typedef struct {
 size_t mcaq_clip_adamw_work_floats(int total);
 int mcaq_clip_adamw(const mcaq_adamw_seg* segs, int nseg, const mcaq_adamw_group* groups, int ngroups,
                     float* steps, float max_norm, float* total_norm, float* work, hipStream_t stream);
+/* The same step as ONE launch (round 6; clipping only, max_norm > 0): the
+ * chunks' squared-norm partials exchanged inside the launch through `sync`
+ * (mcaq_clip_adamw_sync_bytes(total elements, nseg) bytes, zeroed before its
+ * first use and whenever the segments change; word 1 (uint32) is nonzero
+ * after a timed-out exchange).  Bit-identical to mcaq_clip_adamw.
+ * hipErrorInvalidValue when max_norm <= 0, the buffer is missing or short, or
+ * the step has more than 256 chunks of 1,024 elements (use mcaq_clip_adamw). */
+size_t mcaq_clip_adamw_sync_bytes(int total, int nseg);
+int mcaq_clip_adamw_fused(const mcaq_adamw_seg* segs, int nseg, const mcaq_adamw_group* groups, int ngroups,
+                          float* steps, float max_norm, float* total_norm, void* sync, size_t sync_bytes,
+                          hipStream_t stream);
 
 /* ---- data-parallel QAT step: unpack one all-gather ------------------------
  * g: every rank's send buffer back to back, [world][stride] floats

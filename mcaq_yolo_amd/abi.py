@@ -77,6 +77,7 @@ class SmaskParams(ctypes.Structure):
 
 MCAQ_TRAIN_MAXSEG = 3
 MAPPER_SYNC_STATUS_WORD = 32    # uint32 index of the fused mapper sync buffer's status word
+ADAMW_SYNC_STATUS_WORD = 1      # ... and of the one-launch ClipAdamW's
 
 
 class MapperSeg(ctypes.Structure):
@@ -161,6 +162,7 @@ EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats",
            "mcaq_mapper_train_forward_multi", "mcaq_mapper_train_backward_multi", "mcaq_head_train_backward_multi",
            "mcaq_smask_train_backward_multi", "mcaq_train_reduce_multi", "mcaq_ema_stats_multi",
            "mcaq_mapper_train_forward_stage_multi", "mcaq_mapper_train_backward_stage_multi", "mcaq_clip_adamw", "mcaq_clip_adamw_work_floats",
+           "mcaq_clip_adamw_sync_bytes", "mcaq_clip_adamw_fused",
            "mcaq_bit_budget_forward", "mcaq_qat_smask_backward_multi", "mcaq_qat_forward_budget",
            "mcaq_ema_stats_multi_running", "mcaq_head_train_backward_multi_ride",
            "mcaq_stats_pack", "mcaq_morph_ema", "mcaq_mapper_train_backward_multi_ride", "mcaq_dp_unpack",
@@ -294,6 +296,10 @@ def _declare(lib):
     lib.mcaq_clip_adamw.argtypes = [ctypes.POINTER(AdamwSeg), I, P, I, P, Fl, P, P, P]
     lib.mcaq_clip_adamw_work_floats.restype = ctypes.c_size_t
     lib.mcaq_clip_adamw_work_floats.argtypes = [I]
+    lib.mcaq_clip_adamw_sync_bytes.restype = ctypes.c_size_t
+    lib.mcaq_clip_adamw_sync_bytes.argtypes = [I, I]
+    lib.mcaq_clip_adamw_fused.restype = I
+    lib.mcaq_clip_adamw_fused.argtypes = [ctypes.POINTER(AdamwSeg), I, P, I, P, Fl, P, P, ctypes.c_size_t, P]
     lib.mcaq_dp_unpack.restype = I
     lib.mcaq_dp_unpack.argtypes = [P, I, I, ctypes.POINTER(DpSeg), I, P]
     lib.mcaq_smask_train_backward.restype = I

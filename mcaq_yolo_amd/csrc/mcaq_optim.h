@@ -250,9 +250,192 @@ __global__ __launch_bounds__(OPT_TH) void mcaq_adamw_update_kernel(AdamwArgs a, 
   }
 }
 
+// ---- ONE launch (round 6): the same two phases, the chunks' squared-norm
+// partials exchanged inside the launch as write-through granules (the data is
+// the flag: mcaq_train.h mapx_*, cdna_hip_programming.md s.6 Guideline 16
+// R2) instead of through a launch boundary; each thread keeps its elements'
+// gradient, parameter and moments in registers from the first phase to the
+// update.  The arithmetic and its order are the two launches', so the
+// results are bit-identical.  Sync buffer: word 0 the epoch, word 1 the
+// status (nonzero after a timed-out exchange), granules from byte 256
+// (chunk-major, nseg per chunk).  Every workgroup must be resident at once:
+// at most OPT_FUSED_MAX_CHUNKS chunks.
+constexpr int OPT_FUSED_MAX_CHUNKS = 256;
+constexpr int OPT_SYNC_HDR = 64;   // header words
+
+__global__ __launch_bounds__(OPT_TH) void mcaq_adamw_fused_kernel(AdamwArgs a, unsigned* sync, int nchunk) {
+  __shared__ mcaq_adamw_seg sg[MCAQ_OPT_MAXSEG];
+  __shared__ int st[MCAQ_OPT_MAXSEG + 1];
+  __shared__ float sq[OPT_CH];
+  __shared__ float seg_acc[MCAQ_OPT_MAXSEG];
+  __shared__ float s_step[MCAQ_OPT_MAXSEG];
+  __shared__ float coef_s;
+  __shared__ float s_bc2s[MCAQ_OPT_MAXSEG], s_ss[MCAQ_OPT_MAXSEG];
+  __shared__ double g_hp[MCAQ_OPT_MAXGROUPS][7];
+  const int tid = (int)threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int nseg = a.nseg;
+  mapx_t* const gran = reinterpret_cast<mapx_t*>(sync + OPT_SYNC_HDR);
+  const unsigned tag = __builtin_amdgcn_readfirstlane(
+                           __hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
+  if (tid < a.ngroups) {
+    const mcaq_adamw_group G = a.g[tid];
+    g_hp[tid][0] = G.lr * G.weight_decay;
+    g_hp[tid][1] = G.beta1; g_hp[tid][2] = 1.0 - G.beta1;
+    g_hp[tid][3] = G.beta2; g_hp[tid][4] = 1.0 - G.beta2;
+    g_hp[tid][5] = G.eps; g_hp[tid][6] = G.lr;
+  }
+  opt_table(a, sg, st);
+  const int total = st[nseg];
+  const int base = (int)blockIdx.x * OPT_CH, e0 = base + tid * OPT_E;
+  // this thread's elements, loaded once for both phases
+  int k = opt_seg_of(st, nseg, imin_(e0, total - 1));
+  int ks[OPT_E];
+  float gv[OPT_E], pv[OPT_E], mv[OPT_E], vv[OPT_E];
+#pragma unroll
+  for (int q = 0; q < OPT_E; ++q) {
+    const int j = imin_(e0 + q, total - 1);
+    while (k + 1 < nseg && j >= st[k + 1]) ++k;
+    ks[q] = k;
+    const mcaq_adamw_seg& S = sg[k];
+    const int e = j - st[k];
+    gv[q] = S.grad[e]; pv[q] = S.param[e]; mv[q] = S.exp_avg[e]; vv[q] = S.exp_avg_sq[e];
+  }
+  if (tid >= 64 && tid < 64 + nseg) {
+    // this step's count and bias corrections (read before this workgroup
+    // publishes: workgroup 0 writes the counts back after its sweep)
+    const int kk = tid - 64;
+    const float step = a.steps[sg[kk].step_idx] + 1.0f;
+    const double* hp = g_hp[sg[kk].group];
+    const float bc1 = (float)(1.0 - pow_int(hp[1], step));
+    s_bc2s[kk] = sqrtf((float)(1.0 - pow_int(hp[3], step)));
+    s_ss[kk] = (float)(hp[6] / (double)bc1);
+    s_step[kk] = step;
+  }
+#pragma unroll
+  for (int q = 0; q < OPT_E; ++q) sq[tid * OPT_E + q] = e0 + q < total ? gv[q] * gv[q] : 0.0f;
+  __syncthreads();
+  // phase 1: this chunk's squared sum of every segment, published
+  for (int kk = wv; kk < nseg; kk += OPT_TH / 64) {
+    const int lo = imax_(st[kk], base), hi = imin_(st[kk + 1], base + OPT_CH);
+    float acc = 0.0f;
+    if (lo < hi) {
+      float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+      int i = lo + lane;
+      for (; i + 192 < hi; i += 256) {
+        a0 += sq[i - base]; a1 += sq[i + 64 - base]; a2 += sq[i + 128 - base]; a3 += sq[i + 192 - base];
+      }
+      for (; i < hi; i += 64) a0 += sq[i - base];
+      acc = (a0 + a1) + (a2 + a3);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    }
+    if (lane == 0) mapx_put(gran + (size_t)blockIdx.x * nseg + kk, tag, acc);
+  }
+  // phase 2: per-tensor squared norms, every chunk's partial in chunk order
+  if (tid < nseg) {
+    float s = 0.0f;
+    for (int w0 = 0; w0 < nchunk; w0 += 8) {
+      mapx_t* gp[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) gp[r] = gran + (size_t)imin_(w0 + r, nchunk - 1) * nseg + tid;
+      float v[8];
+      mapx_get<8>(gp, tag, v, sync + 1);
+#pragma unroll
+      for (int r = 0; r < 8; ++r) s = w0 + r < nchunk ? s + v[r] : s;
+    }
+    seg_acc[tid] = s;
+  }
+  __syncthreads();
+  if (blockIdx.x == 0) {
+    // every workgroup has published, so every workgroup has read the counts
+    // and the epoch: the counts advance, the next launch takes the next epoch
+    if (tid < nseg) a.steps[sg[tid].step_idx] = s_step[tid];
+    if (tid == 0) __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (tid < 64) {
+    float t2 = 0.0f;
+    for (int kk = tid; kk < nseg; kk += 64) {
+      const float nk = sqrtf(seg_acc[kk]);
+      t2 = fmaf(nk, nk, t2);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t2 += __shfl_xor(t2, o, 64);
+    const float tot = sqrtf(t2);
+    if (tid == 0) {
+      if (a.total_norm && blockIdx.x == 0) a.total_norm[0] = tot;
+      const float c = a.max_norm / (tot + 1e-6f);
+      coef_s = c < 1.0f ? c : 1.0f;
+      if (!(c == c)) coef_s = c;
+    }
+  }
+  __syncthreads();
+  const float coef = coef_s;
+  if (e0 < total) {
+#pragma unroll
+    for (int q = 0; q < OPT_E; ++q) {
+      const int j = e0 + q;
+      if (j >= total) break;
+      const mcaq_adamw_seg& S = sg[ks[q]];
+      const int e = j - st[ks[q]];
+      const double* hp = g_hp[S.group];
+      float g = gv[q] * coef;
+      S.grad[e] = g;
+      float p = pv[q];
+      p = (float)((double)p - hp[0] * (double)p);
+      const float m = (float)(hp[1] * (double)mv[q] + hp[2] * (double)g);
+      const float v = (float)(hp[3] * (double)vv[q] + hp[4] * (double)g * (double)g);
+      const float denom = (float)((double)(sqrtf(v) / s_bc2s[ks[q]]) + hp[5]);
+      p = p - s_ss[ks[q]] * m / denom;
+      if (S.project_abs) p = fabsf(p);
+      S.exp_avg[e] = m;
+      S.exp_avg_sq[e] = v;
+      S.param[e] = p;
+    }
+  }
+}
+
 }  // namespace mcaq
 
 extern "C" {
+
+size_t mcaq_clip_adamw_sync_bytes(int total, int nseg) {
+  using namespace mcaq;
+  if (total < 1 || nseg < 1) return 0;
+  return (size_t)OPT_SYNC_HDR * 4 + (size_t)((total + OPT_CH - 1) / OPT_CH) * nseg * 8;
+}
+
+int mcaq_clip_adamw_fused(const mcaq_adamw_seg* segs, int nseg, const mcaq_adamw_group* groups, int ngroups,
+                          float* steps, float max_norm, float* total_norm, void* sync, size_t sync_bytes,
+                          hipStream_t stream) {
+  using namespace mcaq;
+  if (!segs || !groups || !steps || !sync || nseg < 1 || nseg > MCAQ_OPT_MAXSEG || ngroups < 1 ||
+      ngroups > MCAQ_OPT_MAXGROUPS || !(max_norm > 0.0f) || ((uintptr_t)sync & 7) != 0)
+    return (int)hipErrorInvalidValue;
+  AdamwArgs a{};
+  long long total = 0;
+  for (int k = 0; k < nseg; ++k) {
+    const mcaq_adamw_seg& g = segs[k];
+    if (!g.param || !g.grad || !g.exp_avg || !g.exp_avg_sq || g.n < 1 || g.group < 0 || g.group >= ngroups ||
+        g.step_idx < 0)
+      return (int)hipErrorInvalidValue;
+    for (int j = 0; j < k; ++j)
+      if (segs[j].step_idx == g.step_idx) return (int)hipErrorInvalidValue;
+    a.s[k] = g;
+    total += g.n;
+  }
+  const long long nchunk = (total + OPT_CH - 1) / OPT_CH;
+  if (nchunk > OPT_FUSED_MAX_CHUNKS || sync_bytes < mcaq_clip_adamw_sync_bytes((int)total, nseg))
+    return (int)hipErrorInvalidValue;
+  a.g = groups;
+  a.ngroups = ngroups;
+  a.nseg = nseg;
+  a.steps = steps;
+  a.max_norm = max_norm;
+  a.total_norm = total_norm;
+  hipLaunchKernelGGL(mcaq_adamw_fused_kernel, dim3((int)nchunk), dim3(OPT_TH), 0, stream, a,
+                     static_cast<unsigned*>(sync), (int)nchunk);
+  return (int)hipGetLastError();
+}
 
 size_t mcaq_clip_adamw_work_floats(int total) {
   return (size_t)mcaq::OPT_WORK0 + (size_t)((total + mcaq::OPT_CH - 1) / mcaq::OPT_CH) * MCAQ_OPT_MAXSEG;

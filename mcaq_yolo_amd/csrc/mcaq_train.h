@@ -495,10 +495,17 @@ __device__ __forceinline__ void mapper_fwd_stage(const MapperTrainArgs& A, MapFw
   constexpr int WN = kWL ? MapL<S>::K * MapL<S>::N : MTH;
   static_assert(WN % MTH == 0 && WN <= 64 * 32, "mapper weight staging");
   float wst[WN / MTH];
+  // ... and this lane's biases of the MFMA layer (the accumulators' initial
+  // values: loaded where they are used, each MFMA chain waited on them)
+  constexpr int FPWB = kWL ? (MapL<S>::N / 16) / 2 : 1;
+  float bpre[FPWB];
   if constexpr (kWL) {
     const float* wsrc = S == 2 ? P.w2 : P.w3;
 #pragma unroll
     for (int i = 0; i < WN / MTH; ++i) wst[i] = wsrc[tid + i * MTH];
+    const float* bsrc = S == 2 ? P.b2 : P.b3;
+#pragma unroll
+    for (int i = 0; i < FPWB; ++i) bpre[i] = bsrc[((q >> 2) + 2 * i) * 16 + (lane & 15)];
   }
   // this lane's previous-layer activations first: in flight through the
   // batch statistics below
@@ -554,13 +561,13 @@ __device__ __forceinline__ void mapper_fwd_stage(const MapperTrainArgs& A, MapFw
     // 4 lanes (xor 16, xor 32), the 4 tile blocks in order - mean, then M2
     constexpr int K = MapL<S>::K, N = MapL<S>::N, FPW = (N / 16) / 2;
     const int lr = lane & 15, lk = lane >> 4, mtb = q & 3;
-    const float* bb = S == 2 ? P.b2 : P.b3;
     float* aout = S == 2 ? W.a2 : W.a3;
     float* red1 = s_tmp;                 // [4 tile blocks][64] sums
     float* red2 = s_tmp + 256;           //   ... squared deviations
+    static_assert(FPW == FPWB, "bias prefetch");
     float bq[FPW];
 #pragma unroll
-    for (int i = 0; i < FPW; ++i) bq[i] = bb[((q >> 2) + 2 * i) * 16 + lr];
+    for (int i = 0; i < FPW; ++i) bq[i] = bpre[i];
     tr_f4 d[FPW];
 #pragma unroll
     for (int i = 0; i < FPW; ++i) {
@@ -776,14 +783,20 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
   constexpr int KI = S == 4 ? 32 : (S == 1 ? 3 : MapL<S>::K);
   float gyp[S <= 3 ? N1 / MW : 1], asp[S <= 3 ? N1 / MW : 1];
   float ap2[S >= 2 ? KI / MW : 1], ap4[S >= 2 ? KI / MW : 1];   // ap4: SQ x SR values (below)
+  // ... and BN(S)'s forward statistics and gamma for the BN backward (read
+  // after the BN sums, each was one more memory round trip)
+  float pmean = 0.0f, prstd = 0.0f, pgam[S <= 3 ? N1 / MW : 1];
   if constexpr (S <= 3) {
     const float* aS = S == 1 ? W.a1 : (S == 2 ? W.a2 : W.a3);
+    const float* gS = S == 1 ? P.g1 : (S == 2 ? P.g2 : P.g3);
 #pragma unroll
     for (int i = 0; i < N1 / MW; ++i) {
       const int j = q + i * MW;
       gyp[i] = kX ? s_gy[tc - wgi * TR_TPB][j] : W.gy[(size_t)j * A.n + tc];
       asp[i] = aS[(size_t)j * A.n + tc];
+      pgam[i] = gS[j];
     }
+    if (tid < N1) { pmean = W.stat[(S - 1) * 128 + tid]; prstd = W.stat[(S - 1) * 128 + 64 + tid]; }
   }
   // ... and the BN(S-1) statistics and affine parameters of the step-4
   // columns with that step's a(S-1) values (read after the W^T g_a loop, which
@@ -827,7 +840,6 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
     // BN(S) backward: g_a = gamma rstd (g_y - S1/n - xhat S2/n); the BN sums
     // over the workgroups' partials, MW interleaved subsets in parallel
     constexpr int N = MapL<S>::N;
-    const float* g = S == 1 ? P.g1 : (S == 2 ? P.g2 : P.g3);
     {
       const int j = tid & 63, part = tid >> 6;
       if (j < N) {
@@ -876,7 +888,7 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
       // gradient all-reduce)
       s_sg[tid] = A.gworld > 0 ? A.gbsum[tid] : s1;
       s_sgx[tid] = A.gworld > 0 ? A.gbsum[64 + tid] : s2;
-      s_mean[tid] = W.stat[(S - 1) * 128 + tid]; s_rstd[tid] = W.stat[(S - 1) * 128 + 64 + tid];
+      s_mean[tid] = pmean; s_rstd[tid] = prstd;
       // gamma / beta gradients are the BN sums themselves: workgroup 0's
       // partial slot holds them, the others zero
       const int og = S == 1 ? MG_G1 : (S == 2 ? MG_G2 : MG_G3), ob = S == 1 ? MG_BE1 : (S == 2 ? MG_BE2 : MG_BE3);
@@ -895,7 +907,7 @@ __device__ __forceinline__ void mapper_bwd_stage(const MapperTrainArgs& A, MapBw
       const int j = q + i * MW;
       const float gy = gyp[i];
       const float xh = (asp[i] - s_mean[j]) * s_rstd[j];
-      s_g[lane][j] = valid ? g[j] * s_rstd[j] * (gy - s_sg[j] * inv_n - xh * (s_sgx[j] * inv_n)) : 0.0f;
+      s_g[lane][j] = valid ? pgam[i] * s_rstd[j] * (gy - s_sg[j] * inv_n - xh * (s_sgx[j] * inv_n)) : 0.0f;
     }
   }
   if constexpr (S == 3) TSTAMP(43);

@@ -19,13 +19,21 @@ between graph replays).  CPU parameters run the same three steps as
 torch ops.  Values agree with torch's clip + fused AdamW within fp32
 rounding (the norms reduce in another order): tests/test_optim_gpu.py.
 The two launches: per-chunk squared-norm partials, then the norm and the
-update of every chunk (csrc/mcaq_optim.h).
+update of every chunk (csrc/mcaq_optim.h).  With clipping and up to 256
+chunks of 1,024 elements (ONE_LAUNCH) both run in ONE launch, the partials
+exchanged inside it (`mcaq_clip_adamw_fused`, bit-identical).
 """
 import ctypes
+import os
 
 import torch
 
 from . import abi
+
+
+# one launch for the clipped step when its chunks fit the chip at once
+# (MCAQ_ADAMW_ONE_LAUNCH=0: the two launches, A/B)
+ONE_LAUNCH = os.environ.get("MCAQ_ADAMW_ONE_LAUNCH", "1") != "0"
 
 
 class ClipAdamW(torch.optim.Optimizer):
@@ -44,6 +52,7 @@ class ClipAdamW(torch.optim.Optimizer):
         self._hp_host = None
         self._segs = None
         self._seg_key = None
+        self._sync = None
         self._retired = []
 
     def _params(self):
@@ -102,7 +111,7 @@ class ClipAdamW(torch.optim.Optimizer):
         """Forget the launch descriptors; their device buffers stay alive (a
         graph captured earlier may still write into them)."""
         if self._segs is not None:
-            self._retired.append((self._work, self._norm_t))
+            self._retired.append((self._work, self._norm_t, self._sync))
         self._segs = None
         self._seg_key = None
 
@@ -169,12 +178,25 @@ class ClipAdamW(torch.optim.Optimizer):
             self._norm_t = torch.empty(1, device=items[0][1].device)
             total = sum(p.numel() for _, p in items)
             self._work = torch.empty(abi.lib().mcaq_clip_adamw_work_floats(total), device=items[0][1].device)
+            # the one-launch form's exchange buffer: zeroed once per descriptor set
+            self._sync = None
+            if self.max_norm is not None and self.max_norm > 0 and -(-total // 1024) <= 256:
+                nb = abi.lib().mcaq_clip_adamw_sync_bytes(total, len(items))
+                self._sync = torch.zeros((nb + 7) // 8, dtype=torch.int64, device=items[0][1].device)
         mn = self.max_norm if self.max_norm is not None else 0.0
         st = ctypes.c_void_p(torch.cuda.current_stream(items[0][1].device).cuda_stream)
-        abi.check(abi.lib().mcaq_clip_adamw(self._segs, len(items), ctypes.c_void_p(self._hp_t.data_ptr()),
-                                            len(self.param_groups), ctypes.c_void_p(self._steps_t.data_ptr()), mn,
-                                            ctypes.c_void_p(self._norm_t.data_ptr()),
-                                            ctypes.c_void_p(self._work.data_ptr()), st), "mcaq_clip_adamw")
+        L = abi.lib()
+        if ONE_LAUNCH and self._sync is not None and mn > 0:
+            abi.check(L.mcaq_clip_adamw_fused(self._segs, len(items), ctypes.c_void_p(self._hp_t.data_ptr()),
+                                              len(self.param_groups), ctypes.c_void_p(self._steps_t.data_ptr()), mn,
+                                              ctypes.c_void_p(self._norm_t.data_ptr()),
+                                              ctypes.c_void_p(self._sync.data_ptr()), self._sync.numel() * 8, st),
+                      "mcaq_clip_adamw_fused")
+        else:
+            abi.check(L.mcaq_clip_adamw(self._segs, len(items), ctypes.c_void_p(self._hp_t.data_ptr()),
+                                        len(self.param_groups), ctypes.c_void_p(self._steps_t.data_ptr()), mn,
+                                        ctypes.c_void_p(self._norm_t.data_ptr()),
+                                        ctypes.c_void_p(self._work.data_ptr()), st), "mcaq_clip_adamw")
         self.last_total_norm = self._norm_t[0] if self.max_norm is not None else None
         # the kernel updated the tensors through raw pointers: bump their
         # version counters as an in-place torch op would, so caches keyed on

@@ -243,3 +243,56 @@ def test_clip_adamw_per_parameter_steps_and_lr_table():
     torch.cuda.synchronize()
     for k, (p, q) in enumerate(zip(ps, qs)):
         _close(q, p, 1e-5, "param %d after lr change" % k)
+
+
+@pytest.mark.parametrize("sizes", [(97, 2048, 5), (4609, 2881, 33, 1, 1024, 3000)])
+def test_clip_adamw_one_launch_equals_two_launches(sizes):
+    """The clipped step as ONE launch (optim.ONE_LAUNCH: the chunks' norm
+    partials exchanged inside the launch) against the two launches, bit for
+    bit: parameters, clipped gradients, moments, step counts and total norm
+    over eager steps (one parameter without a gradient in step 2: its count
+    stays) and graph replays; the exchange status word stays clear."""
+    from mcaq_yolo_amd import abi, optim
+    from mcaq_yolo_amd.optim import ClipAdamW
+    torch.manual_seed(7)
+    init = [torch.randn(n, device="cuda") for n in sizes]
+    grads = [[torch.randn(n, device="cuda") * (0.1 + it) for n in sizes] for it in range(6)]
+    res = {}
+    for one in (True, False):
+        old = optim.ONE_LAUNCH
+        optim.ONE_LAUNCH = one
+        try:
+            ps = [t.clone().requires_grad_(True) for t in init]
+            o = ClipAdamW(ps, lr=1e-2, weight_decay=0.05, max_norm=0.5, project_abs=[ps[1]])
+            norms = []
+            for it in range(3):
+                for p, g in zip(ps, grads[it]):
+                    p.grad = g.clone()
+                if it == 1:
+                    ps[0].grad = None
+                o.step()
+                norms.append(o.last_total_norm.clone())
+            for p, g in zip(ps, grads[3]):
+                p.grad = g.clone()
+            o.step()                                   # new descriptors (grads reallocated), then capture
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                o.step()
+            for it in (4, 5):
+                for p, g in zip(ps, grads[it]):
+                    p.grad.copy_(g)
+                graph.replay()
+                norms.append(o.last_total_norm.clone())
+            torch.cuda.synchronize()
+            if one:
+                assert o._sync is not None
+                assert int(o._sync.view(torch.int32)[abi.ADAMW_SYNC_STATUS_WORD].item()) == 0
+            res[one] = ([p.detach().clone() for p in ps] + [p.grad.clone() for p in ps] +
+                        [o.state[p][k].clone() for p in ps for k in ("exp_avg", "exp_avg_sq")] + norms,
+                        [float(o.state[p]["step"]) for p in ps])
+        finally:
+            optim.ONE_LAUNCH = old
+    (a, sa), (b, sb) = res[True], res[False]
+    assert sa == sb and sa[0] == 5.0 and sa[1] == 6.0
+    for i, (x, y) in enumerate(zip(a, b)):
+        assert torch.equal(x, y), i

@@ -64,7 +64,7 @@ def test_sharded_step_rccl_allreduce_in_graph(dev, blobs, nccl1, nbat):
         sh.launch(st, nccl1)            # warm-up: communicator setup outside capture
     st.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g, stream=st):
+    with torch.cuda.graph(g, stream=st, capture_error_mode="thread_local"):
         sh.launch(torch.cuda.current_stream(), nccl1)
     for _ in range(2):
         g.replay()
@@ -154,7 +154,7 @@ def test_sharded_qat_step_nccl_graph_equals_unsharded(dev, nccl1):
     torch.cuda.current_stream().wait_stream(side)
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):   # the watchdog thread polls meanwhile
         step1()
     for _ in range(2):
         g.replay()
