@@ -502,6 +502,19 @@ int mcaq_train_reduce_multi(const mcaq_reduce_seg* segs, int nseg, int chain, hi
  * launch of their own (nr = 0: none). */
 int mcaq_head_train_backward_multi_ride(const mcaq_cmlp_params* P, const mcaq_head_seg* segs, int nseg,
                                         const mcaq_reduce_seg* rsegs, int nr, hipStream_t stream);
+/* mcaq_head_train_backward_multi_ride with the complexity MLP's parameter
+ * reduction inside its launch (round 6): out (+)= the chain sum of every
+ * segment's partials, last segment first (as mcaq_train_reduce_multi with
+ * chain 1 over the segments' gpart, accumulate / scale as there), through
+ * `sync` (mcaq_head_sync_bytes(total MLP workgroups = sum of ceil(B ht wt /
+ * 64)), zeroed before first use and whenever the layout changes, one launch
+ * at a time; word 1 nonzero after a timed-out exchange).  Bit-identical to
+ * the separate reduction; gpart is not written.  hipErrorInvalidValue above
+ * mcaq_mapper_fused_max_wg() workgroups. */
+size_t mcaq_head_sync_bytes(int total_wg);
+int mcaq_head_train_backward_fused(const mcaq_cmlp_params* P, const mcaq_head_seg* segs, int nseg,
+                                   const mcaq_reduce_seg* rsegs, int nr, float* out, int accumulate, float scale,
+                                   void* sync, size_t sync_bytes, hipStream_t stream);
 /* mcaq_mapper_train_backward_multi with per-segment reductions (as
  * mcaq_train_reduce_multi with chain 0, segments of equal count) riding on
  * its first (output-layer) stage launch as extra workgroups - the soft masks'

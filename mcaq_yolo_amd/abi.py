@@ -162,7 +162,8 @@ EXPORTS = ("mcaq_abi_version", "mcaq_launch_spatial_quantization", "mcaq_stats",
            "mcaq_mapper_train_forward_multi", "mcaq_mapper_train_backward_multi", "mcaq_head_train_backward_multi",
            "mcaq_smask_train_backward_multi", "mcaq_train_reduce_multi", "mcaq_ema_stats_multi",
            "mcaq_mapper_train_forward_stage_multi", "mcaq_mapper_train_backward_stage_multi", "mcaq_clip_adamw", "mcaq_clip_adamw_work_floats",
-           "mcaq_clip_adamw_sync_bytes", "mcaq_clip_adamw_fused",
+           "mcaq_clip_adamw_sync_bytes", "mcaq_clip_adamw_fused", "mcaq_head_sync_bytes",
+           "mcaq_head_train_backward_fused",
            "mcaq_bit_budget_forward", "mcaq_qat_smask_backward_multi", "mcaq_qat_forward_budget",
            "mcaq_ema_stats_multi_running", "mcaq_head_train_backward_multi_ride",
            "mcaq_stats_pack", "mcaq_morph_ema", "mcaq_mapper_train_backward_multi_ride", "mcaq_dp_unpack",
@@ -260,6 +261,11 @@ def _declare(lib):
     lib.mcaq_mapper_train_backward_fused.restype = I
     lib.mcaq_mapper_train_backward_fused.argtypes = [ctypes.POINTER(MapperParams), ctypes.POINTER(MapperSeg), I, Fl,
                                                      Fl, Fl, ctypes.POINTER(ReduceSeg), I, P, SZ, P]
+    lib.mcaq_head_sync_bytes.restype = SZ
+    lib.mcaq_head_sync_bytes.argtypes = [I]
+    lib.mcaq_head_train_backward_fused.restype = I
+    lib.mcaq_head_train_backward_fused.argtypes = [ctypes.POINTER(CmlpParams), ctypes.POINTER(HeadSeg), I,
+                                                   ctypes.POINTER(ReduceSeg), I, P, I, Fl, P, SZ, P]
     lib.mcaq_head_train_backward_multi_ride.restype = I
     lib.mcaq_head_train_backward_multi_ride.argtypes = [ctypes.POINTER(CmlpParams), ctypes.POINTER(HeadSeg), I,
                                                         ctypes.POINTER(ReduceSeg), I, P]

@@ -1274,7 +1274,10 @@ constexpr int CB_ST = 8 + 64 * 4 + 32 * 4 + 1 + 4;   // per-tile LDS vector (flo
 enum : int { CB_PHI = 0, CB_R1 = 8, CB_GA1 = 72, CB_GY1 = 136, CB_GYX1 = 200, CB_R2 = 264, CB_GA2 = 296,
              CB_GY2 = 328, CB_GYX2 = 360, CB_GA3 = 392 };
 
-__device__ __forceinline__ void mcaq_cmlp_bwd_body(const HeadTrainArgs& A) {
+// kX (fused launch, mcaq_cmlp_bwd_fused_kernel): the weight partials
+// published as granules of gx (this workgroup's CG_SIZE slots) with `tag`
+template <bool kX = false>
+__device__ __forceinline__ void mcaq_cmlp_bwd_body(const HeadTrainArgs& A, mapx_t* gx = nullptr, unsigned tag = 0) {
   constexpr int NW = CB_NW, F1 = 64 / NW, F2 = 32 / NW, NTH = 64 * NW;
   extern __shared__ float smem_tr[];
   float* sv = smem_tr;                       // [TR_TPB][CB_ST]
@@ -1424,6 +1427,10 @@ __device__ __forceinline__ void mcaq_cmlp_bwd_body(const HeadTrainArgs& A) {
   // ---- weight partials over the workgroup's tiles (invalid lanes carry zero
   // gradients).  W2 (32 x 64): thread = one row x 4 columns.
   float* gp = A.gpart + (size_t)wgi * CG_SIZE;
+  auto put = [&](int e, float x) {
+    if constexpr (kX) mapx_put(gx + e, tag, x);
+    else gp[e] = x;
+  };
   auto tvec = [&](int u) { return sv + u * CB_ST; };
   {
     // one 16 x 16 block of W2 per wave on v_mfma_f32_16x16x4_f32: a
@@ -1437,7 +1444,7 @@ __device__ __forceinline__ void mcaq_cmlp_bwd_body(const HeadTrainArgs& A) {
       d = tr_mfma4(w[CB_GA2 + jb * 16 + lr], w[CB_R1 + kb * 16 + lr], d);
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) gp[CG_W2 + (jb * 16 + 4 * lk + r) * 64 + kb * 16 + lr] = d[r];
+    for (int r = 0; r < 4; ++r) put(CG_W2 + (jb * 16 + 4 * lk + r) * 64 + kb * 16 + lr, d[r]);
   }
   TSTAMP(21);
   // W1 (64 x 8) on MFMA as well: waves 0..3, one 16-row block each, the
@@ -1453,7 +1460,7 @@ __device__ __forceinline__ void mcaq_cmlp_bwd_body(const HeadTrainArgs& A) {
     }
     if (lr < 8) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) gp[CG_W1 + (q * 16 + 4 * lk + r) * 8 + lr] = d[r];
+      for (int r = 0; r < 4; ++r) put(CG_W1 + (q * 16 + 4 * lk + r) * 8 + lr, d[r]);
     }
   }
   // the other sums over the tiles - b1 / LN1 (192) and b2 / LN2 / W3 / b3
@@ -1482,7 +1489,7 @@ __device__ __forceinline__ void mcaq_cmlp_bwd_body(const HeadTrainArgs& A) {
         const float bv = w[obc];
         a = fmaf(w[oa], ob >= 0 ? bv : 1.0f, a);
       }
-      gp[e] = a;
+      put(e, a);
     }
   }
   TSTAMP(22);
@@ -2062,6 +2069,73 @@ __global__ __launch_bounds__(MTH) void mcaq_mapper_bwd_multi_kernel(TrMulti<Mapp
 __global__ __launch_bounds__(BL_TH) void mcaq_bilateral_bwd_multi_kernel(TrMulti<HeadTrainArgs> M) {
   mcaq_bilateral_bwd_body(tr_seg(M));
 }
+// the complexity MLP's backward of every segment with its parameter
+// reduction in the same launch: every workgroup publishes its CG_SIZE weight
+// partials as granules (mapx_*: write-through, the epoch tag in each), then
+// sums a slice of the elements over every workgroup's partials - the chain
+// of mcaq_tr_reduce_multi (segments last scale first, each in workgroup
+// order, accumulate / scale as tr_chain_elem), so the values are identical.
+// Sync buffer (mcaq_head_sync_bytes): word 0 the epoch, word 1 the status,
+// granules from byte 256, [workgroup][CG_SIZE].  Every workgroup must be
+// resident at once (at most MAPPER_COOP_MAX_WG).
+struct CmlpRed {
+  unsigned* sync;
+  float* out;
+  int accumulate;
+  float scale;
+  int nwg;             // workgroups of the launch (every segment's)
+};
+__global__ __launch_bounds__(64 * CB_NW) void mcaq_cmlp_bwd_fused_kernel(TrMulti<HeadTrainArgs> M, CmlpRed R) {
+  extern __shared__ float smem_tr[];
+  const HeadTrainArgs& A = tr_seg(M);
+  mapx_t* const gran = reinterpret_cast<mapx_t*>(R.sync + MAPX_HDR);
+  const unsigned tag = __builtin_amdgcn_readfirstlane(
+                           __hip_atomic_load(R.sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) + 1u;
+  mcaq_cmlp_bwd_body<true>(A, gran + (size_t)blockIdx.x * CG_SIZE, tag);
+  __syncthreads();
+  // this workgroup's slice of the elements, every workgroup's partial of each
+  // into LDS (one granule load per thread per pass, all in flight), then one
+  // thread per element sums them in the chain's order
+  const int W = R.nwg, per = (CG_SIZE + W - 1) / W;
+  const int e0 = (int)blockIdx.x * per, ne = imin_(per, CG_SIZE - e0);
+  float* buf = smem_tr;                       // [ne][W]
+  const int tid = (int)threadIdx.x;
+  constexpr int NTH = 64 * CB_NW;
+  for (int i0 = 0; i0 < ne * W; i0 += 4 * NTH) {
+    mapx_t* gp[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = imin_(i0 + r * NTH + tid, ne * W - 1);
+      const int el = i / W, w = i - el * W;
+      gp[r] = gran + (size_t)w * CG_SIZE + e0 + el;
+    }
+    float v[4];
+    if (ne > 0) mapx_get<4>(gp, tag, v, R.sync + 1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = i0 + r * NTH + tid;
+      if (i < ne * W) buf[i] = v[r];
+    }
+  }
+  __syncthreads();
+  if (blockIdx.x == 0 && tid == 0)   // every workgroup published (slice 0 read them all): next epoch
+    __hip_atomic_fetch_add(R.sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int el = tid; el < ne; el += NTH) {   // a slice can exceed the workgroup (few workgroups)
+    const int e = e0 + el;
+    const float* row = buf + (size_t)el * W;
+    const bool sc = R.scale != 0.0f && R.scale != 1.0f;
+    float acc = 0.0f;
+    for (int c = 0; c < M.nseg; ++c) {
+      const HeadTrainArgs& G = M.s[M.nseg - 1 - c];   // the chain: last segment first
+      float sum = 0.0f;
+      for (int w = 0; w < G.nwg; ++w) sum = sum + row[G.wg0 + w];
+      acc = c == 0 ? ((R.accumulate && !sc) ? R.out[e] + sum : sum) : acc + sum;
+    }
+    if (sc) acc = R.accumulate ? R.out[e] + acc * R.scale : acc * R.scale;
+    R.out[e] = acc;
+  }
+}
+
 __global__ __launch_bounds__(64 * CB_NW) void mcaq_cmlp_bwd_multi_kernel(TrMulti<HeadTrainArgs> M) {
   mcaq_cmlp_bwd_body(tr_seg(M));
 }
@@ -2751,6 +2825,70 @@ int mcaq_head_train_backward_multi_ride(const mcaq_cmlp_params* P, const mcaq_he
 
 int mcaq_head_train_backward_multi(const mcaq_cmlp_params* P, const mcaq_head_seg* segs, int nseg, hipStream_t stream) {
   return mcaq_head_train_backward_multi_ride(P, segs, nseg, nullptr, 0, stream);
+}
+
+size_t mcaq_head_sync_bytes(int total_wg) {
+  using namespace mcaq;
+  return total_wg < 1 ? 0 : (size_t)MAPX_HDR * 4 + (size_t)total_wg * CG_SIZE * 8;
+}
+
+int mcaq_head_train_backward_fused(const mcaq_cmlp_params* P, const mcaq_head_seg* segs, int nseg,
+                                   const mcaq_reduce_seg* rsegs, int nr, float* out, int accumulate, float scale,
+                                   void* sync, size_t sync_bytes, hipStream_t stream) {
+  using namespace mcaq;
+  if (!P || !segs || nseg < 1 || nseg > TR_MAXSEG || nr < 0 || nr > TR_MAXSEG || (nr > 0 && !rsegs) || !out ||
+      !sync || ((uintptr_t)sync & 7) != 0)
+    return (int)hipErrorInvalidValue;
+  TrMulti<TrReduceSeg> R{};
+  for (int k = 0; k < nr; ++k) {
+    const mcaq_reduce_seg& g = rsegs[k];
+    if (!g.part || (!g.out && k == 0) || g.nparts < 1 || g.stride < g.count || g.count < 1 || g.count != rsegs[0].count)
+      return (int)hipErrorInvalidValue;
+    R.s[k] = TrReduceSeg{g.part, g.out, g.nparts, g.stride, g.count, g.accumulate, g.scale};
+  }
+  R.nseg = nr;
+  TrMulti<HeadTrainArgs> Mb{}, Mc{};
+  int wb = 0, wc = 0;
+  size_t lb = 0;
+  for (int k = 0; k < nseg; ++k) {
+    const mcaq_head_seg& g = segs[k];
+    if (!g.phi || !g.craw || !g.gC || !g.gcraw || !g.gpart || g.B < 1 || g.ht < 1 || g.wt < 1)
+      return (int)hipErrorInvalidValue;
+    HeadTrainArgs A{};
+    A.P = *P; A.phi = g.phi; A.craw = g.craw; A.gC = g.gC; A.gcraw = g.gcraw; A.gpart = g.gpart;
+    A.B = g.B; A.ht = g.ht; A.wt = g.wt; A.n = g.B * g.ht * g.wt; A.nwg = (A.n + TR_TPB - 1) / TR_TPB;
+    const size_t l = (size_t)53 * g.ht * g.wt * sizeof(float);
+    if (l > 160 * 1024 - 1024) return (int)hipErrorInvalidValue;
+    lb = l > lb ? l : lb;
+    Mb.s[k] = A; Mb.s[k].wg0 = wb; wb += A.B;
+    Mc.s[k] = A; Mc.s[k].wg0 = wc; wc += A.nwg;
+  }
+  Mb.nseg = Mc.nseg = nseg;
+  if (wc > MAPPER_COOP_MAX_WG || sync_bytes < mcaq_head_sync_bytes(wc)) return (int)hipErrorInvalidValue;
+  const size_t lc = (size_t)(TR_TPB * CB_ST + CB_NW * TR_TPB + 4096) * sizeof(float);
+  static_assert((size_t)TR_TPB * CB_ST >= (size_t)CG_SIZE + MAPPER_COOP_MAX_WG, "slice buffer in the tile vectors");
+  static int set = 0;
+  if (!set) {
+    hipError_t e = hipFuncSetAttribute((const void*)mcaq_cmlp_bwd_fused_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lc);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)mcaq_bilateral_bwd_multi_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024 - 1024);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)mcaq_bilateral_bwd_ride_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024 - 1024);
+    if (e != hipSuccess) return (int)e;
+    set = 1;
+  }
+  if (nr > 0) {
+    const int rw = (R.s[0].count + BL_TH - 1) / BL_TH;
+    hipLaunchKernelGGL(mcaq_bilateral_bwd_ride_kernel, dim3(wb + rw), dim3(BL_TH), lb, stream, Mb, R, wb);
+  } else {
+    hipLaunchKernelGGL(mcaq_bilateral_bwd_multi_kernel, dim3(wb), dim3(BL_TH), lb, stream, Mb);
+  }
+  const CmlpRed cr{static_cast<unsigned*>(sync), out, accumulate, scale, wc};
+  hipLaunchKernelGGL(mcaq_cmlp_bwd_fused_kernel, dim3(wc), dim3(64 * CB_NW), lc, stream, Mc, cr);
+  return (int)hipGetLastError();
 }
 
 int mcaq_smask_train_backward_multi(const mcaq_smask_seg* segs, int nseg, hipStream_t stream) {

@@ -317,16 +317,25 @@ class _HeadMulti(torch.autograd.Function):
             sg.B, sg.ht, sg.wt = B, ht, wt
         ride = _PENDING_REDUCE["segs"]
         _PENDING_REDUCE["segs"] = None
-        if ride is not None:     # the mapper's gradient reduction as extra workgroups of the bilateral launch
-            abi.check(L.mcaq_head_train_backward_multi_ride(ctypes.byref(q), segs, n, ride[0], ride[1], _stream()),
-                      "mcaq_head_train_backward_multi_ride")
-        else:
-            abi.check(L.mcaq_head_train_backward_multi(ctypes.byref(q), segs, n, _stream()),
-                      "mcaq_head_train_backward_multi")
         mod_params = _cmlp_params(ctx.an)
         sink = ctx.an._gsink.target(mod_params) if len(mod_params) == len(params) else None
         gflat, acc = sink if sink is not None else (torch.empty(core._CM_SIZE, device=dev), 0)
-        _reduce_chain(gparts, gflat, acc, core._CM_SIZE)
+        sync = _sync_buffer(ctx.an, dev, [c.numel() for c in craws], L.mcaq_head_sync_bytes) if HEAD_FUSED else None
+        if sync is not None:
+            # the MLP's parameter reduction inside its own launch; the mapper's
+            # (if pending) riding on the bilateral launch
+            abi.check(L.mcaq_head_train_backward_fused(ctypes.byref(q), segs, n, ride[0] if ride else None,
+                                                       ride[1] if ride else 0, _p(gflat), acc, 0.0, _p(sync),
+                                                       sync.numel() * 8, _stream()),
+                      "mcaq_head_train_backward_fused")
+        else:
+            if ride is not None:     # the mapper's gradient reduction as extra workgroups of the bilateral launch
+                abi.check(L.mcaq_head_train_backward_multi_ride(ctypes.byref(q), segs, n, ride[0], ride[1],
+                                                                _stream()), "mcaq_head_train_backward_multi_ride")
+            else:
+                abi.check(L.mcaq_head_train_backward_multi(ctypes.byref(q), segs, n, _stream()),
+                          "mcaq_head_train_backward_multi")
+            _reduce_chain(gparts, gflat, acc, core._CM_SIZE)
         grads = (None,) * len(params) if sink is not None else tuple(core._split_flat(gflat, params))
         return (None, None, None) + (None,) * n + grads
 
@@ -407,31 +416,48 @@ DP_GLOBAL_MAPPER = True
 MAPPER_FUSED = os.environ.get("MCAQ_MAPPER_FUSED", "1") != "0"
 
 
-def _mapx_buffer(mod, dev, ns):
-    """The fused mapper launches' sync buffer for segments of ns tiles: one
-    per mapper module and segment layout (forward and backward share it),
-    zeroed when made; None when the launch would exceed the resident limit."""
+def _sync_buffer(mod, dev, ns, nbytes):
+    """An in-launch exchange's sync buffer for segments of ns tiles (64 per
+    workgroup): one per module and segment layout, zeroed when made (epochs
+    and granules start over); None above the resident-workgroup limit."""
     L = abi.lib()
     wgs = tuple((int(n) + 63) // 64 for n in ns)
     total = sum(wgs)
-    if not MAPPER_FUSED or total > L.mcaq_mapper_fused_max_wg():
+    if total > L.mcaq_mapper_fused_max_wg():
         return None
     cache = mod.__dict__.setdefault("_mapx", {})
-    key = (str(dev), wgs)
+    key = (str(dev), nbytes.__name__, wgs)
     buf = cache.get(key)
     if buf is None:
-        buf = torch.zeros((L.mcaq_mapper_sync_bytes(total) + 7) // 8, dtype=torch.int64, device=dev)
+        buf = torch.zeros((nbytes(total) + 7) // 8, dtype=torch.int64, device=dev)
         cache[key] = buf
     return buf
 
 
+def _mapx_buffer(mod, dev, ns):
+    """The fused mapper launches' sync buffer (forward and backward share it)."""
+    return _sync_buffer(mod, dev, ns, abi.lib().mcaq_mapper_sync_bytes) if MAPPER_FUSED else None
+
+
 def mapper_sync_status(mod):
-    """Nonzero when an in-launch exchange of a fused mapper launch of `mod`
-    timed out (its results are then invalid); 0 otherwise.  Synchronises."""
+    """Nonzero when an in-launch exchange of a fused launch of `mod` (the
+    mapper's, or the analyzer head's backward) timed out (its results are
+    then invalid); 0 otherwise.  Synchronises."""
     st = 0
-    for buf in getattr(mod, "_mapx", {}).values():
-        st |= int(buf.view(torch.int32)[abi.MAPPER_SYNC_STATUS_WORD].item())
+    for key, buf in getattr(mod, "_mapx", {}).items():
+        w = abi.MAPPER_SYNC_STATUS_WORD if key[1] == "mcaq_mapper_sync_bytes" else abi.ADAMW_SYNC_STATUS_WORD
+        st |= int(buf.view(torch.int32)[w].item())
     return st
+
+
+# The complexity MLP's backward with its parameter reduction inside the
+# launch (mcaq_head_train_backward_fused: partials exchanged as granules,
+# bit-identical to the separate chain reduction).  Off by default: measured
+# no faster than the separate launch (19.8 vs 13.9 + 5.7 us, step within
+# noise: profiles/r06_fuse/r06_fuse3) - the 2,881 partials per workgroup
+# cost as much written and swept write-through as the launch boundary they
+# replace.  MCAQ_HEAD_FUSED=1 selects it.
+HEAD_FUSED = os.environ.get("MCAQ_HEAD_FUSED", "0") == "1"
 
 
 def _consecutive(ts):

@@ -36,6 +36,23 @@ def test_fused_mapper_equals_staged_graph():
           _with(False, steps=4, fused_mq=True, budget=True))
 
 
+@pytest.mark.parametrize("graph", [False, True])
+def test_fused_head_reduction_equals_separate(graph):
+    """train_step.HEAD_FUSED: the complexity MLP's parameter reduction inside
+    its backward launch (granule exchange) against the separate chain
+    reduction launch, bit for bit, eager and graph-replayed; status clear."""
+    from mcaq_yolo_amd import train_step
+    res = []
+    for fused in (True, False):
+        old = train_step.HEAD_FUSED
+        train_step.HEAD_FUSED = fused
+        try:
+            res.append(_run(False, multi=True, steps=3, graph=graph, fused_mq=True, budget=True))
+        finally:
+            train_step.HEAD_FUSED = old
+    _same(res[0], res[1])
+
+
 def test_fused_mapper_one_launch_per_direction_and_layouts():
     """One fused forward and one fused backward call per step (no staged
     call); batches of 4, 2, 4 images (the layout changes, then comes back to a
@@ -74,6 +91,7 @@ def test_fused_mapper_one_launch_per_direction_and_layouts():
             out += [b.clone() for b in h.bit_mapper.buffers()]
             if fused:
                 assert train_step.mapper_sync_status(h.bit_mapper) == 0
+                assert train_step.mapper_sync_status(h.complexity_analyzer) == 0
                 assert len(h.bit_mapper._mapx) == 2          # two layouts, the first one reused
             res[fused] = out
         finally:

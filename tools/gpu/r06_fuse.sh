@@ -1,5 +1,6 @@
 #!/bin/bash
-# Round-6 in-launch exchanges (fused mapper, one-launch ClipAdamW): their GPU
+# Round-6 in-launch exchanges (fused mapper, one-launch ClipAdamW, the MLP
+# backward's in-launch parameter reduction): their GPU
 # tests + the train-path tests they feed, config-5 QAT lines for every on/off
 # combination (interleaved), a rocprofv3 kernel trace of the default step and
 # the fused mapper's stage stamps.  Tag $1 -> gpurun_out/$1/.
@@ -14,9 +15,10 @@ timeout -k 10 600 python -u -m pytest tests/test_mapper_fused_gpu.py tests/test_
   tests/test_qat_gpu.py -x -v --timeout 200 --timeout-method thread > $OUT/pytest.log 2>&1
 rc=$?; grep -E "passed|failed|error" $OUT/pytest.log | tail -1; [ $rc -eq 0 ] || { grep -E "FAIL|Error|assert" $OUT/pytest.log | head -30; exit $rc; }
 for i in 1 2; do
-  for v in "1 1" "1 0" "0 1" "0 0"; do
+  for v in "1 1 1" "1 1 0" "1 0 1" "0 1 1" "0 0 0"; do
     set -- $v
-    MCAQ_MAPPER_FUSED=$1 MCAQ_ADAMW_ONE_LAUNCH=$2 timeout -k 10 300 python bench.py --config 5 --no-cpu > $OUT/c5_m$1_o$2_$i.json 2> $OUT/c5_m$1_o$2_$i.err || { tail -5 $OUT/c5_m$1_o$2_$i.err; exit 1; }
+    n=c5_m$1_o$2_h$3_$i
+    MCAQ_MAPPER_FUSED=$1 MCAQ_ADAMW_ONE_LAUNCH=$2 MCAQ_HEAD_FUSED=$3 timeout -k 10 300 python bench.py --config 5 --no-cpu > $OUT/$n.json 2> $OUT/$n.err || { tail -5 $OUT/$n.err; exit 1; }
   done
 done
 MCAQ_BENCH_SHARDED=1 timeout -k 10 300 python bench.py --config 5 --no-cpu > $OUT/c5_sharded.json 2> $OUT/c5_sharded.err || { tail -5 $OUT/c5_sharded.err; exit 1; }
