@@ -167,14 +167,16 @@ def main_qat(args, world, rank, dev, pg):
     # the reference's optimizer end of the step (train.py:140-150, 626-641:
     # clip_grad_norm_ 1.0, AdamW lr 1e-3 weight decay 0.05 betas 0.9 / 0.999,
     # the mapper's |W| projection): by default optim.ClipAdamW, all three in
-    # two launches; --torch-optim: torch's clip + fused capturable AdamW + the
+    # one launch; --torch-optim: torch's clip + fused capturable AdamW + the
     # projection as separate kernels (~14 per step)
     fused_opt = not args.torch_optim
     if fused_opt:
         from mcaq_yolo_amd.optim import ClipAdamW
         opt = ClipAdamW(params_, lr=1e-3, weight_decay=0.05, betas=(0.9, 0.999), max_norm=1.0,
                         project_abs=h.bit_mapper.constrained_weights())
-        opt_kind = "optim.ClipAdamW (clip_grad_norm 1.0 + AdamW + |W| projection, two launches)"
+        from mcaq_yolo_amd import optim as _optim
+        opt_kind = "optim.ClipAdamW (clip_grad_norm 1.0 + AdamW + |W| projection, %s)" % (
+            "one launch" if _optim.ONE_LAUNCH else "two launches")
     else:
         try:
             opt = torch.optim.AdamW(params_, lr=1e-3, weight_decay=0.05, betas=(0.9, 0.999), fused=True,

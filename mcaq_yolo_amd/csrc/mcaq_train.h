@@ -7,7 +7,9 @@
 //     z = [C, C^2, log1p C] -> 3 x (Linear, BatchNorm1d over the batch's
 //     tiles, ReLU) -> Linear -> sigmoid -> b_min + (b_max - b_min) h, x T,
 //     straight-through clamp (and round);  forward = 4 launches (one per
-//     batch-statistics barrier), backward = 4 + 1 (parameter reduction)
+//     batch-statistics barrier), backward = 4 + 1 (parameter reduction); or
+//     (round 6) ONE launch per direction, the batch statistics exchanged
+//     inside it as write-through granules (mapx_*, *_fused)
 //   analyzer head backward (morphology.py:81-97, 309-354, 959-968):
 //     bilateral adjoint per image, then the complexity MLP (Linear-LN-ReLU x2,
 //     Linear, sigmoid) recomputed and differentiated per tile
