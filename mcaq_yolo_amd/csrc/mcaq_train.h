@@ -233,6 +233,9 @@ constexpr int MTH = 64 * MW;
 // read it by then), so granules of earlier launches never match.  The buffer
 // is zeroed whenever its segment layout changes (train_step._mapx_buffer).
 // Bounded spins: a timeout sets the status word and goes on (tests check it).
+#ifndef MCAQ_MAPX_SLEEP   // s_sleep between two sweeps of unpublished granules (A/B build option)
+#define MCAQ_MAPX_SLEEP 2
+#endif
 typedef unsigned long long mapx_t;
 constexpr int MAPX_STRIDE = 129;   // granules per workgroup per exchange: [0, 128) partials, 128 count
 constexpr int MAPX_HDR = 64;       // header words (epochs of the segments, status at MAPX_STATUS)
@@ -257,7 +260,7 @@ __device__ __forceinline__ void mapx_get(mapx_t* const (&g)[R], unsigned tag, fl
       __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       return;
     }
-    __builtin_amdgcn_s_sleep(2);
+    if constexpr (MCAQ_MAPX_SLEEP > 0) __builtin_amdgcn_s_sleep(MCAQ_MAPX_SLEEP);
   }
 }
 // this launch's epoch of the segment, in a register of every wave
