@@ -36,6 +36,7 @@ def timed(L, fn, reps=20):
 def main():
     dev = torch.device("cuda:0")
     name, B, chans, grid, mapper = bench.CONFIGS[int(os.environ.get("CFG", "2"))]
+    B = int(os.environ.get("BATCH", B))        # e.g. 16: the QAT step's per-GPU batch
     cm, mm, sm = bench.load_blobs(dev)
     geoms = [ScaleGeom(B, c, h, w, grid) for c, (h, w) in zip(chans, bench.SIZES)]
     feats = [bench.synth_features(B, c, h, w, 1000 + i, dev) for i, (c, (h, w)) in enumerate(zip(chans, bench.SIZES))]
