@@ -217,7 +217,7 @@ __device__ __forceinline__ void map_bn(const mcaq_mapper_params& P, int L, const
 }
 
 constexpr int MW = 8;               // waves per mapper workgroup (lane = tile, waves split the features)
-constexpr int MAPPER_COOP_MAX_WG = 256;   // one-launch (grid-barrier) mapper up to this many workgroups
+constexpr int MAPPER_COOP_MAX_WG = 256;   // one-launch mapper (grid barrier / granule exchanges) up to this many workgroups
 constexpr int MTH = 64 * MW;
 
 // ---- fused mapper launches: the batch-statistic partials exchanged inside
@@ -230,8 +230,8 @@ constexpr int MTH = 64 * MW;
 // takes a fence or a counter.  tag = epoch * 8 + exchange: the segment's
 // epoch word is read by every wave at launch and advanced by the segment's
 // first workgroup after its last exchange (every workgroup of the segment has
-// read it by then), so granules of earlier launches never match.  The buffer
-// is zeroed whenever its segment layout changes (train_step._mapx_buffer).
+// read it by then), so granules of earlier launches never match.  A buffer
+// serves one segment layout and starts zeroed (train_step._sync_buffer).
 // Bounded spins: a timeout sets the status word and goes on (tests check it).
 #ifndef MCAQ_MAPX_SLEEP   // s_sleep between two sweeps of unpublished granules (A/B build option)
 #define MCAQ_MAPX_SLEEP 2
