@@ -245,8 +245,41 @@ __device__ __forceinline__ void mapx_put(mapx_t* g, unsigned tag, float v) {
   __hip_atomic_store(g, ((mapx_t)tag << 32) | (mapx_t)__float_as_uint(v), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
 }
+#ifndef MCAQ_MAPX_PIPE   // > 0: polls issued every s_sleep(MCAQ_MAPX_PIPE) with the previous one in flight (A/B)
+#define MCAQ_MAPX_PIPE 0
+#endif
 template <int R>
 __device__ __forceinline__ void mapx_get(mapx_t* const (&g)[R], unsigned tag, float (&v)[R], unsigned* status) {
+  if constexpr (MCAQ_MAPX_PIPE > 0) {
+    // two polls in flight: the next batch of loads is issued before the
+    // previous one is checked, so a publish is seen about one round trip
+    // after it lands instead of up to two
+    mapx_t a[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) a[r] = __hip_atomic_load(g[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (unsigned spins = 0;; ++spins) {
+      __builtin_amdgcn_s_sleep(MCAQ_MAPX_PIPE);
+      mapx_t b[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) b[r] = __hip_atomic_load(g[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      bool ok = true;
+#pragma unroll
+      for (int r = 0; r < R; ++r) ok = ok && (unsigned)(a[r] >> 32) == tag;
+      if (ok) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[r] = __uint_as_float((unsigned)a[r]);
+        return;
+      }
+      if (spins >= (1u << 20)) {
+        __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int r = 0; r < R; ++r) v[r] = __uint_as_float((unsigned)b[r]);
+        return;
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) a[r] = b[r];
+    }
+  }
   for (unsigned spins = 0;; ++spins) {
     bool ok = true;
 #pragma unroll
