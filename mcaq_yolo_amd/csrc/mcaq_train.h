@@ -237,6 +237,9 @@ constexpr int MTH = 64 * MW;
 #define MCAQ_MAPX_SLEEP 2
 #endif
 typedef unsigned long long mapx_t;
+#if defined(MCAQ_STAMPS_WG)
+__device__ unsigned long long g_mapx_wg[64];   // diagnostic build only (tools/probe/mapx_skew.py)
+#endif
 constexpr int MAPX_STRIDE = 129;   // granules per workgroup per exchange: [0, 128) partials, 128 count
 constexpr int MAPX_HDR = 64;       // header words (epochs of the segments, status at MAPX_STATUS)
 constexpr int MAPX_STATUS = 32;
@@ -2285,8 +2288,16 @@ __global__ __launch_bounds__(MTH) void mcaq_mapper_fwd_fused_kernel(TrMulti<Mapp
   const MapperTrainArgs& A = tr_seg(M);
   const unsigned E = mapx_epoch(A);
   TSTAMP(23);
+#if defined(MCAQ_STAMPS_WG) && defined(__HIP_DEVICE_COMPILE__)
+  // diagnostic build only: workgroups 0..31's start and end of stage 1 (the
+  // global 100 MHz clock), tools/probe/mapx_skew.py
+  if (threadIdx.x == 0 && blockIdx.x < 32) g_mapx_wg[blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#endif
   mapper_fwd_stage<1, true>(A, L, E, s_a);
   __syncthreads();
+#if defined(MCAQ_STAMPS_WG) && defined(__HIP_DEVICE_COMPILE__)
+  if (threadIdx.x == 0 && blockIdx.x < 32) g_mapx_wg[32 + blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+#endif
   TSTAMP(24);
   mapper_fwd_stage<2, true>(A, L, E, s_a);
   __syncthreads();
@@ -2713,6 +2724,12 @@ int mcaq_mapper_train_backward_multi(const mcaq_mapper_params* P, const mcaq_map
                                      float min_bits, float max_bits, float temperature, hipStream_t stream) {
   return mcaq_mapper_train_backward_multi_ride(P, segs, nseg, min_bits, max_bits, temperature, nullptr, 0, stream);
 }
+
+#if defined(MCAQ_STAMPS_WG)
+int mcaq_read_wg_stamps(unsigned long long* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(mcaq::g_mapx_wg), sizeof(mcaq::g_mapx_wg));
+}
+#endif
 
 size_t mcaq_mapper_sync_bytes(int total_wg) {
   using namespace mcaq;
