@@ -53,6 +53,7 @@ class ClipAdamW(torch.optim.Optimizer):
         self._segs = None
         self._seg_key = None
         self._sync = None
+        self._sync_key = None
         self._retired = []
 
     def _params(self):
@@ -178,11 +179,16 @@ class ClipAdamW(torch.optim.Optimizer):
             self._norm_t = torch.empty(1, device=items[0][1].device)
             total = sum(p.numel() for _, p in items)
             self._work = torch.empty(abi.lib().mcaq_clip_adamw_work_floats(total), device=items[0][1].device)
-            # the one-launch form's exchange buffer: zeroed once per descriptor set
-            self._sync = None
-            if self.max_norm is not None and self.max_norm > 0 and -(-total // 1024) <= 256:
+            # the one-launch form's exchange buffer: one per (elements,
+            # tensors) layout, zeroed when made - descriptors rebuilt for moved
+            # gradients (set_to_none) keep it, its epoch carries on
+            lay = (total, len(items), items[0][1].device)
+            if self.max_norm is None or self.max_norm <= 0 or -(-total // 1024) > 256:
+                self._sync, self._sync_key = None, None
+            elif self._sync is None or self._sync_key != lay:
                 nb = abi.lib().mcaq_clip_adamw_sync_bytes(total, len(items))
                 self._sync = torch.zeros((nb + 7) // 8, dtype=torch.int64, device=items[0][1].device)
+                self._sync_key = lay
         mn = self.max_norm if self.max_norm is not None else 0.0
         st = ctypes.c_void_p(torch.cuda.current_stream(items[0][1].device).cuda_stream)
         L = abi.lib()
