@@ -722,6 +722,10 @@ class Runner(_RunMixin):
         # all-reduce is issued eagerly between two replays - on the process
         # group's own stream, in the host's (rank-identical) order.
         capturable = pg is None or (_backend(pg) == "nccl" and (_world(pg) == 1 or depth == 1))
+        if pg is not None and os.environ.get("MCAQ_BENCH_EAGER_COLLECTIVE") == "1":
+            # rehearsal of the N > 1 schedule on one rank: split graphs around
+            # the eager all-reduce even where capture would be allowed
+            capturable = False
         self.captured_collective = use_graph and pg is not None and capturable
         if use_graph:
             torch.cuda.synchronize()
