@@ -245,13 +245,14 @@ def test_clip_adamw_per_parameter_steps_and_lr_table():
         _close(q, p, 1e-5, "param %d after lr change" % k)
 
 
-@pytest.mark.parametrize("sizes", [(97, 2048, 5), (4609, 2881, 33, 1, 1024, 3000)])
+@pytest.mark.parametrize("sizes", [(97, 2048, 5), (4609, 2881, 33, 1, 1024, 3000), (261144, 1000)])
 def test_clip_adamw_one_launch_equals_two_launches(sizes):
     """The clipped step as ONE launch (optim.ONE_LAUNCH: the chunks' norm
     partials exchanged inside the launch) against the two launches, bit for
     bit: parameters, clipped gradients, moments, step counts and total norm
     over eager steps (one parameter without a gradient in step 2: its count
-    stays) and graph replays; the exchange status word stays clear."""
+    stays) and graph replays; the exchange status word stays clear.  The
+    last case is the one-launch maximum: 256 chunks of 1,024 elements."""
     from mcaq_yolo_amd import abi, optim
     from mcaq_yolo_amd.optim import ClipAdamW
     torch.manual_seed(7)
